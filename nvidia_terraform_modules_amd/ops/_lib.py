@@ -1,0 +1,91 @@
+"""ctypes binding to ``libntm_validation.so`` (the gfx950 HIP kernels).
+
+The library is loaded AFTER ``torch`` so that its ``libamdhip64.so.7``
+dependency binds to the HIP runtime PyTorch already mapped (same soname): one
+runtime, one set of streams. Loading fails loudly - there is deliberately no
+eager/PyTorch fallback for the validation kernels.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+import torch  # noqa: F401  (must be imported before the HIP library)
+
+_HERE = Path(__file__).resolve().parent
+LIB_PATH = _HERE / "libntm_validation.so"
+
+_lib: ctypes.CDLL | None = None
+
+
+class NativeLibraryMissing(RuntimeError):
+    pass
+
+
+def _declare(lib: ctypes.CDLL) -> None:
+    c_int, c_size, c_float, c_vp = ctypes.c_int, ctypes.c_size_t, ctypes.c_float, ctypes.c_void_p
+    sig = {
+        "ntm_version": ([], ctypes.c_char_p),
+        "ntm_gemm_shape_ok": ([c_int, c_int, c_int], c_int),
+        "ntm_gemm_bf16": ([c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp], c_int),
+        "ntm_fill_uniform_bf16": ([c_vp, c_size, ctypes.c_ulonglong, c_float, c_vp], c_int),
+        "ntm_ref_gemm_f32": ([c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp], c_int),
+        "ntm_verify_bf16": ([c_vp, c_vp, c_size, c_float, c_float, c_vp, c_vp], c_int),
+        "ntm_verify_result_bytes": ([], c_int),
+        "ntm_stream_copy": ([c_vp, c_vp, c_size, c_vp], c_int),
+        "ntm_stream_read": ([c_vp, c_size, c_vp, c_vp], c_int),
+    }
+    optional = {
+        "ntm_xgmi_allreduce_sum_bf16": (
+            [c_vp, c_vp, c_int, c_int, c_size, c_vp, c_vp], c_int),
+        "ntm_xgmi_reduce_local_bf16": ([c_vp, c_vp, c_int, c_size, c_vp], c_int),
+    }
+    for name, (argt, rest) in sig.items():
+        fn = getattr(lib, name)
+        fn.argtypes = argt
+        fn.restype = rest
+    for name, (argt, rest) in optional.items():
+        fn = getattr(lib, name, None)
+        if fn is not None:
+            fn.argtypes = argt
+            fn.restype = rest
+
+
+def lib() -> ctypes.CDLL:
+    """Return the loaded library, raising if it has not been built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not LIB_PATH.exists():
+        raise NativeLibraryMissing(
+            f"{LIB_PATH} not found. Build it with "
+            "`python -m nvidia_terraform_modules_amd.ops.build` (needs hipcc, gfx950)."
+        )
+    mode = os.RTLD_NOW | getattr(os, "RTLD_GLOBAL", 0)
+    _lib = ctypes.CDLL(str(LIB_PATH), mode=mode)
+    _declare(_lib)
+    return _lib
+
+
+def available() -> bool:
+    try:
+        lib()
+        return True
+    except (NativeLibraryMissing, OSError):
+        return False
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise RuntimeError(f"{what} failed with hipError {rc}")
+
+
+def stream_handle(stream: "torch.cuda.Stream | None" = None) -> int:
+    if stream is None:
+        stream = torch.cuda.current_stream()
+    return int(stream.cuda_stream)
+
+
+def version() -> str:
+    return lib().ntm_version().decode()

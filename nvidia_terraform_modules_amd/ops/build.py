@@ -1,0 +1,117 @@
+"""Build the MI355X-native validation code (gfx950 only).
+
+Outputs (all in-tree, so they travel to the GPU box with the repo snapshot):
+
+* ``nvidia_terraform_modules_amd/ops/libntm_validation.so`` - K1/K2/K3 kernels
+  behind a C ABI, loaded by :mod:`nvidia_terraform_modules_amd.ops._lib`.
+* ``validation/build/amdgpu-validate`` - the standalone validation-Job binary
+  (HIP + RCCL, no Python/PyTorch in the container image).
+
+The reference has no native code at all; this replaces the
+CUDA ``vectorAdd`` validator that the NVIDIA GPU Operator chart ran
+(``/root/reference/eks/main.tf:185-203``).
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import shutil
+import subprocess
+import sys
+from pathlib import Path
+
+ARCH = "gfx950"
+REPO = Path(__file__).resolve().parents[2]
+VALIDATION = REPO / "validation"
+INCLUDE = VALIDATION / "include"
+SRC = VALIDATION / "src"
+BUILD = VALIDATION / "build"
+PKG_OPS = Path(__file__).resolve().parent
+LIB_NAME = "libntm_validation.so"
+BIN_NAME = "amdgpu-validate"
+
+COMMON_FLAGS = [
+    f"--offload-arch={ARCH}",
+    "-O3",
+    "-std=c++17",
+    "-fPIC",
+    f"-I{INCLUDE}",
+    "-Wall",
+    "-Wno-unused-function",
+]
+
+
+def hipcc() -> str:
+    exe = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    if not os.path.exists(exe):
+        raise RuntimeError("hipcc not found: the ROCm toolchain is required to build")
+    return exe
+
+
+def _run(cmd: list[str], verbose: bool) -> None:
+    if verbose:
+        print("+", " ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+
+
+def _stale(target: Path, deps: list[Path]) -> bool:
+    if not target.exists():
+        return True
+    t = target.stat().st_mtime
+    return any(d.stat().st_mtime > t for d in deps)
+
+
+def _deps() -> list[Path]:
+    return sorted(INCLUDE.rglob("*.hpp")) + sorted(SRC.glob("*.hip")) + sorted(SRC.glob("*.cpp"))
+
+
+def build_library(force: bool = False, verbose: bool = True) -> Path:
+    out = PKG_OPS / LIB_NAME
+    srcs = [SRC / "ntm_validation.hip", SRC / "xgmi_allreduce.hip"]
+    srcs = [s for s in srcs if s.exists()]
+    if force or _stale(out, _deps()):
+        BUILD.mkdir(parents=True, exist_ok=True)
+        tmp = BUILD / (LIB_NAME + ".tmp")
+        _run([hipcc(), *COMMON_FLAGS, "-shared", *map(str, srcs), "-o", str(tmp)], verbose)
+        os.replace(tmp, out)
+    return out
+
+
+def build_binary(force: bool = False, verbose: bool = True) -> Path:
+    out = BUILD / BIN_NAME
+    main = SRC / "validate_main.cpp"
+    if not main.exists():
+        return out
+    if force or _stale(out, _deps()):
+        BUILD.mkdir(parents=True, exist_ok=True)
+        srcs = [SRC / "ntm_validation.hip", SRC / "xgmi_allreduce.hip"]
+        srcs = [str(s) for s in srcs if s.exists()]
+        cmd = [
+            hipcc(), *COMMON_FLAGS, "-x", "hip", str(main), *srcs,
+            "-I/opt/rocm/include", "-L/opt/rocm/lib", "-lrccl", "-lpthread",
+            "-Wl,-rpath,/opt/rocm/lib", "-o", str(out) + ".tmp",
+        ]
+        _run(cmd, verbose)
+        os.replace(str(out) + ".tmp", out)
+    return out
+
+
+def build_all(force: bool = False, verbose: bool = True) -> dict[str, str]:
+    lib = build_library(force=force, verbose=verbose)
+    binary = build_binary(force=force, verbose=verbose)
+    return {"library": str(lib), "binary": str(binary)}
+
+
+def main(argv: list[str] | None = None) -> int:
+    ap = argparse.ArgumentParser(description=__doc__)
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("-q", "--quiet", action="store_true")
+    args = ap.parse_args(argv)
+    res = build_all(force=args.force, verbose=not args.quiet)
+    for k, v in res.items():
+        print(f"{k}: {v}")
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

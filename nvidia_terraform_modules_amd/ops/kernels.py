@@ -1,0 +1,140 @@
+"""Python entry points for the gfx950 validation kernels (K1, K2, K3).
+
+All functions launch on the current PyTorch stream and never synchronise, so
+they can be captured in a ``torch.cuda.CUDAGraph`` (HIP graph on ROCm).
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import torch
+
+from ._lib import check, lib, stream_handle
+
+BM = BN = 256
+BK = 64
+
+
+def gemm_shape_ok(m: int, n: int, k: int) -> bool:
+    """True iff the 256x256x64 MFMA kernel tiles (M, N, K) exactly."""
+    return m > 0 and n > 0 and k >= 2 * BK and m % BM == 0 and n % BN == 0 and k % BK == 0
+
+
+def _require(t: torch.Tensor, name: str, dtype: torch.dtype) -> None:
+    if not t.is_cuda:
+        raise ValueError(f"{name} must be a GPU tensor")
+    if t.dtype != dtype:
+        raise ValueError(f"{name} must be {dtype}, got {t.dtype}")
+    if t.dim() != 2 or t.stride(1) != 1:
+        raise ValueError(f"{name} must be 2-D with unit inner stride")
+
+
+def gemm_bf16(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """K1: ``out = a @ b.T`` in bf16 with fp32 accumulation on MFMA.
+
+    a: [M, K] bf16, b: [N, K] bf16 (both K-contiguous), out: [M, N] bf16.
+    """
+    _require(a, "a", torch.bfloat16)
+    _require(b, "b", torch.bfloat16)
+    m, k = a.shape
+    n, kb = b.shape
+    if k != kb:
+        raise ValueError(f"K mismatch: a has {k}, b has {kb}")
+    if not gemm_shape_ok(m, n, k):
+        raise ValueError(f"shape ({m},{n},{k}) not tiled by the 256x256x64 kernel")
+    if out is None:
+        out = torch.empty((m, n), dtype=torch.bfloat16, device=a.device)
+    _require(out, "out", torch.bfloat16)
+    if tuple(out.shape) != (m, n):
+        raise ValueError("out has the wrong shape")
+    rc = lib().ntm_gemm_bf16(
+        a.data_ptr(), b.data_ptr(), out.data_ptr(), m, n, k,
+        a.stride(0), b.stride(0), out.stride(0), stream_handle())
+    check(rc, "ntm_gemm_bf16")
+    return out
+
+
+def fill_uniform_(t: torch.Tensor, seed: int, scale: float = 1.0) -> torch.Tensor:
+    """K3: fill a bf16 tensor in place with ``scale * U[-1, 1)`` (hash RNG)."""
+    if t.dtype != torch.bfloat16 or not t.is_cuda or not t.is_contiguous():
+        raise ValueError("fill_uniform_ needs a contiguous bf16 GPU tensor")
+    rc = lib().ntm_fill_uniform_bf16(t.data_ptr(), t.numel(), seed & (2**64 - 1), float(scale),
+                                     stream_handle())
+    check(rc, "ntm_fill_uniform_bf16")
+    return t
+
+
+def ref_gemm_f32(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """K3: independent fp32-FMA reference ``a @ b.T`` (no MFMA, no hipBLASLt)."""
+    _require(a, "a", torch.bfloat16)
+    _require(b, "b", torch.bfloat16)
+    m, k = a.shape
+    n = b.shape[0]
+    out = torch.empty((m, n), dtype=torch.float32, device=a.device)
+    rc = lib().ntm_ref_gemm_f32(a.data_ptr(), b.data_ptr(), out.data_ptr(), m, n, k,
+                                a.stride(0), b.stride(0), out.stride(0), stream_handle())
+    check(rc, "ntm_ref_gemm_f32")
+    return out
+
+
+@dataclass
+class VerifyReport:
+    n: int
+    bad: int
+    max_abs_err: float
+    rel_rms_err: float
+
+    @property
+    def ok(self) -> bool:
+        return self.bad == 0
+
+    def as_dict(self) -> dict:
+        return {"n": self.n, "bad": self.bad, "max_abs_err": self.max_abs_err,
+                "rel_rms_err": self.rel_rms_err, "ok": self.ok}
+
+
+def verify_bf16(c: torch.Tensor, ref: torch.Tensor, atol: float, rtol: float) -> VerifyReport:
+    """K3: element-wise ``|c - ref| <= atol + rtol*|ref|`` on device (synchronises)."""
+    if c.dtype != torch.bfloat16 or ref.dtype != torch.float32:
+        raise ValueError("verify_bf16 expects bf16 c and fp32 ref")
+    if c.shape != ref.shape or not c.is_contiguous() or not ref.is_contiguous():
+        raise ValueError("c and ref must be contiguous and of equal shape")
+    nbytes = lib().ntm_verify_result_bytes()
+    res = torch.zeros(nbytes, dtype=torch.uint8, device=c.device)
+    rc = lib().ntm_verify_bf16(c.data_ptr(), ref.data_ptr(), c.numel(), float(atol), float(rtol),
+                               res.data_ptr(), stream_handle())
+    check(rc, "ntm_verify_bf16")
+    raw = res.cpu().numpy().tobytes()
+    bad = int.from_bytes(raw[0:8], "little")
+    max_err = ctypes.c_float.from_buffer_copy(raw[8:12]).value
+    sse = ctypes.c_double.from_buffer_copy(raw[16:24]).value
+    ssr = ctypes.c_double.from_buffer_copy(raw[24:32]).value
+    rel = (sse / ssr) ** 0.5 if ssr > 0 else float("inf")
+    return VerifyReport(n=c.numel(), bad=bad, max_abs_err=max_err, rel_rms_err=rel)
+
+
+def stream_copy(src: torch.Tensor, dst: torch.Tensor) -> None:
+    """K2: float4 non-temporal HBM copy of ``src`` into ``dst`` (byte-identical)."""
+    nbytes = src.numel() * src.element_size()
+    if dst.numel() * dst.element_size() < nbytes or nbytes % 16:
+        raise ValueError("stream_copy needs 16-byte multiple sizes and a large enough dst")
+    check(lib().ntm_stream_copy(src.data_ptr(), dst.data_ptr(), nbytes, stream_handle()),
+          "ntm_stream_copy")
+
+
+def stream_read(src: torch.Tensor, sink: torch.Tensor) -> None:
+    """K2: read-only HBM sweep of ``src`` (``sink`` only written on NaN/inf)."""
+    nbytes = src.numel() * src.element_size()
+    if nbytes % 16:
+        raise ValueError("stream_read needs a 16-byte multiple size")
+    check(lib().ntm_stream_read(src.data_ptr(), nbytes, sink.data_ptr(), stream_handle()),
+          "ntm_stream_read")
+
+
+def gemm_tolerance(k: int) -> tuple[float, float]:
+    """(atol, rtol) for bf16-rounded output of an fp32-accumulated K-term dot product
+    of U[-1,1) operands: bf16 output rounding (2^-8 relative) dominates; the fp32
+    summation-order difference grows ~sqrt(K) * 2^-24 * |terms|."""
+    atol = 1e-3 + 4.0 * (k ** 0.5) * 2.0 ** -20
+    return atol, 2.0 ** -7

@@ -1,0 +1,321 @@
+// K1: bf16 GEMM on CDNA4 matrix cores (v_mfma_f32_16x16x32_bf16).
+//
+//   C[M x N] (bf16) = A[M x K] (bf16, row-major) * B[N x K]^T (bf16, row-major)
+//   fp32 accumulation, round-to-nearest-even on the way out.
+//
+// This is the validation-Job workload that replaces the NVIDIA GPU Operator's
+// CUDA validator (reference: helm_release.gpu_operator, /root/reference/eks/
+// main.tf:185-203, gke/main.tf:195-213, aks/main.tf:89-91). Spec: SURVEY.md
+// §2.7 K1. Design follows the CDNA4 playbook
+// (/opt/skills/guides/cdna_hip_programming.md §5 "256^2 8-phase template"),
+// re-derived here for a [N][K] B operand:
+//
+//  * 256x256 macro tile, BK = 64, 512 threads = 8 waves (2 M x 4 N). Each
+//    wave owns 4 quadrants of 64x32 outputs; 128 fp32 accumulators / lane.
+//  * Operands are staged HBM -> LDS with global_load_lds_dwordx4 (LDS-DMA,
+//    no VGPR round trip) into a 128 KiB double buffer cut into four 16 KiB
+//    half-tiles (A-lo, A-hi, B-lo, B-hi). Every half-tile is an array of
+//    16x32 bf16 subtiles (1 KiB = one MFMA fragment); inside a subtile the
+//    16-byte chunk index is XOR-swizzled with row bit 3, which makes the
+//    ds_read_b128 fragment read bank-conflict free. glds writes LDS lane-
+//    linearly, so the swizzle is applied to the per-lane SOURCE address and
+//    the same involution on the read (playbook §5.4 rule 21).
+//  * One K-tile = 4 phases; each phase = {ds_read fragments, issue one
+//    half-tile of LDS-DMA prefetch, counted vmcnt, s_barrier, 16 MFMAs,
+//    s_barrier}. Loads run 4-6 phases ahead of their reader, the counted
+//    s_waitcnt vmcnt(8) never drains the pipe inside the main loop, and the
+//    two wave groups (wr = 0 / 1) are staggered by one barrier so that on
+//    every SIMD one wave is in its MFMA segment while its partner reads LDS
+//    and issues DMA (ping-pong).
+//  * Bijective XCD-aware block remap + GROUP_M tile raster so that the 32
+//    co-resident tiles of one XCD share A/B panels in that XCD's L2.
+//
+// LDS-ordering proof (barrier indices; group 1 lags group 0 by one barrier):
+//  issue schedule  : phase 4t+0 B-hi(t+1), 4t+1 A-hi(t+1), 4t+2 A-lo(t+2),
+//                    4t+3 B-lo(t+2)    (prologue: A-lo0 B-lo0 B-hi0 A-hi0
+//                    A-lo1 B-lo1)
+//  read schedule   : phase 4t+0 A-lo(t),B-lo(t); 4t+1 B-hi(t); 4t+2 A-hi(t)
+//  RAW: a load issued in phase i is retired by vmcnt(8) in phase i+4 and may
+//       be read in phase >= i+5 by either group; min issue->read distance is 5.
+//  WAR: a half may be re-staged >= 2 phases after its last ds_read (reads are
+//       retired by the MFMAs that consume them before the phase's 2nd
+//       barrier); min distance in the schedule is 2 (A-lo).
+#pragma once
+
+#include "ntm/common.hpp"
+
+namespace ntm {
+namespace gemm {
+
+constexpr int BM = 256;
+constexpr int BN = 256;
+constexpr int BK = 64;
+constexpr int kThreads = 512;
+constexpr int kHalfBytes = 128 * BK * 2;    // 16 KiB: 128 rows x 64 k bf16
+constexpr int kTileBytes = 4 * kHalfBytes;  // A-lo, A-hi, B-lo, B-hi
+constexpr int kLdsBytes = 2 * kTileBytes;   // double buffer: 128 KiB
+constexpr int kGroupM = 8;                  // tile-raster group height
+
+enum : int { kALo = 0, kAHi = 1, kBLo = 2, kBHi = 3 };
+
+struct GemmArgs {
+  const __bf16* A;
+  const __bf16* B;
+  __bf16* C;
+  int M, N, K;
+  int lda, ldb, ldc;
+};
+
+// Shapes the fast kernel accepts; the host launcher rejects anything else.
+__host__ __device__ inline bool shape_ok(int M, int N, int K) {
+  return M > 0 && N > 0 && K >= 2 * BK && (M % BM) == 0 && (N % BN) == 0 &&
+         (K % BK) == 0;
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= -1 && N <= 8, "vmcnt range");
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+}
+
+// Raw workgroup barrier. NOT __syncthreads(): that one carries a fence that
+// makes hipcc emit s_waitcnt vmcnt(0), which would drain the LDS-DMA
+// prefetch in flight (playbook §5 "Pipelining across barriers").
+__device__ __forceinline__ void raw_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_barrier" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+__device__ __forceinline__ void glds16(const __bf16* gsrc, char* lds_dst) {
+  __builtin_amdgcn_global_load_lds((const void NTM_AS1*)gsrc,
+                                   (void NTM_AS3*)lds_dst, 16, 0, 0);
+}
+
+struct Frags {
+  bf16x8 a[4][2];   // [m-tile][k-step]   (64 rows of the current A half)
+  bf16x8 bl[2][2];  // [n-tile][k-step]   (32 cols of B-lo)
+  bf16x8 bh[2][2];  // [n-tile][k-step]   (32 cols of B-hi)
+};
+
+struct Ctx {
+  char* lds;             // LDS base (one __shared__ array only)
+  const __bf16* src[4];  // per-lane glds source for each half, K-tile 0
+  int frag_off;          // per-lane byte offset of an MFMA fragment read
+  int w, wr, wc;         // wave id, wave row (0..1), wave col (0..3)
+};
+
+// Issue the two glds of this wave for half-tile H of K-tile kt into buffer.
+template <int H>
+__device__ __forceinline__ void issue_half(const Ctx& c, int kt, int buf) {
+  const __bf16* s = c.src[H] + (size_t)kt * BK;
+  char* d = c.lds + buf * kTileBytes + H * kHalfBytes + (2 * c.w) * 1024;
+  glds16(s, d);
+  glds16(s + 32, d + 1024);
+}
+
+template <int H>
+__device__ __forceinline__ void read_a(const Ctx& c, Frags& f, int buf) {
+  const char* base = c.lds + buf * kTileBytes + H * kHalfBytes + c.frag_off;
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+      f.a[mt][ks] = *(const bf16x8*)(base + ((c.wr * 4 + mt) * 2 + ks) * 1024);
+}
+
+template <int H>
+__device__ __forceinline__ void read_b(const Ctx& c, bf16x8 (&b)[2][2],
+                                       int buf) {
+  const char* base = c.lds + buf * kTileBytes + H * kHalfBytes + c.frag_off;
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+      b[nt][ks] = *(const bf16x8*)(base + ((c.wc * 2 + nt) * 2 + ks) * 1024);
+}
+
+// 16 MFMAs: one 64x32 quadrant over K = 64. Operand order is swapped (B
+// fragment first) so each lane ends up holding 4 consecutive output columns
+// of one row -> 8-byte stores in the epilogue.
+__device__ __forceinline__ void mma_quadrant(f32x4 (&acc)[4][2],
+                                             const bf16x8 (&a)[4][2],
+                                             const bf16x8 (&b)[2][2]) {
+  __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt)
+        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+            b[nt][ks], a[mt][ks], acc[mt][nt], 0, 0, 0);
+  __builtin_amdgcn_s_setprio(0);
+}
+
+// One phase of the K loop. P: phase within the K-tile (0..3); ISSUE: whether
+// the prefetch item of this phase exists; VMC: counted vmcnt (-1 = none).
+template <int P, bool ISSUE, int VMC>
+__device__ __forceinline__ void phase(const Ctx& c, Frags& f,
+                                      f32x4 (&acc)[2][2][4][2], int t) {
+  const int cur = t & 1, nxt = cur ^ 1;
+  // 1. fragment reads for this phase
+  if constexpr (P == 0) {
+    read_b<kBLo>(c, f.bl, cur);
+    read_a<kALo>(c, f, cur);
+  } else if constexpr (P == 1) {
+    read_b<kBHi>(c, f.bh, cur);
+  } else if constexpr (P == 2) {
+    read_a<kAHi>(c, f, cur);
+  }
+  // 2. LDS-DMA prefetch of one half-tile
+  if constexpr (ISSUE) {
+    if constexpr (P == 0) issue_half<kBHi>(c, t + 1, nxt);
+    if constexpr (P == 1) issue_half<kAHi>(c, t + 1, nxt);
+    if constexpr (P == 2) issue_half<kALo>(c, t + 2, cur);
+    if constexpr (P == 3) issue_half<kBLo>(c, t + 2, cur);
+  }
+  // 3. retire the loads the NEXT phase reads (never vmcnt(0) in steady state)
+  wait_vmcnt<VMC>();
+  raw_barrier();
+  // 4. matrix work for one quadrant
+  if constexpr (P == 0) mma_quadrant(acc[0][0], f.a, f.bl);
+  if constexpr (P == 1) mma_quadrant(acc[0][1], f.a, f.bh);
+  if constexpr (P == 2) mma_quadrant(acc[1][1], f.a, f.bh);
+  if constexpr (P == 3) mma_quadrant(acc[1][0], f.a, f.bl);
+  raw_barrier();
+}
+
+// Block -> output tile. Bijective XCD remap (nwg % 8 != 0 safe), then a
+// GROUP_M raster inside each XCD's contiguous chunk.
+__device__ __forceinline__ void tile_coords(int M, int N, int& tm, int& tn) {
+  const int nwg = gridDim.x;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7;
+  const int q = nwg >> 3, r = nwg & 7;
+  const int wgid =
+      (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  const int tiles_m = M / BM, tiles_n = N / BN;
+  const int group = kGroupM * tiles_n;
+  const int gid = wgid / group;
+  const int first_m = gid * kGroupM;
+  const int gsz = min(tiles_m - first_m, kGroupM);
+  const int in_group = wgid - gid * group;
+  tm = first_m + in_group % gsz;
+  tn = in_group / gsz;
+}
+
+__global__ void __launch_bounds__(kThreads, 2)
+    gemm_bf16_256x256_kernel(GemmArgs p) {
+  __shared__ __attribute__((aligned(16))) char smem[kLdsBytes];
+
+  int tm, tn;
+  tile_coords(p.M, p.N, tm, tn);
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  Ctx c;
+  c.lds = smem;
+  const int lane = threadIdx.x & 63;
+  c.w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  c.wr = c.w >> 2;
+  c.wc = c.w & 3;
+  // glds: lane -> (stored row, stored chunk) of the wave's subtile; source is
+  // the logical chunk (inverse swizzle == swizzle, an involution).
+  {
+    const int r = lane >> 2;
+    const int cl = (lane & 3) ^ (((r >> 3) & 1) << 1);
+    const __bf16* a0 = p.A + (size_t)(m0 + c.w * 16 + r) * p.lda + cl * 8;
+    const __bf16* b0 = p.B + (size_t)(n0 + c.w * 16 + r) * p.ldb + cl * 8;
+    c.src[kALo] = a0;
+    c.src[kAHi] = a0 + (size_t)128 * p.lda;
+    c.src[kBLo] = b0;
+    c.src[kBHi] = b0 + (size_t)128 * p.ldb;
+  }
+  c.frag_off = (lane & 15) * 64 + ((lane >> 4) ^ ((lane >> 2) & 2)) * 16;
+
+  f32x4 acc[2][2][4][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int n = 0; n < 2; ++n) acc[i][j][m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  Frags f;
+  const int T = p.K / BK;
+
+  // Prologue: K-tile 0 complete + A-lo/B-lo of K-tile 1 (6 half-tiles).
+  issue_half<kALo>(c, 0, 0);
+  issue_half<kBLo>(c, 0, 0);
+  issue_half<kBHi>(c, 0, 0);
+  issue_half<kAHi>(c, 0, 0);
+  issue_half<kALo>(c, 1, 1);
+  issue_half<kBLo>(c, 1, 1);
+  wait_vmcnt<8>();
+  raw_barrier();
+  // Ping-pong stagger: wave row 1 runs one barrier behind wave row 0.
+  if (c.wr == 1) raw_barrier();
+
+  int t = 0;
+  for (; t < T - 2; ++t) {
+    phase<0, true, 8>(c, f, acc, t);
+    phase<1, true, 8>(c, f, acc, t);
+    phase<2, true, 8>(c, f, acc, t);
+    phase<3, true, 8>(c, f, acc, t);
+  }
+  // K-tile T-2: only K-tile T-1's hi halves remain to be loaded.
+  phase<0, true, 8>(c, f, acc, t);
+  phase<1, true, 8>(c, f, acc, t);
+  phase<2, false, 6>(c, f, acc, t);
+  phase<3, false, 4>(c, f, acc, t);
+  ++t;
+  // K-tile T-1: drain.
+  phase<0, false, 2>(c, f, acc, t);
+  phase<1, false, 0>(c, f, acc, t);
+  phase<2, false, -1>(c, f, acc, t);
+  phase<3, false, -1>(c, f, acc, t);
+  // balance the stagger so both groups execute the same barrier count
+  if (c.wr == 0) raw_barrier();
+
+  // Epilogue: lane holds C[row][col .. col+3] per 16x16 tile.
+#pragma unroll
+  for (int mh = 0; mh < 2; ++mh)
+#pragma unroll
+    for (int nh = 0; nh < 2; ++nh)
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) {
+          const int row = m0 + mh * 128 + c.wr * 64 + mt * 16 + (lane & 15);
+          const int col = n0 + nh * 128 + c.wc * 32 + nt * 16 + (lane >> 4) * 4;
+          const f32x4 v = acc[mh][nh][mt][nt];
+          typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+          bf16x4 o;
+          o[0] = (__bf16)v[0];
+          o[1] = (__bf16)v[1];
+          o[2] = (__bf16)v[2];
+          o[3] = (__bf16)v[3];
+          *(bf16x4*)(p.C + (size_t)row * p.ldc + col) = o;
+        }
+}
+
+// Host launcher. Returns hipErrorInvalidValue for shapes the kernel does not
+// tile (callers fall back to nothing: validation shapes are fixed).
+inline hipError_t launch_gemm_bf16(const GemmArgs& a, hipStream_t stream) {
+  if (!shape_ok(a.M, a.N, a.K) || a.lda < a.K || a.ldb < a.K || a.ldc < a.N ||
+      (a.lda % 8) || (a.ldb % 8) || (a.ldc % 4))
+    return hipErrorInvalidValue;
+  const unsigned grid = (unsigned)((a.M / BM) * (a.N / BN));
+  hipLaunchKernelGGL(gemm_bf16_256x256_kernel, dim3(grid), dim3(kThreads), 0,
+                     stream, a);
+  return hipGetLastError();
+}
+
+}  // namespace gemm
+}  // namespace ntm

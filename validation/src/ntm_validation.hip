@@ -1,0 +1,96 @@
+// C ABI over the MI355X validation kernels (K1 GEMM, K2 HBM stream,
+// K3 fill/reference/verify). Built for gfx950 only into
+//   nvidia_terraform_modules_amd/ops/libntm_validation.so   (Python, ctypes)
+//   validation/build/amdgpu-validate                        (Job entrypoint)
+// Every entry point is stream-ordered, allocation-free and sync-free, so it
+// can be captured in a hipGraph (playbook §6 Guideline 9).
+#include "ntm/aux_kernels.hpp"
+#include "ntm/gemm_bf16.hpp"
+
+#define NTM_API extern "C" __attribute__((visibility("default")))
+
+namespace {
+inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
+inline unsigned stream_grid(size_t work_items, unsigned block) {
+  // memory-bound: min(work / block, 256 CUs x 8 blocks)
+  size_t g = (work_items + block - 1) / block;
+  if (g > 2048) g = 2048;
+  if (g == 0) g = 1;
+  return (unsigned)g;
+}
+}  // namespace
+
+NTM_API const char* ntm_version() { return "ntm-validation 0.1.0 gfx950"; }
+
+NTM_API int ntm_gemm_shape_ok(int M, int N, int K) {
+  return ntm::gemm::shape_ok(M, N, K) ? 1 : 0;
+}
+
+NTM_API int ntm_gemm_bf16(const void* A, const void* B, void* C, int M, int N,
+                          int K, int lda, int ldb, int ldc, void* stream) {
+  ntm::gemm::GemmArgs a;
+  a.A = (const __bf16*)A;
+  a.B = (const __bf16*)B;
+  a.C = (__bf16*)C;
+  a.M = M;
+  a.N = N;
+  a.K = K;
+  a.lda = lda;
+  a.ldb = ldb;
+  a.ldc = ldc;
+  return (int)ntm::gemm::launch_gemm_bf16(a, S(stream));
+}
+
+NTM_API int ntm_fill_uniform_bf16(void* out, size_t n, unsigned long long seed,
+                                  float scale, void* stream) {
+  if (n == 0) return 0;
+  const unsigned grid = stream_grid((n + 7) / 8, 256);
+  hipLaunchKernelGGL(ntm::aux::fill_uniform_bf16_kernel, dim3(grid), dim3(256),
+                     0, S(stream), (__bf16*)out, n, (uint64_t)seed, scale);
+  return (int)hipGetLastError();
+}
+
+NTM_API int ntm_ref_gemm_f32(const void* A, const void* B, float* C, int M,
+                             int N, int K, int lda, int ldb, int ldc,
+                             void* stream) {
+  if (M <= 0 || N <= 0 || K <= 0) return (int)hipErrorInvalidValue;
+  dim3 grid((N + ntm::aux::kRefTile - 1) / ntm::aux::kRefTile,
+            (M + ntm::aux::kRefTile - 1) / ntm::aux::kRefTile);
+  hipLaunchKernelGGL(ntm::aux::ref_gemm_f32_kernel, grid, dim3(256), 0,
+                     S(stream), (const __bf16*)A, (const __bf16*)B, C, M, N, K,
+                     lda, ldb, ldc);
+  return (int)hipGetLastError();
+}
+
+// result: device pointer to a zeroed ntm::aux::VerifyResult (32 bytes)
+NTM_API int ntm_verify_bf16(const void* C, const float* R, size_t n,
+                            float atol, float rtol, void* result,
+                            void* stream) {
+  const unsigned grid = stream_grid(n, 256);
+  hipLaunchKernelGGL(ntm::aux::verify_bf16_kernel, dim3(grid), dim3(256), 0,
+                     S(stream), (const __bf16*)C, R, n, atol, rtol,
+                     (ntm::aux::VerifyResult*)result);
+  return (int)hipGetLastError();
+}
+
+NTM_API int ntm_verify_result_bytes() {
+  return (int)sizeof(ntm::aux::VerifyResult);
+}
+
+NTM_API int ntm_stream_copy(const void* src, void* dst, size_t bytes,
+                            void* stream) {
+  if (bytes % 16) return (int)hipErrorInvalidValue;
+  const size_t n4 = bytes / 16;
+  hipLaunchKernelGGL(ntm::aux::stream_copy_kernel, dim3(2048), dim3(256), 0,
+                     S(stream), (const ntm::f32x4*)src, (ntm::f32x4*)dst, n4);
+  return (int)hipGetLastError();
+}
+
+NTM_API int ntm_stream_read(const void* src, size_t bytes, float* sink,
+                            void* stream) {
+  if (bytes % 16) return (int)hipErrorInvalidValue;
+  const size_t n4 = bytes / 16;
+  hipLaunchKernelGGL(ntm::aux::stream_read_kernel, dim3(2048), dim3(256), 0,
+                     S(stream), (const ntm::f32x4*)src, n4, sink);
+  return (int)hipGetLastError();
+}
