@@ -1,0 +1,195 @@
+#!/usr/bin/env python3
+"""Headline benchmark: validation-Job bf16 GEMM TFLOP/s on 1/2/4/8 MI355X.
+
+BASELINE.json metric: "cluster time-to-GPU-ready (s) + validation HIP GEMM
+TFLOPS at 1/2/4/8 MI355X". The cloud half (apply -> Job Succeeded) cannot run
+without a cloud account; this measures the GPU half on real hardware:
+
+* one process per GPU (``torch.distributed.run``), RCCL over xGMI,
+* each step = one hand-written K1 GEMM, M = N = K = 8192 bf16 (fp32 acc) per
+  GPU on synthetic uniform[-1,1) operands generated on device (weak scaling),
+* W untimed warmup steps, then EXACTLY K steps bracketed by barrier +
+  synchronize, max over ranks; ``value`` = aggregate TFLOP/s over all GPUs,
+* after the timed region (never inside it): full-matrix verification against
+  an independent fp32 reference, hipBLASLt comparison on the same data, K2 HBM
+  check, C1 RCCL all-reduce busbw sweep (N > 1), and the in-node
+  time-to-GPU-ready phases (process start -> HIP init -> verified).
+
+Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--size 8192]
+For N > 1 the driver launches it under ``torch.distributed.run``; launched
+directly with --gpus N > 1 it starts that launcher as a child process.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+from nvidia_terraform_modules_amd.gpu_ready.phases import PhaseClock
+
+_CLOCK = PhaseClock()
+
+METRIC = "validation HIP GEMM TFLOPS at 1/2/4/8 MI355X"
+BASELINE_METRIC = "cluster time-to-GPU-ready (s) + validation HIP GEMM TFLOPS at 1/2/4/8 MI355X"
+BASELINE_CONFIG = ("EKS 8xMI355X node, amdgpu-dkms DaemonSet + 288 GB HBM sizing, "
+                   "full 1/2/4/8-GPU scaling sweep")
+
+
+def parse(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--size", type=int, default=8192, help="M = N = K of the per-GPU GEMM")
+    ap.add_argument("--no-check", action="store_true", help="skip full-matrix verification")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="skip hipBLASLt comparison, HBM and all-reduce sweeps")
+    ap.add_argument("--allreduce-max-mib", type=int, default=1024)
+    ap.add_argument("--out", default="", help="also write the JSON line to this file")
+    return ap.parse_args(argv)
+
+
+def relaunch_distributed(args) -> int:
+    """Start torch.distributed.run as a CHILD process (never exec) and return its rc."""
+    port = os.environ.get("MASTER_PORT", "29531")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1", f"--master-port={port}",
+           os.path.abspath(__file__), *sys.argv[1:]]
+    return subprocess.call(cmd)
+
+
+def main(argv=None) -> int:
+    args = parse(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return relaunch_distributed(args)
+
+    import torch
+
+    from nvidia_terraform_modules_amd import ops
+    from nvidia_terraform_modules_amd.models.validation_job import GemmWorkload, hbm_check
+    from nvidia_terraform_modules_amd.parallel import collectives as coll
+    from nvidia_terraform_modules_amd.parallel import dist
+
+    _CLOCK.mark("runtime_import")
+    env = dist.init()
+    if env.world_size != args.gpus and env.is_main:
+        print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={env.world_size}; "
+              f"using WORLD_SIZE", file=sys.stderr)
+    n = env.world_size
+    dev = env.device
+    _ = torch.empty(1, device=dev)
+    _CLOCK.mark("hip_init")
+
+    wl = GemmWorkload(args.size, dev, seed=20250117 + env.rank)
+    torch.cuda.synchronize(dev)
+    _CLOCK.mark("buffers_ready")
+
+    # ---- warmup (untimed)
+    for _ in range(max(1, args.warmup)):
+        wl.step()
+    torch.cuda.synchronize(dev)
+    _CLOCK.mark("first_kernel")
+
+    # ---- timed region: exactly K steps, barrier + sync on both sides
+    dist.barrier(env)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        wl.step()
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    dist.barrier(env)
+    elapsed = dist.all_reduce_max(env, t1 - t0)
+    ms_per_step = elapsed / args.steps * 1e3
+    total_tflops = n * wl.flops * args.steps / elapsed / 1e12
+
+    # ---- after the timed region: verification + context measurements
+    extras: dict = {}
+    verified = None
+    if not args.no_check:
+        rep = wl.verify()
+        bad = dist.all_reduce_sum(env, float(rep.bad))
+        verified = bad == 0
+        extras["verify_rank0"] = rep.as_dict()
+        extras["verify_bad_total"] = int(bad)
+    _CLOCK.mark("gemm_verified")
+
+    if not args.no_extras:
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        cc = torch.empty_like(wl.c)
+        for _ in range(5):
+            torch.matmul(wl.a, wl.b.T, out=cc)
+        ev[0].record()
+        for _ in range(50):
+            torch.matmul(wl.a, wl.b.T, out=cc)
+        ev[1].record()
+        torch.cuda.synchronize(dev)
+        hb_ms = ev[0].elapsed_time(ev[1]) / 50
+        extras["hipblaslt_tflops_per_gpu_rank0"] = wl.flops / hb_ms / 1e9
+        extras["ours_tflops_per_gpu"] = total_tflops / n
+        del cc
+    del wl
+    torch.cuda.empty_cache()
+
+    if not args.no_extras:
+        h = hbm_check(dev, 2 << 30, 10)
+        extras["hbm_copy_GBps_rank0"] = h["copy_GBps"]
+        extras["hbm_read_GBps_rank0"] = h["read_GBps"]
+        extras["hbm_capacity_gb"] = h["capacity_total_gb"]
+    _CLOCK.mark("hbm_checked")
+
+    if not args.no_extras and n > 1:
+        sizes = coll.sweep_sizes(1 << 20, args.allreduce_max_mib << 20, factor=4)
+        res = coll.all_reduce_sweep(env, sizes, dtype="bf16", iters=10, warmup=3)
+        extras["allreduce_bf16"] = [
+            {"bytes": r.bytes, "time_us": round(r.time_us, 1), "busbw_GBps": round(r.busbw_GBps, 1),
+             "errors": r.errors} for r in res]
+        extras["allreduce_peak_busbw_GBps"] = coll.peak_busbw(res)
+        if any(r.errors for r in res):
+            verified = False
+    _CLOCK.mark("collectives_checked")
+    _CLOCK.mark("done")
+
+    line = {
+        "metric": METRIC,
+        "value": round(total_tflops, 2),
+        "unit": "TFLOP/s",
+        "n_gpus": n,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "bf16",
+        "data": "synthetic (uniform[-1,1) bf16 operands generated on device, hash RNG)",
+        "config": {
+            "model": f"validation-job K1 GEMM C[{args.size}x{args.size}] = A[{args.size}x{args.size}]"
+                     f" * B[{args.size}x{args.size}]^T, bf16 in/out, fp32 accumulate",
+            "global_batch": n,
+            "seq_len": args.size,
+            "parallelism": f"dp{n}",
+            "baseline_metric": BASELINE_METRIC,
+            "baseline_config": BASELINE_CONFIG,
+        },
+        "verified": verified,
+        "time_to_gpu_ready_in_node_s": round(_CLOCK.elapsed("gemm_verified"), 3),
+        "in_node_phases_s": {k: round(v, 4) for k, v in _CLOCK.durations().items()},
+        "vs_baseline_note": "reference publishes no TFLOP/s or busbw (BASELINE.json published={})",
+        **extras,
+    }
+    if env.is_main:
+        s = json.dumps(line)
+        print(s, flush=True)
+        if args.out:
+            with open(args.out, "w") as f:
+                f.write(s + "\n")
+    dist.shutdown(env)
+    return 0 if verified in (None, True) else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())

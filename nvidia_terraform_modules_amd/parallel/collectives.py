@@ -1,0 +1,139 @@
+"""C1: all-reduce bandwidth sweep (nccl-tests semantics) over RCCL / xGMI.
+
+SURVEY.md §2.7 C1: ``AllReduce(sum, bf16 and fp32)``, sizes 8 B -> 8 GiB
+doubling, ranks 2/4/8 on one node, one process + one GPU per rank, report
+algbw and busbw = algbw * 2(n-1)/n.
+
+MI355X sizing notes (not a translation of any NCCL pattern; the reference
+has none): an 8x MI355X node is a fully connected xGMI mesh, 7 links x
+~153 GB/s per GPU. A ring moves every chunk over one link per hop, so a single
+ring is per-link bound; RCCL gets more by running channels over disjoint
+links. The hand-written mesh path in :mod:`.xgmi` drives all 7 links at once.
+
+Correctness: rank r contributes ``r + 1`` (plus a position-dependent integer
+pattern small enough to stay exact in bf16), so the expected sum is known
+exactly and every element is checked, not a sample.
+"""
+from __future__ import annotations
+
+import math
+import time
+from dataclasses import asdict, dataclass
+
+import torch
+import torch.distributed as tdist
+
+from .dist import DistEnv, all_reduce_max, barrier
+
+_DTYPES = {"bf16": torch.bfloat16, "fp32": torch.float32, "fp16": torch.float16}
+
+
+def bus_factor(op: str, n: int) -> float:
+    """nccl-tests bus-bandwidth factor for ``op`` at ``n`` ranks."""
+    if n <= 1:
+        return 1.0 if op != "all_reduce" else 0.0
+    if op == "all_reduce":
+        return 2.0 * (n - 1) / n
+    if op in ("all_gather", "reduce_scatter", "all_to_all"):
+        return (n - 1) / n
+    if op in ("broadcast", "reduce"):
+        return 1.0
+    raise ValueError(op)
+
+
+def sweep_sizes(min_bytes: int, max_bytes: int, factor: int = 2) -> list[int]:
+    if min_bytes <= 0 or max_bytes < min_bytes or factor < 2:
+        raise ValueError("bad sweep bounds")
+    out, s = [], min_bytes
+    while s <= max_bytes:
+        out.append(s)
+        s *= factor
+    return out
+
+
+@dataclass
+class CollResult:
+    op: str
+    dtype: str
+    bytes: int
+    count: int
+    ranks: int
+    time_us: float
+    algbw_GBps: float
+    busbw_GBps: float
+    errors: int
+
+    def as_dict(self) -> dict:
+        return asdict(self)
+
+
+def _pattern(count: int, rank: int, dtype: torch.dtype, device) -> torch.Tensor:
+    # 2^(i%4) * (rank+1): every partial sum is 2^j * s with s <= n(n+1)/2 <= 36
+    # for n <= 8, an integer < 256 -> exact in bf16 whatever the reduction order
+    base = torch.bitwise_left_shift(torch.ones(count, device=device, dtype=torch.int64),
+                                    torch.arange(count, device=device, dtype=torch.int64) % 4)
+    return (base * (rank + 1)).to(dtype)
+
+
+def _expected(count: int, n: int, dtype: torch.dtype, device) -> torch.Tensor:
+    base = torch.bitwise_left_shift(torch.ones(count, device=device, dtype=torch.int64),
+                                    torch.arange(count, device=device, dtype=torch.int64) % 4)
+    return (base * (n * (n + 1) // 2)).to(dtype)
+
+
+def _sync(env: DistEnv) -> None:
+    if env.device.type == "cuda":
+        torch.cuda.synchronize(env.device)
+
+
+def all_reduce_sweep(env: DistEnv, sizes: list[int], dtype: str = "bf16", iters: int = 20,
+                     warmup: int = 5, check: bool = True,
+                     impl=None) -> list[CollResult]:
+    """Time ``all_reduce(sum)`` at every size; returns one result per size.
+
+    ``impl(tensor)`` overrides the collective (e.g. the xGMI mesh path); the
+    default is ``torch.distributed.all_reduce`` (RCCL on GPUs, gloo on CPU).
+    """
+    tdt = _DTYPES[dtype]
+    esz = torch.empty((), dtype=tdt).element_size()
+    n = env.world_size
+    run = impl or (lambda t: tdist.all_reduce(t) if n > 1 else None)
+    results = []
+    for nbytes in sizes:
+        count = max(1, nbytes // esz)
+        buf = _pattern(count, env.rank, tdt, env.device)
+        errors = 0
+        if check:
+            run(buf)
+            _sync(env)
+            exp = _expected(count, n, tdt, env.device)
+            errors = int((buf != exp).sum().item())
+        for _ in range(warmup):
+            run(buf)
+        _sync(env)
+        barrier(env)
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            run(buf)
+        _sync(env)
+        dt = (time.perf_counter() - t0) / iters
+        dt = all_reduce_max(env, dt)
+        algbw = count * esz / dt / 1e9 if dt > 0 else math.inf
+        results.append(CollResult(
+            op="all_reduce", dtype=dtype, bytes=count * esz, count=count, ranks=n,
+            time_us=dt * 1e6, algbw_GBps=algbw, busbw_GBps=algbw * bus_factor("all_reduce", n),
+            errors=errors))
+    return results
+
+
+def peak_busbw(results: list[CollResult]) -> float:
+    return max((r.busbw_GBps for r in results), default=0.0)
+
+
+def format_table(results: list[CollResult]) -> str:
+    lines = [f"{'bytes':>12} {'count':>11} {'type':>5} {'time(us)':>10} {'algbw(GB/s)':>12} "
+             f"{'busbw(GB/s)':>12} {'#wrong':>7}"]
+    for r in results:
+        lines.append(f"{r.bytes:>12d} {r.count:>11d} {r.dtype:>5} {r.time_us:>10.1f} "
+                     f"{r.algbw_GBps:>12.2f} {r.busbw_GBps:>12.2f} {r.errors:>7d}")
+    return "\n".join(lines)

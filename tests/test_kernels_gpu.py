@@ -1,0 +1,131 @@
+"""GPU numerics for the gfx950 kernels: every HIP kernel vs a plain PyTorch
+fp32 reference of the same op (run on a real MI355X via gpurun)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ops():
+    from nvidia_terraform_modules_amd import ops as o
+    from nvidia_terraform_modules_amd.ops import _lib
+
+    _lib.lib()  # must load the in-tree native library: no fallback
+    assert _lib.LIB_PATH.exists()
+    return o
+
+
+def _rand(ops, shape, seed):
+    t = torch.empty(shape, dtype=torch.bfloat16, device="cuda")
+    return ops.fill_uniform_(t, seed)
+
+
+@pytest.mark.parametrize("m,n,k", [
+    (256, 256, 128), (512, 768, 320), (768, 512, 1024), (1024, 1024, 4096),
+    (2048, 256, 192), (256, 2304, 256), (4096, 4096, 4096),
+])
+def test_gemm_vs_torch_fp32(ops, m, n, k):
+    a = _rand(ops, (m, k), 11 + m)
+    b = _rand(ops, (n, k), 13 + n)
+    c = ops.gemm_bf16(a, b)
+    ref = a.float() @ b.float().T
+    atol, rtol = ops.gemm_tolerance(k)
+    err = (c.float() - ref).abs()
+    assert torch.all(err <= atol + rtol * ref.abs()), float(err.max())
+    rel = (err.pow(2).sum() / ref.pow(2).sum()).sqrt().item()
+    assert rel < 4e-3
+
+
+def test_gemm_identity_asymmetric(ops):
+    # A = I with an asymmetric B catches a transposed C-write (playbook §3).
+    n, k = 256, 256
+    a = torch.eye(n, k, dtype=torch.bfloat16, device="cuda")
+    b = (torch.arange(n * k, device="cuda", dtype=torch.float32).reshape(n, k) % 97 - 48).to(torch.bfloat16)
+    c = ops.gemm_bf16(a, b)
+    assert torch.equal(c, b.T.contiguous())
+
+
+def test_gemm_strided_ld(ops):
+    m, n, k = 512, 512, 256
+    abig = _rand(ops, (m, k + 64), 3)
+    bbig = _rand(ops, (n, k + 128), 4)
+    a, b = abig[:, :k], bbig[:, :k]
+    out = torch.zeros((m, n + 256), dtype=torch.bfloat16, device="cuda")
+    ops.gemm_bf16(a, b, out[:, :n])
+    ref = a.float() @ b.float().T
+    atol, rtol = ops.gemm_tolerance(k)
+    assert torch.all((out[:, :n].float() - ref).abs() <= atol + rtol * ref.abs())
+    assert torch.count_nonzero(out[:, n:]) == 0  # no write past the ldc window
+
+
+def test_gemm_rejects_bad_shapes(ops):
+    a = torch.zeros((300, 256), dtype=torch.bfloat16, device="cuda")
+    b = torch.zeros((256, 256), dtype=torch.bfloat16, device="cuda")
+    with pytest.raises(ValueError):
+        ops.gemm_bf16(a, b)
+    with pytest.raises(ValueError):
+        ops.gemm_bf16(b[:, :64], b[:, :64])  # K < 128
+
+
+def test_fill_uniform_distribution(ops):
+    t = _rand(ops, (1 << 20,), 99)
+    f = t.float()
+    assert f.min() >= -1.0 and f.max() <= 1.0
+    assert abs(f.mean().item()) < 5e-3
+    assert abs(f.var().item() - 1.0 / 3.0) < 5e-3
+    t2 = _rand(ops, (1 << 20,), 99)
+    assert torch.equal(t, t2)  # deterministic in (seed, index)
+    t3 = _rand(ops, (1 << 20,), 100)
+    assert not torch.equal(t, t3)
+
+
+def test_ref_gemm_matches_torch(ops):
+    a = _rand(ops, (96, 200), 5)   # odd shapes: reference kernel is general
+    b = _rand(ops, (70, 200), 6)
+    r = ops.ref_gemm_f32(a, b)
+    t = a.float() @ b.float().T
+    assert torch.allclose(r, t, atol=1e-4, rtol=1e-5)
+
+
+def test_verify_detects_corruption(ops):
+    a = _rand(ops, (512, 256), 1)
+    b = _rand(ops, (512, 256), 2)
+    c = ops.gemm_bf16(a, b)
+    ref = ops.ref_gemm_f32(a, b)
+    atol, rtol = ops.gemm_tolerance(256)
+    assert ops.verify_bf16(c, ref, atol, rtol).ok
+    c.view(-1)[777] += 2.0
+    c.view(-1)[778] = float("nan")
+    rep = ops.verify_bf16(c, ref, atol, rtol)
+    assert rep.bad == 2 and not rep.ok
+
+
+def test_stream_copy_and_read(ops):
+    src = torch.randn(1 << 22, device="cuda")
+    dst = torch.empty_like(src)
+    ops.stream_copy(src, dst)
+    sink = torch.zeros(2048, device="cuda")
+    ops.stream_read(src, sink)
+    torch.cuda.synchronize()
+    assert torch.equal(src, dst)
+    assert torch.count_nonzero(sink) == 0
+
+
+def test_gemm_graph_capture(ops):
+    a = _rand(ops, (1024, 512), 21)
+    b = _rand(ops, (1024, 512), 22)
+    c = torch.empty((1024, 1024), dtype=torch.bfloat16, device="cuda")
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        ops.gemm_bf16(a, b, c)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        ops.gemm_bf16(a, b, c)
+    c.zero_()
+    g.replay()
+    torch.cuda.synchronize()
+    ref = a.float() @ b.float().T
+    atol, rtol = ops.gemm_tolerance(512)
+    assert torch.all((c.float() - ref).abs() <= atol + rtol * ref.abs())
