@@ -1,0 +1,119 @@
+/********************************************
+  Post-provision validation Job
+  -----------------------------
+  The reference has no readiness gate: `apply` returns before the NVIDIA
+  operator has even loaded a driver (~5 min later per gke/README.md:50) and
+  its helm_release count-gate on data.aws_instances never actually waits
+  (eks/main.tf:186). Here `apply` blocks on a Job that requests amd.com/gpu
+  (so it only schedules once the device plugin has registered GPUs) and runs
+  the hand-written HIP bf16 MFMA GEMM + HBM stream + RCCL all-reduce over
+  xGMI. Job completion timestamp == end of time-to-GPU-ready.
+********************************************/
+locals {
+  validation_args = [
+    "--gpus", tostring(var.validation_gpu_count),
+    "--size", tostring(var.validation_gemm_size),
+    "--tflops-floor", tostring(var.validation_tflops_floor),
+    "--min-hbm-gb", tostring(var.validation_min_hbm_gb),
+    "--allreduce-max-mib", tostring(var.validation_allreduce_max_mib),
+    "--json",
+  ]
+  validation_env = merge({
+    # RCCL over the xGMI mesh inside one node; no host network transport needed
+    NCCL_IB_DISABLE      = "1"
+    NCCL_SOCKET_IFNAME   = "lo"
+    HSA_NO_SCRATCH_RECLAIM = "1"
+  }, var.validation_env)
+}
+
+resource "kubernetes_job_v1" "gpu_validation" {
+  count = var.validation_enabled ? 1 : 0
+
+  metadata {
+    name      = "amd-gpu-validation"
+    namespace = local.namespace
+    labels    = merge(local.common_labels, { "app.kubernetes.io/name" = "amd-gpu-validation" })
+    annotations = {
+      "amd-gpu-stack/gpu-node-pools" = local.node_pool_hash
+      "amd-gpu-stack/stack-mode"     = var.gpu_stack_mode
+    }
+  }
+
+  spec {
+    backoff_limit              = var.validation_backoff_limit
+    active_deadline_seconds    = var.validation_active_deadline_seconds
+    ttl_seconds_after_finished = 86400
+    completions                = 1
+    parallelism                = 1
+
+    template {
+      metadata {
+        labels = merge(local.common_labels, { "app.kubernetes.io/name" = "amd-gpu-validation" })
+      }
+      spec {
+        restart_policy = "Never"
+        host_ipc       = true # RCCL peer-to-peer IPC between the ranks' GPU buffers
+        node_selector  = var.gpu_node_selector
+
+        toleration {
+          key      = var.gpu_node_taint_key
+          operator = "Exists"
+          effect   = "NoSchedule"
+        }
+
+        container {
+          name    = "amdgpu-validate"
+          image   = var.validation_image
+          command = ["/opt/ntm/bin/amdgpu-validate"]
+          args    = local.validation_args
+
+          dynamic "env" {
+            for_each = local.validation_env
+            content {
+              name  = env.key
+              value = env.value
+            }
+          }
+
+          resources {
+            limits = {
+              (local.gpu_resource) = tostring(var.validation_gpu_count)
+              memory               = "64Gi"
+            }
+            requests = {
+              (local.gpu_resource) = tostring(var.validation_gpu_count)
+              cpu                  = tostring(var.validation_gpu_count * 2)
+              memory               = "32Gi"
+            }
+          }
+
+          volume_mount {
+            name       = "dshm"
+            mount_path = "/dev/shm"
+          }
+        }
+
+        volume {
+          name = "dshm"
+          empty_dir {
+            medium     = "Memory"
+            size_limit = "16Gi"
+          }
+        }
+      }
+    }
+  }
+
+  wait_for_completion = var.wait_for_validation
+
+  timeouts {
+    create = var.validation_timeout
+    update = var.validation_timeout
+  }
+
+  depends_on = [
+    helm_release.device_config,
+    kubernetes_daemon_set_v1.rocm_device_plugin,
+    kubernetes_daemon_set_v1.amdgpu_dkms,
+  ]
+}

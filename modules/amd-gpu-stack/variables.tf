@@ -1,0 +1,255 @@
+/************************
+  Identity
+*************************/
+variable "cluster_name" {
+  type        = string
+  description = "Name of the Kubernetes cluster (used for labels and object names)."
+}
+
+variable "labels" {
+  type        = map(string)
+  default     = {}
+  description = "Extra labels applied to every Kubernetes object this module creates."
+}
+
+/************************
+  Deployment mode
+*************************/
+variable "gpu_stack_mode" {
+  type        = string
+  default     = "operator"
+  description = "How the amdgpu driver and the amd.com/gpu device plugin get onto GPU nodes: \"operator\" (AMD GPU Operator Helm chart + DeviceConfig CR) or \"daemonsets\" (explicit amdgpu-dkms installer + rocm/k8s-device-plugin + node labeller DaemonSets, no operator)."
+
+  validation {
+    condition     = contains(["operator", "daemonsets"], var.gpu_stack_mode)
+    error_message = "gpu_stack_mode must be \"operator\" or \"daemonsets\"."
+  }
+}
+
+/************************
+  AMD GPU Operator (names kept from the reference's gpu_operator_* variables)
+*************************/
+variable "gpu_operator_version" {
+  type        = string
+  default     = "v1.3.0"
+  description = "AMD GPU Operator Helm chart version (chart gpu-operator-charts). Pin a release that lists gfx950 / MI355X support."
+}
+
+variable "gpu_operator_driver_version" {
+  type        = string
+  default     = "7.0.2"
+  description = "amdgpu kernel driver version (ROCm release) the operator / DKMS installer puts on GPU nodes. ROCm 7.x is required for gfx950."
+
+  validation {
+    condition     = can(regex("^[0-9]+\\.[0-9]+(\\.[0-9]+)?$", var.gpu_operator_driver_version)) && tonumber(split(".", var.gpu_operator_driver_version)[0]) >= 7
+    error_message = "gpu_operator_driver_version must be a ROCm release >= 7.0 (MI355X / gfx950 needs ROCm 7)."
+  }
+}
+
+variable "gpu_operator_namespace" {
+  type        = string
+  default     = "kube-amd-gpu"
+  description = "Namespace for the AMD GPU Operator / device plugin / exporter / validation Job."
+}
+
+variable "gpu_operator_chart_repository" {
+  type        = string
+  default     = "https://rocm.github.io/gpu-operator"
+  description = "Helm repository of the AMD GPU Operator chart."
+}
+
+variable "gpu_operator_chart_name" {
+  type        = string
+  default     = "gpu-operator-charts"
+  description = "Chart name inside gpu_operator_chart_repository."
+}
+
+variable "create_namespace" {
+  type        = bool
+  default     = true
+  description = "Create gpu_operator_namespace (set false when it already exists)."
+}
+
+variable "critical_pod_quota" {
+  type        = bool
+  default     = false
+  description = "Create a ResourceQuota admitting system-node-critical / system-cluster-critical pods in the namespace (required on GKE for critical-priority DaemonSets outside kube-system; reference gke/main.tf:173-191)."
+}
+
+variable "install_node_feature_discovery" {
+  type        = bool
+  default     = true
+  description = "Let the operator chart install Node Feature Discovery (labels feature.node.kubernetes.io/amd-gpu)."
+}
+
+variable "helm_timeout_seconds" {
+  type        = number
+  default     = 900
+  description = "Helm wait timeout for the operator release."
+}
+
+/************************
+  Driver / device plugin / labeller / exporter
+*************************/
+variable "driver_enabled" {
+  type        = bool
+  default     = true
+  description = "Install the amdgpu driver on GPU nodes (false only for node images that ship amdgpu for gfx950 already)."
+}
+
+variable "driver_image_repository" {
+  type        = string
+  default     = ""
+  description = "Optional registry for operator-built driver images (DeviceConfig spec.driver.image). Empty = operator default."
+}
+
+variable "amdgpu_dkms_image" {
+  type        = string
+  default     = "docker.io/library/ubuntu:22.04"
+  description = "daemonsets mode: image of the privileged, hostPID installer pod; it only needs nsenter (util-linux) because the install runs in the host's namespaces."
+}
+
+variable "amdgpu_repo_base_url" {
+  type        = string
+  default     = "https://repo.radeon.com/amdgpu-install"
+  description = "daemonsets mode: base URL of the amdgpu-install packages (mirror it for air-gapped node pools)."
+}
+
+variable "device_plugin_image" {
+  type        = string
+  default     = "docker.io/rocm/k8s-device-plugin:1.31.0.7"
+  description = "rocm/k8s-device-plugin image (registers amd.com/gpu with the kubelet)."
+}
+
+variable "node_labeller_image" {
+  type        = string
+  default     = "docker.io/rocm/k8s-device-plugin:labeller-1.31.0.7"
+  description = "rocm/k8s-device-plugin node labeller image (amd.com/gpu.family, .device-id, .vram ...)."
+}
+
+variable "metrics_exporter_enabled" {
+  type        = bool
+  default     = true
+  description = "Deploy the AMD device-metrics-exporter (GPU utilisation, HBM, power, xGMI counters) on GPU nodes."
+}
+
+variable "metrics_exporter_image" {
+  type        = string
+  default     = "docker.io/rocm/device-metrics-exporter:v1.3.0"
+  description = "AMD device-metrics-exporter image."
+}
+
+variable "metrics_exporter_port" {
+  type        = number
+  default     = 5000
+  description = "Port the metrics exporter serves Prometheus metrics on."
+}
+
+variable "service_monitor_enabled" {
+  type        = bool
+  default     = false
+  description = "Create a Prometheus-operator ServiceMonitor for the exporter (needs the monitoring.coreos.com CRDs, e.g. from the CNPack Prometheus stack)."
+}
+
+variable "gpu_node_selector" {
+  type        = map(string)
+  default     = { "amd.com/gpu.present" = "true" }
+  description = "Node labels that identify MI355X GPU nodes (set by the node pools of the root modules)."
+}
+
+variable "gpu_node_taint_key" {
+  type        = string
+  default     = "amd.com/gpu"
+  description = "Taint key placed on GPU node pools; every GPU DaemonSet / Job tolerates it."
+}
+
+variable "gpu_node_pool_ids" {
+  type        = list(string)
+  default     = []
+  description = "IDs of the GPU node pools. Only the validation Job depends on them, so the namespace / operator / DeviceConfig install overlaps with GPU node boot (the operator controller runs on CPU nodes)."
+}
+
+/************************
+  Post-provision validation Job
+*************************/
+variable "validation_enabled" {
+  type        = bool
+  default     = true
+  description = "Run the MI355X validation Job (HIP bf16 MFMA GEMM + HBM stream + RCCL all-reduce over xGMI) after the stack is up."
+}
+
+variable "validation_image" {
+  type        = string
+  default     = "ghcr.io/amd-instinct-terraform-modules/amdgpu-validate:0.1.0"
+  description = "Image built from validation/image/Dockerfile (contains only the amdgpu-validate binary + ROCm runtime + RCCL)."
+}
+
+variable "validation_gpu_count" {
+  type        = number
+  default     = 8
+  description = "amd.com/gpu requested by the validation Job (1, 2, 4 or 8 MI355X on one node)."
+
+  validation {
+    condition     = contains([1, 2, 4, 8], var.validation_gpu_count)
+    error_message = "validation_gpu_count must be 1, 2, 4 or 8 (GPUs of one MI355X node)."
+  }
+}
+
+variable "validation_gemm_size" {
+  type        = number
+  default     = 8192
+  description = "M = N = K of the per-GPU validation GEMM (multiple of 256)."
+
+  validation {
+    condition     = var.validation_gemm_size >= 256 && var.validation_gemm_size % 256 == 0
+    error_message = "validation_gemm_size must be a positive multiple of 256."
+  }
+}
+
+variable "validation_tflops_floor" {
+  type        = number
+  default     = 1000
+  description = "Per-GPU bf16 GEMM TFLOP/s below which the Job fails (MI355X dense bf16 peak ~2500; the hand-written kernel measures ~1490 at 8192^3)."
+}
+
+variable "validation_min_hbm_gb" {
+  type        = number
+  default     = 250
+  description = "Per-GPU HBM capacity floor in GB (MI355X: 288 GB HBM3E)."
+}
+
+variable "validation_allreduce_max_mib" {
+  type        = number
+  default     = 1024
+  description = "Largest RCCL all-reduce message in the busbw sweep."
+}
+
+variable "validation_backoff_limit" {
+  type        = number
+  default     = 1
+  description = "Job backoffLimit."
+}
+
+variable "validation_active_deadline_seconds" {
+  type        = number
+  default     = 900
+  description = "Job activeDeadlineSeconds (hard stop for a hung GPU)."
+}
+
+variable "validation_timeout" {
+  type        = string
+  default     = "20m"
+  description = "How long terraform waits for the Job to complete (wait_for_completion)."
+}
+
+variable "wait_for_validation" {
+  type        = bool
+  default     = true
+  description = "Make terraform apply block until the validation Job succeeded: apply returning == GPUs proven usable."
+}
+
+variable "validation_env" {
+  type        = map(string)
+  default     = {}
+  description = "Extra environment for the validation container (e.g. NCCL_DEBUG=INFO)."
+}

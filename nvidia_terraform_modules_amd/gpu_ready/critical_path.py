@@ -1,0 +1,159 @@
+"""Offline time-to-GPU-ready model: critical path through the plan graph.
+
+Terraform applies independent nodes in parallel (default -parallelism=10),
+so apply wall time ~= the longest dependency chain weighted by each node's
+create time. This module weights the graph from
+:mod:`nvidia_terraform_modules_amd.tfcheck.graph` with per-resource-type
+durations and returns the critical path and its length, split into the six
+BASELINE phases.
+
+The durations are PRIORS (documented cloud-API behaviour, [ext]) and are
+meant to be replaced by measured ones: :func:`durations_from_timeline`
+derives them from a ``terraform apply -json`` log (see
+:mod:`.apply_timeline`), and the in-node validation phase is measured on real
+MI355X hardware by ``bench.py`` / the validation binary.
+
+Reference anchor: the only number the reference publishes is the ~5 min from
+"apply returned" to "GPU operator Running" (/root/reference/gke/README.md:50),
+i.e. work that happens OFF its critical path after apply; here that work is
+ON the path (apply waits for the validation Job), so the comparable figure is
+operator_deployed -> validation_done.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+from ..tfcheck.graph import Graph
+
+# seconds; priors by resource type / module source (EKS/GKE/AKS docs [ext])
+DEFAULT_DURATIONS = {
+    # network
+    "module.vpc": 150.0,                     # VPC + subnets + NAT gateways
+    "google_compute_network": 25.0,
+    "google_compute_subnetwork": 20.0,
+    "azurerm_resource_group": 5.0,
+    # control plane
+    "module.eks": 780.0,                     # cluster ACTIVE (~10 min) + node groups
+    "google_container_cluster": 420.0,
+    "azurerm_kubernetes_cluster": 360.0,
+    # node pools (GPU nodes boot + join + Ready)
+    "google_container_node_pool": 300.0,
+    "azurerm_kubernetes_cluster_node_pool": 420.0,
+    # IAM / add-ons
+    "module.ebs_csi_irsa_role": 15.0,
+    "terraform_data": 0.0,
+    # GPU software stack
+    "kubernetes_namespace_v1": 2.0,
+    "kubernetes_resource_quota_v1": 1.0,
+    "helm_release": 120.0,                   # operator chart wait=true
+    "kubernetes_daemon_set_v1": 30.0,
+    "kubernetes_service_v1": 1.0,
+    "kubernetes_service_account_v1": 1.0,
+    "kubernetes_cluster_role_v1": 1.0,
+    "kubernetes_cluster_role_binding_v1": 1.0,
+    # validation Job: pod schedule + image pull + run (in-node part measured)
+    "kubernetes_job_v1": 90.0,
+}
+
+# extra readiness that happens INSIDE nodes after their Terraform resource
+# completed: driver install (DKMS build or operator KMM), device plugin
+# registration. Attributed to the node that waits on it.
+DRIVER_READY_S = {"operator": 240.0, "daemonsets": 300.0}
+
+PHASE_OF_KIND = [
+    ("network", ("module.vpc", "google_compute_network", "google_compute_subnetwork",
+                 "azurerm_resource_group")),
+    ("control_plane", ("google_container_cluster", "azurerm_kubernetes_cluster.",
+                       "module.ebs_csi_irsa_role")),
+    ("gpu_nodes_ready", ("module.eks", "google_container_node_pool",
+                         "azurerm_kubernetes_cluster_node_pool")),
+    ("operator_deployed", ("helm_release.amd_gpu_operator", "helm_release.device_config",
+                           "kubernetes_namespace_v1", "kubernetes_resource_quota_v1")),
+    ("gpu_allocatable", ("kubernetes_daemon_set_v1", "kubernetes_service", "kubernetes_cluster_role",
+                         "helm_release.service_monitor")),
+    ("validation_done", ("kubernetes_job_v1",)),
+]
+
+
+def node_type(addr: str) -> str:
+    """Resource type (or module key) of a flattened graph address."""
+    parts = addr.split(".")
+    # strip leading module.X. prefixes of LOCAL modules
+    while len(parts) > 2 and parts[0] == "module" and parts[2] in ("module",) + tuple(
+            k for k in DEFAULT_DURATIONS if "." not in k):
+        parts = parts[2:]
+    while len(parts) > 3 and parts[0] == "module":
+        parts = parts[2:]
+    if parts[0] == "module":
+        return ".".join(parts[:2])
+    if parts[0] == "data":
+        return "data." + parts[1]
+    if parts[0] == "provider":
+        return "provider"
+    return parts[0]
+
+
+def phase_of(addr: str) -> str:
+    for phase, keys in PHASE_OF_KIND:
+        for k in keys:
+            if k in addr:
+                return phase
+    return "other"
+
+
+@dataclass
+class CriticalPath:
+    total_s: float
+    path: list           # [(address, duration_s)] in execution order
+    phases: dict         # phase -> seconds on the critical path
+
+    def as_dict(self) -> dict:
+        return {"total_s": self.total_s, "path": self.path, "phases": self.phases}
+
+
+def critical_path(g: Graph, durations: dict | None = None, stack_mode: str = "operator") -> CriticalPath:
+    dur = dict(DEFAULT_DURATIONS)
+    dur.update(durations or {})
+
+    def d(addr: str) -> float:
+        if addr in dur:
+            return dur[addr]
+        t = node_type(addr)
+        base = dur.get(t, 0.0)
+        if t == "kubernetes_job_v1":
+            base += DRIVER_READY_S.get(stack_mode, 0.0)  # GPUs allocatable only after the driver
+        return base
+
+    finish: dict = {}
+    parent: dict = {}
+    for n in g.topo_order():
+        start, best = 0.0, None
+        for dep in g.deps(n):
+            f = finish.get(dep, 0.0)
+            if f > start:
+                start, best = f, dep
+        finish[n] = start + d(n)
+        parent[n] = best
+    if not finish:
+        return CriticalPath(0.0, [], {})
+    end = max(finish, key=lambda k: finish[k])
+    chain = []
+    cur = end
+    while cur is not None:
+        chain.append((cur, d(cur)))
+        cur = parent[cur]
+    chain.reverse()
+    phases: dict = {}
+    for addr, s in chain:
+        ph = phase_of(addr)
+        phases[ph] = phases.get(ph, 0.0) + s
+    return CriticalPath(finish[end], chain, phases)
+
+
+def durations_from_timeline(events: list[dict]) -> dict:
+    """{address: seconds} from apply_timeline.parse_apply_json() events."""
+    out = {}
+    for ev in events:
+        if ev.get("elapsed_s") is not None:
+            out[ev["address"]] = float(ev["elapsed_s"])
+    return out

@@ -1,0 +1,70 @@
+"""CLI: ``python -m nvidia_terraform_modules_amd.tfcheck [DIR ...]``
+
+Recursively finds Terraform modules under each DIR (default: repo root,
+skipping the ``.terraform`` caches), parses every file, runs the static
+checks, and (``--contract FIXTURE``) diffs the call surface against the
+reference. Exit status 1 on any error finding.
+
+This is the offline stand-in for ``terraform fmt -check && terraform
+validate`` (CONTRIBUTING.md in the reference asks for both, manually); it
+does NOT validate provider schemas, which needs the network.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+from pathlib import Path
+
+from .analysis import analyze, errors
+from .config import find_modules, load_module
+from .contract import compare, load_expected
+from .lexer import HCLSyntaxError
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(prog="tfcheck", description=__doc__,
+                                 formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("dirs", nargs="*", default=["."])
+    ap.add_argument("--no-vendor-lint", action="store_true")
+    ap.add_argument("--no-fmt", action="store_true")
+    ap.add_argument("--warnings-as-errors", action="store_true")
+    ap.add_argument("--contract", help="reference surface fixture (JSON) to diff against")
+    ap.add_argument("--json", action="store_true")
+    args = ap.parse_args(argv)
+
+    results = {}
+    nerr = 0
+    for d in args.dirs:
+        for mdir in find_modules(d):
+            if any(part in ("charts", "fixtures") for part in mdir.parts):
+                continue
+            try:
+                mod = load_module(mdir)
+            except HCLSyntaxError as e:
+                results[str(mdir)] = [f"error: [parse] {e}"]
+                nerr += 1
+                continue
+            fs = analyze(mod, vendor_lint=not args.no_vendor_lint, check_fmt=not args.no_fmt)
+            bad = fs if args.warnings_as_errors else errors(fs)
+            nerr += len(bad)
+            results[str(mdir)] = [str(f) for f in fs]
+    if args.contract:
+        root = Path(args.dirs[0])
+        for diff in compare(load_expected(args.contract), root):
+            if not diff.ok:
+                nerr += 1
+            results[f"contract:{diff.module}"] = [] if diff.ok else [str(diff)]
+    if args.json:
+        print(json.dumps(results, indent=2))
+    else:
+        for k, v in results.items():
+            print(f"{k}: {'ok' if not v else ''}")
+            for line in v:
+                print(f"  {line}")
+        print(f"{nerr} error(s)")
+    return 1 if nerr else 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,333 @@
+"""Static checks over a parsed Terraform module (``terraform validate``-like,
+minus provider schemas, which need the network).
+
+Rules (each finding is ``Finding(rule, severity, where, message)``):
+
+ref-undefined      var./local./module./data./resource references that resolve nowhere
+ref-context        each.* outside for_each, count.* outside count, self outside provisioners
+unused-variable    declared variable never referenced (reference had 5: SURVEY §2.6)
+unused-local       local never referenced (reference: local.ami_id, eks/main.tf:179)
+unused-data        data source never referenced (reference: gke/data.tf:4-8, aks/main.tf:61-65)
+provider-missing   resource/provider type not declared in required_providers
+count-and-foreach  both meta-arguments on one block
+depends-on         depends_on entry that names no resource/module
+module-source      local module source directory missing
+module-input       argument not declared as a variable of a local callee
+module-required    required variable of a local callee not passed
+module-output      module.X.Y where Y is not an output of local callee X
+unknown-function   call to a function Terraform does not have
+vendor-lint        NVIDIA/CUDA-specific strings in literals (AMD-only build)
+fmt                tabs / trailing whitespace (terraform fmt would rewrite)
+"""
+from __future__ import annotations
+
+import re
+from dataclasses import dataclass
+from pathlib import Path
+
+from .config import Module, load_module, provider_of_type
+from .hcl import Block, Body, Traversal, iter_calls, iter_strings, walk_refs
+
+BUILTIN_ROOTS = {"path", "terraform"}
+
+TF_FUNCTIONS = {
+    # numeric
+    "abs", "ceil", "floor", "log", "max", "min", "parseint", "pow", "signum",
+    # string
+    "chomp", "endswith", "format", "formatlist", "indent", "join", "lower", "regex", "regexall",
+    "replace", "split", "startswith", "strcontains", "strrev", "substr", "templatestring", "title",
+    "trim", "trimprefix", "trimspace", "trimsuffix", "upper",
+    # collection
+    "alltrue", "anytrue", "chunklist", "coalesce", "coalescelist", "compact", "concat", "contains",
+    "distinct", "element", "flatten", "index", "keys", "length", "list", "lookup", "map", "matchkeys",
+    "merge", "one", "range", "reverse", "setintersection", "setproduct", "setsubtract", "setunion",
+    "slice", "sort", "sum", "transpose", "values", "zipmap",
+    # encoding
+    "base64decode", "base64encode", "base64gzip", "csvdecode", "jsondecode", "jsonencode",
+    "textdecodebase64", "textencodebase64", "urlencode", "yamldecode", "yamlencode",
+    # filesystem
+    "abspath", "dirname", "pathexpand", "basename", "file", "fileexists", "fileset", "filebase64",
+    "templatefile",
+    # date/time
+    "formatdate", "plantimestamp", "timeadd", "timecmp", "timestamp",
+    # hash/crypto
+    "base64sha256", "base64sha512", "bcrypt", "filebase64sha256", "filebase64sha512", "filemd5",
+    "filesha1", "filesha256", "filesha512", "md5", "rsadecrypt", "sha1", "sha256", "sha512", "uuid",
+    "uuidv5",
+    # ip
+    "cidrhost", "cidrnetmask", "cidrsubnet", "cidrsubnets",
+    # type conversion
+    "can", "issensitive", "nonsensitive", "sensitive", "tobool", "tolist", "tomap", "tonumber",
+    "toset", "tostring", "try", "type",
+}
+
+# type-constraint keywords appear as calls / bare words inside `type = ...`
+TYPE_WORDS = {"string", "number", "bool", "any", "list", "map", "set", "object", "tuple", "optional"}
+
+VENDOR_PATTERNS = [
+    re.compile(p, re.I) for p in (
+        r"nvidia\.com/gpu", r"helm\.ngc\.nvidia\.com", r"\bcuda\b", r"nvidia-smi", r"\bdcgm",
+        r"nvidia/gpu-operator", r"nvidia-tesla", r"\bnvidia-(?:driver|container|device)",
+    )
+]
+
+
+@dataclass(frozen=True)
+class Finding:
+    rule: str
+    severity: str   # "error" | "warning"
+    where: str
+    message: str
+
+    def __str__(self) -> str:
+        return f"{self.severity}: [{self.rule}] {self.where}: {self.message}"
+
+
+class _Scope:
+    def __init__(self, block_type: str, has_count: bool, has_for_each: bool, iterators: set,
+                 in_provisioner: bool):
+        self.block_type = block_type
+        self.has_count = has_count
+        self.has_for_each = has_for_each
+        self.iterators = iterators
+        self.in_provisioner = in_provisioner
+
+
+def _iter_body_exprs(body: Body, scope: _Scope, skip_attrs: tuple = ()):
+    """Yield (expr, scope, line) for every attribute expression, descending
+    into nested blocks (dynamic blocks add their iterator name)."""
+    for name, attr in body.attributes.items():
+        if name in skip_attrs:
+            continue
+        yield attr.expr, scope, attr.line, name
+    for b in body.blocks:
+        if b.type == "dynamic":
+            it = b.labels[0] if b.labels else "dynamic"
+            it_expr = b.body.attr("iterator")
+            if isinstance(it_expr, Traversal):
+                it = it_expr.root
+            fe = b.body.attr("for_each")
+            if fe is not None:
+                yield fe, scope, b.line, "for_each"
+            inner = _Scope(scope.block_type, scope.has_count, scope.has_for_each,
+                           scope.iterators | {it}, scope.in_provisioner)
+            for c in b.body.blocks_of("content"):
+                yield from _iter_body_exprs(c.body, inner)
+            for an, attr in b.body.attributes.items():
+                if an in ("for_each", "iterator", "labels"):
+                    continue
+                yield attr.expr, inner, attr.line, an
+        elif b.type in ("provisioner", "connection"):
+            inner = _Scope(scope.block_type, scope.has_count, scope.has_for_each, scope.iterators, True)
+            yield from _iter_body_exprs(b.body, inner)
+        elif b.type == "lifecycle":
+            for an, attr in b.body.attributes.items():
+                if an in ("ignore_changes", "replace_triggered_by"):
+                    continue  # bare attribute names, not references
+                yield attr.expr, scope, attr.line, an
+            for c in b.body.blocks:
+                yield from _iter_body_exprs(c.body, scope)
+        else:
+            yield from _iter_body_exprs(b.body, scope)
+
+
+def _block_scope(b: Block) -> _Scope:
+    return _Scope(b.type, "count" in b.body.attributes, "for_each" in b.body.attributes, set(), False)
+
+
+def module_exprs(mod: Module):
+    """Yield (expr, scope, where, attr_name, owner) over the whole module."""
+    for fname, body in mod.files.items():
+        for b in body.blocks:
+            if b.type in ("resource", "data", "module"):
+                owner = ".".join(([] if b.type == "resource" else [b.type]) + list(b.labels))
+                skip = ("source", "version", "providers") if b.type == "module" else ("provider",)
+                for e, sc, line, an in _iter_body_exprs(b.body, _block_scope(b), skip):
+                    yield e, sc, f"{fname}:{line}", an, owner
+            elif b.type in ("output", "locals", "provider", "check"):
+                sc = _Scope(b.type, False, False, set(), False)
+                for e, s2, line, an in _iter_body_exprs(b.body, sc):
+                    yield e, s2, f"{fname}:{line}", an, b.type
+            elif b.type == "variable":
+                sc = _Scope("variable", False, False, set(), False)
+                for e, s2, line, an in _iter_body_exprs(b.body, sc):
+                    if an == "type":
+                        continue
+                    yield e, s2, f"{fname}:{line}", an, f"var.{b.labels[0]}"
+            elif b.type == "terraform":
+                continue
+
+
+def analyze(mod: Module, *, strict_unused: bool = True, vendor_lint: bool = True,
+            check_fmt: bool = True, callee_loader=load_module) -> list[Finding]:
+    out: list[Finding] = [Finding("parse", "error", str(mod.path), e) for e in mod.errors]
+    used_vars: set[str] = set()
+    used_locals: set[str] = set()
+    used_data: set[str] = set()
+    used_resources: set[str] = set()
+    used_modules: set[str] = set()
+    resource_types = {r.type for r in mod.managed}
+    data_types = {r.type for r in mod.data}
+    callees: dict[str, Module] = {}
+    for name, mc in mod.modules.items():
+        if mc.is_local:
+            p = (mod.path / mc.source).resolve()
+            if not p.is_dir() or not list(p.glob("*.tf")):
+                out.append(Finding("module-source", "error", f"{mc.file}:{mc.block.line}",
+                                   f"module {name!r}: source {mc.source!r} not found"))
+            else:
+                callees[name] = callee_loader(p)
+
+    for expr, scope, where, attr, owner in module_exprs(mod):
+        if attr == "depends_on":
+            for ref, _ in walk_refs(expr):
+                tgt = ".".join([ref.root] + ref.path()[:2 if ref.root == "data" else 1])
+                if ref.root == "module":
+                    ok = bool(ref.path()) and ref.path()[0] in mod.modules
+                    if ok:
+                        used_modules.add(ref.path()[0])
+                elif ref.root == "data":
+                    ok = tgt in mod.resources
+                    used_data.add(tgt)
+                else:
+                    ok = tgt in mod.resources
+                    used_resources.add(tgt)
+                if not ok:
+                    out.append(Finding("depends-on", "error", where, f"depends_on entry {tgt!r} not found"))
+            continue
+        for call in iter_calls(expr):
+            if call.name not in TF_FUNCTIONS and not (attr == "type" and call.name in TYPE_WORDS):
+                out.append(Finding("unknown-function", "error", where, f"unknown function {call.name}()"))
+        for ref, bound in walk_refs(expr):
+            root = ref.root
+            path = ref.path()
+            if root in bound or root in scope.iterators:
+                continue
+            if root == "var":
+                if not path or path[0] not in mod.variables:
+                    out.append(Finding("ref-undefined", "error", where, f"undefined variable var.{path[0] if path else '?'}"))
+                else:
+                    used_vars.add(path[0])
+            elif root == "local":
+                if not path or path[0] not in mod.locals:
+                    out.append(Finding("ref-undefined", "error", where, f"undefined local.{path[0] if path else '?'}"))
+                else:
+                    used_locals.add(path[0])
+            elif root == "module":
+                if not path or path[0] not in mod.modules:
+                    out.append(Finding("ref-undefined", "error", where, f"undefined module.{path[0] if path else '?'}"))
+                else:
+                    used_modules.add(path[0])
+                    callee = callees.get(path[0])
+                    if callee is not None and len(path) > 1 and path[1] not in callee.outputs \
+                            and not path[1].isdigit():
+                        out.append(Finding("module-output", "error", where,
+                                           f"module.{path[0]} has no output {path[1]!r}"))
+            elif root == "data":
+                if len(path) < 2 or f"data.{path[0]}.{path[1]}" not in mod.resources:
+                    out.append(Finding("ref-undefined", "error", where, f"undefined data.{'.'.join(path[:2])}"))
+                else:
+                    used_data.add(f"data.{path[0]}.{path[1]}")
+            elif root == "each":
+                if not scope.has_for_each:
+                    out.append(Finding("ref-context", "error", where, "each.* used without for_each"))
+            elif root == "count":
+                if not scope.has_count:
+                    out.append(Finding("ref-context", "error", where, "count.* used without count"))
+            elif root == "self":
+                if not scope.in_provisioner:
+                    out.append(Finding("ref-context", "error", where, "self used outside a provisioner"))
+            elif root in BUILTIN_ROOTS:
+                continue
+            elif root in resource_types:
+                addr = f"{root}.{path[0]}" if path else root
+                if addr not in mod.resources:
+                    out.append(Finding("ref-undefined", "error", where, f"undefined resource {addr}"))
+                used_resources.add(addr)
+            elif attr == "type" or root in TYPE_WORDS and owner.startswith("var."):
+                continue
+            else:
+                out.append(Finding("ref-undefined", "error", where, f"unknown reference root {root!r}"))
+
+    # module call arguments vs callee variables
+    for name, mc in mod.modules.items():
+        callee = callees.get(name)
+        if callee is None:
+            continue
+        meta = {"source", "version", "count", "for_each", "providers", "depends_on"}
+        passed = set(mc.block.body.attributes) - meta
+        for arg in sorted(passed - set(callee.variables)):
+            out.append(Finding("module-input", "error", f"{mc.file}:{mc.block.line}",
+                               f"module {name!r}: callee has no variable {arg!r}"))
+        for v in sorted(n for n, var in callee.variables.items() if var.required and n not in passed):
+            out.append(Finding("module-required", "error", f"{mc.file}:{mc.block.line}",
+                               f"module {name!r}: required variable {v!r} not set"))
+
+    if strict_unused:
+        for n, v in mod.variables.items():
+            if n not in used_vars:
+                out.append(Finding("unused-variable", "warning", f"{v.file}:{v.block.line}",
+                                   f"variable {n!r} is never used"))
+        for n, (_, f, line) in mod.locals.items():
+            if n not in used_locals:
+                out.append(Finding("unused-local", "warning", f"{f}:{line}", f"local {n!r} is never used"))
+        for r in mod.data:
+            if r.address not in used_data:
+                out.append(Finding("unused-data", "warning", f"{r.file}:{r.block.line}",
+                                   f"{r.address} is never referenced"))
+
+    # providers
+    declared = set(mod.required_providers) | {"terraform"}
+    for r in mod.resources.values():
+        p = r.provider_name
+        if p not in declared:
+            out.append(Finding("provider-missing", "error", f"{r.file}:{r.block.line}",
+                               f"{r.address}: provider {p!r} not in required_providers"))
+    for pb in mod.providers:
+        if pb.labels and pb.labels[0] not in declared:
+            out.append(Finding("provider-missing", "error", f"provider:{pb.line}",
+                               f"provider block {pb.labels[0]!r} not in required_providers"))
+
+    for r in list(mod.resources.values()) + list(mod.modules.values()):
+        attrs = r.block.body.attributes
+        if "count" in attrs and "for_each" in attrs:
+            out.append(Finding("count-and-foreach", "error", f"{r.file}:{r.block.line}",
+                               "count and for_each are mutually exclusive"))
+
+    if vendor_lint:
+        out.extend(vendor_findings(mod))
+    if check_fmt:
+        out.extend(fmt_findings(mod.path))
+    return out
+
+
+def vendor_findings(mod: Module) -> list[Finding]:
+    out = []
+    for expr, _, where, _, _ in module_exprs(mod):
+        for s in iter_strings(expr):
+            for pat in VENDOR_PATTERNS:
+                if pat.search(s):
+                    out.append(Finding("vendor-lint", "error", where,
+                                       f"NVIDIA/CUDA-specific string {s.strip()[:60]!r}"))
+    for fname, body in mod.tfvars.items():
+        for name, attr in body.attributes.items():
+            for s in iter_strings(attr.expr):
+                if any(p.search(s) for p in VENDOR_PATTERNS):
+                    out.append(Finding("vendor-lint", "error", f"{fname}:{attr.line}",
+                                       f"NVIDIA/CUDA-specific string in {name}"))
+    return out
+
+
+def fmt_findings(path: Path) -> list[Finding]:
+    out = []
+    for f in sorted(Path(path).glob("*.tf")) + sorted(Path(path).glob("*.tfvars")):
+        for i, line in enumerate(f.read_text().splitlines(), 1):
+            if "\t" in line:
+                out.append(Finding("fmt", "warning", f"{f.name}:{i}", "tab character"))
+            if line != line.rstrip():
+                out.append(Finding("fmt", "warning", f"{f.name}:{i}", "trailing whitespace"))
+    return out
+
+
+def errors(findings: list[Finding]) -> list[Finding]:
+    return [f for f in findings if f.severity == "error"]
