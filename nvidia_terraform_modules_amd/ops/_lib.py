@@ -29,6 +29,8 @@ def _declare(lib: ctypes.CDLL) -> None:
         "ntm_version": ([], ctypes.c_char_p),
         "ntm_gemm_shape_ok": ([c_int, c_int, c_int], c_int),
         "ntm_gemm_bf16": ([c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp], c_int),
+        "ntm_gemm_bf16_variant": (
+            [c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp], c_int),
         "ntm_fill_uniform_bf16": ([c_vp, c_size, ctypes.c_ulonglong, c_float, c_vp], c_int),
         "ntm_ref_gemm_f32": ([c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp], c_int),
         "ntm_verify_bf16": ([c_vp, c_vp, c_size, c_float, c_float, c_vp, c_vp], c_int),

@@ -30,10 +30,16 @@ def _require(t: torch.Tensor, name: str, dtype: torch.dtype) -> None:
         raise ValueError(f"{name} must be 2-D with unit inner stride")
 
 
-def gemm_bf16(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+GEMM_VARIANTS = {"default": 0, "pingpong8": 1, "wave128": 2, "wave128d4": 3}
+
+
+def gemm_bf16(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
+              variant: str = "default") -> torch.Tensor:
     """K1: ``out = a @ b.T`` in bf16 with fp32 accumulation on MFMA.
 
     a: [M, K] bf16, b: [N, K] bf16 (both K-contiguous), out: [M, N] bf16.
+    ``variant``: "wave128" (4 waves, 128x128 per wave; the default) or
+    "pingpong8" (8 waves, two per SIMD, staggered) - see validation/include.
     """
     _require(a, "a", torch.bfloat16)
     _require(b, "b", torch.bfloat16)
@@ -48,8 +54,8 @@ def gemm_bf16(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None)
     _require(out, "out", torch.bfloat16)
     if tuple(out.shape) != (m, n):
         raise ValueError("out has the wrong shape")
-    rc = lib().ntm_gemm_bf16(
-        a.data_ptr(), b.data_ptr(), out.data_ptr(), m, n, k,
+    rc = lib().ntm_gemm_bf16_variant(
+        GEMM_VARIANTS[variant], a.data_ptr(), b.data_ptr(), out.data_ptr(), m, n, k,
         a.stride(0), b.stride(0), out.stride(0), stream_handle())
     check(rc, "ntm_gemm_bf16")
     return out

@@ -1,10 +1,11 @@
-"""Quick K1 numerics + throughput check on one MI355X (developer tool).
+"""K1 numerics + throughput check on one MI355X (developer tool).
 
-    python tools/gemm_check.py [--sizes 4096,8192] [--iters 50]
+    python tools/gemm_check.py [--sizes 4096,8192] [--iters 50] [--variants wave128,pingpong8]
 
-Prints one JSON line per size with: max error vs the fp32 reference kernel and
-vs torch (hipBLASLt) fp32, our TFLOP/s and torch.matmul's TFLOP/s on the same
-uniform [-1,1) data (interleaved rounds in one process, playbook rule 24).
+For every size: full verification of each variant against the independent
+fp32 reference kernel, then interleaved timing rounds of every variant and of
+torch.matmul (hipBLASLt) on the same uniform [-1,1) data in ONE process
+(playbook rule 24). Prints one JSON line per size.
 """
 from __future__ import annotations
 
@@ -34,8 +35,10 @@ def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--sizes", default="4096,8192")
     ap.add_argument("--iters", type=int, default=50)
-    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--variants", default="wave128,pingpong8")
     args = ap.parse_args()
+    variants = args.variants.split(",")
     dev = torch.device("cuda:0")
     print(json.dumps({"device": torch.cuda.get_device_name(0), "lib": ops.version()}), flush=True)
     for s in [int(x) for x in args.sizes.split(",")]:
@@ -44,26 +47,28 @@ def main() -> int:
         b = torch.empty((n, k), dtype=torch.bfloat16, device=dev)
         ops.fill_uniform_(a, seed=1)
         ops.fill_uniform_(b, seed=2)
-        c = ops.gemm_bf16(a, b)
-        torch.cuda.synchronize()
         atol, rtol = ops.gemm_tolerance(k)
         ref = ops.ref_gemm_f32(a, b)
-        rep = ops.verify_bf16(c, ref, atol, rtol)
-        tref = a.float() @ b.float().T
-        err_torch = (c.float() - tref).abs().max().item()
-        del tref
+        res = {"size": s}
+        cc = torch.empty((m, n), dtype=torch.bfloat16, device=dev)
+        for v in variants:
+            cc.fill_(float("nan"))
+            ops.gemm_bf16(a, b, cc, variant=v)
+            res[f"verify_{v}"] = ops.verify_bf16(cc, ref, atol, rtol).as_dict()
+        del ref
         flops = 2.0 * m * n * k
-        ours, theirs = [], []
-        cc = torch.empty_like(c)
+        times = {v: [] for v in variants + ["torch"]}
         for _ in range(args.rounds):
-            ours.append(timed(lambda: ops.gemm_bf16(a, b, cc), args.iters))
-            theirs.append(timed(lambda: torch.matmul(a, b.T, out=cc), args.iters))
-        print(json.dumps({
-            "size": s, "verify": rep.as_dict(), "max_err_vs_torch_fp32": err_torch,
-            "ours_ms": min(ours), "ours_tflops": flops / min(ours) / 1e9,
-            "torch_ms": min(theirs), "torch_tflops": flops / min(theirs) / 1e9,
-            "ours_all_ms": ours, "torch_all_ms": theirs,
-        }), flush=True)
+            for v in variants:
+                times[v].append(timed(lambda: ops.gemm_bf16(a, b, cc, variant=v), args.iters))
+            times["torch"].append(timed(lambda: torch.matmul(a, b.T, out=cc), args.iters))
+        for v, t in times.items():
+            t = sorted(t)
+            res[f"{v}_ms_min"] = t[0]
+            res[f"{v}_ms_med"] = t[len(t) // 2]
+            res[f"{v}_tflops_best"] = flops / t[0] / 1e9
+            res[f"{v}_tflops_med"] = flops / t[len(t) // 2] / 1e9
+        print(json.dumps(res), flush=True)
     return 0
 
 

@@ -1,0 +1,44 @@
+"""Run our K1 GEMM and torch.matmul (hipBLASLt) back to back on the same
+random operands - a profiling target for rocprofv3 (developer tool).
+
+    rocprofv3 --pmc SQ_WAVE_CYCLES ... -- python3 tools/gemm_pair.py --size 8192 --iters 20
+"""
+from __future__ import annotations
+
+import argparse
+import sys
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+
+import torch  # noqa: E402
+
+from nvidia_terraform_modules_amd import ops  # noqa: E402
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--size", type=int, default=8192)
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--which", default="both", choices=["both", "ours", "torch", "all"])
+    ap.add_argument("--variant", default="wave128")
+    args = ap.parse_args()
+    s = args.size
+    a = torch.empty((s, s), dtype=torch.bfloat16, device="cuda")
+    b = torch.empty((s, s), dtype=torch.bfloat16, device="cuda")
+    c = torch.empty((s, s), dtype=torch.bfloat16, device="cuda")
+    ops.fill_uniform_(a, 1)
+    ops.fill_uniform_(b, 2)
+    for _ in range(args.iters):
+        if args.which in ("both", "ours", "all"):
+            ops.gemm_bf16(a, b, c, variant=args.variant)
+        if args.which == "all":
+            ops.gemm_bf16(a, b, c, variant="pingpong8")
+        if args.which in ("both", "torch", "all"):
+            torch.matmul(a, b.T, out=c)
+    torch.cuda.synchronize()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

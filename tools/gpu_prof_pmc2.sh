@@ -1,0 +1,15 @@
+#!/bin/bash
+# PMC profile of K1 variants vs hipBLASLt (counters in their own runs).
+set -o pipefail
+cd /root/repo
+export TMPDIR=/tmp
+OUT=gpurun_out/pmc2
+mkdir -p $OUT
+run() {
+  local name=$1; shift
+  timeout -k 10 240 rocprofv3 --pmc "$@" --kernel-trace --output-format csv -d $OUT/$name -o run -- python3 tools/gemm_pair.py --size 8192 --iters 6 --which ${WHICH:-both} > $OUT/$name.log 2>&1 || { echo "FAIL $name"; tail -20 $OUT/$name.log; return 1; }
+}
+run sq1 SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE && \
+run sq2 SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_WAIT_INST_LDS && \
+run sq3 SQ_INST_CYCLES_VMEM SQ_INSTS_VALU SQ_INSTS_SALU SQ_LDS_IDX_ACTIVE SQ_INSTS_VMEM && \
+run tcc TCC_HIT_sum TCC_MISS_sum TCP_TCC_READ_REQ_sum

@@ -6,6 +6,7 @@
 // can be captured in a hipGraph (playbook §6 Guideline 9).
 #include "ntm/aux_kernels.hpp"
 #include "ntm/gemm_bf16.hpp"
+#include "ntm/gemm_bf16_w4.hpp"
 
 #define NTM_API extern "C" __attribute__((visibility("default")))
 
@@ -26,19 +27,46 @@ NTM_API int ntm_gemm_shape_ok(int M, int N, int K) {
   return ntm::gemm::shape_ok(M, N, K) ? 1 : 0;
 }
 
+// K1 variants: 1 = 8-wave ping-pong (gemm_bf16.hpp); 2 / 3 = 4-wave, 128x128
+// per wave (gemm_bf16_w4.hpp) with prefetch distance 3 / 4 k-steps.
+// 0 = default: the fastest measured variant whose shape rules admit (M,N,K).
+// Measured on MI355X (tools/gemm_check.py, 8192^3 random bf16): 1 ~1500 TF,
+// 2 ~1310-1380 TF, 3 ~1110-1430 TF; hipBLASLt ~1650 TF on the same data.
+constexpr int kDefaultVariant = 1;
+
+NTM_API int ntm_gemm_bf16_variant(int variant, const void* A, const void* B,
+                                  void* C, int M, int N, int K, int lda,
+                                  int ldb, int ldc, void* stream) {
+  if (variant == 0) {
+    variant = kDefaultVariant;
+    if (variant == 3 && !ntm::gemm4::shape_ok<4>(M, N, K)) variant = 1;
+    if (variant == 2 && !ntm::gemm4::shape_ok<3>(M, N, K)) variant = 1;
+  }
+  if (variant == 1) {
+    ntm::gemm::GemmArgs a;
+    a.A = (const __bf16*)A;
+    a.B = (const __bf16*)B;
+    a.C = (__bf16*)C;
+    a.M = M;
+    a.N = N;
+    a.K = K;
+    a.lda = lda;
+    a.ldb = ldb;
+    a.ldc = ldc;
+    return (int)ntm::gemm::launch_gemm_bf16(a, S(stream));
+  }
+  if (variant == 2 || variant == 3) {
+    ntm::gemm4::Args a{(const __bf16*)A, (const __bf16*)B, (__bf16*)C, M, N, K,
+                       lda, ldb, ldc};
+    return variant == 2 ? (int)ntm::gemm4::launch<3>(a, S(stream))
+                        : (int)ntm::gemm4::launch<4>(a, S(stream));
+  }
+  return (int)hipErrorInvalidValue;
+}
+
 NTM_API int ntm_gemm_bf16(const void* A, const void* B, void* C, int M, int N,
                           int K, int lda, int ldb, int ldc, void* stream) {
-  ntm::gemm::GemmArgs a;
-  a.A = (const __bf16*)A;
-  a.B = (const __bf16*)B;
-  a.C = (__bf16*)C;
-  a.M = M;
-  a.N = N;
-  a.K = K;
-  a.lda = lda;
-  a.ldb = ldb;
-  a.ldc = ldc;
-  return (int)ntm::gemm::launch_gemm_bf16(a, S(stream));
+  return ntm_gemm_bf16_variant(0, A, B, C, M, N, K, lda, ldb, ldc, stream);
 }
 
 NTM_API int ntm_fill_uniform_bf16(void* out, size_t n, unsigned long long seed,
