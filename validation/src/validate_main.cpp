@@ -1,0 +1,548 @@
+// amdgpu-validate: the post-provision validation Job entrypoint.
+//
+// Runs on the MI355X GPUs granted to the Kubernetes Job (amd.com/gpu: N) and
+// proves them usable, replacing the NVIDIA GPU Operator's CUDA validator
+// (reference: helm_release.gpu_operator, /root/reference/eks/main.tf:185-203):
+//
+//   K1  hand-written bf16 MFMA GEMM per GPU (TFLOP/s + full verification
+//       against an independent fp32 reference kernel)
+//   K2  HBM stream copy bandwidth + capacity check (288 GB class)
+//   C1  RCCL all-reduce sweep over xGMI (ncclCommInitAll, one process owns
+//       all GPUs; every element checked)
+//   C2  hand-written two-shot all-reduce over peer-mapped xGMI, vs RCCL
+//
+// One process, one host thread per GPU for K1/K2; no Python, no PyTorch - the
+// container is small and starts fast (time-to-GPU-ready). Prints ONE JSON
+// document; exit 0 = all checks passed, 1 = a check failed, 2 = environment
+// error (no GPUs, not gfx950, HIP/RCCL error).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <mutex>
+#include <sstream>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include <unistd.h>
+
+#include "ntm/common.hpp"
+
+namespace ntm {
+namespace xgmi {
+constexpr int kMaxRanks = 8;  // = ntm/xgmi_allreduce.hpp (kernels live in its .hip)
+}
+}  // namespace ntm
+
+// C ABI of ntm_validation.hip / xgmi_allreduce.hip (linked into this binary)
+extern "C" {
+int ntm_gemm_bf16(const void*, const void*, void*, int, int, int, int, int, int, void*);
+int ntm_gemm_shape_ok(int, int, int);
+int ntm_fill_uniform_bf16(void*, size_t, unsigned long long, float, void*);
+int ntm_ref_gemm_f32(const void*, const void*, float*, int, int, int, int, int, int, void*);
+int ntm_verify_bf16(const void*, const float*, size_t, float, float, void*, void*);
+int ntm_verify_result_bytes();
+int ntm_stream_copy(const void*, void*, size_t, void*);
+int ntm_xgmi_allreduce_bf16(const void* const*, void* const*, unsigned* const*, int, int,
+                            int, int, size_t, unsigned, unsigned*, int, void*);
+size_t ntm_xgmi_signal_bytes(int);
+}
+
+namespace {
+
+using Clock = std::chrono::steady_clock;
+
+double wall_now() {
+  return std::chrono::duration<double>(std::chrono::system_clock::now().time_since_epoch())
+      .count();
+}
+
+double process_start_epoch() {
+  std::ifstream st("/proc/self/stat"), up("/proc/uptime");
+  std::string s((std::istreambuf_iterator<char>(st)), std::istreambuf_iterator<char>());
+  double uptime = 0;
+  up >> uptime;
+  const size_t rp = s.rfind(')');
+  if (rp == std::string::npos || uptime <= 0) return wall_now();
+  std::istringstream rest(s.substr(rp + 2));
+  std::string tok;
+  long long start_ticks = 0;
+  for (int i = 0; i < 20 && rest >> tok; ++i)
+    if (i == 19) start_ticks = std::atoll(tok.c_str());
+  const long hz = sysconf(_SC_CLK_TCK);
+  return wall_now() - uptime + (double)start_ticks / (double)hz;
+}
+
+struct Opts {
+  int gpus = 0;  // 0 = all visible
+  int size = 8192;
+  int iters = 50;
+  double tflops_floor = 0;
+  double min_hbm_gb = 0;
+  double hbm_floor_gbps = 0;
+  long allreduce_max_mib = 1024;
+  bool xgmi = true;
+  bool json = true;
+  std::string out;
+};
+
+void usage() {
+  std::fprintf(stderr,
+               "usage: amdgpu-validate [--gpus N] [--size 8192] [--iters 50]\n"
+               "       [--tflops-floor TF] [--min-hbm-gb GB] [--hbm-floor-gbps GBps]\n"
+               "       [--allreduce-max-mib MiB] [--no-xgmi] [--json] [--out FILE]\n");
+}
+
+bool parse(int argc, char** argv, Opts& o) {
+  for (int i = 1; i < argc; ++i) {
+    std::string a = argv[i];
+    auto next = [&](const char* name) -> const char* {
+      if (i + 1 >= argc) {
+        std::fprintf(stderr, "missing value for %s\n", name);
+        return nullptr;
+      }
+      return argv[++i];
+    };
+    const char* v = nullptr;
+    if (a == "--gpus") { if (!(v = next("--gpus"))) return false; o.gpus = std::atoi(v); }
+    else if (a == "--size") { if (!(v = next("--size"))) return false; o.size = std::atoi(v); }
+    else if (a == "--iters") { if (!(v = next("--iters"))) return false; o.iters = std::atoi(v); }
+    else if (a == "--tflops-floor") { if (!(v = next(a.c_str()))) return false; o.tflops_floor = std::atof(v); }
+    else if (a == "--min-hbm-gb") { if (!(v = next(a.c_str()))) return false; o.min_hbm_gb = std::atof(v); }
+    else if (a == "--hbm-floor-gbps") { if (!(v = next(a.c_str()))) return false; o.hbm_floor_gbps = std::atof(v); }
+    else if (a == "--allreduce-max-mib") { if (!(v = next(a.c_str()))) return false; o.allreduce_max_mib = std::atol(v); }
+    else if (a == "--no-xgmi") o.xgmi = false;
+    else if (a == "--json") o.json = true;
+    else if (a == "--out") { if (!(v = next("--out"))) return false; o.out = v; }
+    else if (a == "-h" || a == "--help") { usage(); std::exit(0); }
+    else { std::fprintf(stderr, "unknown argument %s\n", a.c_str()); return false; }
+  }
+  return o.size > 0 && o.iters > 0;
+}
+
+// ------------------------------------------------------------ JSON helpers
+std::string jnum(double v) {
+  if (!std::isfinite(v)) return "null";
+  char b[64];
+  std::snprintf(b, sizeof b, "%.6g", v);
+  return b;
+}
+std::string jstr(const std::string& s) {
+  std::string o = "\"";
+  for (char c : s) {
+    if (c == '"' || c == '\\') o += '\\';
+    if ((unsigned char)c < 0x20) continue;
+    o += c;
+  }
+  return o + "\"";
+}
+
+std::mutex g_fail_mu;
+std::vector<std::string> g_failures;
+void fail(const std::string& why) {
+  std::lock_guard<std::mutex> l(g_fail_mu);
+  g_failures.push_back(why);
+}
+
+#define CK(expr)                                                              \
+  do {                                                                        \
+    hipError_t _e = (hipError_t)(expr);                                       \
+    if (_e != hipSuccess) {                                                   \
+      fail(std::string("HIP error ") + hipGetErrorString(_e) + " at " #expr); \
+      return false;                                                           \
+    }                                                                         \
+  } while (0)
+
+// ------------------------------------------------- pattern kernels (C1/C2)
+// rank r contributes 2^(i%4) * (r+1): every partial sum is exact in bf16 for
+// n <= 8 ranks, so the result is checked element by element, exactly.
+__global__ void fill_pattern(uint16_t* x, size_t n, int rank) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+       i += (size_t)gridDim.x * blockDim.x)
+    x[i] = ntm::f32_to_bf16_bits((float)(1u << (i & 3)) * (float)(rank + 1));
+}
+
+__global__ void check_pattern(const uint16_t* x, size_t n, int nranks,
+                              unsigned long long* bad) {
+  unsigned long long b = 0;
+  const float s = (float)(nranks * (nranks + 1) / 2);
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+       i += (size_t)gridDim.x * blockDim.x)
+    b += ntm::bf16_bits_to_f32(x[i]) != (float)(1u << (i & 3)) * s;
+  if (b) atomicAdd(bad, b);
+}
+
+// -------------------------------------------------------------- per GPU
+struct GpuResult {
+  int device = -1;
+  std::string name, arch;
+  double total_gb = 0, free_gb = 0;
+  double gemm_ms = 0, gemm_tflops = 0;
+  unsigned long long gemm_bad = ~0ull;
+  float gemm_max_err = NAN;
+  double hbm_copy_gbps = 0;
+  bool hbm_copy_ok = false;
+  double t_init = 0, t_gemm = 0, t_hbm = 0;
+};
+
+bool run_gpu(int dev, const Opts& o, GpuResult& r) {
+  r.device = dev;
+  CK(hipSetDevice(dev));
+  hipDeviceProp_t prop;
+  CK(hipGetDeviceProperties(&prop, dev));
+  r.name = prop.name;
+  r.arch = prop.gcnArchName;
+  if (r.arch.find("gfx950") == std::string::npos) {
+    fail("device " + std::to_string(dev) + " is " + r.arch + ", not gfx950 (MI355X)");
+    return false;
+  }
+  size_t fre = 0, tot = 0;
+  CK(hipMemGetInfo(&fre, &tot));
+  r.total_gb = tot / 1e9;
+  r.free_gb = fre / 1e9;
+  hipStream_t s;
+  CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  r.t_init = wall_now();
+
+  // ---- K1
+  const int n = o.size;
+  if (!ntm_gemm_shape_ok(n, n, n)) {
+    fail("--size must be a multiple of 256 (>= 256)");
+    return false;
+  }
+  const size_t e = (size_t)n * n;
+  void *A, *B, *C, *V;
+  float* R;
+  CK(hipMalloc(&A, e * 2));
+  CK(hipMalloc(&B, e * 2));
+  CK(hipMalloc(&C, e * 2));
+  CK(hipMalloc(&R, e * 4));
+  CK(hipMalloc(&V, 64));
+  CK(ntm_fill_uniform_bf16(A, e, 1000 + 2 * dev, 1.0f, s));
+  CK(ntm_fill_uniform_bf16(B, e, 1001 + 2 * dev, 1.0f, s));
+  CK(ntm_gemm_bf16(A, B, C, n, n, n, n, n, n, s));  // warm-up + verified result
+  CK(ntm_ref_gemm_f32(A, B, R, n, n, n, n, n, n, s));
+  CK(hipMemsetAsync(V, 0, 64, s));
+  const float atol = 1e-3f + 4.0f * std::sqrt((float)n) * std::ldexp(1.0f, -20);
+  CK(ntm_verify_bf16(C, R, e, atol, std::ldexp(1.0f, -7), V, s));
+  unsigned char vr[64];
+  CK(hipMemcpyAsync(vr, V, ntm_verify_result_bytes(), hipMemcpyDeviceToHost, s));
+  CK(hipStreamSynchronize(s));
+  std::memcpy(&r.gemm_bad, vr, 8);
+  std::memcpy(&r.gemm_max_err, vr + 8, 4);
+  CK(hipFree(R));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  for (int i = 0; i < 5; ++i) CK(ntm_gemm_bf16(A, B, C, n, n, n, n, n, n, s));
+  CK(hipEventRecord(e0, s));
+  for (int i = 0; i < o.iters; ++i) CK(ntm_gemm_bf16(A, B, C, n, n, n, n, n, n, s));
+  CK(hipEventRecord(e1, s));
+  CK(hipEventSynchronize(e1));
+  float ms = 0;
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  r.gemm_ms = ms / o.iters;
+  r.gemm_tflops = 2.0 * n * (double)n * n / (r.gemm_ms * 1e-3) / 1e12;
+  CK(hipFree(A));
+  CK(hipFree(B));
+  CK(hipFree(C));
+  CK(hipFree(V));
+  r.t_gemm = wall_now();
+
+  // ---- K2: 2 GiB float4 copy
+  const size_t hb = std::min<size_t>((size_t)2 << 30, fre / 4) / 16 * 16;
+  void *src, *dst;
+  CK(hipMalloc(&src, hb));
+  CK(hipMalloc(&dst, hb));
+  CK(ntm_fill_uniform_bf16(src, hb / 2, 77 + dev, 1.0f, s));
+  CK(ntm_stream_copy(src, dst, hb, s));
+  CK(hipEventRecord(e0, s));
+  for (int i = 0; i < 10; ++i) CK(ntm_stream_copy(src, dst, hb, s));
+  CK(hipEventRecord(e1, s));
+  CK(hipEventSynchronize(e1));
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  r.hbm_copy_gbps = 2.0 * hb * 10 / (ms * 1e-3) / 1e9;
+  {  // byte-exact copy check on a sample window (first + last 16 MiB)
+    const size_t w = std::min<size_t>(hb, 16u << 20);
+    std::vector<unsigned char> h0(w), h1(w);
+    bool ok = true;
+    for (size_t off : {(size_t)0, hb - w}) {
+      CK(hipMemcpy(h0.data(), (char*)src + off, w, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(h1.data(), (char*)dst + off, w, hipMemcpyDeviceToHost));
+      ok = ok && std::memcmp(h0.data(), h1.data(), w) == 0;
+    }
+    r.hbm_copy_ok = ok;
+  }
+  CK(hipFree(src));
+  CK(hipFree(dst));
+  CK(hipEventDestroy(e0));
+  CK(hipEventDestroy(e1));
+  CK(hipStreamDestroy(s));
+  r.t_hbm = wall_now();
+  return true;
+}
+
+struct CollRow {
+  size_t bytes;
+  double us, algbw, busbw;
+  unsigned long long bad;
+};
+
+double bus_factor(int n) { return n > 1 ? 2.0 * (n - 1) / n : 0.0; }
+
+// C1: RCCL all-reduce sweep, single process owning all devices.
+bool run_rccl(const std::vector<int>& devs, const Opts& o, std::vector<CollRow>& rows) {
+  const int n = (int)devs.size();
+  std::vector<ncclComm_t> comms(n);
+  if (ncclCommInitAll(comms.data(), n, devs.data()) != ncclSuccess) {
+    fail("ncclCommInitAll failed");
+    return false;
+  }
+  std::vector<hipStream_t> st(n);
+  std::vector<void*> buf(n);
+  std::vector<unsigned long long*> bad(n);
+  const size_t maxb = (size_t)o.allreduce_max_mib << 20;
+  for (int i = 0; i < n; ++i) {
+    CK(hipSetDevice(devs[i]));
+    CK(hipStreamCreateWithFlags(&st[i], hipStreamNonBlocking));
+    CK(hipMalloc(&buf[i], maxb));
+    CK(hipMalloc(&bad[i], 8));
+  }
+  bool ok = true;
+  for (size_t bytes = 1 << 20; bytes <= maxb; bytes *= 4) {
+    const size_t cnt = bytes / 2;
+    auto run_once = [&]() -> bool {
+      if (ncclGroupStart() != ncclSuccess) return false;
+      for (int i = 0; i < n; ++i)
+        if (ncclAllReduce(buf[i], buf[i], cnt, ncclBfloat16, ncclSum, comms[i], st[i]) !=
+            ncclSuccess)
+          return false;
+      return ncclGroupEnd() == ncclSuccess;
+    };
+    for (int i = 0; i < n; ++i) {
+      CK(hipSetDevice(devs[i]));
+      hipLaunchKernelGGL(fill_pattern, dim3(1024), dim3(256), 0, st[i], (uint16_t*)buf[i], cnt, i);
+      CK(hipMemsetAsync(bad[i], 0, 8, st[i]));
+    }
+    if (!run_once()) { fail("ncclAllReduce failed"); return false; }
+    unsigned long long tot_bad = 0;
+    for (int i = 0; i < n; ++i) {
+      CK(hipSetDevice(devs[i]));
+      hipLaunchKernelGGL(check_pattern, dim3(1024), dim3(256), 0, st[i], (const uint16_t*)buf[i], cnt, n, bad[i]);
+      unsigned long long b = 0;
+      CK(hipMemcpyAsync(&b, bad[i], 8, hipMemcpyDeviceToHost, st[i]));
+      CK(hipStreamSynchronize(st[i]));
+      tot_bad += b;
+    }
+    const int iters = 10;
+    for (int w = 0; w < 2; ++w) run_once();
+    for (int i = 0; i < n; ++i) { CK(hipSetDevice(devs[i])); CK(hipStreamSynchronize(st[i])); }
+    const auto t0 = Clock::now();
+    for (int it = 0; it < iters; ++it) run_once();
+    for (int i = 0; i < n; ++i) { CK(hipSetDevice(devs[i])); CK(hipStreamSynchronize(st[i])); }
+    const double sec = std::chrono::duration<double>(Clock::now() - t0).count() / iters;
+    const double alg = bytes / sec / 1e9;
+    rows.push_back({bytes, sec * 1e6, alg, alg * bus_factor(n), tot_bad});
+    if (tot_bad) ok = false;
+  }
+  for (int i = 0; i < n; ++i) {
+    (void)hipSetDevice(devs[i]);
+    (void)hipFree(buf[i]);
+    (void)hipFree(bad[i]);
+    (void)hipStreamDestroy(st[i]);
+    ncclCommDestroy(comms[i]);
+  }
+  if (!ok) fail("RCCL all-reduce produced wrong elements");
+  return ok;
+}
+
+// C2: hand-written two-shot all-reduce over peer-mapped xGMI.
+bool run_xgmi(const std::vector<int>& devs, const Opts& o, std::vector<CollRow>& rows) {
+  const int n = (int)devs.size();
+  if (n < 2 || n > ntm::xgmi::kMaxRanks) return true;
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < n; ++j) {
+      if (i == j) continue;
+      int can = 0;
+      CK(hipDeviceCanAccessPeer(&can, devs[i], devs[j]));
+      if (!can) {
+        fail("no peer access between GPUs " + std::to_string(devs[i]) + " and " + std::to_string(devs[j]));
+        return false;
+      }
+      CK(hipSetDevice(devs[i]));
+      hipError_t e = hipDeviceEnablePeerAccess(devs[j], 0);
+      if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) CK(e);
+    }
+  const int nblk = 64;
+  const size_t maxb = std::min<size_t>((size_t)o.allreduce_max_mib << 20, (size_t)1 << 30);
+  std::vector<void*> in(n), out(n);
+  std::vector<unsigned*> sig(n);
+  std::vector<unsigned*> err(n);
+  std::vector<hipStream_t> st(n);
+  for (int i = 0; i < n; ++i) {
+    CK(hipSetDevice(devs[i]));
+    CK(hipStreamCreateWithFlags(&st[i], hipStreamNonBlocking));
+    CK(hipMalloc(&in[i], maxb));
+    CK(hipMalloc(&out[i], maxb));
+    CK(hipExtMallocWithFlags((void**)&sig[i], ntm_xgmi_signal_bytes(nblk), hipDeviceMallocUncached));
+    CK(hipMemset(sig[i], 0, ntm_xgmi_signal_bytes(nblk)));
+    CK(hipMalloc(&err[i], 4));
+    CK(hipMemset(err[i], 0, 4));
+  }
+  unsigned epoch = 0;
+  bool ok = true;
+  for (size_t bytes = 1 << 20; bytes <= maxb; bytes *= 4) {
+    const size_t cnt = bytes / 2;
+    auto run_once = [&]() -> bool {
+      ++epoch;
+      for (int i = 0; i < n; ++i) {
+        if (hipSetDevice(devs[i]) != hipSuccess) return false;
+        if (ntm_xgmi_allreduce_bf16((const void* const*)in.data(), out.data(), sig.data(), n, i, 1,
+                                    nblk, cnt, epoch, err[i], 0, st[i]) != 0)
+          return false;
+      }
+      return true;
+    };
+    for (int i = 0; i < n; ++i) {
+      CK(hipSetDevice(devs[i]));
+      hipLaunchKernelGGL(fill_pattern, dim3(1024), dim3(256), 0, st[i], (uint16_t*)in[i], cnt, i);
+      CK(hipStreamSynchronize(st[i]));
+    }
+    if (!run_once()) { fail("xGMI all-reduce launch failed"); return false; }
+    unsigned long long tot_bad = 0;
+    for (int i = 0; i < n; ++i) {
+      CK(hipSetDevice(devs[i]));
+      CK(hipStreamSynchronize(st[i]));
+      unsigned e = 0;
+      CK(hipMemcpy(&e, err[i], 4, hipMemcpyDeviceToHost));
+      if (e) { fail("xGMI all-reduce barrier timed out (phase " + std::to_string(e - 1) + ")"); return false; }
+      unsigned long long* bad;
+      CK(hipMalloc(&bad, 8));
+      CK(hipMemset(bad, 0, 8));
+      hipLaunchKernelGGL(check_pattern, dim3(1024), dim3(256), 0, st[i], (const uint16_t*)out[i], cnt, n, bad);
+      unsigned long long b = 0;
+      CK(hipMemcpyAsync(&b, bad, 8, hipMemcpyDeviceToHost, st[i]));
+      CK(hipStreamSynchronize(st[i]));
+      CK(hipFree(bad));
+      tot_bad += b;
+    }
+    const int iters = 10;
+    const auto t0 = Clock::now();
+    for (int it = 0; it < iters; ++it) run_once();
+    for (int i = 0; i < n; ++i) { CK(hipSetDevice(devs[i])); CK(hipStreamSynchronize(st[i])); }
+    const double sec = std::chrono::duration<double>(Clock::now() - t0).count() / iters;
+    const double alg = bytes / sec / 1e9;
+    rows.push_back({bytes, sec * 1e6, alg, alg * bus_factor(n), tot_bad});
+    if (tot_bad) ok = false;
+  }
+  for (int i = 0; i < n; ++i) {
+    (void)hipSetDevice(devs[i]);
+    (void)hipFree(in[i]);
+    (void)hipFree(out[i]);
+    (void)hipFree(sig[i]);
+    (void)hipFree(err[i]);
+    (void)hipStreamDestroy(st[i]);
+  }
+  if (!ok) fail("xGMI all-reduce produced wrong elements");
+  return ok;
+}
+
+std::string coll_json(const std::vector<CollRow>& rows) {
+  std::string s = "[";
+  for (size_t i = 0; i < rows.size(); ++i) {
+    const auto& r = rows[i];
+    s += (i ? "," : "") + std::string("{\"bytes\":") + std::to_string(r.bytes) +
+         ",\"time_us\":" + jnum(r.us) + ",\"algbw_GBps\":" + jnum(r.algbw) +
+         ",\"busbw_GBps\":" + jnum(r.busbw) + ",\"wrong\":" + std::to_string(r.bad) + "}";
+  }
+  return s + "]";
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  const double t_start = process_start_epoch();
+  Opts o;
+  if (!parse(argc, argv, o)) {
+    usage();
+    return 2;
+  }
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+    std::printf("{\"passed\":false,\"failures\":[\"no AMD GPU visible\"]}\n");
+    return 2;
+  }
+  const int n = o.gpus > 0 ? std::min(o.gpus, ndev) : ndev;
+  if (o.gpus > ndev) fail("requested " + std::to_string(o.gpus) + " GPUs, " + std::to_string(ndev) + " visible");
+  std::vector<int> devs(n);
+  for (int i = 0; i < n; ++i) devs[i] = i;
+  const double t_hip = wall_now();
+
+  std::vector<GpuResult> res(n);
+  std::vector<std::thread> th;
+  for (int i = 0; i < n; ++i) th.emplace_back([&, i] { run_gpu(devs[i], o, res[i]); });
+  for (auto& t : th) t.join();
+  const double t_local = wall_now();
+
+  for (auto& r : res) {
+    const std::string d = "gpu" + std::to_string(r.device) + ": ";
+    if (r.gemm_bad != 0) fail(d + "GEMM verification failed (" + std::to_string(r.gemm_bad) + " elements)");
+    if (o.tflops_floor > 0 && r.gemm_tflops < o.tflops_floor)
+      fail(d + "GEMM " + jnum(r.gemm_tflops) + " TFLOP/s below floor " + jnum(o.tflops_floor));
+    if (o.min_hbm_gb > 0 && r.total_gb < o.min_hbm_gb)
+      fail(d + "HBM " + jnum(r.total_gb) + " GB below " + jnum(o.min_hbm_gb) + " GB");
+    if (!r.hbm_copy_ok) fail(d + "HBM copy mismatch");
+    if (o.hbm_floor_gbps > 0 && r.hbm_copy_gbps < o.hbm_floor_gbps)
+      fail(d + "HBM copy " + jnum(r.hbm_copy_gbps) + " GB/s below floor");
+  }
+
+  std::vector<CollRow> rccl_rows, xgmi_rows;
+  if (n > 1) run_rccl(devs, o, rccl_rows);
+  const double t_rccl = wall_now();
+  if (n > 1 && o.xgmi) run_xgmi(devs, o, xgmi_rows);
+  const double t_end = wall_now();
+
+  double agg = 0;
+  for (auto& r : res) agg += r.gemm_tflops;
+  std::string js = "{";
+  js += "\"tool\":\"amdgpu-validate\",\"passed\":" + std::string(g_failures.empty() ? "true" : "false");
+  js += ",\"n_gpus\":" + std::to_string(n) + ",\"gemm_size\":" + std::to_string(o.size);
+  js += ",\"gemm_tflops_aggregate\":" + jnum(agg);
+  js += ",\"gpus\":[";
+  for (int i = 0; i < n; ++i) {
+    const auto& r = res[i];
+    js += (i ? "," : "") + std::string("{\"device\":") + std::to_string(r.device) +
+          ",\"name\":" + jstr(r.name) + ",\"arch\":" + jstr(r.arch) +
+          ",\"hbm_total_gb\":" + jnum(r.total_gb) + ",\"gemm_ms\":" + jnum(r.gemm_ms) +
+          ",\"gemm_tflops\":" + jnum(r.gemm_tflops) +
+          ",\"gemm_wrong\":" + (r.gemm_bad == ~0ull ? std::string("null") : std::to_string(r.gemm_bad)) +
+          ",\"gemm_max_abs_err\":" + jnum(r.gemm_max_err) +
+          ",\"hbm_copy_GBps\":" + jnum(r.hbm_copy_gbps) + "}";
+  }
+  js += "],\"rccl_allreduce_bf16\":" + coll_json(rccl_rows);
+  js += ",\"xgmi_allreduce_bf16\":" + coll_json(xgmi_rows);
+  double t_gemm = t_hip, t_hbm = t_hip;
+  for (auto& r : res) { t_gemm = std::max(t_gemm, r.t_gemm); t_hbm = std::max(t_hbm, r.t_hbm); }
+  js += ",\"phases_s\":{\"process_start_to_hip_init\":" + jnum(t_hip - t_start) +
+        ",\"gemm_done\":" + jnum(t_gemm - t_start) + ",\"hbm_done\":" + jnum(t_hbm - t_start) +
+        ",\"rccl_done\":" + jnum(t_rccl - t_start) + ",\"end\":" + jnum(t_end - t_start) + "}";
+  js += ",\"start_epoch_s\":" + jnum(t_start) + ",\"end_epoch_s\":" + jnum(t_end);
+  js += ",\"failures\":[";
+  for (size_t i = 0; i < g_failures.size(); ++i) js += (i ? "," : "") + jstr(g_failures[i]);
+  js += "]}";
+  (void)t_local;
+  std::printf("%s\n", js.c_str());
+  if (!o.out.empty()) {
+    std::ofstream f(o.out);
+    f << js << "\n";
+  }
+  return g_failures.empty() ? 0 : 1;
+}

@@ -1,0 +1,68 @@
+// C ABI for C2, the hand-written xGMI all-reduce (see ntm/xgmi_allreduce.hpp).
+#include "ntm/xgmi_allreduce.hpp"
+
+#define NTM_API extern "C" __attribute__((visibility("default")))
+
+// in_ptrs/out_ptrs/sig_ptrs: host arrays of `nranks` device pointers (peer-
+// accessible from the launching device). Launches ranks rank_base ..
+// rank_base + nranks_here - 1 on `stream` (nranks_here = nranks simulates the
+// whole communicator on one device). `err` (device u32, zeroed by the caller)
+// receives 1/2 if a phase-0/1 barrier timed out. count % (8*nranks) == 0.
+NTM_API int ntm_xgmi_allreduce_bf16(const void* const* in_ptrs,
+                                    void* const* out_ptrs,
+                                    unsigned* const* sig_ptrs, int nranks,
+                                    int rank_base, int nranks_here, int nblk,
+                                    size_t count, unsigned epoch, unsigned* err,
+                                    int one_shot, void* stream) {
+  using namespace ntm::xgmi;
+  if (nranks < 1 || nranks > kMaxRanks || nranks_here < 1 ||
+      rank_base + nranks_here > nranks || nblk < 1 || epoch == 0 ||
+      count % (8 * (size_t)nranks) != 0)
+    return (int)hipErrorInvalidValue;
+  Peers p{};
+  for (int r = 0; r < nranks; ++r) {
+    p.in[r] = (const __bf16*)in_ptrs[r];
+    p.out[r] = (__bf16*)out_ptrs[r];
+    p.sig[r] = sig_ptrs ? sig_ptrs[r] : nullptr;
+  }
+  const dim3 grid((unsigned)(nranks_here * nblk));
+  if (one_shot) {
+    hipLaunchKernelGGL(allreduce_1shot_kernel, grid, dim3(kThreads), 0,
+                       (hipStream_t)stream, p, nranks, rank_base, nblk, count);
+  } else {
+    if (!sig_ptrs) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(allreduce_2shot_kernel, grid, dim3(kThreads), 0,
+                       (hipStream_t)stream, p, nranks, rank_base, nblk, count,
+                       epoch, err);
+  }
+  return (int)hipGetLastError();
+}
+
+NTM_API size_t ntm_xgmi_signal_bytes(int nblk) {
+  return ntm::xgmi::signal_bytes(nblk);
+}
+
+// ---- buffers + IPC for the one-process-per-GPU path (torch.distributed):
+// every rank allocates its in/out/signal buffers here, exchanges the 64-byte
+// IPC handles (all_gather_object) and opens the peers' ones.
+NTM_API int ntm_malloc(void** p, size_t bytes, int uncached) {
+  return uncached ? (int)hipExtMallocWithFlags(p, bytes, hipDeviceMallocUncached)
+                  : (int)hipMalloc(p, bytes);
+}
+NTM_API int ntm_free(void* p) { return (int)hipFree(p); }
+NTM_API int ntm_memset_async(void* p, int v, size_t bytes, void* stream) {
+  return (int)hipMemsetAsync(p, v, bytes, (hipStream_t)stream);
+}
+NTM_API int ntm_ipc_handle(void* p, void* out64) {
+  hipIpcMemHandle_t h;
+  const hipError_t e = hipIpcGetMemHandle(&h, p);
+  if (e == hipSuccess) __builtin_memcpy(out64, &h, sizeof(h) < 64 ? sizeof(h) : 64);
+  return (int)e;
+}
+NTM_API int ntm_ipc_open(const void* in64, void** p) {
+  hipIpcMemHandle_t h;
+  __builtin_memcpy(&h, in64, sizeof(h) < 64 ? sizeof(h) : 64);
+  return (int)hipIpcOpenMemHandle(p, h, hipIpcMemLazyEnablePeerAccess);
+}
+NTM_API int ntm_ipc_close(void* p) { return (int)hipIpcCloseMemHandle(p); }
+NTM_API int ntm_ipc_handle_bytes() { return (int)sizeof(hipIpcMemHandle_t); }
