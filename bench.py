@@ -131,6 +131,17 @@ def main(argv=None) -> int:
         extras["hipblaslt_tflops_per_gpu_rank0"] = wl.flops / hb_ms / 1e9
         extras["ours_tflops_per_gpu"] = total_tflops / n
         del cc
+        # same K1 with the fused ABFT row-checksum epilogue, then its O(n^2) check
+        ev[0].record()
+        for _ in range(50):
+            wl.step_checked()
+        ev[1].record()
+        torch.cuda.synchronize(dev)
+        extras["abft_gemm_tflops_per_gpu_rank0"] = wl.flops / (ev[0].elapsed_time(ev[1]) / 50) / 1e9
+        ab = wl.abft()
+        extras["abft_rank0"] = ab.as_dict()
+        if not ab.ok:
+            verified = False
     del wl
     torch.cuda.empty_cache()
 

@@ -6,7 +6,8 @@ what ``bench.py`` times. It replaces the NVIDIA operator-validator's CUDA
 ``vectorAdd`` (implicit in /root/reference/eks/main.tf:185-203) with:
 
 * K1 - hand-written bf16 MFMA GEMM (TFLOP/s, fully verified against an
-  independent fp32 FMA reference),
+  independent fp32 FMA reference once, then ABFT row-checksummed on every
+  checked launch through the fused epilogue - cheap enough to run always),
 * K2 - HBM stream bandwidth + capacity check (288 GB class),
 * C1 - RCCL all-reduce sweep over xGMI (every element checked),
 
@@ -36,6 +37,7 @@ class ValidationConfig:
     gemm_iters: int = 50            # timed K1 launches for the TFLOP/s figure
     gemm_warmup: int = 5
     check: bool = True              # full-matrix verification vs fp32 reference
+    abft_iters: int = 3             # checksum-verified K1 launches (0 = off)
     hbm_bytes: int = 2 * GiB        # K2 copy size (src + dst = 2x this)
     hbm_iters: int = 10
     allreduce_min_bytes: int = 1 << 20
@@ -67,6 +69,7 @@ class GemmWorkload:
         self.c = torch.empty((self.m, self.n), dtype=torch.bfloat16, device=device)
         self.ops.fill_uniform_(self.a, seed=seed * 2 + 1)
         self.ops.fill_uniform_(self.b, seed=seed * 2 + 2)
+        self.rowsum = torch.empty(self.m, dtype=torch.float32, device=device)
 
     @property
     def flops(self) -> float:
@@ -74,6 +77,16 @@ class GemmWorkload:
 
     def step(self) -> None:
         self.ops.gemm_bf16(self.a, self.b, self.c)
+
+    def step_checked(self) -> None:
+        """K1 with the fused ABFT row-checksum epilogue."""
+        self.ops.gemm_bf16_rowsum(self.a, self.b, self.c, self.rowsum)
+
+    def abft(self, corrupt: bool = False):
+        """Check the last ``step_checked`` output in O(n^2)."""
+        if corrupt:
+            self.c.view(-1)[4321 % self.c.numel()] += 256.0
+        return self.ops.abft_check(self.a, self.b, self.c, self.rowsum)
 
     def verify(self, corrupt: bool = False):
         if corrupt:
@@ -176,6 +189,15 @@ def run_validation(env: DistEnv, cfg: ValidationConfig, clock: PhaseClock | None
     gemm["tflops"] = wl.flops / sec / 1e12
     if cfg.tflops_floor and gemm["tflops"] < cfg.tflops_floor:
         failures.append(f"gemm {gemm['tflops']:.1f} TFLOP/s below floor {cfg.tflops_floor}")
+    if cfg.abft_iters:
+        sec_chk = _time_loop(wl.step_checked, cfg.abft_iters, dev)
+        corrupt = fi == "corrupt_abft" and env.rank == env.world_size - 1
+        rep = wl.abft(corrupt=corrupt)
+        gemm["abft"] = rep.as_dict()
+        gemm["abft_tflops"] = wl.flops / sec_chk / 1e12
+        if not rep.ok:
+            failures.append(f"gemm ABFT checksum: {rep.bad_acc} accumulator / "
+                            f"{rep.bad_store} stored rows inconsistent")
     clock.mark("gemm_verified")
     del wl
 

@@ -1,17 +1,22 @@
 """MI355X (gfx950) HIP kernels used by the post-provision validation Job.
 
-K1 ``gemm_bf16``      - 256x256x64 LDS-DMA + MFMA bf16 GEMM (the headline).
-K2 ``stream_copy``    - float4 HBM stream.
-K3 ``fill_uniform_``, ``ref_gemm_f32``, ``verify_bf16`` - synthetic data and checks.
+K1 ``gemm_bf16``      - 256x256x64 LDS-DMA + MFMA bf16 GEMM (the headline);
+   ``gemm_bf16_rowsum`` - same kernel with the fused ABFT row-checksum epilogue.
+K2 ``stream_copy``, ``stream_read`` - tuned float4 HBM streams.
+K3 ``fill_uniform_``, ``ref_gemm_f32``, ``verify_bf16``, ``abft_check`` - synthetic
+   data, full fp32 reference check and the O(n^2) checksum check.
 
 Import is cheap; the native library is loaded on first kernel call and raises
 ``NativeLibraryMissing`` if it was not built (no silent fallback).
 """
 from ._lib import NativeLibraryMissing, available, version  # noqa: F401
 from .kernels import (  # noqa: F401
+    AbftReport,
     VerifyReport,
+    abft_check,
     fill_uniform_,
     gemm_bf16,
+    gemm_bf16_rowsum,
     gemm_shape_ok,
     gemm_tolerance,
     ref_gemm_f32,

@@ -31,27 +31,24 @@ def _declare(lib: ctypes.CDLL) -> None:
         "ntm_gemm_bf16": ([c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp], c_int),
         "ntm_gemm_bf16_variant": (
             [c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp], c_int),
+        "ntm_gemm_bf16_rowsum": (
+            [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp], c_int),
+        "ntm_abft_check": ([c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int,
+                            c_vp, c_vp, c_vp], c_int),
+        "ntm_abft_result_bytes": ([], c_int),
         "ntm_fill_uniform_bf16": ([c_vp, c_size, ctypes.c_ulonglong, c_float, c_vp], c_int),
         "ntm_ref_gemm_f32": ([c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp], c_int),
         "ntm_verify_bf16": ([c_vp, c_vp, c_size, c_float, c_float, c_vp, c_vp], c_int),
         "ntm_verify_result_bytes": ([], c_int),
         "ntm_stream_copy": ([c_vp, c_vp, c_size, c_vp], c_int),
         "ntm_stream_read": ([c_vp, c_size, c_vp, c_vp], c_int),
-    }
-    optional = {
-        "ntm_xgmi_allreduce_sum_bf16": (
-            [c_vp, c_vp, c_int, c_int, c_size, c_vp, c_vp], c_int),
-        "ntm_xgmi_reduce_local_bf16": ([c_vp, c_vp, c_int, c_size, c_vp], c_int),
+        "ntm_stream_copy_ex": ([c_vp, c_vp, c_size, c_int, c_int, c_int, c_vp], c_int),
+        "ntm_stream_read_ex": ([c_vp, c_size, c_vp, c_int, c_int, c_int, c_vp], c_int),
     }
     for name, (argt, rest) in sig.items():
         fn = getattr(lib, name)
         fn.argtypes = argt
         fn.restype = rest
-    for name, (argt, rest) in optional.items():
-        fn = getattr(lib, name, None)
-        if fn is not None:
-            fn.argtypes = argt
-            fn.restype = rest
 
 
 def lib() -> ctypes.CDLL:

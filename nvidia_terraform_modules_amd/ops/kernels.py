@@ -38,8 +38,9 @@ def gemm_bf16(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
     """K1: ``out = a @ b.T`` in bf16 with fp32 accumulation on MFMA.
 
     a: [M, K] bf16, b: [N, K] bf16 (both K-contiguous), out: [M, N] bf16.
-    ``variant``: "wave128" (4 waves, 128x128 per wave; the default) or
-    "pingpong8" (8 waves, two per SIMD, staggered) - see validation/include.
+    ``variant``: "default" = "pingpong8" (8 waves, two per SIMD, staggered;
+    fastest measured), or the experimental "wave128"/"wave128d4" (4 waves,
+    128x128 per wave, AGPR-pinned accumulators) - see validation/include.
     """
     _require(a, "a", torch.bfloat16)
     _require(b, "b", torch.bfloat16)
@@ -59,6 +60,72 @@ def gemm_bf16(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
         a.stride(0), b.stride(0), out.stride(0), stream_handle())
     check(rc, "ntm_gemm_bf16")
     return out
+
+
+def gemm_bf16_rowsum(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
+                     rowsum: torch.Tensor | None = None) -> tuple[torch.Tensor, torch.Tensor]:
+    """K1 with the fused ABFT epilogue: returns ``(out, rowsum)`` where
+    ``rowsum[m]`` is the fp32 sum over n of the accumulators of row m (the
+    8-wave kernel; ``rowsum`` is zeroed here, stream-ordered)."""
+    _require(a, "a", torch.bfloat16)
+    _require(b, "b", torch.bfloat16)
+    m, k = a.shape
+    n = b.shape[0]
+    if b.shape[1] != k or not gemm_shape_ok(m, n, k):
+        raise ValueError(f"shape ({m},{n},{k}) not tiled by the 256x256x64 kernel")
+    if out is None:
+        out = torch.empty((m, n), dtype=torch.bfloat16, device=a.device)
+    _require(out, "out", torch.bfloat16)
+    if rowsum is None:
+        rowsum = torch.empty(m, dtype=torch.float32, device=a.device)
+    if rowsum.dtype != torch.float32 or rowsum.numel() < m or not rowsum.is_contiguous():
+        raise ValueError("rowsum must be a contiguous fp32 tensor of >= M entries")
+    rowsum.zero_()
+    rc = lib().ntm_gemm_bf16_rowsum(a.data_ptr(), b.data_ptr(), out.data_ptr(), rowsum.data_ptr(),
+                                    m, n, k, a.stride(0), b.stride(0), out.stride(0),
+                                    stream_handle())
+    check(rc, "ntm_gemm_bf16_rowsum")
+    return out, rowsum
+
+
+@dataclass
+class AbftReport:
+    rows: int
+    bad_acc: int        # rows whose fused fp32 checksum disagrees with A . colsum(B)
+    bad_store: int      # rows whose stored bf16 sum disagrees with the checksum
+    max_rel_acc: float  # max |err| / ||C_m||_2
+    max_rel_store: float
+
+    @property
+    def ok(self) -> bool:
+        return self.bad_acc == 0 and self.bad_store == 0
+
+    def as_dict(self) -> dict:
+        return {"rows": self.rows, "bad_acc": self.bad_acc, "bad_store": self.bad_store,
+                "max_rel_acc": self.max_rel_acc, "max_rel_store": self.max_rel_store,
+                "ok": self.ok}
+
+
+def abft_check(a: torch.Tensor, b: torch.Tensor, c: torch.Tensor,
+               rowsum: torch.Tensor) -> AbftReport:
+    """K3: O(MK + NK + MN) ABFT check of ``c = a @ b.T`` against the fused
+    row checksum (see aux_kernels.hpp). Synchronises to read the result."""
+    m, k = a.shape
+    n = b.shape[0]
+    if c.shape != (m, n) or c.dtype != torch.bfloat16 or c.stride(1) != 1:
+        raise ValueError("c must be [M, N] bf16 with unit inner stride")
+    scratch = torch.empty(k, dtype=torch.float64, device=a.device)
+    res = torch.empty(lib().ntm_abft_result_bytes(), dtype=torch.uint8, device=a.device)
+    rc = lib().ntm_abft_check(a.data_ptr(), b.data_ptr(), c.data_ptr(), rowsum.data_ptr(),
+                              m, n, k, a.stride(0), b.stride(0), c.stride(0),
+                              scratch.data_ptr(), res.data_ptr(), stream_handle())
+    check(rc, "ntm_abft_check")
+    raw = res.cpu().numpy().tobytes()
+    return AbftReport(
+        rows=m, bad_acc=int.from_bytes(raw[0:8], "little"),
+        bad_store=int.from_bytes(raw[8:16], "little"),
+        max_rel_acc=ctypes.c_float.from_buffer_copy(raw[16:20]).value,
+        max_rel_store=ctypes.c_float.from_buffer_copy(raw[20:24]).value)
 
 
 def fill_uniform_(t: torch.Tensor, seed: int, scale: float = 1.0) -> torch.Tensor:
@@ -120,22 +187,37 @@ def verify_bf16(c: torch.Tensor, ref: torch.Tensor, atol: float, rtol: float) ->
     return VerifyReport(n=c.numel(), bad=bad, max_abs_err=max_err, rel_rms_err=rel)
 
 
-def stream_copy(src: torch.Tensor, dst: torch.Tensor) -> None:
-    """K2: float4 non-temporal HBM copy of ``src`` into ``dst`` (byte-identical)."""
+# (unroll, policy, grid) of the block-tiled K2 kernels; policy bit0 =
+# nontemporal loads, bit1 = nontemporal stores, bit2 = software-pipelined
+# copy, grid 0 = auto; unroll 1 = the original grid-stride kernel. Chosen
+# by tools/hbm_sweep.py on MI355X (4 GiB, profiles/r1_hbm_sweep/):
+#   copy  (4, 7, 256)  5.75 TB/s  (torch copy_ 4.74, grid-stride 4.84)
+#   read  (8, 1, 1024) 7.13 TB/s  (grid-stride 6.11)
+STREAM_COPY_CONFIG: tuple[int, int, int] = (4, 7, 256)
+STREAM_READ_CONFIG: tuple[int, int, int] = (8, 1, 1024)
+
+
+def stream_copy(src: torch.Tensor, dst: torch.Tensor,
+                config: tuple[int, int, int] | None | str = "tuned") -> None:
+    """K2: float4 HBM copy of ``src`` into ``dst`` (byte-identical)."""
     nbytes = src.numel() * src.element_size()
     if dst.numel() * dst.element_size() < nbytes or nbytes % 16:
         raise ValueError("stream_copy needs 16-byte multiple sizes and a large enough dst")
-    check(lib().ntm_stream_copy(src.data_ptr(), dst.data_ptr(), nbytes, stream_handle()),
-          "ntm_stream_copy")
+    cfg = STREAM_COPY_CONFIG if config == "tuned" else (config or (1, 0, 0))
+    rc = lib().ntm_stream_copy_ex(src.data_ptr(), dst.data_ptr(), nbytes, *cfg, stream_handle())
+    check(rc, "ntm_stream_copy")
 
 
-def stream_read(src: torch.Tensor, sink: torch.Tensor) -> None:
+def stream_read(src: torch.Tensor, sink: torch.Tensor,
+                config: tuple[int, int, int] | None | str = "tuned") -> None:
     """K2: read-only HBM sweep of ``src`` (``sink`` only written on NaN/inf)."""
     nbytes = src.numel() * src.element_size()
     if nbytes % 16:
         raise ValueError("stream_read needs a 16-byte multiple size")
-    check(lib().ntm_stream_read(src.data_ptr(), nbytes, sink.data_ptr(), stream_handle()),
-          "ntm_stream_read")
+    cfg = STREAM_READ_CONFIG if config == "tuned" else (config or (1, 0, 0))
+    rc = lib().ntm_stream_read_ex(src.data_ptr(), nbytes, sink.data_ptr(), *cfg,
+                                  stream_handle())
+    check(rc, "ntm_stream_read")
 
 
 def gemm_tolerance(k: int) -> tuple[float, float]:

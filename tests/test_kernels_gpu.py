@@ -112,6 +112,22 @@ def test_stream_copy_and_read(ops):
     assert torch.count_nonzero(sink) == 0
 
 
+@pytest.mark.parametrize("nbytes", [16, 4096 + 48, (1 << 20) * 3 + 16 * 7])
+def test_stream_copy_all_configs_exact(ops, nbytes):
+    """Every (unroll, policy) copy kernel is byte-exact, including sub-tile
+    tails and a grid larger than the tile count."""
+    src = torch.randint(0, 255, (nbytes,), dtype=torch.uint8, device="cuda")
+    for cfg in [(1, 0, 0)] + [(u, p, g) for u in (2, 4, 8, 16) for p in range(8)
+                              for g in (0, 7, 256)]:
+        dst = torch.zeros_like(src)
+        ops.stream_copy(src, dst, config=cfg)
+        assert torch.equal(src, dst), cfg
+    sink = torch.zeros(8192, device="cuda")
+    for cfg in [(u, p, g) for u in (2, 4, 8, 16) for p in (0, 1) for g in (0, 5)]:
+        ops.stream_read(src, sink, config=cfg)   # must not fault on tails
+    torch.cuda.synchronize()
+
+
 def test_gemm_graph_capture(ops):
     a = _rand(ops, (1024, 512), 21)
     b = _rand(ops, (1024, 512), 22)
@@ -129,3 +145,40 @@ def test_gemm_graph_capture(ops):
     ref = a.float() @ b.float().T
     atol, rtol = ops.gemm_tolerance(512)
     assert torch.all((c.float() - ref).abs() <= atol + rtol * ref.abs())
+
+
+@pytest.mark.parametrize("m,n,k", [(256, 256, 128), (512, 1024, 320), (2048, 2048, 2048),
+                                   (8192, 8192, 8192)])
+def test_abft_rowsum_matches_fp64(ops, m, n, k):
+    """The fused epilogue's row checksum equals the fp64 row sums of the exact
+    product, and the O(n^2) checker passes a clean GEMM."""
+    a = _rand(ops, (m, k), 31 + k)
+    b = _rand(ops, (n, k), 37 + n)
+    c, rs = ops.gemm_bf16_rowsum(a, b)
+    exact = (a.double() @ b.double().sum(0)) if m * k < 2**27 else None
+    if exact is not None:
+        norm = (a.float() @ b.float().T).double().norm(dim=1)
+        assert torch.all((rs.double() - exact).abs() <= 1e-3 + 2**-14 * norm)
+    c_plain = ops.gemm_bf16(a, b)
+    assert torch.equal(c, c_plain)  # the checksum epilogue does not change C
+    rep = ops.abft_check(a, b, c, rs)
+    assert rep.ok, rep.as_dict()
+    assert rep.max_rel_acc < 2**-17
+
+
+def test_abft_detects_corruption(ops):
+    a = _rand(ops, (1024, 512), 41)
+    b = _rand(ops, (1024, 512), 42)
+    c, rs = ops.gemm_bf16_rowsum(a, b)
+    assert ops.abft_check(a, b, c, rs).ok
+    c2 = c.clone()
+    c2[17, 300] += 64.0                       # a stored-output fault
+    rep = ops.abft_check(a, b, c2, rs)
+    assert rep.bad_store == 1 and rep.bad_acc == 0
+    rs2 = rs.clone()
+    rs2[900] += 0.5                           # an accumulator-path fault
+    rep = ops.abft_check(a, b, c, rs2)
+    assert rep.bad_acc == 1
+    c3 = c.clone()
+    c3[5, 5] = float("nan")
+    assert not ops.abft_check(a, b, c3, rs).ok

@@ -43,3 +43,23 @@ def test_validation_job_tflops_floor():
     rep = run_validation(_env(), cfg, with_hbm=False)
     assert not rep.passed and "below floor" in rep.failures[0]
     torch.cuda.synchronize()
+
+
+def test_validation_job_abft_detects_injected_fault():
+    from nvidia_terraform_modules_amd.models.validation_job import ValidationConfig, run_validation
+
+    cfg = ValidationConfig(size=1024, gemm_iters=2, check=False, abft_iters=2,
+                           fault_inject="corrupt_abft")
+    rep = run_validation(_env(), cfg, with_hbm=False)
+    assert not rep.passed
+    assert any("ABFT" in f for f in rep.failures)
+    assert rep.gemm["abft"]["bad_store"] == 1
+
+
+def test_validation_job_reports_abft_clean():
+    from nvidia_terraform_modules_amd.models.validation_job import ValidationConfig, run_validation
+
+    cfg = ValidationConfig(size=2048, gemm_iters=3, abft_iters=3, fault_inject="")
+    rep = run_validation(_env(), cfg, with_hbm=False)
+    assert rep.passed, rep.failures
+    assert rep.gemm["abft"]["ok"] and rep.gemm["abft_tflops"] > 10

@@ -149,6 +149,85 @@ __global__ void __launch_bounds__(256)
   }
 }
 
+// ------------------------------------------------- K3: ABFT row checksum
+// Online check of a K1 GEMM in O(MK + NK + MN) instead of the O(MNK) fp32
+// reference (Huang-Abraham checksums): since C = A B^T,
+//   sum_n C[m,n] = sum_k A[m,k] * bsum[k],   bsum[k] = sum_n B[n,k].
+// K1's epilogue accumulates rowsum[m] from its fp32 accumulators
+// (gemm_bf16.hpp, kRowSum). Two comparisons per row, both scaled by the
+// row's L2 norm ||C_m|| (the natural size of fp32 summation error):
+//   acc   : |rowsum[m] - A_m . bsum|      <= 1e-3 + 2^-14 ||C_m||   (MFMA math)
+//   store : |sum_n bf16(C[m,n]) - rowsum| <= 1e-3 + 2^-6  ||C_m||   (bf16 out)
+// The store bound is ~8 sigma of independent round-to-nearest errors; it
+// assumes rounding errors are uncorrelated (true for random operands).
+struct AbftResult {
+  unsigned long long bad_acc;
+  unsigned long long bad_store;
+  unsigned int max_rel_acc_bits;    // float bits of max err / ||C_m||
+  unsigned int max_rel_store_bits;
+};
+
+__global__ void __launch_bounds__(256)
+    abft_colsum_kernel(const __bf16* __restrict__ B, int N, int K, int ldb,
+                       int rows_per_chunk, double* __restrict__ bsum) {
+  const int k = blockIdx.x * 256 + threadIdx.x;
+  if (k >= K) return;
+  const int n0 = blockIdx.y * rows_per_chunk;
+  const int n1 = min(N, n0 + rows_per_chunk);
+  double s = 0.0;
+  for (int n = n0; n < n1; ++n)
+    s += bf16_bits_to_f32(((const uint16_t*)B)[(size_t)n * ldb + k]);
+  unsafeAtomicAdd(bsum + k, s);
+}
+
+__device__ __forceinline__ double block_sum_256(double v, double* s_tmp) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) s_tmp[threadIdx.x >> 6] = v;
+  __syncthreads();
+  return s_tmp[0] + s_tmp[1] + s_tmp[2] + s_tmp[3];
+}
+
+__device__ __forceinline__ void atomic_max_nonneg(unsigned int* p, float v) {
+  unsigned int bits;
+  __builtin_memcpy(&bits, &v, 4);
+  if (v != v) bits = 0x7fc00000u;
+  atomicMax(p, bits);
+}
+
+__global__ void __launch_bounds__(256)
+    abft_row_check_kernel(const __bf16* __restrict__ A, int lda,
+                          const __bf16* __restrict__ C, int ldc,
+                          const float* __restrict__ rowsum,
+                          const double* __restrict__ bsum, int N, int K,
+                          AbftResult* __restrict__ out) {
+  __shared__ double s_tmp[4];
+  const int m = blockIdx.x;
+  const uint16_t* a = (const uint16_t*)A + (size_t)m * lda;
+  const uint16_t* c = (const uint16_t*)C + (size_t)m * ldc;
+  double r = 0.0, sc = 0.0, ss = 0.0;
+  for (int k = threadIdx.x; k < K; k += 256) r += bf16_bits_to_f32(a[k]) * bsum[k];
+  for (int n = threadIdx.x; n < N; n += 256) {
+    const double v = bf16_bits_to_f32(c[n]);
+    sc += v;
+    ss += v * v;
+  }
+  r = block_sum_256(r, s_tmp);
+  sc = block_sum_256(sc, s_tmp);
+  ss = block_sum_256(ss, s_tmp);
+  if (threadIdx.x == 0) {
+    const double norm = sqrt(ss);
+    const double rs = (double)rowsum[m];
+    const double e_acc = fabs(rs - r), e_st = fabs(sc - rs);
+    // NaN-safe: !(e <= tol) flags NaN
+    if (!(e_acc <= 1e-3 + 0x1p-14 * norm)) atomicAdd(&out->bad_acc, 1ull);
+    if (!(e_st <= 1e-3 + 0x1p-6 * norm)) atomicAdd(&out->bad_store, 1ull);
+    const double den = norm > 1e-30 ? norm : 1e-30;
+    atomic_max_nonneg(&out->max_rel_acc_bits, (float)(e_acc / den));
+    atomic_max_nonneg(&out->max_rel_store_bits, (float)(e_st / den));
+  }
+}
+
 // ------------------------------------------------------------ K2: stream
 // float4 copy, grid-stride, 16 B / lane (1 KiB per wave-instruction). Sized
 // by the host to 256 CUs x 8 blocks (playbook Guideline 11).
@@ -197,6 +276,94 @@ __global__ void __launch_bounds__(256)
   }
   const float s = acc.x + acc.y + acc.z + acc.w;
   // only a NaN/inf can make this store happen; keeps the loads live
+  if (s != s || s == __builtin_huge_valf()) sink[blockIdx.x] = s;
+}
+
+// ---- K2 tuned: block-tiled stream, U independent 16-byte vectors in flight
+// per lane, load/store cache policy chosen at compile time (0 = default,
+// 1 = nontemporal). A block owns whole 256*U-vector tiles (one 4*U KiB
+// contiguous span) and strides over tiles; the sub-tile tail is spread over
+// the grid. Swept by tools/hbm_sweep.py; the C ABI default is the winner.
+template <int P>
+__device__ __forceinline__ f32x4 ld(const f32x4* p) {
+  if constexpr (P == 1) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+template <int P>
+__device__ __forceinline__ void st(f32x4* p, f32x4 v) {
+  if constexpr (P == 1) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+
+template <int U, int LP, int SP>
+__global__ void __launch_bounds__(256)
+    stream_copy_tiled_kernel(const f32x4* __restrict__ src,
+                             f32x4* __restrict__ dst, size_t n4) {
+  constexpr size_t kTile = 256 * U;
+  const size_t ntiles = n4 / kTile;
+  for (size_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const size_t base = t * kTile + threadIdx.x;
+    f32x4 v[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) v[j] = ld<LP>(src + base + j * 256);
+#pragma unroll
+    for (int j = 0; j < U; ++j) st<SP>(dst + base + j * 256, v[j]);
+  }
+  for (size_t i = ntiles * kTile + (size_t)blockIdx.x * 256 + threadIdx.x;
+       i < n4; i += (size_t)gridDim.x * 256)
+    dst[i] = src[i];
+}
+
+// Software-pipelined copy: tile t+grid's loads are in flight while tile t is
+// stored, so the store stream never waits on a fresh load round trip.
+template <int U, int LP, int SP>
+__global__ void __launch_bounds__(256)
+    stream_copy_pipe_kernel(const f32x4* __restrict__ src,
+                            f32x4* __restrict__ dst, size_t n4) {
+  constexpr size_t kTile = 256 * U;
+  const size_t ntiles = n4 / kTile;
+  size_t t = blockIdx.x;
+  f32x4 v[U];
+  if (t < ntiles) {
+#pragma unroll
+    for (int j = 0; j < U; ++j) v[j] = ld<LP>(src + t * kTile + threadIdx.x + j * 256);
+  }
+  for (; t < ntiles; t += gridDim.x) {
+    const size_t tn = t + gridDim.x;
+    f32x4 w[U];
+    if (tn < ntiles) {
+#pragma unroll
+      for (int j = 0; j < U; ++j) w[j] = ld<LP>(src + tn * kTile + threadIdx.x + j * 256);
+    }
+#pragma unroll
+    for (int j = 0; j < U; ++j) st<SP>(dst + t * kTile + threadIdx.x + j * 256, v[j]);
+#pragma unroll
+    for (int j = 0; j < U; ++j) v[j] = w[j];
+  }
+  for (size_t i = ntiles * kTile + (size_t)blockIdx.x * 256 + threadIdx.x;
+       i < n4; i += (size_t)gridDim.x * 256)
+    dst[i] = src[i];
+}
+
+template <int U, int LP>
+__global__ void __launch_bounds__(256)
+    stream_read_tiled_kernel(const f32x4* __restrict__ src, size_t n4,
+                             float* __restrict__ sink) {
+  constexpr size_t kTile = 256 * U;
+  const size_t ntiles = n4 / kTile;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (size_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const size_t base = t * kTile + threadIdx.x;
+    f32x4 v[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) v[j] = ld<LP>(src + base + j * 256);
+#pragma unroll
+    for (int j = 0; j < U; ++j) acc += v[j];
+  }
+  for (size_t i = ntiles * kTile + (size_t)blockIdx.x * 256 + threadIdx.x;
+       i < n4; i += (size_t)gridDim.x * 256)
+    acc += src[i];
+  const float s = acc.x + acc.y + acc.z + acc.w;
   if (s != s || s == __builtin_huge_valf()) sink[blockIdx.x] = s;
 }
 

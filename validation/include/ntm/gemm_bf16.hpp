@@ -64,6 +64,9 @@ struct GemmArgs {
   __bf16* C;
   int M, N, K;
   int lda, ldb, ldc;
+  // optional ABFT checksum: rowsum[m] += sum_n of the fp32 accumulators of
+  // row m (caller zeroes it). nullptr selects the plain kernel.
+  float* rowsum = nullptr;
 };
 
 // Shapes the fast kernel accepts; the host launcher rejects anything else.
@@ -209,6 +212,7 @@ __device__ __forceinline__ void tile_coords(int M, int N, int& tm, int& tn) {
   tn = in_group / gsz;
 }
 
+template <bool kRowSum>
 __global__ void __launch_bounds__(kThreads, 2)
     gemm_bf16_256x256_kernel(GemmArgs p) {
   __shared__ __attribute__((aligned(16))) char smem[kLdsBytes];
@@ -303,6 +307,29 @@ __global__ void __launch_bounds__(kThreads, 2)
           o[3] = (__bf16)v[3];
           *(bf16x4*)(p.C + (size_t)row * p.ldc + col) = o;
         }
+
+  if constexpr (kRowSum) {
+    // Fused ABFT row checksum: the 4 lanes {l, l+16, l+32, l+48} share row
+    // (l & 15); reduce their 16 accumulators each with two xor-shuffles, one
+    // fp32 atomic per (row, wave). 4 column-waves x N/256 tiles add per row.
+#pragma unroll
+    for (int mh = 0; mh < 2; ++mh)
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        float s = 0.f;
+#pragma unroll
+        for (int nh = 0; nh < 2; ++nh)
+#pragma unroll
+          for (int nt = 0; nt < 2; ++nt) {
+            const f32x4 v = acc[mh][nh][mt][nt];
+            s += (v[0] + v[1]) + (v[2] + v[3]);
+          }
+        s += __shfl_xor(s, 16);
+        s += __shfl_xor(s, 32);
+        if (lane < 16)
+          unsafeAtomicAdd(p.rowsum + m0 + mh * 128 + c.wr * 64 + mt * 16 + lane, s);
+      }
+  }
 }
 
 // Host launcher. Returns hipErrorInvalidValue for shapes the kernel does not
@@ -312,8 +339,12 @@ inline hipError_t launch_gemm_bf16(const GemmArgs& a, hipStream_t stream) {
       (a.lda % 8) || (a.ldb % 8) || (a.ldc % 4))
     return hipErrorInvalidValue;
   const unsigned grid = (unsigned)((a.M / BM) * (a.N / BN));
-  hipLaunchKernelGGL(gemm_bf16_256x256_kernel, dim3(grid), dim3(kThreads), 0,
-                     stream, a);
+  if (a.rowsum)
+    hipLaunchKernelGGL(gemm_bf16_256x256_kernel<true>, dim3(grid),
+                       dim3(kThreads), 0, stream, a);
+  else
+    hipLaunchKernelGGL(gemm_bf16_256x256_kernel<false>, dim3(grid),
+                       dim3(kThreads), 0, stream, a);
   return hipGetLastError();
 }
 

@@ -69,6 +69,56 @@ NTM_API int ntm_gemm_bf16(const void* A, const void* B, void* C, int M, int N,
   return ntm_gemm_bf16_variant(0, A, B, C, M, N, K, lda, ldb, ldc, stream);
 }
 
+// K1 with the fused ABFT row checksum (8-wave kernel): rowsum[m] (fp32, M
+// entries) must be zeroed by the caller on `stream` before the call.
+NTM_API int ntm_gemm_bf16_rowsum(const void* A, const void* B, void* C,
+                                 float* rowsum, int M, int N, int K, int lda,
+                                 int ldb, int ldc, void* stream) {
+  if (!rowsum) return (int)hipErrorInvalidValue;
+  ntm::gemm::GemmArgs a;
+  a.A = (const __bf16*)A;
+  a.B = (const __bf16*)B;
+  a.C = (__bf16*)C;
+  a.M = M;
+  a.N = N;
+  a.K = K;
+  a.lda = lda;
+  a.ldb = ldb;
+  a.ldc = ldc;
+  a.rowsum = rowsum;
+  return (int)ntm::gemm::launch_gemm_bf16(a, S(stream));
+}
+
+// ABFT check of C = A B^T against the fused rowsum. scratch: K doubles;
+// result: ntm::aux::AbftResult (both zeroed here, stream-ordered).
+NTM_API int ntm_abft_check(const void* A, const void* B, const void* C,
+                           const float* rowsum, int M, int N, int K, int lda,
+                           int ldb, int ldc, double* scratch, void* result,
+                           void* stream) {
+  if (M <= 0 || N <= 0 || K <= 0 || !rowsum || !scratch || !result)
+    return (int)hipErrorInvalidValue;
+  hipError_t e = hipMemsetAsync(scratch, 0, sizeof(double) * (size_t)K, S(stream));
+  if (e != hipSuccess) return (int)e;
+  e = hipMemsetAsync(result, 0, sizeof(ntm::aux::AbftResult), S(stream));
+  if (e != hipSuccess) return (int)e;
+  // ~2048 column blocks x row chunks: enough parallelism for 256 CUs
+  const int kb = (K + 255) / 256;
+  int chunks = (2048 + kb - 1) / kb;
+  if (chunks > N) chunks = N;
+  const int rpc = (N + chunks - 1) / chunks;
+  chunks = (N + rpc - 1) / rpc;
+  hipLaunchKernelGGL(ntm::aux::abft_colsum_kernel, dim3(kb, chunks), dim3(256),
+                     0, S(stream), (const __bf16*)B, N, K, ldb, rpc, scratch);
+  hipLaunchKernelGGL(ntm::aux::abft_row_check_kernel, dim3(M), dim3(256), 0,
+                     S(stream), (const __bf16*)A, lda, (const __bf16*)C, ldc,
+                     rowsum, scratch, N, K, (ntm::aux::AbftResult*)result);
+  return (int)hipGetLastError();
+}
+
+NTM_API int ntm_abft_result_bytes() {
+  return (int)sizeof(ntm::aux::AbftResult);
+}
+
 NTM_API int ntm_fill_uniform_bf16(void* out, size_t n, unsigned long long seed,
                                   float scale, void* stream) {
   if (n == 0) return 0;
@@ -105,20 +155,94 @@ NTM_API int ntm_verify_result_bytes() {
   return (int)sizeof(ntm::aux::VerifyResult);
 }
 
+// K2 entry points. unroll in {2,4,8,16} selects the block-tiled kernels
+// (policy bit0 = nontemporal loads, bit1 = nontemporal stores, bit2 (copy
+// only) = software-pipelined; grid 0 = one block per tile capped at 8192);
+// unroll 1 selects the first grid-stride kernel (2048 x 256, nt), kept as
+// the sweep baseline. Defaults measured by tools/hbm_sweep.py on MI355X.
+namespace {
+template <int U>
+int copy_u(const void* src, void* dst, size_t n4, int policy, unsigned grid,
+           hipStream_t s) {
+  using namespace ntm::aux;
+  const auto* a = (const ntm::f32x4*)src;
+  auto* b = (ntm::f32x4*)dst;
+  switch (policy) {
+    case 0: hipLaunchKernelGGL((stream_copy_tiled_kernel<U, 0, 0>), dim3(grid), dim3(256), 0, s, a, b, n4); break;
+    case 1: hipLaunchKernelGGL((stream_copy_tiled_kernel<U, 1, 0>), dim3(grid), dim3(256), 0, s, a, b, n4); break;
+    case 2: hipLaunchKernelGGL((stream_copy_tiled_kernel<U, 0, 1>), dim3(grid), dim3(256), 0, s, a, b, n4); break;
+    case 3: hipLaunchKernelGGL((stream_copy_tiled_kernel<U, 1, 1>), dim3(grid), dim3(256), 0, s, a, b, n4); break;
+    case 4: hipLaunchKernelGGL((stream_copy_pipe_kernel<U, 0, 0>), dim3(grid), dim3(256), 0, s, a, b, n4); break;
+    case 5: hipLaunchKernelGGL((stream_copy_pipe_kernel<U, 1, 0>), dim3(grid), dim3(256), 0, s, a, b, n4); break;
+    case 6: hipLaunchKernelGGL((stream_copy_pipe_kernel<U, 0, 1>), dim3(grid), dim3(256), 0, s, a, b, n4); break;
+    case 7: hipLaunchKernelGGL((stream_copy_pipe_kernel<U, 1, 1>), dim3(grid), dim3(256), 0, s, a, b, n4); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+  return (int)hipGetLastError();
+}
+template <int U>
+int read_u(const void* src, size_t n4, float* sink, int policy, unsigned grid,
+           hipStream_t s) {
+  using namespace ntm::aux;
+  const auto* a = (const ntm::f32x4*)src;
+  if (policy & 1)
+    hipLaunchKernelGGL((stream_read_tiled_kernel<U, 1>), dim3(grid), dim3(256), 0, s, a, n4, sink);
+  else
+    hipLaunchKernelGGL((stream_read_tiled_kernel<U, 0>), dim3(grid), dim3(256), 0, s, a, n4, sink);
+  return (int)hipGetLastError();
+}
+unsigned tiled_grid(size_t n4, int unroll, int grid) {
+  if (grid > 0) return (unsigned)grid;
+  const size_t tiles = n4 / (256 * (size_t)unroll);
+  return (unsigned)(tiles < 1 ? 1 : (tiles > 8192 ? 8192 : tiles));
+}
+}  // namespace
+
+NTM_API int ntm_stream_copy_ex(const void* src, void* dst, size_t bytes,
+                               int unroll, int policy, int grid, void* stream) {
+  if (bytes % 16 || grid < 0) return (int)hipErrorInvalidValue;
+  const size_t n4 = bytes / 16;
+  if (unroll == 1) {
+    hipLaunchKernelGGL(ntm::aux::stream_copy_kernel, dim3(2048), dim3(256), 0,
+                       S(stream), (const ntm::f32x4*)src, (ntm::f32x4*)dst, n4);
+    return (int)hipGetLastError();
+  }
+  const unsigned g = tiled_grid(n4, unroll, grid);
+  switch (unroll) {
+    case 2: return copy_u<2>(src, dst, n4, policy, g, S(stream));
+    case 4: return copy_u<4>(src, dst, n4, policy, g, S(stream));
+    case 8: return copy_u<8>(src, dst, n4, policy, g, S(stream));
+    case 16: return copy_u<16>(src, dst, n4, policy, g, S(stream));
+    default: return (int)hipErrorInvalidValue;
+  }
+}
+
+NTM_API int ntm_stream_read_ex(const void* src, size_t bytes, float* sink,
+                               int unroll, int policy, int grid, void* stream) {
+  if (bytes % 16 || grid < 0) return (int)hipErrorInvalidValue;
+  const size_t n4 = bytes / 16;
+  if (unroll == 1) {
+    hipLaunchKernelGGL(ntm::aux::stream_read_kernel, dim3(2048), dim3(256), 0,
+                       S(stream), (const ntm::f32x4*)src, n4, sink);
+    return (int)hipGetLastError();
+  }
+  const unsigned g = tiled_grid(n4, unroll, grid);
+  switch (unroll) {
+    case 2: return read_u<2>(src, n4, sink, policy, g, S(stream));
+    case 4: return read_u<4>(src, n4, sink, policy, g, S(stream));
+    case 8: return read_u<8>(src, n4, sink, policy, g, S(stream));
+    case 16: return read_u<16>(src, n4, sink, policy, g, S(stream));
+    default: return (int)hipErrorInvalidValue;
+  }
+}
+
+// Tuned defaults (5.75 TB/s copy, 7.13 TB/s read at 4 GiB on MI355X).
 NTM_API int ntm_stream_copy(const void* src, void* dst, size_t bytes,
                             void* stream) {
-  if (bytes % 16) return (int)hipErrorInvalidValue;
-  const size_t n4 = bytes / 16;
-  hipLaunchKernelGGL(ntm::aux::stream_copy_kernel, dim3(2048), dim3(256), 0,
-                     S(stream), (const ntm::f32x4*)src, (ntm::f32x4*)dst, n4);
-  return (int)hipGetLastError();
+  return ntm_stream_copy_ex(src, dst, bytes, 4, 7, 256, stream);
 }
 
 NTM_API int ntm_stream_read(const void* src, size_t bytes, float* sink,
                             void* stream) {
-  if (bytes % 16) return (int)hipErrorInvalidValue;
-  const size_t n4 = bytes / 16;
-  hipLaunchKernelGGL(ntm::aux::stream_read_kernel, dim3(2048), dim3(256), 0,
-                     S(stream), (const ntm::f32x4*)src, n4, sink);
-  return (int)hipGetLastError();
+  return ntm_stream_read_ex(src, bytes, sink, 8, 1, 1024, stream);
 }
