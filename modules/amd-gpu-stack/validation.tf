@@ -17,6 +17,8 @@ locals {
     "--min-hbm-gb", tostring(var.validation_min_hbm_gb),
     "--allreduce-max-mib", tostring(var.validation_allreduce_max_mib),
     "--json",
+    # one-line verdict surfaced as the pod's termination message
+    "--termination-log", "/dev/termination-log",
   ]
   validation_env = merge({
     # RCCL over the xGMI mesh inside one node; no host network transport needed
@@ -66,6 +68,17 @@ resource "kubernetes_job_v1" "gpu_validation" {
           image   = var.validation_image
           command = ["/opt/ntm/bin/amdgpu-validate"]
           args    = local.validation_args
+
+          termination_message_path   = "/dev/termination-log"
+          termination_message_policy = "FallbackToLogsOnError"
+
+          security_context {
+            allow_privilege_escalation = false
+            read_only_root_filesystem  = true
+            capabilities {
+              drop = ["ALL"]
+            }
+          }
 
           dynamic "env" {
             for_each = local.validation_env

@@ -1,0 +1,133 @@
+"""The standalone ``amdgpu-validate`` Job binary (validation/src/validate_main.cpp).
+
+CPU tests cover argument handling and the no-GPU environment error (exit 2);
+GPU tests run the real checks on one MI355X, including native fault injection
+(the binary must exit 1 and name the failed check) and the Kubernetes
+termination-message / Prometheus textfile outputs.
+"""
+import json
+import os
+import subprocess
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+BIN = ROOT / "validation" / "build" / "amdgpu-validate"
+
+
+def _have_bin():
+    if not BIN.exists():
+        pytest.skip("amdgpu-validate not built (python -m nvidia_terraform_modules_amd.ops.build)")
+
+
+def _run(*args, env=None, timeout=300):
+    e = dict(os.environ)
+    e.pop("NTM_FAULT_INJECT", None)
+    e.update(env or {})
+    p = subprocess.run([str(BIN), *args], capture_output=True, text=True, timeout=timeout, env=e)
+    return p.returncode, p.stdout, p.stderr
+
+
+def test_rejects_unknown_argument():
+    _have_bin()
+    rc, _, err = _run("--definitely-not-an-option", timeout=60)
+    assert rc == 2 and "usage" in err
+
+
+def test_no_gpu_is_environment_error():
+    _have_bin()
+    try:
+        import torch
+        if torch.cuda.device_count() > 0:
+            pytest.skip("a GPU is visible")
+    except ImportError:
+        pass
+    rc, out, _ = _run("--size", "256", timeout=60)
+    assert rc == 2
+    assert json.loads(out.strip().splitlines()[-1])["passed"] is False
+
+
+def _last_json(out):
+    return json.loads(out.strip().splitlines()[-1])
+
+
+@pytest.mark.gpu
+def test_binary_passes_and_writes_sidecar_outputs(tmp_path):
+    _have_bin()
+    term, prom, full = tmp_path / "term", tmp_path / "m.prom", tmp_path / "full.json"
+    rc, out, err = _run("--gpus", "1", "--size", "2048", "--iters", "10", "--min-hbm-gb", "250",
+                        "--termination-log", str(term), "--prom-out", str(prom),
+                        "--out", str(full))
+    assert rc == 0, out + err
+    rep = _last_json(out)
+    assert rep["passed"] and rep["gpus"][0]["gemm_wrong"] == 0
+    assert rep["gpus"][0]["abft_bad_rows"] == 0
+    assert rep["gpus"][0]["hbm_read_GBps"] > 1000
+    assert rep["start_epoch_s"] > 1.6e9 and rep["end_epoch_s"] >= rep["start_epoch_s"]
+    t = json.loads(term.read_text())
+    assert t["passed"] is True and len(term.read_bytes()) < 4096
+    metrics = prom.read_text()
+    assert "amdgpu_validate_passed 1" in metrics
+    assert 'amdgpu_validate_gemm_tflops{gpu="0"}' in metrics
+    assert json.loads(full.read_text()) == rep
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,needle", [("corrupt_gemm", "GEMM verification failed"),
+                                         ("corrupt_abft", "ABFT")])
+def test_binary_fault_injection_fails_loudly(tmp_path, kind, needle):
+    _have_bin()
+    term = tmp_path / "term"
+    rc, out, _ = _run("--size", "1024", "--iters", "5", "--termination-log", str(term),
+                      env={"NTM_FAULT_INJECT": kind})
+    assert rc == 1
+    rep = _last_json(out)
+    assert not rep["passed"] and any(needle in f for f in rep["failures"])
+    assert json.loads(term.read_text())["passed"] is False
+
+
+# ------------------------------------------------ validation image runtime
+COLLECT = ROOT / "validation" / "image" / "collect-runtime.sh"
+
+
+@pytest.fixture(scope="module")
+def closure(tmp_path_factory):
+    _have_bin()
+    dest = tmp_path_factory.mktemp("rt")
+    subprocess.run(["bash", str(COLLECT), str(BIN), str(dest)], check=True, timeout=600,
+                   capture_output=True)
+    return dest
+
+
+def _loaded_from(out_err: str) -> set:
+    return {ln.split()[-1] for ln in out_err.splitlines() if "calling init:" in ln}
+
+
+def _run_closure(closure, *args, timeout=300):
+    env = dict(os.environ, LD_LIBRARY_PATH=str(closure / "lib"), LD_DEBUG="libs")
+    env.pop("NTM_FAULT_INJECT", None)
+    p = subprocess.run([str(closure / "bin" / "amdgpu-validate"), *args], capture_output=True,
+                       text=True, timeout=timeout, env=env)
+    return p.returncode, p.stdout, p.stderr
+
+
+def test_runtime_closure_is_self_contained(closure):
+    """What the runtime image ships is enough: no library of the ROCm SDK
+    install is loaded when only the closure is on the search path."""
+    names = {p.name for p in (closure / "lib").iterdir()}
+    assert {"libamdhip64.so.7", "librccl.so.1", "libhsa-runtime64.so.1"} <= names
+    assert not any(n.startswith(("libhipblaslt", "librocblas", "libMIOpen")) for n in names)
+    rc, out, err = _run_closure(closure, "--size", "256", "--iters", "1", timeout=120)
+    loaded = _loaded_from(err)
+    assert loaded, err[-2000:]
+    assert not [p for p in loaded if p.startswith("/opt/rocm")], loaded
+    assert rc in (0, 2)   # 2 = no GPU in this container
+
+
+@pytest.mark.gpu
+def test_runtime_closure_runs_validation_on_gpu(closure):
+    rc, out, err = _run_closure(closure, "--size", "1024", "--iters", "5")
+    assert rc == 0, out + err[-3000:]
+    assert _last_json(out)["passed"]
+    assert not [p for p in _loaded_from(err) if p.startswith("/opt/rocm")]

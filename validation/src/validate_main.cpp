@@ -51,6 +51,12 @@ int ntm_ref_gemm_f32(const void*, const void*, float*, int, int, int, int, int, 
 int ntm_verify_bf16(const void*, const float*, size_t, float, float, void*, void*);
 int ntm_verify_result_bytes();
 int ntm_stream_copy(const void*, void*, size_t, void*);
+int ntm_stream_read(const void*, size_t, float*, void*);
+int ntm_gemm_bf16_rowsum(const void*, const void*, void*, float*, int, int, int, int, int, int,
+                         void*);
+int ntm_abft_check(const void*, const void*, const void*, const float*, int, int, int, int, int,
+                   int, double*, void*, void*);
+int ntm_abft_result_bytes();
 int ntm_xgmi_allreduce_bf16(const void* const*, void* const*, unsigned* const*, int, int,
                             int, int, size_t, unsigned, unsigned*, int, void*);
 size_t ntm_xgmi_signal_bytes(int);
@@ -92,13 +98,19 @@ struct Opts {
   bool xgmi = true;
   bool json = true;
   std::string out;
+  std::string termination_log;  // k8s terminationMessagePath (<= 4 KiB summary)
+  std::string prom_out;         // Prometheus textfile-collector metrics
+  std::string fault;            // fault injection: corrupt_gemm | corrupt_abft | corrupt_allreduce
 };
 
 void usage() {
   std::fprintf(stderr,
                "usage: amdgpu-validate [--gpus N] [--size 8192] [--iters 50]\n"
                "       [--tflops-floor TF] [--min-hbm-gb GB] [--hbm-floor-gbps GBps]\n"
-               "       [--allreduce-max-mib MiB] [--no-xgmi] [--json] [--out FILE]\n");
+               "       [--allreduce-max-mib MiB] [--no-xgmi] [--json] [--out FILE]\n"
+               "       [--termination-log FILE] [--prom-out FILE] [--fault-inject KIND]\n"
+               "fault-inject (also env NTM_FAULT_INJECT): corrupt_gemm | corrupt_abft |\n"
+               "       corrupt_allreduce - corrupts the LAST GPU's data to prove detection\n");
 }
 
 bool parse(int argc, char** argv, Opts& o) {
@@ -122,6 +134,9 @@ bool parse(int argc, char** argv, Opts& o) {
     else if (a == "--no-xgmi") o.xgmi = false;
     else if (a == "--json") o.json = true;
     else if (a == "--out") { if (!(v = next("--out"))) return false; o.out = v; }
+    else if (a == "--termination-log") { if (!(v = next(a.c_str()))) return false; o.termination_log = v; }
+    else if (a == "--prom-out") { if (!(v = next(a.c_str()))) return false; o.prom_out = v; }
+    else if (a == "--fault-inject") { if (!(v = next(a.c_str()))) return false; o.fault = v; }
     else if (a == "-h" || a == "--help") { usage(); std::exit(0); }
     else { std::fprintf(stderr, "unknown argument %s\n", a.c_str()); return false; }
   }
@@ -132,7 +147,7 @@ bool parse(int argc, char** argv, Opts& o) {
 std::string jnum(double v) {
   if (!std::isfinite(v)) return "null";
   char b[64];
-  std::snprintf(b, sizeof b, "%.6g", v);
+  std::snprintf(b, sizeof b, "%.15g", v);
   return b;
 }
 std::string jstr(const std::string& s) {
@@ -188,12 +203,15 @@ struct GpuResult {
   double gemm_ms = 0, gemm_tflops = 0;
   unsigned long long gemm_bad = ~0ull;
   float gemm_max_err = NAN;
-  double hbm_copy_gbps = 0;
+  unsigned long long abft_bad_acc = ~0ull, abft_bad_store = ~0ull;
+  float abft_max_rel_acc = NAN;
+  double abft_tflops = 0;
+  double hbm_copy_gbps = 0, hbm_read_gbps = 0;
   bool hbm_copy_ok = false;
   double t_init = 0, t_gemm = 0, t_hbm = 0;
 };
 
-bool run_gpu(int dev, const Opts& o, GpuResult& r) {
+bool run_gpu(int dev, bool last, const Opts& o, GpuResult& r) {
   r.device = dev;
   CK(hipSetDevice(dev));
   hipDeviceProp_t prop;
@@ -229,6 +247,13 @@ bool run_gpu(int dev, const Opts& o, GpuResult& r) {
   CK(ntm_fill_uniform_bf16(A, e, 1000 + 2 * dev, 1.0f, s));
   CK(ntm_fill_uniform_bf16(B, e, 1001 + 2 * dev, 1.0f, s));
   CK(ntm_gemm_bf16(A, B, C, n, n, n, n, n, n, s));  // warm-up + verified result
+  if (last && o.fault == "corrupt_gemm") {  // flip one output element's exponent
+    uint16_t h;
+    CK(hipMemcpyAsync(&h, (uint16_t*)C + 4321, 2, hipMemcpyDeviceToHost, s));
+    CK(hipStreamSynchronize(s));
+    h ^= 0x0100;
+    CK(hipMemcpyAsync((uint16_t*)C + 4321, &h, 2, hipMemcpyHostToDevice, s));
+  }
   CK(ntm_ref_gemm_f32(A, B, R, n, n, n, n, n, n, s));
   CK(hipMemsetAsync(V, 0, 64, s));
   const float atol = 1e-3f + 4.0f * std::sqrt((float)n) * std::ldexp(1.0f, -20);
@@ -251,6 +276,47 @@ bool run_gpu(int dev, const Opts& o, GpuResult& r) {
   CK(hipEventElapsedTime(&ms, e0, e1));
   r.gemm_ms = ms / o.iters;
   r.gemm_tflops = 2.0 * n * (double)n * n / (r.gemm_ms * 1e-3) / 1e12;
+
+  // ---- K1 + fused ABFT row checksum, checked in O(n^2) (every launch of a
+  // long-running health check can afford this; the fp32 reference cannot)
+  {
+    float* rowsum;
+    double* scratch;
+    void* ab;
+    CK(hipMalloc(&rowsum, sizeof(float) * n));
+    CK(hipMalloc(&scratch, sizeof(double) * n));
+    CK(hipMalloc(&ab, 64));
+    const int it = std::max(1, o.iters / 5);
+    CK(hipEventRecord(e0, s));
+    for (int i = 0; i < it; ++i) {
+      CK(hipMemsetAsync(rowsum, 0, sizeof(float) * n, s));
+      CK(ntm_gemm_bf16_rowsum(A, B, C, rowsum, n, n, n, n, n, n, s));
+    }
+    CK(hipEventRecord(e1, s));
+    CK(hipEventSynchronize(e1));
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    r.abft_tflops = 2.0 * n * (double)n * n / (ms / it * 1e-3) / 1e12;
+    if (last && o.fault == "corrupt_abft") {
+      const float bump = 64.0f;
+      float v;
+      CK(hipMemcpyAsync(&v, rowsum + 7, 4, hipMemcpyDeviceToHost, s));
+      CK(hipStreamSynchronize(s));
+      v += bump;
+      CK(hipMemcpyAsync(rowsum + 7, &v, 4, hipMemcpyHostToDevice, s));
+    }
+    CK(ntm_abft_check(A, B, C, rowsum, n, n, n, n, n, n, scratch, ab, s));
+    unsigned char abr[64];
+    CK(hipMemcpyAsync(abr, ab, ntm_abft_result_bytes(), hipMemcpyDeviceToHost, s));
+    CK(hipStreamSynchronize(s));
+    std::memcpy(&r.abft_bad_acc, abr, 8);
+    std::memcpy(&r.abft_bad_store, abr + 8, 8);
+    unsigned bits;
+    std::memcpy(&bits, abr + 16, 4);
+    std::memcpy(&r.abft_max_rel_acc, &bits, 4);
+    CK(hipFree(rowsum));
+    CK(hipFree(scratch));
+    CK(hipFree(ab));
+  }
   CK(hipFree(A));
   CK(hipFree(B));
   CK(hipFree(C));
@@ -270,6 +336,18 @@ bool run_gpu(int dev, const Opts& o, GpuResult& r) {
   CK(hipEventSynchronize(e1));
   CK(hipEventElapsedTime(&ms, e0, e1));
   r.hbm_copy_gbps = 2.0 * hb * 10 / (ms * 1e-3) / 1e9;
+  {
+    float* sink;
+    CK(hipMalloc(&sink, sizeof(float) * 8192));
+    CK(ntm_stream_read(src, hb, sink, s));
+    CK(hipEventRecord(e0, s));
+    for (int i = 0; i < 10; ++i) CK(ntm_stream_read(src, hb, sink, s));
+    CK(hipEventRecord(e1, s));
+    CK(hipEventSynchronize(e1));
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    r.hbm_read_gbps = (double)hb * 10 / (ms * 1e-3) / 1e9;
+    CK(hipFree(sink));
+  }
   {  // byte-exact copy check on a sample window (first + last 16 MiB)
     const size_t w = std::min<size_t>(hb, 16u << 20);
     std::vector<unsigned char> h0(w), h1(w);
@@ -329,7 +407,9 @@ bool run_rccl(const std::vector<int>& devs, const Opts& o, std::vector<CollRow>&
     };
     for (int i = 0; i < n; ++i) {
       CK(hipSetDevice(devs[i]));
-      hipLaunchKernelGGL(fill_pattern, dim3(1024), dim3(256), 0, st[i], (uint16_t*)buf[i], cnt, i);
+      // fault injection: the last rank contributes the wrong pattern
+      const int contrib = (o.fault == "corrupt_allreduce" && i == n - 1) ? i + 1 : i;
+      hipLaunchKernelGGL(fill_pattern, dim3(1024), dim3(256), 0, st[i], (uint16_t*)buf[i], cnt, contrib);
       CK(hipMemsetAsync(bad[i], 0, 8, st[i]));
     }
     if (!run_once()) { fail("ncclAllReduce failed"); return false; }
@@ -475,6 +555,8 @@ int main(int argc, char** argv) {
     usage();
     return 2;
   }
+  if (o.fault.empty())
+    if (const char* f = std::getenv("NTM_FAULT_INJECT")) o.fault = f;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
     std::printf("{\"passed\":false,\"failures\":[\"no AMD GPU visible\"]}\n");
@@ -488,13 +570,17 @@ int main(int argc, char** argv) {
 
   std::vector<GpuResult> res(n);
   std::vector<std::thread> th;
-  for (int i = 0; i < n; ++i) th.emplace_back([&, i] { run_gpu(devs[i], o, res[i]); });
+  for (int i = 0; i < n; ++i)
+    th.emplace_back([&, i] { run_gpu(devs[i], i == n - 1, o, res[i]); });
   for (auto& t : th) t.join();
   const double t_local = wall_now();
 
   for (auto& r : res) {
     const std::string d = "gpu" + std::to_string(r.device) + ": ";
     if (r.gemm_bad != 0) fail(d + "GEMM verification failed (" + std::to_string(r.gemm_bad) + " elements)");
+    if (r.abft_bad_acc != 0 || r.abft_bad_store != 0)
+      fail(d + "GEMM ABFT checksum failed (" + std::to_string(r.abft_bad_acc) + " accumulator / " +
+           std::to_string(r.abft_bad_store) + " stored rows)");
     if (o.tflops_floor > 0 && r.gemm_tflops < o.tflops_floor)
       fail(d + "GEMM " + jnum(r.gemm_tflops) + " TFLOP/s below floor " + jnum(o.tflops_floor));
     if (o.min_hbm_gb > 0 && r.total_gb < o.min_hbm_gb)
@@ -525,7 +611,12 @@ int main(int argc, char** argv) {
           ",\"gemm_tflops\":" + jnum(r.gemm_tflops) +
           ",\"gemm_wrong\":" + (r.gemm_bad == ~0ull ? std::string("null") : std::to_string(r.gemm_bad)) +
           ",\"gemm_max_abs_err\":" + jnum(r.gemm_max_err) +
-          ",\"hbm_copy_GBps\":" + jnum(r.hbm_copy_gbps) + "}";
+          ",\"abft_tflops\":" + jnum(r.abft_tflops) +
+          ",\"abft_bad_rows\":" + (r.abft_bad_acc == ~0ull ? std::string("null")
+                                     : std::to_string(r.abft_bad_acc + r.abft_bad_store)) +
+          ",\"abft_max_rel_err\":" + jnum(r.abft_max_rel_acc) +
+          ",\"hbm_copy_GBps\":" + jnum(r.hbm_copy_gbps) +
+          ",\"hbm_read_GBps\":" + jnum(r.hbm_read_gbps) + "}";
   }
   js += "],\"rccl_allreduce_bf16\":" + coll_json(rccl_rows);
   js += ",\"xgmi_allreduce_bf16\":" + coll_json(xgmi_rows);
@@ -544,5 +635,47 @@ int main(int argc, char** argv) {
     std::ofstream f(o.out);
     f << js << "\n";
   }
-  return g_failures.empty() ? 0 : 1;
+  const bool passed = g_failures.empty();
+  double peak_rccl = 0, peak_xgmi = 0;
+  for (auto& c : rccl_rows) peak_rccl = std::max(peak_rccl, c.busbw);
+  for (auto& c : xgmi_rows) peak_xgmi = std::max(peak_xgmi, c.busbw);
+  if (!o.termination_log.empty()) {
+    // Kubernetes surfaces this file as the pod's termination message
+    // (truncated at 4 KiB): the one-line verdict an operator sees first.
+    std::string t = "{\"passed\":" + std::string(passed ? "true" : "false") +
+                    ",\"n_gpus\":" + std::to_string(n) + ",\"gemm_tflops_aggregate\":" + jnum(agg) +
+                    ",\"rccl_peak_busbw_GBps\":" + jnum(peak_rccl) +
+                    ",\"seconds\":" + jnum(t_end - t_start) + ",\"failures\":[";
+    for (size_t i = 0; i < g_failures.size() && t.size() < 3500; ++i)
+      t += (i ? "," : "") + jstr(g_failures[i].substr(0, 200));
+    t += "]}";
+    std::ofstream f(o.termination_log);
+    f << t << "\n";
+  }
+  if (!o.prom_out.empty()) {
+    // node-exporter textfile-collector format (metrics exporter sidecar /
+    // Pushgateway body); labels carry the device index.
+    std::ostringstream p;
+    p << "# HELP amdgpu_validate_passed 1 if every validation check passed.\n"
+      << "# TYPE amdgpu_validate_passed gauge\n"
+      << "amdgpu_validate_passed " << (passed ? 1 : 0) << "\n"
+      << "# TYPE amdgpu_validate_seconds gauge\n"
+      << "amdgpu_validate_seconds " << jnum(t_end - t_start) << "\n"
+      << "# TYPE amdgpu_validate_gemm_tflops gauge\n";
+    for (auto& r : res)
+      p << "amdgpu_validate_gemm_tflops{gpu=\"" << r.device << "\"} " << jnum(r.gemm_tflops) << "\n";
+    p << "# TYPE amdgpu_validate_hbm_copy_gbps gauge\n";
+    for (auto& r : res)
+      p << "amdgpu_validate_hbm_copy_gbps{gpu=\"" << r.device << "\"} " << jnum(r.hbm_copy_gbps) << "\n";
+    p << "# TYPE amdgpu_validate_hbm_total_gb gauge\n";
+    for (auto& r : res)
+      p << "amdgpu_validate_hbm_total_gb{gpu=\"" << r.device << "\"} " << jnum(r.total_gb) << "\n";
+    if (n > 1)
+      p << "# TYPE amdgpu_validate_allreduce_busbw_gbps gauge\n"
+        << "amdgpu_validate_allreduce_busbw_gbps{impl=\"rccl\"} " << jnum(peak_rccl) << "\n"
+        << "amdgpu_validate_allreduce_busbw_gbps{impl=\"xgmi\"} " << jnum(peak_xgmi) << "\n";
+    std::ofstream f(o.prom_out);
+    f << p.str();
+  }
+  return passed ? 0 : 1;
 }
