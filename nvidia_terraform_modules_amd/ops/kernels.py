@@ -30,7 +30,7 @@ def _require(t: torch.Tensor, name: str, dtype: torch.dtype) -> None:
         raise ValueError(f"{name} must be 2-D with unit inner stride")
 
 
-GEMM_VARIANTS = {"default": 0, "pingpong8": 1, "wave128": 2, "wave128d4": 3}
+GEMM_VARIANTS = {"default": 0, "pingpong8": 1, "wave128": 2, "wave128d4": 3, "pingpong8b": 4}
 
 
 def gemm_bf16(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
@@ -38,9 +38,10 @@ def gemm_bf16(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
     """K1: ``out = a @ b.T`` in bf16 with fp32 accumulation on MFMA.
 
     a: [M, K] bf16, b: [N, K] bf16 (both K-contiguous), out: [M, N] bf16.
-    ``variant``: "default" = "pingpong8" (8 waves, two per SIMD, staggered;
-    fastest measured), or the experimental "wave128"/"wave128d4" (4 waves,
-    128x128 per wave, AGPR-pinned accumulators) - see validation/include.
+    ``variant``: "default" = "pingpong8b" (8 waves, two per SIMD, staggered,
+    balanced 8/4/8/4 LDS read schedule; fastest measured), "pingpong8" (the
+    first 12/4/8/0 schedule), or the experimental "wave128"/"wave128d4" (4
+    waves, 128x128 per wave, AGPR-pinned accumulators) - see validation/include.
     """
     _require(a, "a", torch.bfloat16)
     _require(b, "b", torch.bfloat16)
@@ -66,7 +67,7 @@ def gemm_bf16_rowsum(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None 
                      rowsum: torch.Tensor | None = None) -> tuple[torch.Tensor, torch.Tensor]:
     """K1 with the fused ABFT epilogue: returns ``(out, rowsum)`` where
     ``rowsum[m]`` is the fp32 sum over n of the accumulators of row m (the
-    8-wave kernel; ``rowsum`` is zeroed here, stream-ordered)."""
+    default kernel; ``rowsum`` is zeroed here, stream-ordered)."""
     _require(a, "a", torch.bfloat16)
     _require(b, "b", torch.bfloat16)
     m, k = a.shape

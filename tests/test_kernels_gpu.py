@@ -159,7 +159,7 @@ def test_abft_rowsum_matches_fp64(ops, m, n, k):
     if exact is not None:
         norm = (a.float() @ b.float().T).double().norm(dim=1)
         assert torch.all((rs.double() - exact).abs() <= 1e-3 + 2**-14 * norm)
-    c_plain = ops.gemm_bf16(a, b)
+    c_plain = ops.gemm_bf16(a, b)   # default variant = the one the rowsum path runs
     assert torch.equal(c, c_plain)  # the checksum epilogue does not change C
     rep = ops.abft_check(a, b, c, rs)
     assert rep.ok, rep.as_dict()
@@ -182,3 +182,19 @@ def test_abft_detects_corruption(ops):
     c3 = c.clone()
     c3[5, 5] = float("nan")
     assert not ops.abft_check(a, b, c3, rs).ok
+
+
+@pytest.mark.parametrize("variant", ["pingpong8", "pingpong8b"])
+@pytest.mark.parametrize("m,n,k", [(256, 256, 128), (512, 256, 192), (256, 512, 256),
+                                   (768, 1024, 320), (1024, 768, 2048), (2048, 2048, 4096)])
+def test_gemm_variants_vs_torch_fp32(ops, variant, m, n, k):
+    """Every 8-wave schedule, including K-tile counts T = 2, 3, 4, 5 that
+    exercise each prologue/tail path (T = K / 64)."""
+    a = _rand(ops, (m, k), 71 + k)
+    b = _rand(ops, (n, k), 73 + n)
+    c = ops.gemm_bf16(a, b, variant=variant)
+    ref = a.float() @ b.float().T
+    atol, rtol = ops.gemm_tolerance(k)
+    err = (c.float() - ref).abs()
+    assert torch.all(err <= atol + rtol * ref.abs()), float(err.max())
+    assert torch.equal(c, ops.gemm_bf16(a, b, variant="pingpong8"))  # same math, same order

@@ -1,0 +1,72 @@
+"""Race screen for the LDS-DMA GEMM templates (cdna_hip_programming.md: "a
+sync-structure edit makes a NEW template: screen it for races over many runs
+at several sizes").
+
+The K1 kernels are deterministic (fixed MFMA order, no atomics), so every
+repeat must be BITWISE identical to the first run, and the first run must
+pass the fp32 reference check. A concurrent HBM copy on a second stream
+perturbs DMA/L2 timing so that a read placed too early (RAW) or a restage
+placed too early (WAR) shows up as a changed tile.
+
+    python tools/race_screen.py [--variants pingpong8b] [--repeats 200]
+"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from nvidia_terraform_modules_amd import ops  # noqa: E402
+
+SHAPES = [(256, 256, 128), (256, 512, 192), (512, 768, 320), (2304, 1536, 640),
+          (4096, 4096, 4096), (8192, 8192, 8192)]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--variants", default="pingpong8,pingpong8b")
+    ap.add_argument("--repeats", type=int, default=200)
+    ap.add_argument("--noise-mib", type=int, default=512)
+    args = ap.parse_args()
+    dev = torch.device("cuda:0")
+    noise_s = torch.cuda.Stream()
+    nsrc = torch.empty(args.noise_mib << 18, dtype=torch.float32, device=dev)
+    ndst = torch.empty_like(nsrc)
+    report = {"repeats": args.repeats, "results": []}
+    failed = False
+    for v in args.variants.split(","):
+        for (m, n, k) in SHAPES:
+            a = ops.fill_uniform_(torch.empty((m, k), dtype=torch.bfloat16, device=dev), 5 + m)
+            b = ops.fill_uniform_(torch.empty((n, k), dtype=torch.bfloat16, device=dev), 6 + n)
+            first = ops.gemm_bf16(a, b, variant=v)
+            ref = ops.ref_gemm_f32(a, b)
+            atol, rtol = ops.gemm_tolerance(k)
+            ok_ref = ops.verify_bf16(first, ref, atol, rtol).ok
+            del ref
+            reps = max(20, min(args.repeats, int(args.repeats * 2**31 / (m * n * k))))
+            out = torch.empty_like(first)
+            mismatches = 0
+            for i in range(reps):
+                if i % 2 == 0:
+                    with torch.cuda.stream(noise_s):
+                        ops.stream_copy(nsrc, ndst)
+                out.fill_(float("nan"))
+                ops.gemm_bf16(a, b, out, variant=v)
+                if not torch.equal(out, first):
+                    mismatches += 1
+            torch.cuda.synchronize()
+            row = {"variant": v, "shape": [m, n, k], "repeats": reps, "ref_ok": ok_ref,
+                   "bitwise_mismatches": mismatches}
+            failed |= (not ok_ref) or mismatches > 0
+            report["results"].append(row)
+            print(json.dumps(row), flush=True)
+    report["passed"] = not failed
+    print(json.dumps({"passed": not failed}))
+    return 1 if failed else 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

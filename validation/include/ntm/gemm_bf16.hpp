@@ -77,12 +77,14 @@ __host__ __device__ inline bool shape_ok(int M, int N, int K) {
 
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
-  static_assert(N >= -1 && N <= 8, "vmcnt range");
+  static_assert(N >= -1 && N <= 12, "vmcnt range");
   if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
   if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
   if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
   if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  if constexpr (N == 10) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+  if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
 }
 
 // Raw workgroup barrier. NOT __syncthreads(): that one carries a fence that
@@ -122,13 +124,13 @@ __device__ __forceinline__ void issue_half(const Ctx& c, int kt, int buf) {
 }
 
 template <int H>
-__device__ __forceinline__ void read_a(const Ctx& c, Frags& f, int buf) {
+__device__ __forceinline__ void read_a(const Ctx& c, bf16x8 (&a)[4][2], int buf) {
   const char* base = c.lds + buf * kTileBytes + H * kHalfBytes + c.frag_off;
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
-      f.a[mt][ks] = *(const bf16x8*)(base + ((c.wr * 4 + mt) * 2 + ks) * 1024);
+      a[mt][ks] = *(const bf16x8*)(base + ((c.wr * 4 + mt) * 2 + ks) * 1024);
 }
 
 template <int H>
@@ -169,11 +171,11 @@ __device__ __forceinline__ void phase(const Ctx& c, Frags& f,
   // 1. fragment reads for this phase
   if constexpr (P == 0) {
     read_b<kBLo>(c, f.bl, cur);
-    read_a<kALo>(c, f, cur);
+    read_a<kALo>(c, f.a, cur);
   } else if constexpr (P == 1) {
     read_b<kBHi>(c, f.bh, cur);
   } else if constexpr (P == 2) {
-    read_a<kAHi>(c, f, cur);
+    read_a<kAHi>(c, f.a, cur);
   }
   // 2. LDS-DMA prefetch of one half-tile
   if constexpr (ISSUE) {
@@ -210,6 +212,57 @@ __device__ __forceinline__ void tile_coords(int M, int N, int& tm, int& tn) {
   const int in_group = wgid - gid * group;
   tm = first_m + in_group % gsz;
   tn = in_group / gsz;
+}
+
+// Epilogue shared by the K1 kernels: bf16 RNE stores (8 B per lane per
+// 16x16 tile) and, with kRowSum, the fused ABFT row checksum.
+template <bool kRowSum>
+__device__ __forceinline__ void store_tile(const GemmArgs& p, const Ctx& c,
+                                           const f32x4 (&acc)[2][2][4][2],
+                                           int m0, int n0, int lane) {
+  // Epilogue: lane holds C[row][col .. col+3] per 16x16 tile.
+#pragma unroll
+  for (int mh = 0; mh < 2; ++mh)
+#pragma unroll
+    for (int nh = 0; nh < 2; ++nh)
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) {
+          const int row = m0 + mh * 128 + c.wr * 64 + mt * 16 + (lane & 15);
+          const int col = n0 + nh * 128 + c.wc * 32 + nt * 16 + (lane >> 4) * 4;
+          const f32x4 v = acc[mh][nh][mt][nt];
+          typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+          bf16x4 o;
+          o[0] = (__bf16)v[0];
+          o[1] = (__bf16)v[1];
+          o[2] = (__bf16)v[2];
+          o[3] = (__bf16)v[3];
+          *(bf16x4*)(p.C + (size_t)row * p.ldc + col) = o;
+        }
+
+  if constexpr (kRowSum) {
+    // Fused ABFT row checksum: the 4 lanes {l, l+16, l+32, l+48} share row
+    // (l & 15); reduce their 16 accumulators each with two xor-shuffles, one
+    // fp32 atomic per (row, wave). 4 column-waves x N/256 tiles add per row.
+#pragma unroll
+    for (int mh = 0; mh < 2; ++mh)
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        float s = 0.f;
+#pragma unroll
+        for (int nh = 0; nh < 2; ++nh)
+#pragma unroll
+          for (int nt = 0; nt < 2; ++nt) {
+            const f32x4 v = acc[mh][nh][mt][nt];
+            s += (v[0] + v[1]) + (v[2] + v[3]);
+          }
+        s += __shfl_xor(s, 16);
+        s += __shfl_xor(s, 32);
+        if (lane < 16)
+          unsafeAtomicAdd(p.rowsum + m0 + mh * 128 + c.wr * 64 + mt * 16 + lane, s);
+      }
+  }
 }
 
 template <bool kRowSum>
@@ -287,49 +340,7 @@ __global__ void __launch_bounds__(kThreads, 2)
   // balance the stagger so both groups execute the same barrier count
   if (c.wr == 0) raw_barrier();
 
-  // Epilogue: lane holds C[row][col .. col+3] per 16x16 tile.
-#pragma unroll
-  for (int mh = 0; mh < 2; ++mh)
-#pragma unroll
-    for (int nh = 0; nh < 2; ++nh)
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-        for (int nt = 0; nt < 2; ++nt) {
-          const int row = m0 + mh * 128 + c.wr * 64 + mt * 16 + (lane & 15);
-          const int col = n0 + nh * 128 + c.wc * 32 + nt * 16 + (lane >> 4) * 4;
-          const f32x4 v = acc[mh][nh][mt][nt];
-          typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-          bf16x4 o;
-          o[0] = (__bf16)v[0];
-          o[1] = (__bf16)v[1];
-          o[2] = (__bf16)v[2];
-          o[3] = (__bf16)v[3];
-          *(bf16x4*)(p.C + (size_t)row * p.ldc + col) = o;
-        }
-
-  if constexpr (kRowSum) {
-    // Fused ABFT row checksum: the 4 lanes {l, l+16, l+32, l+48} share row
-    // (l & 15); reduce their 16 accumulators each with two xor-shuffles, one
-    // fp32 atomic per (row, wave). 4 column-waves x N/256 tiles add per row.
-#pragma unroll
-    for (int mh = 0; mh < 2; ++mh)
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt) {
-        float s = 0.f;
-#pragma unroll
-        for (int nh = 0; nh < 2; ++nh)
-#pragma unroll
-          for (int nt = 0; nt < 2; ++nt) {
-            const f32x4 v = acc[mh][nh][mt][nt];
-            s += (v[0] + v[1]) + (v[2] + v[3]);
-          }
-        s += __shfl_xor(s, 16);
-        s += __shfl_xor(s, 32);
-        if (lane < 16)
-          unsafeAtomicAdd(p.rowsum + m0 + mh * 128 + c.wr * 64 + mt * 16 + lane, s);
-      }
-  }
+  store_tile<kRowSum>(p, c, acc, m0, n0, lane);
 }
 
 // Host launcher. Returns hipErrorInvalidValue for shapes the kernel does not
