@@ -31,7 +31,27 @@ def main(argv=None) -> int:
     ap.add_argument("--warnings-as-errors", action="store_true")
     ap.add_argument("--contract", help="reference surface fixture (JSON) to diff against")
     ap.add_argument("--json", action="store_true")
+    ap.add_argument("--docs", action="store_true",
+                    help="regenerate the terraform-docs tables in every module README")
+    ap.add_argument("--docs-check", action="store_true",
+                    help="exit 1 if any module README's generated tables are stale")
     args = ap.parse_args(argv)
+
+    if args.docs or args.docs_check:
+        from .docs import update
+
+        stale = []
+        for d in args.dirs:
+            for mdir in find_modules(d):
+                if any(part in ("charts", "fixtures") for part in mdir.parts):
+                    continue
+                if not update(load_module(mdir), check=args.docs_check):
+                    stale.append(str(mdir))
+        verb = "stale" if args.docs_check else "updated"
+        for m in stale:
+            print(f"{verb}: {m}")
+        print(f"{len(stale)} README(s) {verb}")
+        return 1 if (stale and args.docs_check) else 0
 
     results = {}
     nerr = 0
