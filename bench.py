@@ -48,6 +48,9 @@ def parse(argv=None):
     ap.add_argument("--no-extras", action="store_true",
                     help="skip hipBLASLt comparison, HBM and all-reduce sweeps")
     ap.add_argument("--allreduce-max-mib", type=int, default=1024)
+    ap.add_argument("--xgmi", action="store_true",
+                    help="N > 1: also sweep the hand-written xGMI all-reduce (C2, HIP IPC); its "
+                         "time includes staging copies + a host barrier per call")
     ap.add_argument("--out", default="", help="also write the JSON line to this file")
     return ap.parse_args(argv)
 
@@ -161,6 +164,19 @@ def main(argv=None) -> int:
         extras["allreduce_peak_busbw_GBps"] = coll.peak_busbw(res)
         if any(r.errors for r in res):
             verified = False
+        if args.xgmi:
+            from nvidia_terraform_modules_amd.parallel.xgmi import XgmiAllReduce
+
+            xs = [b for b in sizes if b <= 256 << 20]
+            ar = XgmiAllReduce(env, max_bytes=max(xs), nblk=64)
+            xr = coll.all_reduce_sweep(env, xs, dtype="bf16", iters=10, warmup=2, impl=ar)
+            extras["xgmi_allreduce_bf16"] = [
+                {"bytes": r.bytes, "time_us": round(r.time_us, 1),
+                 "busbw_GBps": round(r.busbw_GBps, 1), "errors": r.errors} for r in xr]
+            extras["xgmi_timed_out"] = ar.timed_out()
+            ar.close()
+            if any(r.errors for r in xr) or extras["xgmi_timed_out"]:
+                verified = False
     _CLOCK.mark("collectives_checked")
     _CLOCK.mark("done")
 

@@ -77,8 +77,16 @@ def build_library(force: bool = False, verbose: bool = True) -> Path:
     return out
 
 
-def build_binary(force: bool = False, verbose: bool = True) -> Path:
-    out = BUILD / BIN_NAME
+# Host-only AddressSanitizer / UBSan variant of the Job binary: instruments the
+# host code (argument parsing, per-GPU threads, RCCL driver, JSON/report
+# writers) and leaves the gfx950 device code untouched - GPU ASan / xnack+ code
+# objects are not used. Each -fsanitize= sits directly after -Xarch_host.
+ASAN_FLAGS = ["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fsanitize=undefined",
+              "-Xarch_host", "-fno-omit-frame-pointer", "-g"]
+
+
+def build_binary(force: bool = False, verbose: bool = True, asan: bool = False) -> Path:
+    out = BUILD / (BIN_NAME + ("-asan" if asan else ""))
     main = SRC / "validate_main.cpp"
     if not main.exists():
         return out
@@ -87,7 +95,7 @@ def build_binary(force: bool = False, verbose: bool = True) -> Path:
         srcs = [SRC / "ntm_validation.hip", SRC / "xgmi_allreduce.hip"]
         srcs = [str(s) for s in srcs if s.exists()]
         cmd = [
-            hipcc(), *COMMON_FLAGS, "-x", "hip", str(main), *srcs,
+            hipcc(), *COMMON_FLAGS, *(ASAN_FLAGS if asan else []), "-x", "hip", str(main), *srcs,
             "-I/opt/rocm/include", "-L/opt/rocm/lib", "-lrccl", "-lpthread",
             "-Wl,-rpath,/opt/rocm/lib", "-o", str(out) + ".tmp",
         ]
@@ -96,18 +104,23 @@ def build_binary(force: bool = False, verbose: bool = True) -> Path:
     return out
 
 
-def build_all(force: bool = False, verbose: bool = True) -> dict[str, str]:
+def build_all(force: bool = False, verbose: bool = True, asan: bool = False) -> dict[str, str]:
     lib = build_library(force=force, verbose=verbose)
     binary = build_binary(force=force, verbose=verbose)
-    return {"library": str(lib), "binary": str(binary)}
+    res = {"library": str(lib), "binary": str(binary)}
+    if asan:
+        res["binary_asan"] = str(build_binary(force=force, verbose=verbose, asan=True))
+    return res
 
 
 def main(argv: list[str] | None = None) -> int:
     ap = argparse.ArgumentParser(description=__doc__)
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-q", "--quiet", action="store_true")
+    ap.add_argument("--asan", action="store_true",
+                    help="also build the host-ASan/UBSan amdgpu-validate-asan")
     args = ap.parse_args(argv)
-    res = build_all(force=args.force, verbose=not args.quiet)
+    res = build_all(force=args.force, verbose=not args.quiet, asan=args.asan)
     for k, v in res.items():
         print(f"{k}: {v}")
     return 0

@@ -131,3 +131,37 @@ def test_runtime_closure_runs_validation_on_gpu(closure):
     assert rc == 0, out + err[-3000:]
     assert _last_json(out)["passed"]
     assert not [p for p in _loaded_from(err) if p.startswith("/opt/rocm")]
+
+
+# ------------------------------------------- host AddressSanitizer / UBSan
+ASAN_BIN = ROOT / "validation" / "build" / "amdgpu-validate-asan"
+
+
+def _run_asan(*args, leaks=True, timeout=300):
+    if not ASAN_BIN.exists():
+        pytest.skip("asan binary not built (python -m nvidia_terraform_modules_amd.ops.build --asan)")
+    env = dict(os.environ, ASAN_OPTIONS=f"detect_leaks={1 if leaks else 0}:abort_on_error=0",
+               UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1")
+    env.pop("NTM_FAULT_INJECT", None)
+    p = subprocess.run([str(ASAN_BIN), *args], capture_output=True, text=True, timeout=timeout,
+                       env=env)
+    return p.returncode, p.stdout, p.stderr
+
+
+def test_asan_host_paths_clean_without_gpu():
+    rc, out, err = _run_asan("--size", "256", "--termination-log", "/dev/null")
+    assert "AddressSanitizer" not in err and "runtime error" not in err, err[-3000:]
+    assert rc in (0, 2)
+    rc, _, err = _run_asan("--gpus", "x", "--size")          # malformed arguments
+    assert rc == 2 and "AddressSanitizer" not in err
+
+
+@pytest.mark.gpu
+def test_asan_full_validation_on_gpu(tmp_path):
+    # the HIP runtime keeps allocations alive until exit: leak checking off
+    rc, out, err = _run_asan("--size", "1024", "--iters", "5",
+                             "--termination-log", str(tmp_path / "t"),
+                             "--prom-out", str(tmp_path / "m"), leaks=False)
+    assert "AddressSanitizer" not in err and "runtime error" not in err, err[-3000:]
+    assert rc == 0, out + err[-2000:]
+    assert _last_json(out)["passed"]

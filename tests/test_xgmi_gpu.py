@@ -43,3 +43,39 @@ def test_rejects_bad_counts():
     ins = [torch.zeros(100, dtype=torch.bfloat16, device="cuda") for _ in range(2)]
     with pytest.raises(ValueError):
         simulate_allreduce(ins)
+
+
+def test_ipc_allreduce_two_processes():
+    """XgmiAllReduce across two PROCESSES (IPC handles + cross-process flags),
+    both on the one GPU of the box; every element checked exactly."""
+    import json
+    import os
+    import socket
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    worker = Path(__file__).with_name("xgmi_ipc_worker.py")
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, str(worker)], env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    outs = []
+    try:
+        for p in procs:
+            o, e = p.communicate(timeout=240)
+            assert p.returncode == 0, e[-3000:]
+            outs.append(json.loads(o.strip().splitlines()[-1]))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    for rep in outs:
+        for r in rep["results"]:
+            assert not r["timeout"], rep
+            assert r["wrong"] == 0, rep

@@ -1,0 +1,37 @@
+"""Worker for tests/test_xgmi_gpu.py::test_ipc_allreduce_two_processes: one
+rank of XgmiAllReduce. Both ranks share cuda:0 (one-GPU box), so this runs
+the real multi-process path - HIP IPC handle exchange, peer-mapped buffers,
+cross-process release/acquire flags - minus only the xGMI link itself."""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+os.environ["LOCAL_RANK"] = "0"          # every rank on cuda:0
+
+import torch  # noqa: E402
+
+from nvidia_terraform_modules_amd.parallel.dist import init, shutdown  # noqa: E402
+from nvidia_terraform_modules_amd.parallel.xgmi import XgmiAllReduce  # noqa: E402
+
+
+def main():
+    env = init(backend="gloo", device_type="cuda")
+    ar = XgmiAllReduce(env, max_bytes=8 << 20, nblk=16)
+    n = env.world_size
+    results = []
+    for count in (8 * n * 64, 8 * n * 4096 + 8 * n * 5, (8 << 20) // 2):
+        i = torch.arange(count, device=env.device)
+        t = ((2.0 ** (i % 4)) * (env.rank + 1)).to(torch.bfloat16)
+        ar(t)
+        torch.cuda.synchronize()
+        exp = ((2.0 ** (i % 4)) * (n * (n + 1) / 2)).to(torch.bfloat16)
+        results.append({"count": count, "wrong": int((t != exp).sum()),
+                        "timeout": ar.timed_out()})
+    ar.close()
+    print(json.dumps({"rank": env.rank, "results": results}), flush=True)
+    shutdown(env)
+
+
+if __name__ == "__main__":
+    main()
