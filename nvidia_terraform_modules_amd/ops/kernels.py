@@ -30,7 +30,8 @@ def _require(t: torch.Tensor, name: str, dtype: torch.dtype) -> None:
         raise ValueError(f"{name} must be 2-D with unit inner stride")
 
 
-GEMM_VARIANTS = {"default": 0, "pingpong8": 1, "wave128": 2, "wave128d4": 3, "pingpong8b": 4}
+GEMM_VARIANTS = {"default": 0, "pingpong8": 1, "wave128": 2, "wave128d4": 3, "pingpong8b": 4,
+                 "pingpong8c": 5}
 
 
 def gemm_bf16(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
@@ -38,10 +39,12 @@ def gemm_bf16(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
     """K1: ``out = a @ b.T`` in bf16 with fp32 accumulation on MFMA.
 
     a: [M, K] bf16, b: [N, K] bf16 (both K-contiguous), out: [M, N] bf16.
-    ``variant``: "default" = "pingpong8b" (8 waves, two per SIMD, staggered,
-    balanced 8/4/8/4 LDS read schedule; fastest measured), "pingpong8" (the
-    first 12/4/8/0 schedule), or the experimental "wave128"/"wave128d4" (4
-    waves, 128x128 per wave, AGPR-pinned accumulators) - see validation/include.
+    ``variant``: "default" = "pingpong8c" when K % 128 == 0, else
+    "pingpong8b" (8 waves, two per SIMD, staggered, balanced 8/4/8/4 LDS read
+    schedule; 8c adds parity-alternating B buffers and a tail-free K loop -
+    fastest measured), "pingpong8" (the first 12/4/8/0 schedule), or the
+    experimental "wave128"/"wave128d4" (4 waves, 128x128 per wave,
+    AGPR-pinned accumulators) - see validation/include.
     """
     _require(a, "a", torch.bfloat16)
     _require(b, "b", torch.bfloat16)

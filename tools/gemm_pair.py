@@ -21,7 +21,7 @@ def main() -> int:
     ap.add_argument("--size", type=int, default=8192)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--which", default="both", choices=["both", "ours", "torch", "all"])
-    ap.add_argument("--variant", default="wave128")
+    ap.add_argument("--variant", default="default")
     args = ap.parse_args()
     s = args.size
     a = torch.empty((s, s), dtype=torch.bfloat16, device="cuda")

@@ -21,13 +21,13 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from nvidia_terraform_modules_amd import ops  # noqa: E402
 
-SHAPES = [(256, 256, 128), (256, 512, 192), (512, 768, 320), (2304, 1536, 640),
+SHAPES = [(256, 256, 128), (256, 512, 256), (512, 768, 384), (2304, 1536, 640),
           (4096, 4096, 4096), (8192, 8192, 8192)]
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--variants", default="pingpong8,pingpong8b")
+    ap.add_argument("--variants", default="pingpong8,pingpong8b,pingpong8c")
     ap.add_argument("--repeats", type=int, default=200)
     ap.add_argument("--noise-mib", type=int, default=512)
     args = ap.parse_args()

@@ -1,0 +1,168 @@
+// K1 v4 ("pingpong8c"): pingpong8b's balanced 8/4/8/4 read schedule with
+// (a) B fragment buffers that alternate by K-tile parity (no b1 -> b0 copy)
+// and (b) a UNIFORM K loop: every K-tile, including the last two, issues its
+// four LDS-DMA pieces. Pieces that would stage a tile >= T instead re-read an
+// L2-hot, in-bounds slice into a 16 KiB scratch region of LDS that nobody
+// reads, so the counted vmcnt(10) is right in every phase and there is no
+// tail code at all.
+//
+// Why: in pingpong8b the compiler sinks the b1 -> b0 copy into phase 0 of the
+// next tile and has to put s_waitcnt lgkmcnt(0) BEFORE phase 0's mid
+// barrier, exposing the LDS latency of 8 A reads on the critical path (see
+// gemm_bf16_pp2.hpp); letting the buffers alternate under the old
+// pair-loop + two-parity tail made the register allocator spill ~250 VGPRs.
+// One straight 2-tile loop body keeps the register roles fixed at the back
+// edge, so neither happens.
+//
+// Schedule and ordering proof: identical to gemm_bf16_pp2.hpp (reads at
+// 4t+0..3 = A-lo(t), B-hi(t), A-hi(t), B-lo(t+1); issues A-hi(t+1),
+// B-lo(t+2), A-lo(t+2), B-hi(t+2); RAW distance 6 with vmcnt(10); WAR
+// distance 2). Dummy pieces only write the scratch region (WAW among
+// themselves is harmless) and are drained by vmcnt(0) before the epilogue,
+// so no LDS-DMA is in flight when the workgroup exits.
+// Shape rule: T = K / 64 even (K % 128 == 0), T >= 2; M, N % 256.
+#pragma once
+
+#include "ntm/gemm_bf16.hpp"
+
+namespace ntm {
+namespace gemm3 {
+
+using namespace ::ntm::gemm;
+
+constexpr int kScratch = kLdsBytes;                 // 128 KiB: dummy DMA target
+constexpr int kLdsBytes3 = kLdsBytes + kHalfBytes;  // 144 KiB (1 WG / CU anyway)
+
+__host__ __device__ inline bool shape_ok3(int M, int N, int K) {
+  return shape_ok(M, N, K) && (K % (2 * BK)) == 0;
+}
+
+struct Frags3 {
+  bf16x8 a[4][2];
+  bf16x8 b0[2][2];
+  bf16x8 b1[2][2];
+};
+
+// Stage half H of K-tile kt into buffer buf, or a dummy piece if kt >= T.
+template <int H>
+__device__ __forceinline__ void issue_half3(const Ctx& c, int kt, int buf, int T) {
+  const bool real = kt < T;
+  const int k_eff = real ? kt : T - 1;
+  const __bf16* s = c.src[H] + (size_t)k_eff * BK;
+  const int off = real ? buf * kTileBytes + H * kHalfBytes : kScratch;
+  char* d = c.lds + off + (2 * c.w) * 1024;
+  glds16(s, d);
+  glds16(s + 32, d + 1024);
+}
+
+template <int P, bool ODD>
+__device__ __forceinline__ void phase3(const Ctx& c, Frags3& f,
+                                       f32x4 (&acc)[2][2][4][2], int t, int T) {
+  bf16x8(&bcur)[2][2] = ODD ? f.b1 : f.b0;
+  bf16x8(&both)[2][2] = ODD ? f.b0 : f.b1;
+  const int cur = t & 1;
+  if constexpr (P == 0) read_a<kALo>(c, f.a, cur);
+  if constexpr (P == 1) read_b<kBHi>(c, both, cur);
+  if constexpr (P == 2) read_a<kAHi>(c, f.a, cur);
+  if constexpr (P == 3) read_b<kBLo>(c, both, cur ^ 1);  // tile t+1 (junk at t = T-1)
+  if constexpr (P == 0) issue_half3<kAHi>(c, t + 1, cur ^ 1, T);
+  if constexpr (P == 1) issue_half3<kBLo>(c, t + 2, cur, T);
+  if constexpr (P == 2) issue_half3<kALo>(c, t + 2, cur, T);
+  if constexpr (P == 3) issue_half3<kBHi>(c, t + 2, cur, T);
+  wait_vmcnt<10>();
+  raw_barrier();
+  if constexpr (P == 0) mma_quadrant(acc[0][0], f.a, bcur);
+  if constexpr (P == 1) mma_quadrant(acc[0][1], f.a, both);
+  if constexpr (P == 2) mma_quadrant(acc[1][1], f.a, both);
+  if constexpr (P == 3) mma_quadrant(acc[1][0], f.a, bcur);
+  raw_barrier();
+}
+
+template <bool ODD>
+__device__ __forceinline__ void tile3(const Ctx& c, Frags3& f,
+                                      f32x4 (&acc)[2][2][4][2], int t, int T) {
+  phase3<0, ODD>(c, f, acc, t, T);
+  phase3<1, ODD>(c, f, acc, t, T);
+  phase3<2, ODD>(c, f, acc, t, T);
+  phase3<3, ODD>(c, f, acc, t, T);
+}
+
+template <bool kRowSum>
+__global__ void __launch_bounds__(kThreads, 2)
+    gemm_bf16_pp3_kernel(GemmArgs p) {
+  __shared__ __attribute__((aligned(16))) char smem[kLdsBytes3];
+
+  int tm, tn;
+  tile_coords(p.M, p.N, tm, tn);
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  Ctx c;
+  c.lds = smem;
+  const int lane = threadIdx.x & 63;
+  c.w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  c.wr = c.w >> 2;
+  c.wc = c.w & 3;
+  {
+    const int r = lane >> 2;
+    const int cl = (lane & 3) ^ (((r >> 3) & 1) << 1);
+    const __bf16* a0 = p.A + (size_t)(m0 + c.w * 16 + r) * p.lda + cl * 8;
+    const __bf16* b0 = p.B + (size_t)(n0 + c.w * 16 + r) * p.ldb + cl * 8;
+    c.src[kALo] = a0;
+    c.src[kAHi] = a0 + (size_t)128 * p.lda;
+    c.src[kBLo] = b0;
+    c.src[kBHi] = b0 + (size_t)128 * p.ldb;
+  }
+  c.frag_off = (lane & 15) * 64 + ((lane >> 4) ^ ((lane >> 2) & 2)) * 16;
+
+  f32x4 acc[2][2][4][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int n = 0; n < 2; ++n) acc[i][j][m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  Frags3 f;
+  const int T = p.K / BK;
+
+  // prologue: B-lo0 A-lo0 B-hi0 A-hi0 B-lo1 A-lo1 B-hi1 (virtual phases -7..-1)
+  issue_half<kBLo>(c, 0, 0);
+  issue_half<kALo>(c, 0, 0);
+  issue_half<kBHi>(c, 0, 0);
+  issue_half<kAHi>(c, 0, 0);
+  issue_half<kBLo>(c, 1, 1);
+  issue_half<kALo>(c, 1, 1);
+  issue_half<kBHi>(c, 1, 1);
+  wait_vmcnt<10>();
+  raw_barrier();
+  read_b<kBLo>(c, f.b0, 0);
+  if (c.wr == 1) raw_barrier();  // ping-pong stagger
+
+  for (int t = 0; t < T; t += 2) {
+    tile3<false>(c, f, acc, t, T);
+    tile3<true>(c, f, acc, t + 1, T);
+  }
+  if (c.wr == 0) raw_barrier();
+  wait_vmcnt<0>();  // dummy pieces: nothing may land after the WG exits
+
+  store_tile<kRowSum>(p, c, acc, m0, n0, lane);
+}
+
+inline hipError_t launch_gemm_bf16_pp3(const GemmArgs& a, hipStream_t stream) {
+  if (!shape_ok3(a.M, a.N, a.K) || a.lda < a.K || a.ldb < a.K || a.ldc < a.N ||
+      (a.lda % 8) || (a.ldb % 8) || (a.ldc % 4))
+    return hipErrorInvalidValue;
+  const unsigned grid = (unsigned)((a.M / BM) * (a.N / BN));
+  if (a.rowsum)
+    hipLaunchKernelGGL(gemm_bf16_pp3_kernel<true>, dim3(grid), dim3(kThreads),
+                       0, stream, a);
+  else
+    hipLaunchKernelGGL(gemm_bf16_pp3_kernel<false>, dim3(grid), dim3(kThreads),
+                       0, stream, a);
+  return hipGetLastError();
+}
+
+}  // namespace gemm3
+}  // namespace ntm

@@ -7,6 +7,7 @@
 #include "ntm/aux_kernels.hpp"
 #include "ntm/gemm_bf16.hpp"
 #include "ntm/gemm_bf16_pp2.hpp"
+#include "ntm/gemm_bf16_pp3.hpp"
 #include "ntm/gemm_bf16_w4.hpp"
 
 #define NTM_API extern "C" __attribute__((visibility("default")))
@@ -30,19 +31,24 @@ NTM_API int ntm_gemm_shape_ok(int M, int N, int K) {
 
 // K1 variants: 1 = 8-wave ping-pong (gemm_bf16.hpp); 2 / 3 = 4-wave, 128x128
 // per wave (gemm_bf16_w4.hpp) with prefetch distance 3 / 4 k-steps; 4 = the
-// 8-wave kernel with the balanced 8/4/8/4 read schedule (gemm_bf16_pp2.hpp).
+// 8-wave kernel with the balanced 8/4/8/4 read schedule (gemm_bf16_pp2.hpp);
+// 5 = the same schedule with parity-alternating B buffers and a uniform,
+// tail-free K loop (gemm_bf16_pp3.hpp; K % 128 == 0).
 // 0 = default: the fastest measured variant whose shape rules admit (M,N,K).
-// Measured on MI355X (tools/gemm_check.py, random bf16, median of 7 rounds):
-//   8192^3: 4 1499 TF, 1 1489, 2 ~1310-1380, 3 ~1110-1430; hipBLASLt 1652
-//   4096^3: 4 1416 TF, 1 1393;                             hipBLASLt 1556
-// Variant 4 passes tools/race_screen.py (bitwise-stable under HBM noise).
-constexpr int kDefaultVariant = 4;
+// Measured on MI355X (tools/gemm_check.py, random bf16, median of 7 rounds,
+// profiles/r1_pp3/):
+//   8192^3: 5 1567 TF, 4 1530, 1 1521, 2 ~1310-1380; hipBLASLt 1667
+//   4096^3: 5 1479 TF, 4 1435, 1 1424;               hipBLASLt 1562
+// Variants 4 and 5 pass tools/race_screen.py (bitwise-stable under HBM noise).
+// Default: 5 when K % 128 == 0, else 4 (both need K % 64 == 0, K >= 128).
+constexpr int kDefaultVariant = 5;
 
 NTM_API int ntm_gemm_bf16_variant(int variant, const void* A, const void* B,
                                   void* C, int M, int N, int K, int lda,
                                   int ldb, int ldc, void* stream) {
   if (variant == 0) {
     variant = kDefaultVariant;
+    if (variant == 5 && !ntm::gemm3::shape_ok3(M, N, K)) variant = 4;
     if (variant == 3 && !ntm::gemm4::shape_ok<4>(M, N, K)) variant = 1;
     if (variant == 2 && !ntm::gemm4::shape_ok<3>(M, N, K)) variant = 1;
   }
@@ -59,7 +65,7 @@ NTM_API int ntm_gemm_bf16_variant(int variant, const void* A, const void* B,
     a.ldc = ldc;
     return (int)ntm::gemm::launch_gemm_bf16(a, S(stream));
   }
-  if (variant == 4) {
+  if (variant == 4 || variant == 5) {
     ntm::gemm::GemmArgs a;
     a.A = (const __bf16*)A;
     a.B = (const __bf16*)B;
@@ -70,7 +76,8 @@ NTM_API int ntm_gemm_bf16_variant(int variant, const void* A, const void* B,
     a.lda = lda;
     a.ldb = ldb;
     a.ldc = ldc;
-    return (int)ntm::gemm2::launch_gemm_bf16_pp2(a, S(stream));
+    return variant == 5 ? (int)ntm::gemm3::launch_gemm_bf16_pp3(a, S(stream))
+                        : (int)ntm::gemm2::launch_gemm_bf16_pp2(a, S(stream));
   }
   if (variant == 2 || variant == 3) {
     ntm::gemm4::Args a{(const __bf16*)A, (const __bf16*)B, (__bf16*)C, M, N, K,
@@ -103,7 +110,8 @@ NTM_API int ntm_gemm_bf16_rowsum(const void* A, const void* B, void* C,
   a.ldb = ldb;
   a.ldc = ldc;
   a.rowsum = rowsum;
-  return (int)ntm::gemm2::launch_gemm_bf16_pp2(a, S(stream));
+  return ntm::gemm3::shape_ok3(M, N, K) ? (int)ntm::gemm3::launch_gemm_bf16_pp3(a, S(stream))
+                                        : (int)ntm::gemm2::launch_gemm_bf16_pp2(a, S(stream));
 }
 
 // ABFT check of C = A B^T against the fused rowsum. scratch: K doubles;
