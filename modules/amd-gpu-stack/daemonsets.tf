@@ -287,7 +287,9 @@ resource "kubernetes_daemon_set_v1" "metrics_exporter" {
         }
         container {
           name  = "exporter"
-          image = var.metrics_exporter_image
+          image = var.metrics_exporter_native ? var.validation_image : var.metrics_exporter_image
+          # native exporter: validation/src/amdgpu_exporter.cpp (AMD SMI, /metrics + /healthz)
+          command = var.metrics_exporter_native ? ["/opt/ntm/bin/amdgpu-exporter", "--port", tostring(var.metrics_exporter_port)] : null
           port {
             name           = "metrics"
             container_port = var.metrics_exporter_port

@@ -139,6 +139,12 @@ variable "metrics_exporter_image" {
   description = "AMD device-metrics-exporter image."
 }
 
+variable "metrics_exporter_native" {
+  type        = bool
+  default     = false
+  description = "Run the native amdgpu-exporter (AMD SMI, shipped in validation_image) instead of metrics_exporter_image in daemonsets mode."
+}
+
 variable "metrics_exporter_port" {
   type        = number
   default     = 5000

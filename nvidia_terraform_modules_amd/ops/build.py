@@ -104,10 +104,27 @@ def build_binary(force: bool = False, verbose: bool = True, asan: bool = False) 
     return out
 
 
+def build_exporter(force: bool = False, verbose: bool = True) -> Path:
+    """amdgpu-exporter: host-only C++ on libamd_smi (no device code)."""
+    out = BUILD / "amdgpu-exporter"
+    src = SRC / "amdgpu_exporter.cpp"
+    if not src.exists():
+        return out
+    if force or _stale(out, [src]):
+        BUILD.mkdir(parents=True, exist_ok=True)
+        cxx = shutil.which("g++") or "/opt/rocm/llvm/bin/clang++"
+        cmd = [cxx, "-std=c++17", "-O2", "-Wall", "-I/opt/rocm/include", str(src),
+               "-L/opt/rocm/lib", "-lamd_smi", "-Wl,-rpath,/opt/rocm/lib", "-o", str(out) + ".tmp"]
+        _run(cmd, verbose)
+        os.replace(str(out) + ".tmp", out)
+    return out
+
+
 def build_all(force: bool = False, verbose: bool = True, asan: bool = False) -> dict[str, str]:
     lib = build_library(force=force, verbose=verbose)
     binary = build_binary(force=force, verbose=verbose)
-    res = {"library": str(lib), "binary": str(binary)}
+    res = {"library": str(lib), "binary": str(binary),
+           "exporter": str(build_exporter(force=force, verbose=verbose))}
     if asan:
         res["binary_asan"] = str(build_binary(force=force, verbose=verbose, asan=True))
     return res
