@@ -52,6 +52,9 @@ def parse(argv=None):
                     help="N > 1: also sweep the hand-written xGMI all-reduce (C2, HIP IPC); its "
                          "time includes staging copies + a host barrier per call")
     ap.add_argument("--out", default="", help="also write the JSON line to this file")
+    ap.add_argument("--rehearsal", action="store_true",
+                    help="CPU/gloo + PyTorch reference ops: rehearses the multi-process "
+                         "orchestration and the JSON contract; NOT a measurement (tests only)")
     return ap.parse_args(argv)
 
 
@@ -71,38 +74,47 @@ def main(argv=None) -> int:
 
     import torch
 
-    from nvidia_terraform_modules_amd import ops
     from nvidia_terraform_modules_amd.models.validation_job import GemmWorkload, hbm_check
     from nvidia_terraform_modules_amd.parallel import collectives as coll
     from nvidia_terraform_modules_amd.parallel import dist
 
+    if args.rehearsal:
+        from nvidia_terraform_modules_amd.ops import reference as backend
+    else:
+        from nvidia_terraform_modules_amd import ops as backend
+
     _CLOCK.mark("runtime_import")
-    env = dist.init()
+    env = dist.init(backend="gloo", device_type="cpu") if args.rehearsal else dist.init()
     if env.world_size != args.gpus and env.is_main:
         print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={env.world_size}; "
               f"using WORLD_SIZE", file=sys.stderr)
     n = env.world_size
     dev = env.device
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+
     _ = torch.empty(1, device=dev)
     _CLOCK.mark("hip_init")
 
-    wl = GemmWorkload(args.size, dev, seed=20250117 + env.rank)
-    torch.cuda.synchronize(dev)
+    wl = GemmWorkload(args.size, dev, seed=20250117 + env.rank, backend=backend)
+    sync()
     _CLOCK.mark("buffers_ready")
 
     # ---- warmup (untimed)
     for _ in range(max(1, args.warmup)):
         wl.step()
-    torch.cuda.synchronize(dev)
+    sync()
     _CLOCK.mark("first_kernel")
 
     # ---- timed region: exactly K steps, barrier + sync on both sides
     dist.barrier(env)
-    torch.cuda.synchronize(dev)
+    sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         wl.step()
-    torch.cuda.synchronize(dev)
+    sync()
     t1 = time.perf_counter()
     dist.barrier(env)
     elapsed = dist.all_reduce_max(env, t1 - t0)
@@ -120,7 +132,8 @@ def main(argv=None) -> int:
         extras["verify_bad_total"] = int(bad)
     _CLOCK.mark("gemm_verified")
 
-    if not args.no_extras:
+    gpu_extras = not args.no_extras and not args.rehearsal
+    if gpu_extras:
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
         cc = torch.empty_like(wl.c)
         for _ in range(5):
@@ -146,9 +159,10 @@ def main(argv=None) -> int:
         if not ab.ok:
             verified = False
     del wl
-    torch.cuda.empty_cache()
+    if dev.type == "cuda":
+        torch.cuda.empty_cache()
 
-    if not args.no_extras:
+    if gpu_extras:
         h = hbm_check(dev, 2 << 30, 10)
         extras["hbm_copy_GBps_rank0"] = h["copy_GBps"]
         extras["hbm_read_GBps_rank0"] = h["read_GBps"]
@@ -156,15 +170,20 @@ def main(argv=None) -> int:
     _CLOCK.mark("hbm_checked")
 
     if not args.no_extras and n > 1:
+        # nccl-tests style: bf16 from 8 B (latency end) and fp32 from 1 MiB, x4 steps
         sizes = coll.sweep_sizes(1 << 20, args.allreduce_max_mib << 20, factor=4)
-        res = coll.all_reduce_sweep(env, sizes, dtype="bf16", iters=10, warmup=3)
-        extras["allreduce_bf16"] = [
-            {"bytes": r.bytes, "time_us": round(r.time_us, 1), "busbw_GBps": round(r.busbw_GBps, 1),
-             "errors": r.errors} for r in res]
+        res = coll.all_reduce_sweep(env, coll.sweep_sizes(8, args.allreduce_max_mib << 20, 4),
+                                    dtype="bf16", iters=10, warmup=3)
+        res32 = coll.all_reduce_sweep(env, sizes, dtype="fp32", iters=10, warmup=3)
+        for key, rs in (("allreduce_bf16", res), ("allreduce_fp32", res32)):
+            extras[key] = [
+                {"bytes": r.bytes, "time_us": round(r.time_us, 1),
+                 "busbw_GBps": round(r.busbw_GBps, 1), "errors": r.errors} for r in rs]
         extras["allreduce_peak_busbw_GBps"] = coll.peak_busbw(res)
-        if any(r.errors for r in res):
+        extras["allreduce_fp32_peak_busbw_GBps"] = coll.peak_busbw(res32)
+        if any(r.errors for r in res + res32):
             verified = False
-        if args.xgmi:
+        if args.xgmi and not args.rehearsal:
             from nvidia_terraform_modules_amd.parallel.xgmi import XgmiAllReduce
 
             xs = [b for b in sizes if b <= 256 << 20]
@@ -192,7 +211,9 @@ def main(argv=None) -> int:
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "bf16",
-        "data": "synthetic (uniform[-1,1) bf16 operands generated on device, hash RNG)",
+        "data": ("REHEARSAL: CPU/gloo + PyTorch reference ops - orchestration test, NOT a "
+                 "measurement" if args.rehearsal else
+                 "synthetic (uniform[-1,1) bf16 operands generated on device, hash RNG)"),
         "config": {
             "model": f"validation-job K1 GEMM C[{args.size}x{args.size}] = A[{args.size}x{args.size}]"
                      f" * B[{args.size}x{args.size}]^T, bf16 in/out, fp32 accumulate",
@@ -206,6 +227,7 @@ def main(argv=None) -> int:
         "time_to_gpu_ready_in_node_s": round(_CLOCK.elapsed("gemm_verified"), 3),
         "in_node_phases_s": {k: round(v, 4) for k, v in _CLOCK.durations().items()},
         "vs_baseline_note": "reference publishes no TFLOP/s or busbw (BASELINE.json published={})",
+        **({"rehearsal": True} if args.rehearsal else {}),
         **extras,
     }
     if env.is_main:

@@ -19,6 +19,7 @@ rank's data to prove the detector fires (failure detection).
 from __future__ import annotations
 
 import os
+import time
 from dataclasses import asdict, dataclass, field
 
 import torch
@@ -98,8 +99,18 @@ class GemmWorkload:
         return rep
 
 
+def _sync(device: torch.device) -> None:
+    if device.type == "cuda":
+        torch.cuda.synchronize(device)
+
+
 def _time_loop(fn, iters: int, device: torch.device) -> float:
-    """Seconds per call, events on the current stream."""
+    """Seconds per call: events on the current stream (wall clock on CPU)."""
+    if device.type != "cuda":
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            fn()
+        return (time.perf_counter() - t0) / iters
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record()
     for _ in range(iters):
@@ -113,13 +124,16 @@ def hbm_check(device: torch.device, nbytes: int, iters: int, backend=None) -> di
     from .. import ops as native
 
     o = backend or native
-    free, total = torch.cuda.mem_get_info(device)
+    if device.type == "cuda":
+        free, total = torch.cuda.mem_get_info(device)
+    else:  # rehearsal: host memory stands in, capacity not meaningful
+        free, total = 4 * nbytes, 0
     nbytes = min(nbytes, int(free * 0.4)) // 16 * 16
     src = torch.empty(nbytes // 4, dtype=torch.float32, device=device)
     dst = torch.empty_like(src)
     src.uniform_()
     o.stream_copy(src, dst)
-    torch.cuda.synchronize(device)
+    _sync(device)
     copy_ok = bool(torch.equal(src, dst))
     sink = torch.zeros(2048, dtype=torch.float32, device=device)
     t_copy = _time_loop(lambda: o.stream_copy(src, dst), iters, device)
@@ -157,21 +171,26 @@ class ValidationReport:
 
 
 def run_validation(env: DistEnv, cfg: ValidationConfig, clock: PhaseClock | None = None,
-                   with_hbm: bool = True, with_allreduce: bool = True) -> ValidationReport:
-    """Run the whole validation Job on this rank's GPU; collective across ranks."""
+                   with_hbm: bool = True, with_allreduce: bool = True,
+                   backend=None) -> ValidationReport:
+    """Run the whole validation Job on this rank's GPU; collective across ranks.
+
+    ``backend`` defaults to the native gfx950 ops; ``ops.reference`` (CPU)
+    is for rehearsing the multi-rank logic in tests only."""
     clock = clock or PhaseClock()
     dev = env.device
-    torch.cuda.init()
+    if dev.type == "cuda":
+        torch.cuda.init()
     _ = torch.empty(1, device=dev)
     clock.mark("hip_init")
     failures: list[str] = []
     fi = cfg.fault_inject
 
-    wl = GemmWorkload(cfg.size, dev, cfg.seed + env.rank)
-    torch.cuda.synchronize(dev)
+    wl = GemmWorkload(cfg.size, dev, cfg.seed + env.rank, backend=backend)
+    _sync(dev)
     clock.mark("buffers_ready")
     wl.step()
-    torch.cuda.synchronize(dev)
+    _sync(dev)
     clock.mark("first_kernel")
 
     gemm: dict = {"m": wl.m, "n": wl.n, "k": wl.k}
@@ -203,7 +222,7 @@ def run_validation(env: DistEnv, cfg: ValidationConfig, clock: PhaseClock | None
 
     hbm: dict = {}
     if with_hbm:
-        hbm = hbm_check(dev, cfg.hbm_bytes, cfg.hbm_iters)
+        hbm = hbm_check(dev, cfg.hbm_bytes, cfg.hbm_iters, backend=backend)
         if not hbm["copy_ok"]:
             failures.append("hbm copy mismatch")
         if cfg.hbm_floor_GBps and hbm["copy_GBps"] < cfg.hbm_floor_GBps:
@@ -238,5 +257,6 @@ def run_validation(env: DistEnv, cfg: ValidationConfig, clock: PhaseClock | None
     clock.mark("done")
     return ValidationReport(
         rank=env.rank, world_size=env.world_size,
-        device_name=torch.cuda.get_device_name(dev), gemm=gemm, hbm=hbm, allreduce=ar,
+        device_name=torch.cuda.get_device_name(dev) if dev.type == "cuda" else "cpu",
+        gemm=gemm, hbm=hbm, allreduce=ar,
         phases=clock.as_dict(), failures=failures)

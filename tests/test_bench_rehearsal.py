@@ -1,0 +1,74 @@
+"""bench.py's multi-process orchestration, rehearsed on CPU (gloo + reference
+ops): the same launch path the driver uses for N = 2/4/8 on an MI355X node
+(torch.distributed.run, RANK/WORLD_SIZE env, barrier + max over ranks, ONE
+JSON line from rank 0). Numbers here are not measurements."""
+import json
+import os
+import socket
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+CONTRACT_KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+                 "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config"}
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _json_lines(stdout):
+    out = []
+    for ln in stdout.splitlines():
+        ln = ln.strip()
+        if ln.startswith("{"):
+            out.append(json.loads(ln))
+    return out
+
+
+def _env():
+    e = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        e.pop(k, None)
+    e["OMP_NUM_THREADS"] = "1"
+    return e
+
+
+@pytest.mark.parametrize("nproc", [1, 2, 4])
+def test_torchrun_launch_one_json_line(nproc):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={nproc}", "--master-addr=127.0.0.1", f"--master-port={_port()}",
+           str(ROOT / "bench.py"), "--gpus", str(nproc), "--steps", "3", "--warmup", "1",
+           "--size", "256", "--allreduce-max-mib", "1", "--rehearsal"]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=_env(), cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = _json_lines(p.stdout)
+    assert len(lines) == 1, p.stdout[-2000:]          # rank 0 only
+    d = lines[0]
+    assert CONTRACT_KEYS <= set(d)
+    assert d["n_gpus"] == nproc and d["steps"] == 3 and d["warmup"] == 1
+    assert d["config"]["parallelism"] == f"dp{nproc}" and d["config"]["global_batch"] == nproc
+    assert d["higher_is_better"] is True and d["scaling"] == "weak" and d["dtype"] == "bf16"
+    assert d["value"] > 0 and d["verified"] is True and d["rehearsal"] is True
+    assert "NOT a measurement" in d["data"]
+    if nproc > 1:
+        assert all(r["errors"] == 0 for r in d["allreduce_bf16"] + d["allreduce_fp32"])
+        assert d["allreduce_bf16"][0]["bytes"] == 8
+
+
+def test_self_relaunch_as_child_process():
+    """`python bench.py --gpus 2` without WORLD_SIZE starts torch.distributed.run
+    as a CHILD (never exec) and propagates its exit status."""
+    env = _env()
+    env["MASTER_PORT"] = str(_port())
+    cmd = [sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--size", "256", "--allreduce-max-mib", "1", "--rehearsal"]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = _json_lines(p.stdout)
+    assert len(lines) == 1 and lines[0]["n_gpus"] == 2

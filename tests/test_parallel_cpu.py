@@ -110,3 +110,30 @@ def test_single_rank_sweep_has_no_group():
     assert env.world_size == 1 and env.is_main
     res = coll.all_reduce_sweep(env, [64], iters=1, warmup=0)
     assert res[0].errors == 0 and res[0].busbw_GBps == 0.0
+
+
+def _validation_job(env):
+    """The validation Job's multi-rank logic (reference ops on CPU): the last
+    rank's GEMM is corrupted; EVERY rank must report failure (consensus)."""
+    from nvidia_terraform_modules_amd.models.validation_job import ValidationConfig, run_validation
+    from nvidia_terraform_modules_amd.ops import reference
+
+    cfg = ValidationConfig(size=256, gemm_iters=2, gemm_warmup=1, abft_iters=1,
+                           hbm_bytes=1 << 16, hbm_iters=1, allreduce_min_bytes=1 << 10,
+                           allreduce_max_bytes=1 << 14, allreduce_iters=1,
+                           fault_inject="corrupt_gemm")
+    rep = run_validation(env, cfg, backend=reference)
+    clean = ValidationConfig(size=256, gemm_iters=2, gemm_warmup=1, abft_iters=1,
+                             hbm_bytes=1 << 16, hbm_iters=1, allreduce_min_bytes=1 << 10,
+                             allreduce_max_bytes=1 << 14, allreduce_iters=1, fault_inject="")
+    rep2 = run_validation(env, clean, backend=reference)
+    return rep.passed, rep.failures, rep2.passed, len(rep2.allreduce)
+
+
+def test_validation_job_consensus_world2():
+    out = _run(2, "_validation_job")
+    # rank 1 (last) is corrupted: it names the GEMM, rank 0 learns via consensus
+    assert out[1][0] is False and any("gemm verification" in f for f in out[1][1])
+    assert out[0][0] is False and any("another rank" in f for f in out[0][1])
+    for rank in (0, 1):
+        assert out[rank][2] is True and out[rank][3] > 0   # clean run passes, sweep ran

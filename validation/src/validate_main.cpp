@@ -179,19 +179,33 @@ void fail(const std::string& why) {
 // ------------------------------------------------- pattern kernels (C1/C2)
 // rank r contributes 2^(i%4) * (r+1): every partial sum is exact in bf16 for
 // n <= 8 ranks, so the result is checked element by element, exactly.
-__global__ void fill_pattern(uint16_t* x, size_t n, int rank) {
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
-       i += (size_t)gridDim.x * blockDim.x)
-    x[i] = ntm::f32_to_bf16_bits((float)(1u << (i & 3)) * (float)(rank + 1));
+// (exact in fp32 too). T = uint16_t holds bf16 bits, T = float holds fp32.
+template <typename T>
+__device__ __forceinline__ T to_elem(float v) {
+  if constexpr (sizeof(T) == 2) return ntm::f32_to_bf16_bits(v);
+  else return v;
+}
+template <typename T>
+__device__ __forceinline__ float from_elem(T v) {
+  if constexpr (sizeof(T) == 2) return ntm::bf16_bits_to_f32(v);
+  else return v;
 }
 
-__global__ void check_pattern(const uint16_t* x, size_t n, int nranks,
+template <typename T>
+__global__ void fill_pattern(T* x, size_t n, int rank) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+       i += (size_t)gridDim.x * blockDim.x)
+    x[i] = to_elem<T>((float)(1u << (i & 3)) * (float)(rank + 1));
+}
+
+template <typename T>
+__global__ void check_pattern(const T* x, size_t n, int nranks,
                               unsigned long long* bad) {
   unsigned long long b = 0;
   const float s = (float)(nranks * (nranks + 1) / 2);
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
        i += (size_t)gridDim.x * blockDim.x)
-    b += ntm::bf16_bits_to_f32(x[i]) != (float)(1u << (i & 3)) * s;
+    b += from_elem<T>(x[i]) != (float)(1u << (i & 3)) * s;
   if (b) atomicAdd(bad, b);
 }
 
@@ -369,6 +383,7 @@ bool run_gpu(int dev, bool last, const Opts& o, GpuResult& r) {
 }
 
 struct CollRow {
+  const char* dtype;
   size_t bytes;
   double us, algbw, busbw;
   unsigned long long bad;
@@ -395,28 +410,38 @@ bool run_rccl(const std::vector<int>& devs, const Opts& o, std::vector<CollRow>&
     CK(hipMalloc(&bad[i], 8));
   }
   bool ok = true;
-  for (size_t bytes = 1 << 20; bytes <= maxb; bytes *= 4) {
-    const size_t cnt = bytes / 2;
+  // nccl-tests style: 8 B .. max, x4 per step, bf16 then fp32
+  for (const bool f32 : {false, true})
+  for (size_t bytes = 8; bytes <= maxb; bytes *= 4) {
+    const size_t esz = f32 ? 4 : 2;
+    const size_t cnt = bytes / esz;
+    const ncclDataType_t dt = f32 ? ncclFloat32 : ncclBfloat16;
     auto run_once = [&]() -> bool {
       if (ncclGroupStart() != ncclSuccess) return false;
       for (int i = 0; i < n; ++i)
-        if (ncclAllReduce(buf[i], buf[i], cnt, ncclBfloat16, ncclSum, comms[i], st[i]) !=
-            ncclSuccess)
+        if (ncclAllReduce(buf[i], buf[i], cnt, dt, ncclSum, comms[i], st[i]) != ncclSuccess)
           return false;
       return ncclGroupEnd() == ncclSuccess;
     };
+    const unsigned blocks = (unsigned)std::min<size_t>(1024, (cnt + 255) / 256);
     for (int i = 0; i < n; ++i) {
       CK(hipSetDevice(devs[i]));
       // fault injection: the last rank contributes the wrong pattern
       const int contrib = (o.fault == "corrupt_allreduce" && i == n - 1) ? i + 1 : i;
-      hipLaunchKernelGGL(fill_pattern, dim3(1024), dim3(256), 0, st[i], (uint16_t*)buf[i], cnt, contrib);
+      if (f32)
+        hipLaunchKernelGGL(fill_pattern<float>, dim3(blocks), dim3(256), 0, st[i], (float*)buf[i], cnt, contrib);
+      else
+        hipLaunchKernelGGL(fill_pattern<uint16_t>, dim3(blocks), dim3(256), 0, st[i], (uint16_t*)buf[i], cnt, contrib);
       CK(hipMemsetAsync(bad[i], 0, 8, st[i]));
     }
     if (!run_once()) { fail("ncclAllReduce failed"); return false; }
     unsigned long long tot_bad = 0;
     for (int i = 0; i < n; ++i) {
       CK(hipSetDevice(devs[i]));
-      hipLaunchKernelGGL(check_pattern, dim3(1024), dim3(256), 0, st[i], (const uint16_t*)buf[i], cnt, n, bad[i]);
+      if (f32)
+        hipLaunchKernelGGL(check_pattern<float>, dim3(blocks), dim3(256), 0, st[i], (const float*)buf[i], cnt, n, bad[i]);
+      else
+        hipLaunchKernelGGL(check_pattern<uint16_t>, dim3(blocks), dim3(256), 0, st[i], (const uint16_t*)buf[i], cnt, n, bad[i]);
       unsigned long long b = 0;
       CK(hipMemcpyAsync(&b, bad[i], 8, hipMemcpyDeviceToHost, st[i]));
       CK(hipStreamSynchronize(st[i]));
@@ -430,7 +455,7 @@ bool run_rccl(const std::vector<int>& devs, const Opts& o, std::vector<CollRow>&
     for (int i = 0; i < n; ++i) { CK(hipSetDevice(devs[i])); CK(hipStreamSynchronize(st[i])); }
     const double sec = std::chrono::duration<double>(Clock::now() - t0).count() / iters;
     const double alg = bytes / sec / 1e9;
-    rows.push_back({bytes, sec * 1e6, alg, alg * bus_factor(n), tot_bad});
+    rows.push_back({f32 ? "fp32" : "bf16", bytes, sec * 1e6, alg, alg * bus_factor(n), tot_bad});
     if (tot_bad) ok = false;
   }
   for (int i = 0; i < n; ++i) {
@@ -493,7 +518,7 @@ bool run_xgmi(const std::vector<int>& devs, const Opts& o, std::vector<CollRow>&
     };
     for (int i = 0; i < n; ++i) {
       CK(hipSetDevice(devs[i]));
-      hipLaunchKernelGGL(fill_pattern, dim3(1024), dim3(256), 0, st[i], (uint16_t*)in[i], cnt, i);
+      hipLaunchKernelGGL(fill_pattern<uint16_t>, dim3(1024), dim3(256), 0, st[i], (uint16_t*)in[i], cnt, i);
       CK(hipStreamSynchronize(st[i]));
     }
     if (!run_once()) { fail("xGMI all-reduce launch failed"); return false; }
@@ -507,7 +532,7 @@ bool run_xgmi(const std::vector<int>& devs, const Opts& o, std::vector<CollRow>&
       unsigned long long* bad;
       CK(hipMalloc(&bad, 8));
       CK(hipMemset(bad, 0, 8));
-      hipLaunchKernelGGL(check_pattern, dim3(1024), dim3(256), 0, st[i], (const uint16_t*)out[i], cnt, n, bad);
+      hipLaunchKernelGGL(check_pattern<uint16_t>, dim3(1024), dim3(256), 0, st[i], (const uint16_t*)out[i], cnt, n, bad);
       unsigned long long b = 0;
       CK(hipMemcpyAsync(&b, bad, 8, hipMemcpyDeviceToHost, st[i]));
       CK(hipStreamSynchronize(st[i]));
@@ -520,7 +545,7 @@ bool run_xgmi(const std::vector<int>& devs, const Opts& o, std::vector<CollRow>&
     for (int i = 0; i < n; ++i) { CK(hipSetDevice(devs[i])); CK(hipStreamSynchronize(st[i])); }
     const double sec = std::chrono::duration<double>(Clock::now() - t0).count() / iters;
     const double alg = bytes / sec / 1e9;
-    rows.push_back({bytes, sec * 1e6, alg, alg * bus_factor(n), tot_bad});
+    rows.push_back({"bf16", bytes, sec * 1e6, alg, alg * bus_factor(n), tot_bad});
     if (tot_bad) ok = false;
   }
   for (int i = 0; i < n; ++i) {
@@ -539,7 +564,8 @@ std::string coll_json(const std::vector<CollRow>& rows) {
   std::string s = "[";
   for (size_t i = 0; i < rows.size(); ++i) {
     const auto& r = rows[i];
-    s += (i ? "," : "") + std::string("{\"bytes\":") + std::to_string(r.bytes) +
+    s += (i ? "," : "") + std::string("{\"dtype\":\"") + r.dtype + "\",\"bytes\":" +
+         std::to_string(r.bytes) +
          ",\"time_us\":" + jnum(r.us) + ",\"algbw_GBps\":" + jnum(r.algbw) +
          ",\"busbw_GBps\":" + jnum(r.busbw) + ",\"wrong\":" + std::to_string(r.bad) + "}";
   }
@@ -618,7 +644,7 @@ int main(int argc, char** argv) {
           ",\"hbm_copy_GBps\":" + jnum(r.hbm_copy_gbps) +
           ",\"hbm_read_GBps\":" + jnum(r.hbm_read_gbps) + "}";
   }
-  js += "],\"rccl_allreduce_bf16\":" + coll_json(rccl_rows);
+  js += "],\"rccl_allreduce\":" + coll_json(rccl_rows);
   js += ",\"xgmi_allreduce_bf16\":" + coll_json(xgmi_rows);
   double t_gemm = t_hip, t_hbm = t_hip;
   for (auto& r : res) { t_gemm = std::max(t_gemm, r.t_gemm); t_hbm = std::max(t_hbm, r.t_hbm); }
