@@ -1,6 +1,7 @@
 """Time-to-GPU-ready instrumentation: phase clock, apply-log timeline and the
 plan-graph critical-path model (all CPU)."""
 import json
+from pathlib import Path
 
 import pytest
 
@@ -104,3 +105,91 @@ def test_critical_path_uses_measured_durations(repo):
     base = critical_path(g).total_s
     faster = critical_path(g, {"azurerm_kubernetes_cluster_node_pool.holoscan": 60.0}).total_s
     assert faster < base
+
+
+# --------------------------------------------------------------- CLI record
+TF_STUB = r'''#!/usr/bin/env python3
+import json, sys, time
+from datetime import datetime, timezone
+def ts(): return datetime.now(timezone.utc).isoformat()
+def emit(typ, addr, action="create", **kw):
+    hook = {"resource": {"addr": addr}, "action": action, **kw}
+    print(json.dumps({"@timestamp": ts(), "type": typ, "hook": hook}), flush=True)
+print(json.dumps({"@timestamp": ts(), "type": "version", "terraform": "1.9.0"}), flush=True)
+for addr in ["module.vpc.aws_vpc.this[0]", "module.eks.aws_eks_cluster.this[0]",
+             "module.amd_gpu_stack.helm_release.amd_gpu_operator[0]",
+             "module.amd_gpu_stack.kubernetes_job_v1.gpu_validation[0]"]:
+    emit("apply_start", addr)
+    time.sleep(0.3)
+    emit("apply_complete", addr, elapsed_seconds=0.3)
+'''
+
+KUBECTL_STUB = r'''#!/usr/bin/env python3
+import json, sys, os
+state = os.environ["STUB_STATE"]
+n = int(open(state).read()) if os.path.exists(state) else 0
+open(state, "w").write(str(n + 1))
+args = sys.argv[1:]
+if n < 2:
+    sys.exit(1)                       # cluster not there yet
+if "nodes" in args:
+    print(json.dumps({"items": [{"metadata": {"name": "gpu-node-0"},
+                                 "status": {"allocatable": {"amd.com/gpu": "8"}}}]}))
+elif "pods" in args:
+    msg = json.dumps({"passed": True, "n_gpus": 8, "gemm_tflops_aggregate": 12345.0})
+    print(json.dumps({"items": [{"status": {"containerStatuses": [{"state": {"terminated": {
+        "exitCode": 0, "message": msg, "finishedAt": "2030-01-01T00:00:00Z"}}}]}}]}))
+else:
+    sys.exit(1)
+'''
+
+
+def _stub(path, body):
+    path.write_text(body)
+    path.chmod(0o755)
+
+
+def test_cli_record_with_stub_terraform_and_kubectl(tmp_path):
+    import os
+    import subprocess
+    import sys
+
+    bindir = tmp_path / "bin"
+    bindir.mkdir()
+    _stub(bindir / "terraform", TF_STUB)
+    _stub(bindir / "kubectl", KUBECTL_STUB)
+    env = dict(os.environ, PATH=f"{bindir}:{os.environ['PATH']}",
+               STUB_STATE=str(tmp_path / "kstate"))
+    out = tmp_path / "run"
+    p = subprocess.run([sys.executable, "-m", "nvidia_terraform_modules_amd.gpu_ready", "record",
+                        "--out", str(out), "--kubectl", "kubectl", "--poll", "0.2", "--",
+                        "terraform", "apply", "-json", "-auto-approve"],
+                       capture_output=True, text=True, env=env, timeout=120,
+                       cwd=Path(__file__).resolve().parents[1])
+    assert p.returncode == 0, p.stderr
+    assert "time_to_gpu_ready_s" in p.stdout
+    ev = json.loads((out / "k8s_events.json").read_text())["items"]
+    assert ev and "amd.com/gpu allocatable 8" in ev[0]["message"]
+    rep = json.loads((out / "validation.json").read_text())
+    assert rep["passed"] and rep["end_epoch_s"] > 1.8e9          # finishedAt 2030
+    tl = json.loads((out / "timeline.json").read_text())
+    assert tl["phase_end"]["gpu_allocatable"] <= tl["phase_end"]["validation_done"]
+    assert tl["time_to_gpu_ready_s"] > 0
+    # the saved log replays through the `timeline` subcommand
+    p2 = subprocess.run([sys.executable, "-m", "nvidia_terraform_modules_amd.gpu_ready", "timeline",
+                         str(out / "apply.jsonl"), "--json"], capture_output=True, text=True,
+                        timeout=60, cwd=Path(__file__).resolve().parents[1])
+    assert p2.returncode == 0 and json.loads(p2.stdout)["resources"]
+
+
+def test_cli_critical_path_json(tmp_path):
+    import subprocess
+    import sys
+
+    root = Path(__file__).resolve().parents[1]
+    p = subprocess.run([sys.executable, "-m", "nvidia_terraform_modules_amd.gpu_ready",
+                        "critical-path", str(root / "gke"), "--json"], capture_output=True,
+                       text=True, timeout=60, cwd=root)
+    assert p.returncode == 0, p.stderr
+    d = json.loads(p.stdout)
+    assert d["total_s"] > 0 and d["path"][-1][0].endswith("kubernetes_job_v1.gpu_validation")
