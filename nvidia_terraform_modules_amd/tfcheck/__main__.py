@@ -35,7 +35,32 @@ def main(argv=None) -> int:
                     help="regenerate the terraform-docs tables in every module README")
     ap.add_argument("--docs-check", action="store_true",
                     help="exit 1 if any module README's generated tables are stale")
+    ap.add_argument("--plan", action="store_true",
+                    help="offline plan of the FIRST dir: variables + validations, count/for_each "
+                         "expansion, preconditions, local child modules")
+    ap.add_argument("--var-file", action="append", default=[])
+    ap.add_argument("--var", action="append", default=[], help="NAME=VALUE (repeatable)")
     args = ap.parse_args(argv)
+
+    if args.plan:
+        from .plan import plan
+
+        res = plan(args.dirs[0], args.var_file, args.var)
+        if args.json:
+            print(json.dumps(res.as_dict(), indent=2))
+        else:
+            for a in res.data_sources:
+                print(f" <= {a}")
+            for a in res.resources:
+                print(f"  + {a}")
+            for m in res.registry_modules:
+                print(f"  ? {m}")
+            for w in res.warnings:
+                print(f"warning: {w}")
+            for e in res.errors:
+                print(f"error: {e}")
+            print(res.summary())
+        return 0 if res.ok else 1
 
     if args.docs or args.docs_check:
         from .docs import update
