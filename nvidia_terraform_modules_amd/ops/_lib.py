@@ -31,6 +31,8 @@ def _declare(lib: ctypes.CDLL) -> None:
         "ntm_gemm_bf16": ([c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp], c_int),
         "ntm_gemm_bf16_variant": (
             [c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp], c_int),
+        "ntm_gemm_bf16_knob": (
+            [c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp], c_int),
         "ntm_gemm_bf16_rowsum": (
             [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp], c_int),
         "ntm_abft_check": ([c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int,

@@ -59,6 +59,12 @@ def gemm_bf16(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
     _require(out, "out", torch.bfloat16)
     if tuple(out.shape) != (m, n):
         raise ValueError("out has the wrong shape")
+    if variant.startswith("knob"):            # experimental tuning sweep: "knob<N>"
+        rc = lib().ntm_gemm_bf16_knob(int(variant[4:]), a.data_ptr(), b.data_ptr(),
+                                      out.data_ptr(), m, n, k, a.stride(0), b.stride(0),
+                                      out.stride(0), stream_handle())
+        check(rc, "ntm_gemm_bf16_knob")
+        return out
     rc = lib().ntm_gemm_bf16_variant(
         GEMM_VARIANTS[variant], a.data_ptr(), b.data_ptr(), out.data_ptr(), m, n, k,
         a.stride(0), b.stride(0), out.stride(0), stream_handle())

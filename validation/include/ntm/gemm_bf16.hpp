@@ -147,10 +147,11 @@ __device__ __forceinline__ void read_b(const Ctx& c, bf16x8 (&b)[2][2],
 // 16 MFMAs: one 64x32 quadrant over K = 64. Operand order is swapped (B
 // fragment first) so each lane ends up holding 4 consecutive output columns
 // of one row -> 8-byte stores in the epilogue.
+template <bool PRIO = true>
 __device__ __forceinline__ void mma_quadrant(f32x4 (&acc)[4][2],
                                              const bf16x8 (&a)[4][2],
                                              const bf16x8 (&b)[2][2]) {
-  __builtin_amdgcn_s_setprio(1);
+  if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
   for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
@@ -159,7 +160,7 @@ __device__ __forceinline__ void mma_quadrant(f32x4 (&acc)[4][2],
       for (int nt = 0; nt < 2; ++nt)
         acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
             b[nt][ks], a[mt][ks], acc[mt][nt], 0, 0, 0);
-  __builtin_amdgcn_s_setprio(0);
+  if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
 }
 
 // One phase of the K loop. P: phase within the K-tile (0..3); ISSUE: whether
@@ -197,6 +198,7 @@ __device__ __forceinline__ void phase(const Ctx& c, Frags& f,
 
 // Block -> output tile. Bijective XCD remap (nwg % 8 != 0 safe), then a
 // GROUP_M raster inside each XCD's contiguous chunk.
+template <int GROUP_M = kGroupM>
 __device__ __forceinline__ void tile_coords(int M, int N, int& tm, int& tn) {
   const int nwg = gridDim.x;
   const int bid = blockIdx.x;
@@ -205,10 +207,10 @@ __device__ __forceinline__ void tile_coords(int M, int N, int& tm, int& tn) {
   const int wgid =
       (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
   const int tiles_m = M / BM, tiles_n = N / BN;
-  const int group = kGroupM * tiles_n;
+  const int group = GROUP_M * tiles_n;
   const int gid = wgid / group;
-  const int first_m = gid * kGroupM;
-  const int gsz = min(tiles_m - first_m, kGroupM);
+  const int first_m = gid * GROUP_M;
+  const int gsz = min(tiles_m - first_m, GROUP_M);
   const int in_group = wgid - gid * group;
   tm = first_m + in_group % gsz;
   tn = in_group / gsz;

@@ -55,7 +55,7 @@ __device__ __forceinline__ void issue_half3(const Ctx& c, int kt, int buf, int T
   glds16(s + 32, d + 1024);
 }
 
-template <int P, bool ODD>
+template <int P, bool ODD, bool PRIO>
 __device__ __forceinline__ void phase3(const Ctx& c, Frags3& f,
                                        f32x4 (&acc)[2][2][4][2], int t, int T) {
   bf16x8(&bcur)[2][2] = ODD ? f.b1 : f.b0;
@@ -71,29 +71,34 @@ __device__ __forceinline__ void phase3(const Ctx& c, Frags3& f,
   if constexpr (P == 3) issue_half3<kBHi>(c, t + 2, cur, T);
   wait_vmcnt<10>();
   raw_barrier();
-  if constexpr (P == 0) mma_quadrant(acc[0][0], f.a, bcur);
-  if constexpr (P == 1) mma_quadrant(acc[0][1], f.a, both);
-  if constexpr (P == 2) mma_quadrant(acc[1][1], f.a, both);
-  if constexpr (P == 3) mma_quadrant(acc[1][0], f.a, bcur);
+  if constexpr (P == 0) mma_quadrant<PRIO>(acc[0][0], f.a, bcur);
+  if constexpr (P == 1) mma_quadrant<PRIO>(acc[0][1], f.a, both);
+  if constexpr (P == 2) mma_quadrant<PRIO>(acc[1][1], f.a, both);
+  if constexpr (P == 3) mma_quadrant<PRIO>(acc[1][0], f.a, bcur);
   raw_barrier();
 }
 
-template <bool ODD>
+template <bool ODD, bool PRIO>
 __device__ __forceinline__ void tile3(const Ctx& c, Frags3& f,
                                       f32x4 (&acc)[2][2][4][2], int t, int T) {
-  phase3<0, ODD>(c, f, acc, t, T);
-  phase3<1, ODD>(c, f, acc, t, T);
-  phase3<2, ODD>(c, f, acc, t, T);
-  phase3<3, ODD>(c, f, acc, t, T);
+  phase3<0, ODD, PRIO>(c, f, acc, t, T);
+  phase3<1, ODD, PRIO>(c, f, acc, t, T);
+  phase3<2, ODD, PRIO>(c, f, acc, t, T);
+  phase3<3, ODD, PRIO>(c, f, acc, t, T);
 }
 
-template <bool kRowSum>
+// GROUP_M / PRIO are tuning knobs (tools/gemm_check.py --variants knobN). The
+// defaults are the measured best (profiles/r1_pp3_knobs, 15 interleaved
+// rounds): s_setprio(1) around the MFMA block COSTS 1.3-1.7 % here - the
+// partner group's LDS reads and DMA issue are what the ping-pong must not
+// starve - and GROUP_M 4 vs 8 is a tie (16 / 32 thrash the XCD's L2: -6/-18 %).
+template <bool kRowSum, int GROUP_M = kGroupM, bool PRIO = false>
 __global__ void __launch_bounds__(kThreads, 2)
     gemm_bf16_pp3_kernel(GemmArgs p) {
   __shared__ __attribute__((aligned(16))) char smem[kLdsBytes3];
 
   int tm, tn;
-  tile_coords(p.M, p.N, tm, tn);
+  tile_coords<GROUP_M>(p.M, p.N, tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
 
   Ctx c;
@@ -141,8 +146,8 @@ __global__ void __launch_bounds__(kThreads, 2)
   if (c.wr == 1) raw_barrier();  // ping-pong stagger
 
   for (int t = 0; t < T; t += 2) {
-    tile3<false>(c, f, acc, t, T);
-    tile3<true>(c, f, acc, t + 1, T);
+    tile3<false, PRIO>(c, f, acc, t, T);
+    tile3<true, PRIO>(c, f, acc, t + 1, T);
   }
   if (c.wr == 0) raw_barrier();
   wait_vmcnt<0>();  // dummy pieces: nothing may land after the WG exits
@@ -161,6 +166,29 @@ inline hipError_t launch_gemm_bf16_pp3(const GemmArgs& a, hipStream_t stream) {
   else
     hipLaunchKernelGGL(gemm_bf16_pp3_kernel<false>, dim3(grid), dim3(kThreads),
                        0, stream, a);
+  return hipGetLastError();
+}
+
+// Experimental knob sweep: knob = GROUP_M code (0:4, 1:8, 2:16, 3:32) + 4 * !PRIO;
+// 8..11: GROUP_M 1, 2, 3, 6 without setprio.
+inline hipError_t launch_gemm_bf16_pp3_knob(const GemmArgs& a, int knob, hipStream_t s) {
+  if (!shape_ok3(a.M, a.N, a.K) || a.rowsum) return hipErrorInvalidValue;
+  const dim3 g((unsigned)((a.M / BM) * (a.N / BN))), b(kThreads);
+  switch (knob) {
+    case 0: hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, 4, true>), g, b, 0, s, a); break;
+    case 1: hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, 8, true>), g, b, 0, s, a); break;
+    case 2: hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, 16, true>), g, b, 0, s, a); break;
+    case 3: hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, 32, true>), g, b, 0, s, a); break;
+    case 4: hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, 4, false>), g, b, 0, s, a); break;
+    case 5: hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, 8, false>), g, b, 0, s, a); break;
+    case 6: hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, 16, false>), g, b, 0, s, a); break;
+    case 7: hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, 32, false>), g, b, 0, s, a); break;
+    case 8: hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, 1, false>), g, b, 0, s, a); break;
+    case 9: hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, 2, false>), g, b, 0, s, a); break;
+    case 10: hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, 3, false>), g, b, 0, s, a); break;
+    case 11: hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, 6, false>), g, b, 0, s, a); break;
+    default: return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 

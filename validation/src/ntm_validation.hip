@@ -39,6 +39,7 @@ NTM_API int ntm_gemm_shape_ok(int M, int N, int K) {
 // profiles/r1_pp3/):
 //   8192^3: 5 1567 TF, 4 1530, 1 1521, 2 ~1310-1380; hipBLASLt 1667
 //   4096^3: 5 1479 TF, 4 1435, 1 1424;               hipBLASLt 1562
+// then variant 5 without s_setprio: +1.3-1.7 % (profiles/r1_pp3_knobs).
 // Variants 4 and 5 pass tools/race_screen.py (bitwise-stable under HBM noise).
 // Default: 5 when K % 128 == 0, else 4 (both need K % 64 == 0, K >= 128).
 constexpr int kDefaultVariant = 5;
@@ -86,6 +87,23 @@ NTM_API int ntm_gemm_bf16_variant(int variant, const void* A, const void* B,
                         : (int)ntm::gemm4::launch<4>(a, S(stream));
   }
   return (int)hipErrorInvalidValue;
+}
+
+// Experimental: pingpong8c tuning knobs (see launch_gemm_bf16_pp3_knob).
+NTM_API int ntm_gemm_bf16_knob(int knob, const void* A, const void* B, void* C,
+                               int M, int N, int K, int lda, int ldb, int ldc,
+                               void* stream) {
+  ntm::gemm::GemmArgs a;
+  a.A = (const __bf16*)A;
+  a.B = (const __bf16*)B;
+  a.C = (__bf16*)C;
+  a.M = M;
+  a.N = N;
+  a.K = K;
+  a.lda = lda;
+  a.ldb = ldb;
+  a.ldc = ldc;
+  return (int)ntm::gemm3::launch_gemm_bf16_pp3_knob(a, knob, S(stream));
 }
 
 NTM_API int ntm_gemm_bf16(const void* A, const void* B, void* C, int M, int N,
