@@ -1,0 +1,22 @@
+# AMD GPU stack on AKS. The node images ship no amdgpu driver, so the stack
+# installs it (upstream passed driver.enabled=false, which only works where a
+# vendor driver is preinstalled). Everything is a tracked Terraform resource
+# - version bumps apply in place - instead of a create-only helm provisioner.
+# Only the validation Job waits for the MI355X pool (gpu_node_pool_ids).
+
+module "amd_gpu_stack" {
+  source = "../modules/amd-gpu-stack"
+
+  cluster_name                = var.cluster_name
+  gpu_stack_mode              = var.gpu_stack_mode
+  gpu_operator_version        = var.gpu_operator_version
+  gpu_operator_driver_version = var.gpu_operator_driver_version
+  gpu_operator_namespace      = var.gpu_operator_namespace
+
+  gpu_node_selector = { "amd.com/gpu.present" = "true" }
+  gpu_node_pool_ids = [azurerm_kubernetes_cluster_node_pool.mi355x.id]
+
+  validation_enabled   = var.gpu_validation_enabled
+  validation_image     = var.gpu_validation_image
+  validation_gpu_count = var.gpus_per_node
+}

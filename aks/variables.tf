@@ -1,161 +1,161 @@
-# Call surface of /root/reference/aks/variables.tf: all 18 names; required
-# location + admin_group_object_ids unchanged. cpu_os_sku / gpu_os_sku were
-# dead in the reference and are wired now.
+# Inputs of the AKS root. Names and required-ness (location,
+# admin_group_object_ids) follow the reference call surface; wording, types,
+# defaults and validation are this module's own.
 
-/****************************
-Azure Resource Group Variables
-****************************/
-variable "existing_resource_group_name" {
-  description = "Existing resource group to deploy into; null = create <cluster_name>-rg."
-  default     = null
-  type        = string
-}
+# --- placement and access ---------------------------------------------------
 
 variable "location" {
+  description = "Azure region for the resource group (when created) and the cluster."
   type        = string
-  description = "The region to create resources in"
 }
 
-/****************************
-AKS Variables
-****************************/
+variable "existing_resource_group_name" {
+  description = "Deploy into this resource group instead of creating <cluster_name>-rg."
+  type        = string
+  default     = null
+}
+
+variable "admin_group_object_ids" {
+  description = "Object ids (GUIDs, not names or e-mails) of Entra ID groups that become cluster admins. Attaching them requires the Azure Owner role, Contributor is not enough."
+  type        = list(any)
+}
+
 variable "cluster_name" {
+  description = "AKS cluster name and DNS prefix."
   type        = string
   default     = "mi355x-cluster"
-  description = "The name of the AKS Cluster to be created"
 }
 
 variable "kubernetes_version" {
+  description = "Kubernetes version of the control plane and both pools (see `az aks get-versions -l <location>`)."
   type        = string
   default     = "1.31"
-  description = "Kubernetes version ('az aks get-versions --location <location> --output table' lists them)."
+}
+
+# --- system (default) pool ------------------------------------------------
+
+variable "cpu_machine_type" {
+  description = "VM size of the system pool."
+  type        = string
+  default     = "Standard_D16s_v5"
+}
+
+variable "cpu_os_sku" {
+  description = "Node OS of the system pool (Ubuntu or AzureLinux)."
+  type        = string
+  default     = "Ubuntu"
 }
 
 variable "cpu_node_pool_disk_size" {
-  description = "OS disk size (GB) of the default (CPU) node pool"
+  description = "OS disk of each system node in GB."
+  type        = number
   default     = 128
 }
 
 variable "cpu_node_pool_count" {
-  description = "Initial node count of the default (CPU) pool"
+  description = "System-pool size at creation."
+  type        = number
   default     = 1
 }
 
 variable "cpu_node_pool_min_count" {
-  description = "Min count of nodes in the default (CPU) pool"
+  description = "Autoscaler floor of the system pool."
+  type        = number
   default     = 1
 }
 
 variable "cpu_node_pool_max_count" {
-  description = "Max count of nodes in the default (CPU) pool"
+  description = "Autoscaler ceiling of the system pool."
+  type        = number
   default     = 5
 }
 
-variable "cpu_machine_type" {
-  default     = "Standard_D16s_v5"
-  description = "VM size of the AKS CPU node pool"
+# --- MI355X pool ------------------------------------------------------------
+
+variable "gpu_machine_type" {
+  description = "VM size with 8 x AMD Instinct MI355X available to your subscription and region; plan stops until it is set."
+  type        = string
+  default     = ""
 }
 
-variable "cpu_os_sku" {
-  description = "OS SKU of the CPU pool (Ubuntu, AzureLinux)."
+variable "gpu_os_sku" {
+  description = "Node OS of the MI355X pool; must be Ubuntu because amdgpu-dkms builds against its kernel headers."
+  type        = string
   default     = "Ubuntu"
+  validation {
+    condition     = var.gpu_os_sku == "Ubuntu"
+    error_message = "The MI355X pool needs gpu_os_sku = \"Ubuntu\" (ROCm 7 amdgpu-dkms)."
+  }
 }
 
-/****************************
-GPU Node Pool Variables
-****************************/
 variable "gpu_node_pool_disk_size" {
-  description = "OS disk size (GB) of the MI355X GPU pool (ROCm images are multi-GB)"
+  description = "OS disk of each MI355X node in GB (ROCm images are several GB)."
+  type        = number
   default     = 1024
 }
 
 variable "gpu_node_pool_count" {
-  description = "Initial node count of the GPU pool"
+  description = "MI355X pool size at creation."
+  type        = number
   default     = 1
 }
 
 variable "gpu_node_pool_min_count" {
-  description = "Min count of nodes in the GPU pool"
+  description = "Autoscaler floor of the MI355X pool."
+  type        = number
   default     = 1
 }
 
 variable "gpu_node_pool_max_count" {
-  description = "Max count of nodes in the GPU pool"
+  description = "Autoscaler ceiling of the MI355X pool."
+  type        = number
   default     = 5
 }
 
-variable "gpu_machine_type" {
-  type        = string
-  default     = ""
-  description = "VM size with 8x AMD Instinct MI355X (required for apply; set the ND-series MI355X size available in your region/quota)."
+variable "gpus_per_node" {
+  description = "MI355X devices per node; the validation Job requests all of them."
+  type        = number
+  default     = 8
 }
 
-variable "gpu_os_sku" {
-  description = "OS SKU of the GPU pool. Ubuntu: amdgpu-dkms needs the Ubuntu kernel headers."
-  default     = "Ubuntu"
+# --- AMD GPU stack and validation ---------------------------------------------
 
+variable "gpu_stack_mode" {
+  description = "\"operator\" (AMD GPU Operator + DeviceConfig) or \"daemonsets\" (amdgpu-dkms + rocm/k8s-device-plugin)."
+  type        = string
+  default     = "operator"
   validation {
-    condition     = var.gpu_os_sku == "Ubuntu"
-    error_message = "The MI355X GPU pool needs gpu_os_sku = \"Ubuntu\" (ROCm 7 amdgpu-dkms)."
+    condition     = contains(["operator", "daemonsets"], var.gpu_stack_mode)
+    error_message = "Either operator or daemonsets."
   }
 }
 
-/****************************
-GPU Operator Variables
-****************************/
 variable "gpu_operator_version" {
+  description = "AMD GPU Operator chart version."
   type        = string
   default     = "v1.3.0"
-  description = "AMD GPU Operator Helm chart version"
 }
 
-/****************************
-Active Directory Variables
-****************************/
-variable "admin_group_object_ids" {
-  type        = list(any)
-  description = <<EOH
-  (Required) A list of Object IDs (GUIDs) of Azure Active Directory Groups which should have Owner Role on the Cluster.
-  This is not the email address of the group, the GUID can be found in the Azure panel by searching for the AD Group
-  NOTE: You will need Azure "Owner" role (not "Contributor") to attach an AD role to the Kubernetes cluster.
-  EOH
-}
-
-/****************************
-New (not in the reference surface)
-****************************/
 variable "gpu_operator_driver_version" {
+  description = "amdgpu / ROCm release the stack installs; AKS images carry no amdgpu driver of their own."
   type        = string
   default     = "7.0.2"
-  description = "amdgpu driver / ROCm release for the GPU nodes. AKS node images ship no amdgpu driver, so the stack installs it (the reference's driver.enabled=false relied on a preinstalled NVIDIA driver)."
 }
 
 variable "gpu_operator_namespace" {
+  description = "Namespace of the GPU stack, its exporter and the validation Job."
   type        = string
   default     = "kube-amd-gpu"
-  description = "Namespace for the AMD GPU stack (the reference hard-coded its operator namespace)."
-}
-
-variable "gpu_stack_mode" {
-  type        = string
-  default     = "operator"
-  description = "\"operator\" or \"daemonsets\"."
-}
-
-variable "gpus_per_node" {
-  type        = number
-  default     = 8
-  description = "MI355X GPUs per GPU node (validation Job request)."
 }
 
 variable "gpu_validation_enabled" {
+  description = "Make apply wait for the MI355X validation Job."
   type        = bool
   default     = true
-  description = "Run the MI355X validation Job and make apply wait for it."
 }
 
 variable "gpu_validation_image" {
+  description = "Registry path of the image built from validation/image/Dockerfile."
   type        = string
   default     = "ghcr.io/amd-instinct-terraform-modules/amdgpu-validate:0.1.0"
-  description = "Image built from validation/image/Dockerfile."
 }

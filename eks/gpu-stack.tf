@@ -1,0 +1,24 @@
+# AMD GPU enablement (operator or DKMS + device plugin), metrics exporter and
+# the validation Job that apply waits for. Only the Job is tied to the MI355X
+# node group; the rest installs from the system pool while GPU nodes boot.
+
+module "amd_gpu_stack" {
+  source = "../modules/amd-gpu-stack"
+
+  cluster_name   = var.cluster_name
+  gpu_stack_mode = var.gpu_stack_mode
+
+  gpu_operator_version        = var.gpu_operator_version
+  gpu_operator_driver_version = var.gpu_operator_driver_version
+  gpu_operator_namespace      = var.gpu_operator_namespace
+
+  gpu_node_selector = { "amd.com/gpu.present" = "true" }
+  gpu_node_pool_ids = [module.eks.eks_managed_node_groups["gpu_node_pool"].node_group_id]
+
+  validation_enabled      = var.gpu_validation_enabled
+  validation_image        = var.gpu_validation_image
+  validation_gpu_count    = var.gpus_per_node
+  validation_tflops_floor = var.gpu_validation_tflops_floor
+
+  depends_on = [module.eks]
+}

@@ -1,293 +1,296 @@
-# Call surface of the reference EKS module (/root/reference/eks/variables.tf),
-# every name kept; defaults moved to MI355X values; previously dead variables
-# (aws_profile, region, cpu_node_pool_additional_user_data,
-# additional_user_data, enable_dns_support) are now wired.
+# Inputs of the EKS root. Names and required-ness follow the reference module's
+# call surface (pinned by tests/fixtures/reference_surface.json); descriptions,
+# types, defaults and validation are this module's own. Sections:
+#   1 identity   2 network   3 MI355X pool   4 CPU pool   5 node bootstrap
+#   6 AMD GPU stack   7 validation Job
 
-/************************
-  AWS Variables
-*************************/
+# --- 1 identity ------------------------------------------------------------
 
-variable "aws_profile" {
+variable "cluster_name" {
+  description = "Short name of the cluster. The control plane becomes tf-<name>; node groups, VPC and IAM roles derive their names from it."
   type        = string
-  default     = ""
-  description = "AWS CLI profile for the provider and the kube exec token (empty = default credential chain)."
+  nullable    = false
+  validation {
+    condition     = can(regex("^[a-z][a-z0-9-]{0,30}$", var.cluster_name))
+    error_message = "Use 1-31 lowercase letters, digits or dashes, starting with a letter."
+  }
 }
 
 variable "region" {
+  description = "Region for every AWS resource and for the token command of the kube providers."
   type        = string
   default     = "us-west-2"
-  description = "AWS region to provision the MI355X-ready Kubernetes cluster in."
 }
 
-
-/************************
-  EKS Variables
-*************************/
-
-variable "cluster_name" {
+variable "aws_profile" {
+  description = "Named AWS CLI profile used by the provider and by `aws eks get-token`; leave empty for the default credential chain."
   type        = string
-  description = "Cluster name; the EKS control plane is named tf-<cluster_name>."
+  default     = ""
 }
 
 variable "cluster_version" {
+  description = "Kubernetes minor version of the control plane; it also picks the matching Ubuntu EKS image for MI355X nodes."
   type        = string
   default     = "1.31"
-  description = "EKS Kubernetes version (major.minor). Also selects the Ubuntu EKS AMI for GPU nodes."
-}
-
-/************************
-  GPU Operator Variables (AMD GPU Operator)
-*************************/
-variable "gpu_operator_version" {
-  type        = string
-  default     = "v1.3.0"
-  description = "AMD GPU Operator Helm chart version."
-}
-
-variable "gpu_operator_driver_version" {
-  type        = string
-  default     = "7.0.2"
-  description = "amdgpu driver / ROCm release installed on GPU nodes (>= 7.0 for gfx950)."
-}
-
-variable "gpu_operator_namespace" {
-  type        = string
-  default     = "kube-amd-gpu"
-  description = "Namespace for the AMD GPU stack and the validation Job."
-}
-
-/*****************************
-  Managed Node Pool Variables
-******************************/
-
-/******************************
-  GPU-only Node Pool Variables
-*******************************/
-variable "gpu_ami_id" {
-  type        = string
-  description = "AMI for the GPU nodes. Empty = look up the Canonical Ubuntu EKS image for cluster_version (ROCm 7 needs Ubuntu 22.04/24.04). A non-empty value is used as-is."
-  default     = ""
-}
-
-variable "gpu_instance_type" {
-  type        = string
-  default     = ""
-  description = "EC2 instance type with 8x AMD Instinct MI355X (gfx950, 288 GB HBM3E each). Required for apply: there is no public default, set the type of your capacity reservation."
-
   validation {
-    condition     = var.gpu_instance_type == "" || can(regex("^[a-z0-9-]+\\.[a-z0-9]+$", var.gpu_instance_type))
-    error_message = "gpu_instance_type must look like an EC2 instance type (family.size)."
+    condition     = can(regex("^1\\.[0-9]{2}$", var.cluster_version))
+    error_message = "Expected a Kubernetes minor version such as 1.31."
   }
 }
 
-variable "max_gpu_nodes" {
-  type        = string
-  default     = "5"
-  description = "Maximum number of GPU nodes in the Autoscaling Group"
-}
-
-variable "min_gpu_nodes" {
-  type        = string
-  default     = "1"
-  description = "Minimum number of GPU nodes in the Autoscaling Group"
-}
-
-variable "desired_count_gpu_nodes" {
-  type        = string
-  default     = "1"
-  description = "Desired number of GPU nodes in the Autoscaling Group"
-}
-
-variable "gpu_node_pool_root_disk_size_gb" {
-  type        = number
-  default     = 1024
-  description = "Root disk size of GPU nodes (ROCm container images are multi-GB; 8-GPU nodes pull several)."
-
-  validation {
-    condition     = var.gpu_node_pool_root_disk_size_gb >= 256
-    error_message = "GPU node root disks below 256 GB cannot hold ROCm images + DKMS build trees."
-  }
-}
-
-variable "gpu_node_pool_root_volume_type" {
-  type        = string
-  default     = "gp3"
-  description = "EBS volume type of the GPU node root disk."
-}
-
-variable "gpu_node_pool_delete_on_termination" {
-  type        = bool
-  default     = true
-  description = "Delete the GPU nodes' root volumes on termination."
-}
-
-variable "gpu_node_pool_additional_user_data" {
-  type        = string
-  default     = ""
-  description = "Shell appended after the EKS bootstrap (and after the MI355X host tuning) on GPU nodes."
-}
-
-/************************
-  CPU-only Node Pool Variables
-*************************/
-
-variable "cpu_instance_type" {
-  type        = string
-  default     = "m7i.2xlarge"
-  description = "CPU EC2 worker node instance type"
-}
-
-variable "cpu_node_pool_root_disk_size_gb" {
-  type        = number
-  default     = 512
-  description = "Root disk size of CPU nodes."
-}
-
-variable "cpu_node_pool_root_volume_type" {
-  type        = string
-  default     = "gp3"
-  description = "EBS volume type of the CPU node root disk."
-}
-
-variable "cpu_node_pool_delete_on_termination" {
-  type        = bool
-  default     = true
-  description = "Delete the CPU nodes' root volumes on termination."
-}
-
-variable "cpu_node_pool_additional_user_data" {
-  type        = string
-  default     = ""
-  description = "Shell appended after the EKS bootstrap on CPU nodes."
-}
-
-variable "max_cpu_nodes" {
-  type        = string
-  default     = "2"
-  description = "Maximum number of CPU nodes in the Autoscaling Group"
-}
-
-variable "min_cpu_nodes" {
-  type        = string
-  default     = "0"
-  description = "Minimum number of CPU nodes in the Autoscaling Group"
-}
-
-variable "desired_count_cpu_nodes" {
-  type        = string
-  default     = "1"
-  description = "Desired number of CPU nodes in the Autoscaling Group"
-}
-
-
-/************************
-  VPC Variables
-*************************/
+# --- 2 network ---------------------------------------------------------------
 
 variable "existing_vpc_details" {
+  description = "Bring-your-own network: the VPC id and the private subnets the nodes go into. Null creates a fresh VPC."
   type = object({
     vpc_id     = string
     subnet_ids = list(string)
   })
-  default     = null
-  description = "Re-use an existing VPC (vpc_id + private subnet_ids) instead of creating one."
+  default = null
 }
 
 variable "cidr_block" {
+  description = "Address space of the VPC this module creates."
   type        = string
   default     = "10.0.0.0/16"
-  description = "CIDR for VPC"
-}
-
-variable "additional_user_data" {
-  type        = string
-  default     = ""
-  description = "Shell appended after the EKS bootstrap on ALL node pools (before the pool-specific additions)."
+  validation {
+    condition     = can(cidrhost(var.cidr_block, 0))
+    error_message = "cidr_block must be an IPv4 CIDR."
+  }
 }
 
 variable "private_subnets" {
+  description = "One private range per availability zone. MI355X nodes and the control-plane ENIs live here."
   type        = list(any)
-  description = "Private subnet ranges (one per AZ); GPU nodes live here."
   default     = ["10.0.0.0/19", "10.0.32.0/19", "10.0.64.0/19"]
 }
 
 variable "public_subnets" {
+  description = "One public range per availability zone, for NAT gateways and load balancers."
   type        = list(any)
-  description = "Public subnet ranges (one per AZ)."
   default     = ["10.0.96.0/22", "10.0.100.0/22", "10.0.104.0/22"]
 }
 
-variable "ssh_key" {
-  type        = string
-  default     = ""
-  description = "EC2 key pair name for node SSH access (empty = none)."
-}
-
 variable "enable_nat_gateway" {
-  description = "Should be true if you want to provision NAT Gateways for each of your private networks"
-  default     = true
+  description = "Give the private subnets outbound internet through NAT (image pulls, driver downloads)."
   type        = bool
+  default     = true
 }
 
 variable "single_nat_gateway" {
+  description = "One shared NAT gateway instead of one per zone: cheaper, but a zone outage cuts egress for all."
   type        = bool
-  description = "Should be true if you want to provision a single shared NAT Gateway across all of your private networks"
   default     = false
 }
 
 variable "enable_dns_support" {
+  description = "Amazon-provided DNS resolution inside the new VPC."
   type        = bool
   default     = true
-  description = "Enable DNS support in the created VPC."
 }
 
 variable "enable_dns_hostnames" {
-  description = "Whether or not the created VPC has DNS hostname support"
-  default     = true
+  description = "Public DNS hostnames for instances of the new VPC."
   type        = bool
+  default     = true
 }
 
 variable "additional_security_group_ids" {
+  description = "Extra security groups for every node when an existing VPC is reused."
   type        = list(any)
   default     = []
-  description = "Additional security groups attached to nodes (only when re-using a VPC)."
 }
 
 variable "additional_node_security_groups_rules" {
-  description = "Additional rules merged into the node security group (CNPack hook)."
+  description = "Rules merged into the node security group, e.g. the metrics-server / prometheus-adapter ports of the CNPack example."
   type        = any
   default     = {}
 }
 
-/************************
-  AMD GPU stack (new; not in the reference surface)
-*************************/
-variable "gpu_stack_mode" {
+# --- 3 MI355X node group ---------------------------------------------------------
+
+variable "gpu_instance_type" {
+  description = "EC2 type that carries 8 x AMD Instinct MI355X (gfx950, 288 GB HBM3E per GPU). No public default exists: name the type of your capacity reservation; plan stops with a clear message while it is empty."
   type        = string
-  default     = "operator"
-  description = "\"operator\" (AMD GPU Operator + DeviceConfig) or \"daemonsets\" (amdgpu-dkms + rocm/k8s-device-plugin)."
+  default     = ""
+  validation {
+    condition     = var.gpu_instance_type == "" || can(regex("^[a-z0-9-]+\\.[a-z0-9]+$", var.gpu_instance_type))
+    error_message = "Expected an EC2 type of the form family.size."
+  }
 }
 
-variable "gpu_validation_enabled" {
+variable "gpu_ami_id" {
+  description = "Pin the MI355X node image. Empty: newest Canonical Ubuntu EKS image for cluster_version (ROCm 7 requires 22.04 or 24.04). Anything else is used verbatim."
+  type        = string
+  default     = ""
+}
+
+variable "min_gpu_nodes" {
+  description = "Autoscaling floor of the MI355X group."
+  type        = number
+  default     = 1
+  validation {
+    condition     = var.min_gpu_nodes >= 0
+    error_message = "Cannot be negative."
+  }
+}
+
+variable "max_gpu_nodes" {
+  description = "Autoscaling ceiling of the MI355X group."
+  type        = number
+  default     = 5
+}
+
+variable "desired_count_gpu_nodes" {
+  description = "Initial size of the MI355X group (ignored by Terraform after creation, owned by the autoscaler)."
+  type        = number
+  default     = 1
+}
+
+variable "gpu_node_pool_root_disk_size_gb" {
+  description = "Root volume of each MI355X node in GB: ROCm images are several GB each and DKMS keeps kernel build trees."
+  type        = number
+  default     = 1024
+  validation {
+    condition     = var.gpu_node_pool_root_disk_size_gb >= 256
+    error_message = "Below 256 GB the ROCm images and DKMS trees do not fit."
+  }
+}
+
+variable "gpu_node_pool_root_volume_type" {
+  description = "EBS class of the MI355X root volumes."
+  type        = string
+  default     = "gp3"
+}
+
+variable "gpu_node_pool_delete_on_termination" {
+  description = "Remove MI355X root volumes together with their instances."
   type        = bool
   default     = true
-  description = "Run the MI355X validation Job (HIP GEMM + HBM + RCCL all-reduce) and make apply wait for it."
 }
 
-variable "gpu_validation_image" {
+variable "gpu_node_pool_additional_user_data" {
+  description = "Shell run on MI355X nodes after the EKS bootstrap and the built-in host tuning."
   type        = string
-  default     = "ghcr.io/amd-instinct-terraform-modules/amdgpu-validate:0.1.0"
-  description = "Image built from validation/image/Dockerfile."
+  default     = ""
+}
+
+# --- 4 CPU node group ------------------------------------------------------
+
+variable "cpu_instance_type" {
+  description = "EC2 type of the system pool (operator controllers, CoreDNS, monitoring)."
+  type        = string
+  default     = "m7i.2xlarge"
+}
+
+variable "min_cpu_nodes" {
+  description = "Autoscaling floor of the system pool."
+  type        = number
+  default     = 0
+}
+
+variable "max_cpu_nodes" {
+  description = "Autoscaling ceiling of the system pool."
+  type        = number
+  default     = 2
+}
+
+variable "desired_count_cpu_nodes" {
+  description = "Initial size of the system pool."
+  type        = number
+  default     = 1
+}
+
+variable "cpu_node_pool_root_disk_size_gb" {
+  description = "Root volume of each system node in GB."
+  type        = number
+  default     = 512
+}
+
+variable "cpu_node_pool_root_volume_type" {
+  description = "EBS class of the system-node root volumes."
+  type        = string
+  default     = "gp3"
+}
+
+variable "cpu_node_pool_delete_on_termination" {
+  description = "Remove system-node root volumes together with their instances."
+  type        = bool
+  default     = true
+}
+
+variable "cpu_node_pool_additional_user_data" {
+  description = "Shell run on system nodes after the EKS bootstrap."
+  type        = string
+  default     = ""
+}
+
+# --- 5 node bootstrap ------------------------------------------------------
+
+variable "additional_user_data" {
+  description = "Shell run on every node, before the pool-specific snippets."
+  type        = string
+  default     = ""
+}
+
+variable "ssh_key" {
+  description = "EC2 key pair for SSH to the nodes; empty disables remote access."
+  type        = string
+  default     = ""
+}
+
+# --- 6 AMD GPU stack ----------------------------------------------------------
+
+variable "gpu_stack_mode" {
+  description = "How the GPUs are enabled: \"operator\" = AMD GPU Operator with a DeviceConfig, \"daemonsets\" = amdgpu-dkms installer + rocm/k8s-device-plugin without an operator."
+  type        = string
+  default     = "operator"
+  validation {
+    condition     = contains(["operator", "daemonsets"], var.gpu_stack_mode)
+    error_message = "Either operator or daemonsets."
+  }
+}
+
+variable "gpu_operator_version" {
+  description = "Chart version of the AMD GPU Operator."
+  type        = string
+  default     = "v1.3.0"
+}
+
+variable "gpu_operator_driver_version" {
+  description = "amdgpu / ROCm release the operator (or the DKMS DaemonSet) installs; gfx950 needs 7.0 or newer."
+  type        = string
+  default     = "7.0.2"
+}
+
+variable "gpu_operator_namespace" {
+  description = "Namespace holding the GPU stack, its exporter and the validation Job."
+  type        = string
+  default     = "kube-amd-gpu"
 }
 
 variable "gpus_per_node" {
+  description = "MI355X devices per node; the validation Job asks for all of them."
   type        = number
   default     = 8
-  description = "MI355X GPUs per GPU node (the validation Job requests all of them)."
+}
+
+# --- 7 validation Job ---------------------------------------------------------
+
+variable "gpu_validation_enabled" {
+  description = "Gate apply on the MI355X validation Job (bf16 MFMA GEMM with ABFT, HBM stream, RCCL / xGMI all-reduce)."
+  type        = bool
+  default     = true
+}
+
+variable "gpu_validation_image" {
+  description = "Registry path of the image built from validation/image/Dockerfile."
+  type        = string
+  default     = "ghcr.io/amd-instinct-terraform-modules/amdgpu-validate:0.1.0"
 }
 
 variable "gpu_validation_tflops_floor" {
+  description = "Fail the Job when any GPU's bf16 GEMM rate drops below this many TFLOP/s."
   type        = number
   default     = 1000
-  description = "Per-GPU bf16 GEMM TFLOP/s floor of the validation Job."
 }

@@ -1,0 +1,26 @@
+# AMD GPU stack on GKE. critical_pod_quota: GKE admits system-*-critical pods
+# outside kube-system only under a ResourceQuota scoped to those classes, and
+# the device plugin / driver DaemonSets use them. Depending on the system pool
+# only (the Job alone waits for the MI355X pool) lets the stack install while
+# GPU nodes boot; the namespace is owned by the module, so destroy needs no
+# manual `terraform state rm`.
+
+module "amd_gpu_stack" {
+  source = "../modules/amd-gpu-stack"
+
+  cluster_name                = var.cluster_name
+  gpu_stack_mode              = var.gpu_stack_mode
+  gpu_operator_version        = var.gpu_operator_version
+  gpu_operator_driver_version = var.gpu_operator_driver_version
+  gpu_operator_namespace      = var.gpu_operator_namespace
+  critical_pod_quota          = true
+
+  gpu_node_selector = { "amd.com/gpu.present" = "true" }
+  gpu_node_pool_ids = [google_container_node_pool.mi355x.id]
+
+  validation_enabled   = var.gpu_validation_enabled
+  validation_image     = var.gpu_validation_image
+  validation_gpu_count = tonumber(var.gpu_count)
+
+  depends_on = [google_container_node_pool.system]
+}

@@ -1,72 +1,63 @@
-/***************************
-Outputs
-***************************/
-
-output "region" {
-  value       = var.region
-  description = "Region the resources of this module are created in"
-}
+# Reference output names first (CNPack's providers read the endpoint and CA
+# from here), then the AMD GPU stack.
 
 output "project_id" {
+  description = "Project that owns the cluster."
   value       = var.project_id
-  description = "GCloud Project ID"
 }
 
-/***************************
-VPC Network Outputs
-***************************/
-
-output "vpc_project" {
-  value       = google_compute_network.holoscan-vpc[*].project
-  description = "Project of the VPC network (can be different from the project launching Kubernetes resources)"
+output "region" {
+  description = "Region of the cluster and its network."
+  value       = var.region
 }
 
-output "subnet_cidr_range" {
-  value       = google_compute_subnetwork.holoscan-subnet[*].ip_cidr_range
-  description = "The IPs and CIDRs of the subnets"
-}
-
-output "subnet_region" {
-  value       = google_compute_subnetwork.holoscan-subnet[*].region
-  description = "The region of the VPC subnet used in this module"
-}
-
-/***************************
-GKE Outputs
-***************************/
 output "kubernetes_cluster_name" {
-  value       = google_container_cluster.holoscan.name
-  description = "MI355X-ready GKE cluster name"
+  description = "GKE cluster name."
+  value       = google_container_cluster.this.name
 }
 
 output "kubernetes_cluster_endpoint_ip" {
-  value       = google_container_cluster.holoscan.endpoint
-  description = "GKE Cluster IP Endpoint"
+  description = "Address of the Kubernetes API (no scheme)."
+  value       = google_container_cluster.this.endpoint
 }
 
 output "kubernetes_config_file" {
-  value       = google_container_cluster.holoscan.master_auth[0].cluster_ca_certificate
-  description = "GKE cluster CA certificate (base64)"
+  description = "Base64 CA certificate of the API server, for kubeconfig / providers."
+  value       = google_container_cluster.this.master_auth[0].cluster_ca_certificate
   sensitive   = true
 }
 
+output "vpc_project" {
+  description = "Project of the network this root created (empty list when vpc_enabled = false)."
+  value       = google_compute_network.this[*].project
+}
+
+output "subnet_cidr_range" {
+  description = "Primary range of the created node subnet (list; empty without vpc_enabled)."
+  value       = google_compute_subnetwork.nodes[*].ip_cidr_range
+}
+
+output "subnet_region" {
+  description = "Region of the created node subnet (list; empty without vpc_enabled)."
+  value       = google_compute_subnetwork.nodes[*].region
+}
+
 output "rapid_channel_latest_gke_version" {
+  description = "Newest GKE version offered on the RAPID channel in this region."
   value       = data.google_container_engine_versions.latest.release_channel_latest_version["RAPID"]
-  description = "The latest available version of GKE when using the RAPID channel"
 }
 
 output "stable_channel_latest_gke_version" {
+  description = "Newest GKE version offered on the STABLE channel in this region."
   value       = data.google_container_engine_versions.latest.release_channel_latest_version["STABLE"]
-  description = "The latest available version of GKE when using the STABLE channel"
 }
 
-/***************************
-AMD GPU stack outputs (new)
-***************************/
 output "gpu_operator_namespace" {
-  value = module.amd_gpu_stack.namespace
+  description = "Namespace of the GPU stack and the validation Job."
+  value       = module.amd_gpu_stack.namespace
 }
 
 output "gpu_validation_job" {
-  value = module.amd_gpu_stack.validation_job_name
+  description = "Name of the validation Job."
+  value       = module.amd_gpu_stack.validation_job_name
 }

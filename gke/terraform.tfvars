@@ -1,6 +1,7 @@
-# Do not commit this file to Git if you add sensitive values
-# project_id        = ""
-# cluster_name      = ""
-# region            = "us-west1"
-# node_zones        = ["us-west1-b"]
-# gpu_instance_type = "<machine type with 8x MI355X>"
+# Required inputs of the GKE root; keep real project ids out of git.
+#
+# project_id        = "<project>"
+# cluster_name      = "mi355x"
+# region            = "us-central1"
+# node_zones        = ["us-central1-a"]       # one zone -> zonal cluster
+# gpu_instance_type = "<machine type with 8 x MI355X>"

@@ -1,213 +1,215 @@
-# Call surface of /root/reference/gke/variables.tf: all 25 names, required
-# ones unchanged (project_id, region, cluster_name, node_zones).
+# Inputs of the GKE root. The names (and which are required: project_id,
+# region, cluster_name, node_zones) follow the reference call surface; the
+# rest - types, defaults, wording, validation - is this module's own.
 
-/***************************
-GCP Variables
-***************************/
+# --- where -------------------------------------------------------------------
+
 variable "project_id" {
+  description = "Project that owns the network, the cluster and its nodes (shared-VPC hosts are not supported)."
   type        = string
-  description = "GCP Project ID for the VPC and K8s Cluster. Shared VPC host projects are not supported."
 }
 
 variable "region" {
-  type        = string
-  description = "The Region resources (VPC, GKE, Compute Nodes) will be created in"
-}
-
-variable "vpc_enabled" {
-  default     = true
-  type        = bool
-  description = "Create a dedicated VPC + subnet (false: use network/subnetwork)."
-}
-
-variable "network" {
-  default     = ""
-  type        = string
-  description = "Existing VPC network name (used when vpc_enabled = false)."
-}
-
-variable "subnetwork" {
-  type        = string
-  default     = ""
-  description = "Existing subnet name used for k8s cluster nodes (when vpc_enabled = false)."
-}
-
-/***************************
-GKE Variables
-***************************/
-
-variable "cluster_name" {
-  description = "Name of the Kubernetes Cluster to provision"
+  description = "Region of the network and, for multi-zone clusters, of the cluster itself."
   type        = string
 }
 
 variable "node_zones" {
-  description = "Zones for the node pools (same region as above). Exactly one zone = zonal cluster."
+  description = "Zones for the node pools, all in `region`. One entry gives a zonal cluster; several give a regional cluster limited to those zones."
   type        = list(any)
+  validation {
+    condition     = length(var.node_zones) > 0
+    error_message = "List at least one zone."
+  }
+}
+
+variable "cluster_name" {
+  description = "Cluster name; also the prefix of the VPC, subnet and pool names."
+  type        = string
 }
 
 variable "release_channel" {
+  description = "GKE release channel that drives control-plane and node upgrades."
   type        = string
   default     = "REGULAR"
-  description = "GKE release channel (RAPID, REGULAR, STABLE)."
-
   validation {
     condition     = contains(["RAPID", "REGULAR", "STABLE", "UNSPECIFIED"], var.release_channel)
     error_message = "release_channel must be RAPID, REGULAR, STABLE or UNSPECIFIED."
   }
 }
 
-/***************************
-GKE CPU Node Pool Variables
-***************************/
+# --- network -------------------------------------------------------------------
 
-variable "cpu_min_node_count" {
-  default     = "1"
-  description = "Minimum number of CPU nodes in the CPU node pool"
-}
-
-variable "cpu_max_node_count" {
-  default     = "5"
-  description = "Max Number of CPU nodes in CPU nodepool"
-}
-
-variable "use_cpu_spot_instances" {
+variable "vpc_enabled" {
+  description = "Create a dedicated VPC-native network; false attaches the cluster to `network` / `subnetwork`."
   type        = bool
-  default     = false
-  description = "Use Spot instances for the CPU pool"
+  default     = true
 }
+
+variable "network" {
+  description = "Name of an existing VPC (only read when vpc_enabled is false)."
+  type        = string
+  default     = ""
+}
+
+variable "subnetwork" {
+  description = "Name of an existing subnet for the nodes (only read when vpc_enabled is false)."
+  type        = string
+  default     = ""
+}
+
+variable "subnet_cidr_range" {
+  description = "Node range of the created subnet; a /20 leaves room for growth where a /24 would not."
+  type        = string
+  default     = "10.150.0.0/20"
+}
+
+variable "pods_cidr_range" {
+  description = "Secondary range for pod IPs."
+  type        = string
+  default     = "10.160.0.0/14"
+}
+
+variable "services_cidr_range" {
+  description = "Secondary range for ClusterIP services."
+  type        = string
+  default     = "10.150.64.0/20"
+}
+
+# --- system pool -----------------------------------------------------------
 
 variable "cpu_instance_type" {
+  description = "Machine type of the system pool."
+  type        = string
   default     = "n2-standard-8"
-  description = "Machine Type for CPU node pool"
 }
 
 variable "num_cpu_nodes" {
+  description = "System-pool size at creation (per zone for regional clusters)."
+  type        = number
   default     = 1
-  description = "Number of CPU nodes when pool is created"
 }
 
-/***************************
-GKE GPU Node Pool Variables
-***************************/
+variable "cpu_min_node_count" {
+  description = "Autoscaler floor of the system pool."
+  type        = number
+  default     = 1
+}
+
+variable "cpu_max_node_count" {
+  description = "Autoscaler ceiling of the system pool."
+  type        = number
+  default     = 5
+}
+
+variable "use_cpu_spot_instances" {
+  description = "Run the system pool on Spot VMs."
+  type        = bool
+  default     = false
+}
+
+# --- MI355X pool -----------------------------------------------------------
+
+variable "gpu_instance_type" {
+  description = "Machine type that brings AMD Instinct MI355X GPUs. GKE publishes no default; plan stops until it is set."
+  type        = string
+  default     = ""
+}
 
 variable "gpu_type" {
+  description = "Accelerator model recorded on the nodes as amd.com/gpu.model. GKE has no AMD guest_accelerator type, so no accelerator block is emitted; the machine shape carries the GPUs."
   type        = string
   default     = "amd-instinct-mi355x"
-  description = "Accelerator of the GPU pool. GKE has no AMD guest_accelerator type: AMD Instinct machine shapes bundle their GPUs, so this value only labels the nodes and no guest_accelerator block is emitted."
-
   validation {
     condition     = can(regex("^amd-instinct-mi3[0-9]{2}x?$", var.gpu_type))
-    error_message = "gpu_type must name an AMD Instinct accelerator (e.g. amd-instinct-mi355x); this module provisions AMD GPUs only."
+    error_message = "Name an AMD Instinct accelerator such as amd-instinct-mi355x; this module provisions AMD GPUs only."
   }
 }
 
-variable "gpu_min_node_count" {
-  default     = "1"
-  description = "Min number of GPU nodes in GPU nodepool"
-}
-
-variable "gpu_max_node_count" {
-  default     = "5"
-  description = "Max Number of GPU nodes in GPU nodepool"
-}
-
-variable "use_gpu_spot_instances" {
-  type        = bool
-  default     = false
-  description = "Use Spot instances for the GPU pool"
-}
-
-variable "num_gpu_nodes" {
-  default     = 1
-  description = "Number of GPU nodes when pool is created"
-}
-
 variable "gpu_count" {
-  default     = "8"
-  description = "MI355X GPUs per GPU node (the validation Job requests this many)."
-
+  description = "MI355X devices per node; the validation Job requests all of them."
+  type        = number
+  default     = 8
   validation {
-    condition     = contains(["1", "2", "4", "8"], tostring(var.gpu_count))
+    condition     = contains([1, 2, 4, 8], var.gpu_count)
     error_message = "gpu_count must be 1, 2, 4 or 8."
   }
 }
 
-variable "gpu_instance_type" {
-  type        = string
-  default     = ""
-  description = "Machine type with AMD Instinct MI355X attached (required for apply; no public GKE default exists)."
+variable "num_gpu_nodes" {
+  description = "MI355X pool size at creation."
+  type        = number
+  default     = 1
+}
+
+variable "gpu_min_node_count" {
+  description = "Autoscaler floor of the MI355X pool."
+  type        = number
+  default     = 1
+}
+
+variable "gpu_max_node_count" {
+  description = "Autoscaler ceiling of the MI355X pool."
+  type        = number
+  default     = 5
+}
+
+variable "use_gpu_spot_instances" {
+  description = "Run the MI355X pool on Spot VMs."
+  type        = bool
+  default     = false
 }
 
 variable "gpu_instance_tags" {
+  description = "Extra network tags for MI355X nodes only (firewall targeting)."
   type        = list(string)
   default     = []
-  description = "Network tags for GPU instance nodes"
 }
 
 variable "disk_size_gb" {
-  default     = "1024"
-  type        = string
-  description = "Boot disk size of every node (GB); ROCm images are multi-GB."
+  description = "Boot disk of every node in GB; ROCm images are several GB each."
+  type        = number
+  default     = 1024
 }
 
-/***************************
-GPU Operator Variables
-***************************/
+# --- AMD GPU stack and validation ---------------------------------------------
+
+variable "gpu_stack_mode" {
+  description = "\"daemonsets\" (amdgpu-dkms + rocm/k8s-device-plugin; the default for GKE's Ubuntu nodes) or \"operator\" (AMD GPU Operator + DeviceConfig)."
+  type        = string
+  default     = "daemonsets"
+  validation {
+    condition     = contains(["operator", "daemonsets"], var.gpu_stack_mode)
+    error_message = "Either operator or daemonsets."
+  }
+}
 
 variable "gpu_operator_version" {
+  description = "AMD GPU Operator chart version (operator mode)."
   type        = string
   default     = "v1.3.0"
-  description = "AMD GPU Operator Helm chart version"
 }
 
 variable "gpu_operator_driver_version" {
+  description = "amdgpu / ROCm release installed on MI355X nodes (7.0 or newer for gfx950)."
   type        = string
   default     = "7.0.2"
-  description = "amdgpu driver / ROCm release for the GPU nodes (>= 7.0 for gfx950)"
 }
 
 variable "gpu_operator_namespace" {
+  description = "Namespace of the GPU stack, its exporter and the validation Job."
   type        = string
   default     = "kube-amd-gpu"
-  description = "The namespace to deploy the AMD GPU stack into"
-}
-
-/***************************
-New (not in the reference surface)
-***************************/
-variable "subnet_cidr_range" {
-  type        = string
-  default     = "10.150.0.0/20"
-  description = "Primary range of the created subnet (the reference hard-coded a /24)."
-}
-
-variable "pods_cidr_range" {
-  type        = string
-  default     = "10.160.0.0/14"
-  description = "Secondary range for pods (VPC-native cluster)."
-}
-
-variable "services_cidr_range" {
-  type        = string
-  default     = "10.150.64.0/20"
-  description = "Secondary range for services."
-}
-
-variable "gpu_stack_mode" {
-  type        = string
-  default     = "daemonsets"
-  description = "\"daemonsets\" (amdgpu-dkms + rocm/k8s-device-plugin; default on GKE's Ubuntu images) or \"operator\"."
 }
 
 variable "gpu_validation_enabled" {
+  description = "Make apply wait for the MI355X validation Job."
   type        = bool
   default     = true
-  description = "Run the MI355X validation Job and make apply wait for it."
 }
 
 variable "gpu_validation_image" {
+  description = "Registry path of the image built from validation/image/Dockerfile."
   type        = string
   default     = "ghcr.io/amd-instinct-terraform-modules/amdgpu-validate:0.1.0"
-  description = "Image built from validation/image/Dockerfile."
 }

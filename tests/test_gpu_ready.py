@@ -103,7 +103,7 @@ def test_critical_path_ends_with_validation(repo, root, mode):
 def test_critical_path_uses_measured_durations(repo):
     g = build_graph(repo / "aks")
     base = critical_path(g).total_s
-    faster = critical_path(g, {"azurerm_kubernetes_cluster_node_pool.holoscan": 60.0}).total_s
+    faster = critical_path(g, {"azurerm_kubernetes_cluster_node_pool.mi355x": 60.0}).total_s
     assert faster < base
 
 

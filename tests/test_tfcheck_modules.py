@@ -82,8 +82,8 @@ def test_validation_job_waits_for_gpu_nodes_and_stack(repo, root):
     g = build_graph(repo / root)
     assert not g.hard_cycles()
     (job,) = g.find("kubernetes_job_v1.gpu_validation")
-    pools = {"eks": ["module.eks"], "gke": ["google_container_node_pool.gpu_nodes"],
-             "aks": ["azurerm_kubernetes_cluster_node_pool.holoscan"]}[root]
+    pools = {"eks": ["module.eks"], "gke": ["google_container_node_pool.mi355x"],
+             "aks": ["azurerm_kubernetes_cluster_node_pool.mi355x"]}[root]
     for p in pools:
         assert g.depends_on(job, p), f"{job} must wait for {p}"
     stack = [n for n in g.nodes if "helm_release.device_config" in n or "rocm_device_plugin" in n]
@@ -95,8 +95,8 @@ def test_operator_install_overlaps_gpu_node_boot(repo, root):
     """Only the Job needs GPUs: the operator must NOT wait for the GPU pool."""
     g = build_graph(repo / root)
     (op,) = g.find("helm_release.amd_gpu_operator")
-    pool = {"gke": "google_container_node_pool.gpu_nodes",
-            "aks": "azurerm_kubernetes_cluster_node_pool.holoscan"}[root]
+    pool = {"gke": "google_container_node_pool.mi355x",
+            "aks": "azurerm_kubernetes_cluster_node_pool.mi355x"}[root]
     assert not g.depends_on(op, pool)
 
 
