@@ -1,11 +1,7 @@
-// Cluster Variables
-# cluster_name           = "cnpack-mi355x"
-# location               = "West US 2"
-# admin_group_object_ids = []
-# gpu_machine_type       = "<Azure VM size with 8x MI355X>"
-
-// Fluentbit/Azure Log Configuration Variables
-# fluentbit-workspace-name = "fluentbit-test"
-
-// Prometheus/Azure Monitor Configuration Variables
-# prometheus-name = "cnpack-prometheus"
+# Required before apply:
+# cluster_name             = "cnpack-mi355x"
+# location                 = "westus3"
+# admin_group_object_ids   = ["<Entra ID group object id>"]
+# gpu_machine_type         = "<VM size with 8 x MI355X>"
+# prometheus-name          = "cnpack-prometheus"
+# fluentbit-workspace-name = "cnpack-fluentbit"

@@ -1,77 +1,62 @@
-/****************************
-Azure Variables
-****************************/
-variable "location" {
-  type        = string
-  description = "The region to create resources in (can be set in terraform.tfvars)"
-}
+# Inputs of the AKS CNPack example (upstream names, own wording).
 
-variable "az_monitor-user-managed-id" {
-  type        = string
-  default     = "tf-amd-monitor-identity"
-  description = "Name of the user-assigned managed identity created for Azure Monitor remote-write (granted Monitoring Metrics Publisher on the workspace's data collection rule)."
-}
-
-/****************************
-Active Directory Variables
-****************************/
-variable "admin_group_object_ids" {
-  type        = list(any)
-  description = <<EOH
-  (Required) A list of Object IDs (GUIDs) of Azure Active Directory Groups which should have Owner Role on the Cluster.
-  This is not the email address of the group, the GUID can be found in the Azure panel by searching for the AD Group
-  NOTE: You will need Azure "Owner" role (not "Contributor") to attach an AD role to the Kubernetes cluster.
-  EOH
-}
-
-/*******************************************
-Cluster Variables
-*******************************************/
 variable "cluster_name" {
+  description = "Name handed to the AKS root module."
   type        = string
-  description = "Name of the cluster"
+}
+
+variable "location" {
+  description = "Azure region of the cluster and its resource group."
+  type        = string
+}
+
+variable "admin_group_object_ids" {
+  description = "Object ids of the Entra ID groups that administer the cluster (GUIDs; requires the Owner role to assign)."
+  type        = list(any)
 }
 
 variable "gpu_machine_type" {
+  description = "VM size with 8 x AMD Instinct MI355X, handed to the root module."
   type        = string
   default     = ""
-  description = "Azure VM size with 8x AMD Instinct MI355X."
 }
 
-/*******************************************
-Fluentbit (Azure Logging) Variables
-*******************************************/
+variable "prometheus-name" {
+  description = "Name of the Azure Monitor (managed Prometheus) workspace."
+  type        = string
+}
+
+variable "prometheus_resource_group_name" {
+  description = "Resource group for the monitor workspace; empty uses the cluster's node resource group."
+  type        = string
+  default     = ""
+}
+
+variable "az_monitor-user-managed-id" {
+  description = "Name of the user-assigned identity Prometheus uses for remote_write."
+  type        = string
+  default     = "tf-amd-monitor-identity"
+}
+
 variable "fluentbit_enabled" {
+  description = "Create the Log Analytics workspace and the Fluent Bit secret."
   type        = bool
   default     = true
-  description = "Create the Log Analytics workspace and the fluentbit secret (was declared but ignored in the reference)"
 }
 
 variable "fluentbit-workspace-name" {
-  description = "Name of the Azure Log Workspace for Fluentbit to be created"
+  description = "Name of the Log Analytics workspace for Fluent Bit."
   type        = string
 }
 
 variable "azure_log_analytics_sku" {
-  description = "SKU of the Log Analytics Workspace (Free, PerNode, Premium, Standard, Standalone, Unlimited, CapacityReservation, PerGB2018)."
+  description = "Pricing tier of the Log Analytics workspace."
+  type        = string
   default     = "PerGB2018"
 }
 
 variable "azure_log_analytics_retention_in_days" {
+  description = "Days of log retention (7 on the Free tier, otherwise 30-730)."
+  type        = number
   default     = 30
-  description = "Workspace data retention in days (7 on Free, else 30-730)"
-}
-
-/*******************************************
-Prometheus (Azure Monitor) Variables
-*******************************************/
-variable "prometheus_resource_group_name" {
-  type        = string
-  default     = ""
-  description = "Resource group for the Azure Monitor workspace (empty = the cluster's node resource group)."
-}
-
-variable "prometheus-name" {
-  type        = string
-  description = "The name of the Azure Monitor Workspace for Prometheus"
 }

@@ -1,67 +1,48 @@
-/*******************************************
-Cluster Variables
-*******************************************/
+# Inputs of the EKS CNPack example: the upstream example's names, own wording.
+
 variable "cluster_name" {
+  description = "Name handed to the EKS root module."
   type        = string
-  description = "Name of the cluster"
 }
 
-/*******************************************
-AWS Managed Prometheus Variables
-*******************************************/
+variable "gpu_instance_type" {
+  description = "EC2 type with 8 x AMD Instinct MI355X, handed to the root module."
+  type        = string
+  default     = ""
+}
+
 variable "amp_enabled" {
+  description = "Create the Managed Prometheus workspace, its log group and ingest identities."
   type        = bool
   default     = true
-  description = "Set to true to enable, false to disable"
 }
 
-/*******************************************
-AWS Private Certificate Authority Variables
-*******************************************/
 variable "pca_enabled" {
+  description = "Create the private root CA and the node policy cert-manager needs."
   type        = bool
   default     = true
-  description = "Set to true to enable, false to disable"
 }
 
 variable "common_name" {
+  description = "Subject CN of the private root CA."
   type        = string
   default     = "cluster.local"
-  description = "Common Name for PCA Creation"
 }
 
-/*******************************************
-AWS Fluentbit Variables
-*******************************************/
 variable "fluentbit_enabled" {
+  description = "Grant the node roles CloudWatch agent permissions for Fluent Bit."
   type        = bool
   default     = true
-  description = "Set to true to enable, false to disable"
 }
 
-/*******************************************
-Prometheus Adapter Variables
-*******************************************/
-variable "prom_adapter_enabled" {
-  type        = bool
-  default     = true
-  description = "Set to true to enable the network support for Prometheus Adapter, false to disable"
-}
-
-/*******************************************
-Metrics Server Variables
-*******************************************/
 variable "metrics_server_enabled" {
+  description = "Open the API-server-to-node path of the metrics-server (TCP 4443)."
   type        = bool
   default     = true
-  description = "Set to true to enable the network support for Metrics Server, false to disable"
 }
 
-/*******************************************
-MI355X node pool (new; passed through to the root module)
-*******************************************/
-variable "gpu_instance_type" {
-  type        = string
-  default     = ""
-  description = "EC2 instance type with 8x AMD Instinct MI355X."
+variable "prom_adapter_enabled" {
+  description = "Open the API-server-to-node path of the prometheus-adapter (TCP 6443)."
+  type        = bool
+  default     = true
 }

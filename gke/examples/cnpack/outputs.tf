@@ -1,10 +1,9 @@
-/*******************************************
-CNPack-equivalent Example Outputs
-*******************************************/
 output "gcp_service_account_email_for_prometheus" {
-  value = var.gke_managed_prometheus_enabled ? google_service_account.prometheus_service_account[0].email : null
+  description = "Annotate the Prometheus KSA with this (iam.gke.io/gcp-service-account); null when disabled."
+  value       = var.gke_managed_prometheus_enabled ? google_service_account.prometheus["gmp"].email : null
 }
 
 output "gpu_validation_job" {
-  value = module.holoscan-ready-gke.gpu_validation_job
+  description = "Validation Job of the cluster's AMD GPU stack."
+  value       = module.mi355x_gke.gpu_validation_job
 }

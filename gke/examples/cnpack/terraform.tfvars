@@ -1,5 +1,7 @@
-cluster_name                   = ""
+# Fill in before applying (project_id and cluster_name have no defaults).
+project_id   = ""
+cluster_name = ""
+region       = "us-central1"
+node_zones   = ["us-central1-a"]
+
 gke_managed_prometheus_enabled = true
-node_zones                     = ["us-west1-b"]
-project_id                     = ""
-region                         = "us-west1"

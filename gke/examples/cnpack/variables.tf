@@ -1,40 +1,33 @@
-/***************************
-GCP Variables
-***************************/
+# Inputs of the GKE CNPack example (upstream names, own wording).
+
 variable "project_id" {
+  description = "Project for the cluster and the Prometheus service account."
   type        = string
-  description = "GCP Project ID for the VPC and K8s Cluster. Shared VPC host projects are not supported."
 }
 
 variable "region" {
-  type        = string
-  description = "The Region resources (VPC, GKE, Compute Nodes) will be created in"
-}
-
-/***************************
-GKE Variables
-***************************/
-variable "cluster_name" {
-  description = "Name of the Kubernetes Cluster to provision"
+  description = "Region of the cluster."
   type        = string
 }
 
 variable "node_zones" {
-  description = "Zones for the node pools (must be in the region above)"
+  description = "Node zones inside `region` (one zone gives a zonal cluster)."
   type        = list(string)
 }
 
-variable "gpu_instance_type" {
+variable "cluster_name" {
+  description = "Name handed to the GKE root module."
   type        = string
-  default     = ""
-  description = "Machine type with AMD Instinct MI355X attached."
 }
 
-/*******************************************
-GCP Managed Prometheus Variables
-*******************************************/
+variable "gpu_instance_type" {
+  description = "Machine type with AMD Instinct MI355X, handed to the root module."
+  type        = string
+  default     = ""
+}
+
 variable "gke_managed_prometheus_enabled" {
+  description = "Create the Managed Prometheus writer identity for the in-cluster Prometheus."
   type        = bool
   default     = true
-  description = "Set to true to enable, false to disable"
 }

@@ -69,10 +69,10 @@ def test_k8s_events_override_allocatable():
 
 
 def test_errored_resource_is_flagged():
-    lines = SYNTH_APPLY[:3] + [_ev("apply_start", "google_container_cluster.holoscan", "2025-01-17T10:03:00Z"),
-                               _ev("apply_errored", "google_container_cluster.holoscan", "2025-01-17T10:04:00Z")]
+    lines = SYNTH_APPLY[:3] + [_ev("apply_start", "google_container_cluster.this", "2025-01-17T10:03:00Z"),
+                               _ev("apply_errored", "google_container_cluster.this", "2025-01-17T10:04:00Z")]
     res = {r["address"]: r for r in parse_apply_json(lines)}
-    assert res["google_container_cluster.holoscan"]["errored"]
+    assert res["google_container_cluster.this"]["errored"]
 
 
 def test_phase_clock_monotone():
