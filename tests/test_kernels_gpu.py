@@ -184,15 +184,16 @@ def test_abft_detects_corruption(ops):
     assert not ops.abft_check(a, b, c3, rs).ok
 
 
-@pytest.mark.parametrize("variant", ["pingpong8", "pingpong8b", "pingpong8c"])
+@pytest.mark.parametrize("variant", ["pingpong8", "pingpong8b", "pingpong8c", "pingpong8p"])
 @pytest.mark.parametrize("m,n,k", [(256, 256, 128), (512, 256, 192), (256, 512, 256),
                                    (768, 1024, 320), (1024, 768, 2048), (2048, 2048, 4096),
-                                   (512, 512, 384)])
+                                   (512, 512, 384), (4096, 4352, 256), (8192, 8192, 512)])
 def test_gemm_variants_vs_torch_fp32(ops, variant, m, n, k):
     """Every 8-wave schedule, including K-tile counts T = 2..6 that exercise
-    each prologue/tail path (T = K / 64; pingpong8c needs T even)."""
-    if variant == "pingpong8c" and (k // 64) % 2:
-        pytest.skip("pingpong8c needs K % 128 == 0")
+    each prologue/tail path (T = K / 64; pingpong8c/8p need T even) and, for
+    the persistent pingpong8p, 1..4 tiles per workgroup (272 / 1024 tiles)."""
+    if variant in ("pingpong8c", "pingpong8p") and (k // 64) % 2:
+        pytest.skip(f"{variant} needs K % 128 == 0")
     a = _rand(ops, (m, k), 71 + k)
     b = _rand(ops, (n, k), 73 + n)
     c = ops.gemm_bf16(a, b, variant=variant)

@@ -22,7 +22,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from nvidia_terraform_modules_amd import ops  # noqa: E402
 
 SHAPES = [(256, 256, 128), (256, 512, 256), (512, 768, 384), (2304, 1536, 640),
-          (4096, 4096, 4096), (8192, 8192, 8192)]
+          (4096, 4352, 512), (4096, 4096, 4096), (8192, 8192, 8192)]
 
 
 def main():

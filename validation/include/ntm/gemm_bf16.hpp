@@ -197,11 +197,11 @@ __device__ __forceinline__ void phase(const Ctx& c, Frags& f,
 }
 
 // Block -> output tile. Bijective XCD remap (nwg % 8 != 0 safe), then a
-// GROUP_M raster inside each XCD's contiguous chunk.
+// GROUP_M raster inside each XCD's contiguous chunk. `bid` is the virtual
+// block id (blockIdx.x, or a persistent kernel's tile index) out of `nwg`.
 template <int GROUP_M = kGroupM>
-__device__ __forceinline__ void tile_coords(int M, int N, int& tm, int& tn) {
-  const int nwg = gridDim.x;
-  const int bid = blockIdx.x;
+__device__ __forceinline__ void tile_coords_of(int bid, int nwg, int M, int N,
+                                               int& tm, int& tn) {
   const int xcd = bid & 7;
   const int q = nwg >> 3, r = nwg & 7;
   const int wgid =
@@ -214,6 +214,11 @@ __device__ __forceinline__ void tile_coords(int M, int N, int& tm, int& tn) {
   const int in_group = wgid - gid * group;
   tm = first_m + in_group % gsz;
   tn = in_group / gsz;
+}
+
+template <int GROUP_M = kGroupM>
+__device__ __forceinline__ void tile_coords(int M, int N, int& tm, int& tn) {
+  tile_coords_of<GROUP_M>((int)blockIdx.x, (int)gridDim.x, M, N, tm, tn);
 }
 
 // Epilogue shared by the K1 kernels: bf16 RNE stores (8 B per lane per

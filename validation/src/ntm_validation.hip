@@ -8,6 +8,7 @@
 #include "ntm/gemm_bf16.hpp"
 #include "ntm/gemm_bf16_pp2.hpp"
 #include "ntm/gemm_bf16_pp3.hpp"
+#include "ntm/gemm_bf16_pp4.hpp"
 #include "ntm/gemm_bf16_w4.hpp"
 
 #define NTM_API extern "C" __attribute__((visibility("default")))
@@ -33,13 +34,16 @@ NTM_API int ntm_gemm_shape_ok(int M, int N, int K) {
 // per wave (gemm_bf16_w4.hpp) with prefetch distance 3 / 4 k-steps; 4 = the
 // 8-wave kernel with the balanced 8/4/8/4 read schedule (gemm_bf16_pp2.hpp);
 // 5 = the same schedule with parity-alternating B buffers and a uniform,
-// tail-free K loop (gemm_bf16_pp3.hpp; K % 128 == 0).
+// tail-free K loop (gemm_bf16_pp3.hpp; K % 128 == 0); 6 = 5 made persistent
+// (one WG per CU, DMA pipeline across tiles; gemm_bf16_pp4.hpp).
 // 0 = default: the fastest measured variant whose shape rules admit (M,N,K).
 // Measured on MI355X (tools/gemm_check.py, random bf16, median of 7 rounds,
 // profiles/r1_pp3/):
 //   8192^3: 5 1567 TF, 4 1530, 1 1521, 2 ~1310-1380; hipBLASLt 1667
 //   4096^3: 5 1479 TF, 4 1435, 1 1424;               hipBLASLt 1562
 // then variant 5 without s_setprio: +1.3-1.7 % (profiles/r1_pp3_knobs).
+// Variant 6 (persistent 5) is correct and race-free but measured no faster
+// (8192^3 1586 vs 1594, 4096^3 1512 vs 1509; profiles/r1_pp4): not default.
 // Variants 4 and 5 pass tools/race_screen.py (bitwise-stable under HBM noise).
 // Default: 5 when K % 128 == 0, else 4 (both need K % 64 == 0, K >= 128).
 constexpr int kDefaultVariant = 5;
@@ -66,7 +70,7 @@ NTM_API int ntm_gemm_bf16_variant(int variant, const void* A, const void* B,
     a.ldc = ldc;
     return (int)ntm::gemm::launch_gemm_bf16(a, S(stream));
   }
-  if (variant == 4 || variant == 5) {
+  if (variant == 4 || variant == 5 || variant == 6) {
     ntm::gemm::GemmArgs a;
     a.A = (const __bf16*)A;
     a.B = (const __bf16*)B;
@@ -77,6 +81,7 @@ NTM_API int ntm_gemm_bf16_variant(int variant, const void* A, const void* B,
     a.lda = lda;
     a.ldb = ldb;
     a.ldc = ldc;
+    if (variant == 6) return (int)ntm::gemmp::launch_gemm_bf16_pp4(a, S(stream));
     return variant == 5 ? (int)ntm::gemm3::launch_gemm_bf16_pp3(a, S(stream))
                         : (int)ntm::gemm2::launch_gemm_bf16_pp2(a, S(stream));
   }
