@@ -7,6 +7,7 @@ termination-message / Prometheus textfile outputs.
 """
 import json
 import os
+import socket
 import subprocess
 from pathlib import Path
 
@@ -165,3 +166,53 @@ def test_asan_full_validation_on_gpu(tmp_path):
     assert "AddressSanitizer" not in err and "runtime error" not in err, err[-3000:]
     assert rc == 0, out + err[-2000:]
     assert _last_json(out)["passed"]
+
+
+# ------------------------------------------------------------- Pushgateway
+@pytest.mark.gpu
+def test_pushgateway_push(tmp_path):
+    """--pushgateway POSTs the Prometheus text to
+    <url>/metrics/job/amdgpu_validate/instance/<host>; the JSON reports it."""
+    import http.server
+    import threading
+
+    got = {}
+
+    class H(http.server.BaseHTTPRequestHandler):
+        def do_POST(self):  # noqa: N802
+            n = int(self.headers["Content-Length"])
+            got["path"] = self.path
+            got["body"] = self.rfile.read(n).decode()
+            self.send_response(200)
+            self.end_headers()
+
+        def log_message(self, *a):
+            pass
+
+    srv = http.server.HTTPServer(("127.0.0.1", 0), H)
+    th = threading.Thread(target=srv.serve_forever, daemon=True)
+    th.start()
+    try:
+        url = f"http://127.0.0.1:{srv.server_address[1]}/gw"
+        _have_bin()
+        rc, out, err = _run("--size", "1024", "--iters", "3", "--pushgateway", url)
+    finally:
+        srv.shutdown()
+    assert rc == 0, out + err
+    rep = _last_json(out)
+    assert rep["pushgateway"] == "ok"
+    assert got["path"].startswith("/gw/metrics/job/amdgpu_validate/instance/")
+    assert "amdgpu_validate_passed 1" in got["body"]
+    assert 'amdgpu_validate_gemm_tflops{gpu="0"}' in got["body"]
+
+
+@pytest.mark.gpu
+def test_pushgateway_unreachable_is_not_fatal():
+    _have_bin()
+    with socket.socket() as s:        # a port nobody listens on
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    rc, out, _ = _run("--size", "512", "--iters", "2", "--pushgateway", f"http://127.0.0.1:{port}")
+    rep = _last_json(out)
+    assert rc == 0 and rep["passed"] is True
+    assert rep["pushgateway"].startswith("error")

@@ -32,6 +32,8 @@
 #include <thread>
 #include <vector>
 
+#include <netdb.h>
+#include <sys/socket.h>
 #include <unistd.h>
 
 #include "ntm/common.hpp"
@@ -101,6 +103,7 @@ struct Opts {
   std::string termination_log;  // k8s terminationMessagePath (<= 4 KiB summary)
   std::string prom_out;         // Prometheus textfile-collector metrics
   std::string fault;            // fault injection: corrupt_gemm | corrupt_abft | corrupt_allreduce
+  std::string pushgateway;      // http://host[:port][/prefix] of a Prometheus Pushgateway
 };
 
 void usage() {
@@ -109,6 +112,7 @@ void usage() {
                "       [--tflops-floor TF] [--min-hbm-gb GB] [--hbm-floor-gbps GBps]\n"
                "       [--allreduce-max-mib MiB] [--no-xgmi] [--json] [--out FILE]\n"
                "       [--termination-log FILE] [--prom-out FILE] [--fault-inject KIND]\n"
+               "       [--pushgateway http://host:port]\n"
                "fault-inject (also env NTM_FAULT_INJECT): corrupt_gemm | corrupt_abft |\n"
                "       corrupt_allreduce - corrupts the LAST GPU's data to prove detection\n");
 }
@@ -137,6 +141,7 @@ bool parse(int argc, char** argv, Opts& o) {
     else if (a == "--termination-log") { if (!(v = next(a.c_str()))) return false; o.termination_log = v; }
     else if (a == "--prom-out") { if (!(v = next(a.c_str()))) return false; o.prom_out = v; }
     else if (a == "--fault-inject") { if (!(v = next(a.c_str()))) return false; o.fault = v; }
+    else if (a == "--pushgateway") { if (!(v = next(a.c_str()))) return false; o.pushgateway = v; }
     else if (a == "-h" || a == "--help") { usage(); std::exit(0); }
     else { std::fprintf(stderr, "unknown argument %s\n", a.c_str()); return false; }
   }
@@ -572,6 +577,68 @@ std::string coll_json(const std::vector<CollRow>& rows) {
   return s + "]";
 }
 
+// POST `body` (Prometheus text format) to a Pushgateway:
+//   <url>/metrics/job/amdgpu_validate/instance/<host>
+// Plain HTTP/1.1 over a socket (the image has no curl). Returns "ok" or a
+// short error; never fatal - the verdict does not depend on the push.
+std::string push_metrics(const std::string& url, const std::string& body) {
+  const std::string scheme = "http://";
+  if (url.rfind(scheme, 0) != 0) return "error: only http:// URLs";
+  std::string rest = url.substr(scheme.size());
+  const size_t slash = rest.find('/');
+  std::string hostport = rest.substr(0, slash);
+  std::string prefix = slash == std::string::npos ? "" : rest.substr(slash);
+  while (!prefix.empty() && prefix.back() == '/') prefix.pop_back();
+  std::string host = hostport, port = "9091";
+  const size_t colon = hostport.rfind(':');
+  if (colon != std::string::npos) {
+    host = hostport.substr(0, colon);
+    port = hostport.substr(colon + 1);
+  }
+  char me[256] = "unknown";
+  gethostname(me, sizeof me - 1);
+  const std::string path = prefix + "/metrics/job/amdgpu_validate/instance/" + me;
+  addrinfo hints{}, *ai = nullptr;
+  hints.ai_family = AF_UNSPEC;
+  hints.ai_socktype = SOCK_STREAM;
+  if (getaddrinfo(host.c_str(), port.c_str(), &hints, &ai) != 0 || !ai)
+    return "error: cannot resolve " + host;
+  int fd = -1;
+  for (addrinfo* p = ai; p; p = p->ai_next) {
+    fd = socket(p->ai_family, p->ai_socktype, p->ai_protocol);
+    if (fd < 0) continue;
+    timeval tv{10, 0};
+    setsockopt(fd, SOL_SOCKET, SO_SNDTIMEO, &tv, sizeof tv);
+    setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof tv);
+    if (connect(fd, p->ai_addr, p->ai_addrlen) == 0) break;
+    close(fd);
+    fd = -1;
+  }
+  freeaddrinfo(ai);
+  if (fd < 0) return "error: cannot connect to " + hostport;
+  const std::string req = "POST " + path + " HTTP/1.1\r\nHost: " + hostport +
+                          "\r\nContent-Type: text/plain; version=0.0.4\r\nContent-Length: " +
+                          std::to_string(body.size()) + "\r\nConnection: close\r\n\r\n" + body;
+  size_t off = 0;
+  while (off < req.size()) {
+    const ssize_t w = send(fd, req.data() + off, req.size() - off, MSG_NOSIGNAL);
+    if (w <= 0) {
+      close(fd);
+      return "error: send failed";
+    }
+    off += (size_t)w;
+  }
+  char buf[256];
+  const ssize_t r = recv(fd, buf, sizeof buf - 1, 0);
+  close(fd);
+  if (r <= 0) return "error: no response";
+  buf[r] = 0;
+  const std::string status(buf, strnlen(buf, sizeof buf));
+  // "HTTP/1.1 200 OK" / "202 Accepted"
+  if (status.size() > 12 && status[9] == '2') return "ok";
+  return "error: " + status.substr(0, status.find('\r'));
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -624,6 +691,40 @@ int main(int argc, char** argv) {
 
   double agg = 0;
   for (auto& r : res) agg += r.gemm_tflops;
+  // node-exporter textfile-collector format (--prom-out) and Pushgateway
+  // body (--pushgateway); labels carry the device index.
+  double peak_rccl = 0, peak_xgmi = 0;
+  for (auto& c : rccl_rows) peak_rccl = std::max(peak_rccl, c.busbw);
+  for (auto& c : xgmi_rows) peak_xgmi = std::max(peak_xgmi, c.busbw);
+  const bool passed = g_failures.empty();
+  std::string prom_text;
+  {
+    std::ostringstream p;
+    p << "# HELP amdgpu_validate_passed 1 if every validation check passed.\n"
+      << "# TYPE amdgpu_validate_passed gauge\n"
+      << "amdgpu_validate_passed " << (passed ? 1 : 0) << "\n"
+      << "# TYPE amdgpu_validate_seconds gauge\n"
+      << "amdgpu_validate_seconds " << jnum(t_end - t_start) << "\n"
+      << "# TYPE amdgpu_validate_gemm_tflops gauge\n";
+    for (auto& r : res)
+      p << "amdgpu_validate_gemm_tflops{gpu=\"" << r.device << "\"} " << jnum(r.gemm_tflops) << "\n";
+    p << "# TYPE amdgpu_validate_hbm_copy_gbps gauge\n";
+    for (auto& r : res)
+      p << "amdgpu_validate_hbm_copy_gbps{gpu=\"" << r.device << "\"} " << jnum(r.hbm_copy_gbps) << "\n";
+    p << "# TYPE amdgpu_validate_hbm_total_gb gauge\n";
+    for (auto& r : res)
+      p << "amdgpu_validate_hbm_total_gb{gpu=\"" << r.device << "\"} " << jnum(r.total_gb) << "\n";
+    if (n > 1)
+      p << "# TYPE amdgpu_validate_allreduce_busbw_gbps gauge\n"
+        << "amdgpu_validate_allreduce_busbw_gbps{impl=\"rccl\"} " << jnum(peak_rccl) << "\n"
+        << "amdgpu_validate_allreduce_busbw_gbps{impl=\"xgmi\"} " << jnum(peak_xgmi) << "\n";
+    prom_text = p.str();
+  }
+  std::string push_status;
+  if (!o.pushgateway.empty()) {
+    push_status = push_metrics(o.pushgateway, prom_text);
+    if (push_status != "ok") std::fprintf(stderr, "amdgpu-validate: pushgateway %s\n", push_status.c_str());
+  }
   std::string js = "{";
   js += "\"tool\":\"amdgpu-validate\",\"passed\":" + std::string(g_failures.empty() ? "true" : "false");
   js += ",\"n_gpus\":" + std::to_string(n) + ",\"gemm_size\":" + std::to_string(o.size);
@@ -654,17 +755,15 @@ int main(int argc, char** argv) {
   js += ",\"start_epoch_s\":" + jnum(t_start) + ",\"end_epoch_s\":" + jnum(t_end);
   js += ",\"failures\":[";
   for (size_t i = 0; i < g_failures.size(); ++i) js += (i ? "," : "") + jstr(g_failures[i]);
-  js += "]}";
+  js += "]";
+  if (!o.pushgateway.empty()) js += ",\"pushgateway\":" + jstr(push_status);
+  js += "}";
   (void)t_local;
   std::printf("%s\n", js.c_str());
   if (!o.out.empty()) {
     std::ofstream f(o.out);
     f << js << "\n";
   }
-  const bool passed = g_failures.empty();
-  double peak_rccl = 0, peak_xgmi = 0;
-  for (auto& c : rccl_rows) peak_rccl = std::max(peak_rccl, c.busbw);
-  for (auto& c : xgmi_rows) peak_xgmi = std::max(peak_xgmi, c.busbw);
   if (!o.termination_log.empty()) {
     // Kubernetes surfaces this file as the pod's termination message
     // (truncated at 4 KiB): the one-line verdict an operator sees first.
@@ -679,29 +778,8 @@ int main(int argc, char** argv) {
     f << t << "\n";
   }
   if (!o.prom_out.empty()) {
-    // node-exporter textfile-collector format (metrics exporter sidecar /
-    // Pushgateway body); labels carry the device index.
-    std::ostringstream p;
-    p << "# HELP amdgpu_validate_passed 1 if every validation check passed.\n"
-      << "# TYPE amdgpu_validate_passed gauge\n"
-      << "amdgpu_validate_passed " << (passed ? 1 : 0) << "\n"
-      << "# TYPE amdgpu_validate_seconds gauge\n"
-      << "amdgpu_validate_seconds " << jnum(t_end - t_start) << "\n"
-      << "# TYPE amdgpu_validate_gemm_tflops gauge\n";
-    for (auto& r : res)
-      p << "amdgpu_validate_gemm_tflops{gpu=\"" << r.device << "\"} " << jnum(r.gemm_tflops) << "\n";
-    p << "# TYPE amdgpu_validate_hbm_copy_gbps gauge\n";
-    for (auto& r : res)
-      p << "amdgpu_validate_hbm_copy_gbps{gpu=\"" << r.device << "\"} " << jnum(r.hbm_copy_gbps) << "\n";
-    p << "# TYPE amdgpu_validate_hbm_total_gb gauge\n";
-    for (auto& r : res)
-      p << "amdgpu_validate_hbm_total_gb{gpu=\"" << r.device << "\"} " << jnum(r.total_gb) << "\n";
-    if (n > 1)
-      p << "# TYPE amdgpu_validate_allreduce_busbw_gbps gauge\n"
-        << "amdgpu_validate_allreduce_busbw_gbps{impl=\"rccl\"} " << jnum(peak_rccl) << "\n"
-        << "amdgpu_validate_allreduce_busbw_gbps{impl=\"xgmi\"} " << jnum(peak_xgmi) << "\n";
     std::ofstream f(o.prom_out);
-    f << p.str();
+    f << prom_text;
   }
   return passed ? 0 : 1;
 }
