@@ -31,7 +31,9 @@ def _require(t: torch.Tensor, name: str, dtype: torch.dtype) -> None:
 
 
 GEMM_VARIANTS = {"default": 0, "pingpong8": 1, "wave128": 2, "wave128d4": 3, "pingpong8b": 4,
-                 "pingpong8c": 5, "pingpong8p": 6}
+                 "pingpong8c": 5, "pingpong8p": 6, "pingpong8w": 7, "pingpong8wi": 8,
+                 "pingpong8ww": 9, "pingpong8cw": 10, "pingpong8cwe": 11,
+                 "pingpong8cwn": 12, "pingpong8cwne": 13, "pingpong8pw": 14}
 
 
 def gemm_bf16(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,

@@ -184,15 +184,19 @@ def test_abft_detects_corruption(ops):
     assert not ops.abft_check(a, b, c3, rs).ok
 
 
-@pytest.mark.parametrize("variant", ["pingpong8", "pingpong8b", "pingpong8c", "pingpong8p"])
+@pytest.mark.parametrize("variant", ["pingpong8", "pingpong8b", "pingpong8c", "pingpong8p",
+                                     "pingpong8w", "pingpong8wi", "pingpong8ww", "pingpong8cw",
+                                     "pingpong8cwe", "pingpong8cwn", "pingpong8cwne",
+                                     "pingpong8pw"])
 @pytest.mark.parametrize("m,n,k", [(256, 256, 128), (512, 256, 192), (256, 512, 256),
                                    (768, 1024, 320), (1024, 768, 2048), (2048, 2048, 4096),
                                    (512, 512, 384), (4096, 4352, 256), (8192, 8192, 512)])
 def test_gemm_variants_vs_torch_fp32(ops, variant, m, n, k):
     """Every 8-wave schedule, including K-tile counts T = 2..6 that exercise
     each prologue/tail path (T = K / 64; pingpong8c/8p need T even) and, for
-    the persistent pingpong8p, 1..4 tiles per workgroup (272 / 1024 tiles)."""
-    if variant in ("pingpong8c", "pingpong8p") and (k // 64) % 2:
+    the persistent pingpong8p, 1..4 tiles per workgroup (272 / 1024 tiles).
+    pingpong8w* (32-MFMA segments) and the widened *w epilogues need K % 128."""
+    if variant not in ("pingpong8", "pingpong8b") and (k // 64) % 2:
         pytest.skip(f"{variant} needs K % 128 == 0")
     a = _rand(ops, (m, k), 71 + k)
     b = _rand(ops, (n, k), 73 + n)

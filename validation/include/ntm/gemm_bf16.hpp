@@ -221,6 +221,31 @@ __device__ __forceinline__ void tile_coords(int M, int N, int& tm, int& tn) {
   tile_coords_of<GROUP_M>((int)blockIdx.x, (int)gridDim.x, M, N, tm, tn);
 }
 
+// Fused ABFT row checksum: the 4 lanes {l, l+16, l+32, l+48} share row
+// (l & 15); reduce their 16 accumulators each with two xor-shuffles, one
+// fp32 atomic per (row, wave). 4 column-waves x N/256 tiles add per row.
+__device__ __forceinline__ void abft_rowsum(const GemmArgs& p, const Ctx& c,
+                                            const f32x4 (&acc)[2][2][4][2],
+                                            int m0, int lane) {
+#pragma unroll
+  for (int mh = 0; mh < 2; ++mh)
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      float s = 0.f;
+#pragma unroll
+      for (int nh = 0; nh < 2; ++nh)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) {
+          const f32x4 v = acc[mh][nh][mt][nt];
+          s += (v[0] + v[1]) + (v[2] + v[3]);
+        }
+      s += __shfl_xor(s, 16);
+      s += __shfl_xor(s, 32);
+      if (lane < 16)
+        unsafeAtomicAdd(p.rowsum + m0 + mh * 128 + c.wr * 64 + mt * 16 + lane, s);
+    }
+}
+
 // Epilogue shared by the K1 kernels: bf16 RNE stores (8 B per lane per
 // 16x16 tile) and, with kRowSum, the fused ABFT row checksum.
 template <bool kRowSum>
@@ -247,29 +272,68 @@ __device__ __forceinline__ void store_tile(const GemmArgs& p, const Ctx& c,
           o[3] = (__bf16)v[3];
           *(bf16x4*)(p.C + (size_t)row * p.ldc + col) = o;
         }
+  if constexpr (kRowSum) abft_rowsum(p, c, acc, m0, lane);
+}
 
-  if constexpr (kRowSum) {
-    // Fused ABFT row checksum: the 4 lanes {l, l+16, l+32, l+48} share row
-    // (l & 15); reduce their 16 accumulators each with two xor-shuffles, one
-    // fp32 atomic per (row, wave). 4 column-waves x N/256 tiles add per row.
+// Widened epilogue (playbook T21, adapted to the 16x16 layout): a lane holds
+// 4 columns of tile nt = 0 and the same 4 columns + 16 of tile nt = 1. One
+// v_permlane16_swap per dword pair exchanges lanes 16-31 (48-63) of the nt = 0
+// register with lanes 0-15 (32-47) of the nt = 1 register, after which every
+// lane holds 8 consecutive columns: lane group g = lane >> 4 stores 16 B at
+// column offset (g & 1) * 16 + (g >> 1) * 8 of the 32-column pair. 16
+// dwordx4 stores per wave instead of 32 dwordx2, same bytes.
+__device__ __forceinline__ unsigned pack_bf16x2(float lo, float hi) {
+  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+  const bf16x2 q = {(__bf16)lo, (__bf16)hi};
+  return __builtin_bit_cast(unsigned, q);
+}
+
+template <bool kRowSum, bool NT = false>
+__device__ __forceinline__ void store_tile_wide(const GemmArgs& p, const Ctx& c,
+                                                const f32x4 (&acc)[2][2][4][2],
+                                                int m0, int n0, int lane) {
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  const int g = lane >> 4;
+  const int coff = (g & 1) * 16 + (g >> 1) * 8;
 #pragma unroll
-    for (int mh = 0; mh < 2; ++mh)
+  for (int mh = 0; mh < 2; ++mh)
+#pragma unroll
+    for (int nh = 0; nh < 2; ++nh)
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt) {
-        float s = 0.f;
+        const int row = m0 + mh * 128 + c.wr * 64 + mt * 16 + (lane & 15);
+        const int col = n0 + nh * 128 + c.wc * 32 + coff;
+        const f32x4 v0 = acc[mh][nh][mt][0], v1 = acc[mh][nh][mt][1];
+        unsigned w0[2], w1[2];
 #pragma unroll
-        for (int nh = 0; nh < 2; ++nh)
-#pragma unroll
-          for (int nt = 0; nt < 2; ++nt) {
-            const f32x4 v = acc[mh][nh][mt][nt];
-            s += (v[0] + v[1]) + (v[2] + v[3]);
-          }
-        s += __shfl_xor(s, 16);
-        s += __shfl_xor(s, 32);
-        if (lane < 16)
-          unsafeAtomicAdd(p.rowsum + m0 + mh * 128 + c.wr * 64 + mt * 16 + lane, s);
+        for (int h = 0; h < 2; ++h) {
+          const auto r = __builtin_amdgcn_permlane16_swap(
+              pack_bf16x2(v0[2 * h], v0[2 * h + 1]),
+              pack_bf16x2(v1[2 * h], v1[2 * h + 1]), false, false);
+          w0[h] = r[0];
+          w1[h] = r[1];
+        }
+        u32x4* dst = (u32x4*)(p.C + (size_t)row * p.ldc + col);
+        const u32x4 val = u32x4{w0[0], w0[1], w1[0], w1[1]};
+        if constexpr (NT)
+          __builtin_nontemporal_store(val, dst);
+        else
+          *dst = val;
       }
-  }
+  if constexpr (kRowSum) abft_rowsum(p, c, acc, m0, lane);
+}
+
+// Epilogue selector for the kernels' EPI template bit mask.
+enum : int { kEpiWide = 1, kEpiNT = 2, kEpiEarly = 4 };
+
+template <bool kRowSum, int EPI>
+__device__ __forceinline__ void store_tile_epi(const GemmArgs& p, const Ctx& c,
+                                               const f32x4 (&acc)[2][2][4][2],
+                                               int m0, int n0, int lane) {
+  if constexpr ((EPI & kEpiWide) != 0)
+    store_tile_wide<kRowSum, (EPI & kEpiNT) != 0>(p, c, acc, m0, n0, lane);
+  else
+    store_tile<kRowSum>(p, c, acc, m0, n0, lane);
 }
 
 template <bool kRowSum>

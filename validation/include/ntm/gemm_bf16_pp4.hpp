@@ -132,7 +132,7 @@ __device__ __forceinline__ void ktile_p(const PCtx& c, Frags3& f, f32x4 (&acc)[2
   phase_p<3, ODD>(c, f, acc, cur, nxt, has_next, t, T);
 }
 
-template <bool kRowSum>
+template <bool kRowSum, int EPI = 0>
 __global__ void __launch_bounds__(kThreads, 2)
     gemm_bf16_pp4_kernel(GemmArgs p) {
   __shared__ __attribute__((aligned(16))) char smem[kLdsBytes3];
@@ -193,7 +193,7 @@ __global__ void __launch_bounds__(kThreads, 2)
     }
     // boundary: retire every load in flight BEFORE any store (see header)
     wait_vmcnt<0>();
-    store_tile<kRowSum>(p, Ctx{c.lds, {}, c.frag_off, c.w, c.wr, c.wc}, acc, cur.m0, cur.n0,
+    store_tile_epi<kRowSum, EPI>(p, Ctx{c.lds, {}, c.frag_off, c.w, c.wr, c.wc}, acc, cur.m0, cur.n0,
                         lane);
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -226,16 +226,21 @@ inline int cu_count() {
   return n;
 }
 
-inline hipError_t launch_gemm_bf16_pp4(const GemmArgs& a, hipStream_t stream) {
+// wide = widened dwordx4 epilogue (store_tile_wide, needs ldc % 8).
+inline hipError_t launch_gemm_bf16_pp4(const GemmArgs& a, hipStream_t stream, bool wide = false) {
   if (!shape_ok3(a.M, a.N, a.K) || a.lda < a.K || a.ldb < a.K || a.ldc < a.N ||
-      (a.lda % 8) || (a.ldb % 8) || (a.ldc % 4))
+      (a.lda % 8) || (a.ldb % 8) || (a.ldc % (wide ? 8 : 4)))
     return hipErrorInvalidValue;
   const int ntiles = (a.M / BM) * (a.N / BN);
   int g = cu_count();
   g = g - g % 8;  // keep tile % 8 == blockIdx % 8 (same XCD as the remap assumes)
   if (g <= 0) g = 8;
   if (g > ntiles) g = ntiles;
-  if (a.rowsum)
+  if (wide && a.rowsum)
+    hipLaunchKernelGGL((gemm_bf16_pp4_kernel<true, kEpiWide>), dim3(g), dim3(kThreads), 0, stream, a);
+  else if (wide)
+    hipLaunchKernelGGL((gemm_bf16_pp4_kernel<false, kEpiWide>), dim3(g), dim3(kThreads), 0, stream, a);
+  else if (a.rowsum)
     hipLaunchKernelGGL(gemm_bf16_pp4_kernel<true>, dim3(g), dim3(kThreads), 0, stream, a);
   else
     hipLaunchKernelGGL(gemm_bf16_pp4_kernel<false>, dim3(g), dim3(kThreads), 0, stream, a);

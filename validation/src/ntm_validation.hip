@@ -9,6 +9,7 @@
 #include "ntm/gemm_bf16_pp2.hpp"
 #include "ntm/gemm_bf16_pp3.hpp"
 #include "ntm/gemm_bf16_pp4.hpp"
+#include "ntm/gemm_bf16_pp5.hpp"
 #include "ntm/gemm_bf16_w4.hpp"
 
 #define NTM_API extern "C" __attribute__((visibility("default")))
@@ -35,7 +36,11 @@ NTM_API int ntm_gemm_shape_ok(int M, int N, int K) {
 // 8-wave kernel with the balanced 8/4/8/4 read schedule (gemm_bf16_pp2.hpp);
 // 5 = the same schedule with parity-alternating B buffers and a uniform,
 // tail-free K loop (gemm_bf16_pp3.hpp; K % 128 == 0); 6 = 5 made persistent
-// (one WG per CU, DMA pipeline across tiles; gemm_bf16_pp4.hpp).
+// (one WG per CU, DMA pipeline across tiles; gemm_bf16_pp4.hpp); 7 / 8 / 9 =
+// wide 32-MFMA segments (gemm_bf16_pp5.hpp): reads first / DMA issue first /
+// reads first + widened dwordx4 epilogue; 10 / 11 / 12 / 13 = 5 + widened
+// epilogue / + early row-0 stores / + nontemporal stores / + both; 14 = 6 +
+// widened epilogue.
 // 0 = default: the fastest measured variant whose shape rules admit (M,N,K).
 // Measured on MI355X (tools/gemm_check.py, random bf16, median of 7 rounds,
 // profiles/r1_pp3/):
@@ -84,6 +89,21 @@ NTM_API int ntm_gemm_bf16_variant(int variant, const void* A, const void* B,
     if (variant == 6) return (int)ntm::gemmp::launch_gemm_bf16_pp4(a, S(stream));
     return variant == 5 ? (int)ntm::gemm3::launch_gemm_bf16_pp3(a, S(stream))
                         : (int)ntm::gemm2::launch_gemm_bf16_pp2(a, S(stream));
+  }
+  if (variant >= 7 && variant <= 14) {
+    ntm::gemm::GemmArgs a;
+    a.A = (const __bf16*)A;
+    a.B = (const __bf16*)B;
+    a.C = (__bf16*)C;
+    a.M = M;
+    a.N = N;
+    a.K = K;
+    a.lda = lda;
+    a.ldb = ldb;
+    a.ldc = ldc;
+    if (variant == 14) return (int)ntm::gemmp::launch_gemm_bf16_pp4(a, S(stream), true);
+    if (variant >= 10) return (int)ntm::gemm3::launch_gemm_bf16_pp3_knob(a, variant + 2, S(stream));
+    return (int)ntm::gemm5::launch_gemm_bf16_pp5(a, variant - 7, S(stream));
   }
   if (variant == 2 || variant == 3) {
     ntm::gemm4::Args a{(const __bf16*)A, (const __bf16*)B, (__bf16*)C, M, N, K,
