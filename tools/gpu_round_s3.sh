@@ -10,7 +10,7 @@ timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout
 tail -1 $O/pytest_gpu.log
 timeout -k 10 300 python -u tools/race_screen.py --variants default --repeats 100 > $O/race_default.log 2>&1 || { echo RACE_FAIL; tail -20 $O/race_default.log; exit 1; }
 tail -1 $O/race_default.log
-timeout -k 10 300 python -u tools/gemm_check.py --sizes 8192,4096 --iters 50 --rounds 9 --variants default,knob5,knob16,knob17,knob18 > $O/groupm_check.log 2>&1 || { echo CHECK_FAIL; tail -20 $O/groupm_check.log; exit 1; }
+timeout -k 10 300 python -u tools/gemm_check.py --sizes 8192,4096 --iters 50 --rounds 9 --variants default,knob5,knob16,knob17,knob18,knob19,knob20 > $O/groupm_check.log 2>&1 || { echo CHECK_FAIL; tail -20 $O/groupm_check.log; exit 1; }
 python - <<'PY'
 import json
 for l in open("gpurun_out/s3/groupm_check.log"):

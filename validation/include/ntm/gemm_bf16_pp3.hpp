@@ -95,7 +95,9 @@ __device__ __forceinline__ void tile3(const Ctx& c, Frags3& f,
 // EPI: epilogue options, bit mask of kEpiWide (store_tile_wide), kEpiNT
 // (nontemporal C stores) and kEpiEarly (wave row 0 stores its tile while row 1
 // runs its last MFMA segment, before the stagger-balancing barrier).
-template <bool kRowSum, int GROUP_M = kGroupM, bool PRIO = false, int EPI = 0>
+// SPRIO: static s_setprio(1) for the whole K loop on wave row SPRIO - 1
+// (0 = off); MI355X_MICROARCH.md "Two waves per SIMD" item 4.
+template <bool kRowSum, int GROUP_M = kGroupM, bool PRIO = false, int EPI = 0, int SPRIO = 0>
 __global__ void __launch_bounds__(kThreads, 2)
     gemm_bf16_pp3_kernel(GemmArgs p) {
   __shared__ __attribute__((aligned(16))) char smem[kLdsBytes3];
@@ -147,11 +149,15 @@ __global__ void __launch_bounds__(kThreads, 2)
   raw_barrier();
   read_b<kBLo>(c, f.b0, 0);
   if (c.wr == 1) raw_barrier();  // ping-pong stagger
+  if constexpr (SPRIO != 0) {
+    if (c.wr == SPRIO - 1) __builtin_amdgcn_s_setprio(1);
+  }
 
   for (int t = 0; t < T; t += 2) {
     tile3<false, PRIO>(c, f, acc, t, T);
     tile3<true, PRIO>(c, f, acc, t + 1, T);
   }
+  if constexpr (SPRIO != 0) __builtin_amdgcn_s_setprio(0);
   if constexpr ((EPI & kEpiEarly) != 0) {
     // Row 0 finished its last MFMA one barrier before row 1: drain its (dummy)
     // DMA pieces, store, then meet row 1's last barrier. No LDS is touched.
@@ -224,6 +230,14 @@ inline hipError_t launch_gemm_bf16_pp3_knob(const GemmArgs& a, int knob, hipStre
       if (knob == 16) hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, 4, false, kEpiDefault>), g, b, 0, s, a);
       if (knob == 17) hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, 16, false, kEpiDefault>), g, b, 0, s, a);
       if (knob == 18) hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, 2, false, kEpiDefault>), g, b, 0, s, a);
+      break;
+    }
+    // 19 / 20: default epilogue + static priority for wave row 1 (the lagging,
+    // younger half) / wave row 0
+    case 19: case 20: {
+      if (a.ldc % 8) return hipErrorInvalidValue;
+      if (knob == 19) hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, kGroupM, false, kEpiDefault, 2>), g, b, 0, s, a);
+      if (knob == 20) hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, kGroupM, false, kEpiDefault, 1>), g, b, 0, s, a);
       break;
     }
     default: return hipErrorInvalidValue;
