@@ -33,6 +33,8 @@ def _declare(lib: ctypes.CDLL) -> None:
             [c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp], c_int),
         "ntm_gemm_bf16_knob": (
             [c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp], c_int),
+        "ntm_gemm_bf16_stamp": (
+            [c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp], c_int),
         "ntm_gemm_bf16_rowsum": (
             [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp], c_int),
         "ntm_abft_check": ([c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int,

@@ -46,12 +46,14 @@ def test_gemm_identity_asymmetric(ops):
     assert torch.equal(c, b.T.contiguous())
 
 
-def test_gemm_strided_ld(ops):
-    m, n, k = 512, 512, 256
+@pytest.mark.parametrize("k", [256, 320])        # default kernel: pingpong8c / pingpong8b
+@pytest.mark.parametrize("ldc_pad", [256, 4])    # ldc % 8 == 0: widened epilogue; == 4: dwordx2
+def test_gemm_strided_ld(ops, k, ldc_pad):
+    m, n = 512, 512
     abig = _rand(ops, (m, k + 64), 3)
     bbig = _rand(ops, (n, k + 128), 4)
     a, b = abig[:, :k], bbig[:, :k]
-    out = torch.zeros((m, n + 256), dtype=torch.bfloat16, device="cuda")
+    out = torch.zeros((m, n + ldc_pad), dtype=torch.bfloat16, device="cuda")
     ops.gemm_bf16(a, b, out[:, :n])
     ref = a.float() @ b.float().T
     atol, rtol = ops.gemm_tolerance(k)

@@ -1,0 +1,96 @@
+"""Ablation timing of the K1 default kernel (developer diagnostic).
+
+Times four builds of pingpong8c (validation/include/ntm/gemm_bf16_pp3_stamp.hpp)
+interleaved in one process on random data, after >= 2 s of back-to-back
+launches (MI355X_MICROARCH.md 'DVFS give-back' item 6):
+  real      the kernel as shipped (+ 2 stamps per wave),
+  no_lds    fragment reads + LDS-DMA removed (MFMA + barriers),
+  no_mfma   MFMAs removed (reads + DMA + barriers),
+  mfma_only MFMAs only (no barriers, no loads),
+  reads_no_dma / dma_no_reads  one half of no_lds's removal each,
+and reports each one's wall time, in-kernel clock (s_memtime over
+s_memrealtime, median over waves) and cycles per K-tile per workgroup.
+
+    python tools/gemm_stamp.py [--size 8192] [--warm-s 2] [--rounds 5]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+import time
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+
+import torch  # noqa: E402
+
+from nvidia_terraform_modules_amd import ops  # noqa: E402
+from nvidia_terraform_modules_amd.ops._lib import check, lib, stream_handle  # noqa: E402
+
+SLOTS = 4
+START, END, RT0, RT1 = range(4)
+MODES = {"real": 0, "no_lds": 1, "no_mfma": 2, "mfma_only": 3, "reads_no_dma": 4,
+         "dma_no_reads": 5}
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--size", type=int, default=8192)
+    ap.add_argument("--warm-s", type=float, default=2.0)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--iters", type=int, default=20)
+    args = ap.parse_args()
+    n = args.size
+    dev = torch.device("cuda:0")
+    a = ops.fill_uniform_(torch.empty((n, n), dtype=torch.bfloat16, device=dev), 1)
+    b = ops.fill_uniform_(torch.empty((n, n), dtype=torch.bfloat16, device=dev), 2)
+    c = torch.empty((n, n), dtype=torch.bfloat16, device=dev)
+    nwg = (n // 256) ** 2
+    st = {m: torch.zeros(nwg * 8 * SLOTS, dtype=torch.int64, device=dev) for m in MODES}
+
+    def run(m):
+        rc = lib().ntm_gemm_bf16_stamp(MODES[m], a.data_ptr(), b.data_ptr(), c.data_ptr(),
+                                       n, n, n, n, n, n, st[m].data_ptr(), stream_handle())
+        check(rc, "ntm_gemm_bf16_stamp")
+
+    t_end = time.time() + args.warm_s
+    while time.time() < t_end:
+        for _ in range(args.iters):
+            run("real")
+        torch.cuda.synchronize()
+    times = {m: [] for m in MODES}
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    for _ in range(args.rounds):
+        for m in MODES:
+            ev[0].record()
+            for _ in range(args.iters):
+                run(m)
+            ev[1].record()
+            torch.cuda.synchronize()
+            times[m].append(ev[0].elapsed_time(ev[1]) / args.iters)
+    run("real")
+    ref = ops.ref_gemm_f32(a, b)
+    atol, rtol = ops.gemm_tolerance(n)
+    ok = ops.verify_bf16(c, ref, atol, rtol).ok
+    T = n // 64
+    tiles_per_cu = nwg / 256
+    out = {"size": n, "real_verified": ok}
+    for m in MODES:
+        s = st[m].view(nwg, 8, SLOTS).cpu().double()
+        span = s[:, :, END] - s[:, :, START]
+        rt = (s[:, :, RT1] - s[:, :, RT0]) / 100e6
+        ms = sorted(times[m])[len(times[m]) // 2]
+        clk = float((span / rt).median()) / 1e9
+        out[m] = {"ms": round(ms, 4), "tflops": round(2 * n ** 3 / ms / 1e9, 1),
+                  "clock_GHz": round(clk, 3),
+                  "wg_span_cycles_per_ktile": round(float(span.median()) / T, 1),
+                  "kernel_cycles_per_ktile_per_cu": round(ms * 1e-3 * clk * 1e9 / (T * tiles_per_cu), 1)}
+    # matrix floor: 2 waves/SIMD x 64 v_mfma_f32_16x16x32_bf16 x 16 cycles per K-tile
+    out["mfma_floor_cycles_per_ktile"] = 2048
+    print(json.dumps(out), flush=True)
+    return 0 if ok else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())

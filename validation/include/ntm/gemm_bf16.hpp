@@ -323,14 +323,67 @@ __device__ __forceinline__ void store_tile_wide(const GemmArgs& p, const Ctx& c,
   if constexpr (kRowSum) abft_rowsum(p, c, acc, m0, lane);
 }
 
+// LDS-staged epilogue: the whole 256x256 bf16 tile goes through LDS (row
+// pitch 528 B, so the 8-lane groups of a ds_write_b128 hit distinct banks)
+// and leaves as full 512-B rows, 2 rows per wave instruction. Needs 135 KiB of
+// LDS and a caller that has drained its LDS-DMA (vmcnt(0)); the barrier here
+// orders every wave's last fragment read and DMA before the overwrite.
+constexpr int kStagePitch = 528;
+
+template <bool kRowSum, bool NT>
+__device__ __forceinline__ void store_tile_lds(const GemmArgs& p, const Ctx& c,
+                                               const f32x4 (&acc)[2][2][4][2],
+                                               int m0, int n0, int lane) {
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  raw_barrier();
+  const int g = lane >> 4;
+  const int coff = (g & 1) * 16 + (g >> 1) * 8;
+#pragma unroll
+  for (int mh = 0; mh < 2; ++mh)
+#pragma unroll
+    for (int nh = 0; nh < 2; ++nh)
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        const int row = mh * 128 + c.wr * 64 + mt * 16 + (lane & 15);
+        const int col = nh * 128 + c.wc * 32 + coff;
+        const f32x4 v0 = acc[mh][nh][mt][0], v1 = acc[mh][nh][mt][1];
+        unsigned w0[2], w1[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const auto r = __builtin_amdgcn_permlane16_swap(
+              pack_bf16x2(v0[2 * h], v0[2 * h + 1]),
+              pack_bf16x2(v1[2 * h], v1[2 * h + 1]), false, false);
+          w0[h] = r[0];
+          w1[h] = r[1];
+        }
+        *(u32x4*)(c.lds + row * kStagePitch + col * 2) = u32x4{w0[0], w0[1], w1[0], w1[1]};
+      }
+  raw_barrier();
+  // wave w stores rows 32w .. 32w+31; lane -> (row pair half, 16-B chunk)
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int row = c.w * 32 + i * 2 + (lane >> 5);
+    const int chunk = lane & 31;
+    const u32x4 val = *(const u32x4*)(c.lds + row * kStagePitch + chunk * 16);
+    u32x4* dst = (u32x4*)(p.C + (size_t)(m0 + row) * p.ldc + n0 + chunk * 8);
+    if constexpr (NT)
+      __builtin_nontemporal_store(val, dst);
+    else
+      *dst = val;
+  }
+  if constexpr (kRowSum) abft_rowsum(p, c, acc, m0, lane);
+}
+
 // Epilogue selector for the kernels' EPI template bit mask.
-enum : int { kEpiWide = 1, kEpiNT = 2, kEpiEarly = 4 };
+enum : int { kEpiWide = 1, kEpiNT = 2, kEpiEarly = 4, kEpiLds = 8 };
 
 template <bool kRowSum, int EPI>
 __device__ __forceinline__ void store_tile_epi(const GemmArgs& p, const Ctx& c,
                                                const f32x4 (&acc)[2][2][4][2],
                                                int m0, int n0, int lane) {
-  if constexpr ((EPI & kEpiWide) != 0)
+  if constexpr ((EPI & kEpiLds) != 0)
+    store_tile_lds<kRowSum, (EPI & kEpiNT) != 0>(p, c, acc, m0, n0, lane);
+  else if constexpr ((EPI & kEpiWide) != 0)
     store_tile_wide<kRowSum, (EPI & kEpiNT) != 0>(p, c, acc, m0, n0, lane);
   else
     store_tile<kRowSum>(p, c, acc, m0, n0, lane);

@@ -111,7 +111,7 @@ __device__ __forceinline__ void issue_prologue(const Ctx& c) {
   issue_half<kBHi>(c, 1, 1);
 }
 
-template <bool kRowSum>
+template <bool kRowSum, int EPI = 0>
 __global__ void __launch_bounds__(kThreads, 2)
     gemm_bf16_pp2_kernel(GemmArgs p) {
   __shared__ __attribute__((aligned(16))) char smem[kLdsBytes];
@@ -162,20 +162,25 @@ __global__ void __launch_bounds__(kThreads, 2)
   tail_tiles(c, f, acc, t);
   if (c.wr == 0) raw_barrier();
 
-  store_tile<kRowSum>(p, c, acc, m0, n0, lane);
+  store_tile_epi<kRowSum, EPI>(p, c, acc, m0, n0, lane);
 }
 
+// Same epilogue choice as pingpong8c: widened + nontemporal when ldc % 8 == 0.
 inline hipError_t launch_gemm_bf16_pp2(const GemmArgs& a, hipStream_t stream) {
   if (!shape_ok(a.M, a.N, a.K) || a.lda < a.K || a.ldb < a.K || a.ldc < a.N ||
       (a.lda % 8) || (a.ldb % 8) || (a.ldc % 4))
     return hipErrorInvalidValue;
   const unsigned grid = (unsigned)((a.M / BM) * (a.N / BN));
-  if (a.rowsum)
-    hipLaunchKernelGGL(gemm_bf16_pp2_kernel<true>, dim3(grid), dim3(kThreads),
-                       0, stream, a);
+  constexpr int E = kEpiWide | kEpiNT;
+  const bool wide = (a.ldc % 8) == 0;
+  if (a.rowsum && wide)
+    hipLaunchKernelGGL((gemm_bf16_pp2_kernel<true, E>), dim3(grid), dim3(kThreads), 0, stream, a);
+  else if (a.rowsum)
+    hipLaunchKernelGGL(gemm_bf16_pp2_kernel<true>, dim3(grid), dim3(kThreads), 0, stream, a);
+  else if (wide)
+    hipLaunchKernelGGL((gemm_bf16_pp2_kernel<false, E>), dim3(grid), dim3(kThreads), 0, stream, a);
   else
-    hipLaunchKernelGGL(gemm_bf16_pp2_kernel<false>, dim3(grid), dim3(kThreads),
-                       0, stream, a);
+    hipLaunchKernelGGL(gemm_bf16_pp2_kernel<false>, dim3(grid), dim3(kThreads), 0, stream, a);
   return hipGetLastError();
 }
 

@@ -100,6 +100,8 @@ __device__ __forceinline__ void tile3(const Ctx& c, Frags3& f,
 template <bool kRowSum, int GROUP_M = kGroupM, bool PRIO = false, int EPI = 0, int SPRIO = 0>
 __global__ void __launch_bounds__(kThreads, 2)
     gemm_bf16_pp3_kernel(GemmArgs p) {
+  static_assert(!((EPI & kEpiLds) && (EPI & kEpiEarly)), "LDS staging needs all waves");
+  static_assert(kLdsBytes3 >= BM * kStagePitch, "LDS staging buffer");
   __shared__ __attribute__((aligned(16))) char smem[kLdsBytes3];
 
   int tm, tn;
@@ -230,6 +232,13 @@ inline hipError_t launch_gemm_bf16_pp3_knob(const GemmArgs& a, int knob, hipStre
       if (knob == 16) hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, 4, false, kEpiDefault>), g, b, 0, s, a);
       if (knob == 17) hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, 16, false, kEpiDefault>), g, b, 0, s, a);
       if (knob == 18) hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, 2, false, kEpiDefault>), g, b, 0, s, a);
+      break;
+    }
+    // 21 / 22: LDS-staged full-row epilogue, nontemporal / default policy
+    case 21: case 22: {
+      if (a.ldc % 8) return hipErrorInvalidValue;
+      if (knob == 21) hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, kGroupM, false, kEpiLds | kEpiNT>), g, b, 0, s, a);
+      if (knob == 22) hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, kGroupM, false, kEpiLds>), g, b, 0, s, a);
       break;
     }
     // 19 / 20: default epilogue + static priority for wave row 1 (the lagging,

@@ -226,7 +226,7 @@ inline int cu_count() {
   return n;
 }
 
-// wide = widened dwordx4 epilogue (store_tile_wide, needs ldc % 8).
+// wide = widened nontemporal dwordx4 epilogue (store_tile_wide, needs ldc % 8).
 inline hipError_t launch_gemm_bf16_pp4(const GemmArgs& a, hipStream_t stream, bool wide = false) {
   if (!shape_ok3(a.M, a.N, a.K) || a.lda < a.K || a.ldb < a.K || a.ldc < a.N ||
       (a.lda % 8) || (a.ldb % 8) || (a.ldc % (wide ? 8 : 4)))
@@ -237,9 +237,9 @@ inline hipError_t launch_gemm_bf16_pp4(const GemmArgs& a, hipStream_t stream, bo
   if (g <= 0) g = 8;
   if (g > ntiles) g = ntiles;
   if (wide && a.rowsum)
-    hipLaunchKernelGGL((gemm_bf16_pp4_kernel<true, kEpiWide>), dim3(g), dim3(kThreads), 0, stream, a);
+    hipLaunchKernelGGL((gemm_bf16_pp4_kernel<true, kEpiWide | kEpiNT>), dim3(g), dim3(kThreads), 0, stream, a);
   else if (wide)
-    hipLaunchKernelGGL((gemm_bf16_pp4_kernel<false, kEpiWide>), dim3(g), dim3(kThreads), 0, stream, a);
+    hipLaunchKernelGGL((gemm_bf16_pp4_kernel<false, kEpiWide | kEpiNT>), dim3(g), dim3(kThreads), 0, stream, a);
   else if (a.rowsum)
     hipLaunchKernelGGL(gemm_bf16_pp4_kernel<true>, dim3(g), dim3(kThreads), 0, stream, a);
   else

@@ -9,6 +9,7 @@
 #include "ntm/gemm_bf16_pp2.hpp"
 #include "ntm/gemm_bf16_pp3.hpp"
 #include "ntm/gemm_bf16_pp4.hpp"
+#include "ntm/gemm_bf16_pp3_stamp.hpp"
 #include "ntm/gemm_bf16_pp5.hpp"
 #include "ntm/gemm_bf16_w4.hpp"
 
@@ -134,6 +135,25 @@ NTM_API int ntm_gemm_bf16_knob(int knob, const void* A, const void* B, void* C,
   a.ldb = ldb;
   a.ldc = ldc;
   return (int)ntm::gemm3::launch_gemm_bf16_pp3_knob(a, knob, S(stream));
+}
+
+// DIAGNOSTIC: pingpong8c ablation builds with s_memtime stamps
+// (gemm_bf16_pp3_stamp.hpp; mode 0 real, 1 no LDS traffic, 2 no MFMA, 3 MFMA
+// only). stamps: (M/256)*(N/256)*8*4 u64.
+NTM_API int ntm_gemm_bf16_stamp(int mode, const void* A, const void* B, void* C, int M, int N,
+                                int K, int lda, int ldb, int ldc, void* stamps, void* stream) {
+  ntm::gemm::GemmArgs a;
+  a.A = (const __bf16*)A;
+  a.B = (const __bf16*)B;
+  a.C = (__bf16*)C;
+  a.M = M;
+  a.N = N;
+  a.K = K;
+  a.lda = lda;
+  a.ldb = ldb;
+  a.ldc = ldc;
+  return (int)ntm::gemm3s::launch_gemm_bf16_pp3_stamp(
+      a, mode, (unsigned long long*)stamps, S(stream));
 }
 
 NTM_API int ntm_gemm_bf16(const void* A, const void* B, void* C, int M, int N,
