@@ -28,8 +28,8 @@ import torch  # noqa: E402
 from nvidia_terraform_modules_amd import ops  # noqa: E402
 from nvidia_terraform_modules_amd.ops._lib import check, lib, stream_handle  # noqa: E402
 
-SLOTS = 4
-START, END, RT0, RT1 = range(4)
+SLOTS = 8
+START, END, RT0, RT1, HWID, XCCID = range(6)
 MODES = {"real": 0, "no_lds": 1, "no_mfma": 2, "mfma_only": 3, "reads_no_dma": 4,
          "dma_no_reads": 5}
 
@@ -86,6 +86,41 @@ def main() -> int:
                   "clock_GHz": round(clk, 3),
                   "wg_span_cycles_per_ktile": round(float(span.median()) / T, 1),
                   "kernel_cycles_per_ktile_per_cu": round(ms * 1e-3 * clk * 1e9 / (T * tiles_per_cu), 1)}
+    # per-CU timeline of the real kernel (last launch): workgroups that ran on the
+    # same CU (HW_ID cu/sh/se fields + XCC id) in start order; gap = next start -
+    # this end (s_memrealtime, 10 ns ticks), lead = first start - launch's first start.
+    s = st["real"].view(nwg, 8, SLOTS).cpu()
+    w0 = s[:, 0, :]
+    hw = w0[:, HWID]
+    cu_key = (w0[:, XCCID] & 0xF) * 4096 + ((hw >> 8) & 0xF) * 256 + ((hw >> 12) & 0x1) * 16 + \
+        ((hw >> 13) & 0x7)
+    rt0, rt1 = w0[:, RT0].double(), w0[:, RT1].double()
+    t0 = float(rt0.min())
+    gaps, leads, tails, per_cu = [], [], [], []
+    for key in torch.unique(cu_key):
+        idx = (cu_key == key).nonzero().flatten()
+        order = idx[torch.argsort(rt0[idx])]
+        per_cu.append(len(order))
+        leads.append(float(rt0[order[0]]) - t0)
+        tails.append(float(rt1.max() - rt1[order[-1]]))
+        for i in range(len(order) - 1):
+            gaps.append(float(rt0[order[i + 1]] - rt1[order[i]]))
+    g = torch.tensor(gaps) * 10e-3 if gaps else torch.zeros(1)
+    out["timeline_real"] = {
+        "cus_seen": len(per_cu), "wgs_per_cu_max": max(per_cu), "wgs_per_cu_min": min(per_cu),
+        "wg_gap_us_median": round(float(g.median()), 3), "wg_gap_us_p90": round(float(g.quantile(0.9)), 3),
+        "first_start_spread_us_p90": round(float(torch.tensor(leads).quantile(0.9)) * 10e-3, 3),
+        "end_spread_us_p90": round(float(torch.tensor(tails).quantile(0.9)) * 10e-3, 3),
+        "wg_span_us_median": round(float((rt1 - rt0).median()) * 10e-3, 2),
+        "launch_span_us": round(float(rt1.max() - rt0.min()) * 10e-3, 2)}
+    xcc = (w0[:, XCCID] & 0xF)
+    out["per_xcd_real"] = {
+        int(x): {"wg_span_us_mean": round(float((rt1 - rt0)[xcc == x].mean()) * 10e-3, 2),
+                 "last_end_us": round(float(rt1[xcc == x].max() - t0) * 10e-3, 2),
+                 "median_cu_end_us": round(float(rt1[xcc == x].median() - t0) * 10e-3, 2),
+                 "clock_GHz": round(float(((s[:, 0, END] - s[:, 0, START]).double() /
+                                          ((rt1 - rt0) / 100e6))[xcc == x].median()) / 1e9, 3)}
+        for x in torch.unique(xcc)}
     # matrix floor: 2 waves/SIMD x 64 v_mfma_f32_16x16x32_bf16 x 16 cycles per K-tile
     out["mfma_floor_cycles_per_ktile"] = 2048
     print(json.dumps(out), flush=True)

@@ -33,7 +33,7 @@ using ::ntm::gemm3::kLdsBytes3;
 using ::ntm::gemm3::shape_ok3;
 
 // u64 slots per wave in the stamp buffer
-enum : int { kStart = 0, kEnd, kRtStart, kRtEnd, kSlots = 4 };
+enum : int { kStart = 0, kEnd, kRtStart, kRtEnd, kHwId, kXccId, kSlots = 8 };
 
 __device__ __forceinline__ void keep(const bf16x8 (&x)[2][2]) {
 #pragma unroll
@@ -166,6 +166,9 @@ __global__ void __launch_bounds__(kThreads, 2)
     o[kEnd] = ts1;
     o[kRtStart] = rt0;
     o[kRtEnd] = rt1;
+    // HW_REG_HW_ID (4) and HW_REG_XCC_ID (20), full 32 bits: which CU ran it
+    o[kHwId] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);
+    o[kXccId] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20);
   }
 }
 
