@@ -14,4 +14,5 @@ run sq2 SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS
 run sq3 SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM SQ_LDS_IDX_ACTIVE && \
 run tcc TCC_HIT_sum TCC_MISS_sum && \
 run fetch FETCH_SIZE && \
+run write WRITE_SIZE && \
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 tools/gemm_pair.py --size 8192 --iters 20 > $OUT/trace.log 2>&1

@@ -4,16 +4,16 @@
 set -o pipefail
 cd /root/repo
 export TMPDIR=/tmp
-O=gpurun_out/s3
+O=gpurun_out/s4
 mkdir -p $O
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { echo PYTEST_FAIL; tail -40 $O/pytest_gpu.log; exit 1; }
 tail -1 $O/pytest_gpu.log
 timeout -k 10 300 python -u tools/race_screen.py --variants default --repeats 100 > $O/race_default.log 2>&1 || { echo RACE_FAIL; tail -20 $O/race_default.log; exit 1; }
 tail -1 $O/race_default.log
-timeout -k 10 300 python -u tools/gemm_check.py --sizes 8192,4096 --iters 50 --rounds 9 --variants default,knob5,knob16,knob17,knob18,knob19,knob20 > $O/groupm_check.log 2>&1 || { echo CHECK_FAIL; tail -20 $O/groupm_check.log; exit 1; }
+timeout -k 10 300 python -u tools/gemm_check.py --sizes 8192,4096 --iters 50 --rounds 9 --variants default,knob5,knob12,knob14 > $O/groupm_check.log 2>&1 || { echo CHECK_FAIL; tail -20 $O/groupm_check.log; exit 1; }
 python - <<'PY'
 import json
-for l in open("gpurun_out/s3/groupm_check.log"):
+for l in open("gpurun_out/s4/groupm_check.log"):
     if l.startswith('{"size"'):
         d=json.loads(l); print(d["size"], {k[:-12]: round(v) for k,v in d.items() if k.endswith("_tflops_med")})
 PY

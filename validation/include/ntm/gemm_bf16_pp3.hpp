@@ -173,12 +173,14 @@ __global__ void __launch_bounds__(kThreads, 2)
   }
 }
 
-// Default epilogue: widened dwordx4 + nontemporal C stores whenever rows are
-// 16-B aligned (ldc % 8 == 0); measured +3.9 % at 8192^3 and +5.5 % at 4096^3
-// over the dwordx2 epilogue (profiles/r1_epilogue). C is written once and
-// never re-read by the kernel, so nontemporal keeps it from evicting the A/B
-// panels the XCD's other tiles are still reading from L2.
-constexpr int kEpiDefault = kEpiWide | kEpiNT;
+// Default epilogue whenever rows are 16-B aligned (ldc % 8 == 0): the tile is
+// staged through LDS and leaves as full 512-B rows with nontemporal stores.
+// Measured over the dwordx2 epilogue: the widened dwordx4 stores +2-4 %,
+// nontemporal +2 % more (C is written once; it no longer evicts the A/B panels
+// the XCD's other tiles still read from L2), then the LDS staging +0.5 % at
+// 8192^3 / +1.5 % at 4096^3 (15 interleaved rounds) and WRITE_SIZE down from
+// 159 MB to the exact 128 MB of C (profiles/r1_epilogue, r1_pmc_r6).
+constexpr int kEpiDefault = kEpiLds | kEpiNT;
 
 inline hipError_t launch_gemm_bf16_pp3(const GemmArgs& a, hipStream_t stream) {
   if (!shape_ok3(a.M, a.N, a.K) || a.lda < a.K || a.ldb < a.K || a.ldc < a.N ||
@@ -241,6 +243,10 @@ inline hipError_t launch_gemm_bf16_pp3_knob(const GemmArgs& a, int knob, hipStre
       if (knob == 22) hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, kGroupM, false, kEpiLds>), g, b, 0, s, a);
       break;
     }
+    case 23:  // LDS-staged nontemporal epilogue + GROUP_M 4
+      if (a.ldc % 8) return hipErrorInvalidValue;
+      hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, 4, false, kEpiLds | kEpiNT>), g, b, 0, s, a);
+      break;
     // 19 / 20: default epilogue + static priority for wave row 1 (the lagging,
     // younger half) / wave row 0
     case 19: case 20: {

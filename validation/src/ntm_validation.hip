@@ -51,9 +51,9 @@ NTM_API int ntm_gemm_shape_ok(int M, int N, int K) {
 // Variant 6 (persistent 5) is correct and race-free but measured no faster
 // (8192^3 1586 vs 1594, 4096^3 1512 vs 1509; profiles/r1_pp4): not default.
 // Variants 4 and 5 pass tools/race_screen.py (bitwise-stable under HBM noise).
-// Variant 5 then took the widened (v_permlane16_swap -> dwordx4) nontemporal
-// epilogue whenever ldc % 8 == 0 (profiles/r1_epilogue, r1_round6):
-//   8192^3: 1650 TF vs hipBLASLt 1654, 4096^3: 1536 vs 1526 (same process).
+// Variant 5 then took the LDS-staged full-row nontemporal epilogue whenever
+// ldc % 8 == 0 (profiles/r1_epilogue, r1_round7): 8192^3 1623-1635 TF vs
+// hipBLASLt 1632-1648, 4096^3 1536 vs 1532-1544 (same processes).
 // Variants 7-9 (32-MFMA segments) measured no faster than 5 with the same
 // epilogue; 11/13 (early row-0 stores) tie with 10/12.
 // Default: 5 when K % 128 == 0, else 4 (both need K % 64 == 0, K >= 128).
