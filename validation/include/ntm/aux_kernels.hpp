@@ -345,6 +345,40 @@ __global__ void __launch_bounds__(256)
     dst[i] = src[i];
 }
 
+// Chunked copy: block b owns one contiguous span of ceil(tiles / grid) tiles
+// and walks it with the same one-tile-ahead software pipeline, so each CU
+// streams through its own DRAM pages instead of all CUs marching through the
+// same region (the tiled kernels above).
+template <int U, int LP, int SP>
+__global__ void __launch_bounds__(256)
+    stream_copy_chunk_kernel(const f32x4* __restrict__ src,
+                             f32x4* __restrict__ dst, size_t n4) {
+  constexpr size_t kTile = 256 * U;
+  const size_t ntiles = n4 / kTile;
+  const size_t per = (ntiles + gridDim.x - 1) / gridDim.x;
+  size_t t = (size_t)blockIdx.x * per;
+  const size_t end = t + per < ntiles ? t + per : ntiles;
+  f32x4 v[U];
+  if (t < end) {
+#pragma unroll
+    for (int j = 0; j < U; ++j) v[j] = ld<LP>(src + t * kTile + threadIdx.x + j * 256);
+  }
+  for (; t < end; ++t) {
+    f32x4 w[U];
+    if (t + 1 < end) {
+#pragma unroll
+      for (int j = 0; j < U; ++j) w[j] = ld<LP>(src + (t + 1) * kTile + threadIdx.x + j * 256);
+    }
+#pragma unroll
+    for (int j = 0; j < U; ++j) st<SP>(dst + t * kTile + threadIdx.x + j * 256, v[j]);
+#pragma unroll
+    for (int j = 0; j < U; ++j) v[j] = w[j];
+  }
+  for (size_t i = ntiles * kTile + (size_t)blockIdx.x * 256 + threadIdx.x;
+       i < n4; i += (size_t)gridDim.x * 256)
+    dst[i] = src[i];
+}
+
 template <int U, int LP>
 __global__ void __launch_bounds__(256)
     stream_read_tiled_kernel(const f32x4* __restrict__ src, size_t n4,

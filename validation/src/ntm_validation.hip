@@ -269,6 +269,10 @@ int copy_u(const void* src, void* dst, size_t n4, int policy, unsigned grid,
     case 5: hipLaunchKernelGGL((stream_copy_pipe_kernel<U, 1, 0>), dim3(grid), dim3(256), 0, s, a, b, n4); break;
     case 6: hipLaunchKernelGGL((stream_copy_pipe_kernel<U, 0, 1>), dim3(grid), dim3(256), 0, s, a, b, n4); break;
     case 7: hipLaunchKernelGGL((stream_copy_pipe_kernel<U, 1, 1>), dim3(grid), dim3(256), 0, s, a, b, n4); break;
+    case 9: hipLaunchKernelGGL((stream_copy_chunk_kernel<U, 1, 0>), dim3(grid), dim3(256), 0, s, a, b, n4); break;
+    case 11: hipLaunchKernelGGL((stream_copy_chunk_kernel<U, 1, 1>), dim3(grid), dim3(256), 0, s, a, b, n4); break;
+    case 8: hipLaunchKernelGGL((stream_copy_chunk_kernel<U, 0, 0>), dim3(grid), dim3(256), 0, s, a, b, n4); break;
+    case 10: hipLaunchKernelGGL((stream_copy_chunk_kernel<U, 0, 1>), dim3(grid), dim3(256), 0, s, a, b, n4); break;
     default: return (int)hipErrorInvalidValue;
   }
   return (int)hipGetLastError();
