@@ -1,7 +1,8 @@
 """MI355X (gfx950) HIP kernels used by the post-provision validation Job.
 
 K1 ``gemm_bf16``      - 256x256x64 LDS-DMA + MFMA bf16 GEMM (the headline);
-   ``gemm_bf16_rowsum`` - same kernel with the fused ABFT row-checksum epilogue.
+   ``gemm_bf16_rowsum`` - same kernel with the fused ABFT row-checksum epilogue;
+   ``gemm_fp8``         - the same schedule on OCP e4m3 operands (MX-scaled MFMA).
 K2 ``stream_copy``, ``stream_read`` - tuned float4 HBM streams.
 K3 ``fill_uniform_``, ``ref_gemm_f32``, ``verify_bf16``, ``abft_check`` - synthetic
    data, full fp32 reference check and the O(n^2) checksum check.
@@ -17,6 +18,8 @@ from .kernels import (  # noqa: F401
     fill_uniform_,
     gemm_bf16,
     gemm_bf16_rowsum,
+    gemm_fp8,
+    gemm_fp8_shape_ok,
     gemm_shape_ok,
     gemm_tolerance,
     ref_gemm_f32,

@@ -35,6 +35,10 @@ def _declare(lib: ctypes.CDLL) -> None:
             [c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp], c_int),
         "ntm_gemm_bf16_stamp": (
             [c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp], c_int),
+        "ntm_mfma_f8_probe": ([c_vp, c_vp, c_vp, c_vp], c_int),
+        "ntm_gemm_fp8": ([c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp], c_int),
+        "ntm_gemm_fp8_shape_ok": ([c_int, c_int, c_int], c_int),
+        "ntm_mfma_rate": ([c_int, c_int, c_int, c_vp, c_vp, c_vp], c_int),
         "ntm_gemm_bf16_rowsum": (
             [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp], c_int),
         "ntm_abft_check": ([c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int,

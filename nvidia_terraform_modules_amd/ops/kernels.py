@@ -74,6 +74,37 @@ def gemm_bf16(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
     return out
 
 
+def gemm_fp8_shape_ok(m: int, n: int, k: int) -> bool:
+    return bool(lib().ntm_gemm_fp8_shape_ok(m, n, k))
+
+
+def gemm_fp8(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """K1-fp8: ``out = a @ b.T`` with OCP e4m3 operands (``torch.float8_e4m3fn``),
+    fp32 accumulation on the MX-scaled MFMA path (unit scales), bf16 output.
+
+    a: [M, K], b: [N, K] (K-contiguous, rows 16-byte aligned), out: [M, N] bf16.
+    M, N % 256 and K % 256. Same 8-wave schedule and LDS image as the bf16
+    default; twice the MFMA rate per clock.
+    """
+    _require(a, "a", torch.float8_e4m3fn)
+    _require(b, "b", torch.float8_e4m3fn)
+    m, k = a.shape
+    n, kb = b.shape
+    if k != kb:
+        raise ValueError(f"K mismatch: a has {k}, b has {kb}")
+    if not gemm_fp8_shape_ok(m, n, k):
+        raise ValueError(f"shape ({m},{n},{k}) not tiled by the fp8 kernel (M, N, K % 256)")
+    if out is None:
+        out = torch.empty((m, n), dtype=torch.bfloat16, device=a.device)
+    _require(out, "out", torch.bfloat16)
+    if tuple(out.shape) != (m, n):
+        raise ValueError("out has the wrong shape")
+    rc = lib().ntm_gemm_fp8(a.data_ptr(), b.data_ptr(), out.data_ptr(), m, n, k, a.stride(0),
+                            b.stride(0), out.stride(0), stream_handle())
+    check(rc, "ntm_gemm_fp8")
+    return out
+
+
 def gemm_bf16_rowsum(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
                      rowsum: torch.Tensor | None = None) -> tuple[torch.Tensor, torch.Tensor]:
     """K1 with the fused ABFT epilogue: returns ``(out, rowsum)`` where

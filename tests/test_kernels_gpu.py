@@ -116,10 +116,10 @@ def test_stream_copy_and_read(ops):
 
 @pytest.mark.parametrize("nbytes", [16, 4096 + 48, (1 << 20) * 3 + 16 * 7])
 def test_stream_copy_all_configs_exact(ops, nbytes):
-    """Every (unroll, policy) copy kernel is byte-exact, including sub-tile
+    """Every (unroll, policy) copy kernel (tiled, pipelined, chunked) is byte-exact, including sub-tile
     tails and a grid larger than the tile count."""
     src = torch.randint(0, 255, (nbytes,), dtype=torch.uint8, device="cuda")
-    for cfg in [(1, 0, 0)] + [(u, p, g) for u in (2, 4, 8, 16) for p in range(8)
+    for cfg in [(1, 0, 0)] + [(u, p, g) for u in (2, 4, 8, 16) for p in range(12)
                               for g in (0, 7, 256)]:
         dst = torch.zeros_like(src)
         ops.stream_copy(src, dst, config=cfg)
@@ -208,3 +208,63 @@ def test_gemm_variants_vs_torch_fp32(ops, variant, m, n, k):
     err = (c.float() - ref).abs()
     assert torch.all(err <= atol + rtol * ref.abs()), float(err.max())
     assert torch.equal(c, ops.gemm_bf16(a, b, variant="pingpong8"))  # same math, same order
+
+
+def _rand_fp8(shape, seed):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    x = torch.rand(shape, generator=g, device="cuda") * 2 - 1      # uniform [-1, 1)
+    return x.to(torch.float8_e4m3fn)
+
+
+@pytest.mark.parametrize("m,n,k", [(256, 256, 256), (512, 256, 768), (256, 768, 512),
+                                   (1024, 1024, 2048), (2048, 4352, 1280)])
+def test_gemm_fp8_vs_torch_fp32(ops, m, n, k):
+    """K1-fp8 against a plain fp32 matmul of the same (dequantised) e4m3 values:
+    products of e4m3 values are exact in fp32, so the only error is the
+    accumulation order and the bf16 output rounding."""
+    a = _rand_fp8((m, k), 11 + k)
+    b = _rand_fp8((n, k), 13 + n)
+    c = ops.gemm_fp8(a, b)
+    ref = a.float() @ b.float().T
+    atol, rtol = ops.gemm_tolerance(k)
+    err = (c.float() - ref).abs()
+    assert torch.all(err <= atol + rtol * ref.abs()), float(err.max())
+    assert torch.equal(c, ops.gemm_fp8(a, b))    # deterministic
+
+
+def test_gemm_fp8_operand_map_probe(ops):
+    """The f8f6f4 MFMA sums over k, so A and B only need the SAME k order per
+    lane; rows must be lane & 15. Pin both with exact small-integer data."""
+    from nvidia_terraform_modules_amd.ops._lib import check, lib, stream_handle
+    torch.manual_seed(0)
+    a = torch.randint(-3, 4, (16, 128)).float().to(torch.float8_e4m3fn)
+    b = torch.randint(-3, 4, (16, 128)).float().to(torch.float8_e4m3fn)
+    ref = a.float() @ b.float().T
+
+    def stage(mat, perm):
+        u8 = mat.view(torch.uint8)
+        rows = torch.arange(64) & 15
+        return torch.gather(u8[rows], 1, perm[torch.arange(64) >> 4]).contiguous().cuda()
+
+    # the kernel's map ("halves16"): lane group g holds k 16g..16g+15, 64+16g..64+16g+15
+    perm = torch.stack([torch.cat([torch.arange(16 * g, 16 * g + 16),
+                                   torch.arange(64 + 16 * g, 64 + 16 * g + 16)]) for g in range(4)])
+    d = torch.empty((64, 4), dtype=torch.float32, device="cuda")
+    sa, sb = stage(a, perm), stage(b, perm)      # keep both alive across the launch
+    check(lib().ntm_mfma_f8_probe(sa.data_ptr(), sb.data_ptr(), d.data_ptr(), stream_handle()),
+          "probe")
+    torch.cuda.synchronize()
+    got = torch.empty((16, 16))
+    dc = d.cpu()
+    for lane in range(64):
+        for r in range(4):
+            got[4 * (lane >> 4) + r, lane & 15] = dc[lane, r]
+    assert torch.equal(got, ref)
+
+
+def test_gemm_fp8_rejects_bad_shapes(ops):
+    a = torch.zeros((256, 128), dtype=torch.float8_e4m3fn, device="cuda")
+    with pytest.raises(ValueError):
+        ops.gemm_fp8(a, a)                       # K % 256
+    with pytest.raises(ValueError):
+        ops.gemm_fp8(a.to(torch.bfloat16), a.to(torch.bfloat16))

@@ -1,0 +1,69 @@
+"""Pin the operand lane map of v_mfma_scale_f32_16x16x128_f8f6f4 (e4m3) with
+exact integer data (playbook: 'Other dtypes: check the map with exact integer
+data'). Lane l always holds row / column l & 15; candidate maps differ in which
+k each of its 32 bytes carries. Prints which (A map, B map) pair reproduces
+A @ B^T exactly.
+
+    python tools/fp8_layout_probe.py
+"""
+from __future__ import annotations
+
+import itertools
+import json
+import sys
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+
+import torch  # noqa: E402
+
+from nvidia_terraform_modules_amd.ops._lib import check, lib, stream_handle  # noqa: E402
+
+CANDIDATES = {
+    "contig32": lambda g, j: 32 * g + j,
+    "halves16": lambda g, j: 16 * g + j if j < 16 else 64 + 16 * g + (j - 16),
+    "quads8": lambda g, j: 8 * g + (j % 8) + 32 * (j // 8),
+    "oct4": lambda g, j: 4 * g + (j % 4) + 16 * (j // 4),
+}
+
+
+def stage(mat: torch.Tensor, kmap) -> torch.Tensor:
+    """mat: [16, 128] fp8 -> [64 lanes, 32 bytes] uint8 in lane order."""
+    u8 = mat.view(torch.uint8)
+    out = torch.empty((64, 32), dtype=torch.uint8)
+    for lane in range(64):
+        g, r = lane >> 4, lane & 15
+        for j in range(32):
+            out[lane, j] = u8[r, kmap(g, j)]
+    return out
+
+
+def main() -> int:
+    torch.manual_seed(0)
+    a = torch.randint(-3, 4, (16, 128)).float().to(torch.float8_e4m3fn)
+    b = torch.randint(-3, 4, (16, 128)).float().to(torch.float8_e4m3fn)
+    ref = a.float() @ b.float().T                       # D[i][j], exact in fp32
+    d = torch.empty((64, 4), dtype=torch.float32, device="cuda")
+    found = []
+    for (na, ka), (nb, kb) in itertools.product(CANDIDATES.items(), repeat=2):
+        sa = stage(a, ka).cuda()
+        sb = stage(b, kb).cuda()
+        check(lib().ntm_mfma_f8_probe(sa.data_ptr(), sb.data_ptr(), d.data_ptr(),
+                                      stream_handle()), "ntm_mfma_f8_probe")
+        torch.cuda.synchronize()
+        got = torch.empty((16, 16))
+        dc = d.cpu()
+        for lane in range(64):
+            for r in range(4):
+                got[4 * (lane >> 4) + r, lane & 15] = dc[lane, r]
+        ok = torch.equal(got, ref)
+        print(json.dumps({"A": na, "B": nb, "exact": ok,
+                          "max_err": float((got - ref).abs().max())}), flush=True)
+        if ok:
+            found.append((na, nb))
+    print(json.dumps({"matching": found}))
+    return 0 if found else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())

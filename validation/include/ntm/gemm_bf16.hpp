@@ -163,6 +163,50 @@ __device__ __forceinline__ void mma_quadrant(f32x4 (&acc)[4][2],
   if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
 }
 
+// fp8 (OCP e4m3) form of mma_quadrant for the same LDS image: the K-tile's
+// 128 bytes per row are 128 fp8 values, and a lane's two bf16x8 fragment reads
+// (ks = 0, 1: bytes 16c..16c+15 and 64+16c..64+16c+15 of its row, c = the
+// lane's 16-B chunk) concatenate into one 32-byte operand of
+// v_mfma_scale_f32_16x16x128_f8f6f4 (unit E8M0 scales). A dot product only
+// needs A and B to use the same k order, which they do (same image, same
+// reads; pinned by tools/fp8_layout_probe.py). 8 MFMAs of 32 cycles do twice
+// the bf16 quadrant's work in the same 256 cycles.
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ i32x8 cat_f8(const bf16x8& lo, const bf16x8& hi) {
+  typedef int i32x4 __attribute__((ext_vector_type(4)));
+  const i32x4 x = __builtin_bit_cast(i32x4, lo), y = __builtin_bit_cast(i32x4, hi);
+  return __builtin_shufflevector(x, y, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+// The accumulators are pinned to AGPRs and updated in place by inline asm: with
+// the builtin, hipcc (ROCm 7.2) writes each result to fresh VGPRs and the
+// 8-register-aligned operand tuples push the kernel to 256 VGPRs + 13 spilled;
+// the scratch reloads' vmcnt(0) then drained the LDS-DMA pipeline 4x per
+// K-tile pair (2.06 PF vs hipBLASLt's 3.2 PF). hipcc pads nothing inside asm:
+// operands come from ds_read (hipcc waits lgkmcnt on "v" inputs), the AGPR
+// accumulators are never written by VALU inside the loop, and the kernel
+// drains the MFMA pipe (mfma_drain) before any VALU reads them.
+__device__ __forceinline__ void mfma_f8_agpr(f32x4& acc, const i32x8& a, const i32x8& b) {
+  asm("v_mfma_scale_f32_16x16x128_f8f6f4 %0, %1, %2, %0, %3, %3 op_sel_hi:[0,0,0]"
+      : "+a"(acc)
+      : "v"(a), "v"(b), "v"(127));  // fmt e4m3 x e4m3 (cbsz = blgp = 0), E8M0 scale 2^0
+}
+
+__device__ __forceinline__ void mfma_drain() {
+  asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");
+}
+
+__device__ __forceinline__ void mma_quadrant_f8(f32x4 (&acc)[4][2],
+                                                const bf16x8 (&a)[4][2],
+                                                const bf16x8 (&b)[2][2]) {
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+      mfma_f8_agpr(acc[mt][nt], cat_f8(b[nt][0], b[nt][1]), cat_f8(a[mt][0], a[mt][1]));
+}
+
 // One phase of the K loop. P: phase within the K-tile (0..3); ISSUE: whether
 // the prefetch item of this phase exists; VMC: counted vmcnt (-1 = none).
 template <int P, bool ISSUE, int VMC>

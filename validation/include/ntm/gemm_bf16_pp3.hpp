@@ -55,7 +55,7 @@ __device__ __forceinline__ void issue_half3(const Ctx& c, int kt, int buf, int T
   glds16(s + 32, d + 1024);
 }
 
-template <int P, bool ODD, bool PRIO>
+template <int P, bool ODD, bool PRIO, bool F8 = false>
 __device__ __forceinline__ void phase3(const Ctx& c, Frags3& f,
                                        f32x4 (&acc)[2][2][4][2], int t, int T) {
   bf16x8(&bcur)[2][2] = ODD ? f.b1 : f.b0;
@@ -71,20 +71,27 @@ __device__ __forceinline__ void phase3(const Ctx& c, Frags3& f,
   if constexpr (P == 3) issue_half3<kBHi>(c, t + 2, cur, T);
   wait_vmcnt<10>();
   raw_barrier();
-  if constexpr (P == 0) mma_quadrant<PRIO>(acc[0][0], f.a, bcur);
-  if constexpr (P == 1) mma_quadrant<PRIO>(acc[0][1], f.a, both);
-  if constexpr (P == 2) mma_quadrant<PRIO>(acc[1][1], f.a, both);
-  if constexpr (P == 3) mma_quadrant<PRIO>(acc[1][0], f.a, bcur);
+  if constexpr (F8) {
+    if constexpr (P == 0) mma_quadrant_f8(acc[0][0], f.a, bcur);
+    if constexpr (P == 1) mma_quadrant_f8(acc[0][1], f.a, both);
+    if constexpr (P == 2) mma_quadrant_f8(acc[1][1], f.a, both);
+    if constexpr (P == 3) mma_quadrant_f8(acc[1][0], f.a, bcur);
+  } else {
+    if constexpr (P == 0) mma_quadrant<PRIO>(acc[0][0], f.a, bcur);
+    if constexpr (P == 1) mma_quadrant<PRIO>(acc[0][1], f.a, both);
+    if constexpr (P == 2) mma_quadrant<PRIO>(acc[1][1], f.a, both);
+    if constexpr (P == 3) mma_quadrant<PRIO>(acc[1][0], f.a, bcur);
+  }
   raw_barrier();
 }
 
-template <bool ODD, bool PRIO>
+template <bool ODD, bool PRIO, bool F8 = false>
 __device__ __forceinline__ void tile3(const Ctx& c, Frags3& f,
                                       f32x4 (&acc)[2][2][4][2], int t, int T) {
-  phase3<0, ODD, PRIO>(c, f, acc, t, T);
-  phase3<1, ODD, PRIO>(c, f, acc, t, T);
-  phase3<2, ODD, PRIO>(c, f, acc, t, T);
-  phase3<3, ODD, PRIO>(c, f, acc, t, T);
+  phase3<0, ODD, PRIO, F8>(c, f, acc, t, T);
+  phase3<1, ODD, PRIO, F8>(c, f, acc, t, T);
+  phase3<2, ODD, PRIO, F8>(c, f, acc, t, T);
+  phase3<3, ODD, PRIO, F8>(c, f, acc, t, T);
 }
 
 // GROUP_M / PRIO are tuning knobs (tools/gemm_check.py --variants knobN). The
@@ -97,7 +104,10 @@ __device__ __forceinline__ void tile3(const Ctx& c, Frags3& f,
 // runs its last MFMA segment, before the stagger-balancing barrier).
 // SPRIO: static s_setprio(1) for the whole K loop on wave row SPRIO - 1
 // (0 = off); MI355X_MICROARCH.md "Two waves per SIMD" item 4.
-template <bool kRowSum, int GROUP_M = kGroupM, bool PRIO = false, int EPI = 0, int SPRIO = 0>
+// F8: the operands are OCP e4m3 (K1-fp8, gemm_fp8.hpp); p's K / lda / ldb are
+// then counted in bf16-sized pairs of fp8 values (the LDS image is the same).
+template <bool kRowSum, int GROUP_M = kGroupM, bool PRIO = false, int EPI = 0, int SPRIO = 0,
+          bool F8 = false>
 __global__ void __launch_bounds__(kThreads, 2)
     gemm_bf16_pp3_kernel(GemmArgs p) {
   static_assert(!((EPI & kEpiLds) && (EPI & kEpiEarly)), "LDS staging needs all waves");
@@ -156,10 +166,11 @@ __global__ void __launch_bounds__(kThreads, 2)
   }
 
   for (int t = 0; t < T; t += 2) {
-    tile3<false, PRIO>(c, f, acc, t, T);
-    tile3<true, PRIO>(c, f, acc, t + 1, T);
+    tile3<false, PRIO, F8>(c, f, acc, t, T);
+    tile3<true, PRIO, F8>(c, f, acc, t + 1, T);
   }
   if constexpr (SPRIO != 0) __builtin_amdgcn_s_setprio(0);
+  if constexpr (F8) mfma_drain();  // asm MFMAs: results must land before VALU reads
   if constexpr ((EPI & kEpiEarly) != 0) {
     // Row 0 finished its last MFMA one barrier before row 1: drain its (dummy)
     // DMA pieces, store, then meet row 1's last barrier. No LDS is touched.

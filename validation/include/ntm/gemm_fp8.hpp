@@ -1,0 +1,123 @@
+// K1-fp8: OCP e4m3 GEMM on the MX-scaled matrix path of CDNA4
+// (v_mfma_scale_f32_16x16x128_f8f6f4, unit E8M0 scales): twice the bf16
+// MFMA rate per CU clock (cdna_hip_programming.md "MFMA rate per dtype").
+//
+// The validation Job uses it to exercise the fp8 matrix cores that MI355X
+// inference workloads run on; the reference's GPU Operator validator has no
+// counterpart (SURVEY.md §2.7 lists only the bf16 K1).
+//
+// mfma_f8_probe: one wave, one MFMA on operands pre-arranged per lane by the
+// host (64 lanes x 32 bytes each for A and B) -> the 16x16 fp32 result in the
+// dtype-independent C/D layout (col = lane & 15, row = 4 * (lane >> 4) + j).
+// Used by tests/test_kernels_gpu.py to pin the operand lane map with exact
+// data before the GEMM relies on it (playbook: "Other dtypes: check the map
+// with exact integer data").
+#pragma once
+
+#include "ntm/common.hpp"
+#include "ntm/gemm_bf16_pp3.hpp"
+
+namespace ntm {
+namespace fp8 {
+
+using ::ntm::gemm::i32x8;
+
+// fmt codes of the f8f6f4 instruction (cbsz / blgp): 0 = fp8 e4m3, 1 = bf8 e5m2
+constexpr int kFmtE4M3 = 0;
+constexpr int kScaleOne = 127;  // E8M0 exponent bias: 2^(127-127) = 1
+
+__device__ __forceinline__ f32x4 mfma_f8(const i32x8& a, const i32x8& b, f32x4 c) {
+  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, kFmtE4M3, kFmtE4M3, 0,
+                                                          kScaleOne, 0, kScaleOne);
+}
+
+__global__ void __launch_bounds__(64) mfma_f8_probe_kernel(const i32x8* a, const i32x8* b,
+                                                           f32x4* d) {
+  const int l = threadIdx.x;
+  d[l] = mfma_f8(a[l], b[l], f32x4{0.f, 0.f, 0.f, 0.f});
+}
+
+// C[M x N] (bf16) = A[M x K] (e4m3) * B[N x K]^T (e4m3), fp32 accumulation,
+// on the pingpong8c schedule (gemm_bf16_pp3.hpp, F8 = true) with its default
+// LDS-staged epilogue. lda / ldb / ldc in elements (fp8 for A/B, bf16 for C).
+// Shape rule: M, N % 256, K % 256 (128-value K-tiles, an even count), 16-byte
+// aligned rows.
+__host__ __device__ inline bool shape_ok(int M, int N, int K) {
+  return M > 0 && N > 0 && K >= 256 && (M % 256) == 0 && (N % 256) == 0 && (K % 256) == 0;
+}
+
+inline hipError_t launch_gemm_fp8(const void* A, const void* B, __bf16* C, int M, int N, int K,
+                                  int lda, int ldb, int ldc, hipStream_t stream) {
+  using namespace ::ntm::gemm;
+  if (!shape_ok(M, N, K) || lda < K || ldb < K || ldc < N || (lda % 16) || (ldb % 16) ||
+      (ldc % 8))
+    return hipErrorInvalidValue;
+  GemmArgs a;
+  a.A = (const __bf16*)A;  // byte image: two fp8 per bf16 slot
+  a.B = (const __bf16*)B;
+  a.C = C;
+  a.M = M;
+  a.N = N;
+  a.K = K / 2;
+  a.lda = lda / 2;
+  a.ldb = ldb / 2;
+  a.ldc = ldc;
+  const dim3 g((unsigned)((M / BM) * (N / BN))), b(kThreads);
+  hipLaunchKernelGGL((::ntm::gemm3::gemm_bf16_pp3_kernel<false, kGroupM, false,
+                                                         ::ntm::gemm3::kEpiDefault, 0, true>),
+                     g, b, 0, stream, a);
+  return hipGetLastError();
+}
+
+// Matrix-core rate probe: every wave issues iters x 8 independent MFMAs
+// (operands in registers, random bits from the seed) between two s_memtime
+// stamps; one 256-thread workgroup (one wave per SIMD) per CU. F8 selects
+// v_mfma_scale_f32_16x16x128_f8f6f4 (e4m3, unit scales), else
+// v_mfma_f32_16x16x32_bf16. out[wave] = {cycles, realtime ticks}; the sums
+// keep the accumulators live.
+template <bool F8>
+__global__ void __launch_bounds__(256) mfma_rate_kernel(int iters, unsigned seed,
+                                                        unsigned long long* out, float* sink) {
+  const int lane = threadIdx.x & 63;
+  i32x8 a, b;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    // e4m3 / bf16 bit patterns with the exponent kept small (no inf / nan)
+    const unsigned h = (unsigned)mix64(((unsigned long long)seed << 32) ^ (lane * 8 + i));
+    a[i] = (int)(h & 0x3B3B3B3Bu);
+    b[i] = (int)((h >> 3) & 0x3B3B3B3Bu);
+  }
+  f32x4 acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+  const unsigned long long r0 = __builtin_amdgcn_s_memrealtime();
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if constexpr (F8) {
+        acc[j] = mfma_f8(a, b, acc[j]);
+      } else {
+        typedef int i32x4 __attribute__((ext_vector_type(4)));
+        const i32x4 al = {a[0], a[1], a[2], a[3]}, bl = {b[0], b[1], b[2], b[3]};
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, al),
+                                                         __builtin_bit_cast(bf16x8, bl),
+                                                         acc[j], 0, 0, 0);
+      }
+    }
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s += acc[j][0] + acc[j][1] + acc[j][2] + acc[j][3];
+  const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+  const unsigned long long r1 = __builtin_amdgcn_s_memrealtime();
+  if (s == 12345.678f) sink[0] = s;
+  if (lane == 0) {
+    const size_t w = (size_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+    out[2 * w] = t1 - t0;
+    out[2 * w + 1] = r1 - r0;
+  }
+}
+
+}  // namespace fp8
+}  // namespace ntm

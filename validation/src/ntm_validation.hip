@@ -6,6 +6,7 @@
 // can be captured in a hipGraph (playbook §6 Guideline 9).
 #include "ntm/aux_kernels.hpp"
 #include "ntm/gemm_bf16.hpp"
+#include "ntm/gemm_fp8.hpp"
 #include "ntm/gemm_bf16_pp2.hpp"
 #include "ntm/gemm_bf16_pp3.hpp"
 #include "ntm/gemm_bf16_pp4.hpp"
@@ -154,6 +155,39 @@ NTM_API int ntm_gemm_bf16_stamp(int mode, const void* A, const void* B, void* C,
   a.ldc = ldc;
   return (int)ntm::gemm3s::launch_gemm_bf16_pp3_stamp(
       a, mode, (unsigned long long*)stamps, S(stream));
+}
+
+// K1-fp8: C (bf16) = A (e4m3) * B (e4m3)^T, fp32 accumulation (gemm_fp8.hpp).
+NTM_API int ntm_gemm_fp8(const void* A, const void* B, void* C, int M, int N, int K, int lda,
+                         int ldb, int ldc, void* stream) {
+  return (int)ntm::fp8::launch_gemm_fp8(A, B, (__bf16*)C, M, N, K, lda, ldb, ldc, S(stream));
+}
+
+// DIAGNOSTIC: matrix-core issue rate (gemm_fp8.hpp mfma_rate_kernel); out:
+// 2 u64 per wave (grid x 4 waves), sink: 1 float.
+NTM_API int ntm_mfma_rate(int f8, int grid, int iters, void* out, float* sink, void* stream) {
+  if (grid <= 0 || iters <= 0) return (int)hipErrorInvalidValue;
+  if (f8)
+    hipLaunchKernelGGL(ntm::fp8::mfma_rate_kernel<true>, dim3(grid), dim3(256), 0, S(stream),
+                       iters, 7u, (unsigned long long*)out, sink);
+  else
+    hipLaunchKernelGGL(ntm::fp8::mfma_rate_kernel<false>, dim3(grid), dim3(256), 0, S(stream),
+                       iters, 7u, (unsigned long long*)out, sink);
+  return (int)hipGetLastError();
+}
+
+NTM_API int ntm_gemm_fp8_shape_ok(int M, int N, int K) {
+  return ntm::fp8::shape_ok(M, N, K) ? 1 : 0;
+}
+
+// One v_mfma_scale_f32_16x16x128_f8f6f4 (e4m3 x e4m3, unit scales) on
+// per-lane operands: a_stage / b_stage 64 x 32 B, d 64 x 4 fp32.
+NTM_API int ntm_mfma_f8_probe(const void* a_stage, const void* b_stage, float* d,
+                              void* stream) {
+  hipLaunchKernelGGL(ntm::fp8::mfma_f8_probe_kernel, dim3(1), dim3(64), 0, S(stream),
+                     (const ntm::fp8::i32x8*)a_stage, (const ntm::fp8::i32x8*)b_stage,
+                     (ntm::f32x4*)d);
+  return (int)hipGetLastError();
 }
 
 NTM_API int ntm_gemm_bf16(const void* A, const void* B, void* C, int M, int N,
