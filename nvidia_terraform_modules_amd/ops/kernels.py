@@ -172,24 +172,29 @@ def abft_check(a: torch.Tensor, b: torch.Tensor, c: torch.Tensor,
 
 
 def fill_uniform_(t: torch.Tensor, seed: int, scale: float = 1.0) -> torch.Tensor:
-    """K3: fill a bf16 tensor in place with ``scale * U[-1, 1)`` (hash RNG)."""
-    if t.dtype != torch.bfloat16 or not t.is_cuda or not t.is_contiguous():
-        raise ValueError("fill_uniform_ needs a contiguous bf16 GPU tensor")
-    rc = lib().ntm_fill_uniform_bf16(t.data_ptr(), t.numel(), seed & (2**64 - 1), float(scale),
-                                     stream_handle())
-    check(rc, "ntm_fill_uniform_bf16")
+    """K3: fill a bf16 (or OCP e4m3, ``torch.float8_e4m3fn``) tensor in place
+    with ``scale * U[-1, 1)`` (hash RNG; e4m3 rounds to nearest even)."""
+    if t.dtype not in (torch.bfloat16, torch.float8_e4m3fn) or not t.is_cuda or \
+            not t.is_contiguous():
+        raise ValueError("fill_uniform_ needs a contiguous bf16 or float8_e4m3fn GPU tensor")
+    fn = lib().ntm_fill_uniform_bf16 if t.dtype == torch.bfloat16 else lib().ntm_fill_uniform_e4m3
+    rc = fn(t.data_ptr(), t.numel(), seed & (2**64 - 1), float(scale), stream_handle())
+    check(rc, "ntm_fill_uniform")
     return t
 
 
 def ref_gemm_f32(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
-    """K3: independent fp32-FMA reference ``a @ b.T`` (no MFMA, no hipBLASLt)."""
-    _require(a, "a", torch.bfloat16)
-    _require(b, "b", torch.bfloat16)
+    """K3: independent fp32-FMA reference ``a @ b.T`` (no MFMA, no hipBLASLt) for
+    bf16 or OCP e4m3 operands (both of the same dtype)."""
+    dt = a.dtype if a.dtype in (torch.bfloat16, torch.float8_e4m3fn) else torch.bfloat16
+    _require(a, "a", dt)
+    _require(b, "b", dt)
     m, k = a.shape
     n = b.shape[0]
     out = torch.empty((m, n), dtype=torch.float32, device=a.device)
-    rc = lib().ntm_ref_gemm_f32(a.data_ptr(), b.data_ptr(), out.data_ptr(), m, n, k,
-                                a.stride(0), b.stride(0), out.stride(0), stream_handle())
+    fn = lib().ntm_ref_gemm_f32 if dt == torch.bfloat16 else lib().ntm_ref_gemm_f32_e4m3
+    rc = fn(a.data_ptr(), b.data_ptr(), out.data_ptr(), m, n, k, a.stride(0), b.stride(0),
+            out.stride(0), stream_handle())
     check(rc, "ntm_ref_gemm_f32")
     return out
 

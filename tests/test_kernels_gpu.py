@@ -268,3 +268,51 @@ def test_gemm_fp8_rejects_bad_shapes(ops):
         ops.gemm_fp8(a, a)                       # K % 256
     with pytest.raises(ValueError):
         ops.gemm_fp8(a.to(torch.bfloat16), a.to(torch.bfloat16))
+
+
+def _uniform_pm1_host(seed: int, n: int):
+    """Host replica of ntm::uniform_pm1 (common.hpp): splitmix64 hash -> 24 bits."""
+    import numpy as np
+
+    def mix64(x):
+        x = x + np.uint64(0x9E3779B97F4A7C15)
+        x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return x ^ (x >> np.uint64(31))
+
+    with np.errstate(over="ignore"):
+        idx = np.arange(n, dtype=np.uint64)
+        h = mix64((np.uint64(seed) * np.uint64(0x100000001B3)) ^ mix64(idx))
+    u = (h >> np.uint64(40)).astype(np.float32) * np.float32(1.0 / 16777216.0)
+    return torch.from_numpy(np.float32(2.0) * u - np.float32(1.0))
+
+
+def test_fill_e4m3_matches_torch_rounding(ops):
+    """The device e4m3 encoder (RNE, saturating) agrees bit for bit with torch's
+    float8_e4m3fn conversion of the same uniform stream, replicated on the host."""
+    n = 1 << 16
+    t = ops.fill_uniform_(torch.empty((n,), dtype=torch.float8_e4m3fn, device="cuda"), 77)
+    want = _uniform_pm1_host(77, n).to(torch.float8_e4m3fn)
+    assert torch.equal(t.cpu().view(torch.uint8), want.view(torch.uint8))
+    f = t.float()
+    assert f.min() >= -1.0 and f.max() <= 1.0 and abs(f.mean().item()) < 2e-2
+    # the decoder, edge cases included, through the reference GEMM: A = x on the diagonal, B = I
+    vals = torch.tensor([0.0, 2 ** -9, 3 * 2 ** -10, 2 ** -6, 0.9375, 1.0, 448.0, 500.0, -17.0],
+                        device="cuda")
+    want = vals.to(torch.float8_e4m3fn)
+    a = torch.zeros((256, 256), device="cuda").to(torch.float8_e4m3fn)
+    a.view(torch.uint8)[torch.arange(9), torch.arange(9)] = want.view(torch.uint8)
+    eye = torch.eye(256, device="cuda").to(torch.float8_e4m3fn)
+    got = ops.ref_gemm_f32(a, eye).diagonal()[:9]   # torch maps 500 to NaN (0x7f): decoded too
+    assert torch.allclose(got, want.float(), rtol=0, atol=0, equal_nan=True)
+
+
+def test_gemm_fp8_vs_independent_reference(ops):
+    """K1-fp8 against the fp32-FMA reference kernel on device-filled e4m3."""
+    m = n = k = 1024
+    a = ops.fill_uniform_(torch.empty((m, k), dtype=torch.float8_e4m3fn, device="cuda"), 5)
+    b = ops.fill_uniform_(torch.empty((n, k), dtype=torch.float8_e4m3fn, device="cuda"), 6)
+    ref = ops.ref_gemm_f32(a, b)
+    assert torch.allclose(ref, a.float() @ b.float().T, atol=1e-4, rtol=1e-5)
+    atol, rtol = ops.gemm_tolerance(k)
+    assert ops.verify_bf16(ops.gemm_fp8(a, b), ref, atol, rtol).ok

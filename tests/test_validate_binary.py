@@ -64,6 +64,7 @@ def test_binary_passes_and_writes_sidecar_outputs(tmp_path):
     rep = _last_json(out)
     assert rep["passed"] and rep["gpus"][0]["gemm_wrong"] == 0
     assert rep["gpus"][0]["abft_bad_rows"] == 0
+    assert rep["gpus"][0]["gemm_fp8_wrong"] == 0 and rep["gpus"][0]["gemm_fp8_tflops"] > 0
     assert rep["gpus"][0]["hbm_read_GBps"] > 1000
     assert rep["start_epoch_s"] > 1.6e9 and rep["end_epoch_s"] >= rep["start_epoch_s"]
     t = json.loads(term.read_text())
@@ -71,12 +72,14 @@ def test_binary_passes_and_writes_sidecar_outputs(tmp_path):
     metrics = prom.read_text()
     assert "amdgpu_validate_passed 1" in metrics
     assert 'amdgpu_validate_gemm_tflops{gpu="0"}' in metrics
+    assert 'amdgpu_validate_gemm_fp8_tflops{gpu="0"}' in metrics
     assert json.loads(full.read_text()) == rep
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("kind,needle", [("corrupt_gemm", "GEMM verification failed"),
-                                         ("corrupt_abft", "ABFT")])
+                                         ("corrupt_abft", "ABFT"),
+                                         ("corrupt_fp8", "fp8 GEMM verification failed")])
 def test_binary_fault_injection_fails_loudly(tmp_path, kind, needle):
     _have_bin()
     term = tmp_path / "term"
@@ -86,6 +89,15 @@ def test_binary_fault_injection_fails_loudly(tmp_path, kind, needle):
     rep = _last_json(out)
     assert not rep["passed"] and any(needle in f for f in rep["failures"])
     assert json.loads(term.read_text())["passed"] is False
+
+
+@pytest.mark.gpu
+def test_binary_no_fp8_skips_the_fp8_check():
+    _have_bin()
+    rc, out, _ = _run("--size", "1024", "--iters", "3", "--no-fp8")
+    assert rc == 0
+    g = _last_json(out)["gpus"][0]
+    assert g["gemm_fp8_wrong"] is None and g["gemm_fp8_tflops"] == 0
 
 
 # ------------------------------------------------ validation image runtime

@@ -38,13 +38,44 @@ __global__ void __launch_bounds__(256)
   }
 }
 
+// e4m3 operands for K1-fp8: the same uniform [-1, 1) stream, rounded to e4m3,
+// 16 values (one 16-byte store) per lane per iteration.
+__global__ void __launch_bounds__(256)
+    fill_uniform_e4m3_kernel(uint8_t* __restrict__ out, size_t n, uint64_t seed, float scale) {
+  const size_t nvec = n / 16;
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  const size_t gid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (size_t v = gid; v < nvec; v += stride) {
+    typedef unsigned char u8x16 __attribute__((ext_vector_type(16)));
+    u8x16 o;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) o[j] = f32_to_e4m3_bits(scale * uniform_pm1(seed, v * 16 + j));
+    *(u8x16*)(out + v * 16) = o;
+  }
+  const size_t t0 = nvec * 16;
+  if (t0 + gid < n) out[t0 + gid] = f32_to_e4m3_bits(scale * uniform_pm1(seed, t0 + gid));
+}
+
 // ------------------------------------------------- K3: fp32 reference GEMM
 // Straightforward LDS-tiled fp32 FMA GEMM, C_ref = A * B^T. Independent of
 // the MFMA path on purpose (different unit, different summation order) so a
 // systematic error in K1 cannot cancel against its own reference.
 constexpr int kRefTile = 32;
+
+template <typename T>
+__device__ __forceinline__ float ref_load(const T* p, size_t i);
+template <>
+__device__ __forceinline__ float ref_load<__bf16>(const __bf16* p, size_t i) {
+  return bf16_bits_to_f32(((const uint16_t*)p)[i]);
+}
+template <>
+__device__ __forceinline__ float ref_load<uint8_t>(const uint8_t* p, size_t i) {
+  return e4m3_bits_to_f32(p[i]);  // e4m3 operands of K1-fp8
+}
+
+template <typename T>
 __global__ void __launch_bounds__(256)
-    ref_gemm_f32_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B,
+    ref_gemm_f32_kernel(const T* __restrict__ A, const T* __restrict__ B,
                         float* __restrict__ C, int M, int N, int K, int lda,
                         int ldb, int ldc) {
   __shared__ float As[kRefTile][kRefTile + 1];
@@ -59,12 +90,8 @@ __global__ void __launch_bounds__(256)
     for (int i = 0; i < 4; ++i) {
       const int r = ty * 4 + i;
       const int ga = row0 + r, gb = col0 + r, gk = k0 + tx;
-      As[r][tx] = (ga < M && gk < K)
-                      ? bf16_bits_to_f32(((const uint16_t*)A)[(size_t)ga * lda + gk])
-                      : 0.f;
-      Bs[r][tx] = (gb < N && gk < K)
-                      ? bf16_bits_to_f32(((const uint16_t*)B)[(size_t)gb * ldb + gk])
-                      : 0.f;
+      As[r][tx] = (ga < M && gk < K) ? ref_load(A, (size_t)ga * lda + gk) : 0.f;
+      Bs[r][tx] = (gb < N && gk < K) ? ref_load(B, (size_t)gb * ldb + gk) : 0.f;
     }
     __syncthreads();
 #pragma unroll 8

@@ -40,6 +40,58 @@ __host__ __device__ inline float bf16_bits_to_f32(uint16_t h) {
   return f;
 }
 
+// OCP e4m3 ("fn": no infinities, S.1111.111 is NaN, max 448) <-> f32.
+// Round-to-nearest-even with saturation to +-448, matching torch's
+// float8_e4m3fn conversion (tests/test_kernels_gpu.py pins the equality).
+__host__ __device__ inline uint8_t f32_to_e4m3_bits(float f) {
+  uint32_t u;
+  __builtin_memcpy(&u, &f, 4);
+  const uint32_t sign = (u >> 24) & 0x80u;
+  u &= 0x7fffffffu;
+  if (u > 0x7f800000u) return (uint8_t)(sign | 0x7f);  // NaN
+  float a;
+  __builtin_memcpy(&a, &u, 4);
+  uint32_t code;
+  const int E = (int)(u >> 23) - 127;
+  if (E < -6) {  // subnormal range: units of 2^-9, RNE (code 8 == smallest normal)
+    const float q = a * 512.0f;
+    uint32_t m = (uint32_t)q;
+    const float rem = q - (float)m;
+    if (rem > 0.5f || (rem == 0.5f && (m & 1u))) ++m;
+    code = m;
+  } else {
+    uint32_t r = (u & 0x7fffffu) >> 20;
+    const uint32_t rem = u & 0xfffffu, half = 0x80000u;
+    if (rem > half || (rem == half && (r & 1u))) ++r;
+    int e = E + 7;
+    if (r == 8) {
+      r = 0;
+      ++e;
+    }
+    if (e > 15 || (e == 15 && r == 7)) {  // saturate to 448 = S.1111.110
+      e = 15;
+      r = 6;
+    }
+    code = ((uint32_t)e << 3) | r;
+  }
+  return (uint8_t)(sign | code);
+}
+
+__host__ __device__ inline float e4m3_bits_to_f32(uint8_t v) {
+  const int e = (v >> 3) & 0xf, m = v & 7;
+  float f;
+  if (e == 0xf && m == 7) {
+    uint32_t q = 0x7fc00000u;
+    __builtin_memcpy(&f, &q, 4);
+    return f;
+  }
+  if (e == 0)
+    f = (float)m * (1.0f / 512.0f);
+  else
+    f = (1.0f + (float)m * 0.125f) * __builtin_ldexpf(1.0f, e - 7);
+  return (v & 0x80) ? -f : f;
+}
+
 // Stateless counter-based hash (splitmix64 finaliser). Used for the
 // synthetic uniform [-1, 1) operands so every rank / run is reproducible
 // from (seed, index) without any host->device copy.

@@ -90,22 +90,22 @@ __global__ void __launch_bounds__(256) mfma_rate_kernel(int iters, unsigned seed
   f32x4 acc[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  typedef int i32x4 __attribute__((ext_vector_type(4)));
+  const i32x4 al = {a[0], a[1], a[2], a[3]}, bl = {b[0], b[1], b[2], b[3]};
   const unsigned long long t0 = __builtin_amdgcn_s_memtime();
   const unsigned long long r0 = __builtin_amdgcn_s_memrealtime();
   for (int it = 0; it < iters; ++it) {
+    // in-place AGPR accumulators (asm): the builtin form let hipcc rotate the
+    // 8 accumulators through v_accvgpr_mov chains every iteration
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      if constexpr (F8) {
-        acc[j] = mfma_f8(a, b, acc[j]);
-      } else {
-        typedef int i32x4 __attribute__((ext_vector_type(4)));
-        const i32x4 al = {a[0], a[1], a[2], a[3]}, bl = {b[0], b[1], b[2], b[3]};
-        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, al),
-                                                         __builtin_bit_cast(bf16x8, bl),
-                                                         acc[j], 0, 0, 0);
-      }
+      if constexpr (F8)
+        ::ntm::gemm::mfma_f8_agpr(acc[j], a, b);
+      else
+        asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[j]) : "v"(al), "v"(bl));
     }
   }
+  ::ntm::gemm::mfma_drain();
   float s = 0.f;
 #pragma unroll
   for (int j = 0; j < 8; ++j) s += acc[j][0] + acc[j][1] + acc[j][2] + acc[j][3];

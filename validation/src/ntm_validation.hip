@@ -261,9 +261,30 @@ NTM_API int ntm_ref_gemm_f32(const void* A, const void* B, float* C, int M,
   if (M <= 0 || N <= 0 || K <= 0) return (int)hipErrorInvalidValue;
   dim3 grid((N + ntm::aux::kRefTile - 1) / ntm::aux::kRefTile,
             (M + ntm::aux::kRefTile - 1) / ntm::aux::kRefTile);
-  hipLaunchKernelGGL(ntm::aux::ref_gemm_f32_kernel, grid, dim3(256), 0,
+  hipLaunchKernelGGL(ntm::aux::ref_gemm_f32_kernel<__bf16>, grid, dim3(256), 0,
                      S(stream), (const __bf16*)A, (const __bf16*)B, C, M, N, K,
                      lda, ldb, ldc);
+  return (int)hipGetLastError();
+}
+
+// K3 for K1-fp8: e4m3 operands (uniform [-1, 1) rounded RNE) and the fp32
+// FMA reference over their exact values.
+NTM_API int ntm_fill_uniform_e4m3(void* out, size_t n, unsigned long long seed, float scale,
+                                  void* stream) {
+  if (n == 0) return 0;
+  const unsigned grid = stream_grid((n + 15) / 16, 256);
+  hipLaunchKernelGGL(ntm::aux::fill_uniform_e4m3_kernel, dim3(grid), dim3(256), 0, S(stream),
+                     (uint8_t*)out, n, (uint64_t)seed, scale);
+  return (int)hipGetLastError();
+}
+
+NTM_API int ntm_ref_gemm_f32_e4m3(const void* A, const void* B, float* C, int M, int N, int K,
+                                  int lda, int ldb, int ldc, void* stream) {
+  if (M <= 0 || N <= 0 || K <= 0) return (int)hipErrorInvalidValue;
+  dim3 grid((N + ntm::aux::kRefTile - 1) / ntm::aux::kRefTile,
+            (M + ntm::aux::kRefTile - 1) / ntm::aux::kRefTile);
+  hipLaunchKernelGGL(ntm::aux::ref_gemm_f32_kernel<uint8_t>, grid, dim3(256), 0, S(stream),
+                     (const uint8_t*)A, (const uint8_t*)B, C, M, N, K, lda, ldb, ldc);
   return (int)hipGetLastError();
 }
 

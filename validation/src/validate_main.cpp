@@ -48,6 +48,10 @@ constexpr int kMaxRanks = 8;  // = ntm/xgmi_allreduce.hpp (kernels live in its .
 extern "C" {
 int ntm_gemm_bf16(const void*, const void*, void*, int, int, int, int, int, int, void*);
 int ntm_gemm_shape_ok(int, int, int);
+int ntm_gemm_fp8(const void*, const void*, void*, int, int, int, int, int, int, void*);
+int ntm_gemm_fp8_shape_ok(int, int, int);
+int ntm_fill_uniform_e4m3(void*, size_t, unsigned long long, float, void*);
+int ntm_ref_gemm_f32_e4m3(const void*, const void*, float*, int, int, int, int, int, int, void*);
 int ntm_fill_uniform_bf16(void*, size_t, unsigned long long, float, void*);
 int ntm_ref_gemm_f32(const void*, const void*, float*, int, int, int, int, int, int, void*);
 int ntm_verify_bf16(const void*, const float*, size_t, float, float, void*, void*);
@@ -98,6 +102,8 @@ struct Opts {
   double hbm_floor_gbps = 0;
   long allreduce_max_mib = 1024;
   bool xgmi = true;
+  bool fp8 = true;              // K1-fp8 check of the e4m3 MX-scaled matrix path
+  double fp8_tflops_floor = 0;
   bool json = true;
   std::string out;
   std::string termination_log;  // k8s terminationMessagePath (<= 4 KiB summary)
@@ -110,11 +116,13 @@ void usage() {
   std::fprintf(stderr,
                "usage: amdgpu-validate [--gpus N] [--size 8192] [--iters 50]\n"
                "       [--tflops-floor TF] [--min-hbm-gb GB] [--hbm-floor-gbps GBps]\n"
-               "       [--allreduce-max-mib MiB] [--no-xgmi] [--json] [--out FILE]\n"
+               "       [--allreduce-max-mib MiB] [--no-xgmi] [--no-fp8] [--fp8-tflops-floor TF]\n"
+               "       [--json] [--out FILE]\n"
                "       [--termination-log FILE] [--prom-out FILE] [--fault-inject KIND]\n"
                "       [--pushgateway http://host:port]\n"
                "fault-inject (also env NTM_FAULT_INJECT): corrupt_gemm | corrupt_abft |\n"
-               "       corrupt_allreduce - corrupts the LAST GPU's data to prove detection\n");
+               "       corrupt_fp8 | corrupt_allreduce - corrupts the LAST GPU's data to prove\n"
+               "       detection\n");
 }
 
 bool parse(int argc, char** argv, Opts& o) {
@@ -136,6 +144,8 @@ bool parse(int argc, char** argv, Opts& o) {
     else if (a == "--hbm-floor-gbps") { if (!(v = next(a.c_str()))) return false; o.hbm_floor_gbps = std::atof(v); }
     else if (a == "--allreduce-max-mib") { if (!(v = next(a.c_str()))) return false; o.allreduce_max_mib = std::atol(v); }
     else if (a == "--no-xgmi") o.xgmi = false;
+    else if (a == "--no-fp8") o.fp8 = false;
+    else if (a == "--fp8-tflops-floor") { if (!(v = next(a.c_str()))) return false; o.fp8_tflops_floor = std::atof(v); }
     else if (a == "--json") o.json = true;
     else if (a == "--out") { if (!(v = next("--out"))) return false; o.out = v; }
     else if (a == "--termination-log") { if (!(v = next(a.c_str()))) return false; o.termination_log = v; }
@@ -225,6 +235,9 @@ struct GpuResult {
   unsigned long long abft_bad_acc = ~0ull, abft_bad_store = ~0ull;
   float abft_max_rel_acc = NAN;
   double abft_tflops = 0;
+  double fp8_ms = 0, fp8_tflops = 0;
+  unsigned long long fp8_bad = ~0ull;  // stays ~0 when --no-fp8
+  float fp8_max_err = NAN;
   double hbm_copy_gbps = 0, hbm_read_gbps = 0;
   bool hbm_copy_ok = false;
   double t_init = 0, t_gemm = 0, t_hbm = 0;
@@ -338,6 +351,43 @@ bool run_gpu(int dev, bool last, const Opts& o, GpuResult& r) {
   }
   CK(hipFree(A));
   CK(hipFree(B));
+
+  // ---- K1-fp8: the same schedule on e4m3 operands (MX-scaled MFMA, unit
+  // scales), checked element-wise against the fp32 reference of the e4m3 values
+  if (o.fp8 && ntm_gemm_fp8_shape_ok(n, n, n)) {
+    void *A8, *B8;
+    CK(hipMalloc(&A8, e));
+    CK(hipMalloc(&B8, e));
+    CK(hipMalloc(&R, e * 4));
+    CK(ntm_fill_uniform_e4m3(A8, e, 3000 + 2 * dev, 1.0f, s));
+    CK(ntm_fill_uniform_e4m3(B8, e, 3001 + 2 * dev, 1.0f, s));
+    CK(ntm_gemm_fp8(A8, B8, C, n, n, n, n, n, n, s));
+    if (last && o.fault == "corrupt_fp8") {
+      uint16_t h;
+      CK(hipMemcpyAsync(&h, (uint16_t*)C + 777, 2, hipMemcpyDeviceToHost, s));
+      CK(hipStreamSynchronize(s));
+      h ^= 0x0100;
+      CK(hipMemcpyAsync((uint16_t*)C + 777, &h, 2, hipMemcpyHostToDevice, s));
+    }
+    CK(ntm_ref_gemm_f32_e4m3(A8, B8, R, n, n, n, n, n, n, s));
+    CK(hipMemsetAsync(V, 0, 64, s));
+    CK(ntm_verify_bf16(C, R, e, atol, std::ldexp(1.0f, -7), V, s));
+    CK(hipMemcpyAsync(vr, V, ntm_verify_result_bytes(), hipMemcpyDeviceToHost, s));
+    CK(hipStreamSynchronize(s));
+    std::memcpy(&r.fp8_bad, vr, 8);
+    std::memcpy(&r.fp8_max_err, vr + 8, 4);
+    CK(hipFree(R));
+    for (int i = 0; i < 5; ++i) CK(ntm_gemm_fp8(A8, B8, C, n, n, n, n, n, n, s));
+    CK(hipEventRecord(e0, s));
+    for (int i = 0; i < o.iters; ++i) CK(ntm_gemm_fp8(A8, B8, C, n, n, n, n, n, n, s));
+    CK(hipEventRecord(e1, s));
+    CK(hipEventSynchronize(e1));
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    r.fp8_ms = ms / o.iters;
+    r.fp8_tflops = 2.0 * n * (double)n * n / (r.fp8_ms * 1e-3) / 1e12;
+    CK(hipFree(A8));
+    CK(hipFree(B8));
+  }
   CK(hipFree(C));
   CK(hipFree(V));
   r.t_gemm = wall_now();
@@ -676,6 +726,12 @@ int main(int argc, char** argv) {
            std::to_string(r.abft_bad_store) + " stored rows)");
     if (o.tflops_floor > 0 && r.gemm_tflops < o.tflops_floor)
       fail(d + "GEMM " + jnum(r.gemm_tflops) + " TFLOP/s below floor " + jnum(o.tflops_floor));
+    if (o.fp8 && r.fp8_bad != 0)
+      fail(d + "fp8 GEMM verification failed (" +
+           (r.fp8_bad == ~0ull ? std::string("not run: --size must be a multiple of 256")
+                               : std::to_string(r.fp8_bad) + " elements") + ")");
+    if (o.fp8 && o.fp8_tflops_floor > 0 && r.fp8_tflops < o.fp8_tflops_floor)
+      fail(d + "fp8 GEMM " + jnum(r.fp8_tflops) + " TFLOP/s below floor " + jnum(o.fp8_tflops_floor));
     if (o.min_hbm_gb > 0 && r.total_gb < o.min_hbm_gb)
       fail(d + "HBM " + jnum(r.total_gb) + " GB below " + jnum(o.min_hbm_gb) + " GB");
     if (!r.hbm_copy_ok) fail(d + "HBM copy mismatch");
@@ -708,6 +764,11 @@ int main(int argc, char** argv) {
       << "# TYPE amdgpu_validate_gemm_tflops gauge\n";
     for (auto& r : res)
       p << "amdgpu_validate_gemm_tflops{gpu=\"" << r.device << "\"} " << jnum(r.gemm_tflops) << "\n";
+    if (o.fp8) {
+      p << "# TYPE amdgpu_validate_gemm_fp8_tflops gauge\n";
+      for (auto& r : res)
+        p << "amdgpu_validate_gemm_fp8_tflops{gpu=\"" << r.device << "\"} " << jnum(r.fp8_tflops) << "\n";
+    }
     p << "# TYPE amdgpu_validate_hbm_copy_gbps gauge\n";
     for (auto& r : res)
       p << "amdgpu_validate_hbm_copy_gbps{gpu=\"" << r.device << "\"} " << jnum(r.hbm_copy_gbps) << "\n";
@@ -742,6 +803,9 @@ int main(int argc, char** argv) {
           ",\"abft_bad_rows\":" + (r.abft_bad_acc == ~0ull ? std::string("null")
                                      : std::to_string(r.abft_bad_acc + r.abft_bad_store)) +
           ",\"abft_max_rel_err\":" + jnum(r.abft_max_rel_acc) +
+          ",\"gemm_fp8_tflops\":" + jnum(r.fp8_tflops) +
+          ",\"gemm_fp8_wrong\":" + (r.fp8_bad == ~0ull ? std::string("null") : std::to_string(r.fp8_bad)) +
+          ",\"gemm_fp8_max_abs_err\":" + jnum(r.fp8_max_err) +
           ",\"hbm_copy_GBps\":" + jnum(r.hbm_copy_gbps) +
           ",\"hbm_read_GBps\":" + jnum(r.hbm_read_gbps) + "}";
   }
