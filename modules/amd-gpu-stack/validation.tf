@@ -10,16 +10,19 @@
   xGMI. Job completion timestamp == end of time-to-GPU-ready.
 ********************************************/
 locals {
-  validation_args = [
+  validation_args = concat([
     "--gpus", tostring(var.validation_gpu_count),
     "--size", tostring(var.validation_gemm_size),
     "--tflops-floor", tostring(var.validation_tflops_floor),
     "--min-hbm-gb", tostring(var.validation_min_hbm_gb),
     "--allreduce-max-mib", tostring(var.validation_allreduce_max_mib),
     "--json",
+  ], var.validation_fp8 ? [
+    "--fp8-tflops-floor", tostring(var.validation_fp8_tflops_floor),
+  ] : ["--no-fp8"], [
     # one-line verdict surfaced as the pod's termination message
     "--termination-log", "/dev/termination-log",
-  ]
+  ])
   validation_env = merge({
     # RCCL over the xGMI mesh inside one node; no host network transport needed
     NCCL_IB_DISABLE      = "1"

@@ -215,7 +215,24 @@ variable "validation_gemm_size" {
 variable "validation_tflops_floor" {
   type        = number
   default     = 1000
-  description = "Per-GPU bf16 GEMM TFLOP/s below which the Job fails (MI355X dense bf16 peak ~2500; the hand-written kernel measures ~1490 at 8192^3)."
+  description = "Per-GPU bf16 GEMM TFLOP/s below which the Job fails (MI355X dense bf16 peak ~2500; the hand-written kernel measures ~1600 at 8192^3)."
+}
+
+variable "validation_fp8" {
+  type        = bool
+  default     = true
+  description = "Also run and verify the OCP e4m3 GEMM on the MX-scaled matrix cores (K1-fp8)."
+}
+
+variable "validation_fp8_tflops_floor" {
+  type        = number
+  default     = 2000
+  description = "Per-GPU e4m3 GEMM TFLOP/s below which the Job fails (the hand-written kernel measures ~3100 at 8192^3; 0 disables the floor)."
+
+  validation {
+    condition     = var.validation_fp8_tflops_floor >= 0
+    error_message = "validation_fp8_tflops_floor must be >= 0."
+  }
 }
 
 variable "validation_min_hbm_gb" {

@@ -78,13 +78,15 @@ def gemm_fp8_shape_ok(m: int, n: int, k: int) -> bool:
     return bool(lib().ntm_gemm_fp8_shape_ok(m, n, k))
 
 
-def gemm_fp8(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+def gemm_fp8(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
+             knob: int = 0) -> torch.Tensor:
     """K1-fp8: ``out = a @ b.T`` with OCP e4m3 operands (``torch.float8_e4m3fn``),
     fp32 accumulation on the MX-scaled MFMA path (unit scales), bf16 output.
 
     a: [M, K], b: [N, K] (K-contiguous, rows 16-byte aligned), out: [M, N] bf16.
     M, N % 256 and K % 256. Same 8-wave schedule and LDS image as the bf16
-    default; twice the MFMA rate per clock.
+    default; twice the MFMA rate per clock. ``knob`` != 0 selects an
+    experimental schedule variant (gemm_fp8.hpp ``launch_gemm_fp8_knob``).
     """
     _require(a, "a", torch.float8_e4m3fn)
     _require(b, "b", torch.float8_e4m3fn)
@@ -99,8 +101,13 @@ def gemm_fp8(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None) 
     _require(out, "out", torch.bfloat16)
     if tuple(out.shape) != (m, n):
         raise ValueError("out has the wrong shape")
-    rc = lib().ntm_gemm_fp8(a.data_ptr(), b.data_ptr(), out.data_ptr(), m, n, k, a.stride(0),
-                            b.stride(0), out.stride(0), stream_handle())
+    if knob:
+        rc = lib().ntm_gemm_fp8_knob(a.data_ptr(), b.data_ptr(), out.data_ptr(), m, n, k,
+                                     a.stride(0), b.stride(0), out.stride(0), int(knob),
+                                     stream_handle())
+    else:
+        rc = lib().ntm_gemm_fp8(a.data_ptr(), b.data_ptr(), out.data_ptr(), m, n, k,
+                                a.stride(0), b.stride(0), out.stride(0), stream_handle())
     check(rc, "ntm_gemm_fp8")
     return out
 

@@ -138,3 +138,29 @@ def test_cli_plan_json():
     assert p.returncode == 1                      # admin_group_object_ids is required
     assert any("admin_group_object_ids" in e for e in d["errors"])
     assert d["summary"].startswith("Plan: ")
+
+
+def _stack_local(name, **overrides):
+    """Evaluate local.<name> of modules/amd-gpu-stack with variable defaults + overrides."""
+    from nvidia_terraform_modules_amd.tfcheck.config import load_module
+
+    mod = load_module(ROOT / "modules" / "amd-gpu-stack")
+    ev = Evaluator()
+    variables = {}
+    for vn, v in mod.variables.items():
+        if vn in overrides:
+            variables[vn] = overrides[vn]
+        elif not v.required:
+            variables[vn] = convert(ev.eval(v.block.body.attr("default"), Scope({}, {})),
+                                    v.type_expr)
+    scope = Scope(variables, {n: e for n, (e, _, _) in mod.locals.items()}, str(mod.path))
+    return ev.eval(mod.locals[name][0], scope)
+
+
+def test_validation_job_args_carry_the_fp8_check():
+    args = _stack_local("validation_args")
+    i = args.index("--fp8-tflops-floor")
+    assert float(args[i + 1]) == 2000 and "--no-fp8" not in args
+    assert args[-2:] == ["--termination-log", "/dev/termination-log"]
+    off = _stack_local("validation_args", validation_fp8=False)
+    assert "--no-fp8" in off and "--fp8-tflops-floor" not in off

@@ -37,7 +37,9 @@ def main() -> int:
     ap.add_argument("--sizes", default="4096,8192")
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--knobs", default="", help="comma list of experimental fp8 knobs to time too")
     args = ap.parse_args()
+    knobs = [int(x) for x in args.knobs.split(",") if x]
     dev = torch.device("cuda:0")
     ok_all = True
     for s in [int(x) for x in args.sizes.split(",")]:
@@ -56,6 +58,12 @@ def main() -> int:
         cb = torch.empty((s, s), dtype=torch.bfloat16, device=dev)
         fns = {"ours_fp8": lambda: ops.gemm_fp8(a, b, c),
                "ours_bf16": lambda: ops.gemm_bf16(ab, bb, cb)}
+        for kn in knobs:
+            ck = ops.gemm_fp8(a, b, knob=kn)
+            kbad = int(((ck.float() - c.float()).abs() > 1e-2 * (1 + c.float().abs())).sum())
+            ok_all &= kbad == 0
+            print(json.dumps({"size": s, "knob": kn, "mismatch_vs_default": kbad}), flush=True)
+            fns[f"knob{kn}_fp8"] = (lambda kn=kn: ops.gemm_fp8(a, b, c, knob=kn))
         one = torch.ones((), device=dev)
         try:
             torch._scaled_mm(a, b.T, scale_a=one, scale_b=one, out_dtype=torch.bfloat16)

@@ -1,6 +1,6 @@
 """Split GEMM time into K-loop cost and fixed per-tile overhead: time at
 fixed M = N over several K, least-squares fit t = a + b * K, for our K1 and
-for torch.matmul (hipBLASLt). Interleaved rounds, CUDA events."""
+for torch.matmul (hipBLASLt); --dtype fp8: K1-fp8 vs torch._scaled_mm. Interleaved rounds, CUDA events."""
 import argparse
 import json
 import os
@@ -30,18 +30,27 @@ def main():
     ap.add_argument("--ks", default="1024,2048,4096,8192,16384")
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--variant", default="default")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"])
     args = ap.parse_args()
+    fp8 = args.dtype == "fp8"
+    dt = torch.float8_e4m3fn if fp8 else torch.bfloat16
+    one = torch.ones((), device="cuda")
     mn = args.mn
     ks = [int(k) for k in args.ks.split(",")]
     res = {}
     for k in ks:
-        a = ops.fill_uniform_(torch.empty((mn, k), dtype=torch.bfloat16, device="cuda"), 1)
-        b = ops.fill_uniform_(torch.empty((mn, k), dtype=torch.bfloat16, device="cuda"), 2)
+        a = ops.fill_uniform_(torch.empty((mn, k), dtype=dt, device="cuda"), 1)
+        b = ops.fill_uniform_(torch.empty((mn, k), dtype=dt, device="cuda"), 2)
         c = torch.empty((mn, mn), dtype=torch.bfloat16, device="cuda")
         ours, theirs = [], []
         for _ in range(args.rounds):
-            ours.append(timed(lambda: ops.gemm_bf16(a, b, c, variant=args.variant), 20))
-            theirs.append(timed(lambda: torch.matmul(a, b.T, out=c), 20))
+            if fp8:
+                ours.append(timed(lambda: ops.gemm_fp8(a, b, c), 20))
+                theirs.append(timed(lambda: torch._scaled_mm(a, b.T, scale_a=one, scale_b=one,
+                                                             out_dtype=torch.bfloat16), 20))
+            else:
+                ours.append(timed(lambda: ops.gemm_bf16(a, b, c, variant=args.variant), 20))
+                theirs.append(timed(lambda: torch.matmul(a, b.T, out=c), 20))
         res[k] = (sorted(ours)[len(ours) // 2], sorted(theirs)[len(theirs) // 2])
         print(json.dumps({"k": k, "ours_us": res[k][0], "torch_us": res[k][1],
                           "ours_tf": 2 * mn * mn * k / res[k][0] / 1e6,

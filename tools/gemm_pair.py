@@ -22,8 +22,11 @@ def main() -> int:
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--which", default="both", choices=["both", "ours", "torch", "all"])
     ap.add_argument("--variant", default="default")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"])
     args = ap.parse_args()
     s = args.size
+    if args.dtype == "fp8":
+        return fp8_pair(s, args.iters, args.which)
     a = torch.empty((s, s), dtype=torch.bfloat16, device="cuda")
     b = torch.empty((s, s), dtype=torch.bfloat16, device="cuda")
     c = torch.empty((s, s), dtype=torch.bfloat16, device="cuda")
@@ -36,6 +39,21 @@ def main() -> int:
             ops.gemm_bf16(a, b, c, variant="pingpong8")
         if args.which in ("both", "torch", "all"):
             torch.matmul(a, b.T, out=c)
+    torch.cuda.synchronize()
+    return 0
+
+
+def fp8_pair(s: int, iters: int, which: str) -> int:
+    """K1-fp8 vs hipBLASLt's fp8 GEMM (torch._scaled_mm, unit scales, bf16 out)."""
+    a = ops.fill_uniform_(torch.empty((s, s), dtype=torch.float8_e4m3fn, device="cuda"), 1)
+    b = ops.fill_uniform_(torch.empty((s, s), dtype=torch.float8_e4m3fn, device="cuda"), 2)
+    c = torch.empty((s, s), dtype=torch.bfloat16, device="cuda")
+    one = torch.ones((), device="cuda")
+    for _ in range(iters):
+        if which in ("both", "ours", "all"):
+            ops.gemm_fp8(a, b, c)
+        if which in ("both", "torch", "all"):
+            torch._scaled_mm(a, b.T, scale_a=one, scale_b=one, out_dtype=torch.bfloat16)
     torch.cuda.synchronize()
     return 0
 

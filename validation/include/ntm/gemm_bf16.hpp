@@ -197,14 +197,25 @@ __device__ __forceinline__ void mfma_drain() {
   asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");
 }
 
+// ORD 1: A-fragment outer (srcB held for 2 MFMAs); ORD 2 (experimental, knob 1):
+// B-fragment outer (srcA held for 4 MFMAs).
+template <int ORD = 1>
 __device__ __forceinline__ void mma_quadrant_f8(f32x4 (&acc)[4][2],
                                                 const bf16x8 (&a)[4][2],
                                                 const bf16x8 (&b)[2][2]) {
-#pragma unroll
-  for (int mt = 0; mt < 4; ++mt)
+  if constexpr (ORD == 2) {
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt)
-      mfma_f8_agpr(acc[mt][nt], cat_f8(b[nt][0], b[nt][1]), cat_f8(a[mt][0], a[mt][1]));
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+        mfma_f8_agpr(acc[mt][nt], cat_f8(b[nt][0], b[nt][1]), cat_f8(a[mt][0], a[mt][1]));
+  } else {
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt)
+        mfma_f8_agpr(acc[mt][nt], cat_f8(b[nt][0], b[nt][1]), cat_f8(a[mt][0], a[mt][1]));
+  }
 }
 
 // One phase of the K loop. P: phase within the K-tile (0..3); ISSUE: whether

@@ -55,7 +55,7 @@ __device__ __forceinline__ void issue_half3(const Ctx& c, int kt, int buf, int T
   glds16(s + 32, d + 1024);
 }
 
-template <int P, bool ODD, bool PRIO, bool F8 = false>
+template <int P, bool ODD, bool PRIO, int F8 = 0>
 __device__ __forceinline__ void phase3(const Ctx& c, Frags3& f,
                                        f32x4 (&acc)[2][2][4][2], int t, int T) {
   bf16x8(&bcur)[2][2] = ODD ? f.b1 : f.b0;
@@ -72,10 +72,10 @@ __device__ __forceinline__ void phase3(const Ctx& c, Frags3& f,
   wait_vmcnt<10>();
   raw_barrier();
   if constexpr (F8) {
-    if constexpr (P == 0) mma_quadrant_f8(acc[0][0], f.a, bcur);
-    if constexpr (P == 1) mma_quadrant_f8(acc[0][1], f.a, both);
-    if constexpr (P == 2) mma_quadrant_f8(acc[1][1], f.a, both);
-    if constexpr (P == 3) mma_quadrant_f8(acc[1][0], f.a, bcur);
+    if constexpr (P == 0) mma_quadrant_f8<F8>(acc[0][0], f.a, bcur);
+    if constexpr (P == 1) mma_quadrant_f8<F8>(acc[0][1], f.a, both);
+    if constexpr (P == 2) mma_quadrant_f8<F8>(acc[1][1], f.a, both);
+    if constexpr (P == 3) mma_quadrant_f8<F8>(acc[1][0], f.a, bcur);
   } else {
     if constexpr (P == 0) mma_quadrant<PRIO>(acc[0][0], f.a, bcur);
     if constexpr (P == 1) mma_quadrant<PRIO>(acc[0][1], f.a, both);
@@ -85,7 +85,7 @@ __device__ __forceinline__ void phase3(const Ctx& c, Frags3& f,
   raw_barrier();
 }
 
-template <bool ODD, bool PRIO, bool F8 = false>
+template <bool ODD, bool PRIO, int F8 = 0>
 __device__ __forceinline__ void tile3(const Ctx& c, Frags3& f,
                                       f32x4 (&acc)[2][2][4][2], int t, int T) {
   phase3<0, ODD, PRIO, F8>(c, f, acc, t, T);
@@ -104,10 +104,11 @@ __device__ __forceinline__ void tile3(const Ctx& c, Frags3& f,
 // runs its last MFMA segment, before the stagger-balancing barrier).
 // SPRIO: static s_setprio(1) for the whole K loop on wave row SPRIO - 1
 // (0 = off); MI355X_MICROARCH.md "Two waves per SIMD" item 4.
-// F8: the operands are OCP e4m3 (K1-fp8, gemm_fp8.hpp); p's K / lda / ldb are
-// then counted in bf16-sized pairs of fp8 values (the LDS image is the same).
+// F8 (nonzero): the operands are OCP e4m3 (K1-fp8, gemm_fp8.hpp); p's K / lda /
+// ldb are then counted in bf16-sized pairs of fp8 values (the LDS image is the
+// same); the value is mma_quadrant_f8's MFMA order (1 = default).
 template <bool kRowSum, int GROUP_M = kGroupM, bool PRIO = false, int EPI = 0, int SPRIO = 0,
-          bool F8 = false>
+          int F8 = 0>
 __global__ void __launch_bounds__(kThreads, 2)
     gemm_bf16_pp3_kernel(GemmArgs p) {
   static_assert(!((EPI & kEpiLds) && (EPI & kEpiEarly)), "LDS staging needs all waves");

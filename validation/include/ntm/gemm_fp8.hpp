@@ -64,8 +64,43 @@ inline hipError_t launch_gemm_fp8(const void* A, const void* B, __bf16* C, int M
   a.ldc = ldc;
   const dim3 g((unsigned)((M / BM) * (N / BN))), b(kThreads);
   hipLaunchKernelGGL((::ntm::gemm3::gemm_bf16_pp3_kernel<false, kGroupM, false,
-                                                         ::ntm::gemm3::kEpiDefault, 0, true>),
+                                                         ::ntm::gemm3::kEpiDefault, 0, 1>),
                      g, b, 0, stream, a);
+  return hipGetLastError();
+}
+
+// Experimental knobs (tools/gemm_fp8_check.py --knobs): 0 = the default above;
+// 1 = B-fragment-outer MFMA order; 2 = GROUP_M 4; 3 = static s_setprio(1) on
+// wave row 1; 4 = register (widened + nontemporal) epilogue instead of the
+// LDS-staged one.
+inline hipError_t launch_gemm_fp8_knob(const void* A, const void* B, __bf16* C, int M, int N,
+                                       int K, int lda, int ldb, int ldc, int knob,
+                                       hipStream_t s) {
+  using namespace ::ntm::gemm;
+  using ::ntm::gemm3::gemm_bf16_pp3_kernel;
+  using ::ntm::gemm3::kEpiDefault;
+  if (!shape_ok(M, N, K) || lda < K || ldb < K || ldc < N || (lda % 16) || (ldb % 16) ||
+      (ldc % 8))
+    return hipErrorInvalidValue;
+  GemmArgs a;
+  a.A = (const __bf16*)A;
+  a.B = (const __bf16*)B;
+  a.C = C;
+  a.M = M;
+  a.N = N;
+  a.K = K / 2;
+  a.lda = lda / 2;
+  a.ldb = ldb / 2;
+  a.ldc = ldc;
+  const dim3 g((unsigned)((M / BM) * (N / BN))), b(kThreads);
+  switch (knob) {
+    case 0: return launch_gemm_fp8(A, B, C, M, N, K, lda, ldb, ldc, s);
+    case 1: hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, kGroupM, false, kEpiDefault, 0, 2>), g, b, 0, s, a); break;
+    case 2: hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, 4, false, kEpiDefault, 0, 1>), g, b, 0, s, a); break;
+    case 3: hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, kGroupM, false, kEpiDefault, 2, 1>), g, b, 0, s, a); break;
+    case 4: hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, kGroupM, false, kEpiWide | kEpiNT, 0, 1>), g, b, 0, s, a); break;
+    default: return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 

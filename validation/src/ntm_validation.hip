@@ -176,6 +176,13 @@ NTM_API int ntm_mfma_rate(int f8, int grid, int iters, void* out, float* sink, v
   return (int)hipGetLastError();
 }
 
+// EXPERIMENTAL: K1-fp8 schedule knobs (gemm_fp8.hpp launch_gemm_fp8_knob).
+NTM_API int ntm_gemm_fp8_knob(const void* A, const void* B, void* C, int M, int N, int K,
+                              int lda, int ldb, int ldc, int knob, void* stream) {
+  return (int)ntm::fp8::launch_gemm_fp8_knob(A, B, (__bf16*)C, M, N, K, lda, ldb, ldc, knob,
+                                             S(stream));
+}
+
 NTM_API int ntm_gemm_fp8_shape_ok(int M, int N, int K) {
   return ntm::fp8::shape_ok(M, N, K) ? 1 : 0;
 }
