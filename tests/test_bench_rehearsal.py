@@ -51,6 +51,8 @@ def test_torchrun_launch_one_json_line(nproc):
     assert len(lines) == 1, p.stdout[-2000:]          # rank 0 only
     d = lines[0]
     assert CONTRACT_KEYS <= set(d)
+    baseline = json.loads((ROOT / "BASELINE.json").read_text())
+    assert d["metric"] == baseline["metric"]                # BASELINE.json's metric, verbatim
     assert d["n_gpus"] == nproc and d["steps"] == 3 and d["warmup"] == 1
     assert d["config"]["parallelism"] == f"dp{nproc}" and d["config"]["global_batch"] == nproc
     assert d["higher_is_better"] is True and d["scaling"] == "weak" and d["dtype"] == "bf16"
