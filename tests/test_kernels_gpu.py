@@ -316,3 +316,18 @@ def test_gemm_fp8_vs_independent_reference(ops):
     assert torch.allclose(ref, a.float() @ b.float().T, atol=1e-4, rtol=1e-5)
     atol, rtol = ops.gemm_tolerance(k)
     assert ops.verify_bf16(ops.gemm_fp8(a, b), ref, atol, rtol).ok
+
+
+def test_gemm_fp8_plain_and_scaled_mfma_forms_agree_bitwise(ops):
+    """The default K1-fp8 issues v_mfma_f32_16x16x128_f8f6f4 without the scale
+    prefix; knob 5 is the same schedule on the MX-scaled form with unit E8M0
+    scales. Same products in the same order: the outputs must be identical."""
+    m, n, k = 512, 768, 1024
+    a = ops.fill_uniform_(torch.empty((m, k), dtype=torch.float8_e4m3fn, device="cuda"), 11)
+    b = ops.fill_uniform_(torch.empty((n, k), dtype=torch.float8_e4m3fn, device="cuda"), 12)
+    c0 = ops.gemm_fp8(a, b)
+    c5 = ops.gemm_fp8(a, b, knob=5)
+    assert torch.equal(c0.view(torch.int16), c5.view(torch.int16))
+    ref = a.float() @ b.float().T
+    atol, rtol = ops.gemm_tolerance(k)
+    assert ((c0.float() - ref).abs() <= atol + rtol * ref.abs()).all()

@@ -193,12 +193,28 @@ __device__ __forceinline__ void mfma_f8_agpr(f32x4& acc, const i32x8& a, const i
       : "v"(a), "v"(b), "v"(127));  // fmt e4m3 x e4m3 (cbsz = blgp = 0), E8M0 scale 2^0
 }
 
+// Experimental form (K1-fp8 knob 5): the plain f8f6f4 opcode without the
+// v_mfma_ld_scale_b32 prefix (8 instead of 16 bytes; hardware default scales).
+// (An SGPR scale operand does not assemble: the scales must be VGPRs.)
+__device__ __forceinline__ void mfma_f8_agpr_plain(f32x4& acc, const i32x8& a, const i32x8& b) {
+  asm("v_mfma_f32_16x16x128_f8f6f4 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+}
+
+template <int ORD>
+__device__ __forceinline__ void mfma_f8_ord(f32x4& acc, const i32x8& a, const i32x8& b) {
+  if constexpr (ORD == 3)
+    mfma_f8_agpr_plain(acc, a, b);
+  else
+    mfma_f8_agpr(acc, a, b);
+}
+
 __device__ __forceinline__ void mfma_drain() {
   asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");
 }
 
-// ORD 1: A-fragment outer (srcB held for 2 MFMAs); ORD 2 (experimental, knob 1):
-// B-fragment outer (srcA held for 4 MFMAs).
+// ORD 1: A-fragment outer (srcB held for 2 MFMAs); experimental: ORD 2 (knob 1)
+// B-fragment outer (srcA held for 4 MFMAs); ORD 3 (knob 5) the plain MFMA form
+// of mfma_f8_ord.
 template <int ORD = 1>
 __device__ __forceinline__ void mma_quadrant_f8(f32x4 (&acc)[4][2],
                                                 const bf16x8 (&a)[4][2],
@@ -214,7 +230,7 @@ __device__ __forceinline__ void mma_quadrant_f8(f32x4 (&acc)[4][2],
     for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt)
-        mfma_f8_agpr(acc[mt][nt], cat_f8(b[nt][0], b[nt][1]), cat_f8(a[mt][0], a[mt][1]));
+        mfma_f8_ord<ORD>(acc[mt][nt], cat_f8(b[nt][0], b[nt][1]), cat_f8(a[mt][0], a[mt][1]));
   }
 }
 
