@@ -133,3 +133,78 @@ resource "kubernetes_job_v1" "gpu_validation" {
     kubernetes_daemon_set_v1.amdgpu_dkms,
   ]
 }
+
+/********************************************
+  Validation image pre-pull
+  -------------------------
+  The Job can only schedule once amd.com/gpu is allocatable, i.e. after the
+  amdgpu driver is loaded on a GPU node (minutes: KMM/DKMS). Without help its
+  image pull starts only then and sits on the critical path. This DaemonSet
+  depends on nothing but the namespace, so it lands on every GPU node as the
+  node joins and pulls the image while the driver installs; its init
+  container runs `amdgpu-validate --help`, which also proves the image's
+  runtime-library closure links on the node before any GPU is up.
+  apply does not wait for its rollout (nodes may still be booting).
+********************************************/
+resource "kubernetes_daemon_set_v1" "validation_prepull" {
+  count = var.validation_enabled && var.prepull_validation_image ? 1 : 0
+
+  metadata {
+    name      = "amd-gpu-validation-prepull"
+    namespace = local.namespace
+    labels    = merge(local.common_labels, { "app.kubernetes.io/name" = "amd-gpu-validation-prepull" })
+  }
+
+  wait_for_rollout = false
+
+  spec {
+    selector {
+      match_labels = { "app.kubernetes.io/name" = "amd-gpu-validation-prepull" }
+    }
+    template {
+      metadata {
+        labels = merge(local.common_labels, { "app.kubernetes.io/name" = "amd-gpu-validation-prepull" })
+      }
+      spec {
+        node_selector = var.gpu_node_selector
+        toleration {
+          key      = var.gpu_node_taint_key
+          operator = "Exists"
+          effect   = "NoSchedule"
+        }
+        init_container {
+          name    = "pull-and-link-check"
+          image   = var.validation_image
+          command = ["/opt/ntm/bin/amdgpu-validate", "--help"]
+          security_context {
+            allow_privilege_escalation = false
+            read_only_root_filesystem  = true
+            capabilities {
+              drop = ["ALL"]
+            }
+          }
+        }
+        container {
+          name  = "hold"
+          image = var.pause_image
+          resources {
+            requests = {
+              cpu    = "1m"
+              memory = "8Mi"
+            }
+            limits = {
+              memory = "16Mi"
+            }
+          }
+          security_context {
+            allow_privilege_escalation = false
+            read_only_root_filesystem  = true
+            capabilities {
+              drop = ["ALL"]
+            }
+          }
+        }
+      }
+    }
+  }
+}

@@ -190,6 +190,18 @@ variable "validation_image" {
   description = "Image built from validation/image/Dockerfile (contains only the amdgpu-validate binary + ROCm runtime + RCCL)."
 }
 
+variable "prepull_validation_image" {
+  type        = bool
+  default     = true
+  description = "Pull the validation image on GPU nodes as they join (DaemonSet), in parallel with the driver install, so the Job starts the moment amd.com/gpu is allocatable."
+}
+
+variable "pause_image" {
+  type        = string
+  default     = "registry.k8s.io/pause:3.10"
+  description = "Image of the pre-pull DaemonSet's idle container."
+}
+
 variable "validation_gpu_count" {
   type        = number
   default     = 8

@@ -55,6 +55,12 @@ DEFAULT_DURATIONS = {
     "kubernetes_job_v1": 90.0,
 }
 
+# part of the Job's prior that is the image pull: hidden behind the driver
+# install when the pre-pull DaemonSet (modules/amd-gpu-stack/validation.tf)
+# is in the graph, since it pulls on each GPU node as the node joins
+IMAGE_PULL_S = 60.0
+PREPULL_MARK = "kubernetes_daemon_set_v1.validation_prepull"
+
 # extra readiness that happens INSIDE nodes after their Terraform resource
 # completed: driver install (DKMS build or operator KMM), device plugin
 # registration. Attributed to the node that waits on it.
@@ -115,13 +121,19 @@ def critical_path(g: Graph, durations: dict | None = None, stack_mode: str = "op
     dur = dict(DEFAULT_DURATIONS)
     dur.update(durations or {})
 
+    prepull = any(PREPULL_MARK in n for n in g.topo_order())
+
     def d(addr: str) -> float:
         if addr in dur:
             return dur[addr]
         t = node_type(addr)
         base = dur.get(t, 0.0)
         if t == "kubernetes_job_v1":
-            base += DRIVER_READY_S.get(stack_mode, 0.0)  # GPUs allocatable only after the driver
+            driver = DRIVER_READY_S.get(stack_mode, 0.0)  # GPUs allocatable only after the driver
+            pull = dur.get("image_pull", IMAGE_PULL_S)
+            if prepull:  # pulled while the driver installed: only the excess remains
+                base -= min(pull, driver)
+            base += driver
         return base
 
     finish: dict = {}

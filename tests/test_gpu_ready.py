@@ -107,6 +107,23 @@ def test_critical_path_uses_measured_durations(repo):
     assert faster < base
 
 
+def test_validation_image_prepull_is_off_the_path_and_hides_the_pull(repo, monkeypatch):
+    import nvidia_terraform_modules_amd.gpu_ready.critical_path as cpm
+
+    g = build_graph(repo / "eks")
+    pre = [n for n in g.topo_order() if cpm.PREPULL_MARK in n]
+    assert pre, "modules/amd-gpu-stack should pre-pull the validation image"
+    # it does not wait for the operator / driver stack, and nothing waits for it
+    assert not any("helm_release" in d or "daemon_set" in d for d in g.deps(pre[0]))
+    assert not any(pre[0] in g.deps(n) for n in g.topo_order())
+    job = lambda cp: dict(cp.path)[cp.path[-1][0]]  # noqa: E731
+    with_pull = critical_path(g)
+    monkeypatch.setattr(cpm, "PREPULL_MARK", "no-such-resource")
+    without = critical_path(g)
+    assert job(without) - job(with_pull) == pytest.approx(cpm.IMAGE_PULL_S)
+    assert with_pull.total_s < without.total_s
+
+
 # --------------------------------------------------------------- CLI record
 TF_STUB = r'''#!/usr/bin/env python3
 import json, sys, time
