@@ -228,3 +228,12 @@ def test_pushgateway_unreachable_is_not_fatal():
     rep = _last_json(out)
     assert rc == 0 and rep["passed"] is True
     assert rep["pushgateway"].startswith("error")
+
+
+def test_help_exits_zero_without_touching_the_gpu():
+    """The pre-pull DaemonSet's init container (modules/amd-gpu-stack/validation.tf)
+    runs `amdgpu-validate --help` on nodes whose driver may not be loaded yet:
+    it must link, print usage and exit 0 without any HIP call."""
+    _have_bin()
+    rc, out, err = _run("--help", timeout=60)
+    assert rc == 0 and "usage" in err
