@@ -6,8 +6,9 @@
   its helm_release count-gate on data.aws_instances never actually waits
   (eks/main.tf:186). Here `apply` blocks on a Job that requests amd.com/gpu
   (so it only schedules once the device plugin has registered GPUs) and runs
-  the hand-written HIP bf16 MFMA GEMM + HBM stream + RCCL all-reduce over
-  xGMI. Job completion timestamp == end of time-to-GPU-ready.
+  the hand-written HIP bf16 / fp8 MFMA GEMMs + HBM stream + RCCL all-reduce
+  over xGMI + a per-link xGMI pull matrix. Job completion timestamp == end of
+  time-to-GPU-ready.
 ********************************************/
 locals {
   validation_args = concat([
@@ -19,7 +20,9 @@ locals {
     "--json",
   ], var.validation_fp8 ? [
     "--fp8-tflops-floor", tostring(var.validation_fp8_tflops_floor),
-  ] : ["--no-fp8"], [
+  ] : ["--no-fp8"], var.validation_p2p_floor_gbps > 0 ? [
+    "--p2p-floor-gbps", tostring(var.validation_p2p_floor_gbps),
+  ] : [], [
     # one-line verdict surfaced as the pod's termination message
     "--termination-log", "/dev/termination-log",
   ])

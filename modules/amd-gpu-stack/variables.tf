@@ -247,6 +247,17 @@ variable "validation_fp8_tflops_floor" {
   }
 }
 
+variable "validation_p2p_floor_gbps" {
+  type        = number
+  default     = 0
+  description = "Per-link xGMI pull bandwidth (GB/s, dst <- src, one pair at a time) below which the Job fails; 0 reports the matrix without a floor."
+
+  validation {
+    condition     = var.validation_p2p_floor_gbps >= 0
+    error_message = "validation_p2p_floor_gbps must be >= 0."
+  }
+}
+
 variable "validation_min_hbm_gb" {
   type        = number
   default     = 250

@@ -164,3 +164,6 @@ def test_validation_job_args_carry_the_fp8_check():
     assert args[-2:] == ["--termination-log", "/dev/termination-log"]
     off = _stack_local("validation_args", validation_fp8=False)
     assert "--no-fp8" in off and "--fp8-tflops-floor" not in off
+    assert "--p2p-floor-gbps" not in args
+    p2p = _stack_local("validation_args", validation_p2p_floor_gbps=40)
+    assert p2p[p2p.index("--p2p-floor-gbps") + 1] == "40"

@@ -92,6 +92,30 @@ def test_binary_fault_injection_fails_loudly(tmp_path, kind, needle):
 
 
 @pytest.mark.gpu
+def test_binary_p2p_matrix_loopback_and_fault():
+    """C3 (per-link xGMI pull matrix) on one GPU: --p2p-loopback runs the pair
+    path as 0 <- 0; the copy is verified and a corrupted byte fails the Job."""
+    _have_bin()
+    rc, out, _ = _run("--size", "512", "--iters", "2", "--no-fp8")
+    g = _last_json(out)
+    assert rc == 0 and g["xgmi_p2p_GBps"] == [] and g["xgmi_p2p_min_GBps"] is None
+    rc, out, _ = _run("--size", "512", "--iters", "2", "--no-fp8", "--p2p-loopback",
+                      "--p2p-mib", "64")
+    g = _last_json(out)
+    assert rc == 0, g["failures"]
+    assert len(g["xgmi_p2p_GBps"]) == 1 and g["xgmi_p2p_GBps"][0][0] > 100
+    assert g["xgmi_p2p_bad_pairs"] == 0 and g["xgmi_p2p_min_GBps"] > 100
+    rc, out, _ = _run("--size", "512", "--iters", "2", "--no-fp8", "--p2p-loopback",
+                      "--p2p-mib", "64", env={"NTM_FAULT_INJECT": "corrupt_p2p"})
+    g = _last_json(out)
+    assert rc == 1 and g["xgmi_p2p_bad_pairs"] == 1
+    assert any("xGMI P2P copy" in f for f in g["failures"])
+    rc, out, _ = _run("--size", "512", "--iters", "2", "--no-fp8", "--p2p-loopback",
+                      "--p2p-mib", "64", "--p2p-floor-gbps", "1e9")
+    assert rc == 1 and any("below floor" in f for f in _last_json(out)["failures"])
+
+
+@pytest.mark.gpu
 def test_binary_no_fp8_skips_the_fp8_check():
     _have_bin()
     rc, out, _ = _run("--size", "1024", "--iters", "3", "--no-fp8")

@@ -104,6 +104,10 @@ struct Opts {
   bool xgmi = true;
   bool fp8 = true;              // K1-fp8 check of the e4m3 MX-scaled matrix path
   double fp8_tflops_floor = 0;
+  bool p2p = true;              // C3: per-link xGMI pull matrix (n > 1)
+  bool p2p_loopback = false;    // C3 code path on one GPU (pair 0 <- 0), for tests
+  long p2p_mib = 256;
+  double p2p_floor_gbps = 0;
   bool json = true;
   std::string out;
   std::string termination_log;  // k8s terminationMessagePath (<= 4 KiB summary)
@@ -117,12 +121,13 @@ void usage() {
                "usage: amdgpu-validate [--gpus N] [--size 8192] [--iters 50]\n"
                "       [--tflops-floor TF] [--min-hbm-gb GB] [--hbm-floor-gbps GBps]\n"
                "       [--allreduce-max-mib MiB] [--no-xgmi] [--no-fp8] [--fp8-tflops-floor TF]\n"
+               "       [--no-p2p] [--p2p-mib MiB] [--p2p-floor-gbps GBps] [--p2p-loopback]\n"
                "       [--json] [--out FILE]\n"
                "       [--termination-log FILE] [--prom-out FILE] [--fault-inject KIND]\n"
                "       [--pushgateway http://host:port]\n"
                "fault-inject (also env NTM_FAULT_INJECT): corrupt_gemm | corrupt_abft |\n"
-               "       corrupt_fp8 | corrupt_allreduce - corrupts the LAST GPU's data to prove\n"
-               "       detection\n");
+               "       corrupt_fp8 | corrupt_p2p | corrupt_allreduce - corrupts the LAST GPU's data\n"
+               "       to prove detection\n");
 }
 
 bool parse(int argc, char** argv, Opts& o) {
@@ -145,6 +150,10 @@ bool parse(int argc, char** argv, Opts& o) {
     else if (a == "--allreduce-max-mib") { if (!(v = next(a.c_str()))) return false; o.allreduce_max_mib = std::atol(v); }
     else if (a == "--no-xgmi") o.xgmi = false;
     else if (a == "--no-fp8") o.fp8 = false;
+    else if (a == "--no-p2p") o.p2p = false;
+    else if (a == "--p2p-loopback") o.p2p_loopback = true;
+    else if (a == "--p2p-mib") { if (!(v = next(a.c_str()))) return false; o.p2p_mib = std::atol(v); }
+    else if (a == "--p2p-floor-gbps") { if (!(v = next(a.c_str()))) return false; o.p2p_floor_gbps = std::atof(v); }
     else if (a == "--fp8-tflops-floor") { if (!(v = next(a.c_str()))) return false; o.fp8_tflops_floor = std::atof(v); }
     else if (a == "--json") o.json = true;
     else if (a == "--out") { if (!(v = next("--out"))) return false; o.out = v; }
@@ -155,7 +164,7 @@ bool parse(int argc, char** argv, Opts& o) {
     else if (a == "-h" || a == "--help") { usage(); std::exit(0); }
     else { std::fprintf(stderr, "unknown argument %s\n", a.c_str()); return false; }
   }
-  return o.size > 0 && o.iters > 0;
+  return o.size > 0 && o.iters > 0 && o.p2p_mib > 0;
 }
 
 // ------------------------------------------------------------ JSON helpers
@@ -525,6 +534,111 @@ bool run_rccl(const std::vector<int>& devs, const Opts& o, std::vector<CollRow>&
 }
 
 // C2: hand-written two-shot all-reduce over peer-mapped xGMI.
+// C3: per-link xGMI check. For every ordered pair (dst <- src), GPU dst pulls
+// --p2p-mib MiB out of GPU src's HBM through the peer mapping with the K2 copy
+// kernel, so every read crosses the one dst-src link; timed with events on
+// dst, pairs one at a time, then a sample window is compared byte for byte.
+// A degraded or miswired link is one cell of this matrix, where a ring
+// all-reduce's busbw only shows the slowest ring. --p2p-loopback runs the same
+// code on a single GPU as pair 0 <- 0 (a local copy) so the path is testable
+// on a one-GPU box.
+struct P2pResult {
+  int n = 0;
+  std::vector<double> gbps;  // n x n, row = destination (puller), NAN on the diagonal
+  unsigned long long bad_pairs = 0;
+  double min_gbps = 0;
+};
+
+bool run_p2p(const std::vector<int>& devs, const Opts& o, P2pResult& r) {
+  const int n = o.p2p_loopback ? 1 : (int)devs.size();
+  r.n = n;
+  r.gbps.assign((size_t)n * n, NAN);
+  const size_t bytes = (size_t)o.p2p_mib << 20;
+  std::vector<void*> src(n, nullptr), dst(n, nullptr);
+  std::vector<hipStream_t> st(n);
+  std::vector<hipEvent_t> e0(n), e1(n);
+  for (int i = 0; i < n; ++i) {
+    CK(hipSetDevice(devs[i]));
+    if (!o.p2p_loopback)
+      for (int j = 0; j < n; ++j) {
+        if (i == j) continue;
+        int can = 0;
+        CK(hipDeviceCanAccessPeer(&can, devs[i], devs[j]));
+        if (!can) {
+          fail("no peer access from GPU " + std::to_string(devs[i]) + " to " + std::to_string(devs[j]));
+          return false;
+        }
+        hipError_t e = hipDeviceEnablePeerAccess(devs[j], 0);
+        if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) CK(e);
+      }
+    CK(hipStreamCreateWithFlags(&st[i], hipStreamNonBlocking));
+    CK(hipEventCreate(&e0[i]));
+    CK(hipEventCreate(&e1[i]));
+    CK(hipMalloc(&src[i], bytes));
+    CK(hipMalloc(&dst[i], bytes));
+    CK(ntm_fill_uniform_bf16(src[i], bytes / 2, 4242 + devs[i], 1.0f, st[i]));
+    CK(hipStreamSynchronize(st[i]));
+  }
+  const size_t w = std::min<size_t>(bytes, 1u << 20);
+  std::vector<unsigned char> h0(w), h1(w);
+  double mn = INFINITY;
+  for (int d = 0; d < n; ++d)
+    for (int sidx = 0; sidx < n; ++sidx) {
+      if (sidx == d && !o.p2p_loopback) continue;
+      CK(hipSetDevice(devs[d]));
+      CK(hipMemsetAsync(dst[d], 0, bytes, st[d]));
+      CK(ntm_stream_copy(src[sidx], dst[d], bytes, st[d]));  // warm the mapping
+      const int iters = 5;
+      CK(hipEventRecord(e0[d], st[d]));
+      for (int it = 0; it < iters; ++it) CK(ntm_stream_copy(src[sidx], dst[d], bytes, st[d]));
+      CK(hipEventRecord(e1[d], st[d]));
+      CK(hipEventSynchronize(e1[d]));
+      float ms = 0;
+      CK(hipEventElapsedTime(&ms, e0[d], e1[d]));
+      const double g = (double)bytes * iters / (ms * 1e-3) / 1e9;  // bytes over the link
+      r.gbps[(size_t)d * n + sidx] = g;
+      mn = std::min(mn, g);
+      if (d == n - 1 && sidx == (n > 1 ? 0 : d) && o.fault == "corrupt_p2p") {
+        unsigned char b = 0x5a;
+        CK(hipMemcpy((char*)dst[d] + 4097, &b, 1, hipMemcpyHostToDevice));
+      }
+      bool same = true;
+      for (size_t off : {(size_t)0, bytes - w}) {
+        CK(hipMemcpy(h0.data(), (char*)src[sidx] + off, w, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(h1.data(), (char*)dst[d] + off, w, hipMemcpyDeviceToHost));
+        same = same && std::memcmp(h0.data(), h1.data(), w) == 0;
+      }
+      if (!same) {
+        ++r.bad_pairs;
+        fail("xGMI P2P copy GPU " + std::to_string(devs[sidx]) + " -> GPU " +
+             std::to_string(devs[d]) + " corrupted data");
+      }
+      if (o.p2p_floor_gbps > 0 && g < o.p2p_floor_gbps)
+        fail("xGMI P2P GPU " + std::to_string(devs[sidx]) + " -> GPU " + std::to_string(devs[d]) +
+             " " + jnum(g) + " GB/s below floor " + jnum(o.p2p_floor_gbps));
+    }
+  r.min_gbps = std::isfinite(mn) ? mn : 0;
+  for (int i = 0; i < n; ++i) {
+    CK(hipSetDevice(devs[i]));
+    CK(hipFree(src[i]));
+    CK(hipFree(dst[i]));
+    CK(hipEventDestroy(e0[i]));
+    CK(hipEventDestroy(e1[i]));
+    CK(hipStreamDestroy(st[i]));
+  }
+  return true;
+}
+
+std::string p2p_json(const P2pResult& r) {
+  std::string js = "[";
+  for (int d = 0; d < r.n; ++d) {
+    js += d ? ",[" : "[";
+    for (int s2 = 0; s2 < r.n; ++s2) js += (s2 ? "," : "") + jnum(r.gbps[(size_t)d * r.n + s2]);
+    js += "]";
+  }
+  return js + "]";
+}
+
 bool run_xgmi(const std::vector<int>& devs, const Opts& o, std::vector<CollRow>& rows) {
   const int n = (int)devs.size();
   if (n < 2 || n > ntm::xgmi::kMaxRanks) return true;
@@ -743,6 +857,8 @@ int main(int argc, char** argv) {
   if (n > 1) run_rccl(devs, o, rccl_rows);
   const double t_rccl = wall_now();
   if (n > 1 && o.xgmi) run_xgmi(devs, o, xgmi_rows);
+  P2pResult p2p;
+  if (o.p2p && (n > 1 || o.p2p_loopback)) run_p2p(devs, o, p2p);
   const double t_end = wall_now();
 
   double agg = 0;
@@ -779,6 +895,15 @@ int main(int argc, char** argv) {
       p << "# TYPE amdgpu_validate_allreduce_busbw_gbps gauge\n"
         << "amdgpu_validate_allreduce_busbw_gbps{impl=\"rccl\"} " << jnum(peak_rccl) << "\n"
         << "amdgpu_validate_allreduce_busbw_gbps{impl=\"xgmi\"} " << jnum(peak_xgmi) << "\n";
+    if (p2p.n > 0) {
+      p << "# HELP amdgpu_validate_xgmi_p2p_gbps Pull bandwidth dst <- src over one xGMI link.\n"
+        << "# TYPE amdgpu_validate_xgmi_p2p_gbps gauge\n";
+      for (int d = 0; d < p2p.n; ++d)
+        for (int s2 = 0; s2 < p2p.n; ++s2)
+          if (std::isfinite(p2p.gbps[(size_t)d * p2p.n + s2]))
+            p << "amdgpu_validate_xgmi_p2p_gbps{dst=\"" << devs[d] << "\",src=\"" << devs[s2]
+              << "\"} " << jnum(p2p.gbps[(size_t)d * p2p.n + s2]) << "\n";
+    }
     prom_text = p.str();
   }
   std::string push_status;
@@ -811,6 +936,9 @@ int main(int argc, char** argv) {
   }
   js += "],\"rccl_allreduce\":" + coll_json(rccl_rows);
   js += ",\"xgmi_allreduce_bf16\":" + coll_json(xgmi_rows);
+  js += ",\"xgmi_p2p_GBps\":" + p2p_json(p2p) + ",\"xgmi_p2p_min_GBps\":" +
+        (p2p.n > 0 ? jnum(p2p.min_gbps) : std::string("null")) +
+        ",\"xgmi_p2p_bad_pairs\":" + std::to_string(p2p.bad_pairs);
   double t_gemm = t_hip, t_hbm = t_hip;
   for (auto& r : res) { t_gemm = std::max(t_gemm, r.t_gemm); t_hbm = std::max(t_hbm, r.t_hbm); }
   js += ",\"phases_s\":{\"process_start_to_hip_init\":" + jnum(t_hip - t_start) +
