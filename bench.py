@@ -12,7 +12,8 @@ without a cloud account; this measures the GPU half on real hardware:
   synchronize, max over ranks; ``value`` = aggregate TFLOP/s over all GPUs,
 * after the timed region (never inside it): full-matrix verification against
   an independent fp32 reference, hipBLASLt comparison on the same data, K2 HBM
-  check, C1 RCCL all-reduce busbw sweep (N > 1), and the in-node
+  check, C1 RCCL all-reduce busbw sweep (N > 1; --p2p adds the per-pair
+  send/recv link matrix), and the in-node
   time-to-GPU-ready phases (process start -> HIP init -> verified).
 
 Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--size 8192]
@@ -53,6 +54,9 @@ def parse(argv=None):
     ap.add_argument("--xgmi", action="store_true",
                     help="N > 1: also sweep the hand-written xGMI all-reduce (C2, HIP IPC); its "
                          "time includes staging copies + a host barrier per call")
+    ap.add_argument("--p2p", action="store_true",
+                    help="N > 1: also measure the send/recv bandwidth of every ordered rank pair "
+                         "(one xGMI link each on a fully connected node)")
     ap.add_argument("--out", default="", help="also write the JSON line to this file")
     ap.add_argument("--rehearsal", action="store_true",
                     help="CPU/gloo + PyTorch reference ops: rehearses the multi-process "
@@ -185,6 +189,14 @@ def main(argv=None) -> int:
         extras["allreduce_fp32_peak_busbw_GBps"] = coll.peak_busbw(res32)
         if any(r.errors for r in res + res32):
             verified = False
+        if args.p2p:
+            # per-link check: every ordered pair, one at a time (RCCL send/recv = one xGMI
+            # link). Opt-in: the driver's scaling runs keep to the all-reduce sweep.
+            pm = coll.p2p_matrix(env, nbytes=(64 << 20) if args.rehearsal else (256 << 20),
+                                 iters=3)
+            extras["p2p_send_GBps"] = pm.as_dict()
+            if pm.errors:
+                verified = False
         if args.xgmi and not args.rehearsal:
             from nvidia_terraform_modules_amd.parallel.xgmi import XgmiAllReduce
 

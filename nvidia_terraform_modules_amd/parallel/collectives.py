@@ -126,6 +126,82 @@ def all_reduce_sweep(env: DistEnv, sizes: list[int], dtype: str = "bf16", iters:
     return results
 
 
+@dataclass
+class P2pMatrix:
+    """Point-to-point send bandwidth for every ordered rank pair (one at a time)."""
+    ranks: int
+    bytes: int
+    gbps: list          # gbps[dst][src], None on the diagonal
+    errors: int         # received elements that differ from the sender's pattern
+
+    def min_gbps(self) -> float | None:
+        vals = [v for row in self.gbps for v in row if v is not None]
+        return min(vals) if vals else None
+
+    def as_dict(self) -> dict:
+        return {"ranks": self.ranks, "bytes": self.bytes,
+                "GBps": [[None if v is None else round(v, 1) for v in row] for row in self.gbps],
+                "min_GBps": None if self.min_gbps() is None else round(self.min_gbps(), 1),
+                "errors": self.errors}
+
+
+def p2p_matrix(env: DistEnv, nbytes: int = 256 << 20, iters: int = 3) -> P2pMatrix:
+    """Every ordered pair (src -> dst) in turn: src sends ``iters`` messages of
+    ``nbytes`` to dst (RCCL send/recv over the one xGMI link between the two
+    GPUs, gloo on CPU) while the other ranks wait at the barrier.
+
+    This is the one-process-per-GPU counterpart of amdgpu-validate's C3 link
+    matrix (validation/src/validate_main.cpp ``run_p2p``): on a fully connected
+    8x MI355X mesh every pair is one link, so a degraded link is one cell.
+    Timed on the receiver between the pair's barrier and its last completed
+    receive; the first message of each pair is checked element for element.
+    """
+    n = env.world_size
+    count = max(1, nbytes // 4)
+    gbps = [[None] * n for _ in range(n)]
+    local = torch.zeros(n * n, dtype=torch.float64)
+    errors = 0
+    if n > 1:
+        mine = (torch.arange(count, device=env.device, dtype=torch.int32) % 1021
+                + 1024 * env.rank).to(torch.float32)
+        recv = torch.empty(count, device=env.device, dtype=torch.float32)
+        for src in range(n):
+            for dst in range(n):
+                if src == dst:
+                    continue
+                barrier(env)
+                if env.rank == src:
+                    for _ in range(iters):
+                        tdist.send(mine, dst)
+                    _sync(env)
+                elif env.rank == dst:
+                    t0 = time.perf_counter()
+                    for it in range(iters):
+                        tdist.recv(recv, src)
+                        if it == 0:
+                            _sync(env)
+                            want = (torch.arange(count, device=env.device, dtype=torch.int32)
+                                    % 1021 + 1024 * src).to(torch.float32)
+                            errors += int((recv != want).sum().item())
+                            t0 = time.perf_counter()   # time the remaining messages
+                    _sync(env)
+                    dt = time.perf_counter() - t0
+                    timed = iters - 1 if iters > 1 else 1
+                    local[dst * n + src] = count * 4 * timed / dt / 1e9 if dt > 0 else 0.0
+        barrier(env)
+    # one collective to put the whole matrix (and the error count) on every rank
+    flat = torch.cat([local, torch.tensor([float(errors)], dtype=torch.float64)])
+    if n > 1:
+        dev_flat = flat.to(env.device)
+        tdist.all_reduce(dev_flat)
+        flat = dev_flat.cpu()
+    for d in range(n):
+        for s_ in range(n):
+            if d != s_:
+                gbps[d][s_] = float(flat[d * n + s_])
+    return P2pMatrix(ranks=n, bytes=count * 4, gbps=gbps, errors=int(flat[-1]))
+
+
 def peak_busbw(results: list[CollResult]) -> float:
     return max((r.busbw_GBps for r in results), default=0.0)
 

@@ -44,7 +44,7 @@ def test_torchrun_launch_one_json_line(nproc):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
            f"--nproc-per-node={nproc}", "--master-addr=127.0.0.1", f"--master-port={_port()}",
            str(ROOT / "bench.py"), "--gpus", str(nproc), "--steps", "3", "--warmup", "1",
-           "--size", "256", "--allreduce-max-mib", "1", "--rehearsal"]
+           "--size", "256", "--allreduce-max-mib", "1", "--rehearsal", "--p2p"]
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=_env(), cwd=ROOT)
     assert p.returncode == 0, p.stderr[-3000:]
     lines = _json_lines(p.stdout)
@@ -61,6 +61,8 @@ def test_torchrun_launch_one_json_line(nproc):
     if nproc > 1:
         assert all(r["errors"] == 0 for r in d["allreduce_bf16"] + d["allreduce_fp32"])
         assert d["allreduce_bf16"][0]["bytes"] == 8
+        pm = d["p2p_send_GBps"]
+        assert pm["ranks"] == nproc and pm["errors"] == 0 and pm["min_GBps"] > 0
 
 
 def test_self_relaunch_as_child_process():

@@ -47,6 +47,10 @@ def _sweep(env):
     return [r.as_dict() for r in res + res32]
 
 
+def _p2p(env):
+    return coll.p2p_matrix(env, nbytes=1 << 16, iters=2).as_dict()
+
+
 def _faulty_sweep(env):
     import torch.distributed as tdist
 
@@ -137,3 +141,17 @@ def test_validation_job_consensus_world2():
     assert out[0][0] is False and any("another rank" in f for f in out[0][1])
     for rank in (0, 1):
         assert out[rank][2] is True and out[rank][3] > 0   # clean run passes, sweep ran
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_p2p_matrix_every_ordered_pair(world):
+    out = _run(world, "_p2p")
+    m = out[0]
+    assert all(out[r] == m or out[r]["GBps"] == m["GBps"] for r in out)   # same matrix everywhere
+    assert m["ranks"] == world and m["errors"] == 0 and m["bytes"] == 1 << 16
+    for d in range(world):
+        for s in range(world):
+            v = m["GBps"][d][s]
+            assert (v is None) == (d == s)
+            assert d == s or v > 0
+    assert m["min_GBps"] > 0
