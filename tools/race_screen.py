@@ -9,6 +9,8 @@ perturbs DMA/L2 timing so that a read placed too early (RAW) or a restage
 placed too early (WAR) shows up as a changed tile.
 
     python tools/race_screen.py [--variants pingpong8b] [--repeats 200]
+
+Variant ``fp8`` screens K1-fp8 (ops.gemm_fp8, e4m3 operands, K % 256 shapes).
 """
 import argparse
 import json
@@ -23,6 +25,8 @@ from nvidia_terraform_modules_amd import ops  # noqa: E402
 
 SHAPES = [(256, 256, 128), (256, 512, 256), (512, 768, 384), (2304, 1536, 640),
           (4096, 4352, 512), (4096, 4096, 4096), (8192, 8192, 8192)]
+SHAPES_FP8 = [(256, 256, 256), (256, 512, 512), (512, 768, 768), (2304, 1536, 1280),
+              (4096, 4352, 1024), (4096, 4096, 4096), (8192, 8192, 8192)]
 
 
 def main():
@@ -38,10 +42,16 @@ def main():
     report = {"repeats": args.repeats, "results": []}
     failed = False
     for v in args.variants.split(","):
-        for (m, n, k) in SHAPES:
-            a = ops.fill_uniform_(torch.empty((m, k), dtype=torch.bfloat16, device=dev), 5 + m)
-            b = ops.fill_uniform_(torch.empty((n, k), dtype=torch.bfloat16, device=dev), 6 + n)
-            first = ops.gemm_bf16(a, b, variant=v)
+        fp8 = v == "fp8"
+        dt = torch.float8_e4m3fn if fp8 else torch.bfloat16
+
+        def gemm(a, b, out=None, v=v, fp8=fp8):
+            return ops.gemm_fp8(a, b, out) if fp8 else ops.gemm_bf16(a, b, out, variant=v)
+
+        for (m, n, k) in (SHAPES_FP8 if fp8 else SHAPES):
+            a = ops.fill_uniform_(torch.empty((m, k), dtype=dt, device=dev), 5 + m)
+            b = ops.fill_uniform_(torch.empty((n, k), dtype=dt, device=dev), 6 + n)
+            first = gemm(a, b)
             ref = ops.ref_gemm_f32(a, b)
             atol, rtol = ops.gemm_tolerance(k)
             ok_ref = ops.verify_bf16(first, ref, atol, rtol).ok
@@ -54,7 +64,7 @@ def main():
                     with torch.cuda.stream(noise_s):
                         ops.stream_copy(nsrc, ndst)
                 out.fill_(float("nan"))
-                ops.gemm_bf16(a, b, out, variant=v)
+                gemm(a, b, out)
                 if not torch.equal(out, first):
                     mismatches += 1
             torch.cuda.synchronize()
