@@ -46,6 +46,9 @@ DEFAULT_DURATIONS = {
     "kubernetes_namespace_v1": 2.0,
     "kubernetes_resource_quota_v1": 1.0,
     "helm_release": 120.0,                   # operator chart wait=true
+    # CR-only / monitor-only charts: helm's wait has no workload to wait for
+    "helm_release.device_config": 5.0,
+    "helm_release.service_monitor": 5.0,
     "kubernetes_daemon_set_v1": 30.0,
     "kubernetes_service_v1": 1.0,
     "kubernetes_service_account_v1": 1.0,
@@ -127,7 +130,8 @@ def critical_path(g: Graph, durations: dict | None = None, stack_mode: str = "op
         if addr in dur:
             return dur[addr]
         t = node_type(addr)
-        base = dur.get(t, 0.0)
+        named = f"{t}.{addr.split(t + '.', 1)[1].split('[')[0]}" if (t + ".") in addr else t
+        base = dur.get(named, dur.get(t, 0.0))
         if t == "kubernetes_job_v1":
             driver = DRIVER_READY_S.get(stack_mode, 0.0)  # GPUs allocatable only after the driver
             pull = dur.get("image_pull", IMAGE_PULL_S)

@@ -210,3 +210,14 @@ def test_cli_critical_path_json(tmp_path):
     assert p.returncode == 0, p.stderr
     d = json.loads(p.stdout)
     assert d["total_s"] > 0 and d["path"][-1][0].endswith("kubernetes_job_v1.gpu_validation")
+
+
+def test_named_priors_beat_type_priors(repo):
+    """A CR-only chart (the DeviceConfig) has nothing for helm's wait to wait on:
+    its type.name prior (5 s) applies instead of the operator-chart prior."""
+    cp = critical_path(build_graph(repo / "eks"))
+    path = dict(cp.path)
+    assert path["module.amd_gpu_stack.helm_release.device_config"] == 5.0
+    assert path["module.amd_gpu_stack.helm_release.amd_gpu_operator"] == 120.0
+    over = critical_path(build_graph(repo / "eks"), {"helm_release.device_config": 50.0})
+    assert dict(over.path)["module.amd_gpu_stack.helm_release.device_config"] == 50.0
