@@ -58,6 +58,11 @@ def test_torchrun_launch_one_json_line(nproc):
     assert d["higher_is_better"] is True and d["scaling"] == "weak" and d["dtype"] == "bf16"
     assert d["value"] > 0 and d["verified"] is True and d["rehearsal"] is True
     assert "NOT a measurement" in d["data"]
+    # the Job binary step runs (here: no GPU -> its environment-error verdict) and the
+    # other ranks have left before it without breaking the one-line contract
+    job = d["validation_job"]
+    assert job["ran"] is False or job["passed"] is False
+    assert d["time_to_gpu_ready_in_node_s"] is None
     if nproc > 1:
         assert all(r["errors"] == 0 for r in d["allreduce_bf16"] + d["allreduce_fp32"])
         assert d["allreduce_bf16"][0]["bytes"] == 8
