@@ -81,3 +81,24 @@ def test_self_relaunch_as_child_process():
     assert p.returncode == 0, p.stderr[-3000:]
     lines = _json_lines(p.stdout)
     assert len(lines) == 1 and lines[0]["n_gpus"] == 2
+
+
+@pytest.mark.gpu
+def test_bench_on_one_gpu_json_contract(tmp_path):
+    """The real path on one MI355X (small config): one JSON line with the contract keys,
+    verified GEMM, hipBLASLt comparison, HBM check and the Job binary's verdict time."""
+    out = tmp_path / "b.json"
+    p = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--steps", "5", "--warmup", "2",
+                        "--size", "2048", "--out", str(out)],
+                       capture_output=True, text=True, timeout=300, env=_env(), cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = _json_lines(p.stdout)
+    assert len(lines) == 1
+    d = lines[0]
+    assert CONTRACT_KEYS <= set(d) and d["n_gpus"] == 1 and d["verified"] is True
+    assert d["value"] > 50 and "rehearsal" not in d
+    assert d["hipblaslt_tflops_per_gpu_rank0"] > 0 and d["hbm_copy_GBps_rank0"] > 1000
+    job = d["validation_job"]
+    assert job["ran"] and job["passed"], job
+    assert 0 < d["time_to_gpu_ready_in_node_s"] < 30
+    assert json.loads(out.read_text()) == d
