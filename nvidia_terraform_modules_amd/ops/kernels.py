@@ -33,7 +33,11 @@ def _require(t: torch.Tensor, name: str, dtype: torch.dtype) -> None:
 GEMM_VARIANTS = {"default": 0, "pingpong8": 1, "wave128": 2, "wave128d4": 3, "pingpong8b": 4,
                  "pingpong8c": 5, "pingpong8p": 6, "pingpong8w": 7, "pingpong8wi": 8,
                  "pingpong8ww": 9, "pingpong8cw": 10, "pingpong8cwe": 11,
-                 "pingpong8cwn": 12, "pingpong8cwne": 13, "pingpong8pw": 14}
+                 "pingpong8cwn": 12, "pingpong8cwne": 13, "pingpong8pw": 14, "tile128": 15}
+
+
+def _tile128_shape_ok(m: int, n: int, k: int) -> bool:
+    return m > 0 and n > 0 and m % 128 == 0 and n % 128 == 0 and k >= 128 and k % 128 == 0
 
 
 def gemm_bf16(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
@@ -41,8 +45,9 @@ def gemm_bf16(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
     """K1: ``out = a @ b.T`` in bf16 with fp32 accumulation on MFMA.
 
     a: [M, K] bf16, b: [N, K] bf16 (both K-contiguous), out: [M, N] bf16.
-    ``variant``: "default" = "pingpong8c" when K % 128 == 0, else
-    "pingpong8b" (8 waves, two per SIMD, staggered, balanced 8/4/8/4 LDS read
+    ``variant``: "default" = "tile128" (128x128 tiles, 4 waves) when at most
+    64 tiles of 256x256 would cover C (small problems) and K % 128 == 0, else
+    "pingpong8c" when K % 128 == 0, else "pingpong8b" (8 waves, two per SIMD, staggered, balanced 8/4/8/4 LDS read
     schedule; 8c adds parity-alternating B buffers and a tail-free K loop -
     fastest measured), "pingpong8" (the first 12/4/8/0 schedule), or the
     experimental "wave128"/"wave128d4" (4 waves, 128x128 per wave,
@@ -54,7 +59,13 @@ def gemm_bf16(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
     n, kb = b.shape
     if k != kb:
         raise ValueError(f"K mismatch: a has {k}, b has {kb}")
-    if not gemm_shape_ok(m, n, k):
+    if variant == "tile128":
+        if not _tile128_shape_ok(m, n, k):
+            raise ValueError(f"shape ({m},{n},{k}) not tiled by the 128x128 kernel (K % 128)")
+    elif variant == "default":
+        if not (gemm_shape_ok(m, n, k) or _tile128_shape_ok(m, n, k)):
+            raise ValueError(f"shape ({m},{n},{k}) not tiled by the K1 kernels")
+    elif not gemm_shape_ok(m, n, k):
         raise ValueError(f"shape ({m},{n},{k}) not tiled by the 256x256x64 kernel")
     if out is None:
         out = torch.empty((m, n), dtype=torch.bfloat16, device=a.device)

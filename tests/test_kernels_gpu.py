@@ -210,6 +210,32 @@ def test_gemm_variants_vs_torch_fp32(ops, variant, m, n, k):
     assert torch.equal(c, ops.gemm_bf16(a, b, variant="pingpong8"))  # same math, same order
 
 
+@pytest.mark.parametrize("m,n,k", [(128, 128, 128), (384, 640, 256), (1280, 896, 512),
+                                   (256, 256, 1024), (2048, 2048, 2048), (3072, 1024, 384)])
+def test_gemm_tile128_vs_torch_fp32(ops, m, n, k):
+    """128x128-tile K1 (gemm_bf16_t128.hpp): M, N multiples of 128 (not 256),
+    K-tile counts 2..32 (the 4-slot ring's dummy pieces at every tail length),
+    1..192 workgroups; bitwise equal to the 256x256 kernel where both apply."""
+    a = _rand(ops, (m, k), 171 + k)
+    b = _rand(ops, (n, k), 173 + n)
+    c = ops.gemm_bf16(a, b, variant="tile128")
+    ref = a.float() @ b.float().T
+    atol, rtol = ops.gemm_tolerance(k)
+    err = (c.float() - ref).abs()
+    assert torch.all(err <= atol + rtol * ref.abs()), float(err.max())
+    if m % 256 == 0 and n % 256 == 0:
+        assert torch.equal(c, ops.gemm_bf16(a, b, variant="pingpong8"))
+
+
+def test_gemm_tile128_rejects_bad_shapes(ops):
+    a = torch.zeros((128, 192), dtype=torch.bfloat16, device="cuda")
+    with pytest.raises(ValueError):
+        ops.gemm_bf16(a, a, variant="tile128")    # K % 128
+    a = torch.zeros((192, 128), dtype=torch.bfloat16, device="cuda")
+    with pytest.raises(ValueError):
+        ops.gemm_bf16(a, a, variant="tile128")    # M % 128
+
+
 def _rand_fp8(shape, seed):
     g = torch.Generator(device="cuda").manual_seed(seed)
     x = torch.rand(shape, generator=g, device="cuda") * 2 - 1      # uniform [-1, 1)

@@ -1,0 +1,59 @@
+"""Default-variant policy check (developer tool): interleaved timing of the
+256x256 kernel (pingpong8c), the 128x128 kernel (tile128), the default
+dispatch and hipBLASLt (torch.matmul) on M x N x K shapes; one JSON line each.
+
+    python tools/gemm_policy.py --shapes 2048x2048x2048,4096x2048x4096 [--rounds 7]
+"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from nvidia_terraform_modules_amd import ops  # noqa: E402
+
+
+def timed(fn, iters):
+    fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / iters
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--shapes", default="2048x2048x2048")
+    ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--iters", type=int, default=50)
+    args = ap.parse_args()
+    for sh in args.shapes.split(","):
+        m, n, k = (int(x) for x in sh.split("x"))
+        a = ops.fill_uniform_(torch.empty((m, k), dtype=torch.bfloat16, device="cuda"), 1)
+        b = ops.fill_uniform_(torch.empty((n, k), dtype=torch.bfloat16, device="cuda"), 2)
+        c = torch.empty((m, n), dtype=torch.bfloat16, device="cuda")
+        fns = {"default": lambda: ops.gemm_bf16(a, b, c),
+               "tile128": lambda: ops.gemm_bf16(a, b, c, variant="tile128"),
+               "torch": lambda: torch.matmul(a, b.T, out=c)}
+        if m % 256 == 0 and n % 256 == 0:
+            fns["pingpong8c"] = lambda: ops.gemm_bf16(a, b, c, variant="pingpong8c")
+        t = {name: [] for name in fns}
+        for _ in range(args.rounds):
+            for name, fn in fns.items():
+                t[name].append(timed(fn, args.iters))
+        fl = 2.0 * m * n * k
+        row = {"shape": [m, n, k], "tiles256": (m // 256) * (n // 256)}
+        for name, v in t.items():
+            v.sort()
+            row[f"{name}_tflops"] = round(fl / v[len(v) // 2] / 1e9, 1)
+        print(json.dumps(row), flush=True)
+
+
+if __name__ == "__main__":
+    main()

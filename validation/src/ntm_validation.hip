@@ -12,6 +12,7 @@
 #include "ntm/gemm_bf16_pp4.hpp"
 #include "ntm/gemm_bf16_pp3_stamp.hpp"
 #include "ntm/gemm_bf16_pp5.hpp"
+#include "ntm/gemm_bf16_t128.hpp"
 #include "ntm/gemm_bf16_w4.hpp"
 
 #define NTM_API extern "C" __attribute__((visibility("default")))
@@ -42,7 +43,7 @@ NTM_API int ntm_gemm_shape_ok(int M, int N, int K) {
 // wide 32-MFMA segments (gemm_bf16_pp5.hpp): reads first / DMA issue first /
 // reads first + widened dwordx4 epilogue; 10 / 11 / 12 / 13 = 5 + widened
 // epilogue / + early row-0 stores / + nontemporal stores / + both; 14 = 6 +
-// widened epilogue.
+// widened epilogue; 15 = 128x128 tiles, 4 waves (gemm_bf16_t128.hpp).
 // 0 = default: the fastest measured variant whose shape rules admit (M,N,K).
 // Measured on MI355X (tools/gemm_check.py, random bf16, median of 7 rounds,
 // profiles/r1_pp3/):
@@ -59,12 +60,19 @@ NTM_API int ntm_gemm_shape_ok(int M, int N, int K) {
 // epilogue; 11/13 (early row-0 stores) tie with 10/12.
 // Default: 5 when K % 128 == 0, else 4 (both need K % 64 == 0, K >= 128).
 constexpr int kDefaultVariant = 5;
+constexpr long kSmallGridTiles = 64;  // <= this many 256x256 tiles -> tile128 (variant 15)
 
 NTM_API int ntm_gemm_bf16_variant(int variant, const void* A, const void* B,
                                   void* C, int M, int N, int K, int lda,
                                   int ldb, int ldc, void* stream) {
   if (variant == 0) {
     variant = kDefaultVariant;
+    // So few 256x256 tiles that the 128x128 tiles fit in one round on 256 CUs:
+    // the 128x128 kernel (profiles/r1_t128/policy.log: 2048^3 768 vs 480 TF/s,
+    // 1024^3 175 vs 108, 1536^3 426 vs 260). From 100 big tiles up (2560^3,
+    // 4096x2048x4096) the 256x256 kernel is ahead again (751 vs 709, 964 vs 919).
+    const long tiles256 = (M % 256 == 0 && N % 256 == 0) ? (long)(M / 256) * (N / 256) : 0;
+    if (ntm::gemmt::shape_ok_t(M, N, K) && tiles256 <= kSmallGridTiles) variant = 15;
     if (variant == 5 && !ntm::gemm3::shape_ok3(M, N, K)) variant = 4;
     if (variant == 3 && !ntm::gemm4::shape_ok<4>(M, N, K)) variant = 1;
     if (variant == 2 && !ntm::gemm4::shape_ok<3>(M, N, K)) variant = 1;
@@ -111,6 +119,19 @@ NTM_API int ntm_gemm_bf16_variant(int variant, const void* A, const void* B,
     if (variant == 14) return (int)ntm::gemmp::launch_gemm_bf16_pp4(a, S(stream), true);
     if (variant >= 10) return (int)ntm::gemm3::launch_gemm_bf16_pp3_knob(a, variant + 2, S(stream));
     return (int)ntm::gemm5::launch_gemm_bf16_pp5(a, variant - 7, S(stream));
+  }
+  if (variant == 15) {  // 128x128 tiles (gemm_bf16_t128.hpp)
+    ntm::gemm::GemmArgs a;
+    a.A = (const __bf16*)A;
+    a.B = (const __bf16*)B;
+    a.C = (__bf16*)C;
+    a.M = M;
+    a.N = N;
+    a.K = K;
+    a.lda = lda;
+    a.ldb = ldb;
+    a.ldc = ldc;
+    return (int)ntm::gemmt::launch_gemm_bf16_t128(a, S(stream));
   }
   if (variant == 2 || variant == 3) {
     ntm::gemm4::Args a{(const __bf16*)A, (const __bf16*)B, (__bf16*)C, M, N, K,
