@@ -33,11 +33,12 @@ def _require(t: torch.Tensor, name: str, dtype: torch.dtype) -> None:
 GEMM_VARIANTS = {"default": 0, "pingpong8": 1, "wave128": 2, "wave128d4": 3, "pingpong8b": 4,
                  "pingpong8c": 5, "pingpong8p": 6, "pingpong8w": 7, "pingpong8wi": 8,
                  "pingpong8ww": 9, "pingpong8cw": 10, "pingpong8cwe": 11,
-                 "pingpong8cwn": 12, "pingpong8cwne": 13, "pingpong8pw": 14, "tile128": 15}
+                 "pingpong8cwn": 12, "pingpong8cwne": 13, "pingpong8pw": 14, "tile128": 15,
+                 "tile256x128": 16}
 
 
-def _tile128_shape_ok(m: int, n: int, k: int) -> bool:
-    return m > 0 and n > 0 and m % 128 == 0 and n % 128 == 0 and k >= 128 and k % 128 == 0
+def _tile128_shape_ok(m: int, n: int, k: int, tm: int = 128) -> bool:
+    return m > 0 and n > 0 and m % tm == 0 and n % 128 == 0 and k >= 128 and k % 128 == 0
 
 
 def gemm_bf16(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
@@ -45,9 +46,10 @@ def gemm_bf16(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
     """K1: ``out = a @ b.T`` in bf16 with fp32 accumulation on MFMA.
 
     a: [M, K] bf16, b: [N, K] bf16 (both K-contiguous), out: [M, N] bf16.
-    ``variant``: "default" = "tile128" (128x128 tiles, 4 waves) when at most
-    64 tiles of 256x256 would cover C (small problems) and K % 128 == 0, else
-    "pingpong8c" when K % 128 == 0, else "pingpong8b" (8 waves, two per SIMD, staggered, balanced 8/4/8/4 LDS read
+    ``variant``: "default" = the tile shape with the smallest predicted time
+    (rounds of 256 CUs x tile area / efficiency): "tile128" / "tile256x128"
+    (128x128 / 256x128 tiles, 4 waves, K % 128) for small and mid-size C,
+    else "pingpong8c" when K % 128 == 0, else "pingpong8b" (8 waves, two per SIMD, staggered, balanced 8/4/8/4 LDS read
     schedule; 8c adds parity-alternating B buffers and a tail-free K loop -
     fastest measured), "pingpong8" (the first 12/4/8/0 schedule), or the
     experimental "wave128"/"wave128d4" (4 waves, 128x128 per wave,
@@ -59,9 +61,10 @@ def gemm_bf16(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
     n, kb = b.shape
     if k != kb:
         raise ValueError(f"K mismatch: a has {k}, b has {kb}")
-    if variant == "tile128":
-        if not _tile128_shape_ok(m, n, k):
-            raise ValueError(f"shape ({m},{n},{k}) not tiled by the 128x128 kernel (K % 128)")
+    if variant in ("tile128", "tile256x128"):
+        tm = 128 if variant == "tile128" else 256
+        if not _tile128_shape_ok(m, n, k, tm):
+            raise ValueError(f"shape ({m},{n},{k}) not tiled by the {tm}x128 kernel (K % 128)")
     elif variant == "default":
         if not (gemm_shape_ok(m, n, k) or _tile128_shape_ok(m, n, k)):
             raise ValueError(f"shape ({m},{n},{k}) not tiled by the K1 kernels")

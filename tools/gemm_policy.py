@@ -1,5 +1,6 @@
 """Default-variant policy check (developer tool): interleaved timing of the
-256x256 kernel (pingpong8c), the 128x128 kernel (tile128), the default
+256x256 kernel (pingpong8c), the 128x128 / 256x128 kernels (tile128,
+tile256x128), the default
 dispatch and hipBLASLt (torch.matmul) on M x N x K shapes; one JSON line each.
 
     python tools/gemm_policy.py --shapes 2048x2048x2048,4096x2048x4096 [--rounds 7]
@@ -43,6 +44,8 @@ def main():
                "torch": lambda: torch.matmul(a, b.T, out=c)}
         if m % 256 == 0 and n % 256 == 0:
             fns["pingpong8c"] = lambda: ops.gemm_bf16(a, b, c, variant="pingpong8c")
+        if m % 256 == 0:
+            fns["tile256x128"] = lambda: ops.gemm_bf16(a, b, c, variant="tile256x128")
         t = {name: [] for name in fns}
         for _ in range(args.rounds):
             for name, fn in fns.items():

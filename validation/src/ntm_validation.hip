@@ -43,7 +43,7 @@ NTM_API int ntm_gemm_shape_ok(int M, int N, int K) {
 // wide 32-MFMA segments (gemm_bf16_pp5.hpp): reads first / DMA issue first /
 // reads first + widened dwordx4 epilogue; 10 / 11 / 12 / 13 = 5 + widened
 // epilogue / + early row-0 stores / + nontemporal stores / + both; 14 = 6 +
-// widened epilogue; 15 = 128x128 tiles, 4 waves (gemm_bf16_t128.hpp).
+// widened epilogue; 15 / 16 = 128x128 / 256x128 tiles, 4 waves (gemm_bf16_t128.hpp).
 // 0 = default: the fastest measured variant whose shape rules admit (M,N,K).
 // Measured on MI355X (tools/gemm_check.py, random bf16, median of 7 rounds,
 // profiles/r1_pp3/):
@@ -60,19 +60,36 @@ NTM_API int ntm_gemm_shape_ok(int M, int N, int K) {
 // epilogue; 11/13 (early row-0 stores) tie with 10/12.
 // Default: 5 when K % 128 == 0, else 4 (both need K % 64 == 0, K >= 128).
 constexpr int kDefaultVariant = 5;
-constexpr long kSmallGridTiles = 64;  // <= this many 256x256 tiles -> tile128 (variant 15)
+
+// Tile-shape choice of the default dispatch: the smallest predicted time
+// rounds(tiles) x tile_area / efficiency over 256 CUs, where the efficiencies
+// are each kernel's full-chip rate at 8192^3 relative to the 256x256 kernel
+// (profiles/r1_t128/policy_interleaved.log: 1634 / 1219 / 957 TF/s). It picks
+// 128x128 at 2048^3 (858 vs 467 TF/s for 256x256; hipBLASLt 773), 256x128 at
+// 2560^3 and 4096x2048x4096 (825 / 1107 vs 757 / 950), and 256x256 from
+// 3072^3 up and at 6144^3 (1333 vs 1098).
+constexpr double kCUs = 256.0;
+constexpr double kEff256x128 = 0.75, kEff128 = 0.59;
+
+inline int pick_k1_tile(int M, int N, int K) {
+  auto rounds = [](double tiles) { return tiles <= 0 ? 0.0 : __builtin_ceil(tiles / kCUs); };
+  const double inf = 1e300;
+  const double c256 = (M % 256 == 0 && N % 256 == 0) ? rounds((M / 256.0) * (N / 256.0)) * 4.0 : inf;
+  const double c256x128 = ntm::gemmt::shape_ok_t<8>(M, N, K)
+                              ? rounds((M / 256.0) * (N / 128.0)) * 2.0 / kEff256x128 : inf;
+  const double c128 = ntm::gemmt::shape_ok_t<4>(M, N, K)
+                          ? rounds((M / 128.0) * (N / 128.0)) * 1.0 / kEff128 : inf;
+  if (c128 < c256 && c128 <= c256x128) return 15;
+  if (c256x128 < c256) return 16;
+  return kDefaultVariant;
+}
 
 NTM_API int ntm_gemm_bf16_variant(int variant, const void* A, const void* B,
                                   void* C, int M, int N, int K, int lda,
                                   int ldb, int ldc, void* stream) {
   if (variant == 0) {
     variant = kDefaultVariant;
-    // So few 256x256 tiles that the 128x128 tiles fit in one round on 256 CUs:
-    // the 128x128 kernel (profiles/r1_t128/policy.log: 2048^3 768 vs 480 TF/s,
-    // 1024^3 175 vs 108, 1536^3 426 vs 260). From 100 big tiles up (2560^3,
-    // 4096x2048x4096) the 256x256 kernel is ahead again (751 vs 709, 964 vs 919).
-    const long tiles256 = (M % 256 == 0 && N % 256 == 0) ? (long)(M / 256) * (N / 256) : 0;
-    if (ntm::gemmt::shape_ok_t(M, N, K) && tiles256 <= kSmallGridTiles) variant = 15;
+    variant = pick_k1_tile(M, N, K);
     if (variant == 5 && !ntm::gemm3::shape_ok3(M, N, K)) variant = 4;
     if (variant == 3 && !ntm::gemm4::shape_ok<4>(M, N, K)) variant = 1;
     if (variant == 2 && !ntm::gemm4::shape_ok<3>(M, N, K)) variant = 1;
@@ -120,7 +137,7 @@ NTM_API int ntm_gemm_bf16_variant(int variant, const void* A, const void* B,
     if (variant >= 10) return (int)ntm::gemm3::launch_gemm_bf16_pp3_knob(a, variant + 2, S(stream));
     return (int)ntm::gemm5::launch_gemm_bf16_pp5(a, variant - 7, S(stream));
   }
-  if (variant == 15) {  // 128x128 tiles (gemm_bf16_t128.hpp)
+  if (variant == 15 || variant == 16) {  // 128x128 / 256x128 tiles (gemm_bf16_t128.hpp)
     ntm::gemm::GemmArgs a;
     a.A = (const __bf16*)A;
     a.B = (const __bf16*)B;
@@ -131,7 +148,8 @@ NTM_API int ntm_gemm_bf16_variant(int variant, const void* A, const void* B,
     a.lda = lda;
     a.ldb = ldb;
     a.ldc = ldc;
-    return (int)ntm::gemmt::launch_gemm_bf16_t128(a, S(stream));
+    return variant == 15 ? (int)ntm::gemmt::launch_gemm_bf16_tile<4>(a, S(stream))
+                         : (int)ntm::gemmt::launch_gemm_bf16_tile<8>(a, S(stream));
   }
   if (variant == 2 || variant == 3) {
     ntm::gemm4::Args a{(const __bf16*)A, (const __bf16*)B, (__bf16*)C, M, N, K,
