@@ -1,6 +1,7 @@
 """MI355X (gfx950) HIP kernels used by the post-provision validation Job.
 
-K1 ``gemm_bf16``      - 256x256x64 LDS-DMA + MFMA bf16 GEMM (the headline);
+K1 ``gemm_bf16``      - 256x256x64 LDS-DMA + MFMA bf16 GEMM (the headline; small and
+                        mid-size C also on 128x128 / 256x128 tiles, see ``k1_plan``);
    ``gemm_bf16_rowsum`` - same kernel with the fused ABFT row-checksum epilogue;
    ``gemm_fp8``         - the same schedule on OCP e4m3 operands (MX-scaled MFMA).
 K2 ``stream_copy``, ``stream_read`` - tuned float4 HBM streams.

@@ -41,6 +41,15 @@ def _tile128_shape_ok(m: int, n: int, k: int, tm: int = 128) -> bool:
     return m > 0 and n > 0 and m % tm == 0 and n % 128 == 0 and k >= 128 and k % 128 == 0
 
 
+def k1_plan(m: int, n: int, k: int) -> tuple[int, str]:
+    """The default dispatch's plan: (rows on the 256x256 kernel, variant of the
+    remaining rows) - host-side, no GPU needed."""
+    top, rest = ctypes.c_int(), ctypes.c_int()
+    check(lib().ntm_k1_plan(m, n, k, ctypes.byref(top), ctypes.byref(rest)), "ntm_k1_plan")
+    names = {v: kname for kname, v in GEMM_VARIANTS.items()}
+    return top.value, names[rest.value]
+
+
 def gemm_bf16(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
               variant: str = "default") -> torch.Tensor:
     """K1: ``out = a @ b.T`` in bf16 with fp32 accumulation on MFMA.

@@ -232,6 +232,23 @@ def test_gemm_tile128_vs_torch_fp32(ops, variant, m, n, k):
         assert torch.equal(c, ops.gemm_bf16(a, b, variant="pingpong8"))
 
 
+@pytest.mark.parametrize("m,n,k", [(4352, 4352, 256), (6144, 6144, 128), (4608, 4608, 128)])
+def test_gemm_default_split_plan(ops, m, n, k):
+    """Default dispatch that splits C by rows (k1_plan: top rows on 256x256,
+    the rest on a small tile in a second launch): correct vs fp32 and
+    bitwise equal to the single-kernel 256x256 result (same math, same order)."""
+    top, _ = ops.kernels.k1_plan(m, n, k)
+    assert 0 < top < m
+    a = _rand(ops, (m, k), 271 + k)
+    b = _rand(ops, (n, k), 273 + n)
+    c = ops.gemm_bf16(a, b)
+    ref = a.float() @ b.float().T
+    atol, rtol = ops.gemm_tolerance(k)
+    err = (c.float() - ref).abs()
+    assert torch.all(err <= atol + rtol * ref.abs()), float(err.max())
+    assert torch.equal(c, ops.gemm_bf16(a, b, variant="pingpong8"))
+
+
 def test_gemm_tile128_rejects_bad_shapes(ops):
     a = torch.zeros((128, 192), dtype=torch.bfloat16, device="cuda")
     with pytest.raises(ValueError):

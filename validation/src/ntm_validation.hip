@@ -61,36 +61,77 @@ NTM_API int ntm_gemm_shape_ok(int M, int N, int K) {
 // Default: 5 when K % 128 == 0, else 4 (both need K % 64 == 0, K >= 128).
 constexpr int kDefaultVariant = 5;
 
-// Tile-shape choice of the default dispatch: the smallest predicted time
+// Tile-shape plan of the default dispatch: the smallest predicted time
 // rounds(tiles) x tile_area / efficiency over 256 CUs, where the efficiencies
 // are each kernel's full-chip rate at 8192^3 relative to the 256x256 kernel
-// (profiles/r1_t128/policy_interleaved.log: 1634 / 1219 / 957 TF/s). It picks
-// 128x128 at 2048^3 (858 vs 467 TF/s for 256x256; hipBLASLt 773), 256x128 at
-// 2560^3 and 4096x2048x4096 (825 / 1107 vs 757 / 950), and 256x256 from
-// 3072^3 up and at 6144^3 (1333 vs 1098).
+// (profiles/r1_t128/policy_interleaved.log: 1634 / 1219 / 957 TF/s). The plan
+// may split C by rows: the top rows on the 256x256 kernel in whole rounds, the
+// rest in a second launch on a small tile, so a partial last round of big
+// tiles becomes a full round of small ones (6144^3: 3 rounds of 256x256 ->
+// 2 rounds + one of 256x128). Alone it picks 128x128 at 2048^3 (858 vs 467
+// TF/s for 256x256; hipBLASLt 773), 256x128 at 2560^3 and 4096x2048x4096
+// (825 / 1107 vs 757 / 950) and 256x256 at 3072^3, 4096^3 and 8192^3.
 constexpr double kCUs = 256.0;
 constexpr double kEff256x128 = 0.75, kEff128 = 0.59;
+constexpr double kSplitPenalty = 0.25;  // a second launch, in 128x128-tile-round units
 
-inline int pick_k1_tile(int M, int N, int K) {
+struct K1Plan {
+  int top_rows;      // rows [0, top_rows) on the 256x256 kernel
+  int rest_variant;  // rows [top_rows, M) on 15 (128x128) or 16 (256x128)
+};
+
+inline K1Plan plan_k1(int M, int N, int K) {
   auto rounds = [](double tiles) { return tiles <= 0 ? 0.0 : __builtin_ceil(tiles / kCUs); };
   const double inf = 1e300;
-  const double c256 = (M % 256 == 0 && N % 256 == 0) ? rounds((M / 256.0) * (N / 256.0)) * 4.0 : inf;
-  const double c256x128 = ntm::gemmt::shape_ok_t<8>(M, N, K)
-                              ? rounds((M / 256.0) * (N / 128.0)) * 2.0 / kEff256x128 : inf;
-  const double c128 = ntm::gemmt::shape_ok_t<4>(M, N, K)
-                          ? rounds((M / 128.0) * (N / 128.0)) * 1.0 / kEff128 : inf;
-  if (c128 < c256 && c128 <= c256x128) return 15;
-  if (c256x128 < c256) return 16;
-  return kDefaultVariant;
+  const bool big_ok = N % 256 == 0 && K % 64 == 0 && K >= 128;
+  K1Plan best{M % 256 == 0 ? M : 0, 15};
+  double best_cost = inf;
+  for (int m1 = 0; m1 <= M; m1 += 256) {
+    if (m1 > 0 && !big_ok) break;
+    const int rest = M - m1;
+    const double top = m1 ? rounds((m1 / 256.0) * (N / 256.0)) * 4.0 : 0.0;
+    double bottom = 0.0;
+    int v = 15;
+    if (rest > 0) {
+      const double c128 = ntm::gemmt::shape_ok_t<4>(rest, N, K)
+                              ? rounds((rest / 128.0) * (N / 128.0)) / kEff128 : inf;
+      const double c256x128 = ntm::gemmt::shape_ok_t<8>(rest, N, K)
+                                  ? rounds((rest / 256.0) * (N / 128.0)) * 2.0 / kEff256x128 : inf;
+      bottom = c128 <= c256x128 ? c128 : c256x128;
+      v = c128 <= c256x128 ? 15 : 16;
+    }
+    const double cost = top + bottom + (m1 > 0 && rest > 0 ? kSplitPenalty : 0.0);
+    if (cost <= best_cost) {  // ties: more rows on the 256x256 kernel
+      best_cost = cost;
+      best = K1Plan{m1, v};
+    }
+  }
+  return best;
+}
+
+// The default dispatch's plan for (M, N, K) (host only; tests and tools).
+NTM_API int ntm_k1_plan(int M, int N, int K, int* top_rows, int* rest_variant) {
+  if (M <= 0 || N <= 0 || K <= 0 || !top_rows || !rest_variant) return (int)hipErrorInvalidValue;
+  const K1Plan pl = plan_k1(M, N, K);
+  *top_rows = pl.top_rows;
+  *rest_variant = pl.rest_variant;
+  return 0;
 }
 
 NTM_API int ntm_gemm_bf16_variant(int variant, const void* A, const void* B,
                                   void* C, int M, int N, int K, int lda,
                                   int ldb, int ldc, void* stream) {
   if (variant == 0) {
-    variant = kDefaultVariant;
-    variant = pick_k1_tile(M, N, K);
-    if (variant == 5 && !ntm::gemm3::shape_ok3(M, N, K)) variant = 4;
+    const K1Plan pl = plan_k1(M, N, K);
+    const int top = ntm::gemm3::shape_ok3(pl.top_rows, N, K) ? kDefaultVariant : 4;
+    if (pl.top_rows > 0 && pl.top_rows < M) {
+      const int rc = ntm_gemm_bf16_variant(top, A, B, C, pl.top_rows, N, K, lda, ldb, ldc, stream);
+      if (rc != 0) return rc;
+      return ntm_gemm_bf16_variant(pl.rest_variant, (const __bf16*)A + (size_t)pl.top_rows * lda,
+                                   B, (__bf16*)C + (size_t)pl.top_rows * ldc, M - pl.top_rows, N,
+                                   K, lda, ldb, ldc, stream);
+    }
+    variant = pl.top_rows == M ? top : pl.rest_variant;
     if (variant == 3 && !ntm::gemm4::shape_ok<4>(M, N, K)) variant = 1;
     if (variant == 2 && !ntm::gemm4::shape_ok<3>(M, N, K)) variant = 1;
   }
