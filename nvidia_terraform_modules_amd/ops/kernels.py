@@ -34,11 +34,16 @@ GEMM_VARIANTS = {"default": 0, "pingpong8": 1, "wave128": 2, "wave128d4": 3, "pi
                  "pingpong8c": 5, "pingpong8p": 6, "pingpong8w": 7, "pingpong8wi": 8,
                  "pingpong8ww": 9, "pingpong8cw": 10, "pingpong8cwe": 11,
                  "pingpong8cwn": 12, "pingpong8cwne": 13, "pingpong8pw": 14, "tile128": 15,
-                 "tile256x128": 16}
+                 "tile256x128": 16, "tile160": 17, "tile256x160": 18}
 
 
-def _tile128_shape_ok(m: int, n: int, k: int, tm: int = 128) -> bool:
-    return m > 0 and n > 0 and m % tm == 0 and n % 128 == 0 and k >= 128 and k % 128 == 0
+# (TM, TN) of the 4-wave tile kernels (gemm_bf16_t128.hpp)
+TILE_SHAPES = {"tile128": (128, 128), "tile256x128": (256, 128), "tile160": (160, 160),
+               "tile256x160": (256, 160)}
+
+
+def _tile128_shape_ok(m: int, n: int, k: int, tm: int = 128, tn: int = 128) -> bool:
+    return m > 0 and n > 0 and m % tm == 0 and n % tn == 0 and k >= 128 and k % 128 == 0
 
 
 def k1_plan(m: int, n: int, k: int) -> tuple[int, str]:
@@ -56,8 +61,9 @@ def gemm_bf16(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
 
     a: [M, K] bf16, b: [N, K] bf16 (both K-contiguous), out: [M, N] bf16.
     ``variant``: "default" = the tile shape with the smallest predicted time
-    (rounds of 256 CUs x tile area / efficiency): "tile128" / "tile256x128"
-    (128x128 / 256x128 tiles, 4 waves, K % 128) for small and mid-size C,
+    (rounds of 256 CUs x tile area / efficiency, ``k1_plan``): "tile128" /
+    "tile256x128" / "tile160" / "tile256x160" (128x128 / 256x128 / 160x160 /
+    256x160 tiles, 4 waves, K % 128) for small and mid-size C,
     else "pingpong8c" when K % 128 == 0, else "pingpong8b" (8 waves, two per SIMD, staggered, balanced 8/4/8/4 LDS read
     schedule; 8c adds parity-alternating B buffers and a tail-free K loop -
     fastest measured), "pingpong8" (the first 12/4/8/0 schedule), or the
@@ -70,12 +76,13 @@ def gemm_bf16(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
     n, kb = b.shape
     if k != kb:
         raise ValueError(f"K mismatch: a has {k}, b has {kb}")
-    if variant in ("tile128", "tile256x128"):
-        tm = 128 if variant == "tile128" else 256
-        if not _tile128_shape_ok(m, n, k, tm):
-            raise ValueError(f"shape ({m},{n},{k}) not tiled by the {tm}x128 kernel (K % 128)")
+    if variant in TILE_SHAPES:
+        tm, tn = TILE_SHAPES[variant]
+        if not _tile128_shape_ok(m, n, k, tm, tn):
+            raise ValueError(f"shape ({m},{n},{k}) not tiled by the {tm}x{tn} kernel (K % 128)")
     elif variant == "default":
-        if not (gemm_shape_ok(m, n, k) or _tile128_shape_ok(m, n, k)):
+        if not (gemm_shape_ok(m, n, k)
+                or any(_tile128_shape_ok(m, n, k, tm, tn) for tm, tn in TILE_SHAPES.values())):
             raise ValueError(f"shape ({m},{n},{k}) not tiled by the K1 kernels")
     elif not gemm_shape_ok(m, n, k):
         raise ValueError(f"shape ({m},{n},{k}) not tiled by the 256x256x64 kernel")

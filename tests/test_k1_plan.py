@@ -18,7 +18,9 @@ def k1_plan():
 @pytest.mark.parametrize("m,n,k,top,rest", [
     (1024, 1024, 1024, 0, "tile128"),          # < 1 round of 256x256 tiles: small tile only
     (2048, 2048, 2048, 0, "tile128"),
-    (2560, 2560, 2560, 0, "tile256x128"),
+    (2560, 2560, 2560, 0, "tile160"),         # 256 tiles of 160x160: one full round
+    (1920, 1920, 1920, 0, "tile128"),
+    (256, 160, 128, 0, "tile256x160"),
     (4096, 2048, 4096, 0, "tile256x128"),
     (3072, 3072, 3072, 3072, "tile128"),       # whole rounds: 256x256 only
     (4096, 4096, 4096, 4096, "tile128"),
@@ -35,7 +37,7 @@ def test_plan_matches_cost_model(k1_plan, m, n, k, top, rest):
 def test_plan_is_well_formed(k1_plan, m, n, k):
     top, rest = k1_plan(m, n, k)
     assert 0 <= top <= m and top % 256 == 0
-    assert rest in ("tile128", "tile256x128")
+    assert rest in ("tile128", "tile256x128", "tile160", "tile256x160")
     if top < m and rest == "tile256x128":
         assert (m - top) % 256 == 0
 

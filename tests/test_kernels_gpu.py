@@ -232,6 +232,27 @@ def test_gemm_tile128_vs_torch_fp32(ops, variant, m, n, k):
         assert torch.equal(c, ops.gemm_bf16(a, b, variant="pingpong8"))
 
 
+@pytest.mark.parametrize("variant", ["tile160", "tile256x160"])
+@pytest.mark.parametrize("m,n,k", [(160, 160, 128), (1280, 800, 384), (2560, 2560, 2560),
+                                   (1280, 160, 1024), (2560, 1600, 256), (5120, 320, 128)])
+def test_gemm_tile160_vs_torch_fp32(ops, variant, m, n, k):
+    """160-wide tiles (gemm_bf16_t128.hpp with NT = 5; odd MT / NT split the
+    DMA pieces across waves by global piece index): vs fp32, and bitwise equal
+    to the 128-wide tile kernel where both tile the shape (same MFMA order)."""
+    tm, tn = ops.kernels.TILE_SHAPES[variant]
+    if m % tm or n % tn:
+        pytest.skip(f"{variant} needs M % {tm}, N % {tn}")
+    a = _rand(ops, (m, k), 371 + k)
+    b = _rand(ops, (n, k), 373 + n)
+    c = ops.gemm_bf16(a, b, variant=variant)
+    ref = a.float() @ b.float().T
+    atol, rtol = ops.gemm_tolerance(k)
+    err = (c.float() - ref).abs()
+    assert torch.all(err <= atol + rtol * ref.abs()), float(err.max())
+    if m % 128 == 0 and n % 128 == 0:
+        assert torch.equal(c, ops.gemm_bf16(a, b, variant="tile128"))
+
+
 @pytest.mark.parametrize("m,n,k", [(4352, 4352, 256), (6144, 6144, 128), (4608, 4608, 128)])
 def test_gemm_default_split_plan(ops, m, n, k):
     """Default dispatch that splits C by rows (k1_plan: top rows on 256x256,

@@ -40,12 +40,14 @@ def main():
         b = ops.fill_uniform_(torch.empty((n, k), dtype=torch.bfloat16, device="cuda"), 2)
         c = torch.empty((m, n), dtype=torch.bfloat16, device="cuda")
         fns = {"default": lambda: ops.gemm_bf16(a, b, c),
-               "tile128": lambda: ops.gemm_bf16(a, b, c, variant="tile128"),
                "torch": lambda: torch.matmul(a, b.T, out=c)}
+        if m % 128 == 0 and n % 128 == 0:
+            fns["tile128"] = lambda: ops.gemm_bf16(a, b, c, variant="tile128")
         if m % 256 == 0 and n % 256 == 0:
             fns["pingpong8c"] = lambda: ops.gemm_bf16(a, b, c, variant="pingpong8c")
-        if m % 256 == 0:
-            fns["tile256x128"] = lambda: ops.gemm_bf16(a, b, c, variant="tile256x128")
+        for v, (tm, tn) in ops.kernels.TILE_SHAPES.items():
+            if v != "tile128" and m % tm == 0 and n % tn == 0:
+                fns[v] = lambda v=v: ops.gemm_bf16(a, b, c, variant=v)
         t = {name: [] for name in fns}
         for _ in range(args.rounds):
             for name, fn in fns.items():

@@ -25,6 +25,8 @@ from nvidia_terraform_modules_amd import ops  # noqa: E402
 
 SHAPES = [(256, 256, 128), (256, 512, 256), (512, 768, 384), (2304, 1536, 640),
           (4096, 4352, 512), (4096, 4096, 4096), (8192, 8192, 8192)]
+SHAPES_160 = [(160, 160, 128), (1280, 800, 384), (2560, 1600, 640), (2560, 2560, 2560),
+              (5120, 5120, 1280)]
 SHAPES_FP8 = [(256, 256, 256), (256, 512, 512), (512, 768, 768), (2304, 1536, 1280),
               (4096, 4352, 1024), (4096, 4096, 4096), (8192, 8192, 8192)]
 
@@ -48,7 +50,10 @@ def main():
         def gemm(a, b, out=None, v=v, fp8=fp8):
             return ops.gemm_fp8(a, b, out) if fp8 else ops.gemm_bf16(a, b, out, variant=v)
 
-        for (m, n, k) in (SHAPES_FP8 if fp8 else SHAPES):
+        tm, tn = ops.kernels.TILE_SHAPES.get(v, (0, 0))
+        for (m, n, k) in (SHAPES_FP8 if fp8 else SHAPES_160 if tn == 160 else SHAPES):
+            if tm and m % tm:
+                continue
             a = ops.fill_uniform_(torch.empty((m, k), dtype=dt, device=dev), 5 + m)
             b = ops.fill_uniform_(torch.empty((n, k), dtype=dt, device=dev), 6 + n)
             first = gemm(a, b)

@@ -46,27 +46,29 @@ using ::ntm::gemm::glds16;
 using ::ntm::gemm::raw_barrier;
 
 constexpr int TK = 64;
-constexpr int TN = 128;
 constexpr int kThreadsT = 256;
 constexpr int kGroupMT = 8;
 
-template <int MT>
+template <int MT, int NT = 4>
 struct Cfg {
-  static_assert(MT == 4 || MT == 8, "128x128 or 256x128 tiles");
+  static_assert(MT >= 4 && MT <= 8 && NT >= 4 && NT <= 5, "tile shapes 128..256 x 128..160");
   static constexpr int TM = 32 * MT;
-  static constexpr int S = MT == 4 ? 4 : 3;          // LDS ring depth (K-tiles)
-  static constexpr int P = MT + 4;                   // pieces per wave per K-tile
-  static constexpr int VMC = (S - 2) * P;            // counted wait
+  static constexpr int TN = 32 * NT;
   static constexpr int kA = TM * TK * 2;             // A bytes of a slot
   static constexpr int kSlot = kA + TN * TK * 2;     // + B
+  static constexpr int S = 4 * kSlot + 4096 <= 163840 ? 4 : 3;  // LDS ring depth (K-tiles)
+  static constexpr int P = MT + NT;                  // pieces per wave per K-tile
+  static constexpr int VMC = (S - 2) * P;            // counted wait
   static constexpr int kScratch = S * kSlot;         // dummy-piece target (4 KiB)
-  static constexpr int kLds = kScratch + 4 * 1024;   // 132 / 148 KiB
+  static constexpr int kLds = kScratch + 4 * 1024;   // 132 / 148 / 124 / 160 KiB
+  static_assert(kLds <= 163840, "160 KiB of LDS per CU");
+  static_assert(VMC <= 63, "vmcnt is 6 bits");
 };
 
-template <int MT>
+template <int MT, int NT = 4>
 __host__ __device__ inline bool shape_ok_t(int M, int N, int K) {
-  return M > 0 && N > 0 && K >= 2 * TK && (M % Cfg<MT>::TM) == 0 && (N % TN) == 0 &&
-         (K % (2 * TK)) == 0;
+  return M > 0 && N > 0 && K >= 2 * TK && (M % Cfg<MT, NT>::TM) == 0 &&
+         (N % Cfg<MT, NT>::TN) == 0 && (K % (2 * TK)) == 0;
 }
 
 template <int N>
@@ -77,7 +79,7 @@ __device__ __forceinline__ void wait_vmcnt_n() {
 
 struct CtxT {
   char* lds;
-  const __bf16* a_src;  // this lane's source for its first A row block, k-tile 0
+  const __bf16* a_src;  // this lane's source in A row block 0 of the tile, k-tile 0
   const __bf16* b_src;
   size_t a_rb16;        // 16 rows of A, in elements
   size_t b_rb16;
@@ -85,48 +87,50 @@ struct CtxT {
   int w, wr, wc;
 };
 
-template <int MT>
+template <int MT, int NT = 4>
 struct FragsT {
   bf16x8 a[MT][2];  // [m-tile][k-half]
-  bf16x8 b[4][2];   // [n-tile][k-half]
+  bf16x8 b[NT][2];  // [n-tile][k-half]
 };
 
-// LDS-DMA piece i (0 .. P-1) of this wave for K-tile kt: i < MT are A row
-// block w*MT/2 + i/2, k-half i%2; the last 4 are B row blocks 2w, 2w+1. kt >= T:
-// a dummy piece (source = the last K-tile, in bounds; destination = this
-// wave's 1 KiB of scratch).
-template <int MT>
+// LDS-DMA piece i (0 .. P-1) of this wave for K-tile kt. The tile's A has
+// 4 MT pieces (2 MT row blocks of 16 rows x 2 k-halves), B has 4 NT; wave w
+// stages A pieces g = w MT + i (i < MT) and B pieces g = w NT + (i - MT):
+// row block g / 2, k-half g % 2 (for even MT / NT: row blocks w MT/2 .. and
+// 2w, 2w+1 with both halves). kt >= T: a dummy piece (source = the last
+// K-tile, in bounds; destination = this wave's 1 KiB of scratch).
+template <int MT, int NT>
 __device__ __forceinline__ void issue_piece(const CtxT& c, int kt, int T, int i) {
-  using C = Cfg<MT>;
+  using C = Cfg<MT, NT>;
   const bool real = kt < T;
-  const size_t koff = (size_t)(real ? kt : T - 1) * TK + (i & 1) * 32;
-  char* slot = c.lds + (kt % C::S) * C::kSlot;
   const bool is_a = i < MT;
-  const int j = is_a ? i : i - MT;
-  const int rb = is_a ? c.w * (MT / 2) + (j >> 1) : 2 * c.w + (j >> 1);
-  const __bf16* src = (is_a ? c.a_src + (j >> 1) * c.a_rb16 : c.b_src + (j >> 1) * c.b_rb16) + koff;
-  char* dst = real ? slot + (is_a ? 0 : C::kA) + (rb * 2 + (i & 1)) * 1024
+  const int g = is_a ? c.w * MT + i : c.w * NT + (i - MT);
+  const int rb = g >> 1, kh = g & 1;
+  const size_t koff = (size_t)(real ? kt : T - 1) * TK + kh * 32;
+  char* slot = c.lds + (kt % C::S) * C::kSlot;
+  const __bf16* src = (is_a ? c.a_src + rb * c.a_rb16 : c.b_src + rb * c.b_rb16) + koff;
+  char* dst = real ? slot + (is_a ? 0 : C::kA) + (rb * 2 + kh) * 1024
                    : c.lds + C::kScratch + c.w * 1024;
   glds16(src, dst);
 }
 
-// Fragment read r (0 .. 2 MT + 7) of K-tile kt, k-half 0 first (that is what
-// the next iteration's first MFMAs consume): per k-half MT A then 4 B.
-template <int MT>
-__device__ __forceinline__ void read_frag(const CtxT& c, FragsT<MT>& f, int kt, int r) {
-  using C = Cfg<MT>;
+// Fragment read r (0 .. 2 (MT + NT) - 1) of K-tile kt, k-half 0 first (that
+// is what the next iteration's first MFMAs consume): per k-half MT A then NT B.
+template <int MT, int NT>
+__device__ __forceinline__ void read_frag(const CtxT& c, FragsT<MT, NT>& f, int kt, int r) {
+  using C = Cfg<MT, NT>;
   const char* slot = c.lds + (kt % C::S) * C::kSlot + c.frag_off;
-  const int ks = r / (MT + 4), i = r % (MT + 4);
+  const int ks = r / (MT + NT), i = r % (MT + NT);
   if (i < MT)
     f.a[i][ks] = *(const bf16x8*)(slot + ((c.wr * MT + i) * 2 + ks) * 1024);
   else
-    f.b[i - MT][ks] = *(const bf16x8*)(slot + C::kA + ((c.wc * 4 + (i - MT)) * 2 + ks) * 1024);
+    f.b[i - MT][ks] = *(const bf16x8*)(slot + C::kA + ((c.wc * NT + (i - MT)) * 2 + ks) * 1024);
 }
 
-template <int MT>
-__device__ __forceinline__ void read_frags(const CtxT& c, FragsT<MT>& f, int kt) {
+template <int MT, int NT>
+__device__ __forceinline__ void read_frags(const CtxT& c, FragsT<MT, NT>& f, int kt) {
 #pragma unroll
-  for (int r = 0; r < 2 * MT + 8; ++r) read_frag<MT>(c, f, kt, r);
+  for (int r = 0; r < 2 * (MT + NT); ++r) read_frag<MT, NT>(c, f, kt, r);
 }
 
 // MFMA with the accumulator pinned to AGPRs (asm): with the builtin, hipcc
@@ -142,36 +146,38 @@ __device__ __forceinline__ void mfma_acc(f32x4& acc, const bf16x8& b, const bf16
 // 4 MT MFMAs and the 2 MT + 8 fragment reads over the second half's (order
 // pinned with sched_barrier; B fragment first in every MFMA so a lane holds 4
 // consecutive output columns of one row for the epilogue's 8-byte stores).
-template <int MT>
-__device__ __forceinline__ void ktile(const CtxT& c, f32x4 (&acc)[MT][4], const FragsT<MT>& cur,
-                                      FragsT<MT>& nxt, int t, int T) {
-  constexpr int NM = 4 * MT, P = Cfg<MT>::P, NR = 2 * MT + 8;
+template <int MT, int NT>
+__device__ __forceinline__ void ktile(const CtxT& c, f32x4 (&acc)[MT][NT],
+                                      const FragsT<MT, NT>& cur, FragsT<MT, NT>& nxt, int t,
+                                      int T) {
+  using C = Cfg<MT, NT>;
+  constexpr int NM = NT * MT, P = C::P, NR = 2 * (MT + NT);
 #pragma unroll
   for (int j = 0; j < NM; ++j) {
-    mfma_acc(acc[j / 4][j % 4], cur.b[j % 4][0], cur.a[j / 4][0]);
+    mfma_acc(acc[j / NT][j % NT], cur.b[j % NT][0], cur.a[j / NT][0]);
     if ((j * P) / NM != ((j + 1) * P) / NM)
-      issue_piece<MT>(c, t + Cfg<MT>::S - 1, T, (j * P) / NM);
+      issue_piece<MT, NT>(c, t + C::S - 1, T, (j * P) / NM);
     __builtin_amdgcn_sched_barrier(0);
   }
-  wait_vmcnt_n<Cfg<MT>::VMC>();
+  wait_vmcnt_n<C::VMC>();
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   raw_barrier();
 #pragma unroll
   for (int j = 0; j < NM; ++j) {
-    mfma_acc(acc[j / 4][j % 4], cur.b[j % 4][1], cur.a[j / 4][1]);
+    mfma_acc(acc[j / NT][j % NT], cur.b[j % NT][1], cur.a[j / NT][1]);
     if ((j * NR) / NM != ((j + 1) * NR) / NM)
-      read_frag<MT>(c, nxt, t + 1, (j * NR) / NM);  // t + 1 == T: stale slot, unused
+      read_frag<MT, NT>(c, nxt, t + 1, (j * NR) / NM);  // t + 1 == T: stale slot, unused
     __builtin_amdgcn_sched_barrier(0);
   }
 }
 
-template <int MT>
+template <int MT, int NT>
 __device__ __forceinline__ void tile_coords_t(int M, int N, int& tm, int& tn) {
   const int nwg = gridDim.x, bid = blockIdx.x;
   const int xcd = bid & 7;
   const int q = nwg >> 3, r = nwg & 7;
   const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-  const int tiles_m = M / Cfg<MT>::TM, tiles_n = N / TN;
+  const int tiles_m = M / Cfg<MT, NT>::TM, tiles_n = N / Cfg<MT, NT>::TN;
   const int group = kGroupMT * tiles_n;
   const int gid = wgid / group;
   const int first_m = gid * kGroupMT;
@@ -181,13 +187,13 @@ __device__ __forceinline__ void tile_coords_t(int M, int N, int& tm, int& tn) {
   tn = in_group / gsz;
 }
 
-template <int MT>
+template <int MT, int NT = 4>
 __global__ void __launch_bounds__(kThreadsT, 1) gemm_bf16_tile_kernel(GemmArgs p) {
-  using C = Cfg<MT>;
+  using C = Cfg<MT, NT>;
   __shared__ __attribute__((aligned(16))) char smem[C::kLds];
   int tm, tn;
-  tile_coords_t<MT>(p.M, p.N, tm, tn);
-  const int m0 = tm * C::TM, n0 = tn * TN;
+  tile_coords_t<MT, NT>(p.M, p.N, tm, tn);
+  const int m0 = tm * C::TM, n0 = tn * C::TN;
   const int lane = threadIdx.x & 63;
 
   CtxT c;
@@ -198,35 +204,35 @@ __global__ void __launch_bounds__(kThreadsT, 1) gemm_bf16_tile_kernel(GemmArgs p
   {
     const int r = lane >> 2;
     const int cl = (lane & 3) ^ (((r >> 3) & 1) << 1);
-    c.a_src = p.A + (size_t)(m0 + c.w * (MT / 2) * 16 + r) * p.lda + cl * 8;
-    c.b_src = p.B + (size_t)(n0 + 2 * c.w * 16 + r) * p.ldb + cl * 8;
+    c.a_src = p.A + (size_t)(m0 + r) * p.lda + cl * 8;
+    c.b_src = p.B + (size_t)(n0 + r) * p.ldb + cl * 8;
     c.a_rb16 = (size_t)16 * p.lda;
     c.b_rb16 = (size_t)16 * p.ldb;
   }
   c.frag_off = (lane & 15) * 64 + ((lane >> 4) ^ ((lane >> 2) & 2)) * 16;
 
-  f32x4 acc[MT][4];
+  f32x4 acc[MT][NT];
 #pragma unroll
   for (int i = 0; i < MT; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int T = p.K / TK;
-  FragsT<MT> f0, f1;
+  FragsT<MT, NT> f0, f1;
 #pragma unroll
   for (int s = 0; s < C::S - 1; ++s)
 #pragma unroll
-    for (int i = 0; i < C::P; ++i) issue_piece<MT>(c, s, T, i);
+    for (int i = 0; i < C::P; ++i) issue_piece<MT, NT>(c, s, T, i);
   wait_vmcnt_n<C::VMC>();  // tile 0 landed (tiles 1 .. S-2 may be in flight)
   raw_barrier();
-  read_frags<MT>(c, f0, 0);
+  read_frags<MT, NT>(c, f0, 0);
 
   // T is even (shape rule): one straight loop body keeps the register roles
   // fixed at the back edge (an odd-T tail path made the allocator permute the
   // accumulators with ~63 v_accvgpr_mov at the join).
   for (int t = 0; t < T; t += 2) {
-    ktile<MT>(c, acc, f0, f1, t, T);
-    ktile<MT>(c, acc, f1, f0, t + 1, T);
+    ktile<MT, NT>(c, acc, f0, f1, t, T);
+    ktile<MT, NT>(c, acc, f1, f0, t + 1, T);
   }
 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // dummy pieces drained
@@ -235,9 +241,9 @@ __global__ void __launch_bounds__(kThreadsT, 1) gemm_bf16_tile_kernel(GemmArgs p
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
+    for (int nt = 0; nt < NT; ++nt) {
       const int row = m0 + c.wr * (16 * MT) + mt * 16 + (lane & 15);
-      const int col = n0 + c.wc * 64 + nt * 16 + (lane >> 4) * 4;
+      const int col = n0 + c.wc * (16 * NT) + nt * 16 + (lane >> 4) * 4;
       const f32x4 v = acc[mt][nt];
       bf16x4 o;
       o[0] = (__bf16)v[0];
@@ -248,13 +254,13 @@ __global__ void __launch_bounds__(kThreadsT, 1) gemm_bf16_tile_kernel(GemmArgs p
     }
 }
 
-template <int MT>
+template <int MT, int NT = 4>
 inline hipError_t launch_gemm_bf16_tile(const GemmArgs& a, hipStream_t stream) {
-  if (!shape_ok_t<MT>(a.M, a.N, a.K) || a.lda < a.K || a.ldb < a.K || a.ldc < a.N ||
+  if (!shape_ok_t<MT, NT>(a.M, a.N, a.K) || a.lda < a.K || a.ldb < a.K || a.ldc < a.N ||
       (a.lda % 8) || (a.ldb % 8) || (a.ldc % 4))
     return hipErrorInvalidValue;
-  const unsigned grid = (unsigned)((a.M / Cfg<MT>::TM) * (a.N / TN));
-  hipLaunchKernelGGL(gemm_bf16_tile_kernel<MT>, dim3(grid), dim3(kThreadsT), 0, stream, a);
+  const unsigned grid = (unsigned)((a.M / Cfg<MT, NT>::TM) * (a.N / Cfg<MT, NT>::TN));
+  hipLaunchKernelGGL((gemm_bf16_tile_kernel<MT, NT>), dim3(grid), dim3(kThreadsT), 0, stream, a);
   return hipGetLastError();
 }
 

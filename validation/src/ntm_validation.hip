@@ -69,15 +69,26 @@ constexpr int kDefaultVariant = 5;
 // rest in a second launch on a small tile, so a partial last round of big
 // tiles becomes a full round of small ones (6144^3: 3 rounds of 256x256 ->
 // 2 rounds + one of 256x128). Alone it picks 128x128 at 2048^3 (858 vs 467
-// TF/s for 256x256; hipBLASLt 773), 256x128 at 2560^3 and 4096x2048x4096
-// (825 / 1107 vs 757 / 950) and 256x256 at 3072^3, 4096^3 and 8192^3.
+// TF/s for 256x256; hipBLASLt 773), 160x160 at 2560^3 (958 vs 755; hipBLASLt
+// 934: 256 tiles = one full round), 256x128 at 4096x2048x4096 (1107 vs 950)
+// and 256x256 at 3072^3, 4096^3 and 8192^3.
 constexpr double kCUs = 256.0;
-constexpr double kEff256x128 = 0.75, kEff128 = 0.59;
+// 160-wide tiles: 160x160 at its full-chip rate (1109 TF/s at 5120^3, 4 full
+// rounds, relative to 1634; profiles/r1_t160/policy.log). 256x160 is priced
+// from a full round of it against one of 256x256 at 4096x2560x4096 (1121 vs
+// 1146 TF/s, r1_t160/policy_plan.log), not from its 8192x5120 rate (0.72):
+// at 0.72 the plan split 5120^3 and 8192x5120x4096 onto it and lost 2-3 %.
+struct SmallTile {
+  int variant, tm, tn;
+  double eff;
+};
+constexpr SmallTile kSmallTiles[] = {
+    {15, 128, 128, 0.59}, {16, 256, 128, 0.75}, {17, 160, 160, 0.68}, {18, 256, 160, 0.61}};
 constexpr double kSplitPenalty = 0.25;  // a second launch, in 128x128-tile-round units
 
 struct K1Plan {
   int top_rows;      // rows [0, top_rows) on the 256x256 kernel
-  int rest_variant;  // rows [top_rows, M) on 15 (128x128) or 16 (256x128)
+  int rest_variant;  // rows [top_rows, M) on a kSmallTiles variant (15..18)
 };
 
 inline K1Plan plan_k1(int M, int N, int K) {
@@ -93,12 +104,16 @@ inline K1Plan plan_k1(int M, int N, int K) {
     double bottom = 0.0;
     int v = 15;
     if (rest > 0) {
-      const double c128 = ntm::gemmt::shape_ok_t<4>(rest, N, K)
-                              ? rounds((rest / 128.0) * (N / 128.0)) / kEff128 : inf;
-      const double c256x128 = ntm::gemmt::shape_ok_t<8>(rest, N, K)
-                                  ? rounds((rest / 256.0) * (N / 128.0)) * 2.0 / kEff256x128 : inf;
-      bottom = c128 <= c256x128 ? c128 : c256x128;
-      v = c128 <= c256x128 ? 15 : 16;
+      bottom = inf;
+      for (const SmallTile& st : kSmallTiles) {
+        if (rest % st.tm || N % st.tn || K % 128 || K < 128) continue;
+        const double c = rounds((double)(rest / st.tm) * (N / st.tn)) *
+                         (st.tm * st.tn / 16384.0) / st.eff;
+        if (c < bottom) {
+          bottom = c;
+          v = st.variant;
+        }
+      }
     }
     const double cost = top + bottom + (m1 > 0 && rest > 0 ? kSplitPenalty : 0.0);
     if (cost <= best_cost) {  // ties: more rows on the 256x256 kernel
@@ -178,7 +193,7 @@ NTM_API int ntm_gemm_bf16_variant(int variant, const void* A, const void* B,
     if (variant >= 10) return (int)ntm::gemm3::launch_gemm_bf16_pp3_knob(a, variant + 2, S(stream));
     return (int)ntm::gemm5::launch_gemm_bf16_pp5(a, variant - 7, S(stream));
   }
-  if (variant == 15 || variant == 16) {  // 128x128 / 256x128 tiles (gemm_bf16_t128.hpp)
+  if (variant >= 15 && variant <= 18) {  // 128x128 / 256x128 / 160x160 / 256x160 tiles
     ntm::gemm::GemmArgs a;
     a.A = (const __bf16*)A;
     a.B = (const __bf16*)B;
@@ -189,8 +204,12 @@ NTM_API int ntm_gemm_bf16_variant(int variant, const void* A, const void* B,
     a.lda = lda;
     a.ldb = ldb;
     a.ldc = ldc;
-    return variant == 15 ? (int)ntm::gemmt::launch_gemm_bf16_tile<4>(a, S(stream))
-                         : (int)ntm::gemmt::launch_gemm_bf16_tile<8>(a, S(stream));
+    switch (variant) {  // gemm_bf16_t128.hpp
+      case 15: return (int)ntm::gemmt::launch_gemm_bf16_tile<4>(a, S(stream));
+      case 16: return (int)ntm::gemmt::launch_gemm_bf16_tile<8>(a, S(stream));
+      case 17: return (int)ntm::gemmt::launch_gemm_bf16_tile<5, 5>(a, S(stream));
+      default: return (int)ntm::gemmt::launch_gemm_bf16_tile<8, 5>(a, S(stream));
+    }
   }
   if (variant == 2 || variant == 3) {
     ntm::gemm4::Args a{(const __bf16*)A, (const __bf16*)B, (__bf16*)C, M, N, K,
