@@ -8,10 +8,13 @@ without a cloud account; this measures the GPU half on real hardware:
 * one process per GPU (``torch.distributed.run``), RCCL over xGMI,
 * each step = one hand-written K1 GEMM, M = N = K = 8192 bf16 (fp32 acc) per
   GPU on synthetic uniform[-1,1) operands generated on device (weak scaling),
-* W untimed warmup steps, then EXACTLY K steps bracketed by barrier +
-  synchronize, max over ranks; ``value`` = aggregate TFLOP/s over all GPUs,
+* an untimed clock-settle pre-warm (``--prewarm-s`` wall seconds of K1,
+  reported as ``prewarm_s``), then W untimed warmup steps, then EXACTLY K
+  steps bracketed by barrier + synchronize and timed with HIP events, max over
+  ranks; ``value`` = aggregate TFLOP/s over all GPUs,
 * after the timed region (never inside it): full-matrix verification against
-  an independent fp32 reference, hipBLASLt comparison on the same data, K2 HBM
+  an independent fp32 reference, K1 vs hipBLASLt on the same data measured
+  INTERLEAVED (ABAB rounds, median of each), K2 HBM
   check, C1 RCCL all-reduce busbw sweep (N > 1; --p2p adds the per-pair
   send/recv link matrix), the validation Job's own binary on the same n
   GPUs (its process-start -> verdict time), and the in-node
@@ -48,13 +51,18 @@ def parse(argv=None):
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--size", type=int, default=8192, help="M = N = K of the per-GPU GEMM")
+    ap.add_argument("--prewarm-s", type=float, default=0.5,
+                    help="untimed clock-settle pre-warm before the W warmup steps (wall seconds)")
+    ap.add_argument("--compare-rounds", type=int, default=7,
+                    help="ABAB rounds of the interleaved K1 vs hipBLASLt comparison")
     ap.add_argument("--no-check", action="store_true", help="skip full-matrix verification")
     ap.add_argument("--no-extras", action="store_true",
                     help="skip hipBLASLt comparison, HBM and all-reduce sweeps")
-    ap.add_argument("--allreduce-max-mib", type=int, default=1024)
-    ap.add_argument("--xgmi", action="store_true",
-                    help="N > 1: also sweep the hand-written xGMI all-reduce (C2, HIP IPC); its "
-                         "time includes staging copies + a host barrier per call")
+    ap.add_argument("--allreduce-max-mib", type=int, default=8192,
+                    help="largest all-reduce message (capped by free HBM)")
+    ap.add_argument("--no-xgmi", action="store_true",
+                    help="N > 1: skip the hand-written xGMI all-reduce sweep (C2, HIP IPC, "
+                         "zero-copy in place, device-side barriers) that runs next to RCCL")
     ap.add_argument("--p2p", action="store_true",
                     help="N > 1: also measure the send/recv bandwidth of every ordered rank pair "
                          "(one xGMI link each on a fully connected node)")
@@ -68,6 +76,70 @@ def parse(argv=None):
     return ap.parse_args(argv)
 
 
+class StepTimer:
+    """Stream-ordered timing of a launch sequence: HIP events on the current
+    stream on a GPU, the host clock (after the work returns) on the CPU path."""
+
+    def __init__(self, dev):
+        import torch
+
+        self.dev = dev
+        self.ev = ([torch.cuda.Event(enable_timing=True) for _ in range(2)]
+                   if dev.type == "cuda" else None)
+        self.t = [0.0, 0.0]
+
+    def start(self) -> None:
+        if self.ev:
+            self.ev[0].record()
+        else:
+            self.t[0] = time.perf_counter()
+
+    def stop(self) -> None:
+        if self.ev:
+            self.ev[1].record()
+        else:
+            self.t[1] = time.perf_counter()
+
+    def seconds(self) -> float:
+        """Elapsed seconds (synchronises on the end event)."""
+        if self.ev:
+            self.ev[1].synchronize()
+            return self.ev[0].elapsed_time(self.ev[1]) / 1e3
+        return self.t[1] - self.t[0]
+
+
+def prewarm_settle(fn, sync, min_s: float, chunk: int = 16) -> dict:
+    """Run ``fn`` untimed for at least ``min_s`` seconds of wall time (whole
+    chunks, synchronised), so clocks and power management reach steady state."""
+    t0 = time.perf_counter()
+    launches = 0
+    while True:
+        for _ in range(chunk):
+            fn()
+        launches += chunk
+        sync()
+        el = time.perf_counter() - t0
+        if el >= min_s:
+            return {"seconds": round(el, 3), "launches": launches}
+
+
+def interleaved_compare(fns: dict, dev, rounds: int, launches: int) -> dict:
+    """ABAB timing: in each round every callable runs ``launches`` times under
+    its own events; per-callable median over rounds (seconds per launch)."""
+    import statistics
+
+    per: dict = {k: [] for k in fns}
+    for _ in range(rounds):
+        for k, fn in fns.items():
+            tm = StepTimer(dev)
+            tm.start()
+            for _ in range(launches):
+                fn()
+            tm.stop()
+            per[k].append(tm.seconds() / launches)
+    return {k: {"median_s": statistics.median(v), "rounds_s": v} for k, v in per.items()}
+
+
 def run_validation_job(n: int, timeout_s: float = 240.0) -> dict:
     """Run validation/build/amdgpu-validate on GPUs 0..n-1 as a child process;
     returns a summary of its JSON report (never raises)."""
@@ -75,7 +147,7 @@ def run_validation_job(n: int, timeout_s: float = 240.0) -> dict:
                        "amdgpu-validate")
     if not os.path.exists(exe):
         return {"ran": False, "reason": "amdgpu-validate not built"}
-    cmd = [exe, "--gpus", str(n), "--size", "8192", "--iters", "10", "--no-xgmi", "--json"]
+    cmd = [exe, "--gpus", str(n), "--size", "8192", "--iters", "10", "--json"]
     env = {k: v for k, v in os.environ.items() if k != "NTM_FAULT_INJECT"}
     t0 = time.perf_counter()
     try:
@@ -101,6 +173,10 @@ def run_validation_job(n: int, timeout_s: float = 240.0) -> dict:
         "gemm_fp8_tflops_per_gpu": [g.get("gemm_fp8_tflops") for g in gpus],
         "hbm_copy_GBps_per_gpu": [g.get("hbm_copy_GBps") for g in gpus],
         "rccl_peak_busbw_GBps": max((r.get("busbw_GBps") or 0 for r in rccl), default=None),
+        "rccl_sizes_checked": len(rccl),
+        "rccl_wrong": sum(r.get("wrong") or 0 for r in rccl),
+        "xgmi_peak_busbw_GBps": max((r.get("busbw_GBps") or 0
+                                     for r in rep.get("xgmi_allreduce_bf16") or []), default=None),
         "xgmi_p2p_min_GBps": rep.get("xgmi_p2p_min_GBps"),
         "xgmi_p2p_GBps": p2p,
         "failures": rep.get("failures", [])[:8],
@@ -150,23 +226,37 @@ def main(argv=None) -> int:
     wl = GemmWorkload(args.size, dev, seed=20250117 + env.rank, backend=backend)
     sync()
     _CLOCK.mark("buffers_ready")
-
-    # ---- warmup (untimed)
-    for _ in range(max(1, args.warmup)):
-        wl.step()
+    wl.step()
     sync()
     _CLOCK.mark("first_kernel")
 
-    # ---- timed region: exactly K steps, barrier + sync on both sides
+    # ---- clock-settle pre-warm (untimed, wall-time based). A cold MI355X runs the
+    # first K1 launches at boost clock, overshoots its power limit ~2 ms in and
+    # throttles, then takes ~25 ms of sustained load to settle (rocprofv3 trace:
+    # 695 -> 950 -> 680 us per 8192^3 launch, profiles/r2_bench/). Without this the
+    # timed window of a short run lands on the transient.
+    prewarm = prewarm_settle(wl.step, sync, args.prewarm_s)
+
+    # ---- warmup (untimed): exactly W steps
+    for _ in range(args.warmup):
+        wl.step()
+    sync()
+
+    # ---- timed region: exactly K steps, barrier + sync on both sides; HIP events
+    # on the stream bracket the K launches, the host clock brackets the region
     dist.barrier(env)
     sync()
+    tmr = StepTimer(dev)
     t0 = time.perf_counter()
+    tmr.start()
     for _ in range(args.steps):
         wl.step()
+    tmr.stop()
     sync()
     t1 = time.perf_counter()
     dist.barrier(env)
-    elapsed = dist.all_reduce_max(env, t1 - t0)
+    elapsed = dist.all_reduce_max(env, tmr.seconds())
+    wall_elapsed = dist.all_reduce_max(env, t1 - t0)
     ms_per_step = elapsed / args.steps * 1e3
     total_tflops = n * wl.flops * args.steps / elapsed / 1e12
 
@@ -183,26 +273,34 @@ def main(argv=None) -> int:
 
     gpu_extras = not args.no_extras and not args.rehearsal
     if gpu_extras:
-        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        # K1 vs hipBLASLt on the same operands, INTERLEAVED (ABAB rounds, median of
+        # each), after re-settling the clock on hipBLASLt itself: neither side gets
+        # the warmer chip.
         cc = torch.empty_like(wl.c)
-        for _ in range(5):
-            torch.matmul(wl.a, wl.b.T, out=cc)
-        ev[0].record()
-        for _ in range(50):
-            torch.matmul(wl.a, wl.b.T, out=cc)
-        ev[1].record()
-        torch.cuda.synchronize(dev)
-        hb_ms = ev[0].elapsed_time(ev[1]) / 50
-        extras["hipblaslt_tflops_per_gpu_rank0"] = wl.flops / hb_ms / 1e9
-        extras["ours_tflops_per_gpu"] = total_tflops / n
+        blas = lambda: torch.matmul(wl.a, wl.b.T, out=cc)  # noqa: E731
+        prewarm_settle(blas, sync, 0.3)
+        cmp_ = interleaved_compare({"k1": wl.step, "hipblaslt": blas}, dev,
+                                   rounds=args.compare_rounds, launches=20)
         del cc
+        k1_tf = wl.flops / cmp_["k1"]["median_s"] / 1e12
+        hb_tf = wl.flops / cmp_["hipblaslt"]["median_s"] / 1e12
+        extras["interleaved_compare_rank0"] = {
+            "rounds": args.compare_rounds, "launches_per_round": 20,
+            "k1_tflops_median": round(k1_tf, 1), "hipblaslt_tflops_median": round(hb_tf, 1),
+            "k1_over_hipblaslt": round(k1_tf / hb_tf, 4),
+            "k1_tflops_rounds": [round(wl.flops / s / 1e12, 1) for s in cmp_["k1"]["rounds_s"]],
+            "hipblaslt_tflops_rounds": [round(wl.flops / s / 1e12, 1)
+                                        for s in cmp_["hipblaslt"]["rounds_s"]]}
+        extras["hipblaslt_tflops_per_gpu_rank0"] = hb_tf
+        extras["ours_tflops_per_gpu"] = total_tflops / n
         # same K1 with the fused ABFT row-checksum epilogue, then its O(n^2) check
-        ev[0].record()
+        tm = StepTimer(dev)
+        tm.start()
         for _ in range(50):
             wl.step_checked()
-        ev[1].record()
-        torch.cuda.synchronize(dev)
-        extras["abft_gemm_tflops_per_gpu_rank0"] = wl.flops / (ev[0].elapsed_time(ev[1]) / 50) / 1e9
+        tm.stop()
+        sync()
+        extras["abft_gemm_tflops_per_gpu_rank0"] = wl.flops / (tm.seconds() / 50) / 1e12
         ab = wl.abft()
         extras["abft_rank0"] = ab.as_dict()
         if not ab.ok:
@@ -220,8 +318,10 @@ def main(argv=None) -> int:
 
     if not args.no_extras and n > 1:
         # nccl-tests style: bf16 from 8 B (latency end) and fp32 from 1 MiB, x4 steps
-        sizes = coll.sweep_sizes(1 << 20, args.allreduce_max_mib << 20, factor=4)
-        res = coll.all_reduce_sweep(env, coll.sweep_sizes(8, args.allreduce_max_mib << 20, 4),
+        max_b = int(dist.all_reduce_max(env, -coll.max_message_bytes(
+            env, args.allreduce_max_mib << 20)) * -1)   # the smallest cap over ranks
+        sizes = coll.sweep_sizes(1 << 20, max_b, factor=4)
+        res = coll.all_reduce_sweep(env, coll.sweep_sizes(8, max_b, 4),
                                     dtype="bf16", iters=10, warmup=3)
         res32 = coll.all_reduce_sweep(env, sizes, dtype="fp32", iters=10, warmup=3)
         for key, rs in (("allreduce_bf16", res), ("allreduce_fp32", res32)):
@@ -240,10 +340,12 @@ def main(argv=None) -> int:
             extras["p2p_send_GBps"] = pm.as_dict()
             if pm.errors:
                 verified = False
-        if args.xgmi and not args.rehearsal:
+        if not args.no_xgmi and not args.rehearsal and n <= 8:
+            # C2 next to RCCL: the same sizes, in place on the registered buffer,
+            # no host sync / barrier / staging per call (device-side barriers)
             from nvidia_terraform_modules_amd.parallel.xgmi import XgmiAllReduce
 
-            xs = [b for b in sizes if b <= 256 << 20]
+            xs = [b for b in coll.sweep_sizes(1 << 10, max_b, 4) if b <= 1 << 30]
             ar = XgmiAllReduce(env, max_bytes=max(xs), nblk=64)
             xr = coll.all_reduce_sweep(env, xs, dtype="bf16", iters=10, warmup=2, impl=ar)
             extras["xgmi_allreduce_bf16"] = [
@@ -294,6 +396,11 @@ def main(argv=None) -> int:
             "baseline_config": BASELINE_CONFIG,
         },
         "verified": verified,
+        "timing": "HIP events around the K launches (max over ranks); host clock "
+                  "around the barrier+sync-bracketed region in timed_region_wall_s",
+        "timed_region_wall_s": round(wall_elapsed, 6),
+        "prewarm_s": prewarm["seconds"],
+        "prewarm_launches": prewarm["launches"],
         # in-node part of time-to-GPU-ready = the Job binary's process start -> verdict on
         # these n GPUs; the bench process's own (torch import included) is kept beside it
         "time_to_gpu_ready_in_node_s": (

@@ -1,4 +1,6 @@
-"""ctypes binding to ``libntm_validation.so`` (the gfx950 HIP kernels).
+"""ctypes binding to ``libntm_validation.so`` (the gfx950 HIP kernels) and,
+on demand, ``libntm_experimental.so`` (non-default K1 builds and diagnostics,
+for tests and tools only).
 
 The library is loaded AFTER ``torch`` so that its ``libamdhip64.so.7``
 dependency binds to the HIP runtime PyTorch already mapped (same soname): one
@@ -15,8 +17,10 @@ import torch  # noqa: F401  (must be imported before the HIP library)
 
 _HERE = Path(__file__).resolve().parent
 LIB_PATH = _HERE / "libntm_validation.so"
+EXP_LIB_PATH = _HERE / "libntm_experimental.so"
 
 _lib: ctypes.CDLL | None = None
+_exp: ctypes.CDLL | None = None
 
 
 class NativeLibraryMissing(RuntimeError):
@@ -31,22 +35,14 @@ def _declare(lib: ctypes.CDLL) -> None:
         "ntm_gemm_bf16": ([c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp], c_int),
         "ntm_gemm_bf16_variant": (
             [c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp], c_int),
-        "ntm_gemm_bf16_knob": (
-            [c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp], c_int),
-        "ntm_gemm_bf16_stamp": (
-            [c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp], c_int),
-        "ntm_mfma_f8_probe": ([c_vp, c_vp, c_vp, c_vp], c_int),
         "ntm_gemm_fp8": ([c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp], c_int),
         "ntm_gemm_fp8_shape_ok": ([c_int, c_int, c_int], c_int),
-        "ntm_mfma_rate": ([c_int, c_int, c_int, c_vp, c_vp, c_vp], c_int),
         "ntm_gemm_bf16_rowsum": (
             [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp], c_int),
         "ntm_abft_check": ([c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int,
                             c_vp, c_vp, c_vp], c_int),
         "ntm_abft_result_bytes": ([], c_int),
         "ntm_fill_uniform_bf16": ([c_vp, c_size, ctypes.c_ulonglong, c_float, c_vp], c_int),
-        "ntm_gemm_fp8_knob": ([c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
-                               c_vp], c_int),
         "ntm_k1_plan": ([c_int, c_int, c_int, c_vp, c_vp], c_int),
         "ntm_fill_uniform_e4m3": ([c_vp, c_size, ctypes.c_ulonglong, c_float, c_vp], c_int),
         "ntm_ref_gemm_f32_e4m3": (
@@ -79,6 +75,42 @@ def lib() -> ctypes.CDLL:
     _lib = ctypes.CDLL(str(LIB_PATH), mode=mode)
     _declare(_lib)
     return _lib
+
+
+def _declare_experimental(lib: ctypes.CDLL) -> None:
+    c_int, c_vp = ctypes.c_int, ctypes.c_void_p
+    gemm = [c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp]
+    sig = {
+        "ntm_experimental_version": ([], ctypes.c_char_p),
+        "ntm_gemm_bf16_experimental": (gemm, c_int),
+        "ntm_gemm_bf16_knob": (gemm, c_int),
+        "ntm_gemm_bf16_stamp": (
+            [c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp], c_int),
+        "ntm_mfma_f8_probe": ([c_vp, c_vp, c_vp, c_vp], c_int),
+        "ntm_mfma_rate": ([c_int, c_int, c_int, c_vp, c_vp, c_vp], c_int),
+        "ntm_gemm_fp8_knob": ([c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                               c_vp], c_int),
+    }
+    for name, (argt, rest) in sig.items():
+        fn = getattr(lib, name)
+        fn.argtypes = argt
+        fn.restype = rest
+
+
+def lib_experimental() -> ctypes.CDLL:
+    """The experimental/diagnostic library (non-default K1 builds, schedule
+    knobs, probes). Loaded on first use; the shipping paths never touch it."""
+    global _exp
+    if _exp is not None:
+        return _exp
+    lib()  # HIP runtime binding order: the shipping library (and torch) first
+    if not EXP_LIB_PATH.exists():
+        raise NativeLibraryMissing(
+            f"{EXP_LIB_PATH} not found. Build it with "
+            "`python -m nvidia_terraform_modules_amd.ops.build`.")
+    _exp = ctypes.CDLL(str(EXP_LIB_PATH), mode=os.RTLD_NOW | getattr(os, "RTLD_GLOBAL", 0))
+    _declare_experimental(_exp)
+    return _exp
 
 
 def available() -> bool:

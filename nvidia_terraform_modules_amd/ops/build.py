@@ -4,6 +4,9 @@ Outputs (all in-tree, so they travel to the GPU box with the repo snapshot):
 
 * ``nvidia_terraform_modules_amd/ops/libntm_validation.so`` - K1/K2/K3 kernels
   behind a C ABI, loaded by :mod:`nvidia_terraform_modules_amd.ops._lib`.
+* ``nvidia_terraform_modules_amd/ops/libntm_experimental.so`` - non-default
+  K1 builds, schedule knobs and diagnostics (tests and tools only; never
+  linked into the shipping library or the Job binary).
 * ``validation/build/amdgpu-validate`` - the standalone validation-Job binary
   (HIP + RCCL, no Python/PyTorch in the container image).
 
@@ -28,6 +31,9 @@ SRC = VALIDATION / "src"
 BUILD = VALIDATION / "build"
 PKG_OPS = Path(__file__).resolve().parent
 LIB_NAME = "libntm_validation.so"
+EXP_LIB_NAME = "libntm_experimental.so"
+# the shipping sources: the Job binary and libntm_validation.so link exactly these
+SHIPPING_SRCS = ("ntm_validation.hip", "xgmi_allreduce.hip")
 BIN_NAME = "amdgpu-validate"
 
 COMMON_FLAGS = [
@@ -65,16 +71,22 @@ def _deps() -> list[Path]:
     return sorted(INCLUDE.rglob("*.hpp")) + sorted(SRC.glob("*.hip")) + sorted(SRC.glob("*.cpp"))
 
 
-def build_library(force: bool = False, verbose: bool = True) -> Path:
-    out = PKG_OPS / LIB_NAME
-    srcs = [SRC / "ntm_validation.hip", SRC / "xgmi_allreduce.hip"]
-    srcs = [s for s in srcs if s.exists()]
+def _build_so(name: str, srcs: list[Path], force: bool, verbose: bool) -> Path:
+    out = PKG_OPS / name
     if force or _stale(out, _deps()):
         BUILD.mkdir(parents=True, exist_ok=True)
-        tmp = BUILD / (LIB_NAME + ".tmp")
+        tmp = BUILD / (name + ".tmp")
         _run([hipcc(), *COMMON_FLAGS, "-shared", *map(str, srcs), "-o", str(tmp)], verbose)
         os.replace(tmp, out)
     return out
+
+
+def build_library(force: bool = False, verbose: bool = True) -> Path:
+    return _build_so(LIB_NAME, [SRC / s for s in SHIPPING_SRCS], force, verbose)
+
+
+def build_experimental(force: bool = False, verbose: bool = True) -> Path:
+    return _build_so(EXP_LIB_NAME, [SRC / "ntm_experimental.hip"], force, verbose)
 
 
 # Host-only AddressSanitizer / UBSan variant of the Job binary: instruments the
@@ -92,8 +104,7 @@ def build_binary(force: bool = False, verbose: bool = True, asan: bool = False) 
         return out
     if force or _stale(out, _deps()):
         BUILD.mkdir(parents=True, exist_ok=True)
-        srcs = [SRC / "ntm_validation.hip", SRC / "xgmi_allreduce.hip"]
-        srcs = [str(s) for s in srcs if s.exists()]
+        srcs = [str(SRC / s) for s in SHIPPING_SRCS]
         cmd = [
             hipcc(), *COMMON_FLAGS, *(ASAN_FLAGS if asan else []), "-x", "hip", str(main), *srcs,
             "-I/opt/rocm/include", "-L/opt/rocm/lib", "-lrccl", "-lpthread",
@@ -124,6 +135,7 @@ def build_all(force: bool = False, verbose: bool = True, asan: bool = False) -> 
     lib = build_library(force=force, verbose=verbose)
     binary = build_binary(force=force, verbose=verbose)
     res = {"library": str(lib), "binary": str(binary),
+           "experimental": str(build_experimental(force=force, verbose=verbose)),
            "exporter": str(build_exporter(force=force, verbose=verbose))}
     if asan:
         res["binary_asan"] = str(build_binary(force=force, verbose=verbose, asan=True))

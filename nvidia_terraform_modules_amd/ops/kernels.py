@@ -10,7 +10,7 @@ from dataclasses import dataclass
 
 import torch
 
-from ._lib import check, lib, stream_handle
+from ._lib import check, lib, lib_experimental, stream_handle
 
 BM = BN = 256
 BK = 64
@@ -37,6 +37,13 @@ GEMM_VARIANTS = {"default": 0, "pingpong8": 1, "wave128": 2, "wave128d4": 3, "pi
                  "tile256x128": 16, "tile160": 17, "tile256x160": 18}
 
 
+# variants built only into libntm_experimental.so (tests / tools): never selected
+# by the default dispatch, not present in the shipping library or Job binary
+EXPERIMENTAL_VARIANTS = frozenset({"pingpong8", "wave128", "wave128d4", "pingpong8p",
+                                   "pingpong8w", "pingpong8wi", "pingpong8ww", "pingpong8cw",
+                                   "pingpong8cwe", "pingpong8cwn", "pingpong8cwne",
+                                   "pingpong8pw"})
+
 # (TM, TN) of the 4-wave tile kernels (gemm_bf16_t128.hpp)
 TILE_SHAPES = {"tile128": (128, 128), "tile256x128": (256, 128), "tile160": (160, 160),
                "tile256x160": (256, 160)}
@@ -48,9 +55,12 @@ def _tile128_shape_ok(m: int, n: int, k: int, tm: int = 128, tn: int = 128) -> b
 
 def k1_plan(m: int, n: int, k: int) -> tuple[int, str]:
     """The default dispatch's plan: (rows on the 256x256 kernel, variant of the
-    remaining rows) - host-side, no GPU needed."""
+    remaining rows) - host-side, no GPU needed. Raises ValueError when no
+    combination of the K1 kernels tiles (M, N, K)."""
     top, rest = ctypes.c_int(), ctypes.c_int()
-    check(lib().ntm_k1_plan(m, n, k, ctypes.byref(top), ctypes.byref(rest)), "ntm_k1_plan")
+    rc = lib().ntm_k1_plan(m, n, k, ctypes.byref(top), ctypes.byref(rest))
+    if rc != 0:
+        raise ValueError(f"shape ({m},{n},{k}) not tiled by the K1 kernels")
     names = {v: kname for kname, v in GEMM_VARIANTS.items()}
     return top.value, names[rest.value]
 
@@ -81,9 +91,7 @@ def gemm_bf16(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
         if not _tile128_shape_ok(m, n, k, tm, tn):
             raise ValueError(f"shape ({m},{n},{k}) not tiled by the {tm}x{tn} kernel (K % 128)")
     elif variant == "default":
-        if not (gemm_shape_ok(m, n, k)
-                or any(_tile128_shape_ok(m, n, k, tm, tn) for tm, tn in TILE_SHAPES.values())):
-            raise ValueError(f"shape ({m},{n},{k}) not tiled by the K1 kernels")
+        k1_plan(m, n, k)        # the native plan is the one authority on what it serves
     elif not gemm_shape_ok(m, n, k):
         raise ValueError(f"shape ({m},{n},{k}) not tiled by the 256x256x64 kernel")
     if out is None:
@@ -92,10 +100,16 @@ def gemm_bf16(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
     if tuple(out.shape) != (m, n):
         raise ValueError("out has the wrong shape")
     if variant.startswith("knob"):            # experimental tuning sweep: "knob<N>"
-        rc = lib().ntm_gemm_bf16_knob(int(variant[4:]), a.data_ptr(), b.data_ptr(),
-                                      out.data_ptr(), m, n, k, a.stride(0), b.stride(0),
-                                      out.stride(0), stream_handle())
+        rc = lib_experimental().ntm_gemm_bf16_knob(
+            int(variant[4:]), a.data_ptr(), b.data_ptr(), out.data_ptr(), m, n, k, a.stride(0),
+            b.stride(0), out.stride(0), stream_handle())
         check(rc, "ntm_gemm_bf16_knob")
+        return out
+    if variant in EXPERIMENTAL_VARIANTS:
+        rc = lib_experimental().ntm_gemm_bf16_experimental(
+            GEMM_VARIANTS[variant], a.data_ptr(), b.data_ptr(), out.data_ptr(), m, n, k,
+            a.stride(0), b.stride(0), out.stride(0), stream_handle())
+        check(rc, "ntm_gemm_bf16_experimental")
         return out
     rc = lib().ntm_gemm_bf16_variant(
         GEMM_VARIANTS[variant], a.data_ptr(), b.data_ptr(), out.data_ptr(), m, n, k,
@@ -132,7 +146,7 @@ def gemm_fp8(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
     if tuple(out.shape) != (m, n):
         raise ValueError("out has the wrong shape")
     if knob:
-        rc = lib().ntm_gemm_fp8_knob(a.data_ptr(), b.data_ptr(), out.data_ptr(), m, n, k,
+        rc = lib_experimental().ntm_gemm_fp8_knob(a.data_ptr(), b.data_ptr(), out.data_ptr(), m, n, k,
                                      a.stride(0), b.stride(0), out.stride(0), int(knob),
                                      stream_handle())
     else:

@@ -67,18 +67,34 @@ class CollResult:
         return asdict(self)
 
 
+def _periodic(count: int, scale: int, dtype: torch.dtype, device) -> torch.Tensor:
+    # [1, 2, 4, 8] * scale repeated: no index temporaries, so multi-GiB sweeps
+    # (up to 8 GiB) allocate only the message itself
+    unit = torch.tensor([1, 2, 4, 8], dtype=torch.float32, device=device) * scale
+    return unit.to(dtype).repeat((count + 3) // 4)[:count].contiguous()
+
+
 def _pattern(count: int, rank: int, dtype: torch.dtype, device) -> torch.Tensor:
     # 2^(i%4) * (rank+1): every partial sum is 2^j * s with s <= n(n+1)/2 <= 36
     # for n <= 8, an integer < 256 -> exact in bf16 whatever the reduction order
-    base = torch.bitwise_left_shift(torch.ones(count, device=device, dtype=torch.int64),
-                                    torch.arange(count, device=device, dtype=torch.int64) % 4)
-    return (base * (rank + 1)).to(dtype)
+    return _periodic(count, rank + 1, dtype, device)
 
 
 def _expected(count: int, n: int, dtype: torch.dtype, device) -> torch.Tensor:
-    base = torch.bitwise_left_shift(torch.ones(count, device=device, dtype=torch.int64),
-                                    torch.arange(count, device=device, dtype=torch.int64) % 4)
-    return (base * (n * (n + 1) // 2)).to(dtype)
+    return _periodic(count, n * (n + 1) // 2, dtype, device)
+
+
+def max_message_bytes(env: DistEnv, want: int, buffers: int = 3) -> int:
+    """Largest power-of-two message <= ``want`` such that ``buffers`` copies fit
+    in 40 % of this rank's free HBM (the sweep holds buffer, expected, mask)."""
+    if env.device.type != "cuda":
+        return want
+    free, _ = torch.cuda.mem_get_info(env.device)
+    cap = int(0.4 * free) // buffers
+    b = 8
+    while b * 2 <= min(want, cap):
+        b *= 2
+    return b
 
 
 def _sync(env: DistEnv) -> None:
@@ -93,6 +109,9 @@ def all_reduce_sweep(env: DistEnv, sizes: list[int], dtype: str = "bf16", iters:
 
     ``impl(tensor)`` overrides the collective (e.g. the xGMI mesh path); the
     default is ``torch.distributed.all_reduce`` (RCCL on GPUs, gloo on CPU).
+    An ``impl`` with a ``buffer(count)`` method (``XgmiAllReduce``) gets its
+    operand there, so the sweep times its zero-copy in-place path - the same
+    in-place semantics as RCCL's ``all_reduce(t)``.
     """
     tdt = _DTYPES[dtype]
     esz = torch.empty((), dtype=tdt).element_size()
@@ -102,12 +121,15 @@ def all_reduce_sweep(env: DistEnv, sizes: list[int], dtype: str = "bf16", iters:
     for nbytes in sizes:
         count = max(1, nbytes // esz)
         buf = _pattern(count, env.rank, tdt, env.device)
+        if hasattr(impl, "buffer"):
+            buf = impl.buffer(count).view(tdt).copy_(buf)
         errors = 0
         if check:
             run(buf)
             _sync(env)
             exp = _expected(count, n, tdt, env.device)
             errors = int((buf != exp).sum().item())
+            del exp
         for _ in range(warmup):
             run(buf)
         _sync(env)
@@ -140,8 +162,10 @@ class P2pMatrix:
 
     def as_dict(self) -> dict:
         return {"ranks": self.ranks, "bytes": self.bytes,
-                "GBps": [[None if v is None else round(v, 1) for v in row] for row in self.gbps],
-                "min_GBps": None if self.min_gbps() is None else round(self.min_gbps(), 1),
+                # 4 decimals: a loaded CPU/gloo rehearsal moves < 0.05 GB/s, which
+                # one decimal rounded to 0 and read as a dead link
+                "GBps": [[None if v is None else round(v, 4) for v in row] for row in self.gbps],
+                "min_GBps": None if self.min_gbps() is None else round(self.min_gbps(), 4),
                 "errors": self.errors}
 
 

@@ -10,8 +10,10 @@ xgmi_allreduce.hpp):
 * :class:`XgmiAllReduce` - one process per GPU (torch.distributed env): each
   rank allocates in/out/signal buffers, exchanges HIP IPC handles with
   ``all_gather_object`` and opens its peers' buffers, then every call runs the
-  two-shot kernel over the xGMI mesh. Multi-GPU numbers are pending hardware
-  (this environment exposes one GPU); bench.py runs it only with ``--xgmi``.
+  kernel over the xGMI mesh, in place on the registered buffer, synchronised
+  by the kernel's own device-side barriers (no host sync per call). Multi-GPU
+  numbers are pending hardware (this environment exposes one GPU); bench.py
+  sweeps it next to RCCL at N > 1 by default (``--no-xgmi`` to skip).
 """
 from __future__ import annotations
 
@@ -56,13 +58,19 @@ def _ptrs(xs) -> "ctypes.Array":
 
 
 def simulate_allreduce(inputs: list[torch.Tensor], nblk: int = 16, one_shot: bool = False,
-                       epoch: int = 1) -> tuple[list[torch.Tensor], int]:
+                       epoch: int = 1, inplace: bool = False,
+                       sigs: list[torch.Tensor] | None = None) -> tuple[list[torch.Tensor], int]:
     """All-reduce (sum) N same-shaped bf16 tensors living on ONE device, as N
     simulated ranks. Returns (outputs, timeout_code) - 0 means no barrier
-    timed out."""
+    timed out. ``inplace`` (two-shot only) reduces into the inputs themselves;
+    ``sigs`` reuses signal buffers across calls (epochs must then grow)."""
     n = len(inputs)
     if not 1 <= n <= MAX_RANKS:
         raise ValueError("1..8 ranks")
+    if n * nblk > 1024:
+        raise ValueError("nranks * nblk must be <= 1024 (all blocks co-resident)")
+    if inplace and one_shot:
+        raise ValueError("one-shot cannot run in place")
     count = inputs[0].numel()
     if count % (8 * n):
         raise ValueError("count must be a multiple of 8 * nranks")
@@ -71,9 +79,10 @@ def simulate_allreduce(inputs: list[torch.Tensor], nblk: int = 16, one_shot: boo
             raise ValueError("inputs must be contiguous bf16 of equal size")
     L = _declare()
     dev = inputs[0].device
-    outs = [torch.empty_like(t) for t in inputs]
-    sig_bytes = L.ntm_xgmi_signal_bytes(nblk)
-    sigs = [torch.zeros(sig_bytes // 4, dtype=torch.int32, device=dev) for _ in range(n)]
+    outs = list(inputs) if inplace else [torch.empty_like(t) for t in inputs]
+    if sigs is None:
+        sig_bytes = L.ntm_xgmi_signal_bytes(nblk)
+        sigs = [torch.zeros(sig_bytes // 4, dtype=torch.int32, device=dev) for _ in range(n)]
     err = torch.zeros(1, dtype=torch.int32, device=dev)
     rc = L.ntm_xgmi_allreduce_bf16(
         _ptrs([t.data_ptr() for t in inputs]), _ptrs([t.data_ptr() for t in outs]),
@@ -84,16 +93,37 @@ def simulate_allreduce(inputs: list[torch.Tensor], nblk: int = 16, one_shot: boo
     return outs, int(err.item())
 
 
+class _DeviceArray:
+    """``__cuda_array_interface__`` over a raw device pointer, so torch can
+    view a natively allocated (IPC-registered) buffer without copying."""
+
+    def __init__(self, ptr: int, numel: int):
+        self.__cuda_array_interface__ = {"shape": (numel,), "typestr": "<i2",
+                                         "data": (ptr, False), "version": 3, "strides": None}
+
+
 class XgmiAllReduce:
     """Two-shot all-reduce across the ranks of a torch.distributed group, one
-    process per GPU, buffers shared through HIP IPC (xGMI peer mappings)."""
+    process per GPU, buffers shared through HIP IPC (xGMI peer mappings).
 
-    def __init__(self, env, max_bytes: int, nblk: int = 64):
+    Zero-copy use: write the payload into :meth:`buffer` (a bf16 view of this
+    rank's registered buffer) and call :meth:`run` - the kernel reduces IN
+    PLACE, stream-ordered, with its own device-side entry/exit barriers, so
+    there is no host sync, no host barrier and no staging copy per call.
+    ``ar(t)`` on any other tensor stages it in and out with two stream-ordered
+    copies (still no host sync). Messages up to ``one_shot_max_bytes`` take the
+    one-shot kernel (one read pass over all peers, 2 barriers instead of 3).
+    """
+
+    def __init__(self, env, max_bytes: int, nblk: int = 64, one_shot_max_bytes: int = 256 << 10):
         from .dist import all_gather_obj
 
         if env.world_size > MAX_RANKS:
             raise ValueError("at most 8 ranks (one MI355X node)")
+        if not 1 <= nblk <= 1024:
+            raise ValueError("nblk must be in 1..1024")
         self.env, self.nblk, self.max_bytes = env, nblk, max_bytes
+        self.one_shot_max_bytes = min(one_shot_max_bytes, max_bytes)
         self.L = L = _declare()
         self._own = []
         handles = {}
@@ -123,30 +153,57 @@ class XgmiAllReduce:
         self.epoch = 0
         self.err = torch.zeros(1, dtype=torch.int32, device=env.device)
 
-    def __call__(self, t: torch.Tensor) -> torch.Tensor:
-        """In-place sum over ranks of bf16 tensor ``t`` (staged through the
-        registered buffers)."""
-        nbytes = t.numel() * t.element_size()
-        if t.dtype != torch.bfloat16 or nbytes > self.max_bytes or not t.is_contiguous():
-            raise ValueError("contiguous bf16 up to max_bytes")
-        n = self.env.world_size
-        count = t.numel()
-        if count % (8 * n):
+    def buffer(self, numel: int) -> torch.Tensor:
+        """bf16 view of the first ``numel`` elements of this rank's registered
+        buffer (the in-place operand of :meth:`run`)."""
+        if numel * 2 > self.max_bytes:
+            raise ValueError("numel exceeds max_bytes")
+        arr = _DeviceArray(self.ptrs["in"][self.env.rank], numel)
+        return torch.as_tensor(arr, device=self.env.device).view(torch.bfloat16)
+
+    def _check_count(self, count: int) -> None:
+        if count * 2 > self.max_bytes:
+            raise ValueError("message larger than max_bytes")
+        if count % (8 * self.env.world_size):
             raise ValueError("numel must be a multiple of 8 * world_size")
+
+    def _launch(self, count: int, one_shot: bool) -> None:
         self.epoch += 1
-        # stage t into my registered "in" buffer; the host barrier after the
-        # stream sync guarantees every peer's input is complete before any
-        # rank's kernel reads it over xGMI
-        _copy_d2d(self.ptrs["in"][self.env.rank], t.data_ptr(), nbytes)
-        torch.cuda.current_stream().synchronize()
-        from .dist import barrier
-        barrier(self.env)
+        n = self.env.world_size
+        out = self.ptrs["out"] if one_shot else self.ptrs["in"]
         rc = self.L.ntm_xgmi_allreduce_bf16(
-            _ptrs(self.ptrs["in"]), _ptrs(self.ptrs["out"]), _ptrs(self.ptrs["sig"]), n,
-            self.env.rank, 1, self.nblk, count, self.epoch, self.err.data_ptr(), 0,
-            stream_handle())
+            _ptrs(self.ptrs["in"]), _ptrs(out), _ptrs(self.ptrs["sig"]), n,
+            self.env.rank, 1, self.nblk, count, self.epoch, self.err.data_ptr(),
+            1 if one_shot else 0, stream_handle())
         check(rc, "ntm_xgmi_allreduce_bf16")
-        _copy_d2d(t.data_ptr(), self.ptrs["out"][self.env.rank], nbytes)
+
+    def run(self, numel: int) -> torch.Tensor:
+        """Sum over ranks of ``buffer(numel)``, in place, stream-ordered."""
+        self._check_count(numel)
+        if numel * 2 <= self.one_shot_max_bytes:
+            self._launch(numel, one_shot=True)
+            _copy_d2d(self.ptrs["in"][self.env.rank], self.ptrs["out"][self.env.rank], numel * 2)
+        else:
+            self._launch(numel, one_shot=False)
+        return self.buffer(numel)
+
+    def __call__(self, t: torch.Tensor) -> torch.Tensor:
+        """In-place sum over ranks of bf16 tensor ``t``. Zero-copy when ``t``
+        is :meth:`buffer`; otherwise staged in and out with stream-ordered
+        copies. Never synchronises the host."""
+        nbytes = t.numel() * t.element_size()
+        if t.dtype != torch.bfloat16 or not t.is_contiguous():
+            raise ValueError("contiguous bf16 tensor expected")
+        count = t.numel()
+        self._check_count(count)
+        mine = self.ptrs["in"][self.env.rank]
+        if t.data_ptr() == mine:
+            self.run(count)
+            return t
+        _copy_d2d(mine, t.data_ptr(), nbytes)
+        one = nbytes <= self.one_shot_max_bytes
+        self._launch(count, one_shot=one)
+        _copy_d2d(t.data_ptr(), self.ptrs["out" if one else "in"][self.env.rank], nbytes)
         return t
 
     def timed_out(self) -> bool:

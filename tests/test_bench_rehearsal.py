@@ -44,7 +44,7 @@ def test_torchrun_launch_one_json_line(nproc):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
            f"--nproc-per-node={nproc}", "--master-addr=127.0.0.1", f"--master-port={_port()}",
            str(ROOT / "bench.py"), "--gpus", str(nproc), "--steps", "3", "--warmup", "1",
-           "--size", "256", "--allreduce-max-mib", "1", "--rehearsal", "--p2p"]
+           "--size", "256", "--allreduce-max-mib", "1", "--rehearsal", "--p2p", "--prewarm-s", "0.2"]
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=_env(), cwd=ROOT)
     assert p.returncode == 0, p.stderr[-3000:]
     lines = _json_lines(p.stdout)
@@ -58,6 +58,9 @@ def test_torchrun_launch_one_json_line(nproc):
     assert d["higher_is_better"] is True and d["scaling"] == "weak" and d["dtype"] == "bf16"
     assert d["value"] > 0 and d["verified"] is True and d["rehearsal"] is True
     assert "NOT a measurement" in d["data"]
+    # clock-settle pre-warm (untimed, wall-time based) and event timing are reported
+    assert d["prewarm_s"] >= 0.2 and d["prewarm_launches"] > 0
+    assert d["timed_region_wall_s"] > 0 and "HIP events" in d["timing"]
     # the Job binary step runs (here: no GPU -> its environment-error verdict) and the
     # other ranks have left before it without breaking the one-line contract
     job = d["validation_job"]
@@ -98,6 +101,9 @@ def test_bench_on_one_gpu_json_contract(tmp_path):
     assert CONTRACT_KEYS <= set(d) and d["n_gpus"] == 1 and d["verified"] is True
     assert d["value"] > 50 and "rehearsal" not in d
     assert d["hipblaslt_tflops_per_gpu_rank0"] > 0 and d["hbm_copy_GBps_rank0"] > 1000
+    cmp_ = d["interleaved_compare_rank0"]       # K1 vs hipBLASLt, ABAB rounds
+    assert cmp_["rounds"] == len(cmp_["k1_tflops_rounds"]) == len(cmp_["hipblaslt_tflops_rounds"])
+    assert cmp_["k1_over_hipblaslt"] > 0.5 and d["prewarm_s"] >= 0.5
     job = d["validation_job"]
     assert job["ran"] and job["passed"], job
     assert 0 < d["time_to_gpu_ready_in_node_s"] < 30

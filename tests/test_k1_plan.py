@@ -27,6 +27,8 @@ def k1_plan():
     (8192, 8192, 8192, 8192, "tile128"),
     (6144, 6144, 6144, 5376, "tile256x128"),   # 3 rounds -> 2 + one of 256x128
     (4352, 4352, 4352, 3840, "tile128"),
+    (416, 1280, 128, 256, "tile160"),          # split with a 160-row remainder
+    (1696, 2560, 256, 1536, "tile160"),
 ])
 def test_plan_matches_cost_model(k1_plan, m, n, k, top, rest):
     assert k1_plan(m, n, k) == (top, rest)
@@ -45,3 +47,12 @@ def test_plan_is_well_formed(k1_plan, m, n, k):
 def test_plan_rejects_bad_args(k1_plan):
     with pytest.raises(Exception):
         k1_plan(0, 256, 256)
+
+
+@pytest.mark.parametrize("m,n,k", [(384, 256, 192), (100, 256, 256), (256, 256, 64)])
+def test_plan_reports_infeasible_shapes(k1_plan, m, n, k):
+    """No kernel combination tiles these: the plan says so instead of returning
+    a plan whose second launch would fail after the first one wrote C (ADVICE r1:
+    (384,256,192) used to launch 256 rows, then fail)."""
+    with pytest.raises(ValueError):
+        k1_plan(m, n, k)

@@ -270,6 +270,41 @@ def test_gemm_default_split_plan(ops, m, n, k):
     assert torch.equal(c, ops.gemm_bf16(a, b, variant="pingpong8"))
 
 
+@pytest.mark.parametrize("m,n,k,top", [(2560, 2560, 512, 0), (416, 1280, 128, 256),
+                                       (1696, 2560, 256, 1536)])
+def test_gemm_default_dispatch_tile160(ops, m, n, k, top):
+    """Default dispatch where the plan picks the 160x160 tile alone (2560^2) or
+    as a 160-row remainder after 256x256 rows (A/C row offsets top*lda /
+    top*ldc with 160-row tiles): vs fp32 and bitwise equal to the explicit
+    variants run on the same row ranges."""
+    assert ops.kernels.k1_plan(m, n, k) == (top, "tile160")
+    a = _rand(ops, (m, k), 571 + k)
+    b = _rand(ops, (n, k), 573 + n)
+    c = ops.gemm_bf16(a, b)
+    ref = a.float() @ b.float().T
+    atol, rtol = ops.gemm_tolerance(k)
+    err = (c.float() - ref).abs()
+    assert torch.all(err <= atol + rtol * ref.abs()), float(err.max())
+    if top:
+        assert torch.equal(c[:top], ops.gemm_bf16(a[:top], b, variant="pingpong8c"))
+    assert torch.equal(c[top:], ops.gemm_bf16(a[top:].contiguous(), b, variant="tile160"))
+
+
+def test_gemm_default_rejects_unplannable_shape_before_launch(ops):
+    """an infeasible plan must fail before anything is written."""
+    a = _rand(ops, (384, 192), 5)
+    b = _rand(ops, (256, 192), 6)
+    c = torch.full((384, 256), 7.0, dtype=torch.bfloat16, device="cuda")
+    with pytest.raises(ValueError):
+        ops.gemm_bf16(a, b, c)
+    with pytest.raises(RuntimeError):           # the C ABI alone rejects it too
+        from nvidia_terraform_modules_amd.ops._lib import check, lib, stream_handle
+        check(lib().ntm_gemm_bf16_variant(0, a.data_ptr(), b.data_ptr(), c.data_ptr(), 384, 256,
+                                          192, 192, 192, 256, stream_handle()), "default")
+    torch.cuda.synchronize()
+    assert torch.all(c == 7.0)
+
+
 def test_gemm_tile128_rejects_bad_shapes(ops):
     a = torch.zeros((128, 192), dtype=torch.bfloat16, device="cuda")
     with pytest.raises(ValueError):
@@ -304,7 +339,7 @@ def test_gemm_fp8_vs_torch_fp32(ops, m, n, k):
 def test_gemm_fp8_operand_map_probe(ops):
     """The f8f6f4 MFMA sums over k, so A and B only need the SAME k order per
     lane; rows must be lane & 15. Pin both with exact small-integer data."""
-    from nvidia_terraform_modules_amd.ops._lib import check, lib, stream_handle
+    from nvidia_terraform_modules_amd.ops._lib import check, lib_experimental, stream_handle
     torch.manual_seed(0)
     a = torch.randint(-3, 4, (16, 128)).float().to(torch.float8_e4m3fn)
     b = torch.randint(-3, 4, (16, 128)).float().to(torch.float8_e4m3fn)
@@ -320,7 +355,7 @@ def test_gemm_fp8_operand_map_probe(ops):
                                    torch.arange(64 + 16 * g, 64 + 16 * g + 16)]) for g in range(4)])
     d = torch.empty((64, 4), dtype=torch.float32, device="cuda")
     sa, sb = stage(a, perm), stage(b, perm)      # keep both alive across the launch
-    check(lib().ntm_mfma_f8_probe(sa.data_ptr(), sb.data_ptr(), d.data_ptr(), stream_handle()),
+    check(lib_experimental().ntm_mfma_f8_probe(sa.data_ptr(), sb.data_ptr(), d.data_ptr(), stream_handle()),
           "probe")
     torch.cuda.synchronize()
     got = torch.empty((16, 16))

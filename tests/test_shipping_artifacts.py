@@ -1,0 +1,70 @@
+"""What ships: the validation-Job binary and libntm_validation.so carry ONLY
+the kernels the default K1 dispatch (and K1-fp8 / K2 / K3 / C2) can launch.
+The experimental K1 builds, schedule knobs and diagnostics (w4, pp4, pp5,
+pp3 knobs and stamps, the first ping-pong, fp8 knobs, MFMA probes) live in
+libntm_experimental.so only (VERDICT r1 "Next round" #8). Host-only check of
+the kernel symbols with nm - no GPU needed."""
+import re
+import shutil
+import subprocess
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+BIN = ROOT / "validation" / "build" / "amdgpu-validate"
+LIB = ROOT / "nvidia_terraform_modules_amd" / "ops" / "libntm_validation.so"
+EXP = ROOT / "nvidia_terraform_modules_amd" / "ops" / "libntm_experimental.so"
+
+# K1 kernel instantiations the default dispatch may launch: pingpong8c (LDS-staged
+# epilogue when ldc % 8 == 0, register epilogue otherwise; with/without the ABFT
+# row sum; F8 = 3 is K1-fp8), pingpong8b for K % 128 != 0, and the 4 tile shapes.
+ALLOWED_K1 = {
+    "ntm::gemm3::gemm_bf16_pp3_kernel<false, 8, false, 0, 0, 0>",
+    "ntm::gemm3::gemm_bf16_pp3_kernel<false, 8, false, 10, 0, 0>",
+    "ntm::gemm3::gemm_bf16_pp3_kernel<true, 8, false, 0, 0, 0>",
+    "ntm::gemm3::gemm_bf16_pp3_kernel<true, 8, false, 10, 0, 0>",
+    "ntm::gemm3::gemm_bf16_pp3_kernel<false, 8, false, 10, 0, 3>",
+    "ntm::gemm2::gemm_bf16_pp2_kernel<false, 0>",
+    "ntm::gemm2::gemm_bf16_pp2_kernel<false, 3>",
+    "ntm::gemm2::gemm_bf16_pp2_kernel<true, 0>",
+    "ntm::gemm2::gemm_bf16_pp2_kernel<true, 3>",
+    "ntm::gemmt::gemm_bf16_tile_kernel<4, 4>",
+    "ntm::gemmt::gemm_bf16_tile_kernel<8, 4>",
+    "ntm::gemmt::gemm_bf16_tile_kernel<5, 5>",
+    "ntm::gemmt::gemm_bf16_tile_kernel<8, 5>",
+}
+EXPERIMENTAL_ONLY = ("gemm_bf16_w4_kernel", "gemm_bf16_pp4_kernel", "gemm_bf16_pp5_kernel",
+                     "gemm_bf16_pp3_stamp_kernel", "ntm::gemm::gemm_bf16_kernel",
+                     "mfma_rate_kernel", "mfma_f8_probe_kernel")
+
+
+def _kernels(path: Path) -> set:
+    if not path.exists():
+        pytest.skip(f"{path.name} not built (python -m nvidia_terraform_modules_amd.ops.build)")
+    nm = shutil.which("nm") or "/opt/rocm/llvm/bin/llvm-nm"
+    out = subprocess.run([nm, "-C", str(path)], capture_output=True, text=True, check=True).stdout
+    names = set()
+    for ln in out.splitlines():
+        parts = ln.split(None, 2)
+        if len(parts) == 3 and parts[1] in "VDTW" and "__device_stub__" not in parts[2]:
+            m = re.match(r"(?:void )?(ntm::[\w:]+_kernel(?:<[^>]*>)?)\(", parts[2])
+            if m:
+                names.add(m.group(1))
+    return names
+
+
+@pytest.mark.parametrize("path", [BIN, LIB], ids=["job-binary", "libntm_validation"])
+def test_shipping_artifact_has_only_default_dispatch_k1(path):
+    ks = _kernels(path)
+    k1 = {k for k in ks if "gemm_bf16" in k}
+    assert k1 == ALLOWED_K1, (sorted(k1 - ALLOWED_K1), sorted(ALLOWED_K1 - k1))
+    for bad in EXPERIMENTAL_ONLY:
+        assert not [k for k in ks if bad in k], bad
+
+
+def test_experimental_library_holds_the_experiments():
+    ks = _kernels(EXP)
+    for fam in ("gemm_bf16_w4_kernel", "gemm_bf16_pp4_kernel", "gemm_bf16_pp5_kernel",
+                "gemm_bf16_pp3_stamp_kernel", "mfma_rate_kernel", "mfma_f8_probe_kernel"):
+        assert any(fam in k for k in ks), fam

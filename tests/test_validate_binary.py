@@ -116,6 +116,56 @@ def test_binary_p2p_matrix_loopback_and_fault():
 
 
 @pytest.mark.gpu
+def test_binary_rccl_one_rank_sweep_and_fault():
+    """C1 runs at N = 1 (ncclCommInitAll on one device): the code path the
+    8-GPU node uses, every element checked, busbw factor 0; corrupt_allreduce
+    makes the Job exit 1."""
+    _have_bin()
+    rc, out, _ = _run("--size", "512", "--iters", "2", "--no-fp8")
+    assert rc == 0 and _last_json(out)["rccl_allreduce"] == []     # auto: n > 1 only
+    rc, out, err = _run("--size", "512", "--iters", "2", "--no-fp8", "--rccl",
+                        "--allreduce-max-mib", "64")
+    g = _last_json(out)
+    assert rc == 0, (g["failures"], err[-2000:])
+    rows = g["rccl_allreduce"]
+    assert {r["dtype"] for r in rows} == {"bf16", "fp32"}
+    assert rows[0]["bytes"] == 8 and max(r["bytes"] for r in rows) == 32 << 20
+    assert all(r["wrong"] == 0 and r["busbw_GBps"] == 0 and r["algbw_GBps"] is None
+               for r in rows)
+    rc, out, _ = _run("--size", "512", "--iters", "2", "--no-fp8", "--rccl", "--allreduce-max-mib", "1",
+                      env={"NTM_FAULT_INJECT": "corrupt_allreduce"})
+    g = _last_json(out)
+    assert rc == 1 and any("RCCL all-reduce" in f for f in g["failures"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nsim", [2, 8])
+def test_binary_xgmi_simulated_ranks(nsim):
+    """C2 through the binary's own run_xgmi driver with N simulated ranks on
+    one GPU (--xgmi-sim): one-shot and two-shot sizes, device-side barriers,
+    back-to-back epochs with no host sync; every element checked."""
+    _have_bin()
+    rc, out, err = _run("--size", "512", "--iters", "2", "--no-fp8", "--no-rccl",
+                        "--xgmi-sim", str(nsim), "--allreduce-max-mib", "64")
+    g = _last_json(out)
+    assert rc == 0, (g["failures"], err[-2000:])
+    rows = g["xgmi_allreduce_bf16"]
+    assert g["xgmi_simulated_ranks"] == nsim and g["rccl_allreduce"] == []
+    assert {r["dtype"] for r in rows} == {"bf16", "bf16-1shot"}
+    assert all(r["wrong"] == 0 and r["time_us"] > 0 for r in rows)
+    assert max(r["bytes"] for r in rows) >= 16 << 20
+
+
+@pytest.mark.gpu
+def test_binary_xgmi_simulated_fault_fails():
+    _have_bin()
+    rc, out, _ = _run("--size", "512", "--iters", "2", "--no-fp8", "--no-rccl", "--xgmi-sim", "4",
+                      "--allreduce-max-mib", "4", env={"NTM_FAULT_INJECT": "corrupt_allreduce"})
+    g = _last_json(out)
+    assert rc == 1 and any("xGMI all-reduce" in f for f in g["failures"])
+
+
+@pytest.mark.gpu
 def test_binary_no_fp8_skips_the_fp8_check():
     _have_bin()
     rc, out, _ = _run("--size", "1024", "--iters", "3", "--no-fp8")

@@ -23,15 +23,37 @@ def test_simulated_allreduce_matches_fp32_sum(nranks, one_shot):
         assert torch.equal(o, outs[0])
 
 
-def test_simulated_allreduce_epochs_reuse_signals():
-    """Back-to-back calls with increasing epochs must not see stale flags."""
+@pytest.mark.parametrize("nranks", [2, 8])
+def test_simulated_allreduce_in_place(nranks):
+    """Two-shot with in == out (the zero-copy path of XgmiAllReduce.run)."""
+    from nvidia_terraform_modules_amd import ops
     from nvidia_terraform_modules_amd.parallel.xgmi import simulate_allreduce
 
-    n = 4
-    for epoch in (1, 2, 3):
+    count = 8 * nranks * 8192 + 8 * nranks * 7
+    ins = [ops.fill_uniform_(torch.empty(count, dtype=torch.bfloat16, device="cuda"), seed=r + 11)
+           for r in range(nranks)]
+    ref = torch.stack([t.float() for t in ins]).sum(0)
+    outs, err = simulate_allreduce(ins, nblk=32, inplace=True)
+    assert err == 0
+    for o, i in zip(outs, ins):
+        assert o.data_ptr() == i.data_ptr()
+        assert torch.allclose(o.float(), ref, atol=2e-2, rtol=2 ** -7)
+        assert torch.equal(o, outs[0])
+
+
+def test_simulated_allreduce_epochs_reuse_signals():
+    """Back-to-back calls on the SAME signal buffers with increasing epochs
+    (mixed one-shot / two-shot / in-place) must not see stale flags."""
+    from nvidia_terraform_modules_amd.parallel.xgmi import _declare, simulate_allreduce
+
+    n, nblk = 4, 8
+    sb = _declare().ntm_xgmi_signal_bytes(nblk)
+    sigs = [torch.zeros(sb // 4, dtype=torch.int32, device="cuda") for _ in range(n)]
+    for epoch in range(1, 7):
         ins = [torch.full((8 * n * 1024,), float(r + epoch), dtype=torch.bfloat16, device="cuda")
                for r in range(n)]
-        outs, err = simulate_allreduce(ins, nblk=8, epoch=epoch)
+        outs, err = simulate_allreduce(ins, nblk=nblk, epoch=epoch, sigs=sigs,
+                                       one_shot=epoch % 3 == 0, inplace=epoch % 3 == 1)
         assert err == 0
         exp = sum(r + epoch for r in range(n))
         assert all(torch.all(o == exp) for o in outs)
@@ -43,6 +65,11 @@ def test_rejects_bad_counts():
     ins = [torch.zeros(100, dtype=torch.bfloat16, device="cuda") for _ in range(2)]
     with pytest.raises(ValueError):
         simulate_allreduce(ins)
+    ok = [torch.zeros(8 * 8 * 64, dtype=torch.bfloat16, device="cuda") for _ in range(8)]
+    with pytest.raises(ValueError):      # 8 x 256 blocks cannot all be resident
+        simulate_allreduce(ok, nblk=256)
+    with pytest.raises(ValueError):
+        simulate_allreduce(ok, one_shot=True, inplace=True)
 
 
 def test_ipc_allreduce_two_processes():

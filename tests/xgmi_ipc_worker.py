@@ -27,7 +27,19 @@ def main():
         torch.cuda.synchronize()
         exp = ((2.0 ** (i % 4)) * (n * (n + 1) / 2)).to(torch.bfloat16)
         results.append({"count": count, "wrong": int((t != exp).sum()),
-                        "timeout": ar.timed_out()})
+                        "timeout": ar.timed_out(), "path": "staged"})
+    # zero-copy path: payload written straight into the registered buffer,
+    # reduced in place; several calls back to back with no host sync between
+    for count in (8 * n * 16, 8 * n * 65536, (8 << 20) // 2):
+        i = torch.arange(count, device=env.device)
+        buf = ar.buffer(count)
+        for rep in range(3):
+            buf.copy_(((2.0 ** (i % 4)) * (env.rank + 1 + rep)).to(torch.bfloat16))
+            ar.run(count)
+        torch.cuda.synchronize()
+        exp = ((2.0 ** (i % 4)) * (n * (n + 1) / 2 + 2 * n)).to(torch.bfloat16)
+        results.append({"count": count, "wrong": int((buf != exp).sum()),
+                        "timeout": ar.timed_out(), "path": "in_place"})
     ar.close()
     print(json.dumps({"rank": env.rank, "results": results}), flush=True)
     shutdown(env)

@@ -17,7 +17,7 @@ sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 
 import torch  # noqa: E402
 
-from nvidia_terraform_modules_amd.ops._lib import check, lib, stream_handle  # noqa: E402
+from nvidia_terraform_modules_amd.ops._lib import check, lib_experimental, stream_handle  # noqa: E402
 
 CANDIDATES = {
     "contig32": lambda g, j: 32 * g + j,
@@ -48,7 +48,7 @@ def main() -> int:
     for (na, ka), (nb, kb) in itertools.product(CANDIDATES.items(), repeat=2):
         sa = stage(a, ka).cuda()
         sb = stage(b, kb).cuda()
-        check(lib().ntm_mfma_f8_probe(sa.data_ptr(), sb.data_ptr(), d.data_ptr(),
+        check(lib_experimental().ntm_mfma_f8_probe(sa.data_ptr(), sb.data_ptr(), d.data_ptr(),
                                       stream_handle()), "ntm_mfma_f8_probe")
         torch.cuda.synchronize()
         got = torch.empty((16, 16))

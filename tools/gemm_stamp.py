@@ -26,7 +26,7 @@ sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 import torch  # noqa: E402
 
 from nvidia_terraform_modules_amd import ops  # noqa: E402
-from nvidia_terraform_modules_amd.ops._lib import check, lib, stream_handle  # noqa: E402
+from nvidia_terraform_modules_amd.ops._lib import check, lib_experimental, stream_handle  # noqa: E402
 
 SLOTS = 8
 START, END, RT0, RT1, HWID, XCCID = range(6)
@@ -50,7 +50,7 @@ def main() -> int:
     st = {m: torch.zeros(nwg * 8 * SLOTS, dtype=torch.int64, device=dev) for m in MODES}
 
     def run(m):
-        rc = lib().ntm_gemm_bf16_stamp(MODES[m], a.data_ptr(), b.data_ptr(), c.data_ptr(),
+        rc = lib_experimental().ntm_gemm_bf16_stamp(MODES[m], a.data_ptr(), b.data_ptr(), c.data_ptr(),
                                        n, n, n, n, n, n, st[m].data_ptr(), stream_handle())
         check(rc, "ntm_gemm_bf16_stamp")
 

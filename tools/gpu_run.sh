@@ -1,0 +1,70 @@
+#!/bin/bash
+# One parameterised GPU pass for `gpurun` (replaces the per-round tools/gpu_*.sh
+# scratch scripts). Every GPU step has its own time limit and the first failure
+# ends the pass (no retries); logs land under gpurun_out/<tag>/.
+#
+#   tools/gpu_run.sh <tag> [steps...]
+#
+# steps (run in the order given; default: tests smoke validate bench prof):
+#   tests      pytest -m gpu (one process, per-test 120 s thread timeout)
+#   tests:<k>  pytest -m gpu -k <k>
+#   smoke      __graft_entry__.smoke()
+#   validate   amdgpu-validate on 1 GPU (JSON report)
+#   bench      bench.py exactly as the driver runs it (--steps 20 --warmup 5)
+#   bench200   bench.py --steps 200 --warmup 20
+#   prof       rocprofv3 --kernel-trace --stats of a short bench
+#   py:<file>  python -u <file> (a tool script; its own args via PYARGS)
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+export TMPDIR=/tmp
+TAG=${1:?usage: gpu_run.sh <tag> [steps...]}
+shift
+O=gpurun_out/$TAG
+mkdir -p "$O"
+STEPS=("$@")
+[ ${#STEPS[@]} -eq 0 ] && STEPS=(tests smoke validate bench prof)
+
+fail() { echo "FAIL $1 (rc $2)"; tail -40 "$3"; exit 1; }
+
+for s in "${STEPS[@]}"; do
+  echo "== $s $(date +%T)"
+  case "$s" in
+    tests)
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+        > "$O/pytest_gpu.log" 2>&1 || fail tests $? "$O/pytest_gpu.log"
+      tail -1 "$O/pytest_gpu.log" ;;
+    tests:*)
+      k=${s#tests:}
+      timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "$k" \
+        > "$O/pytest_gpu_k.log" 2>&1 || fail "$s" $? "$O/pytest_gpu_k.log"
+      tail -1 "$O/pytest_gpu_k.log" ;;
+    smoke)
+      timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 \
+        || fail smoke $? "$O/smoke.log"
+      tail -1 "$O/smoke.log" ;;
+    validate)
+      timeout -k 10 300 ./validation/build/amdgpu-validate --gpus 1 --size 8192 --iters 30 \
+        --out "$O/validate_1gpu.json" > "$O/validate.log" 2>&1 || fail validate $? "$O/validate.log"
+      tail -3 "$O/validate.log" ;;
+    bench)
+      timeout -k 10 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 --out "$O/bench.json" \
+        > "$O/bench.log" 2>&1 || fail bench $? "$O/bench.log"
+      tail -c 1500 "$O/bench.json" ;;
+    bench200)
+      timeout -k 10 300 python -u bench.py --gpus 1 --steps 200 --warmup 20 --out "$O/bench200.json" \
+        > "$O/bench200.log" 2>&1 || fail bench200 $? "$O/bench200.log"
+      tail -c 600 "$O/bench200.json" ;;
+    prof)
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof" -o run \
+        -- python3 bench.py --steps 50 --warmup 5 --no-job > "$O/bench_prof.log" 2>&1 \
+        || fail prof $? "$O/bench_prof.log"
+      find "$O/prof" -name '*kernel_stats.csv' -exec head -12 {} \; ;;
+    py:*)
+      f=${s#py:}
+      timeout -k 10 600 python -u "$f" $PYARGS > "$O/$(basename "$f" .py).log" 2>&1 \
+        || fail "$s" $? "$O/$(basename "$f" .py).log"
+      tail -30 "$O/$(basename "$f" .py).log" ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
+echo DONE

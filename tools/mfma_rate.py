@@ -15,7 +15,7 @@ sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 
 import torch  # noqa: E402
 
-from nvidia_terraform_modules_amd.ops._lib import check, lib, stream_handle  # noqa: E402
+from nvidia_terraform_modules_amd.ops._lib import check, lib_experimental, stream_handle  # noqa: E402
 
 
 def main() -> int:
@@ -28,7 +28,7 @@ def main() -> int:
     res = {}
     for name, f8, k in (("bf16_16x16x32", 0, 32), ("fp8_16x16x128_scaled", 1, 128)):
         for _ in range(3):   # warm the clock
-            check(lib().ntm_mfma_rate(f8, args.grid, args.iters, out.data_ptr(), sink.data_ptr(),
+            check(lib_experimental().ntm_mfma_rate(f8, args.grid, args.iters, out.data_ptr(), sink.data_ptr(),
                                       stream_handle()), "ntm_mfma_rate")
         torch.cuda.synchronize()
         o = out.view(-1, 2).cpu().double()

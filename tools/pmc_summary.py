@@ -1,4 +1,4 @@
-"""Summarise rocprofv3 counter + kernel-trace CSVs of tools/gpu_prof_pmc.sh
+"""Summarise rocprofv3 counter + kernel-trace CSVs of a `rocprofv3 --pmc` pass (tools/gpu_run.sh)
 into one JSON (mean per dispatch, per kernel) plus derived rates."""
 import collections
 import csv

@@ -25,6 +25,19 @@
 // A block only ever waits for the block with the SAME index on the other
 // ranks, so no intra-device grid barrier is needed; every spin is bounded and
 // reports a timeout code instead of hanging.
+//
+// Three barriers per call, on per-phase epoch slots:
+//   phase 0 (entry): "my input for this epoch is in place" - the kernel is
+//     stream-ordered after this rank's producer, so passing the entry barrier
+//     means every peer's input is complete. No host sync / host barrier.
+//   phase 1: reduce-scatter done (slice b of my chunk is final).
+//   phase 2 (exit): all-gather done - nobody's buffer is read any more, so the
+//     caller may overwrite its input right after the kernel.
+// Epochs only grow and a rank can reach phase p of epoch e+1 only after every
+// peer signalled phase 2 of epoch e, so a waiter never misses a value; the
+// wait is `slot >= epoch` (robust to a peer that already moved on).
+// With the three barriers the two-shot runs IN PLACE (in == out): phase-1
+// writes only touch slices no peer reads before the next barrier.
 #pragma once
 
 #include "ntm/common.hpp"
@@ -34,12 +47,13 @@ namespace xgmi {
 
 constexpr int kMaxRanks = 8;
 constexpr int kThreads = 256;
+constexpr int kPhases = 3;                 // entry, reduce-scatter done, exit
 constexpr unsigned kSpinLimit = 1u << 24;  // ~ seconds; then report a timeout
 
 struct Peers {
   const __bf16* in[kMaxRanks];
   __bf16* out[kMaxRanks];
-  unsigned* sig[kMaxRanks];  // per rank: [2 phases][kMaxRanks][blocks] u32
+  unsigned* sig[kMaxRanks];  // per rank: [kPhases][kMaxRanks][blocks] u32
 };
 
 typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
@@ -76,7 +90,7 @@ __device__ __forceinline__ bool cross_rank_barrier(const Peers& p, int nranks,
     for (int q = 0; q < nranks && ok; ++q) {
       unsigned* mine = p.sig[rank] + ((size_t)ph * kMaxRanks + q) * nblk + b;
       unsigned spins = 0;
-      while (__hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != epoch) {
+      while ((int)(__hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0) {
         __builtin_amdgcn_s_sleep(2);
         if (++spins > kSpinLimit) {
           ok = false;
@@ -107,36 +121,43 @@ __global__ void __launch_bounds__(kThreads)
   const size_t v1 = v0 + per_blk < nvec ? v0 + per_blk : nvec;
   const size_t base = (size_t)rank * chunk / 8;  // vector index of chunk `rank`
 
-  // phase 0: reduce-scatter - chunk `rank`, slice b, summed over all ranks
+  // phase 0 (entry): every peer's input for this epoch is complete
+  if (!cross_rank_barrier(p, nranks, rank, b, nblk, 0, epoch, err)) return;
+
+  // reduce-scatter - chunk `rank`, slice b, summed over all ranks. Start the
+  // sum at a different peer per rank so the 7 links carry load at once.
   for (size_t v = v0 + threadIdx.x; v < v1; v += kThreads) {
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll 8
-    for (int q = 0; q < nranks; ++q) add8(acc, ((const u16x8*)p.in[q])[base + v]);
+    for (int qq = 0; qq < nranks; ++qq) {
+      const int q = (rank + qq) % nranks;
+      add8(acc, ((const u16x8*)p.in[q])[base + v]);
+    }
     ((u16x8*)p.out[rank])[base + v] = pack8(acc);
   }
-  if (!cross_rank_barrier(p, nranks, rank, b, nblk, 0, epoch, err)) return;
+  if (!cross_rank_barrier(p, nranks, rank, b, nblk, 1, epoch, err)) return;
 
-  // phase 1: all-gather - copy chunk q, slice b, from rank q's output
+  // all-gather - copy chunk q, slice b, from rank q's output
   for (int qq = 1; qq < nranks; ++qq) {
     const int q = (rank + qq) % nranks;  // stagger peers -> all links busy
     const size_t qb = (size_t)q * chunk / 8;
     for (size_t v = v0 + threadIdx.x; v < v1; v += kThreads)
       ((u16x8*)p.out[rank])[qb + v] = ((const u16x8*)p.out[q])[qb + v];
   }
-  // nobody may reuse its output (next call's phase 0) before all peers copied
-  cross_rank_barrier(p, nranks, rank, b, nblk, 1, epoch, err);
+  // phase 2 (exit): nobody may overwrite its buffers before all peers copied
+  cross_rank_barrier(p, nranks, rank, b, nblk, 2, epoch, err);
 }
 
 // One-shot all-reduce (small messages): every rank reads ALL of every peer's
-// input and writes its full output; one barrier-free pass (inputs must be
-// stable: callers order the call after the producers with a stream event /
-// preceding barrier).
+// input and writes its full output (in != out). Entry barrier: peers' inputs
+// are complete; exit barrier: no peer still reads my input when I return.
 __global__ void __launch_bounds__(kThreads)
     allreduce_1shot_kernel(Peers p, int nranks, int rank_base, int nblk,
-                           size_t count) {
+                           size_t count, unsigned epoch, unsigned* err) {
   const int rank = rank_base + (int)(blockIdx.x / nblk);
   const int b = (int)(blockIdx.x % nblk);
   const size_t nvec = count / 8;
+  if (!cross_rank_barrier(p, nranks, rank, b, nblk, 0, epoch, err)) return;
   for (size_t v = (size_t)b * kThreads + threadIdx.x; v < nvec;
        v += (size_t)nblk * kThreads) {
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -144,11 +165,12 @@ __global__ void __launch_bounds__(kThreads)
     for (int q = 0; q < nranks; ++q) add8(acc, ((const u16x8*)p.in[q])[v]);
     ((u16x8*)p.out[rank])[v] = pack8(acc);
   }
+  cross_rank_barrier(p, nranks, rank, b, nblk, 2, epoch, err);
 }
 
 // bytes of one rank's signal area for `nblk` blocks per rank
 inline size_t signal_bytes(int nblk) {
-  return (size_t)2 * kMaxRanks * nblk * sizeof(unsigned);
+  return (size_t)kPhases * kMaxRanks * nblk * sizeof(unsigned);
 }
 
 }  // namespace xgmi

@@ -1,0 +1,115 @@
+// EXPERIMENTAL / DIAGNOSTIC K1 builds -> nvidia_terraform_modules_amd/ops/
+// libntm_experimental.so. Loaded only by tests and tools/ (schedule studies,
+// ablations, rate probes); never linked into libntm_validation.so or the
+// validation-Job binary, which carry only the default-dispatch kernels.
+//
+// K1 variants (bf16, C = A B^T, the numbering of ops.kernels.GEMM_VARIANTS):
+//   1      pingpong8: the first 8-wave 12/4/8/0 LDS-read schedule (gemm_bf16.hpp)
+//   2, 3   wave128 / wave128d4: 4 waves, 128x128 per wave, AGPR-pinned
+//          accumulators, prefetch distance 3 / 4 k-steps (gemm_bf16_w4.hpp)
+//   6, 14  pingpong8p / pingpong8pw: pingpong8c made persistent (one WG per CU,
+//          DMA pipeline across tiles), + widened epilogue (gemm_bf16_pp4.hpp)
+//   7..9   pingpong8w / wi / ww: 32-MFMA segment schedules (gemm_bf16_pp5.hpp)
+//   10..13 pingpong8c epilogue knobs: widened / + early row-0 stores /
+//          nontemporal stores / both (gemm_bf16_pp3.hpp launch_gemm_bf16_pp3_knob)
+// Measured: none beats the shipping default (profiles/r1_pp3, r1_pp4, r1_pp3_knobs,
+// r1_pmc2_w4); kept as the record of what was tried and as ablation baselines.
+#include "ntm/gemm_bf16.hpp"
+#include "ntm/gemm_bf16_pp3.hpp"
+#include "ntm/gemm_bf16_pp3_stamp.hpp"
+#include "ntm/gemm_bf16_pp4.hpp"
+#include "ntm/gemm_bf16_pp5.hpp"
+#include "ntm/gemm_bf16_w4.hpp"
+#include "ntm/gemm_fp8_diag.hpp"
+
+#define NTM_API extern "C" __attribute__((visibility("default")))
+
+namespace {
+inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+ntm::gemm::GemmArgs args(const void* A, const void* B, void* C, int M, int N, int K, int lda,
+                         int ldb, int ldc) {
+  ntm::gemm::GemmArgs a;
+  a.A = (const __bf16*)A;
+  a.B = (const __bf16*)B;
+  a.C = (__bf16*)C;
+  a.M = M;
+  a.N = N;
+  a.K = K;
+  a.lda = lda;
+  a.ldb = ldb;
+  a.ldc = ldc;
+  return a;
+}
+}  // namespace
+
+NTM_API const char* ntm_experimental_version() { return "ntm-experimental 0.2.0 gfx950"; }
+
+NTM_API int ntm_gemm_bf16_experimental(int variant, const void* A, const void* B, void* C, int M,
+                                       int N, int K, int lda, int ldb, int ldc, void* stream) {
+  const ntm::gemm::GemmArgs a = args(A, B, C, M, N, K, lda, ldb, ldc);
+  switch (variant) {
+    case 1: return (int)ntm::gemm::launch_gemm_bf16(a, S(stream));
+    case 2:
+    case 3: {
+      ntm::gemm4::Args w{(const __bf16*)A, (const __bf16*)B, (__bf16*)C, M, N, K, lda, ldb, ldc};
+      return variant == 2 ? (int)ntm::gemm4::launch<3>(w, S(stream))
+                          : (int)ntm::gemm4::launch<4>(w, S(stream));
+    }
+    case 6: return (int)ntm::gemmp::launch_gemm_bf16_pp4(a, S(stream));
+    case 14: return (int)ntm::gemmp::launch_gemm_bf16_pp4(a, S(stream), true);
+    case 7:
+    case 8:
+    case 9: return (int)ntm::gemm5::launch_gemm_bf16_pp5(a, variant - 7, S(stream));
+    case 10:
+    case 11:
+    case 12:
+    case 13: return (int)ntm::gemm3::launch_gemm_bf16_pp3_knob(a, variant + 2, S(stream));
+    default: return (int)hipErrorInvalidValue;
+  }
+}
+
+// pingpong8c tuning knobs (see launch_gemm_bf16_pp3_knob).
+NTM_API int ntm_gemm_bf16_knob(int knob, const void* A, const void* B, void* C, int M, int N,
+                               int K, int lda, int ldb, int ldc, void* stream) {
+  return (int)ntm::gemm3::launch_gemm_bf16_pp3_knob(args(A, B, C, M, N, K, lda, ldb, ldc), knob,
+                                                    S(stream));
+}
+
+// pingpong8c ablation builds with s_memtime stamps (gemm_bf16_pp3_stamp.hpp;
+// mode 0 real, 1 no LDS traffic, 2 no MFMA, 3 MFMA only).
+// stamps: (M/256)*(N/256)*8*4 u64.
+NTM_API int ntm_gemm_bf16_stamp(int mode, const void* A, const void* B, void* C, int M, int N,
+                                int K, int lda, int ldb, int ldc, void* stamps, void* stream) {
+  return (int)ntm::gemm3s::launch_gemm_bf16_pp3_stamp(args(A, B, C, M, N, K, lda, ldb, ldc), mode,
+                                                      (unsigned long long*)stamps, S(stream));
+}
+
+// Matrix-core issue rate (gemm_fp8_diag.hpp mfma_rate_kernel); out: 2 u64 per
+// wave (grid x 4 waves), sink: 1 float.
+NTM_API int ntm_mfma_rate(int f8, int grid, int iters, void* out, float* sink, void* stream) {
+  if (grid <= 0 || iters <= 0) return (int)hipErrorInvalidValue;
+  if (f8)
+    hipLaunchKernelGGL(ntm::fp8::mfma_rate_kernel<true>, dim3(grid), dim3(256), 0, S(stream),
+                       iters, 7u, (unsigned long long*)out, sink);
+  else
+    hipLaunchKernelGGL(ntm::fp8::mfma_rate_kernel<false>, dim3(grid), dim3(256), 0, S(stream),
+                       iters, 7u, (unsigned long long*)out, sink);
+  return (int)hipGetLastError();
+}
+
+// K1-fp8 schedule knobs (gemm_fp8_diag.hpp launch_gemm_fp8_knob).
+NTM_API int ntm_gemm_fp8_knob(const void* A, const void* B, void* C, int M, int N, int K,
+                              int lda, int ldb, int ldc, int knob, void* stream) {
+  return (int)ntm::fp8::launch_gemm_fp8_knob(A, B, (__bf16*)C, M, N, K, lda, ldb, ldc, knob,
+                                             S(stream));
+}
+
+// One v_mfma_scale_f32_16x16x128_f8f6f4 (e4m3 x e4m3, unit scales) on
+// per-lane operands: a_stage / b_stage 64 x 32 B, d 64 x 4 fp32.
+NTM_API int ntm_mfma_f8_probe(const void* a_stage, const void* b_stage, float* d, void* stream) {
+  hipLaunchKernelGGL(ntm::fp8::mfma_f8_probe_kernel, dim3(1), dim3(64), 0, S(stream),
+                     (const ntm::fp8::i32x8*)a_stage, (const ntm::fp8::i32x8*)b_stage,
+                     (ntm::f32x4*)d);
+  return (int)hipGetLastError();
+}

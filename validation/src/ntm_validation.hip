@@ -4,16 +4,16 @@
 //   validation/build/amdgpu-validate                        (Job entrypoint)
 // Every entry point is stream-ordered, allocation-free and sync-free, so it
 // can be captured in a hipGraph (playbook §6 Guideline 9).
+//
+// Only the kernels the default dispatch can select are instantiated here
+// (pingpong8c / pingpong8b 256x256, the four tile shapes, K1-fp8, K2, K3).
+// The non-default K1 builds, schedule knobs and diagnostics live in
+// ntm_experimental.hip -> libntm_experimental.so (tests and tools only).
 #include "ntm/aux_kernels.hpp"
-#include "ntm/gemm_bf16.hpp"
-#include "ntm/gemm_fp8.hpp"
 #include "ntm/gemm_bf16_pp2.hpp"
 #include "ntm/gemm_bf16_pp3.hpp"
-#include "ntm/gemm_bf16_pp4.hpp"
-#include "ntm/gemm_bf16_pp3_stamp.hpp"
-#include "ntm/gemm_bf16_pp5.hpp"
 #include "ntm/gemm_bf16_t128.hpp"
-#include "ntm/gemm_bf16_w4.hpp"
+#include "ntm/gemm_fp8.hpp"
 
 #define NTM_API extern "C" __attribute__((visibility("default")))
 
@@ -34,30 +34,21 @@ NTM_API int ntm_gemm_shape_ok(int M, int N, int K) {
   return ntm::gemm::shape_ok(M, N, K) ? 1 : 0;
 }
 
-// K1 variants: 1 = 8-wave ping-pong (gemm_bf16.hpp); 2 / 3 = 4-wave, 128x128
-// per wave (gemm_bf16_w4.hpp) with prefetch distance 3 / 4 k-steps; 4 = the
-// 8-wave kernel with the balanced 8/4/8/4 read schedule (gemm_bf16_pp2.hpp);
-// 5 = the same schedule with parity-alternating B buffers and a uniform,
-// tail-free K loop (gemm_bf16_pp3.hpp; K % 128 == 0); 6 = 5 made persistent
-// (one WG per CU, DMA pipeline across tiles; gemm_bf16_pp4.hpp); 7 / 8 / 9 =
-// wide 32-MFMA segments (gemm_bf16_pp5.hpp): reads first / DMA issue first /
-// reads first + widened dwordx4 epilogue; 10 / 11 / 12 / 13 = 5 + widened
-// epilogue / + early row-0 stores / + nontemporal stores / + both; 14 = 6 +
-// widened epilogue; 15 / 16 = 128x128 / 256x128 tiles, 4 waves (gemm_bf16_t128.hpp).
-// 0 = default: the fastest measured variant whose shape rules admit (M,N,K).
+// K1 variants in this (shipping) library: 4 = pingpong8b, the 8-wave 256x256
+// kernel with the balanced 8/4/8/4 LDS read schedule (gemm_bf16_pp2.hpp; K %
+// 64); 5 = pingpong8c, the same schedule with parity-alternating B buffers, a
+// uniform tail-free K loop and the LDS-staged nontemporal epilogue
+// (gemm_bf16_pp3.hpp; K % 128); 15 / 16 / 17 / 18 = 128x128 / 256x128 /
+// 160x160 / 256x160 tiles, 4 waves (gemm_bf16_t128.hpp; K % 128).
+// 0 = default: the plan below. Variants 1-3 and 6-14 (the first ping-pong,
+// the 4-wave 128x128-per-wave kernel, the persistent kernel, the 32-MFMA
+// segment schedules, epilogue knobs) are experimental: libntm_experimental.so.
 // Measured on MI355X (tools/gemm_check.py, random bf16, median of 7 rounds,
-// profiles/r1_pp3/):
-//   8192^3: 5 1567 TF, 4 1530, 1 1521, 2 ~1310-1380; hipBLASLt 1667
-//   4096^3: 5 1479 TF, 4 1435, 1 1424;               hipBLASLt 1562
-// then variant 5 without s_setprio: +1.3-1.7 % (profiles/r1_pp3_knobs).
-// Variant 6 (persistent 5) is correct and race-free but measured no faster
-// (8192^3 1586 vs 1594, 4096^3 1512 vs 1509; profiles/r1_pp4): not default.
+// profiles/r1_pp3/): 8192^3: 5 1567 TF, 4 1530; 4096^3: 5 1479, 4 1435; then
+// variant 5 without s_setprio +1.3-1.7 % (profiles/r1_pp3_knobs) and with the
+// LDS-staged epilogue (profiles/r1_epilogue, r1_round7): 8192^3 1623-1635 TF
+// vs hipBLASLt 1632-1648, 4096^3 1536 vs 1532-1544 (same processes).
 // Variants 4 and 5 pass tools/race_screen.py (bitwise-stable under HBM noise).
-// Variant 5 then took the LDS-staged full-row nontemporal epilogue whenever
-// ldc % 8 == 0 (profiles/r1_epilogue, r1_round7): 8192^3 1623-1635 TF vs
-// hipBLASLt 1632-1648, 4096^3 1536 vs 1532-1544 (same processes).
-// Variants 7-9 (32-MFMA segments) measured no faster than 5 with the same
-// epilogue; 11/13 (early row-0 stores) tie with 10/12.
 // Default: 5 when K % 128 == 0, else 4 (both need K % 64 == 0, K >= 128).
 constexpr int kDefaultVariant = 5;
 
@@ -87,16 +78,18 @@ constexpr SmallTile kSmallTiles[] = {
 constexpr double kSplitPenalty = 0.25;  // a second launch, in 128x128-tile-round units
 
 struct K1Plan {
-  int top_rows;      // rows [0, top_rows) on the 256x256 kernel
+  int top_rows;      // rows [0, top_rows) on the 256x256 kernel; -1 = no plan tiles (M,N,K)
   int rest_variant;  // rows [top_rows, M) on a kSmallTiles variant (15..18)
+  bool feasible() const { return top_rows >= 0; }
 };
 
 inline K1Plan plan_k1(int M, int N, int K) {
   auto rounds = [](double tiles) { return tiles <= 0 ? 0.0 : __builtin_ceil(tiles / kCUs); };
   const double inf = 1e300;
   const bool big_ok = N % 256 == 0 && K % 64 == 0 && K >= 128;
-  K1Plan best{M % 256 == 0 ? M : 0, 15};
+  K1Plan best{-1, 15};
   double best_cost = inf;
+  if (M <= 0 || N <= 0 || K <= 0) return best;
   for (int m1 = 0; m1 <= M; m1 += 256) {
     if (m1 > 0 && !big_ok) break;
     const int rest = M - m1;
@@ -116,6 +109,7 @@ inline K1Plan plan_k1(int M, int N, int K) {
       }
     }
     const double cost = top + bottom + (m1 > 0 && rest > 0 ? kSplitPenalty : 0.0);
+    if (cost >= inf) continue;  // no kernel tiles the remainder: never a plan
     if (cost <= best_cost) {  // ties: more rows on the 256x256 kernel
       best_cost = cost;
       best = K1Plan{m1, v};
@@ -128,6 +122,7 @@ inline K1Plan plan_k1(int M, int N, int K) {
 NTM_API int ntm_k1_plan(int M, int N, int K, int* top_rows, int* rest_variant) {
   if (M <= 0 || N <= 0 || K <= 0 || !top_rows || !rest_variant) return (int)hipErrorInvalidValue;
   const K1Plan pl = plan_k1(M, N, K);
+  if (!pl.feasible()) return (int)hipErrorInvalidValue;
   *top_rows = pl.top_rows;
   *rest_variant = pl.rest_variant;
   return 0;
@@ -138,6 +133,7 @@ NTM_API int ntm_gemm_bf16_variant(int variant, const void* A, const void* B,
                                   int ldb, int ldc, void* stream) {
   if (variant == 0) {
     const K1Plan pl = plan_k1(M, N, K);
+    if (!pl.feasible()) return (int)hipErrorInvalidValue;  // nothing launched
     const int top = ntm::gemm3::shape_ok3(pl.top_rows, N, K) ? kDefaultVariant : 4;
     if (pl.top_rows > 0 && pl.top_rows < M) {
       const int rc = ntm_gemm_bf16_variant(top, A, B, C, pl.top_rows, N, K, lda, ldb, ldc, stream);
@@ -147,83 +143,7 @@ NTM_API int ntm_gemm_bf16_variant(int variant, const void* A, const void* B,
                                    K, lda, ldb, ldc, stream);
     }
     variant = pl.top_rows == M ? top : pl.rest_variant;
-    if (variant == 3 && !ntm::gemm4::shape_ok<4>(M, N, K)) variant = 1;
-    if (variant == 2 && !ntm::gemm4::shape_ok<3>(M, N, K)) variant = 1;
   }
-  if (variant == 1) {
-    ntm::gemm::GemmArgs a;
-    a.A = (const __bf16*)A;
-    a.B = (const __bf16*)B;
-    a.C = (__bf16*)C;
-    a.M = M;
-    a.N = N;
-    a.K = K;
-    a.lda = lda;
-    a.ldb = ldb;
-    a.ldc = ldc;
-    return (int)ntm::gemm::launch_gemm_bf16(a, S(stream));
-  }
-  if (variant == 4 || variant == 5 || variant == 6) {
-    ntm::gemm::GemmArgs a;
-    a.A = (const __bf16*)A;
-    a.B = (const __bf16*)B;
-    a.C = (__bf16*)C;
-    a.M = M;
-    a.N = N;
-    a.K = K;
-    a.lda = lda;
-    a.ldb = ldb;
-    a.ldc = ldc;
-    if (variant == 6) return (int)ntm::gemmp::launch_gemm_bf16_pp4(a, S(stream));
-    return variant == 5 ? (int)ntm::gemm3::launch_gemm_bf16_pp3(a, S(stream))
-                        : (int)ntm::gemm2::launch_gemm_bf16_pp2(a, S(stream));
-  }
-  if (variant >= 7 && variant <= 14) {
-    ntm::gemm::GemmArgs a;
-    a.A = (const __bf16*)A;
-    a.B = (const __bf16*)B;
-    a.C = (__bf16*)C;
-    a.M = M;
-    a.N = N;
-    a.K = K;
-    a.lda = lda;
-    a.ldb = ldb;
-    a.ldc = ldc;
-    if (variant == 14) return (int)ntm::gemmp::launch_gemm_bf16_pp4(a, S(stream), true);
-    if (variant >= 10) return (int)ntm::gemm3::launch_gemm_bf16_pp3_knob(a, variant + 2, S(stream));
-    return (int)ntm::gemm5::launch_gemm_bf16_pp5(a, variant - 7, S(stream));
-  }
-  if (variant >= 15 && variant <= 18) {  // 128x128 / 256x128 / 160x160 / 256x160 tiles
-    ntm::gemm::GemmArgs a;
-    a.A = (const __bf16*)A;
-    a.B = (const __bf16*)B;
-    a.C = (__bf16*)C;
-    a.M = M;
-    a.N = N;
-    a.K = K;
-    a.lda = lda;
-    a.ldb = ldb;
-    a.ldc = ldc;
-    switch (variant) {  // gemm_bf16_t128.hpp
-      case 15: return (int)ntm::gemmt::launch_gemm_bf16_tile<4>(a, S(stream));
-      case 16: return (int)ntm::gemmt::launch_gemm_bf16_tile<8>(a, S(stream));
-      case 17: return (int)ntm::gemmt::launch_gemm_bf16_tile<5, 5>(a, S(stream));
-      default: return (int)ntm::gemmt::launch_gemm_bf16_tile<8, 5>(a, S(stream));
-    }
-  }
-  if (variant == 2 || variant == 3) {
-    ntm::gemm4::Args a{(const __bf16*)A, (const __bf16*)B, (__bf16*)C, M, N, K,
-                       lda, ldb, ldc};
-    return variant == 2 ? (int)ntm::gemm4::launch<3>(a, S(stream))
-                        : (int)ntm::gemm4::launch<4>(a, S(stream));
-  }
-  return (int)hipErrorInvalidValue;
-}
-
-// Experimental: pingpong8c tuning knobs (see launch_gemm_bf16_pp3_knob).
-NTM_API int ntm_gemm_bf16_knob(int knob, const void* A, const void* B, void* C,
-                               int M, int N, int K, int lda, int ldb, int ldc,
-                               void* stream) {
   ntm::gemm::GemmArgs a;
   a.A = (const __bf16*)A;
   a.B = (const __bf16*)B;
@@ -234,26 +154,16 @@ NTM_API int ntm_gemm_bf16_knob(int knob, const void* A, const void* B, void* C,
   a.lda = lda;
   a.ldb = ldb;
   a.ldc = ldc;
-  return (int)ntm::gemm3::launch_gemm_bf16_pp3_knob(a, knob, S(stream));
-}
-
-// DIAGNOSTIC: pingpong8c ablation builds with s_memtime stamps
-// (gemm_bf16_pp3_stamp.hpp; mode 0 real, 1 no LDS traffic, 2 no MFMA, 3 MFMA
-// only). stamps: (M/256)*(N/256)*8*4 u64.
-NTM_API int ntm_gemm_bf16_stamp(int mode, const void* A, const void* B, void* C, int M, int N,
-                                int K, int lda, int ldb, int ldc, void* stamps, void* stream) {
-  ntm::gemm::GemmArgs a;
-  a.A = (const __bf16*)A;
-  a.B = (const __bf16*)B;
-  a.C = (__bf16*)C;
-  a.M = M;
-  a.N = N;
-  a.K = K;
-  a.lda = lda;
-  a.ldb = ldb;
-  a.ldc = ldc;
-  return (int)ntm::gemm3s::launch_gemm_bf16_pp3_stamp(
-      a, mode, (unsigned long long*)stamps, S(stream));
+  switch (variant) {
+    case 4: return (int)ntm::gemm2::launch_gemm_bf16_pp2(a, S(stream));
+    case 5: return (int)ntm::gemm3::launch_gemm_bf16_pp3(a, S(stream));
+    // gemm_bf16_t128.hpp: 128x128 / 256x128 / 160x160 / 256x160 tiles
+    case 15: return (int)ntm::gemmt::launch_gemm_bf16_tile<4>(a, S(stream));
+    case 16: return (int)ntm::gemmt::launch_gemm_bf16_tile<8>(a, S(stream));
+    case 17: return (int)ntm::gemmt::launch_gemm_bf16_tile<5, 5>(a, S(stream));
+    case 18: return (int)ntm::gemmt::launch_gemm_bf16_tile<8, 5>(a, S(stream));
+    default: return (int)hipErrorInvalidValue;  // experimental variants: libntm_experimental.so
+  }
 }
 
 // K1-fp8: C (bf16) = A (e4m3) * B (e4m3)^T, fp32 accumulation (gemm_fp8.hpp).
@@ -262,38 +172,8 @@ NTM_API int ntm_gemm_fp8(const void* A, const void* B, void* C, int M, int N, in
   return (int)ntm::fp8::launch_gemm_fp8(A, B, (__bf16*)C, M, N, K, lda, ldb, ldc, S(stream));
 }
 
-// DIAGNOSTIC: matrix-core issue rate (gemm_fp8.hpp mfma_rate_kernel); out:
-// 2 u64 per wave (grid x 4 waves), sink: 1 float.
-NTM_API int ntm_mfma_rate(int f8, int grid, int iters, void* out, float* sink, void* stream) {
-  if (grid <= 0 || iters <= 0) return (int)hipErrorInvalidValue;
-  if (f8)
-    hipLaunchKernelGGL(ntm::fp8::mfma_rate_kernel<true>, dim3(grid), dim3(256), 0, S(stream),
-                       iters, 7u, (unsigned long long*)out, sink);
-  else
-    hipLaunchKernelGGL(ntm::fp8::mfma_rate_kernel<false>, dim3(grid), dim3(256), 0, S(stream),
-                       iters, 7u, (unsigned long long*)out, sink);
-  return (int)hipGetLastError();
-}
-
-// EXPERIMENTAL: K1-fp8 schedule knobs (gemm_fp8.hpp launch_gemm_fp8_knob).
-NTM_API int ntm_gemm_fp8_knob(const void* A, const void* B, void* C, int M, int N, int K,
-                              int lda, int ldb, int ldc, int knob, void* stream) {
-  return (int)ntm::fp8::launch_gemm_fp8_knob(A, B, (__bf16*)C, M, N, K, lda, ldb, ldc, knob,
-                                             S(stream));
-}
-
 NTM_API int ntm_gemm_fp8_shape_ok(int M, int N, int K) {
   return ntm::fp8::shape_ok(M, N, K) ? 1 : 0;
-}
-
-// One v_mfma_scale_f32_16x16x128_f8f6f4 (e4m3 x e4m3, unit scales) on
-// per-lane operands: a_stage / b_stage 64 x 32 B, d 64 x 4 fp32.
-NTM_API int ntm_mfma_f8_probe(const void* a_stage, const void* b_stage, float* d,
-                              void* stream) {
-  hipLaunchKernelGGL(ntm::fp8::mfma_f8_probe_kernel, dim3(1), dim3(64), 0, S(stream),
-                     (const ntm::fp8::i32x8*)a_stage, (const ntm::fp8::i32x8*)b_stage,
-                     (ntm::f32x4*)d);
-  return (int)hipGetLastError();
 }
 
 NTM_API int ntm_gemm_bf16(const void* A, const void* B, void* C, int M, int N,

@@ -100,8 +100,11 @@ struct Opts {
   double tflops_floor = 0;
   double min_hbm_gb = 0;
   double hbm_floor_gbps = 0;
-  long allreduce_max_mib = 1024;
+  long allreduce_max_mib = 8192;  // 8 GiB, capped by free HBM
   bool xgmi = true;
+  int xgmi_sim = 0;             // C2 with N simulated ranks on GPU 0 (one-GPU test path)
+  int rccl = -1;                // C1: -1 auto (n > 1), 0 off, 1 on (--rccl: at n = 1 too)
+  double settle_s = 0.1;        // untimed clock-settle pre-warm before each timed GEMM loop
   bool fp8 = true;              // K1-fp8 check of the e4m3 MX-scaled matrix path
   double fp8_tflops_floor = 0;
   bool p2p = true;              // C3: per-link xGMI pull matrix (n > 1)
@@ -120,7 +123,8 @@ void usage() {
   std::fprintf(stderr,
                "usage: amdgpu-validate [--gpus N] [--size 8192] [--iters 50]\n"
                "       [--tflops-floor TF] [--min-hbm-gb GB] [--hbm-floor-gbps GBps]\n"
-               "       [--allreduce-max-mib MiB] [--no-xgmi] [--no-fp8] [--fp8-tflops-floor TF]\n"
+               "       [--allreduce-max-mib MiB] [--rccl | --no-rccl] [--no-xgmi] [--xgmi-sim N]\n"
+               "       [--settle-s S] [--no-fp8] [--fp8-tflops-floor TF]\n"
                "       [--no-p2p] [--p2p-mib MiB] [--p2p-floor-gbps GBps] [--p2p-loopback]\n"
                "       [--json] [--out FILE]\n"
                "       [--termination-log FILE] [--prom-out FILE] [--fault-inject KIND]\n"
@@ -149,6 +153,10 @@ bool parse(int argc, char** argv, Opts& o) {
     else if (a == "--hbm-floor-gbps") { if (!(v = next(a.c_str()))) return false; o.hbm_floor_gbps = std::atof(v); }
     else if (a == "--allreduce-max-mib") { if (!(v = next(a.c_str()))) return false; o.allreduce_max_mib = std::atol(v); }
     else if (a == "--no-xgmi") o.xgmi = false;
+    else if (a == "--no-rccl") o.rccl = 0;
+    else if (a == "--rccl") o.rccl = 1;
+    else if (a == "--xgmi-sim") { if (!(v = next(a.c_str()))) return false; o.xgmi_sim = std::atoi(v); }
+    else if (a == "--settle-s") { if (!(v = next(a.c_str()))) return false; o.settle_s = std::atof(v); }
     else if (a == "--no-fp8") o.fp8 = false;
     else if (a == "--no-p2p") o.p2p = false;
     else if (a == "--p2p-loopback") o.p2p_loopback = true;
@@ -164,7 +172,8 @@ bool parse(int argc, char** argv, Opts& o) {
     else if (a == "-h" || a == "--help") { usage(); std::exit(0); }
     else { std::fprintf(stderr, "unknown argument %s\n", a.c_str()); return false; }
   }
-  return o.size > 0 && o.iters > 0 && o.p2p_mib > 0;
+  return o.size > 0 && o.iters > 0 && o.p2p_mib > 0 && o.allreduce_max_mib > 0 &&
+         o.xgmi_sim >= 0 && o.xgmi_sim <= ntm::xgmi::kMaxRanks && o.settle_s >= 0;
 }
 
 // ------------------------------------------------------------ JSON helpers
@@ -308,7 +317,19 @@ bool run_gpu(int dev, bool last, const Opts& o, GpuResult& r) {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  for (int i = 0; i < 5; ++i) CK(ntm_gemm_bf16(A, B, C, n, n, n, n, n, n, s));
+  // Untimed clock-settle pre-warm: a cold MI355X runs the first launches at boost
+  // clock, overshoots its power limit a few ms in and throttles, and needs ~25 ms
+  // of sustained load to settle (profiles/r2_bench/). Timing 5 launches after a
+  // cold start measures that transient, not the kernel.
+  auto settle = [&](auto&& launch) -> bool {
+    const auto t0 = Clock::now();
+    do {
+      for (int i = 0; i < 8; ++i) CK(launch());
+      CK(hipStreamSynchronize(s));
+    } while (std::chrono::duration<double>(Clock::now() - t0).count() < o.settle_s);
+    return true;
+  };
+  if (!settle([&] { return ntm_gemm_bf16(A, B, C, n, n, n, n, n, n, s); })) return false;
   CK(hipEventRecord(e0, s));
   for (int i = 0; i < o.iters; ++i) CK(ntm_gemm_bf16(A, B, C, n, n, n, n, n, n, s));
   CK(hipEventRecord(e1, s));
@@ -386,7 +407,7 @@ bool run_gpu(int dev, bool last, const Opts& o, GpuResult& r) {
     std::memcpy(&r.fp8_bad, vr, 8);
     std::memcpy(&r.fp8_max_err, vr + 8, 4);
     CK(hipFree(R));
-    for (int i = 0; i < 5; ++i) CK(ntm_gemm_fp8(A8, B8, C, n, n, n, n, n, n, s));
+    if (!settle([&] { return ntm_gemm_fp8(A8, B8, C, n, n, n, n, n, n, s); })) return false;
     CK(hipEventRecord(e0, s));
     for (int i = 0; i < o.iters; ++i) CK(ntm_gemm_fp8(A8, B8, C, n, n, n, n, n, n, s));
     CK(hipEventRecord(e1, s));
@@ -455,81 +476,123 @@ struct CollRow {
 
 double bus_factor(int n) { return n > 1 ? 2.0 * (n - 1) / n : 0.0; }
 
-// C1: RCCL all-reduce sweep, single process owning all devices.
+// Largest sweep message: --allreduce-max-mib, capped at 40 % of the smallest
+// free HBM over `devs` and rounded down to a power of two (the sweep doubles).
+size_t sweep_cap(const std::vector<int>& devs, size_t want, int buffers_per_dev) {
+  size_t mn = SIZE_MAX;
+  for (int d : devs) {
+    size_t fre = 0, tot = 0;
+    if (hipSetDevice(d) != hipSuccess || hipMemGetInfo(&fre, &tot) != hipSuccess) return 0;
+    mn = std::min(mn, fre);
+  }
+  const size_t cap = (size_t)(0.4 * (double)mn) / (size_t)buffers_per_dev;
+  size_t b = 8;
+  while (b * 2 <= std::min(want, cap)) b *= 2;
+  return b;
+}
+
+// C1: RCCL all-reduce sweep, single process owning all devices
+// (ncclCommInitAll). Runs at n = 1 too - a one-rank communicator: busbw factor
+// 0, result still checked element by element - so the path the 8-GPU node
+// uses has executed before it gets there. Every RCCL call is checked, in the
+// warm-up and timed loops as well: a failed launch must never turn into a
+// fast, wrong bandwidth figure.
 bool run_rccl(const std::vector<int>& devs, const Opts& o, std::vector<CollRow>& rows) {
   const int n = (int)devs.size();
+  const size_t maxb = sweep_cap(devs, (size_t)o.allreduce_max_mib << 20, 1);
+  if (maxb < 8) { fail("RCCL sweep: no free HBM"); return false; }
   std::vector<ncclComm_t> comms(n);
   if (ncclCommInitAll(comms.data(), n, devs.data()) != ncclSuccess) {
     fail("ncclCommInitAll failed");
     return false;
   }
   std::vector<hipStream_t> st(n);
-  std::vector<void*> buf(n);
-  std::vector<unsigned long long*> bad(n);
-  const size_t maxb = (size_t)o.allreduce_max_mib << 20;
-  for (int i = 0; i < n; ++i) {
-    CK(hipSetDevice(devs[i]));
-    CK(hipStreamCreateWithFlags(&st[i], hipStreamNonBlocking));
-    CK(hipMalloc(&buf[i], maxb));
-    CK(hipMalloc(&bad[i], 8));
-  }
+  std::vector<void*> buf(n, nullptr);
+  std::vector<unsigned long long*> bad(n, nullptr);
   bool ok = true;
-  // nccl-tests style: 8 B .. max, x4 per step, bf16 then fp32 (SURVEY.md C1)
-  for (const bool f32 : {false, true})
-  for (size_t bytes = 8; bytes <= maxb; bytes *= 4) {
-    const size_t esz = f32 ? 4 : 2;
-    const size_t cnt = bytes / esz;
-    const ncclDataType_t dt = f32 ? ncclFloat32 : ncclBfloat16;
-    auto run_once = [&]() -> bool {
-      if (ncclGroupStart() != ncclSuccess) return false;
-      for (int i = 0; i < n; ++i)
-        if (ncclAllReduce(buf[i], buf[i], cnt, dt, ncclSum, comms[i], st[i]) != ncclSuccess)
-          return false;
-      return ncclGroupEnd() == ncclSuccess;
-    };
-    const unsigned blocks = (unsigned)std::min<size_t>(1024, (cnt + 255) / 256);
+  auto cleanup = [&] {
     for (int i = 0; i < n; ++i) {
-      CK(hipSetDevice(devs[i]));
-      // fault injection: the last rank contributes the wrong pattern
-      const int contrib = (o.fault == "corrupt_allreduce" && i == n - 1) ? i + 1 : i;
-      if (f32)
-        hipLaunchKernelGGL(fill_pattern<float>, dim3(blocks), dim3(256), 0, st[i], (float*)buf[i], cnt, contrib);
-      else
-        hipLaunchKernelGGL(fill_pattern<uint16_t>, dim3(blocks), dim3(256), 0, st[i], (uint16_t*)buf[i], cnt, contrib);
-      CK(hipMemsetAsync(bad[i], 0, 8, st[i]));
+      (void)hipSetDevice(devs[i]);
+      if (buf[i]) (void)hipFree(buf[i]);
+      if (bad[i]) (void)hipFree(bad[i]);
+      if (st[i]) (void)hipStreamDestroy(st[i]);
+      ncclCommDestroy(comms[i]);
     }
-    if (!run_once()) { fail("ncclAllReduce failed"); return false; }
-    unsigned long long tot_bad = 0;
-    for (int i = 0; i < n; ++i) {
-      CK(hipSetDevice(devs[i]));
-      if (f32)
-        hipLaunchKernelGGL(check_pattern<float>, dim3(blocks), dim3(256), 0, st[i], (const float*)buf[i], cnt, n, bad[i]);
-      else
-        hipLaunchKernelGGL(check_pattern<uint16_t>, dim3(blocks), dim3(256), 0, st[i], (const uint16_t*)buf[i], cnt, n, bad[i]);
-      unsigned long long b = 0;
-      CK(hipMemcpyAsync(&b, bad[i], 8, hipMemcpyDeviceToHost, st[i]));
-      CK(hipStreamSynchronize(st[i]));
-      tot_bad += b;
-    }
-    const int iters = 10;
-    for (int w = 0; w < 2; ++w) run_once();
-    for (int i = 0; i < n; ++i) { CK(hipSetDevice(devs[i])); CK(hipStreamSynchronize(st[i])); }
-    const auto t0 = Clock::now();
-    for (int it = 0; it < iters; ++it) run_once();
-    for (int i = 0; i < n; ++i) { CK(hipSetDevice(devs[i])); CK(hipStreamSynchronize(st[i])); }
-    const double sec = std::chrono::duration<double>(Clock::now() - t0).count() / iters;
-    const double alg = bytes / sec / 1e9;
-    rows.push_back({f32 ? "fp32" : "bf16", bytes, sec * 1e6, alg, alg * bus_factor(n), tot_bad});
-    if (tot_bad) ok = false;
-  }
+  };
   for (int i = 0; i < n; ++i) {
-    (void)hipSetDevice(devs[i]);
-    (void)hipFree(buf[i]);
-    (void)hipFree(bad[i]);
-    (void)hipStreamDestroy(st[i]);
-    ncclCommDestroy(comms[i]);
+    st[i] = nullptr;
+    if (hipSetDevice(devs[i]) != hipSuccess ||
+        hipStreamCreateWithFlags(&st[i], hipStreamNonBlocking) != hipSuccess ||
+        hipMalloc(&buf[i], maxb) != hipSuccess || hipMalloc(&bad[i], 8) != hipSuccess) {
+      fail("RCCL sweep: buffer allocation failed");
+      cleanup();
+      return false;
+    }
   }
-  if (!ok) fail("RCCL all-reduce produced wrong elements");
+  // nccl-tests style: 8 B .. max, x4 per step, bf16 then fp32 (SURVEY.md C1)
+  for (const bool f32 : {false, true}) {
+    for (size_t bytes = 8; bytes <= maxb && ok; bytes *= 4) {
+      const size_t esz = f32 ? 4 : 2;
+      const size_t cnt = bytes / esz;
+      const ncclDataType_t dt = f32 ? ncclFloat32 : ncclBfloat16;
+      auto run_once = [&]() -> bool {
+        if (ncclGroupStart() != ncclSuccess) return false;
+        bool good = true;
+        for (int i = 0; i < n; ++i)
+          good = good && ncclAllReduce(buf[i], buf[i], cnt, dt, ncclSum, comms[i], st[i]) == ncclSuccess;
+        return (ncclGroupEnd() == ncclSuccess) && good;
+      };
+      auto sync_all = [&]() -> bool {
+        for (int i = 0; i < n; ++i)
+          if (hipSetDevice(devs[i]) != hipSuccess || hipStreamSynchronize(st[i]) != hipSuccess)
+            return false;
+        return true;
+      };
+      const unsigned blocks = (unsigned)std::min<size_t>(1024, (cnt + 255) / 256);
+      for (int i = 0; i < n; ++i) {
+        CK(hipSetDevice(devs[i]));
+        // fault injection: the last rank contributes the wrong pattern
+        const int contrib = (o.fault == "corrupt_allreduce" && i == n - 1) ? i + 1 : i;
+        if (f32)
+          hipLaunchKernelGGL(fill_pattern<float>, dim3(blocks), dim3(256), 0, st[i], (float*)buf[i], cnt, contrib);
+        else
+          hipLaunchKernelGGL(fill_pattern<uint16_t>, dim3(blocks), dim3(256), 0, st[i], (uint16_t*)buf[i], cnt, contrib);
+        CK(hipGetLastError());
+        CK(hipMemsetAsync(bad[i], 0, 8, st[i]));
+      }
+      if (!run_once()) { fail("ncclAllReduce failed"); ok = false; break; }
+      unsigned long long tot_bad = 0;
+      for (int i = 0; i < n; ++i) {
+        CK(hipSetDevice(devs[i]));
+        if (f32)
+          hipLaunchKernelGGL(check_pattern<float>, dim3(blocks), dim3(256), 0, st[i], (const float*)buf[i], cnt, n, bad[i]);
+        else
+          hipLaunchKernelGGL(check_pattern<uint16_t>, dim3(blocks), dim3(256), 0, st[i], (const uint16_t*)buf[i], cnt, n, bad[i]);
+        CK(hipGetLastError());
+        unsigned long long b = 0;
+        CK(hipMemcpyAsync(&b, bad[i], 8, hipMemcpyDeviceToHost, st[i]));
+        CK(hipStreamSynchronize(st[i]));
+        tot_bad += b;
+      }
+      // timing: fewer iterations for the multi-GiB messages
+      const int iters = bytes >= ((size_t)1 << 30) ? 4 : 10;
+      bool run_ok = true;
+      for (int w = 0; w < 2 && run_ok; ++w) run_ok = run_once();
+      run_ok = run_ok && sync_all();
+      const auto t0 = Clock::now();
+      for (int it = 0; it < iters && run_ok; ++it) run_ok = run_once();
+      run_ok = run_ok && sync_all();
+      if (!run_ok) { fail("ncclAllReduce failed in the timed loop"); ok = false; break; }
+      const double sec = std::chrono::duration<double>(Clock::now() - t0).count() / iters;
+      // one rank: RCCL's in-place all-reduce moves nothing - only the check counts
+      const double alg = n > 1 ? bytes / sec / 1e9 : NAN;
+      rows.push_back({f32 ? "fp32" : "bf16", bytes, sec * 1e6, alg, n > 1 ? alg * bus_factor(n) : 0.0,
+                      tot_bad});
+      if (tot_bad) ok = false;
+    }
+  }
+  cleanup();
+  if (!ok) fail("RCCL all-reduce failed or produced wrong elements");
   return ok;
 }
 
@@ -639,93 +702,148 @@ std::string p2p_json(const P2pResult& r) {
   return js + "]";
 }
 
+// C2 driver. Real mode: rank i on GPU devs[i] (peer access between all pairs,
+// one launch per GPU). Simulated mode (--xgmi-sim N): all N ranks on devs[0]
+// in one launch (rank = block / nblk), so the whole protocol - entry barrier,
+// reduce-scatter, all-gather, exit barrier, epochs - runs on a one-GPU box
+// through this same driver. Sizes from 1 KiB; <= 256 KiB takes the one-shot
+// kernel. The kernel synchronises the ranks itself (device-side entry
+// barrier), so the timed loop launches back to back with no host sync.
 bool run_xgmi(const std::vector<int>& devs, const Opts& o, std::vector<CollRow>& rows) {
-  const int n = (int)devs.size();
-  if (n < 2 || n > ntm::xgmi::kMaxRanks) return true;
-  for (int i = 0; i < n; ++i)
-    for (int j = 0; j < n; ++j) {
-      if (i == j) continue;
-      int can = 0;
-      CK(hipDeviceCanAccessPeer(&can, devs[i], devs[j]));
-      if (!can) {
-        fail("no peer access between GPUs " + std::to_string(devs[i]) + " and " + std::to_string(devs[j]));
-        return false;
+  const bool sim = o.xgmi_sim > 0;
+  const int n = sim ? o.xgmi_sim : (int)devs.size();
+  if (n < 1 || n > ntm::xgmi::kMaxRanks) return true;
+  const int ndev = sim ? 1 : n;                    // devices launching
+  auto dev_of = [&](int r) { return sim ? devs[0] : devs[r]; };
+  if (!sim)
+    for (int i = 0; i < n; ++i)
+      for (int j = 0; j < n; ++j) {
+        if (i == j) continue;
+        int can = 0;
+        CK(hipDeviceCanAccessPeer(&can, devs[i], devs[j]));
+        if (!can) {
+          fail("no peer access between GPUs " + std::to_string(devs[i]) + " and " + std::to_string(devs[j]));
+          return false;
+        }
+        CK(hipSetDevice(devs[i]));
+        hipError_t e = hipDeviceEnablePeerAccess(devs[j], 0);
+        if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) CK(e);
       }
-      CK(hipSetDevice(devs[i]));
-      hipError_t e = hipDeviceEnablePeerAccess(devs[j], 0);
-      if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) CK(e);
-    }
-  const int nblk = 64;
-  const size_t maxb = std::min<size_t>((size_t)o.allreduce_max_mib << 20, (size_t)1 << 30);
+  const int nblk = sim ? std::min(64, 1024 / n) : 64;
+  const size_t one_shot_max = (size_t)256 << 10;
+  std::vector<int> used(devs.begin(), devs.begin() + ndev);
+  const size_t maxb = sweep_cap(used, std::min<size_t>((size_t)o.allreduce_max_mib << 20,
+                                                       (size_t)1 << 30), sim ? 2 * n : 2);
   std::vector<void*> in(n), out(n);
   std::vector<unsigned*> sig(n);
-  std::vector<unsigned*> err(n);
-  std::vector<hipStream_t> st(n);
-  for (int i = 0; i < n; ++i) {
+  std::vector<unsigned*> err(ndev);
+  std::vector<unsigned long long*> bad(n);
+  std::vector<hipStream_t> st(ndev);
+  for (int i = 0; i < ndev; ++i) {
     CK(hipSetDevice(devs[i]));
     CK(hipStreamCreateWithFlags(&st[i], hipStreamNonBlocking));
-    CK(hipMalloc(&in[i], maxb));
-    CK(hipMalloc(&out[i], maxb));
-    CK(hipExtMallocWithFlags((void**)&sig[i], ntm_xgmi_signal_bytes(nblk), hipDeviceMallocUncached));
-    CK(hipMemset(sig[i], 0, ntm_xgmi_signal_bytes(nblk)));
     CK(hipMalloc(&err[i], 4));
     CK(hipMemset(err[i], 0, 4));
   }
+  for (int r = 0; r < n; ++r) {
+    CK(hipSetDevice(dev_of(r)));
+    CK(hipMalloc(&in[r], maxb));
+    CK(hipMalloc(&out[r], maxb));
+    CK(hipMalloc(&bad[r], 8));
+    CK(hipExtMallocWithFlags((void**)&sig[r], ntm_xgmi_signal_bytes(nblk), hipDeviceMallocUncached));
+    CK(hipMemset(sig[r], 0, ntm_xgmi_signal_bytes(nblk)));
+  }
   unsigned epoch = 0;
   bool ok = true;
-  for (size_t bytes = 1 << 20; bytes <= maxb; bytes *= 4) {
+  for (size_t bytes = 1024; bytes <= maxb && ok; bytes *= 4) {
     const size_t cnt = bytes / 2;
+    if (cnt % (8 * (size_t)n)) continue;
+    const int one_shot = bytes <= one_shot_max ? 1 : 0;
     auto run_once = [&]() -> bool {
       ++epoch;
-      for (int i = 0; i < n; ++i) {
+      for (int i = 0; i < ndev; ++i) {
         if (hipSetDevice(devs[i]) != hipSuccess) return false;
-        if (ntm_xgmi_allreduce_bf16((const void* const*)in.data(), out.data(), sig.data(), n, i, 1,
-                                    nblk, cnt, epoch, err[i], 0, st[i]) != 0)
+        if (ntm_xgmi_allreduce_bf16((const void* const*)in.data(), out.data(), sig.data(), n,
+                                    sim ? 0 : i, sim ? n : 1, nblk, cnt, epoch, err[i],
+                                    one_shot, st[i]) != 0)
           return false;
       }
       return true;
     };
-    for (int i = 0; i < n; ++i) {
-      CK(hipSetDevice(devs[i]));
-      hipLaunchKernelGGL(fill_pattern<uint16_t>, dim3(1024), dim3(256), 0, st[i], (uint16_t*)in[i], cnt, i);
-      CK(hipStreamSynchronize(st[i]));
+    auto sync_all = [&]() -> bool {
+      for (int i = 0; i < ndev; ++i)
+        if (hipSetDevice(devs[i]) != hipSuccess || hipStreamSynchronize(st[i]) != hipSuccess)
+          return false;
+      return true;
+    };
+    auto timed_out = [&]() -> unsigned {
+      unsigned worst = 0;
+      for (int i = 0; i < ndev; ++i) {
+        unsigned e = 0;
+        if (hipSetDevice(devs[i]) != hipSuccess ||
+            hipMemcpy(&e, err[i], 4, hipMemcpyDeviceToHost) != hipSuccess)
+          return ~0u;
+        worst = std::max(worst, e);
+      }
+      return worst;
+    };
+    for (int r = 0; r < n; ++r) {
+      CK(hipSetDevice(dev_of(r)));
+      const int contrib = (o.fault == "corrupt_allreduce" && r == n - 1) ? r + 1 : r;
+      hipLaunchKernelGGL(fill_pattern<uint16_t>, dim3(1024), dim3(256), 0, st[sim ? 0 : r],
+                         (uint16_t*)in[r], cnt, contrib);
+      CK(hipGetLastError());
+      CK(hipMemsetAsync(bad[r], 0, 8, st[sim ? 0 : r]));
     }
-    if (!run_once()) { fail("xGMI all-reduce launch failed"); return false; }
+    if (!run_once()) { fail("xGMI all-reduce launch failed"); ok = false; break; }
+    if (!sync_all()) { fail("xGMI all-reduce: stream error"); ok = false; break; }
+    if (const unsigned e = timed_out()) {
+      fail("xGMI all-reduce barrier timed out (code " + std::to_string(e) + ")");
+      ok = false;
+      break;
+    }
     unsigned long long tot_bad = 0;
-    for (int i = 0; i < n; ++i) {
-      CK(hipSetDevice(devs[i]));
-      CK(hipStreamSynchronize(st[i]));
-      unsigned e = 0;
-      CK(hipMemcpy(&e, err[i], 4, hipMemcpyDeviceToHost));
-      if (e) { fail("xGMI all-reduce barrier timed out (phase " + std::to_string(e - 1) + ")"); return false; }
-      unsigned long long* bad;
-      CK(hipMalloc(&bad, 8));
-      CK(hipMemset(bad, 0, 8));
-      hipLaunchKernelGGL(check_pattern<uint16_t>, dim3(1024), dim3(256), 0, st[i], (const uint16_t*)out[i], cnt, n, bad);
+    for (int r = 0; r < n; ++r) {
+      CK(hipSetDevice(dev_of(r)));
+      hipStream_t sr = st[sim ? 0 : r];
+      hipLaunchKernelGGL(check_pattern<uint16_t>, dim3(1024), dim3(256), 0, sr,
+                         (const uint16_t*)out[r], cnt, n, bad[r]);
+      CK(hipGetLastError());
       unsigned long long b = 0;
-      CK(hipMemcpyAsync(&b, bad, 8, hipMemcpyDeviceToHost, st[i]));
-      CK(hipStreamSynchronize(st[i]));
-      CK(hipFree(bad));
+      CK(hipMemcpyAsync(&b, bad[r], 8, hipMemcpyDeviceToHost, sr));
+      CK(hipStreamSynchronize(sr));
       tot_bad += b;
     }
     const int iters = 10;
+    bool run_ok = run_once() && sync_all();   // warm-up
     const auto t0 = Clock::now();
-    for (int it = 0; it < iters; ++it) run_once();
-    for (int i = 0; i < n; ++i) { CK(hipSetDevice(devs[i])); CK(hipStreamSynchronize(st[i])); }
+    for (int it = 0; it < iters && run_ok; ++it) run_ok = run_once();
+    run_ok = run_ok && sync_all();
     const double sec = std::chrono::duration<double>(Clock::now() - t0).count() / iters;
+    if (!run_ok) { fail("xGMI all-reduce failed in the timed loop"); ok = false; break; }
+    if (const unsigned e = timed_out()) {
+      fail("xGMI all-reduce barrier timed out in the timed loop (code " + std::to_string(e) + ")");
+      ok = false;
+      break;
+    }
     const double alg = bytes / sec / 1e9;
-    rows.push_back({"bf16", bytes, sec * 1e6, alg, alg * bus_factor(n), tot_bad});
+    rows.push_back({one_shot ? "bf16-1shot" : "bf16", bytes, sec * 1e6, alg, alg * bus_factor(n),
+                    tot_bad});
     if (tot_bad) ok = false;
   }
-  for (int i = 0; i < n; ++i) {
+  for (int r = 0; r < n; ++r) {
+    (void)hipSetDevice(dev_of(r));
+    (void)hipFree(in[r]);
+    (void)hipFree(out[r]);
+    (void)hipFree(sig[r]);
+    (void)hipFree(bad[r]);
+  }
+  for (int i = 0; i < ndev; ++i) {
     (void)hipSetDevice(devs[i]);
-    (void)hipFree(in[i]);
-    (void)hipFree(out[i]);
-    (void)hipFree(sig[i]);
     (void)hipFree(err[i]);
     (void)hipStreamDestroy(st[i]);
   }
-  if (!ok) fail("xGMI all-reduce produced wrong elements");
+  if (!ok) fail("xGMI all-reduce failed or produced wrong elements");
   return ok;
 }
 
@@ -854,9 +972,11 @@ int main(int argc, char** argv) {
   }
 
   std::vector<CollRow> rccl_rows, xgmi_rows;
-  if (n > 1) run_rccl(devs, o, rccl_rows);
+  // C1 by default on n > 1; --rccl runs the one-rank communicator on n = 1 (the
+  // same code path; its ~2 s RCCL init is not worth paying in a 1-GPU Job)
+  if (o.rccl == 1 || (o.rccl < 0 && n > 1)) run_rccl(devs, o, rccl_rows);
   const double t_rccl = wall_now();
-  if (n > 1 && o.xgmi) run_xgmi(devs, o, xgmi_rows);
+  if (o.xgmi && (n > 1 || o.xgmi_sim > 0)) run_xgmi(devs, o, xgmi_rows);
   P2pResult p2p;
   if (o.p2p && (n > 1 || o.p2p_loopback)) run_p2p(devs, o, p2p);
   const double t_end = wall_now();
@@ -891,7 +1011,7 @@ int main(int argc, char** argv) {
     p << "# TYPE amdgpu_validate_hbm_total_gb gauge\n";
     for (auto& r : res)
       p << "amdgpu_validate_hbm_total_gb{gpu=\"" << r.device << "\"} " << jnum(r.total_gb) << "\n";
-    if (n > 1)
+    if (!rccl_rows.empty() || !xgmi_rows.empty())
       p << "# TYPE amdgpu_validate_allreduce_busbw_gbps gauge\n"
         << "amdgpu_validate_allreduce_busbw_gbps{impl=\"rccl\"} " << jnum(peak_rccl) << "\n"
         << "amdgpu_validate_allreduce_busbw_gbps{impl=\"xgmi\"} " << jnum(peak_xgmi) << "\n";
@@ -936,6 +1056,7 @@ int main(int argc, char** argv) {
   }
   js += "],\"rccl_allreduce\":" + coll_json(rccl_rows);
   js += ",\"xgmi_allreduce_bf16\":" + coll_json(xgmi_rows);
+  js += ",\"xgmi_simulated_ranks\":" + std::to_string(o.xgmi_sim);
   js += ",\"xgmi_p2p_GBps\":" + p2p_json(p2p) + ",\"xgmi_p2p_min_GBps\":" +
         (p2p.n > 0 ? jnum(p2p.min_gbps) : std::string("null")) +
         ",\"xgmi_p2p_bad_pairs\":" + std::to_string(p2p.bad_pairs);

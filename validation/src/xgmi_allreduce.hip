@@ -7,7 +7,13 @@
 // accessible from the launching device). Launches ranks rank_base ..
 // rank_base + nranks_here - 1 on `stream` (nranks_here = nranks simulates the
 // whole communicator on one device). `err` (device u32, zeroed by the caller)
-// receives 1/2 if a phase-0/1 barrier timed out. count % (8*nranks) == 0.
+// receives 1/2/3 if the entry / reduce-scatter / exit barrier timed out.
+// count % (8*nranks) == 0. The barriers need every block of the launch
+// resident at once: nranks_here * nblk <= 1024 (256 CUs x 4 blocks of 256
+// threads, far below the CU limit). Two-shot may run in place (in_ptrs == out_ptrs);
+// one-shot needs in != out. Every call on a communicator uses a fresh, larger
+// epoch and the same nblk on all ranks. The kernel synchronises the ranks on
+// the device (entry barrier), so callers need no host sync or host barrier.
 NTM_API int ntm_xgmi_allreduce_bf16(const void* const* in_ptrs,
                                     void* const* out_ptrs,
                                     unsigned* const* sig_ptrs, int nranks,
@@ -15,22 +21,24 @@ NTM_API int ntm_xgmi_allreduce_bf16(const void* const* in_ptrs,
                                     size_t count, unsigned epoch, unsigned* err,
                                     int one_shot, void* stream) {
   using namespace ntm::xgmi;
-  if (nranks < 1 || nranks > kMaxRanks || nranks_here < 1 ||
-      rank_base + nranks_here > nranks || nblk < 1 || epoch == 0 ||
-      count % (8 * (size_t)nranks) != 0)
+  if (nranks < 1 || nranks > kMaxRanks || nranks_here < 1 || rank_base < 0 ||
+      rank_base + nranks_here > nranks || nblk < 1 || nranks_here * nblk > 1024 || epoch == 0 ||
+      count % (8 * (size_t)nranks) != 0 || !sig_ptrs || !err)
     return (int)hipErrorInvalidValue;
+  if (one_shot)
+    for (int r = 0; r < nranks; ++r)
+      if (in_ptrs[r] == out_ptrs[r]) return (int)hipErrorInvalidValue;
   Peers p{};
   for (int r = 0; r < nranks; ++r) {
     p.in[r] = (const __bf16*)in_ptrs[r];
     p.out[r] = (__bf16*)out_ptrs[r];
-    p.sig[r] = sig_ptrs ? sig_ptrs[r] : nullptr;
+    p.sig[r] = sig_ptrs[r];
   }
   const dim3 grid((unsigned)(nranks_here * nblk));
   if (one_shot) {
     hipLaunchKernelGGL(allreduce_1shot_kernel, grid, dim3(kThreads), 0,
-                       (hipStream_t)stream, p, nranks, rank_base, nblk, count);
+                       (hipStream_t)stream, p, nranks, rank_base, nblk, count, epoch, err);
   } else {
-    if (!sig_ptrs) return (int)hipErrorInvalidValue;
     hipLaunchKernelGGL(allreduce_2shot_kernel, grid, dim3(kThreads), 0,
                        (hipStream_t)stream, p, nranks, rank_base, nblk, count,
                        epoch, err);
