@@ -16,7 +16,8 @@ module "amd_gpu_stack" {
   gpu_node_selector = { "amd.com/gpu.present" = "true" }
   gpu_node_pool_ids = [azurerm_kubernetes_cluster_node_pool.mi355x.id]
 
-  validation_enabled   = var.gpu_validation_enabled
-  validation_image     = var.gpu_validation_image
-  validation_gpu_count = var.gpus_per_node
+  validation_enabled      = var.gpu_validation_enabled
+  validation_image        = var.gpu_validation_image
+  validation_tflops_floor = var.gpu_validation_tflops_floor
+  validation_gpu_count    = var.gpus_per_node
 }

@@ -7,7 +7,7 @@ terraform {
 
   required_providers {
     azurerm    = { source = "hashicorp/azurerm", version = ">= 3.110.0, < 4.0.0" }
-    kubernetes = { source = "hashicorp/kubernetes", version = ">= 2.25.0" }
+    kubernetes = { source = "hashicorp/kubernetes", version = ">= 2.25.0, < 3.0.0" }
     helm       = { source = "hashicorp/helm", version = ">= 2.12.0, < 3.0.0" }
   }
 }

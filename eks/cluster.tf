@@ -18,84 +18,71 @@ locals {
   node_sgs = local.byo_network ? var.additional_security_group_ids : []
   node_key = var.ssh_key == "" ? null : var.ssh_key
 
-  # Host preparation for MI355X nodes, after the EKS bootstrap: IOMMU
-  # pass-through for xGMI peer DMA, automatic NUMA balancing off (it
-  # migrates pinned HBM staging buffers), unlimited locked memory for RCCL.
+  # Host preparation for MI355X nodes, BEFORE the EKS bootstrap (kubelet and
+  # every pod start with it in effect):
+  #  * automatic NUMA balancing off - it migrates pinned HBM staging buffers;
+  #  * containerd's systemd unit gets LimitMEMLOCK=infinity, so every pod
+  #    (RCCL pins host memory) inherits an unlimited RLIMIT_MEMLOCK - a
+  #    limits.d file only reaches PAM logins, never containers;
+  #  * IOMMU pass-through (iommu=pt) for xGMI / PCIe peer DMA. A kernel
+  #    argument only takes effect on a boot: "reboot" adds it and reboots once
+  #    before the node joins (cloud-init runs user data once per instance, so a
+  #    one-shot unit re-runs it after the reboot; the second pass sees iommu=pt
+  #    in /proc/cmdline and proceeds to bootstrap); "image" expects it baked
+  #    into gpu_ami_id and only records what the kernel booted with; "off"
+  #    leaves it alone.
+  # (Inlined into the node group's bootstrap script, which already runs
+  # under `set -e`: no shebang, no shell options of its own.)
   mi355x_host_prep = <<-EOT
-    #!/bin/bash
-    set -eux
+    mode="${var.gpu_node_iommu_passthrough}"
+    if [ "$mode" = "reboot" ] && ! grep -qw 'iommu=pt' /proc/cmdline; then
+      grep -q 'iommu=pt' /etc/default/grub ||
+        sed -i 's/^GRUB_CMDLINE_LINUX="/&iommu=pt /' /etc/default/grub
+      update-grub
+      cat > /etc/systemd/system/mi355x-userdata-rerun.service <<'UNIT'
+    [Unit]
+    Description=Re-run EC2 user data once after the iommu=pt reboot
+    After=cloud-final.service
+    [Service]
+    Type=oneshot
+    ExecStartPre=/bin/systemctl disable mi355x-userdata-rerun.service
+    ExecStart=/usr/bin/cloud-init single --name scripts_user --frequency always
+    [Install]
+    WantedBy=multi-user.target
+    UNIT
+      systemctl enable mi355x-userdata-rerun.service
+      systemctl reboot
+      exit 0
+    fi
+    echo "mi355x: iommu mode=$mode cmdline: $(cat /proc/cmdline)" > /var/log/mi355x-host-prep.log
     printf 'kernel.numa_balancing = 0\n' > /etc/sysctl.d/60-mi355x.conf
     sysctl --system
-    grep -q 'iommu=pt' /etc/default/grub || {
-      sed -i 's/^GRUB_CMDLINE_LINUX="/&iommu=pt /' /etc/default/grub && update-grub || true
-    }
-    printf '%s\n' '* soft memlock unlimited' '* hard memlock unlimited' > /etc/security/limits.d/60-rccl.conf
+    mkdir -p /etc/systemd/system/containerd.service.d
+    printf '[Service]\nLimitMEMLOCK=infinity\n' > /etc/systemd/system/containerd.service.d/60-memlock.conf
+    systemctl daemon-reload
+    systemctl restart containerd
   EOT
 
-  pool_base = {
-    vpc_security_group_ids = local.node_sgs
-    key_name               = local.node_key
+  # Node groups live OUTSIDE module "eks" (the eks-managed-node-group
+  # submodule): the GPU stack then depends on the control plane + system
+  # pool only, and installs while the MI355X nodes boot. Inside module "eks"
+  # every dependent of the module waited for the GPU node group too.
+  node_group_common = {
+    cluster_name                      = module.eks.cluster_name
+    cluster_version                   = module.eks.cluster_version
+    cluster_endpoint                  = module.eks.cluster_endpoint
+    cluster_auth_base64               = module.eks.cluster_certificate_authority_data
+    cluster_service_cidr              = module.eks.cluster_service_cidr
+    cluster_primary_security_group_id = module.eks.cluster_primary_security_group_id
+    subnet_ids                        = local.node_subnets
+    vpc_security_group_ids            = concat([module.eks.node_security_group_id], local.node_sgs)
+    key_name                          = local.node_key
     metadata_options = {
       http_endpoint               = "enabled"
       http_tokens                 = "required"
       http_put_response_hop_limit = 2
     }
   }
-
-  gpu_pool = merge(local.pool_base, {
-    name                       = "tf-gpu"
-    instance_types             = [var.gpu_instance_type]
-    min_size                   = var.min_gpu_nodes
-    max_size                   = var.max_gpu_nodes
-    desired_size               = var.desired_count_gpu_nodes
-    ami_type                   = "CUSTOM"
-    ami_id                     = local.gpu_ami_id
-    enable_bootstrap_user_data = true
-    post_bootstrap_user_data = join("\n", compact([
-      local.mi355x_host_prep, var.additional_user_data, var.gpu_node_pool_additional_user_data,
-    ]))
-    labels = {
-      "amd.com/gpu.present"     = "true"
-      "amd.com/gpu.family"      = "mi355x"
-      "amd.com/gpu.arch"        = "gfx950"
-      "node.kubernetes.io/pool" = "gpu"
-    }
-    taints = {
-      amd_gpu = { key = "amd.com/gpu", value = "present", effect = "NO_SCHEDULE" }
-    }
-    block_device_mappings = {
-      root = {
-        device_name = data.aws_ami.lookup.root_device_name
-        ebs = {
-          volume_size           = var.gpu_node_pool_root_disk_size_gb
-          volume_type           = var.gpu_node_pool_root_volume_type
-          delete_on_termination = var.gpu_node_pool_delete_on_termination
-        }
-      }
-    }
-  })
-
-  cpu_pool = merge(local.pool_base, {
-    name           = "tf-cpu"
-    instance_types = [var.cpu_instance_type]
-    min_size       = var.min_cpu_nodes
-    max_size       = var.max_cpu_nodes
-    desired_size   = var.desired_count_cpu_nodes
-    post_bootstrap_user_data = join("\n", compact([
-      var.additional_user_data, var.cpu_node_pool_additional_user_data,
-    ]))
-    labels = { "node.kubernetes.io/pool" = "cpu" }
-    block_device_mappings = {
-      root = {
-        device_name = "/dev/xvda"
-        ebs = {
-          volume_size           = var.cpu_node_pool_root_disk_size_gb
-          volume_type           = var.cpu_node_pool_root_volume_type
-          delete_on_termination = var.cpu_node_pool_delete_on_termination
-        }
-      }
-    }
-  })
 }
 
 module "eks" {
@@ -133,19 +120,106 @@ module "eks" {
   }
   node_security_group_additional_rules = merge(local.node_sg_rules, var.additional_node_security_groups_rules)
 
-  eks_managed_node_groups = {
-    gpu_node_pool = local.gpu_pool
-    cpu_node_pool = local.cpu_pool
-  }
+  depends_on = [terraform_data.gpu_instance_type_guard]
+}
 
-  cluster_addons = {
-    aws-ebs-csi-driver = {
-      most_recent              = true
-      service_account_role_arn = module.ebs_csi_irsa_role.iam_role_arn
+module "gpu_node_pool" {
+  source  = "terraform-aws-modules/eks/aws//modules/eks-managed-node-group"
+  version = "~> 20.31"
+
+  name = "tf-gpu"
+
+  cluster_name                      = local.node_group_common.cluster_name
+  cluster_version                   = local.node_group_common.cluster_version
+  cluster_endpoint                  = local.node_group_common.cluster_endpoint
+  cluster_auth_base64               = local.node_group_common.cluster_auth_base64
+  cluster_service_cidr              = local.node_group_common.cluster_service_cidr
+  cluster_primary_security_group_id = local.node_group_common.cluster_primary_security_group_id
+  subnet_ids                        = local.node_group_common.subnet_ids
+  vpc_security_group_ids            = local.node_group_common.vpc_security_group_ids
+  key_name                          = local.node_group_common.key_name
+  metadata_options                  = local.node_group_common.metadata_options
+
+  instance_types             = [var.gpu_instance_type]
+  min_size                   = var.min_gpu_nodes
+  max_size                   = var.max_gpu_nodes
+  desired_size               = var.desired_count_gpu_nodes
+  ami_type                   = "CUSTOM"
+  ami_id                     = local.gpu_ami_id
+  enable_bootstrap_user_data = true
+  pre_bootstrap_user_data    = local.mi355x_host_prep
+  post_bootstrap_user_data = join("\n", compact([
+    var.additional_user_data, var.gpu_node_pool_additional_user_data,
+  ]))
+
+  labels = {
+    "amd.com/gpu.present"     = "true"
+    "amd.com/gpu.family"      = "mi355x"
+    "amd.com/gpu.arch"        = "gfx950"
+    "node.kubernetes.io/pool" = "gpu"
+  }
+  taints = {
+    amd_gpu = { key = "amd.com/gpu", value = "present", effect = "NO_SCHEDULE" }
+  }
+  block_device_mappings = {
+    root = {
+      device_name = data.aws_ami.lookup.root_device_name
+      ebs = {
+        volume_size           = var.gpu_node_pool_root_disk_size_gb
+        volume_type           = var.gpu_node_pool_root_volume_type
+        delete_on_termination = var.gpu_node_pool_delete_on_termination
+      }
     }
   }
+}
 
-  depends_on = [terraform_data.gpu_instance_type_guard]
+module "cpu_node_pool" {
+  source  = "terraform-aws-modules/eks/aws//modules/eks-managed-node-group"
+  version = "~> 20.31"
+
+  name = "tf-cpu"
+
+  cluster_name                      = local.node_group_common.cluster_name
+  cluster_version                   = local.node_group_common.cluster_version
+  cluster_service_cidr              = local.node_group_common.cluster_service_cidr
+  cluster_primary_security_group_id = local.node_group_common.cluster_primary_security_group_id
+  subnet_ids                        = local.node_group_common.subnet_ids
+  vpc_security_group_ids            = local.node_group_common.vpc_security_group_ids
+  key_name                          = local.node_group_common.key_name
+  metadata_options                  = local.node_group_common.metadata_options
+
+  instance_types = [var.cpu_instance_type]
+  min_size       = var.min_cpu_nodes
+  max_size       = var.max_cpu_nodes
+  desired_size   = var.desired_count_cpu_nodes
+  post_bootstrap_user_data = join("\n", compact([
+    var.additional_user_data, var.cpu_node_pool_additional_user_data,
+  ]))
+
+  labels = { "node.kubernetes.io/pool" = "cpu" }
+  block_device_mappings = {
+    root = {
+      device_name = "/dev/xvda"
+      ebs = {
+        volume_size           = var.cpu_node_pool_root_disk_size_gb
+        volume_type           = var.cpu_node_pool_root_volume_type
+        delete_on_termination = var.cpu_node_pool_delete_on_termination
+      }
+    }
+  }
+}
+
+# EBS CSI add-on: a standalone resource after the system pool (its controller
+# must schedule somewhere; inside module "eks" it would be created before any
+# node exists now that the node groups live outside the module).
+resource "aws_eks_addon" "ebs_csi" {
+  cluster_name                = module.eks.cluster_name
+  addon_name                  = "aws-ebs-csi-driver"
+  service_account_role_arn    = module.ebs_csi_irsa_role.iam_role_arn
+  resolve_conflicts_on_create = "OVERWRITE"
+  resolve_conflicts_on_update = "OVERWRITE"
+
+  depends_on = [module.cpu_node_pool]
 }
 
 # Web-identity role the EBS CSI controller assumes (kube-system SA).

@@ -1,6 +1,9 @@
 # AMD GPU enablement (operator or DKMS + device plugin), metrics exporter and
 # the validation Job that apply waits for. Only the Job is tied to the MI355X
-# node group; the rest installs from the system pool while GPU nodes boot.
+# node group (gpu_node_pool_ids); the rest depends on the control plane and the
+# system pool and installs while the GPU nodes boot (the reference meant to
+# gate on running GPU nodes, /root/reference/eks/main.tf:186, and gated the
+# whole operator instead).
 
 module "amd_gpu_stack" {
   source = "../modules/amd-gpu-stack"
@@ -13,12 +16,12 @@ module "amd_gpu_stack" {
   gpu_operator_namespace      = var.gpu_operator_namespace
 
   gpu_node_selector = { "amd.com/gpu.present" = "true" }
-  gpu_node_pool_ids = [module.eks.eks_managed_node_groups["gpu_node_pool"].node_group_id]
+  gpu_node_pool_ids = [module.gpu_node_pool.node_group_id]
 
   validation_enabled      = var.gpu_validation_enabled
   validation_image        = var.gpu_validation_image
   validation_gpu_count    = var.gpus_per_node
   validation_tflops_floor = var.gpu_validation_tflops_floor
 
-  depends_on = [module.eks]
+  depends_on = [module.eks, module.cpu_node_pool]
 }

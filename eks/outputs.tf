@@ -5,7 +5,7 @@ data "aws_instances" "nodes" {
   instance_state_names = ["running"]
   filter {
     name   = "tag:aws:autoscaling:groupName"
-    values = module.eks.eks_managed_node_groups["gpu_node_pool"]["node_group_autoscaling_group_names"]
+    values = module.gpu_node_pool.node_group_autoscaling_group_names
   }
 }
 
@@ -27,12 +27,12 @@ output "oidc_endpoint" {
 
 output "gpu_node_role_name" {
   description = "IAM role of the MI355X node group (attach node-level policies here)."
-  value       = module.eks.eks_managed_node_groups.gpu_node_pool.iam_role_name
+  value       = module.gpu_node_pool.iam_role_name
 }
 
 output "cpu_node_role_name" {
   description = "IAM role of the system node group."
-  value       = module.eks.eks_managed_node_groups.cpu_node_pool.iam_role_name
+  value       = module.cpu_node_pool.iam_role_name
 }
 
 output "nodes" {

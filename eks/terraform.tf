@@ -7,7 +7,7 @@ terraform {
 
   required_providers {
     aws        = { source = "hashicorp/aws", version = ">= 5.79.0, < 6.0.0" }
-    kubernetes = { source = "hashicorp/kubernetes", version = ">= 2.25.0" }
+    kubernetes = { source = "hashicorp/kubernetes", version = ">= 2.25.0, < 3.0.0" }
     helm       = { source = "hashicorp/helm", version = ">= 2.12.0, < 3.0.0" }
   }
 }

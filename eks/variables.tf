@@ -283,10 +283,20 @@ variable "gpu_validation_enabled" {
   default     = true
 }
 
-variable "gpu_validation_image" {
-  description = "Registry path of the image built from validation/image/Dockerfile."
+variable "gpu_node_iommu_passthrough" {
+  description = "How MI355X nodes get iommu=pt (xGMI / PCIe peer DMA): \"reboot\" (add it, reboot once before joining), \"image\" (already in gpu_ami_id's kernel command line), or \"off\"."
   type        = string
-  default     = "ghcr.io/amd-instinct-terraform-modules/amdgpu-validate:0.1.0"
+  default     = "reboot"
+  validation {
+    condition     = contains(["reboot", "image", "off"], var.gpu_node_iommu_passthrough)
+    error_message = "gpu_node_iommu_passthrough must be reboot, image or off."
+  }
+}
+
+variable "gpu_validation_image" {
+  description = "Registry path of the image built from validation/image/Dockerfile and pushed where the GPU nodes can pull it. Required while gpu_validation_enabled (no public default)."
+  type        = string
+  default     = ""
 }
 
 variable "gpu_validation_tflops_floor" {

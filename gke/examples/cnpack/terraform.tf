@@ -6,7 +6,7 @@
 terraform {
   required_version = ">= 1.5.0"
   required_providers {
-    kubernetes  = { source = "hashicorp/kubernetes", version = ">= 2.25.0" }
+    kubernetes  = { source = "hashicorp/kubernetes", version = ">= 2.25.0, < 3.0.0" }
     google      = { source = "hashicorp/google", version = ">= 5.40.0, < 7.0.0" }
     google-beta = { source = "hashicorp/google-beta", version = ">= 5.40.0, < 7.0.0" }
     random      = { source = "hashicorp/random", version = ">= 3.5.1" }

@@ -18,9 +18,10 @@ module "amd_gpu_stack" {
   gpu_node_selector = { "amd.com/gpu.present" = "true" }
   gpu_node_pool_ids = [google_container_node_pool.mi355x.id]
 
-  validation_enabled   = var.gpu_validation_enabled
-  validation_image     = var.gpu_validation_image
-  validation_gpu_count = tonumber(var.gpu_count)
+  validation_enabled      = var.gpu_validation_enabled
+  validation_image        = var.gpu_validation_image
+  validation_tflops_floor = var.gpu_validation_tflops_floor
+  validation_gpu_count    = tonumber(var.gpu_count)
 
   depends_on = [google_container_node_pool.system]
 }

@@ -8,7 +8,7 @@ terraform {
   required_providers {
     google      = { source = "hashicorp/google", version = ">= 5.40.0, < 7.0.0" }
     google-beta = { source = "hashicorp/google-beta", version = ">= 5.40.0, < 7.0.0" }
-    kubernetes  = { source = "hashicorp/kubernetes", version = ">= 2.25.0" }
+    kubernetes  = { source = "hashicorp/kubernetes", version = ">= 2.25.0, < 3.0.0" }
     helm        = { source = "hashicorp/helm", version = ">= 2.12.0, < 3.0.0" }
   }
 }

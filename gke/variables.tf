@@ -209,7 +209,13 @@ variable "gpu_validation_enabled" {
 }
 
 variable "gpu_validation_image" {
-  description = "Registry path of the image built from validation/image/Dockerfile."
+  description = "Registry path of the image built from validation/image/Dockerfile and pushed where the GPU nodes can pull it. Required while gpu_validation_enabled (no public default)."
   type        = string
-  default     = "ghcr.io/amd-instinct-terraform-modules/amdgpu-validate:0.1.0"
+  default     = ""
+}
+
+variable "gpu_validation_tflops_floor" {
+  description = "Fail the Job when any GPU's bf16 GEMM rate drops below this many TFLOP/s."
+  type        = number
+  default     = 1000
 }

@@ -329,6 +329,13 @@ resource "kubernetes_daemon_set_v1" "metrics_exporter" {
     }
   }
 
+  lifecycle {
+    precondition {
+      condition     = !var.metrics_exporter_native || var.validation_image != ""
+      error_message = "metrics_exporter_native runs amdgpu-exporter from validation_image: set validation_image."
+    }
+  }
+
   depends_on = [kubernetes_daemon_set_v1.amdgpu_dkms]
 }
 

@@ -45,16 +45,22 @@ locals {
     name      = "${var.cluster_name}-mi355x"
     namespace = local.namespace
     spec = {
+      # Every component the operator places on the (tainted) GPU nodes carries
+      # the GPU toleration - the KMM driver build/load pods included: without
+      # it amd.com/gpu never becomes allocatable and apply waits out
+      # validation_timeout. tfcheck rule gpu-toleration enforces this.
       driver = merge({
-        enable    = var.driver_enabled
-        blacklist = true
-        version   = var.gpu_operator_driver_version
+        enable      = var.driver_enabled
+        blacklist   = true
+        version     = var.gpu_operator_driver_version
+        tolerations = local.gpu_tolerations
       }, var.driver_image_repository == "" ? {} : { image = var.driver_image_repository })
       devicePlugin = {
-        devicePluginImage  = var.device_plugin_image
-        nodeLabellerImage  = var.node_labeller_image
-        enableNodeLabeller = true
+        devicePluginImage       = var.device_plugin_image
+        nodeLabellerImage       = var.node_labeller_image
+        enableNodeLabeller      = true
         devicePluginTolerations = local.gpu_tolerations
+        nodeLabellerTolerations = local.gpu_tolerations
       }
       metricsExporter = {
         enable      = var.metrics_exporter_enabled
@@ -113,6 +119,30 @@ resource "kubernetes_resource_quota_v1" "critical_pods" {
 /********************************************
   AMD GPU Operator (operator mode)
 ********************************************/
+# CRD cleanup on destroy. `helm uninstall` of the operator leaves its CRDs
+# (DeviceConfig, KMM, NFD) behind; the reference removed them through the
+# NVIDIA chart's operator.cleanupCRD value (/root/reference/aks/main.tf:89-91).
+# The AMD chart's equivalent cannot be pinned offline, so the module owns it:
+# this release is created BEFORE the operator (which depends on it), hence
+# destroyed AFTER it, and its pre-delete hook Job deletes the CRDs.
+resource "helm_release" "crd_janitor" {
+  count = local.operator_mode && var.gpu_operator_crd_cleanup ? 1 : 0
+
+  name      = "amd-gpu-crd-janitor"
+  chart     = "${path.module}/charts/amd-gpu-crd-janitor"
+  namespace = local.namespace
+  atomic    = true
+  timeout   = var.helm_timeout_seconds
+  values = [yamlencode({
+    name   = "amd-gpu-crd-janitor"
+    image  = var.kubectl_image
+    crds   = var.gpu_operator_crds
+    labels = local.common_labels
+  })]
+
+  depends_on = [kubernetes_resource_quota_v1.critical_pods]
+}
+
 resource "helm_release" "amd_gpu_operator" {
   count = local.operator_mode ? 1 : 0
 
@@ -124,11 +154,12 @@ resource "helm_release" "amd_gpu_operator" {
   create_namespace = false
   atomic           = true
   cleanup_on_fail  = true
+  reset_values     = true # reference eks/main.tf:193-196: no values carried over on upgrade
   wait             = true
   timeout          = var.helm_timeout_seconds
   values           = [yamlencode(local.operator_values)]
 
-  depends_on = [kubernetes_resource_quota_v1.critical_pods]
+  depends_on = [kubernetes_resource_quota_v1.critical_pods, helm_release.crd_janitor]
 }
 
 # The DeviceConfig CR is rendered by a module-local chart instead of

@@ -125,6 +125,13 @@ resource "kubernetes_job_v1" "gpu_validation" {
 
   wait_for_completion = var.wait_for_validation
 
+  lifecycle {
+    precondition {
+      condition     = var.validation_image != ""
+      error_message = "validation_enabled needs validation_image: build validation/image/Dockerfile, push it to a registry the GPU nodes can pull from, and pass its reference (or set validation_enabled = false)."
+    }
+  }
+
   timeouts {
     create = var.validation_timeout
     update = var.validation_timeout

@@ -64,6 +64,32 @@ variable "gpu_operator_chart_name" {
   description = "Chart name inside gpu_operator_chart_repository."
 }
 
+variable "gpu_operator_crd_cleanup" {
+  type        = bool
+  default     = true
+  description = "Delete the operator's CRDs (gpu_operator_crds) on destroy, after the operator release is gone (pre-delete hook of a module-local chart). Parity with the reference's operator.cleanupCRD=true (aks/main.tf:89-91)."
+}
+
+variable "gpu_operator_crds" {
+  type = list(string)
+  default = [
+    "deviceconfigs.amd.com",
+    "modules.kmm.sigs.x-k8s.io",
+    "nodemodulesconfigs.kmm.sigs.x-k8s.io",
+    "preflightvalidations.kmm.sigs.x-k8s.io",
+    "nodefeatures.nfd.k8s-sigs.io",
+    "nodefeaturerules.nfd.k8s-sigs.io",
+    "nodefeaturegroups.nfd.k8s-sigs.io",
+  ]
+  description = "CRDs the AMD GPU Operator chart (with its KMM and NFD subcharts) registers; deleted on destroy when gpu_operator_crd_cleanup."
+}
+
+variable "kubectl_image" {
+  type        = string
+  default     = "docker.io/bitnami/kubectl:1.31"
+  description = "Image with kubectl for the destroy-time CRD cleanup Job."
+}
+
 variable "create_namespace" {
   type        = bool
   default     = true
@@ -186,8 +212,8 @@ variable "validation_enabled" {
 
 variable "validation_image" {
   type        = string
-  default     = "ghcr.io/amd-instinct-terraform-modules/amdgpu-validate:0.1.0"
-  description = "Image built from validation/image/Dockerfile (contains only the amdgpu-validate binary + ROCm runtime + RCCL)."
+  default     = ""
+  description = "Image built from validation/image/Dockerfile and pushed to a registry the nodes can pull from (contains only the amdgpu-validate binary + ROCm runtime + RCCL). Required when validation_enabled (or metrics_exporter_native): there is no public default, and a wrong one would sit in ImagePullBackOff until validation_timeout."
 }
 
 variable "prepull_validation_image" {

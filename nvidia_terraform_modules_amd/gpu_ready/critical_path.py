@@ -33,7 +33,12 @@ DEFAULT_DURATIONS = {
     "google_compute_subnetwork": 20.0,
     "azurerm_resource_group": 5.0,
     # control plane
-    "module.eks": 780.0,                     # cluster ACTIVE (~10 min) + node groups
+    "module.eks": 600.0,                     # cluster ACTIVE (~10 min), no node groups
+    "module.cpu_node_pool": 180.0,           # system nodes boot + join
+    # MI355X nodes boot + join + Ready, incl. the one-time iommu=pt reboot
+    # before the join (eks gpu_node_iommu_passthrough = "reboot", ~90 s)
+    "module.gpu_node_pool": 390.0,
+    "aws_eks_addon": 60.0,
     "google_container_cluster": 420.0,
     "azurerm_kubernetes_cluster": 360.0,
     # node pools (GPU nodes boot + join + Ready)
@@ -49,6 +54,7 @@ DEFAULT_DURATIONS = {
     # CR-only / monitor-only charts: helm's wait has no workload to wait for
     "helm_release.device_config": 5.0,
     "helm_release.service_monitor": 5.0,
+    "helm_release.crd_janitor": 3.0,         # hooks run at destroy only: nothing to wait for
     "kubernetes_daemon_set_v1": 30.0,
     "kubernetes_service_v1": 1.0,
     "kubernetes_service_account_v1": 1.0,
@@ -73,8 +79,9 @@ PHASE_OF_KIND = [
     ("network", ("module.vpc", "google_compute_network", "google_compute_subnetwork",
                  "azurerm_resource_group")),
     ("control_plane", ("google_container_cluster", "azurerm_kubernetes_cluster.",
-                       "module.ebs_csi_irsa_role")),
-    ("gpu_nodes_ready", ("module.eks", "google_container_node_pool",
+                       "module.ebs_csi_irsa_role", "module.eks", "module.cpu_node_pool",
+                       "aws_eks_addon", "google_container_node_pool.system")),
+    ("gpu_nodes_ready", ("module.gpu_node_pool", "google_container_node_pool",
                          "azurerm_kubernetes_cluster_node_pool")),
     ("operator_deployed", ("helm_release.amd_gpu_operator", "helm_release.device_config",
                            "kubernetes_namespace_v1", "kubernetes_resource_quota_v1")),

@@ -17,6 +17,9 @@ module-required    required variable of a local callee not passed
 module-output      module.X.Y where Y is not an output of local callee X
 unknown-function   call to a function Terraform does not have
 vendor-lint        NVIDIA/CUDA-specific strings in literals (AMD-only build)
+gpu-toleration     a pod spec (or operator component) placed on the GPU nodes through
+                   the GPU node selector does not tolerate the GPU node taint, so it
+                   would never schedule and `apply` would wait out validation_timeout
 fmt                tabs / trailing whitespace (terraform fmt would rewrite)
 """
 from __future__ import annotations
@@ -26,7 +29,8 @@ from dataclasses import dataclass
 from pathlib import Path
 
 from .config import Module, load_module, provider_of_type
-from .hcl import Block, Body, Traversal, iter_calls, iter_strings, walk_refs
+from .hcl import (Block, Body, Call, ObjectExpr, Traversal, iter_calls, iter_strings, key_name,
+                  walk_refs)
 
 BUILTIN_ROOTS = {"path", "terraform"}
 
@@ -296,6 +300,7 @@ def analyze(mod: Module, *, strict_unused: bool = True, vendor_lint: bool = True
 
     if vendor_lint:
         out.extend(vendor_findings(mod))
+    out.extend(toleration_findings(mod))
     if check_fmt:
         out.extend(fmt_findings(mod.path))
     return out
@@ -315,6 +320,87 @@ def vendor_findings(mod: Module) -> list[Finding]:
                 if any(p.search(s) for p in VENDOR_PATTERNS):
                     out.append(Finding("vendor-lint", "error", f"{fname}:{attr.line}",
                                        f"NVIDIA/CUDA-specific string in {name}"))
+    return out
+
+
+GPU_SELECTOR = "gpu_node_selector"
+GPU_TAINT = "gpu_node_taint_key"
+GPU_TOLERATIONS = "gpu_tolerations"   # local list built from the taint key
+
+
+def _refers_to(expr, name: str) -> bool:
+    return any(name in ref.path() or ref.root == name for ref, _ in walk_refs(expr))
+
+
+def _pod_specs(body: Body, where: str):
+    """Every block body (recursively) that sets node_selector."""
+    if body.attr("node_selector") is not None:
+        yield body, where
+    for b in body.blocks:
+        yield from _pod_specs(b.body, where)
+
+
+def _tolerates(body: Body) -> bool:
+    for b in body.blocks:
+        if b.type == "toleration" and _refers_to(b.body.attr("key") or ObjectExpr([]), GPU_TAINT):
+            return True
+        if b.type == "dynamic" and b.labels and b.labels[0] == "toleration":
+            fe = b.body.attr("for_each")
+            if fe is not None and (_refers_to(fe, GPU_TOLERATIONS) or _refers_to(fe, GPU_TAINT)):
+                return True
+    return False
+
+
+def _object_keys(expr) -> dict:
+    """Static keys -> values of an object constructor, or of merge(...) of them."""
+    if isinstance(expr, ObjectExpr):
+        return {key_name(k): v for k, v in expr.items if key_name(k)}
+    if isinstance(expr, Call) and expr.name == "merge":
+        out: dict = {}
+        for a in expr.args:
+            out.update(_object_keys(a))
+        return out
+    return {}
+
+
+def _selector_objects(expr):
+    """Object constructors (anywhere inside expr) that carry a `selector` key."""
+    stack = [expr]
+    while stack:
+        e = stack.pop()
+        if isinstance(e, ObjectExpr):
+            if e.get("selector") is not None:
+                yield e
+            stack.extend(v for _, v in e.items)
+        elif isinstance(e, Call):
+            stack.extend(e.args)
+
+
+def toleration_findings(mod: Module) -> list[Finding]:
+    """gpu-toleration: Kubernetes pod specs whose node_selector references the
+    GPU node selector need a toleration keyed on the GPU taint; operator CRs
+    (DeviceConfig) whose `selector` is the GPU node selector need a
+    *olerations entry referencing the GPU tolerations in every component."""
+    out = []
+    for r in mod.managed:
+        for body, _ in _pod_specs(r.block.body, r.address):
+            if _refers_to(body.attr("node_selector"), GPU_SELECTOR) and not _tolerates(body):
+                out.append(Finding("gpu-toleration", "error", f"{r.file}:{r.block.line}",
+                                   f"{r.address}: pod spec selects the GPU nodes but does not "
+                                   f"tolerate var.{GPU_TAINT}"))
+    for name, (expr, f, line) in mod.locals.items():
+        for obj in _selector_objects(expr):
+            if not _refers_to(obj.get("selector"), GPU_SELECTOR):
+                continue
+            for comp, val in _object_keys(obj).items():
+                keys = _object_keys(val)
+                if not keys:
+                    continue      # scalar settings next to the components
+                tol = [v for k, v in keys.items() if k.lower().endswith("tolerations")]
+                if not tol or not all(_refers_to(v, GPU_TOLERATIONS) for v in tol):
+                    out.append(Finding("gpu-toleration", "error", f"{f}:{line}",
+                                       f"local.{name}: component {comp!r} runs on the GPU "
+                                       f"nodes without local.{GPU_TOLERATIONS}"))
     return out
 
 

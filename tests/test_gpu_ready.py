@@ -215,9 +215,11 @@ def test_cli_critical_path_json(tmp_path):
 def test_named_priors_beat_type_priors(repo):
     """A CR-only chart (the DeviceConfig) has nothing for helm's wait to wait on:
     its type.name prior (5 s) applies instead of the operator-chart prior."""
-    cp = critical_path(build_graph(repo / "eks"))
+    # a fast GPU pool puts the stack branch on the critical path
+    fast = {"module.gpu_node_pool": 10.0}
+    cp = critical_path(build_graph(repo / "eks"), fast)
     path = dict(cp.path)
     assert path["module.amd_gpu_stack.helm_release.device_config"] == 5.0
     assert path["module.amd_gpu_stack.helm_release.amd_gpu_operator"] == 120.0
-    over = critical_path(build_graph(repo / "eks"), {"helm_release.device_config": 50.0})
+    over = critical_path(build_graph(repo / "eks"), {**fast, "helm_release.device_config": 50.0})
     assert dict(over.path)["module.amd_gpu_stack.helm_release.device_config"] == 50.0

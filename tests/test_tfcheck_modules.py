@@ -4,6 +4,7 @@ from pathlib import Path
 
 import pytest
 
+from nvidia_terraform_modules_amd.gpu_ready.critical_path import critical_path
 from nvidia_terraform_modules_amd.tfcheck.analysis import analyze, errors
 from nvidia_terraform_modules_amd.tfcheck.config import find_modules, load_module
 from nvidia_terraform_modules_amd.tfcheck.contract import compare, extract, load_expected
@@ -82,7 +83,7 @@ def test_validation_job_waits_for_gpu_nodes_and_stack(repo, root):
     g = build_graph(repo / root)
     assert not g.hard_cycles()
     (job,) = g.find("kubernetes_job_v1.gpu_validation")
-    pools = {"eks": ["module.eks"], "gke": ["google_container_node_pool.mi355x"],
+    pools = {"eks": ["module.gpu_node_pool"], "gke": ["google_container_node_pool.mi355x"],
              "aks": ["azurerm_kubernetes_cluster_node_pool.mi355x"]}[root]
     for p in pools:
         assert g.depends_on(job, p), f"{job} must wait for {p}"
@@ -90,14 +91,161 @@ def test_validation_job_waits_for_gpu_nodes_and_stack(repo, root):
     assert stack and all(g.depends_on(job, s) for s in stack)
 
 
-@pytest.mark.parametrize("root", ["gke", "aks"])
+GPU_POOL = {"eks": "module.gpu_node_pool", "gke": "google_container_node_pool.mi355x",
+            "aks": "azurerm_kubernetes_cluster_node_pool.mi355x"}
+
+
+@pytest.mark.parametrize("root", ROOTS)
 def test_operator_install_overlaps_gpu_node_boot(repo, root):
-    """Only the Job needs GPUs: the operator must NOT wait for the GPU pool."""
+    """Only the Job needs GPUs: the operator, its DeviceConfig and the CRD
+    janitor must NOT wait for the GPU pool (on EKS the whole stack
+    hung off module.eks, which contained the GPU node group)."""
     g = build_graph(repo / root)
+    pool = GPU_POOL[root]
+    for name in ("helm_release.amd_gpu_operator", "helm_release.device_config",
+                 "helm_release.crd_janitor", "kubernetes_namespace_v1.gpu_stack"):
+        (n,) = g.find(name)
+        assert not g.depends_on(n, pool), f"{n} waits for {pool}"
+    (job,) = g.find("kubernetes_job_v1.gpu_validation")
+    assert g.depends_on(job, pool)
+
+
+def test_eks_critical_path_runs_stack_beside_gpu_boot(repo):
+    """With the node groups outside module "eks", the GPU pool boot and the
+    operator install are parallel branches that meet at the validation Job."""
+    from nvidia_terraform_modules_amd.gpu_ready.critical_path import DEFAULT_DURATIONS
+
+    g = build_graph(repo / "eks")
     (op,) = g.find("helm_release.amd_gpu_operator")
-    pool = {"gke": "google_container_node_pool.mi355x",
-            "aks": "azurerm_kubernetes_cluster_node_pool.mi355x"}[root]
-    assert not g.depends_on(op, pool)
+    assert g.depends_on(op, "module.cpu_node_pool") and g.depends_on(op, "module.eks")
+    cp = critical_path(g)
+    serial = (DEFAULT_DURATIONS["module.vpc"] + DEFAULT_DURATIONS["module.eks"]
+              + DEFAULT_DURATIONS["module.gpu_node_pool"] + 2 * DEFAULT_DURATIONS["helm_release"])
+    assert cp.total_s < serial + 300        # not pool-then-operator any more
+    on_path = [a for a, _ in cp.path]
+    assert not ("module.gpu_node_pool" in on_path and any("amd_gpu_operator" in a for a in on_path))
+
+
+def test_gpu_workloads_tolerate_the_gpu_taint(repo):
+    """Every pod spec placed on the tainted MI355X nodes tolerates the taint -
+    the operator's KMM driver pods included (DeviceConfig spec.driver)."""
+    m = load_module(repo / "modules/amd-gpu-stack")
+    assert not [f for f in analyze(m) if f.rule == "gpu-toleration"]
+    dc = m.locals["device_config_values"][0]
+    spec = dc.get("spec")
+    from nvidia_terraform_modules_amd.tfcheck.analysis import _object_keys
+    for comp in ("driver", "devicePlugin", "metricsExporter"):
+        assert any(k.endswith("olerations") for k in _object_keys(spec.get(comp))), comp
+
+
+def test_gpu_toleration_rule_fires(tmp_path):
+    (tmp_path / "main.tf").write_text('''terraform {
+  required_providers {
+    kubernetes = { source = "hashicorp/kubernetes" }
+  }
+}
+variable "gpu_node_selector" {
+  default = {}
+}
+variable "gpu_node_taint_key" {
+  default = "amd.com/gpu"
+}
+locals {
+  gpu_tolerations = [{ key = var.gpu_node_taint_key, operator = "Exists" }]
+  dc = {
+    spec = {
+      driver       = { enable = true }
+      devicePlugin = { devicePluginTolerations = local.gpu_tolerations }
+      selector     = var.gpu_node_selector
+    }
+  }
+}
+resource "kubernetes_daemon_set_v1" "x" {
+  metadata {
+    name = "x"
+  }
+  spec {
+    template {
+      spec {
+        node_selector = var.gpu_node_selector
+        container {
+          name  = "c"
+          image = "i"
+        }
+      }
+    }
+  }
+}
+output "o" {
+  value = local.dc
+}
+''')
+    fs = [f for f in analyze(load_module(tmp_path)) if f.rule == "gpu-toleration"]
+    msgs = " ".join(f.message for f in fs)
+    assert len(fs) == 2 and "kubernetes_daemon_set_v1.x" in msgs and "'driver'" in msgs
+
+
+def test_eks_gpu_node_host_prep_takes_effect(repo):
+    """VERDICT r1 #5: iommu=pt must be in effect on the node's first serving
+    boot and RLIMIT_MEMLOCK must reach pods (containerd's unit, not PAM)."""
+    m = load_module(repo / "eks")
+    prep = "".join(p for p in m.locals["mi355x_host_prep"][0].parts if isinstance(p, str))
+    assert "containerd.service.d" in prep and "LimitMEMLOCK=infinity" in prep
+    assert "systemctl restart containerd" in prep and "limits.d" not in prep
+    assert "/proc/cmdline" in prep and "systemctl reboot" in prep and "update-grub" in prep
+    assert "cloud-init single --name scripts_user --frequency always" in prep
+    assert "set -u" not in prep and "#!/bin/bash" not in prep   # inlined before bootstrap.sh
+    pool = m.modules["gpu_node_pool"].block.body
+    assert "mi355x_host_prep" in str(pool.attr("pre_bootstrap_user_data"))
+    assert m.variables["gpu_node_iommu_passthrough"].default == "reboot"
+    assert m.variables["gpu_node_iommu_passthrough"].validations
+
+
+def test_operator_release_lifecycle_and_destroy_order(repo):
+    """reset_values like the reference (eks/main.tf:193-196); CRDs cleaned up on
+    destroy (reference operator.cleanupCRD=true, aks/main.tf:89-91); destroy
+    order DeviceConfig -> operator -> CRD janitor -> namespace."""
+    m = load_module(repo / "modules/amd-gpu-stack")
+    op = m.resources["helm_release.amd_gpu_operator"].block.body
+    for flag in ("reset_values", "atomic", "cleanup_on_fail"):
+        assert evaluate_static(op.attr(flag)) is True, flag
+    assert m.variables["gpu_operator_crd_cleanup"].default is True
+    crds = m.variables["gpu_operator_crds"].default
+    assert "deviceconfigs.amd.com" in crds and any("kmm" in c for c in crds)
+    chart = repo / "modules/amd-gpu-stack/charts/amd-gpu-crd-janitor/templates/cleanup.yaml"
+    text = chart.read_text()
+    assert "helm.sh/hook: pre-delete" in text and "kubectl" in text and "delete" in text
+    g = build_graph(repo / "eks")
+    (dc,) = g.find("helm_release.device_config")
+    (opn,) = g.find("helm_release.amd_gpu_operator")
+    (jan,) = g.find("helm_release.crd_janitor")
+    (ns,) = g.find("kubernetes_namespace_v1.gpu_stack")
+    # destroy runs in reverse dependency order
+    assert g.depends_on(dc, opn) and g.depends_on(opn, jan) and g.depends_on(jan, ns)
+
+
+def test_validation_image_has_no_unpublished_default(repo):
+    m = load_module(repo / "modules/amd-gpu-stack")
+    assert m.variables["validation_image"].default == ""
+    job = m.resources["kubernetes_job_v1.gpu_validation"].block.body
+    pre = [p for lc in job.blocks_of("lifecycle") for p in lc.body.blocks_of("precondition")]
+    assert pre and "validation_image" in str(pre[0].body.attr("condition"))
+    for root in ROOTS:
+        assert load_module(repo / root).variables["gpu_validation_image"].default == ""
+
+
+@pytest.mark.parametrize("root", ROOTS)
+def test_root_forwards_tflops_floor(repo, root):
+    call = load_module(repo / root).modules["amd_gpu_stack"].block.body
+    assert "gpu_validation_tflops_floor" in str(call.attr("validation_tflops_floor"))
+
+
+def test_kubernetes_and_helm_providers_are_bounded(repo):
+    for d in _modules(repo):
+        for name, req in load_module(d).required_providers.items():
+            if name in ("kubernetes", "helm"):
+                v = str(req)
+                assert "<" in v, f"{d}: {name} {v}"
 
 
 def test_stack_defaults_are_amd_mi355x(repo):

@@ -72,12 +72,23 @@ def _write(tmp_path, text, name="v.tf"):
 
 # ------------------------------------------------------------ plans on the modules
 def test_eks_plan_clean():
-    r = plan(ROOT / "eks", cli_vars=["cluster_name=mi355x", "gpu_instance_type=x.48xlarge"])
+    r = plan(ROOT / "eks", cli_vars=["cluster_name=mi355x", "gpu_instance_type=x.48xlarge",
+                                     "gpu_validation_image=registry.example/amdgpu-validate:1"])
     assert r.ok, r.errors
     assert "module.amd_gpu_stack.kubernetes_job_v1.gpu_validation[0]" in r.resources
     assert "module.amd_gpu_stack.helm_release.amd_gpu_operator[0]" in r.resources
     assert any(m.startswith("module.eks ") for m in r.registry_modules)
     assert "data.aws_ami.lookup" in r.data_sources
+
+
+def test_plan_requires_a_validation_image_while_validating():
+    """No unpublished default image: plan stops with a clear message instead of
+    an apply that sits in ImagePullBackOff for validation_timeout."""
+    r = plan(ROOT / "eks", cli_vars=["cluster_name=mi355x", "gpu_instance_type=x.48xlarge"])
+    assert any("validation_enabled needs validation_image" in e for e in r.errors), r.errors
+    r = plan(ROOT / "eks", cli_vars=["cluster_name=mi355x", "gpu_instance_type=x.48xlarge",
+                                     "gpu_validation_enabled=false"])
+    assert r.ok, r.errors
 
 
 def test_eks_plan_requires_cluster_name_and_instance_type():
@@ -99,7 +110,8 @@ def test_gke_plan_rejects_nvidia_gpu_type():
 
 def test_gke_daemonsets_mode_expands_the_stack(tmp_path):
     vf = _write(tmp_path, 'project_id = "p"\nregion = "us-central1"\ncluster_name = "c"\n'
-                'node_zones = ["us-central1-a"]\ngpu_instance_type = "m"\n', "t.tfvars")
+                'node_zones = ["us-central1-a"]\ngpu_instance_type = "m"\n'
+                'gpu_validation_image = "registry.example/amdgpu-validate:1"\n', "t.tfvars")
     r = plan(ROOT / "gke", var_files=[vf])
     assert r.ok, r.errors
     for a in ("module.amd_gpu_stack.kubernetes_daemon_set_v1.amdgpu_dkms[0]",
