@@ -288,11 +288,14 @@ def verify_bf16(c: torch.Tensor, ref: torch.Tensor, atol: float, rtol: float) ->
 
 # (unroll, policy, grid) of the block-tiled K2 kernels; policy bit0 =
 # nontemporal loads, bit1 = nontemporal stores, bit2 = software-pipelined
-# copy, grid 0 = auto; unroll 1 = the original grid-stride kernel. Chosen
-# by tools/hbm_sweep.py on MI355X (4 GiB, profiles/r1_hbm_sweep/):
-#   copy  (4, 7, 256)  5.75 TB/s  (torch copy_ 4.74, grid-stride 4.84)
-#   read  (8, 1, 1024) 7.13 TB/s  (grid-stride 6.11)
-STREAM_COPY_CONFIG: tuple[int, int, int] = (4, 7, 256)
+# copy, bit3 = chunked; grid 0 = auto; unroll 1 = the original grid-stride
+# kernel. Chosen by tools/hbm_sweep.py on MI355X, interleaved rounds, two
+# boxes (profiles/r2_k2/): (8, 7, 512) is top-3 at 1, 2 and 4 GiB on both -
+# box 1: 5.82 TB/s at 1 GiB, 5.69 at 4 GiB; box 2: 5.78 / 5.57 at 1 / 2 GiB
+# (torch copy_ 5.23 / 5.08). The previous (4, 7, 256) ranged 5.44-6.00 and
+# fell out of box 2's top 20. Box-to-box spread is ~5 %.
+#   read  (8, 1, 1024) 7.08-7.13 TB/s at 1 GiB (grid-stride 6.11)
+STREAM_COPY_CONFIG: tuple[int, int, int] = (8, 7, 512)
 STREAM_READ_CONFIG: tuple[int, int, int] = (8, 1, 1024)
 
 

@@ -1,6 +1,8 @@
-"""Sweep the K2 HBM stream kernels (unroll x cache policy x grid) on one
-MI355X and compare with torch's copy_. GB/s counts read + write bytes for
-copies (the STREAM convention) and read bytes for reads."""
+"""Sweep the K2 HBM stream kernels (unroll x cache policy x grid x buffer
+size) on one MI355X against torch's copy_, in INTERLEAVED rounds (median and
+best per config, one process - cdna_hip_programming.md §5.4 rule 24), and
+check every copy config bytewise. GB/s counts read + write bytes for copies
+(the STREAM convention) and read bytes for reads."""
 import argparse
 import itertools
 import json
@@ -28,39 +30,47 @@ def timed(fn, iters):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gib", type=float, default=4.0)
-    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--gib", default="1,2", help="comma list of buffer sizes (GiB each)")
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--rounds", type=int, default=5, help="interleaved rounds (median reported)")
+    ap.add_argument("--grids", default="256,384,512,768,1024")
     args = ap.parse_args()
-    nbytes = int(args.gib * 2**30) // 4096 * 4096
-    src = torch.empty(nbytes // 2, dtype=torch.bfloat16, device="cuda")
-    ops.fill_uniform_(src, seed=7)
-    dst = torch.empty_like(src)
-    sink = torch.zeros(1 << 16, dtype=torch.float32, device="cuda")
-    rows = []
+    import statistics
 
-    def rec(kind, cfg, t, mult):
-        gbps = mult * nbytes / t / 1e9
-        rows.append({"kind": kind, "cfg": cfg, "ms": round(t * 1e3, 3), "GBps": round(gbps, 1)})
-        print(json.dumps(rows[-1]), flush=True)
-
-    rec("copy", "torch.copy_", timed(lambda: dst.copy_(src), args.iters), 2)
-    rec("copy", "legacy", timed(lambda: ops.stream_copy(src, dst, config=None), args.iters), 2)
-    rec("read", "legacy", timed(lambda: ops.stream_read(src, sink, config=None), args.iters), 1)
-    for u, pol, grid in itertools.product((2, 4, 8), (1, 3, 5, 7), (0, 256, 512, 1024, 2048, 4096)):
-        cfg = (u, pol, grid)
-        rec("copy", list(cfg), timed(lambda: ops.stream_copy(src, dst, config=cfg), args.iters), 2)
-    for u, pol, grid in itertools.product((2, 4, 8, 16), (0, 1), (0, 1024, 2048, 4096)):
-        cfg = (u, pol, grid)
-        rec("read", list(cfg), timed(lambda: ops.stream_read(src, sink, config=cfg), args.iters), 1)
-    # correctness of the best copy
-    best = max((r for r in rows if r["kind"] == "copy" and isinstance(r["cfg"], list)),
-               key=lambda r: r["GBps"])
-    dst.zero_()
-    ops.stream_copy(src, dst, config=tuple(best["cfg"]))
-    assert torch.equal(src, dst), "tuned copy mismatch"
-    bestr = max((r for r in rows if r["kind"] == "read" and isinstance(r["cfg"], list)),
-                key=lambda r: r["GBps"])
-    print("BEST", json.dumps({"copy": best, "read": bestr}))
+    grids = [int(g) for g in args.grids.split(",")]
+    for gib in [float(x) for x in args.gib.split(",")]:
+        nbytes = int(gib * 2**30) // 65536 * 65536
+        src = torch.empty(nbytes // 2, dtype=torch.bfloat16, device="cuda")
+        ops.fill_uniform_(src, seed=7)
+        dst = torch.empty_like(src)
+        sink = torch.zeros(1 << 16, dtype=torch.float32, device="cuda")
+        copies = {"torch.copy_": lambda: dst.copy_(src),
+                  "tuned-default": lambda: ops.stream_copy(src, dst)}
+        for u, pol, grid in itertools.product((2, 4, 8), (3, 7, 11), grids):
+            copies[f"copy {u},{pol},{grid}"] = lambda c=(u, pol, grid): ops.stream_copy(src, dst, config=c)
+        reads = {"tuned-default": lambda: ops.stream_read(src, sink)}
+        for u, pol, grid in itertools.product((4, 8, 16), (1,), (0, 512, 1024, 2048)):
+            reads[f"read {u},{pol},{grid}"] = lambda c=(u, pol, grid): ops.stream_read(src, sink, config=c)
+        for kind, cands, mult in (("copy", copies, 2), ("read", reads, 1)):
+            ts = {k: [] for k in cands}
+            for _ in range(args.rounds):
+                for k, fn in cands.items():
+                    ts[k].append(timed(fn, args.iters))
+            rows = sorted(({"gib": gib, "kind": kind, "cfg": k,
+                            "GBps_median": round(mult * nbytes / statistics.median(v) / 1e9, 1),
+                            "GBps_best": round(mult * nbytes / min(v) / 1e9, 1)}
+                           for k, v in ts.items()), key=lambda r: -r["GBps_median"])
+            for r in rows:
+                print(json.dumps(r), flush=True)
+        for k, fn in copies.items():
+            dst.zero_()
+            fn()
+            torch.cuda.synchronize()
+            assert torch.equal(src, dst), f"copy mismatch: {k}"
+        print(json.dumps({"gib": gib, "all_copies_bytewise_equal": True, "n": len(copies)}),
+              flush=True)
+        del src, dst
+        torch.cuda.empty_cache()
 
 
 if __name__ == "__main__":

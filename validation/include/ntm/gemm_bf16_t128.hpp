@@ -1,5 +1,7 @@
-// K1 "tile128" / "tile256x128": bf16 GEMM with 128x128 or 256x128 macro tiles
-// for the sizes where the 256x256 kernels cannot fill the chip.
+// K1 tile kernels: bf16 GEMM with (32 MT) x (32 NT) macro tiles for the sizes
+// where the 256x256 kernels cannot fill the chip: "tile128" (MT = NT = 4,
+// 128x128), "tile256x128" (8, 4), "tile160" (5, 5, 160x160) and
+// "tile256x160" (8, 5).
 //
 //   C[M x N] (bf16) = A[M x K] (bf16) * B[N x K]^T (bf16), fp32 accumulate.
 //
@@ -8,23 +10,23 @@
 // 128x128 tiles give 256 workgroups there (one per CU); 256x128 tiles fill the
 // chip in one round from 2048 x 4096 up to 4096 x 4096 outputs.
 //
-// Structure (one workgroup per CU, one wave per SIMD), MT = 4 (128x128) or
-// MT = 8 (256x128):
-//  * 4 waves as 2 (M) x 2 (N), each owning (16 MT) x 64 outputs = MT x 4 MFMA
-//    tiles of 16x16 (16 MT fp32 accumulators per lane, AGPR-pinned),
+// Structure (one workgroup per CU, one wave per SIMD):
+//  * 4 waves as 2 (M) x 2 (N), each owning (16 MT) x (16 NT) outputs = MT x NT
+//    MFMA tiles of 16x16 (4 MT NT fp32 accumulators per lane, AGPR-pinned),
 //    v_mfma_f32_16x16x32_bf16.
-//  * LDS ring of S K-tile slots (BK = 64; S = 4 for MT = 4, 3 for MT = 8): a
-//    slot is A[32 MT x 64] then B[128 x 64] as 16x32 subtiles (1 KiB = one
-//    MFMA fragment), the same XOR-swizzled image as the 256x256 kernels
-//    (gemm_bf16.hpp), filled by LDS-DMA (global_load_lds_dwordx4, swizzle
-//    applied to the source). P = MT + 4 pieces per wave per K-tile.
+//  * LDS ring of S K-tile slots (BK = 64; S = the most slots that fit the LDS
+//    budget, at least 3): a slot is A[32 MT x 64] then B[32 NT x 64] as 16x32
+//    subtiles (1 KiB = one MFMA fragment), the same XOR-swizzled image as the
+//    256x256 kernels (gemm_bf16.hpp), filled by LDS-DMA
+//    (global_load_lds_dwordx4, swizzle applied to the source). P = MT + NT
+//    pieces per wave per K-tile (4 (MT + NT) per tile, split by global piece index).
 //  * K loop, iteration t (fragments of tile t already in registers):
-//      4 MT MFMAs (k-half 0 of tile t) with tile t+S-1's DMA pieces among
+//      MT NT MFMAs (k-half 0 of tile t) with tile t+S-1's DMA pieces among
 //        them (past the end: dummy pieces that re-read the last tile into a
 //        scratch region nobody reads, so the counted wait below is exact in
 //        every iteration and there is no tail)
 //      s_waitcnt vmcnt((S-2) P) + lgkmcnt(0), s_barrier  -> tile t+1 visible
-//      4 MT MFMAs (k-half 1 of tile t) with the fragment reads of tile t+1
+//      MT NT MFMAs (k-half 1 of tile t) with the fragment reads of tile t+1
 //  RAW: the wait leaves only tiles t+2 .. t+S-1 ((S-2) P pieces) in flight, so
 //       tile t+1 has landed for this wave; the barrier makes it so for all
 //       waves before anyone reads it.
@@ -32,8 +34,8 @@
 //       read in iteration t-2 and retired (lgkmcnt(0)) before barrier t-1,
 //       which the issuing wave has passed.
 //  Drain: vmcnt(0) before the epilogue, so no DMA lands after the WG exits.
-// Shape rule: M % (32 MT), N % 128, K % 128 (an even K-tile count); 16-byte
-// aligned rows.
+// Shape rule: M % (32 MT), N % (32 NT), K % 128 (an even K-tile count);
+// 16-byte aligned rows.
 #pragma once
 
 #include "ntm/gemm_bf16.hpp"
@@ -143,7 +145,7 @@ __device__ __forceinline__ void mfma_acc(f32x4& acc, const bf16x8& b, const bf16
 
 // One K-tile. With one wave per SIMD nothing else hides an instruction that
 // is not an MFMA, so the P DMA pieces are spread evenly over the first half's
-// 4 MT MFMAs and the 2 MT + 8 fragment reads over the second half's (order
+// MT NT MFMAs and the 2 (MT + NT) fragment reads over the second half's (order
 // pinned with sched_barrier; B fragment first in every MFMA so a lane holds 4
 // consecutive output columns of one row for the epilogue's 8-byte stores).
 template <int MT, int NT>

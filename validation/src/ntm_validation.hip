@@ -374,10 +374,11 @@ NTM_API int ntm_stream_read_ex(const void* src, size_t bytes, float* sink,
   }
 }
 
-// Tuned defaults (5.75 TB/s copy, 7.13 TB/s read at 4 GiB on MI355X).
+// Tuned defaults (= ops.kernels.STREAM_COPY_CONFIG / STREAM_READ_CONFIG; copy
+// 5.6-5.8 TB/s, read 7.1 TB/s on two MI355X boxes, profiles/r2_k2/).
 NTM_API int ntm_stream_copy(const void* src, void* dst, size_t bytes,
                             void* stream) {
-  return ntm_stream_copy_ex(src, dst, bytes, 4, 7, 256, stream);
+  return ntm_stream_copy_ex(src, dst, bytes, 8, 7, 512, stream);
 }
 
 NTM_API int ntm_stream_read(const void* src, size_t bytes, float* sink,
