@@ -342,25 +342,41 @@ def main(argv=None) -> int:
                 verified = False
         if not args.no_xgmi and not args.rehearsal and n <= 8:
             # C2 next to RCCL: the same sizes, in place on the registered buffer,
-            # no host sync / barrier / staging per call (device-side barriers)
+            # no host sync / barrier / staging per call (device-side barriers).
+            # Set-up failures (IPC, peer mapping) are agreed on collectively so no
+            # rank is left waiting in a collective the others skipped; the JSON
+            # line still comes out with the error recorded.
             from nvidia_terraform_modules_amd.parallel.xgmi import XgmiAllReduce
 
             xs = [b for b in coll.sweep_sizes(1 << 10, max_b, 4) if b <= 1 << 30]
-            ar = XgmiAllReduce(env, max_bytes=max(xs), nblk=64)
-            xr = coll.all_reduce_sweep(env, xs, dtype="bf16", iters=10, warmup=2, impl=ar)
-            extras["xgmi_allreduce_bf16"] = [
-                {"bytes": r.bytes, "time_us": round(r.time_us, 1),
-                 "busbw_GBps": round(r.busbw_GBps, 1), "errors": r.errors} for r in xr]
-            extras["xgmi_timed_out"] = ar.timed_out()
-            ar.close()
-            if any(r.errors for r in xr) or extras["xgmi_timed_out"]:
+            ar, err = None, ""
+            try:
+                ar = XgmiAllReduce(env, max_bytes=max(xs), nblk=64)
+            except Exception as e:  # noqa: BLE001 - reported, and agreed on below
+                err = f"{type(e).__name__}: {e}"[:300]
+            if dist.all_reduce_max(env, 1.0 if err else 0.0) > 0:
+                extras["xgmi_error"] = err or "set-up failed on another rank"
                 verified = False
+                if ar is not None:
+                    ar.close()
+            else:
+                xr = coll.all_reduce_sweep(env, xs, dtype="bf16", iters=10, warmup=2, impl=ar)
+                extras["xgmi_allreduce_bf16"] = [
+                    {"bytes": r.bytes, "time_us": round(r.time_us, 1),
+                     "busbw_GBps": round(r.busbw_GBps, 1), "errors": r.errors} for r in xr]
+                extras["xgmi_peak_busbw_GBps"] = coll.peak_busbw(xr)
+                extras["xgmi_timed_out"] = dist.all_reduce_max(
+                    env, 1.0 if ar.timed_out() else 0.0) > 0
+                ar.close()
+                if any(r.errors for r in xr) or extras["xgmi_timed_out"]:
+                    verified = False
     _CLOCK.mark("collectives_checked")
 
     if (gpu_extras or args.rehearsal) and not args.no_job:
         # The Kubernetes validation Job's own entrypoint on this node's n GPUs (one
         # process, all GPUs): its process-start -> verdict time is the in-node part
-        # of time-to-GPU-ready. C2 (the hand-written xGMI all-reduce) stays off here.
+        # of time-to-GPU-ready (it runs C1 RCCL, C2 xGMI and the C3 link matrix
+        # when n > 1).
         # Every rank's GPU work is done (barrier); the other ranks then leave, and
         # rank 0 touches no GPU between the child and its print, so whatever the
         # child does, the JSON line still comes out.

@@ -125,33 +125,49 @@ class XgmiAllReduce:
         self.env, self.nblk, self.max_bytes = env, nblk, max_bytes
         self.one_shot_max_bytes = min(one_shot_max_bytes, max_bytes)
         self.L = L = _declare()
-        self._own = []
-        handles = {}
-        for name, nbytes, uncached in (("in", max_bytes, 0), ("out", max_bytes, 0),
-                                       ("sig", L.ntm_xgmi_signal_bytes(nblk), 1)):
-            p = ctypes.c_void_p()
-            check(L.ntm_malloc(ctypes.byref(p), nbytes, uncached), "ntm_malloc")
-            self._own.append(p.value)
-            h = ctypes.create_string_buffer(64)
-            check(L.ntm_ipc_handle(p.value, h), "ntm_ipc_handle")
-            handles[name] = (p.value, h.raw)
-        check(L.ntm_memset_async(handles["sig"][0], 0, L.ntm_xgmi_signal_bytes(nblk), None),
-              "memset")
-        torch.cuda.synchronize()
-        gathered = all_gather_obj(env, {k: v[1] for k, v in handles.items()})
-        self._opened = []
+        self._own, self._opened = [], []
+        # Collective-safe set-up: every rank reaches both all_gathers whatever
+        # fails locally, and all ranks raise together, so no rank is left
+        # waiting in a collective its peers abandoned.
+        handles, err = {}, ""
+        try:
+            for name, nbytes, uncached in (("in", max_bytes, 0), ("out", max_bytes, 0),
+                                           ("sig", L.ntm_xgmi_signal_bytes(nblk), 1)):
+                p = ctypes.c_void_p()
+                check(L.ntm_malloc(ctypes.byref(p), nbytes, uncached), "ntm_malloc")
+                self._own.append(p.value)
+                h = ctypes.create_string_buffer(64)
+                check(L.ntm_ipc_handle(p.value, h), "ntm_ipc_handle")
+                handles[name] = (p.value, h.raw)
+            check(L.ntm_memset_async(handles["sig"][0], 0, L.ntm_xgmi_signal_bytes(nblk), None),
+                  "memset")
+            torch.cuda.synchronize()
+        except Exception as e:  # noqa: BLE001 - re-raised on every rank below
+            err = f"rank {env.rank}: {e}"
+        gathered = all_gather_obj(env, {"err": err, "h": {k: v[1] for k, v in handles.items()}})
+        self._raise_if_any([g["err"] for g in gathered])
         self.ptrs = {"in": [], "out": [], "sig": []}
-        for r, hs in enumerate(gathered):
-            for k in ("in", "out", "sig"):
-                if r == env.rank:
-                    self.ptrs[k].append(handles[k][0])
-                else:
-                    p = ctypes.c_void_p()
-                    check(L.ntm_ipc_open(hs[k], ctypes.byref(p)), "ntm_ipc_open")
-                    self._opened.append(p.value)
-                    self.ptrs[k].append(p.value)
+        try:
+            for r, g in enumerate(gathered):
+                for k in ("in", "out", "sig"):
+                    if r == env.rank:
+                        self.ptrs[k].append(handles[k][0])
+                    else:
+                        p = ctypes.c_void_p()
+                        check(L.ntm_ipc_open(g["h"][k], ctypes.byref(p)), "ntm_ipc_open")
+                        self._opened.append(p.value)
+                        self.ptrs[k].append(p.value)
+        except Exception as e:  # noqa: BLE001
+            err = f"rank {env.rank}: {e}"
+        self._raise_if_any(all_gather_obj(env, err))
         self.epoch = 0
         self.err = torch.zeros(1, dtype=torch.int32, device=env.device)
+
+    def _raise_if_any(self, errs: list) -> None:
+        errs = [e for e in errs if e]
+        if errs:
+            self.close()
+            raise RuntimeError("XgmiAllReduce set-up failed: " + "; ".join(errs))
 
     def buffer(self, numel: int) -> torch.Tensor:
         """bf16 view of the first ``numel`` elements of this rank's registered
