@@ -39,7 +39,7 @@ def _env():
     return e
 
 
-@pytest.mark.parametrize("nproc", [1, 2, 4])
+@pytest.mark.parametrize("nproc", [1, 2, 4, 8])
 def test_torchrun_launch_one_json_line(nproc):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
            f"--nproc-per-node={nproc}", "--master-addr=127.0.0.1", f"--master-port={_port()}",
