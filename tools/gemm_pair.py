@@ -23,7 +23,10 @@ def main() -> int:
     ap.add_argument("--which", default="both", choices=["both", "ours", "torch", "all"])
     ap.add_argument("--variant", default="default")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"])
+    ap.add_argument("--warm-iters", type=int, default=40,
+                    help="untimed pairs first, so most profiled dispatches run on a settled chip")
     args = ap.parse_args()
+    args.iters += args.warm_iters
     s = args.size
     if args.dtype == "fp8":
         return fp8_pair(s, args.iters, args.which)

@@ -29,7 +29,7 @@ from nvidia_terraform_modules_amd import ops  # noqa: E402
 from nvidia_terraform_modules_amd.ops._lib import check, lib_experimental, stream_handle  # noqa: E402
 
 SLOTS = 8
-START, END, RT0, RT1, HWID, XCCID = range(6)
+START, END, RT0, RT1, HWID, XCCID, RL0, RL1 = range(8)
 MODES = {"real": 0, "no_lds": 1, "no_mfma": 2, "mfma_only": 3, "reads_no_dma": 4,
          "dma_no_reads": 5}
 
@@ -113,6 +113,22 @@ def main() -> int:
         "end_spread_us_p90": round(float(torch.tensor(tails).quantile(0.9)) * 10e-3, 3),
         "wg_span_us_median": round(float((rt1 - rt0).median()) * 10e-3, 2),
         "launch_span_us": round(float(rt1.max() - rt0.min()) * 10e-3, 2)}
+    # per-workgroup phase split (wave 0; 10 ns ticks): start -> loop entry (prologue:
+    # address setup + the first LDS-DMA round trip), the K loop, loop end -> done
+    # (drain + LDS-staged epilogue + stores issued). Split by the WG's round on its CU.
+    rl0, rl1 = w0[:, RL0].double(), w0[:, RL1].double()
+    rounds = {}
+    for key in torch.unique(cu_key):
+        idx = (cu_key == key).nonzero().flatten()
+        order = idx[torch.argsort(rt0[idx])]
+        for r, i in enumerate(order.tolist()):
+            rounds.setdefault(r, []).append(i)
+    def med(x):
+        return round(float(x.median()) * 10e-3, 3)
+    out["phase_split_real_us"] = {
+        f"round{r}": {"prologue": med(rl0[ix] - rt0[ix]), "loop": med(rl1[ix] - rl0[ix]),
+                      "epilogue": med(rt1[ix] - rl1[ix]), "n": len(ix)}
+        for r, ix in sorted(rounds.items())}
     xcc = (w0[:, XCCID] & 0xF)
     out["per_xcd_real"] = {
         int(x): {"wg_span_us_mean": round(float((rt1 - rt0)[xcc == x].mean()) * 10e-3, 2),

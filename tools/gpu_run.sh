@@ -13,6 +13,9 @@
 #   bench      bench.py exactly as the driver runs it (--steps 20 --warmup 5)
 #   bench200   bench.py --steps 200 --warmup 20
 #   prof       rocprofv3 --kernel-trace --stats of a short bench
+#   pmc        PMC passes (counters in their own runs, --kernel-trace only) of K1 vs
+#              hipBLASLt at 8192^3 (PMC_DTYPE=fp8: K1-fp8 vs hipBLASLt fp8) +
+#              tools/pmc_summary.py -> <tag>/pmc/summary.json
 #   py:<file>  python -u <file> (a tool script; its own args via PYARGS)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
@@ -59,6 +62,21 @@ for s in "${STEPS[@]}"; do
         -- python3 bench.py --steps 50 --warmup 5 --no-job > "$O/bench_prof.log" 2>&1 \
         || fail prof $? "$O/bench_prof.log"
       find "$O/prof" -name '*kernel_stats.csv' -exec head -12 {} \; ;;
+    pmc)
+      P="$O/pmc"
+      mkdir -p "$P"
+      pair="tools/gemm_pair.py --size 8192 --iters 10 --dtype ${PMC_DTYPE:-bf16}"
+      for pass in "sq1:SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE" \
+                  "sq2:SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_WAIT_INST_LDS" \
+                  "sq3:SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM SQ_LDS_IDX_ACTIVE" \
+                  "tcc:TCC_HIT_sum TCC_MISS_sum" "fetch:FETCH_SIZE" "write:WRITE_SIZE"; do
+        name=${pass%%:*}
+        timeout -s KILL 120 rocprofv3 --pmc ${pass#*:} --kernel-trace --output-format csv \
+          -d "$P/$name" -o run -- python3 $pair > "$P/$name.log" 2>&1 || fail "pmc $name" $? "$P/$name.log"
+      done
+      timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$P/trace" -o run \
+        -- python3 $pair > "$P/trace.log" 2>&1 || fail "pmc trace" $? "$P/trace.log"
+      python3 tools/pmc_summary.py "$P" > "$P/summary.json" && head -c 3000 "$P/summary.json" ;;
     py:*)
       f=${s#py:}
       timeout -k 10 600 python -u "$f" $PYARGS > "$O/$(basename "$f" .py).log" 2>&1 \

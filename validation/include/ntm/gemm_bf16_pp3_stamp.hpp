@@ -33,7 +33,7 @@ using ::ntm::gemm3::kLdsBytes3;
 using ::ntm::gemm3::shape_ok3;
 
 // u64 slots per wave in the stamp buffer
-enum : int { kStart = 0, kEnd, kRtStart, kRtEnd, kHwId, kXccId, kSlots = 8 };
+enum : int { kStart = 0, kEnd, kRtStart, kRtEnd, kHwId, kXccId, kRtLoop0, kRtLoop1, kSlots = 8 };
 
 __device__ __forceinline__ void keep(const bf16x8 (&x)[2][2]) {
 #pragma unroll
@@ -149,12 +149,16 @@ __global__ void __launch_bounds__(kThreads, 2)
     read_b<kBHi>(c, f.b1, 0);
   }
   if (c.wr == 1) raw_barrier();
+  // prologue / K loop / epilogue split (realtime stamps, 100 MHz): two SMEM
+  // returns per workgroup, outside the loop
+  const unsigned long long rl0 = __builtin_amdgcn_s_memrealtime();
 
   for (int t = 0; t < T; t += 2) {
     tile_a<false, MODE>(c, f, acc, t, T);
     tile_a<true, MODE>(c, f, acc, t + 1, T);
   }
   if (c.wr == 0) raw_barrier();
+  const unsigned long long rl1 = __builtin_amdgcn_s_memrealtime();
   wait_vmcnt<0>();
   store_tile_epi<false, kEpiDefault>(p, c, acc, m0, n0, lane);
   const unsigned long long ts1 = __builtin_amdgcn_s_memtime();
@@ -166,6 +170,8 @@ __global__ void __launch_bounds__(kThreads, 2)
     o[kEnd] = ts1;
     o[kRtStart] = rt0;
     o[kRtEnd] = rt1;
+    o[kRtLoop0] = rl0;
+    o[kRtLoop1] = rl1;
     // HW_REG_HW_ID (4) and HW_REG_XCC_ID (20), full 32 bits: which CU ran it
     o[kHwId] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);
     o[kXccId] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20);

@@ -21,6 +21,7 @@
 #include "ntm/gemm_bf16_pp5.hpp"
 #include "ntm/gemm_bf16_w4.hpp"
 #include "ntm/gemm_fp8_diag.hpp"
+#include "ntm/stream_policy_exp.hpp"
 
 #define NTM_API extern "C" __attribute__((visibility("default")))
 
@@ -111,5 +112,23 @@ NTM_API int ntm_mfma_f8_probe(const void* a_stage, const void* b_stage, float* d
   hipLaunchKernelGGL(ntm::fp8::mfma_f8_probe_kernel, dim3(1), dim3(64), 0, S(stream),
                      (const ntm::fp8::i32x8*)a_stage, (const ntm::fp8::i32x8*)b_stage,
                      (ntm::f32x4*)d);
+  return (int)hipGetLastError();
+}
+
+// K2 store-policy sweep (stream_policy_exp.hpp): unroll in {4, 8}, spol 0..5
+// (none / nt / sc1 / sc0 sc1 / nt sc1 / nt sc0 sc1), grid > 0.
+NTM_API int ntm_stream_copy_spol(const void* src, void* dst, size_t bytes, int unroll, int spol,
+                                 int grid, void* stream) {
+  if (bytes % 16 || grid <= 0 || spol < 0 || spol > 5 || (unroll != 4 && unroll != 8))
+    return (int)hipErrorInvalidValue;
+  const auto* a = (const ntm::f32x4*)src;
+  auto* b = (ntm::f32x4*)dst;
+  const size_t n4 = bytes / 16;
+#define NTM_SPOL(U, P) \
+  if (unroll == U && spol == P) \
+    hipLaunchKernelGGL((ntm::k2x::copy_pipe_spol_kernel<U, P>), dim3(grid), dim3(256), 0, S(stream), a, b, n4);
+  NTM_SPOL(4, 0) NTM_SPOL(4, 1) NTM_SPOL(4, 2) NTM_SPOL(4, 3) NTM_SPOL(4, 4) NTM_SPOL(4, 5)
+  NTM_SPOL(8, 0) NTM_SPOL(8, 1) NTM_SPOL(8, 2) NTM_SPOL(8, 3) NTM_SPOL(8, 4) NTM_SPOL(8, 5)
+#undef NTM_SPOL
   return (int)hipGetLastError();
 }
