@@ -7,7 +7,7 @@ terraform {
   required_version = ">= 1.5.0"
   required_providers {
     azapi      = { source = "Azure/azapi", version = ">= 1.4.0, < 2.0.0" }
-    azuread    = { source = "hashicorp/azuread", version = ">= 2.15.0" }
+    azuread    = { source = "hashicorp/azuread", version = ">= 2.15.0, < 4.0.0" }
     azurerm    = { source = "hashicorp/azurerm", version = ">= 3.110.0, < 4.0.0" }
     kubernetes = { source = "hashicorp/kubernetes", version = ">= 2.25.0, < 3.0.0" }
   }

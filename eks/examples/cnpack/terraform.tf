@@ -7,6 +7,6 @@ terraform {
 
   required_providers {
     aws    = { source = "hashicorp/aws", version = ">= 5.79.0, < 6.0.0" }
-    random = { source = "hashicorp/random", version = ">= 3.5.1" }
+    random = { source = "hashicorp/random", version = ">= 3.5.1, < 4.0.0" }
   }
 }

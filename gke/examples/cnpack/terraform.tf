@@ -9,7 +9,7 @@ terraform {
     kubernetes  = { source = "hashicorp/kubernetes", version = ">= 2.25.0, < 3.0.0" }
     google      = { source = "hashicorp/google", version = ">= 5.40.0, < 7.0.0" }
     google-beta = { source = "hashicorp/google-beta", version = ">= 5.40.0, < 7.0.0" }
-    random      = { source = "hashicorp/random", version = ">= 3.5.1" }
+    random      = { source = "hashicorp/random", version = ">= 3.5.1, < 4.0.0" }
   }
 }
 

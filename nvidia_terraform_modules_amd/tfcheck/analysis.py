@@ -17,6 +17,20 @@ module-required    required variable of a local callee not passed
 module-output      module.X.Y where Y is not an output of local callee X
 unknown-function   call to a function Terraform does not have
 vendor-lint        NVIDIA/CUDA-specific strings in literals (AMD-only build)
+local-exec         a local-exec provisioner: runs on the operator's workstation, only on create,
+                   outside Terraform state (reference: az/kubelogin/helm, aks/main.tf:52-91)
+secret-in-command  a local-exec command interpolating a key/secret/password/token attribute:
+                   the value lands in the process list and logs (reference:
+                   aks/examples/cnpack/azure-fluentbit.tf:28)
+iam-authoritative  an authoritative IAM binding/policy that strips every other member of the
+                   role (reference: gke/examples/cnpack/gcp-prometheus.tf:33)
+duplicate-resource two attachment/member/assignment resources with identical arguments - the
+                   second is a copy-paste that left its intended target unattached (reference:
+                   eks/examples/cnpack/aws-fluentbit.tf:22-25)
+count-object-length count = length(data.X.Y) > 0 counts the data source's ATTRIBUTES, so the
+                   gate is always open (reference: eks/main.tf:186)
+provider-unbounded a provider version constraint with no upper bound (a major release can
+                   change the schema under an unchanged configuration)
 gpu-toleration     a pod spec (or operator component) placed on the GPU nodes through
                    the GPU node selector does not tolerate the GPU node taint, so it
                    would never schedule and `apply` would wait out validation_timeout
@@ -301,6 +315,7 @@ def analyze(mod: Module, *, strict_unused: bool = True, vendor_lint: bool = True
     if vendor_lint:
         out.extend(vendor_findings(mod))
     out.extend(toleration_findings(mod))
+    out.extend(practice_findings(mod))
     if check_fmt:
         out.extend(fmt_findings(mod.path))
     return out
@@ -401,6 +416,83 @@ def toleration_findings(mod: Module) -> list[Finding]:
                     out.append(Finding("gpu-toleration", "error", f"{f}:{line}",
                                        f"local.{name}: component {comp!r} runs on the GPU "
                                        f"nodes without local.{GPU_TOLERATIONS}"))
+    return out
+
+
+SECRET_WORDS = re.compile(r"(key|secret|password|passwd|token|credential)", re.I)
+AUTHORITATIVE_IAM = {"google_project_iam_binding", "google_project_iam_policy",
+                     "google_folder_iam_binding", "google_folder_iam_policy",
+                     "google_organization_iam_binding", "google_organization_iam_policy"}
+DUP_TYPES = re.compile(r"(attachment|iam_member|role_assignment)$")
+CLUSTER_CLIS = re.compile(r"\b(kubectl|helm|kubelogin|az\s+aks|aws\s+eks|gcloud\s+container)\b")
+
+
+def _provisioners(body: Body):
+    for b in body.blocks:
+        if b.type == "provisioner":
+            yield b
+        else:
+            yield from _provisioners(b.body)
+
+
+def _bounded(constraint: str) -> bool:
+    parts = [p.strip() for p in constraint.split(",") if p.strip()]
+    return any(p.startswith(("<", "~>")) or p[0].isdigit() or p.startswith("=") and
+               not p.startswith("=>") for p in parts)
+
+
+def practice_findings(mod: Module) -> list[Finding]:
+    """Deployment-practice rules (each one a defect the reference shipped)."""
+    from .docs import render
+
+    out = []
+    seen_args: dict = {}
+    for r in mod.managed:
+        where = f"{r.file}:{r.block.line}"
+        for pb in _provisioners(r.block.body):
+            if not pb.labels or pb.labels[0] != "local-exec":
+                continue
+            cmd = pb.body.attr("command")
+            text = " ".join(iter_strings(cmd)) if cmd is not None else ""
+            what = ("runs cluster CLIs (kubeconfig side effects) " if CLUSTER_CLIS.search(text)
+                    else "")
+            out.append(Finding("local-exec", "warning", where,
+                               f"{r.address}: local-exec provisioner {what}- create-time only, "
+                               "outside state; use a provider resource"))
+            if cmd is not None:
+                for ref, _ in walk_refs(cmd):
+                    last = (ref.path() or [ref.root])[-1]
+                    if SECRET_WORDS.search(last):
+                        out.append(Finding("secret-in-command", "error", where,
+                                           f"{r.address}: command line carries {ref.root}."
+                                           f"{'.'.join(ref.path())}"))
+        if r.type in AUTHORITATIVE_IAM:
+            out.append(Finding("iam-authoritative", "warning", where,
+                               f"{r.address}: authoritative IAM {r.type} removes every other "
+                               "member of the role; use the *_iam_member form"))
+        if DUP_TYPES.search(r.type):
+            attrs = {k: render(a.expr) for k, a in r.block.body.attributes.items()
+                     if k not in ("count", "for_each", "depends_on", "provider")}
+            key = (r.type, tuple(sorted(attrs.items())))
+            if key in seen_args:
+                out.append(Finding("duplicate-resource", "error", where,
+                                   f"{r.address}: same arguments as {seen_args[key]}"))
+            else:
+                seen_args[key] = r.address
+        cnt = r.block.body.attr("count")
+        if cnt is not None:
+            for call in iter_calls(cnt):
+                if call.name == "length" and len(call.args) == 1 and \
+                        isinstance(call.args[0], Traversal) and call.args[0].root == "data" and \
+                        len(call.args[0].path()) == 2:
+                    out.append(Finding("count-object-length", "warning", where,
+                                       f"{r.address}: length() of data.{'.'.join(call.args[0].path())}"
+                                       " counts its attributes - the gate is always open"))
+    for name, spec in mod.required_providers.items():
+        v = spec.get("version") if isinstance(spec, dict) else None
+        if v and not _bounded(v):
+            out.append(Finding("provider-unbounded", "warning", "terraform",
+                               f"provider {name!r} constraint {v!r} has no upper bound"))
     return out
 
 

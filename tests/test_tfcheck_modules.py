@@ -51,6 +51,19 @@ def test_checker_finds_the_reference_defects():
     aks = analyze(load_module(REF / "aks"))
     assert {f.message for f in aks if f.rule == "unused-variable"} == {
         "variable 'cpu_os_sku' is never used", "variable 'gpu_os_sku' is never used"}
+    # deployment-practice rules (SURVEY §2.4-2.5 / §5 race hazards), each a shipped defect:
+    # az aks get-credentials + kubelogin + helm via local-exec (aks/main.tf:52-91)
+    assert sum(f.rule == "local-exec" for f in aks) == 4
+    # the always-open helm gate count = length(data.aws_instances.nodes) > 0 (eks/main.tf:186)
+    assert any(r == "count-object-length" and "aws_instances.nodes" in m for r, m in eks)
+    eks_cn = analyze(load_module(REF / "eks/examples/cnpack"))
+    dup = [f for f in eks_cn if f.rule == "duplicate-resource"]   # aws-fluentbit.tf:22-25
+    assert len(dup) == 1 and "attach-cloudwatch-to-cpu-ng" in dup[0].message
+    gke_cn = analyze(load_module(REF / "gke/examples/cnpack"))
+    assert any(f.rule == "iam-authoritative" for f in gke_cn)     # gcp-prometheus.tf:33
+    aks_cn = analyze(load_module(REF / "aks/examples/cnpack"))
+    sec = [f for f in aks_cn if f.rule == "secret-in-command"]     # azure-fluentbit.tf:28
+    assert len(sec) == 1 and "primary_shared_key" in sec[0].message
 
 
 def test_no_vendor_strings_anywhere(repo):
