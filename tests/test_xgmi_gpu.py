@@ -106,3 +106,40 @@ def test_ipc_allreduce_two_processes():
         for r in rep["results"]:
             assert not r["timeout"], rep
             assert r["wrong"] == 0, rep
+
+
+@pytest.mark.parametrize("nranks", [2, 8])
+def test_simulated_allreduce_stress_back_to_back(nranks):
+    """Race screen for the device-side barrier protocol: 120 calls back to back
+    on ONE stream with no host sync between them, reusing the signal buffers
+    with growing epochs, alternating one-shot / two-shot / in-place and
+    changing the data every call. Exact integer patterns (every partial sum of
+    <= 8 ranks is exact in bf16), every element of every call checked."""
+    from nvidia_terraform_modules_amd.parallel.xgmi import _declare, _ptrs, MAX_RANKS  # noqa: F401
+    from nvidia_terraform_modules_amd.ops._lib import check, stream_handle
+
+    L = _declare()
+    nblk = 1024 // nranks // 4
+    count = 8 * nranks * 2048 + 8 * nranks * 5
+    sb = L.ntm_xgmi_signal_bytes(nblk)
+    sigs = [torch.zeros(sb // 4, dtype=torch.int32, device="cuda") for _ in range(nranks)]
+    err = torch.zeros(1, dtype=torch.int32, device="cuda")
+    base = (2.0 ** (torch.arange(count, device="cuda") % 4))
+    outs_keep, exps = [], []
+    for it in range(120):
+        one_shot, inplace = it % 3 == 0, it % 3 == 2
+        ins = [(base * ((r + it) % 5 + 1)).to(torch.bfloat16) for r in range(nranks)]
+        outs = ins if inplace else [torch.empty_like(t) for t in ins]
+        rc = L.ntm_xgmi_allreduce_bf16(
+            _ptrs([t.data_ptr() for t in ins]), _ptrs([t.data_ptr() for t in outs]),
+            _ptrs([s.data_ptr() for s in sigs]), nranks, 0, nranks, nblk, count, it + 1,
+            err.data_ptr(), 1 if one_shot else 0, stream_handle())
+        check(rc, "xgmi")
+        outs_keep.append(outs)
+        exps.append(base * sum((r + it) % 5 + 1 for r in range(nranks)))
+    torch.cuda.synchronize()
+    assert int(err.item()) == 0
+    for it, (outs, exp) in enumerate(zip(outs_keep, exps)):
+        e = exp.to(torch.bfloat16)
+        for o in outs:
+            assert torch.equal(o, e), f"call {it}"
