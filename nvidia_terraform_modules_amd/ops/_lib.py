@@ -84,6 +84,7 @@ def _declare_experimental(lib: ctypes.CDLL) -> None:
         "ntm_experimental_version": ([], ctypes.c_char_p),
         "ntm_gemm_bf16_experimental": (gemm, c_int),
         "ntm_gemm_bf16_knob": (gemm, c_int),
+        "ntm_gemm_bf16_ws_knob": ([c_int] + gemm, c_int),
         "ntm_gemm_bf16_stamp": (
             [c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp], c_int),
         "ntm_mfma_f8_probe": ([c_vp, c_vp, c_vp, c_vp], c_int),

@@ -34,7 +34,8 @@ GEMM_VARIANTS = {"default": 0, "pingpong8": 1, "wave128": 2, "wave128d4": 3, "pi
                  "pingpong8c": 5, "pingpong8p": 6, "pingpong8w": 7, "pingpong8wi": 8,
                  "pingpong8ww": 9, "pingpong8cw": 10, "pingpong8cwe": 11,
                  "pingpong8cwn": 12, "pingpong8cwne": 13, "pingpong8pw": 14, "tile128": 15,
-                 "tile256x128": 16, "tile160": 17, "tile256x160": 18}
+                 "tile256x128": 16, "tile160": 17, "tile256x160": 18, "tile128ws": 19,
+                 "tile256x128ws": 20, "tile160ws": 21}
 
 
 # variants built only into libntm_experimental.so (tests / tools): never selected
@@ -42,11 +43,12 @@ GEMM_VARIANTS = {"default": 0, "pingpong8": 1, "wave128": 2, "wave128d4": 3, "pi
 EXPERIMENTAL_VARIANTS = frozenset({"pingpong8", "wave128", "wave128d4", "pingpong8p",
                                    "pingpong8w", "pingpong8wi", "pingpong8ww", "pingpong8cw",
                                    "pingpong8cwe", "pingpong8cwn", "pingpong8cwne",
-                                   "pingpong8pw"})
+                                   "pingpong8pw", "tile128ws", "tile256x128ws", "tile160ws"})
 
 # (TM, TN) of the 4-wave tile kernels (gemm_bf16_t128.hpp)
 TILE_SHAPES = {"tile128": (128, 128), "tile256x128": (256, 128), "tile160": (160, 160),
-               "tile256x160": (256, 160)}
+               "tile256x160": (256, 160), "tile128ws": (128, 128), "tile256x128ws": (256, 128),
+               "tile160ws": (160, 160)}
 
 
 def _tile128_shape_ok(m: int, n: int, k: int, tm: int = 128, tn: int = 128) -> bool:

@@ -266,5 +266,163 @@ inline hipError_t launch_gemm_bf16_tile(const GemmArgs& a, hipStream_t stream) {
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// Wave-specialised tile kernels ("tile128ws" / "tile256x128ws" / "tile160ws").
+//
+// Why: with one wave per SIMD the kernel above exposes the issue cost of every
+// LDS-DMA piece (~60 cycles among bare MFMAs, MI355X_MICROARCH.md constants
+// table) - at 256x128 that is 12 pieces against 64 16-cycle MFMAs per K-tile,
+// about the 25-40 % gap to the 256x256 ping-pong kernel. Here a workgroup is
+// 8 waves, two per SIMD: waves 0-3 ("consumers") own the same output blocks
+// and issue ONLY ds_read_b128 + MFMA; waves 4-7 ("producers") issue ONLY the
+// LDS-DMA pieces (the same pieces, the same LDS image), so a piece's issue
+// cost lands on a wave that has nothing else to do while its SIMD partner
+// keeps the matrix core busy.
+//
+// Registers: two waves per SIMD leave 256 per lane, so the consumers keep ONE
+// fragment set (MT + NT) x 2 k-halves and refill each half as soon as its
+// MFMAs are issued:
+//   K-tile t, first half : MT NT MFMAs on k-half 0 of tile t; reads of
+//                          k-half 1 of tile t (visible since barrier t).
+//   lgkmcnt(0), barrier t+1
+//   second half          : MT NT MFMAs on k-half 1 of tile t; reads of
+//                          k-half 0 of tile t+1 (visible since barrier t+1).
+// A register is refilled only after a barrier separates it from the MFMA
+// that last read it. Producers, per K-tile: issue tile t+S-1's P pieces
+// (dummies into scratch past the end, as above), s_waitcnt vmcnt((S-2) P),
+// barrier t+1. Both roles pass T+1 barriers.
+//   RAW: a producer arrives at barrier t+1 only once its pieces of tile t+1
+//        landed; consumers read tile t+1 only after that barrier.
+//   WAR: tile t+S-1 overwrites the slot of tile t-1, whose last reads (k-half 1,
+//        first half of iteration t-1) every consumer retired (lgkmcnt(0))
+//        before barrier t, which the producer has passed.
+//   Drain: producers vmcnt(0) before exit; MFMA order per accumulator is the
+//        kernel above's, so results are bitwise equal to it.
+// Same shape rule as the kernel above.
+template <int MT, int NT>
+struct CfgWS {
+  static_assert(4 * MT * NT + 8 * (MT + NT) <= 232, "256 registers per lane at 2 waves / SIMD");
+};
+
+// Schedule knobs of the wave-specialised kernel (bitmask; 0 = as described):
+//   kWsBFirst   read each k-half's B fragments before its A fragments: the
+//               first MT NT / MT MFMAs need all NT B fragments but only A[0]
+//   kWsEarly    issue the first half's reads within its first MT NT - 8 MFMAs,
+//               so the lgkmcnt(0) before the barrier finds them landed
+//   kWsPrio     consumers run at s_setprio 1 (MFMA issue wins over DMA issue)
+constexpr int kWsBFirst = 1, kWsEarly = 2, kWsPrio = 4;
+
+template <int MT, int NT, int KNOB>
+__device__ __forceinline__ void read_half(const CtxT& c, FragsT<MT, NT>& f, int kt, int ks, int i) {
+  const int r = (KNOB & kWsBFirst) ? (i < NT ? MT + i : i - NT) : i;
+  read_frag<MT, NT>(c, f, kt, ks * (MT + NT) + r);
+}
+
+template <int MT, int NT = 4, int KNOB = 0>
+__global__ void __launch_bounds__(2 * kThreadsT, 1) gemm_bf16_tile_ws_kernel(GemmArgs p) {
+  using C = Cfg<MT, NT>;
+  (void)sizeof(CfgWS<MT, NT>);
+  __shared__ __attribute__((aligned(16))) char smem[C::kLds];
+  int tm, tn;
+  tile_coords_t<MT, NT>(p.M, p.N, tm, tn);
+  const int m0 = tm * C::TM, n0 = tn * C::TN;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int T = p.K / TK;
+
+  CtxT c;
+  c.lds = smem;
+  c.w = wave & 3;  // producer: whose pieces; consumer: whose output block
+  c.wr = c.w >> 1;
+  c.wc = c.w & 1;
+  {
+    const int r = lane >> 2;
+    const int cl = (lane & 3) ^ (((r >> 3) & 1) << 1);
+    c.a_src = p.A + (size_t)(m0 + r) * p.lda + cl * 8;
+    c.b_src = p.B + (size_t)(n0 + r) * p.ldb + cl * 8;
+    c.a_rb16 = (size_t)16 * p.lda;
+    c.b_rb16 = (size_t)16 * p.ldb;
+  }
+  c.frag_off = (lane & 15) * 64 + ((lane >> 4) ^ ((lane >> 2) & 2)) * 16;
+
+  if (wave >= 4) {  // producer
+#pragma unroll
+    for (int s = 0; s < C::S - 1; ++s)
+#pragma unroll
+      for (int i = 0; i < C::P; ++i) issue_piece<MT, NT>(c, s, T, i);
+    wait_vmcnt_n<C::VMC>();  // tile 0 landed
+    raw_barrier();
+    for (int t = 0; t < T; ++t) {
+#pragma unroll
+      for (int i = 0; i < C::P; ++i) issue_piece<MT, NT>(c, t + C::S - 1, T, i);
+      wait_vmcnt_n<C::VMC>();  // tile t+1 landed
+      raw_barrier();
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // dummy pieces drained
+    return;
+  }
+
+  // consumer
+  if constexpr (KNOB & kWsPrio) __builtin_amdgcn_s_setprio(1);
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  FragsT<MT, NT> f;
+  raw_barrier();  // tile 0 visible
+#pragma unroll
+  for (int i = 0; i < MT + NT; ++i) read_half<MT, NT, KNOB>(c, f, 0, 0, i);
+
+  constexpr int NM = MT * NT, NR = MT + NT;
+  constexpr int NE = (KNOB & kWsEarly) && NM - 8 >= NR ? NM - 8 : NM;  // first-half read span
+  for (int t = 0; t < T; ++t) {
+#pragma unroll
+    for (int j = 0; j < NM; ++j) {
+      mfma_acc(acc[j / NT][j % NT], f.b[j % NT][0], f.a[j / NT][0]);
+      if (j < NE && (j * NR) / NE != ((j + 1) * NR) / NE)
+        read_half<MT, NT, KNOB>(c, f, t, 1, (j * NR) / NE);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    raw_barrier();  // tile t+1 visible; every read of tile t retired
+#pragma unroll
+    for (int j = 0; j < NM; ++j) {
+      mfma_acc(acc[j / NT][j % NT], f.b[j % NT][1], f.a[j / NT][1]);
+      if ((j * NR) / NM != ((j + 1) * NR) / NM)
+        read_half<MT, NT, KNOB>(c, f, t + 1, 0, (j * NR) / NM);  // t + 1 == T: stale, unused
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+
+  ::ntm::gemm::mfma_drain();
+  typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const int row = m0 + c.wr * (16 * MT) + mt * 16 + (lane & 15);
+      const int col = n0 + c.wc * (16 * NT) + nt * 16 + (lane >> 4) * 4;
+      const f32x4 v = acc[mt][nt];
+      bf16x4 o;
+      o[0] = (__bf16)v[0];
+      o[1] = (__bf16)v[1];
+      o[2] = (__bf16)v[2];
+      o[3] = (__bf16)v[3];
+      *(bf16x4*)(p.C + (size_t)row * p.ldc + col) = o;
+    }
+}
+
+template <int MT, int NT = 4, int KNOB = 0>
+inline hipError_t launch_gemm_bf16_tile_ws(const GemmArgs& a, hipStream_t stream) {
+  if (!shape_ok_t<MT, NT>(a.M, a.N, a.K) || a.lda < a.K || a.ldb < a.K || a.ldc < a.N ||
+      (a.lda % 8) || (a.ldb % 8) || (a.ldc % 4))
+    return hipErrorInvalidValue;
+  const unsigned grid = (unsigned)((a.M / Cfg<MT, NT>::TM) * (a.N / Cfg<MT, NT>::TN));
+  hipLaunchKernelGGL((gemm_bf16_tile_ws_kernel<MT, NT, KNOB>), dim3(grid), dim3(2 * kThreadsT), 0,
+                     stream, a);
+  return hipGetLastError();
+}
+
 }  // namespace gemmt
 }  // namespace ntm

@@ -12,6 +12,8 @@
 //   7..9   pingpong8w / wi / ww: 32-MFMA segment schedules (gemm_bf16_pp5.hpp)
 //   10..13 pingpong8c epilogue knobs: widened / + early row-0 stores /
 //          nontemporal stores / both (gemm_bf16_pp3.hpp launch_gemm_bf16_pp3_knob)
+//   19..21 tile128ws / tile256x128ws / tile160ws: the tile kernels with
+//          producer (LDS-DMA) and consumer (MFMA) waves (gemm_bf16_t128.hpp)
 // Measured: none beats the shipping default (profiles/r1_pp3, r1_pp4, r1_pp3_knobs,
 // r1_pmc2_w4); kept as the record of what was tried and as ablation baselines.
 #include "ntm/gemm_bf16.hpp"
@@ -19,6 +21,7 @@
 #include "ntm/gemm_bf16_pp3_stamp.hpp"
 #include "ntm/gemm_bf16_pp4.hpp"
 #include "ntm/gemm_bf16_pp5.hpp"
+#include "ntm/gemm_bf16_t128.hpp"
 #include "ntm/gemm_bf16_w4.hpp"
 #include "ntm/gemm_fp8_diag.hpp"
 #include "ntm/stream_policy_exp.hpp"
@@ -66,6 +69,9 @@ NTM_API int ntm_gemm_bf16_experimental(int variant, const void* A, const void* B
     case 11:
     case 12:
     case 13: return (int)ntm::gemm3::launch_gemm_bf16_pp3_knob(a, variant + 2, S(stream));
+    case 19: return (int)ntm::gemmt::launch_gemm_bf16_tile_ws<4>(a, S(stream));
+    case 20: return (int)ntm::gemmt::launch_gemm_bf16_tile_ws<8>(a, S(stream));
+    case 21: return (int)ntm::gemmt::launch_gemm_bf16_tile_ws<5, 5>(a, S(stream));
     default: return (int)hipErrorInvalidValue;
   }
 }
@@ -97,6 +103,35 @@ NTM_API int ntm_mfma_rate(int f8, int grid, int iters, void* out, float* sink, v
     hipLaunchKernelGGL(ntm::fp8::mfma_rate_kernel<false>, dim3(grid), dim3(256), 0, S(stream),
                        iters, 7u, (unsigned long long*)out, sink);
   return (int)hipGetLastError();
+}
+
+// Wave-specialised tile kernel schedule knobs (gemm_bf16_t128.hpp kWs*):
+// shape 0 = 128x128, 1 = 256x128, 2 = 160x160; knob 0..7.
+template <int MT, int NT>
+static hipError_t ws_knob(const ntm::gemm::GemmArgs& a, int knob, hipStream_t s) {
+  using namespace ntm::gemmt;
+  switch (knob) {
+    case 0: return launch_gemm_bf16_tile_ws<MT, NT, 0>(a, s);
+    case 1: return launch_gemm_bf16_tile_ws<MT, NT, 1>(a, s);
+    case 2: return launch_gemm_bf16_tile_ws<MT, NT, 2>(a, s);
+    case 3: return launch_gemm_bf16_tile_ws<MT, NT, 3>(a, s);
+    case 4: return launch_gemm_bf16_tile_ws<MT, NT, 4>(a, s);
+    case 5: return launch_gemm_bf16_tile_ws<MT, NT, 5>(a, s);
+    case 6: return launch_gemm_bf16_tile_ws<MT, NT, 6>(a, s);
+    case 7: return launch_gemm_bf16_tile_ws<MT, NT, 7>(a, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+NTM_API int ntm_gemm_bf16_ws_knob(int shape, int knob, const void* A, const void* B, void* C,
+                                  int M, int N, int K, int lda, int ldb, int ldc, void* stream) {
+  const ntm::gemm::GemmArgs a = args(A, B, C, M, N, K, lda, ldb, ldc);
+  switch (shape) {
+    case 0: return (int)ws_knob<4, 4>(a, knob, S(stream));
+    case 1: return (int)ws_knob<8, 4>(a, knob, S(stream));
+    case 2: return (int)ws_knob<5, 5>(a, knob, S(stream));
+    default: return (int)hipErrorInvalidValue;
+  }
 }
 
 // K1-fp8 schedule knobs (gemm_fp8_diag.hpp launch_gemm_fp8_knob).
