@@ -34,8 +34,8 @@ GEMM_VARIANTS = {"default": 0, "pingpong8": 1, "wave128": 2, "wave128d4": 3, "pi
                  "pingpong8c": 5, "pingpong8p": 6, "pingpong8w": 7, "pingpong8wi": 8,
                  "pingpong8ww": 9, "pingpong8cw": 10, "pingpong8cwe": 11,
                  "pingpong8cwn": 12, "pingpong8cwne": 13, "pingpong8pw": 14, "tile128": 15,
-                 "tile256x128": 16, "tile160": 17, "tile256x160": 18, "tile128ws": 19,
-                 "tile256x128ws": 20, "tile160ws": 21}
+                 "tile256x128": 16, "tile160": 17, "tile256x160": 18, "tile128w4": 19,
+                 "tile256x128w4": 20, "tile160w4": 21}
 
 
 # variants built only into libntm_experimental.so (tests / tools): never selected
@@ -43,12 +43,12 @@ GEMM_VARIANTS = {"default": 0, "pingpong8": 1, "wave128": 2, "wave128d4": 3, "pi
 EXPERIMENTAL_VARIANTS = frozenset({"pingpong8", "wave128", "wave128d4", "pingpong8p",
                                    "pingpong8w", "pingpong8wi", "pingpong8ww", "pingpong8cw",
                                    "pingpong8cwe", "pingpong8cwn", "pingpong8cwne",
-                                   "pingpong8pw", "tile128ws", "tile256x128ws", "tile160ws"})
+                                   "pingpong8pw", "tile128w4", "tile256x128w4", "tile160w4"})
 
 # (TM, TN) of the 4-wave tile kernels (gemm_bf16_t128.hpp)
 TILE_SHAPES = {"tile128": (128, 128), "tile256x128": (256, 128), "tile160": (160, 160),
-               "tile256x160": (256, 160), "tile128ws": (128, 128), "tile256x128ws": (256, 128),
-               "tile160ws": (160, 160)}
+               "tile256x160": (256, 160), "tile128w4": (128, 128), "tile256x128w4": (256, 128),
+               "tile160w4": (160, 160)}
 
 
 def _tile128_shape_ok(m: int, n: int, k: int, tm: int = 128, tn: int = 128) -> bool:
@@ -75,7 +75,8 @@ def gemm_bf16(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
     ``variant``: "default" = the tile shape with the smallest predicted time
     (rounds of 256 CUs x tile area / efficiency, ``k1_plan``): "tile128" /
     "tile256x128" / "tile160" / "tile256x160" (128x128 / 256x128 / 160x160 /
-    256x160 tiles, 4 waves, K % 128) for small and mid-size C,
+    256x160 tiles, K % 128; the first three with 4 LDS-DMA producer + 4 MFMA
+    consumer waves, 256x160 with 4 waves) for small and mid-size C,
     else "pingpong8c" when K % 128 == 0, else "pingpong8b" (8 waves, two per SIMD, staggered, balanced 8/4/8/4 LDS read
     schedule; 8c adds parity-alternating B buffers and a tail-free K loop -
     fastest measured), "pingpong8" (the first 12/4/8/0 schedule), or the

@@ -210,7 +210,7 @@ def test_gemm_variants_vs_torch_fp32(ops, variant, m, n, k):
     assert torch.equal(c, ops.gemm_bf16(a, b, variant="pingpong8"))  # same math, same order
 
 
-@pytest.mark.parametrize("variant", ["tile128", "tile256x128", "tile128ws", "tile256x128ws"])
+@pytest.mark.parametrize("variant", ["tile128", "tile256x128", "tile128w4", "tile256x128w4"])
 @pytest.mark.parametrize("m,n,k", [(128, 128, 128), (384, 640, 256), (1280, 896, 512),
                                    (256, 256, 1024), (2048, 2048, 2048), (3072, 1024, 384),
                                    (512, 384, 128)])
@@ -230,11 +230,11 @@ def test_gemm_tile128_vs_torch_fp32(ops, variant, m, n, k):
     assert torch.all(err <= atol + rtol * ref.abs()), float(err.max())
     if m % 256 == 0 and n % 256 == 0:
         assert torch.equal(c, ops.gemm_bf16(a, b, variant="pingpong8"))
-    if variant.endswith("ws"):  # producer/consumer waves: same MFMA order as the 4-wave kernel
+    if variant.endswith("w4"):  # 4-wave kernel: same MFMA order as the wave-specialised one
         assert torch.equal(c, ops.gemm_bf16(a, b, variant=variant[:-2]))
 
 
-@pytest.mark.parametrize("variant", ["tile160", "tile256x160", "tile160ws"])
+@pytest.mark.parametrize("variant", ["tile160", "tile256x160", "tile160w4"])
 @pytest.mark.parametrize("m,n,k", [(160, 160, 128), (1280, 800, 384), (2560, 2560, 2560),
                                    (1280, 160, 1024), (2560, 1600, 256), (5120, 320, 128)])
 def test_gemm_tile160_vs_torch_fp32(ops, variant, m, n, k):

@@ -1,7 +1,7 @@
 """Schedule-knob sweep of the wave-specialised tile kernels (developer tool;
 gemm_bf16_t128.hpp kWsBFirst / kWsEarly / kWsPrio): every knob is checked
 bitwise against knob 0 (same MFMA order), then timed in interleaved rounds
-next to the 4-wave tile kernel and hipBLASLt (torch.matmul) after a clock
+next to the 4-wave tile kernel (tile*w4) and hipBLASLt (torch.matmul) after a clock
 settle; one JSON line per (shape, tile).
 
     python tools/ws_knobs.py --shapes 8192x8192x8192 --tiles 1 [--knobs 0,1,2,3]
@@ -17,7 +17,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from nvidia_terraform_modules_amd import ops  # noqa: E402
 from nvidia_terraform_modules_amd.ops._lib import check, lib_experimental, stream_handle  # noqa: E402
 
-TILES = {0: ("tile128", 128, 128), 1: ("tile256x128", 256, 128), 2: ("tile160", 160, 160)}
+TILES = {0: ("tile128w4", 128, 128), 1: ("tile256x128w4", 256, 128), 2: ("tile160w4", 160, 160)}
 
 
 def timed(fn, iters):

@@ -12,8 +12,9 @@
 //   7..9   pingpong8w / wi / ww: 32-MFMA segment schedules (gemm_bf16_pp5.hpp)
 //   10..13 pingpong8c epilogue knobs: widened / + early row-0 stores /
 //          nontemporal stores / both (gemm_bf16_pp3.hpp launch_gemm_bf16_pp3_knob)
-//   19..21 tile128ws / tile256x128ws / tile160ws: the tile kernels with
-//          producer (LDS-DMA) and consumer (MFMA) waves (gemm_bf16_t128.hpp)
+//   19..21 tile128w4 / tile256x128w4 / tile160w4: the 4-wave (one wave per
+//          SIMD) tile kernels that the wave-specialised ones replaced as
+//          variants 15..17 (gemm_bf16_t128.hpp; profiles/r2_ws)
 // Measured: none beats the shipping default (profiles/r1_pp3, r1_pp4, r1_pp3_knobs,
 // r1_pmc2_w4); kept as the record of what was tried and as ablation baselines.
 #include "ntm/gemm_bf16.hpp"
@@ -69,9 +70,9 @@ NTM_API int ntm_gemm_bf16_experimental(int variant, const void* A, const void* B
     case 11:
     case 12:
     case 13: return (int)ntm::gemm3::launch_gemm_bf16_pp3_knob(a, variant + 2, S(stream));
-    case 19: return (int)ntm::gemmt::launch_gemm_bf16_tile_ws<4>(a, S(stream));
-    case 20: return (int)ntm::gemmt::launch_gemm_bf16_tile_ws<8>(a, S(stream));
-    case 21: return (int)ntm::gemmt::launch_gemm_bf16_tile_ws<5, 5>(a, S(stream));
+    case 19: return (int)ntm::gemmt::launch_gemm_bf16_tile<4>(a, S(stream));
+    case 20: return (int)ntm::gemmt::launch_gemm_bf16_tile<8>(a, S(stream));
+    case 21: return (int)ntm::gemmt::launch_gemm_bf16_tile<5, 5>(a, S(stream));
     default: return (int)hipErrorInvalidValue;
   }
 }

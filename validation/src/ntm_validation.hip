@@ -39,7 +39,9 @@ NTM_API int ntm_gemm_shape_ok(int M, int N, int K) {
 // 64); 5 = pingpong8c, the same schedule with parity-alternating B buffers, a
 // uniform tail-free K loop and the LDS-staged nontemporal epilogue
 // (gemm_bf16_pp3.hpp; K % 128); 15 / 16 / 17 / 18 = 128x128 / 256x128 /
-// 160x160 / 256x160 tiles, 4 waves (gemm_bf16_t128.hpp; K % 128).
+// 160x160 / 256x160 tiles (gemm_bf16_t128.hpp; K % 128): the first three on
+// the wave-specialised 8-wave kernel, 256x160 on the 4-wave one (its
+// accumulators + one fragment set do not fit 256 registers).
 // 0 = default: the plan below. Variants 1-3 and 6-14 (the first ping-pong,
 // the 4-wave 128x128-per-wave kernel, the persistent kernel, the 32-MFMA
 // segment schedules, epilogue knobs) are experimental: libntm_experimental.so.
@@ -54,27 +56,27 @@ constexpr int kDefaultVariant = 5;
 
 // Tile-shape plan of the default dispatch: the smallest predicted time
 // rounds(tiles) x tile_area / efficiency over 256 CUs, where the efficiencies
-// are each kernel's full-chip rate at 8192^3 relative to the 256x256 kernel
-// (profiles/r1_t128/policy_interleaved.log: 1634 / 1219 / 957 TF/s). The plan
+// are each kernel's full-chip rate relative to the 256x256 kernel. The plan
 // may split C by rows: the top rows on the 256x256 kernel in whole rounds, the
 // rest in a second launch on a small tile, so a partial last round of big
 // tiles becomes a full round of small ones (6144^3: 3 rounds of 256x256 ->
-// 2 rounds + one of 256x128). Alone it picks 128x128 at 2048^3 (858 vs 467
-// TF/s for 256x256; hipBLASLt 773), 160x160 at 2560^3 (958 vs 755; hipBLASLt
-// 934: 256 tiles = one full round), 256x128 at 4096x2048x4096 (1107 vs 950)
-// and 256x256 at 3072^3, 4096^3 and 8192^3.
+// 2 rounds + one of 256x128). Alone it picks 128x128 at 2048^3, 160x160 at
+// 2560^3 and 3200^3, 256x128 at 2816^3 and 4096x2048x4096, and 256x256 at
+// 3072^3, 4096^3 and 8192^3.
+// Efficiencies (round 2, wave-specialised 128x128 / 256x128 / 160x160):
+// 0.60 / 0.78 at 8192^3 (989 / 1306 vs 1654 TF/s, profiles/r2_ws/policy_ws1.log,
+// interleaved in one process); 160x160 at its full-chip rate at 5120^3 (4 full
+// rounds). 256x160 (4-wave) is priced from a full round of it against one of
+// 256x256 at 4096x2560x4096 (1121 vs 1146 TF/s, r1_t160/policy_plan.log), not
+// from its 8192x5120 rate (0.72): at 0.72 the plan split 5120^3 and
+// 8192x5120x4096 onto it and lost 2-3 %.
 constexpr double kCUs = 256.0;
-// 160-wide tiles: 160x160 at its full-chip rate (1109 TF/s at 5120^3, 4 full
-// rounds, relative to 1634; profiles/r1_t160/policy.log). 256x160 is priced
-// from a full round of it against one of 256x256 at 4096x2560x4096 (1121 vs
-// 1146 TF/s, r1_t160/policy_plan.log), not from its 8192x5120 rate (0.72):
-// at 0.72 the plan split 5120^3 and 8192x5120x4096 onto it and lost 2-3 %.
 struct SmallTile {
   int variant, tm, tn;
   double eff;
 };
 constexpr SmallTile kSmallTiles[] = {
-    {15, 128, 128, 0.59}, {16, 256, 128, 0.75}, {17, 160, 160, 0.68}, {18, 256, 160, 0.61}};
+    {15, 128, 128, 0.60}, {16, 256, 128, 0.78}, {17, 160, 160, 0.72}, {18, 256, 160, 0.61}};
 constexpr double kSplitPenalty = 0.25;  // a second launch, in 128x128-tile-round units
 
 struct K1Plan {
@@ -157,10 +159,11 @@ NTM_API int ntm_gemm_bf16_variant(int variant, const void* A, const void* B,
   switch (variant) {
     case 4: return (int)ntm::gemm2::launch_gemm_bf16_pp2(a, S(stream));
     case 5: return (int)ntm::gemm3::launch_gemm_bf16_pp3(a, S(stream));
-    // gemm_bf16_t128.hpp: 128x128 / 256x128 / 160x160 / 256x160 tiles
-    case 15: return (int)ntm::gemmt::launch_gemm_bf16_tile<4>(a, S(stream));
-    case 16: return (int)ntm::gemmt::launch_gemm_bf16_tile<8>(a, S(stream));
-    case 17: return (int)ntm::gemmt::launch_gemm_bf16_tile<5, 5>(a, S(stream));
+    // gemm_bf16_t128.hpp: 128x128 / 256x128 / 160x160 tiles on the wave-specialised
+    // kernel (4 DMA-producer + 4 MFMA-consumer waves), 256x160 on the 4-wave one
+    case 15: return (int)ntm::gemmt::launch_gemm_bf16_tile_ws<4>(a, S(stream));
+    case 16: return (int)ntm::gemmt::launch_gemm_bf16_tile_ws<8>(a, S(stream));
+    case 17: return (int)ntm::gemmt::launch_gemm_bf16_tile_ws<5, 5>(a, S(stream));
     case 18: return (int)ntm::gemmt::launch_gemm_bf16_tile<8, 5>(a, S(stream));
     default: return (int)hipErrorInvalidValue;  // experimental variants: libntm_experimental.so
   }
