@@ -287,8 +287,10 @@ inline hipError_t launch_gemm_bf16_tile(const GemmArgs& a, hipStream_t stream) {
 //   lgkmcnt(0), barrier t+1
 //   second half          : MT NT MFMAs on k-half 1 of tile t; reads of
 //                          k-half 0 of tile t+1 (visible since barrier t+1).
-// A register is refilled only after a barrier separates it from the MFMA
-// that last read it. Producers, per K-tile: issue tile t+S-1's P pieces
+// A k-half-0 register is refilled only after the barrier that follows its last
+// MFMA; a k-half-1 register at least 5 MFMAs (>= 80 cycles) after its last
+// MFMA (the previous iteration's second half), long after the MFMA read its
+// sources at issue. Producers, per K-tile: issue tile t+S-1's P pieces
 // (dummies into scratch past the end, as above), s_waitcnt vmcnt((S-2) P),
 // barrier t+1. Both roles pass T+1 barriers.
 //   RAW: a producer arrives at barrier t+1 only once its pieces of tile t+1
