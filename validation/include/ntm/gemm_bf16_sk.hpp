@@ -79,6 +79,27 @@ __device__ __forceinline__ void tile_mn(int tile, int M, int N, int& tm, int& tn
   tn = in_group / gsz;
 }
 
+// LDS-DMA piece `piece` of logical K-step i (ring slot i % S) of a segment of
+// n K-steps whose step i reads K-tile (k0 + i) mod T; i >= n: a dummy piece
+// (re-reads the segment's last K-tile into this wave's scratch).
+template <int MT, int NT>
+__device__ __forceinline__ void issue_piece_rot(const CtxT& c, int i, int n, int k0, int T,
+                                                int piece) {
+  using C = Cfg<MT, NT>;
+  const bool real = i < n;
+  int kt = k0 + (real ? i : n - 1);
+  if (kt >= T) kt -= T;
+  const bool is_a = piece < MT;
+  const int g = is_a ? c.w * MT + piece : c.w * NT + (piece - MT);
+  const int rb = g >> 1, kh = g & 1;
+  const size_t koff = (size_t)kt * TK + kh * 32;
+  char* slot = c.lds + (i % C::S) * C::kSlot;
+  const __bf16* src = (is_a ? c.a_src + rb * c.a_rb16 : c.b_src + rb * c.b_rb16) + koff;
+  char* dst = real ? slot + (is_a ? 0 : C::kA) + (rb * 2 + kh) * 1024
+                   : c.lds + C::kScratch + c.w * 1024;
+  glds16(src, dst);
+}
+
 // C store of one consumer wave's block, optionally adding a tail partial
 // (the accumulators are only read: a VALU write would move them to VGPRs).
 template <int MT, int NT, bool ADD>
@@ -129,27 +150,37 @@ __global__ void __launch_bounds__(2 * kThreadsT, 1) gemm_bf16_tile_sk_kernel(SkA
   const int r = lane >> 2;
   const int cl = (lane & 3) ^ (((r >> 3) & 1) << 1);
 
-  for (long long u = u0; u < u1;) {
+  long long u = u0;
+  int tau = 0;  // K-steps this workgroup has run so far (its clock)
+  while (u < u1) {
     const int tile = (int)(u / T);
-    const int kb = (int)(u - (long long)tile * T);
-    const int ke = (int)min((long long)T, (long long)kb + (u1 - u));
-    u += ke - kb;
+    const int pos = (int)(u - (long long)tile * T);
+    const int n = (int)min((long long)(T - pos), u1 - u);
+    // first segment (range starts mid-tile): K-tiles [0, n), partial published;
+    // last segment (range ends mid-tile): K-tiles [T-n, T), partial of the next
+    // workgroup added; full tile: all T K-tiles rotated to start at tau mod T,
+    // so every workgroup reads K-tile (clock mod T) at the same time.
+    const bool publish = pos > 0;
+    const bool fixup = !publish && n < T;
+    const int k0 = publish ? 0 : fixup ? T - n : tau % T;
+    u += n;
+    tau += n;
     int tm, tn;
     tile_mn<MT, NT>(tile, p.M, p.N, tm, tn);
     const int m0 = tm * C::TM, n0 = tn * C::TN;
     c.a_src = p.A + (size_t)(m0 + r) * p.lda + cl * 8;
     c.b_src = p.B + (size_t)(n0 + r) * p.ldb + cl * 8;
 
-    if (wave >= 4) {  // producer: the tile kernel's pipeline on [kb, ke)
+    if (wave >= 4) {  // producer: the tile kernel's pipeline over the n K-steps
 #pragma unroll
       for (int st = 0; st < C::S - 1; ++st)
 #pragma unroll
-        for (int i = 0; i < C::P; ++i) issue_piece<MT, NT>(c, kb + st, ke, i);
+        for (int i = 0; i < C::P; ++i) issue_piece_rot<MT, NT>(c, st, n, k0, T, i);
       wait_vmcnt_n<C::VMC>();
       raw_barrier();
-      for (int t = kb; t < ke; ++t) {
+      for (int t = 0; t < n; ++t) {
 #pragma unroll
-        for (int i = 0; i < C::P; ++i) issue_piece<MT, NT>(c, t + C::S - 1, ke, i);
+        for (int i = 0; i < C::P; ++i) issue_piece_rot<MT, NT>(c, t + C::S - 1, n, k0, T, i);
         wait_vmcnt_n<C::VMC>();
         raw_barrier();
       }
@@ -162,26 +193,27 @@ __global__ void __launch_bounds__(2 * kThreadsT, 1) gemm_bf16_tile_sk_kernel(SkA
 #pragma unroll
     for (int i = 0; i < MT; ++i)
 #pragma unroll
-      for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int jj = 0; jj < NT; ++jj) acc[i][jj] = f32x4{0.f, 0.f, 0.f, 0.f};
     FragsT<MT, NT> f;
-    raw_barrier();  // tile kb visible
+    raw_barrier();  // step 0 visible
 #pragma unroll
-    for (int i = 0; i < MT + NT; ++i) read_half<MT, NT, 0>(c, f, kb, 0, i);
+    for (int i = 0; i < MT + NT; ++i) read_half<MT, NT, 0>(c, f, 0, 0, i);
     constexpr int NM = MT * NT, NR = MT + NT;
-    for (int t = kb; t < ke; ++t) {
+    for (int t = 0; t < n; ++t) {
 #pragma unroll
-      for (int j = 0; j < NM; ++j) {
-        mfma_acc(acc[j / NT][j % NT], f.b[j % NT][0], f.a[j / NT][0]);
-        if ((j * NR) / NM != ((j + 1) * NR) / NM) read_half<MT, NT, 0>(c, f, t, 1, (j * NR) / NM);
+      for (int jj = 0; jj < NM; ++jj) {
+        mfma_acc(acc[jj / NT][jj % NT], f.b[jj % NT][0], f.a[jj / NT][0]);
+        if ((jj * NR) / NM != ((jj + 1) * NR) / NM)
+          read_half<MT, NT, 0>(c, f, t, 1, (jj * NR) / NM);
         __builtin_amdgcn_sched_barrier(0);
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       raw_barrier();
 #pragma unroll
-      for (int j = 0; j < NM; ++j) {
-        mfma_acc(acc[j / NT][j % NT], f.b[j % NT][1], f.a[j / NT][1]);
-        if ((j * NR) / NM != ((j + 1) * NR) / NM)
-          read_half<MT, NT, 0>(c, f, t + 1, 0, (j * NR) / NM);  // t + 1 == ke: stale, unused
+      for (int jj = 0; jj < NM; ++jj) {
+        mfma_acc(acc[jj / NT][jj % NT], f.b[jj % NT][1], f.a[jj / NT][1]);
+        if ((jj * NR) / NM != ((jj + 1) * NR) / NM)
+          read_half<MT, NT, 0>(c, f, t + 1, 0, (jj * NR) / NM);  // t + 1 == n: stale, unused
         __builtin_amdgcn_sched_barrier(0);
       }
     }
@@ -195,8 +227,8 @@ __global__ void __launch_bounds__(2 * kThreadsT, 1) gemm_bf16_tile_sk_kernel(SkA
     asm volatile("v_mov_b32 %0, 0" : "=v"(vz));
     const int ln = lane + vz;
 
-    if (kb > 0 && (s.diag & 2)) continue;
-    if (kb > 0) {  // tail: publish this wave's partial in slot blockIdx
+    if (publish && (s.diag & 2)) continue;
+    if (publish) {  // first segment: publish this wave's partial in slot blockIdx
       f32x4* dst = s.part + (size_t)(bid * 4 + c.w) * NM * 64;  // uniform base
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
@@ -211,7 +243,7 @@ __global__ void __launch_bounds__(2 * kThreadsT, 1) gemm_bf16_tile_sk_kernel(SkA
                            __HIP_MEMORY_SCOPE_AGENT);
       continue;
     }
-    if (ke < T) {  // head: add the tail partial of workgroup j+1 on this XCD (same wave)
+    if (fixup) {  // last segment: add the partial of workgroup j+1 on this XCD (same wave)
       const unsigned* fl = &s.flags[(bid + 8) * 4 + c.w];
       unsigned spins = (s.diag & 1) ? kSkSpinLimit : 0;
       while ((int)(__hip_atomic_load(fl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - s.epoch) <
