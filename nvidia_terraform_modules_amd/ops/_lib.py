@@ -85,8 +85,6 @@ def _declare_experimental(lib: ctypes.CDLL) -> None:
         "ntm_gemm_bf16_experimental": (gemm, c_int),
         "ntm_gemm_bf16_knob": (gemm, c_int),
         "ntm_gemm_bf16_ws_knob": ([c_int] + gemm, c_int),
-        "ntm_gemm_bf16_sk_bytes": ([c_int, c_int, c_int], ctypes.c_size_t),
-        "ntm_gemm_bf16_sk": (gemm[:-1] + [c_vp, c_vp, ctypes.c_uint, c_int, c_int, c_vp], c_int),
         "ntm_gemm_bf16_stamp": (
             [c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp], c_int),
         "ntm_mfma_f8_probe": ([c_vp, c_vp, c_vp, c_vp], c_int),

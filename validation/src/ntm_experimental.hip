@@ -22,7 +22,6 @@
 #include "ntm/gemm_bf16_pp3_stamp.hpp"
 #include "ntm/gemm_bf16_pp4.hpp"
 #include "ntm/gemm_bf16_pp5.hpp"
-#include "ntm/gemm_bf16_sk.hpp"
 #include "ntm/gemm_bf16_t128.hpp"
 #include "ntm/gemm_bf16_w4.hpp"
 #include "ntm/gemm_fp8_diag.hpp"
@@ -132,33 +131,6 @@ NTM_API int ntm_gemm_bf16_ws_knob(int shape, int knob, const void* A, const void
     case 0: return (int)ws_knob<4, 4>(a, knob, S(stream));
     case 1: return (int)ws_knob<8, 4>(a, knob, S(stream));
     case 2: return (int)ws_knob<5, 5>(a, knob, S(stream));
-    default: return (int)hipErrorInvalidValue;
-  }
-}
-
-// Stream-K tile kernels (gemm_bf16_sk.hpp): shape 0 = 128x128, 1 = 256x128,
-// 2 = 160x160; part / flags: workspace of ntm_gemm_bf16_sk_bytes (flags zeroed
-// once, epoch grows by one per launch); grid % 8 == 0; diag = 0 (timing
-// diagnostics only: bit 0 skips the wait, bit 1 the partial store).
-NTM_API size_t ntm_gemm_bf16_sk_bytes(int shape, int grid, int flags) {
-  if (flags) return ntm::gemmsk::sk_flag_bytes(grid);
-  switch (shape) {
-    case 0: return ntm::gemmsk::sk_part_bytes<4, 4>(grid);
-    case 1: return ntm::gemmsk::sk_part_bytes<8, 4>(grid);
-    case 2: return ntm::gemmsk::sk_part_bytes<5, 5>(grid);
-    default: return 0;
-  }
-}
-
-NTM_API int ntm_gemm_bf16_sk(int shape, const void* A, const void* B, void* C, int M, int N, int K,
-                             int lda, int ldb, int ldc, void* part, void* flags, unsigned epoch,
-                             int grid, int diag, void* stream) {
-  const ntm::gemm::GemmArgs a = args(A, B, C, M, N, K, lda, ldb, ldc);
-  using namespace ntm::gemmsk;
-  switch (shape) {
-    case 0: return (int)launch_gemm_bf16_tile_sk<4, 4>(a, part, flags, epoch, grid, S(stream), diag);
-    case 1: return (int)launch_gemm_bf16_tile_sk<8, 4>(a, part, flags, epoch, grid, S(stream), diag);
-    case 2: return (int)launch_gemm_bf16_tile_sk<5, 5>(a, part, flags, epoch, grid, S(stream), diag);
     default: return (int)hipErrorInvalidValue;
   }
 }
