@@ -31,6 +31,10 @@ count-object-length count = length(data.X.Y) > 0 counts the data source's ATTRIB
                    gate is always open (reference: eks/main.tf:186)
 provider-unbounded a provider version constraint with no upper bound (a major release can
                    change the schema under an unchanged configuration)
+namespace-order    a namespaced kubernetes_* / helm_release resource in a module that creates
+                   its namespace neither takes the namespace name from that resource (directly
+                   or through locals) nor depends_on it, so Terraform may create it first and
+                   the API server rejects it ("namespaces ... not found")
 gpu-toleration     a pod spec (or operator component) placed on the GPU nodes through
                    the GPU node selector does not tolerate the GPU node taint, so it
                    would never schedule and `apply` would wait out validation_timeout
@@ -43,8 +47,8 @@ from dataclasses import dataclass
 from pathlib import Path
 
 from .config import Module, load_module, provider_of_type
-from .hcl import (Block, Body, Call, ObjectExpr, Traversal, iter_calls, iter_strings, key_name,
-                  walk_refs)
+from .hcl import (Block, Body, Call, Literal, ObjectExpr, Template, Traversal, iter_calls,
+                  iter_strings, key_name, walk_refs)
 
 BUILTIN_ROOTS = {"path", "terraform"}
 
@@ -316,6 +320,7 @@ def analyze(mod: Module, *, strict_unused: bool = True, vendor_lint: bool = True
         out.extend(vendor_findings(mod))
     out.extend(toleration_findings(mod))
     out.extend(practice_findings(mod))
+    out.extend(namespace_findings(mod))
     if check_fmt:
         out.extend(fmt_findings(mod.path))
     return out
@@ -493,6 +498,68 @@ def practice_findings(mod: Module) -> list[Finding]:
         if v and not _bounded(v):
             out.append(Finding("provider-unbounded", "warning", "terraform",
                                f"provider {name!r} constraint {v!r} has no upper bound"))
+    return out
+
+
+NAMESPACE_TYPES = {"kubernetes_namespace", "kubernetes_namespace_v1"}
+# cluster-scoped kinds: no namespace to wait for
+CLUSTER_SCOPED = re.compile(r"^kubernetes_(namespace|cluster_role|cluster_role_binding|"
+                            r"storage_class|priority_class|persistent_volume|"
+                            r"(validating|mutating)_webhook_configuration|"
+                            r"custom_resource_definition|csi_driver|runtime_class)(_v1)?$")
+
+
+def _namespace_expr(r):
+    """The namespace expression of a namespaced resource, or None."""
+    if r.type == "helm_release":
+        return r.block.body.attr("namespace")
+    if r.type.startswith("kubernetes_") and not CLUSTER_SCOPED.match(r.type):
+        for b in r.block.body.blocks:
+            if b.type == "metadata":
+                return b.body.attr("namespace")
+    return None
+
+
+def _reaches_namespace(expr, mod: Module, seen: set) -> bool:
+    """expr references a namespace resource, directly or through locals."""
+    for ref, _ in walk_refs(expr):
+        if ref.root in NAMESPACE_TYPES:
+            return True
+        if ref.root == "local" and ref.path():
+            name = ref.path()[0]
+            if name in seen or name not in mod.locals:
+                continue
+            seen.add(name)
+            if _reaches_namespace(mod.locals[name][0], mod, seen):
+                return True
+    return False
+
+
+def namespace_findings(mod: Module) -> list[Finding]:
+    """namespace-order: every namespaced resource must be ordered after the
+    namespace resource the module creates (implicit reference or depends_on)."""
+    if not any(r.type in NAMESPACE_TYPES for r in mod.managed):
+        return []
+    out = []
+    for r in mod.managed:
+        ns = _namespace_expr(r)
+        if ns is None:
+            continue
+        cn = r.block.body.attr("create_namespace") if r.type == "helm_release" else None
+        if isinstance(cn, Literal) and cn.value is True:
+            continue  # Helm creates it
+        if isinstance(ns, Template) and ns.literal() in ("default", "kube-system"):
+            continue
+        if isinstance(ns, Literal) and ns.value in ("default", "kube-system"):
+            continue
+        if _reaches_namespace(ns, mod, set()):
+            continue
+        dep = r.block.body.attr("depends_on")
+        if dep is not None and any(ref.root in NAMESPACE_TYPES for ref, _ in walk_refs(dep)):
+            continue
+        out.append(Finding("namespace-order", "error", f"{r.file}:{r.block.line}",
+                           f"{r.address}: namespace is not taken from (nor depends_on) the "
+                           "namespace resource this module creates"))
     return out
 
 

@@ -287,3 +287,78 @@ def test_examples_use_root_module_outputs_that_exist(repo):
     for ex in ("eks/examples/cnpack", "gke/examples/cnpack", "aks/examples/cnpack"):
         fs = [f for f in analyze(load_module(repo / ex)) if f.rule.startswith("module-")]
         assert not fs, fs
+
+
+def test_namespace_order_rule(tmp_path):
+    """namespace-order: a namespaced resource in a module that creates its
+    namespace must take the name from that resource (here through a local) or
+    depend on it; Helm-created and built-in namespaces are exempt."""
+    (tmp_path / "main.tf").write_text('''terraform {
+  required_providers {
+    kubernetes = { source = "hashicorp/kubernetes" }
+    helm       = { source = "hashicorp/helm" }
+  }
+}
+variable "ns" {
+  default = "gpu"
+}
+resource "kubernetes_namespace_v1" "ns" {
+  metadata {
+    name = var.ns
+  }
+}
+locals {
+  namespace = kubernetes_namespace_v1.ns.metadata[0].name
+}
+resource "kubernetes_config_map_v1" "ok_local" {
+  metadata {
+    name      = "a"
+    namespace = local.namespace
+  }
+}
+resource "kubernetes_config_map_v1" "ok_depends" {
+  metadata {
+    name      = "b"
+    namespace = var.ns
+  }
+  depends_on = [kubernetes_namespace_v1.ns]
+}
+resource "kubernetes_config_map_v1" "ok_system" {
+  metadata {
+    name      = "c"
+    namespace = "kube-system"
+  }
+}
+resource "kubernetes_config_map_v1" "racy" {
+  metadata {
+    name      = "d"
+    namespace = var.ns
+  }
+}
+resource "helm_release" "racy_chart" {
+  name      = "x"
+  chart     = "x"
+  namespace = var.ns
+}
+resource "helm_release" "helm_creates" {
+  name             = "y"
+  chart            = "y"
+  namespace        = var.ns
+  create_namespace = true
+}
+resource "kubernetes_cluster_role_v1" "cluster_scoped" {
+  metadata {
+    name = "r"
+  }
+}
+''')
+    fs = [f for f in analyze(load_module(tmp_path)) if f.rule == "namespace-order"]
+    assert sorted(f.message.split(":")[0] for f in fs) == [
+        "helm_release.racy_chart", "kubernetes_config_map_v1.racy"]
+
+
+@pytest.mark.parametrize("root", ["modules/amd-gpu-stack", "eks", "gke", "aks"])
+def test_modules_order_namespaced_resources(repo, root):
+    mod = load_module(repo / root)
+    assert any(r.type == "kubernetes_namespace_v1" for r in mod.managed) or root != "modules/amd-gpu-stack"
+    assert [f for f in analyze(mod) if f.rule == "namespace-order"] == []
