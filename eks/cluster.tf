@@ -192,7 +192,9 @@ module "cpu_node_pool" {
   min_size       = var.min_cpu_nodes
   max_size       = var.max_cpu_nodes
   desired_size   = var.desired_count_cpu_nodes
-  post_bootstrap_user_data = join("\n", compact([
+  # EKS-optimized AMI: the module merges only a pre-bootstrap hook into its
+  # user data (post_bootstrap_user_data would be silently dropped).
+  pre_bootstrap_user_data = join("\n", compact([
     var.additional_user_data, var.cpu_node_pool_additional_user_data,
   ]))
 

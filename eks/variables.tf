@@ -220,7 +220,7 @@ variable "cpu_node_pool_delete_on_termination" {
 }
 
 variable "cpu_node_pool_additional_user_data" {
-  description = "Shell run on system nodes after the EKS bootstrap."
+  description = "Shell run on system nodes before the EKS bootstrap (EKS-optimized AMIs run only a pre-bootstrap hook)."
   type        = string
   default     = ""
 }
@@ -228,7 +228,7 @@ variable "cpu_node_pool_additional_user_data" {
 # --- 5 node bootstrap ------------------------------------------------------
 
 variable "additional_user_data" {
-  description = "Shell run on every node, before the pool-specific snippets."
+  description = "Shell run on every node, before the pool-specific snippets (MI355X nodes: after the EKS bootstrap; system nodes: before it)."
   type        = string
   default     = ""
 }

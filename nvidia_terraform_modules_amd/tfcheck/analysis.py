@@ -31,6 +31,11 @@ count-object-length count = length(data.X.Y) > 0 counts the data source's ATTRIB
                    gate is always open (reference: eks/main.tf:186)
 provider-unbounded a provider version constraint with no upper bound (a major release can
                    change the schema under an unchanged configuration)
+eks-ignored-input  an EKS managed-node-group input the upstream module silently ignores:
+                   `ssh_key` (v18+ reads key_name / remote_access; reference eks/main.tf:109,
+                   :118) or post_bootstrap_user_data on a group without a custom AMI and
+                   enable_bootstrap_user_data = true (EKS-optimized AMIs run only the
+                   pre-bootstrap hook)
 namespace-order    a namespaced kubernetes_* / helm_release resource in a module that creates
                    its namespace neither takes the namespace name from that resource (directly
                    or through locals) nor depends_on it, so Terraform may create it first and
@@ -321,6 +326,7 @@ def analyze(mod: Module, *, strict_unused: bool = True, vendor_lint: bool = True
     out.extend(toleration_findings(mod))
     out.extend(practice_findings(mod))
     out.extend(namespace_findings(mod))
+    out.extend(eks_node_group_findings(mod))
     if check_fmt:
         out.extend(fmt_findings(mod.path))
     return out
@@ -498,6 +504,48 @@ def practice_findings(mod: Module) -> list[Finding]:
         if v and not _bounded(v):
             out.append(Finding("provider-unbounded", "warning", "terraform",
                                f"provider {name!r} constraint {v!r} has no upper bound"))
+    return out
+
+
+EKS_MODULE = "terraform-aws-modules/eks/aws"
+EKS_NG_IGNORED = {"ssh_key": "the module reads key_name (or remote_access)"}
+
+
+def _true(expr) -> bool:
+    return isinstance(expr, Literal) and expr.value is True
+
+
+def _node_group_inputs(mod: Module):
+    """(where, label, get) for every EKS managed node group: entries of module
+    "eks"'s eks_managed_node_groups map, and eks-managed-node-group submodule
+    calls (their own arguments)."""
+    for mc in mod.modules.values():
+        src = mc.source
+        where = f"{mc.file}:{mc.block.line}"
+        if src == EKS_MODULE:
+            groups = mc.block.body.attr("eks_managed_node_groups")
+            if isinstance(groups, ObjectExpr):
+                for k, v in groups.items:
+                    if isinstance(v, ObjectExpr):
+                        yield where, f"module.{mc.name} node group {key_name(k)!r}", v.get
+        elif src.startswith(EKS_MODULE + "//modules/eks-managed-node-group"):
+            yield where, f"module.{mc.name}", mc.block.body.attr
+
+
+def eks_node_group_findings(mod: Module) -> list[Finding]:
+    """eks-ignored-input: node-group inputs the upstream module never reads."""
+    out = []
+    for where, label, get in _node_group_inputs(mod):
+        for key, why in EKS_NG_IGNORED.items():
+            if get(key) is not None:
+                out.append(Finding("eks-ignored-input", "error", where,
+                                   f"{label}: {key} is ignored - {why}"))
+        if get("post_bootstrap_user_data") is not None and not (
+                _true(get("enable_bootstrap_user_data")) and get("ami_id") is not None):
+            out.append(Finding("eks-ignored-input", "error", where,
+                               f"{label}: post_bootstrap_user_data is ignored without a custom "
+                               "ami_id and enable_bootstrap_user_data = true - use "
+                               "pre_bootstrap_user_data"))
     return out
 
 

@@ -56,6 +56,9 @@ def test_checker_finds_the_reference_defects():
     assert sum(f.rule == "local-exec" for f in aks) == 4
     # the always-open helm gate count = length(data.aws_instances.nodes) > 0 (eks/main.tf:186)
     assert any(r == "count-object-length" and "aws_instances.nodes" in m for r, m in eks)
+    # ssh_key in both node groups is not an input of the eks module (eks/main.tf:109, :118)
+    ign = sorted(m for r, m in eks if r == "eks-ignored-input")
+    assert len(ign) == 2 and all("ssh_key is ignored" in m for m in ign)
     eks_cn = analyze(load_module(REF / "eks/examples/cnpack"))
     dup = [f for f in eks_cn if f.rule == "duplicate-resource"]   # aws-fluentbit.tf:22-25
     assert len(dup) == 1 and "attach-cloudwatch-to-cpu-ng" in dup[0].message
@@ -362,3 +365,25 @@ def test_modules_order_namespaced_resources(repo, root):
     mod = load_module(repo / root)
     assert any(r.type == "kubernetes_namespace_v1" for r in mod.managed) or root != "modules/amd-gpu-stack"
     assert [f for f in analyze(mod) if f.rule == "namespace-order"] == []
+
+
+def test_eks_ignored_input_rule(tmp_path):
+    """eks-ignored-input on the node-group submodule: post_bootstrap_user_data
+    needs a custom AMI + enable_bootstrap_user_data; pre_bootstrap is fine."""
+    (tmp_path / "main.tf").write_text('''module "custom" {
+  source                     = "terraform-aws-modules/eks/aws//modules/eks-managed-node-group"
+  ami_id                     = "ami-1"
+  enable_bootstrap_user_data = true
+  post_bootstrap_user_data   = "echo ok"
+}
+module "optimized_pre" {
+  source                  = "terraform-aws-modules/eks/aws//modules/eks-managed-node-group"
+  pre_bootstrap_user_data = "echo ok"
+}
+module "optimized_post" {
+  source                   = "terraform-aws-modules/eks/aws//modules/eks-managed-node-group"
+  post_bootstrap_user_data = "echo dropped"
+}
+''')
+    fs = [f for f in analyze(load_module(tmp_path)) if f.rule == "eks-ignored-input"]
+    assert len(fs) == 1 and "module.optimized_post" in fs[0].message
