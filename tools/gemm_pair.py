@@ -2,6 +2,7 @@
 random operands - a profiling target for rocprofv3 (developer tool).
 
     rocprofv3 --pmc SQ_WAVE_CYCLES ... -- python3 tools/gemm_pair.py --size 8192 --iters 20
+    (--variant A --versus B: two K1 variants instead of K1 vs hipBLASLt)
 """
 from __future__ import annotations
 
@@ -22,6 +23,8 @@ def main() -> int:
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--which", default="both", choices=["both", "ours", "torch", "all"])
     ap.add_argument("--variant", default="default")
+    ap.add_argument("--versus", default="",
+                    help="a second K1 variant to run in place of torch.matmul (e.g. tile256x128w4)")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"])
     ap.add_argument("--warm-iters", type=int, default=40,
                     help="untimed pairs first, so most profiled dispatches run on a settled chip")
@@ -41,7 +44,10 @@ def main() -> int:
         if args.which == "all":
             ops.gemm_bf16(a, b, c, variant="pingpong8")
         if args.which in ("both", "torch", "all"):
-            torch.matmul(a, b.T, out=c)
+            if args.versus:
+                ops.gemm_bf16(a, b, c, variant=args.versus)
+            else:
+                torch.matmul(a, b.T, out=c)
     torch.cuda.synchronize()
     return 0
 

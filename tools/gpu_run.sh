@@ -14,7 +14,8 @@
 #   bench200   bench.py --steps 200 --warmup 20
 #   prof       rocprofv3 --kernel-trace --stats of a short bench
 #   pmc        PMC passes (counters in their own runs, --kernel-trace only) of K1 vs
-#              hipBLASLt at 8192^3 (PMC_DTYPE=fp8: K1-fp8 vs hipBLASLt fp8) +
+#              hipBLASLt at 8192^3 (PMC_DTYPE=fp8: K1-fp8 vs hipBLASLt fp8; PMC_ARGS: extra
+#              tools/gemm_pair.py arguments, e.g. "--variant A --versus B") +
 #              tools/pmc_summary.py -> <tag>/pmc/summary.json
 #   py:<file>  python -u <file> (a tool script; its own args via PYARGS)
 set -o pipefail
@@ -65,7 +66,7 @@ for s in "${STEPS[@]}"; do
     pmc)
       P="$O/pmc"
       mkdir -p "$P"
-      pair="tools/gemm_pair.py --size 8192 --iters 10 --dtype ${PMC_DTYPE:-bf16}"
+      pair="tools/gemm_pair.py --size 8192 --iters 10 --dtype ${PMC_DTYPE:-bf16} ${PMC_ARGS:-}"
       for pass in "sq1:SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE" \
                   "sq2:SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_WAIT_INST_LDS" \
                   "sq3:SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM SQ_LDS_IDX_ACTIVE" \
