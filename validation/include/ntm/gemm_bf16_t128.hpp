@@ -312,7 +312,9 @@ struct CfgWS {
 //   kWsEarly    issue the first half's reads within its first MT NT - 8 MFMAs,
 //               so the lgkmcnt(0) before the barrier finds them landed
 //   kWsPrio     consumers run at s_setprio 1 (MFMA issue wins over DMA issue)
-constexpr int kWsBFirst = 1, kWsEarly = 2, kWsPrio = 4;
+//   kWsShallow  diagnostic: producers look one K-tile less ahead (S-2 tiles in
+//               flight instead of S-1) - measures what prefetch depth is worth
+constexpr int kWsBFirst = 1, kWsEarly = 2, kWsPrio = 4, kWsShallow = 8;
 
 template <int MT, int NT, int KNOB>
 __device__ __forceinline__ void read_half(const CtxT& c, FragsT<MT, NT>& f, int kt, int ks, int i) {
@@ -348,16 +350,18 @@ __global__ void __launch_bounds__(2 * kThreadsT, 1) gemm_bf16_tile_ws_kernel(Gem
   c.frag_off = (lane & 15) * 64 + ((lane >> 4) ^ ((lane >> 2) & 2)) * 16;
 
   if (wave >= 4) {  // producer
+    constexpr int LA = (KNOB & kWsShallow) ? C::S - 2 : C::S - 1;  // tiles issued ahead
+    constexpr int VM = (LA - 1) * C::P;
 #pragma unroll
-    for (int s = 0; s < C::S - 1; ++s)
+    for (int s = 0; s < LA; ++s)
 #pragma unroll
       for (int i = 0; i < C::P; ++i) issue_piece<MT, NT>(c, s, T, i);
-    wait_vmcnt_n<C::VMC>();  // tile 0 landed
+    wait_vmcnt_n<VM>();  // tile 0 landed
     raw_barrier();
     for (int t = 0; t < T; ++t) {
 #pragma unroll
-      for (int i = 0; i < C::P; ++i) issue_piece<MT, NT>(c, t + C::S - 1, T, i);
-      wait_vmcnt_n<C::VMC>();  // tile t+1 landed
+      for (int i = 0; i < C::P; ++i) issue_piece<MT, NT>(c, t + LA, T, i);
+      wait_vmcnt_n<VM>();  // tile t+1 landed
       raw_barrier();
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // dummy pieces drained

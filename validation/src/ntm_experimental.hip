@@ -107,7 +107,7 @@ NTM_API int ntm_mfma_rate(int f8, int grid, int iters, void* out, float* sink, v
 }
 
 // Wave-specialised tile kernel schedule knobs (gemm_bf16_t128.hpp kWs*):
-// shape 0 = 128x128, 1 = 256x128, 2 = 160x160; knob 0..7.
+// shape 0 = 128x128, 1 = 256x128, 2 = 160x160; knob 0..8.
 template <int MT, int NT>
 static hipError_t ws_knob(const ntm::gemm::GemmArgs& a, int knob, hipStream_t s) {
   using namespace ntm::gemmt;
@@ -120,6 +120,7 @@ static hipError_t ws_knob(const ntm::gemm::GemmArgs& a, int knob, hipStream_t s)
     case 5: return launch_gemm_bf16_tile_ws<MT, NT, 5>(a, s);
     case 6: return launch_gemm_bf16_tile_ws<MT, NT, 6>(a, s);
     case 7: return launch_gemm_bf16_tile_ws<MT, NT, 7>(a, s);
+    case 8: return launch_gemm_bf16_tile_ws<MT, NT, 8>(a, s);
     default: return hipErrorInvalidValue;
   }
 }
