@@ -43,7 +43,7 @@ def _declare(lib: ctypes.CDLL) -> None:
                             c_vp, c_vp, c_vp], c_int),
         "ntm_abft_result_bytes": ([], c_int),
         "ntm_fill_uniform_bf16": ([c_vp, c_size, ctypes.c_ulonglong, c_float, c_vp], c_int),
-        "ntm_k1_plan": ([c_int, c_int, c_int, c_vp, c_vp], c_int),
+        "ntm_k1_plan": ([c_int, c_int, c_int, c_vp, c_vp, c_vp], c_int),
         "ntm_fill_uniform_e4m3": ([c_vp, c_size, ctypes.c_ulonglong, c_float, c_vp], c_int),
         "ntm_ref_gemm_f32_e4m3": (
             [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp], c_int),

@@ -55,16 +55,18 @@ def _tile128_shape_ok(m: int, n: int, k: int, tm: int = 128, tn: int = 128) -> b
     return m > 0 and n > 0 and m % tm == 0 and n % tn == 0 and k >= 128 and k % 128 == 0
 
 
-def k1_plan(m: int, n: int, k: int) -> tuple[int, str]:
-    """The default dispatch's plan: (rows on the 256x256 kernel, variant of the
-    remaining rows) - host-side, no GPU needed. Raises ValueError when no
-    combination of the K1 kernels tiles (M, N, K)."""
-    top, rest = ctypes.c_int(), ctypes.c_int()
-    rc = lib().ntm_k1_plan(m, n, k, ctypes.byref(top), ctypes.byref(rest))
+def k1_plan(m: int, n: int, k: int) -> tuple[int, str, str]:
+    """The default dispatch's plan: (rows of C on the top kernel, top kernel,
+    kernel of the remaining rows) - host-side, no GPU needed. The top kernel is
+    the 256x256 one ("pingpong8c" / "pingpong8b") or a small tile; the rest is
+    a small tile (ignored when the top takes every row). Raises ValueError
+    when no combination of the K1 kernels tiles (M, N, K)."""
+    top, tv, rest = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    rc = lib().ntm_k1_plan(m, n, k, ctypes.byref(top), ctypes.byref(tv), ctypes.byref(rest))
     if rc != 0:
         raise ValueError(f"shape ({m},{n},{k}) not tiled by the K1 kernels")
     names = {v: kname for kname, v in GEMM_VARIANTS.items()}
-    return top.value, names[rest.value]
+    return top.value, names[tv.value], names[rest.value]
 
 
 def gemm_bf16(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,

@@ -15,33 +15,42 @@ def k1_plan():
     return f
 
 
-@pytest.mark.parametrize("m,n,k,top,rest", [
-    (1024, 1024, 1024, 0, "tile128"),          # < 1 round of 256x256 tiles: small tile only
-    (2048, 2048, 2048, 0, "tile128"),
-    (2560, 2560, 2560, 0, "tile160"),         # 256 tiles of 160x160: one full round
-    (1920, 1920, 1920, 0, "tile128"),
-    (256, 160, 128, 0, "tile256x160"),
-    (4096, 2048, 4096, 0, "tile256x128"),
-    (3072, 3072, 3072, 3072, "tile128"),       # whole rounds: 256x256 only
-    (4096, 4096, 4096, 4096, "tile128"),
-    (8192, 8192, 8192, 8192, "tile128"),
-    (6144, 6144, 6144, 5376, "tile256x128"),   # 3 rounds -> 2 + one of 256x128
-    (4352, 4352, 4352, 3840, "tile128"),
-    (416, 1280, 128, 256, "tile160"),          # split with a 160-row remainder
-    (1696, 2560, 256, 1536, "tile160"),
+@pytest.mark.parametrize("m,n,k,top,top_variant,rest", [
+    (1024, 1024, 1024, 1024, "tile128", None),       # < 1 round of 256x256 tiles: small tile only
+    (2048, 2048, 2048, 2048, "tile128", None),
+    (2560, 2560, 2560, 2560, "tile160", None),       # 256 tiles of 160x160: one full round
+    (1920, 1920, 1920, 1920, "tile128", None),
+    (256, 160, 128, 256, "tile256x160", None),
+    (2816, 2816, 2816, 2816, "tile256x128", None),   # 242 tiles: one round
+    (4096, 2048, 4096, 4096, "tile256x128", None),
+    (3072, 3072, 3072, 3072, "pingpong8c", None),    # whole rounds: 256x256 only
+    (4096, 4096, 4096, 4096, "pingpong8c", None),
+    (8192, 8192, 8192, 8192, "pingpong8c", None),
+    (8192, 8192, 8128, 8192, "pingpong8b", None),    # K % 128 != 0: the K % 64 kernel
+    (6144, 6144, 6144, 5376, "pingpong8c", "tile256x128"),   # 3 rounds -> 2 + one of 256x128
+    (4352, 4352, 4352, 3840, "pingpong8c", "tile128"),
+    (3200, 3200, 3200, 1280, "tile128", "tile160"),  # mixed small tiles: 2 full rounds
+    (416, 1280, 128, 256, "tile128", "tile160"),     # split with a 160-row remainder
 ])
-def test_plan_matches_cost_model(k1_plan, m, n, k, top, rest):
-    assert k1_plan(m, n, k) == (top, rest)
+def test_plan_matches_cost_model(k1_plan, m, n, k, top, top_variant, rest):
+    got = k1_plan(m, n, k)
+    assert got[:2] == (top, top_variant)
+    if rest is not None:
+        assert got[2] == rest
 
 
 @pytest.mark.parametrize("m,n,k", [(256 * i, 256 * j, 512) for i in range(1, 33, 3)
                                    for j in range(1, 33, 5)])
 def test_plan_is_well_formed(k1_plan, m, n, k):
-    top, rest = k1_plan(m, n, k)
-    assert 0 <= top <= m and top % 256 == 0
-    assert rest in ("tile128", "tile256x128", "tile160", "tile256x160")
-    if top < m and rest == "tile256x128":
-        assert (m - top) % 256 == 0
+    top, top_variant, rest = k1_plan(m, n, k)
+    small = ("tile128", "tile256x128", "tile160", "tile256x160")
+    assert 0 < top <= m and top_variant in small + ("pingpong8c",)
+    assert rest in small
+    tm = {"tile128": 128, "tile256x128": 256, "tile160": 160, "tile256x160": 256,
+          "pingpong8c": 256}
+    assert top % tm[top_variant] == 0
+    if top < m:
+        assert (m - top) % tm[rest] == 0
 
 
 def test_plan_rejects_bad_args(k1_plan):

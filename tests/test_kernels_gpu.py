@@ -260,8 +260,8 @@ def test_gemm_default_split_plan(ops, m, n, k):
     """Default dispatch that splits C by rows (k1_plan: top rows on 256x256,
     the rest on a small tile in a second launch): correct vs fp32 and
     bitwise equal to the single-kernel 256x256 result (same math, same order)."""
-    top, _ = ops.kernels.k1_plan(m, n, k)
-    assert 0 < top < m
+    top, top_variant, _ = ops.kernels.k1_plan(m, n, k)
+    assert 0 < top < m and top_variant == "pingpong8c"
     a = _rand(ops, (m, k), 271 + k)
     b = _rand(ops, (n, k), 273 + n)
     c = ops.gemm_bf16(a, b)
@@ -272,14 +272,19 @@ def test_gemm_default_split_plan(ops, m, n, k):
     assert torch.equal(c, ops.gemm_bf16(a, b, variant="pingpong8"))
 
 
-@pytest.mark.parametrize("m,n,k,top", [(2560, 2560, 512, 0), (416, 1280, 128, 256),
-                                       (1696, 2560, 256, 1536)])
-def test_gemm_default_dispatch_tile160(ops, m, n, k, top):
-    """Default dispatch where the plan picks the 160x160 tile alone (2560^2) or
-    as a 160-row remainder after 256x256 rows (A/C row offsets top*lda /
-    top*ldc with 160-row tiles): vs fp32 and bitwise equal to the explicit
-    variants run on the same row ranges."""
-    assert ops.kernels.k1_plan(m, n, k) == (top, "tile160")
+@pytest.mark.parametrize("m,n,k,plan", [
+    (2560, 2560, 512, (2560, "tile160")),               # 256 tiles of 160x160: one round
+    (416, 1280, 128, (256, "tile128", "tile160")),      # 160-row remainder after 128x128 rows
+    (1696, 2560, 256, (256, "tile128", "tile160")),
+    (3200, 3200, 256, (1280, "tile128", "tile160")),    # two full rounds of mixed tiles
+])
+def test_gemm_default_dispatch_mixed_tiles(ops, m, n, k, plan):
+    """Default dispatch where the plan runs small tiles only: one 160x160 launch,
+    or a row split across two small-tile kernels (A/C row offsets top*lda /
+    top*ldc, 160-row tiles after 128-row ones): vs fp32 and bitwise equal to
+    the explicit variants run on the same row ranges."""
+    top, top_variant, rest = ops.kernels.k1_plan(m, n, k)
+    assert (top, top_variant) == plan[:2] and (top == m or rest == plan[2])
     a = _rand(ops, (m, k), 571 + k)
     b = _rand(ops, (n, k), 573 + n)
     c = ops.gemm_bf16(a, b)
@@ -287,9 +292,9 @@ def test_gemm_default_dispatch_tile160(ops, m, n, k, top):
     atol, rtol = ops.gemm_tolerance(k)
     err = (c.float() - ref).abs()
     assert torch.all(err <= atol + rtol * ref.abs()), float(err.max())
-    if top:
-        assert torch.equal(c[:top], ops.gemm_bf16(a[:top], b, variant="pingpong8c"))
-    assert torch.equal(c[top:], ops.gemm_bf16(a[top:].contiguous(), b, variant="tile160"))
+    assert torch.equal(c[:top], ops.gemm_bf16(a[:top], b, variant=top_variant))
+    if top < m:
+        assert torch.equal(c[top:], ops.gemm_bf16(a[top:].contiguous(), b, variant=rest))
 
 
 def test_gemm_default_rejects_unplannable_shape_before_launch(ops):

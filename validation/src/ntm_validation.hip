@@ -80,52 +80,76 @@ constexpr SmallTile kSmallTiles[] = {
 constexpr double kSplitPenalty = 0.25;  // a second launch, in 128x128-tile-round units
 
 struct K1Plan {
-  int top_rows;      // rows [0, top_rows) on the 256x256 kernel; -1 = no plan tiles (M,N,K)
+  int top_rows;      // rows [0, top_rows) on top_variant; -1 = no plan tiles (M,N,K)
+  int top_variant;   // 5 / 4 (the 256x256 kernel) or a kSmallTiles variant
   int rest_variant;  // rows [top_rows, M) on a kSmallTiles variant (15..18)
   bool feasible() const { return top_rows >= 0; }
 };
 
+// The plan: C split by rows into a top part and a rest part, each on one tile
+// kernel in its own launch (either part may be empty). The top part runs the
+// 256x256 kernel or a small tile, the rest a small tile; the smallest
+// predicted time wins. Mixed small tiles fill whole rounds where one tile
+// shape cannot: 3200^3 = 1920 rows of 160x160 (240 tiles) + 1280 rows of
+// 128x128 (250 tiles), two full rounds instead of 1.56 rounds of 160x160
+// (977 vs 924 TF/s, hipBLASLt 948: profiles/r2_ws/split_3200.log).
+// Ties: fewer launches, then more rows on the 256x256 kernel.
 inline K1Plan plan_k1(int M, int N, int K) {
   auto rounds = [](double tiles) { return tiles <= 0 ? 0.0 : __builtin_ceil(tiles / kCUs); };
   const double inf = 1e300;
   const bool big_ok = N % 256 == 0 && K % 64 == 0 && K >= 128;
-  K1Plan best{-1, 15};
+  const int big_variant = K % 128 == 0 ? kDefaultVariant : 4;
+  K1Plan best{-1, 15, 15};
   double best_cost = inf;
+  int best_launches = 3, best_big_rows = -1;
   if (M <= 0 || N <= 0 || K <= 0) return best;
-  for (int m1 = 0; m1 <= M; m1 += 256) {
-    if (m1 > 0 && !big_ok) break;
-    const int rest = M - m1;
-    const double top = m1 ? rounds((m1 / 256.0) * (N / 256.0)) * 4.0 : 0.0;
-    double bottom = 0.0;
-    int v = 15;
-    if (rest > 0) {
-      bottom = inf;
-      for (const SmallTile& st : kSmallTiles) {
-        if (rest % st.tm || N % st.tn || K % 128 || K < 128) continue;
-        const double c = rounds((double)(rest / st.tm) * (N / st.tn)) *
-                         (st.tm * st.tn / 16384.0) / st.eff;
-        if (c < bottom) {
-          bottom = c;
-          v = st.variant;
+  auto small_ok = [&](const SmallTile& st, int rows) {
+    return rows % st.tm == 0 && N % st.tn == 0 && K % 128 == 0 && K >= 128;
+  };
+  auto small_cost = [&](const SmallTile& st, int rows) {
+    return rounds((double)(rows / st.tm) * (N / st.tn)) * (st.tm * st.tn / 16384.0) / st.eff;
+  };
+  // top candidates: index -1 = the 256x256 kernel, else kSmallTiles[t]
+  const int nsmall = (int)(sizeof(kSmallTiles) / sizeof(kSmallTiles[0]));
+  for (int t = -1; t < nsmall; ++t) {
+    const int tm = t < 0 ? 256 : kSmallTiles[t].tm;
+    if (t < 0 && !big_ok) continue;
+    if (t >= 0 && (N % kSmallTiles[t].tn || K % 128 || K < 128)) continue;
+    for (int m1 = tm; m1 <= M; m1 += tm) {
+      const double top = t < 0 ? rounds((m1 / 256.0) * (N / 256.0)) * 4.0
+                               : small_cost(kSmallTiles[t], m1);
+      const int rest = M - m1;
+      for (int r = 0; r < nsmall; ++r) {
+        if (rest > 0 && !small_ok(kSmallTiles[r], rest)) continue;
+        if (rest == 0 && r > 0) break;  // no rest part: one candidate is enough
+        const double cost = top + (rest > 0 ? small_cost(kSmallTiles[r], rest) + kSplitPenalty : 0.0);
+        const int launches = rest > 0 ? 2 : 1;
+        const int big_rows = t < 0 ? m1 : 0;
+        const bool better = cost < best_cost - 1e-9 ||
+                            (cost <= best_cost + 1e-9 &&
+                             (launches < best_launches ||
+                              (launches == best_launches && big_rows > best_big_rows)));
+        if (better) {
+          best_cost = cost;
+          best_launches = launches;
+          best_big_rows = big_rows;
+          best = K1Plan{m1, t < 0 ? big_variant : kSmallTiles[t].variant,
+                        rest > 0 ? kSmallTiles[r].variant : (t < 0 ? 15 : kSmallTiles[t].variant)};
         }
       }
-    }
-    const double cost = top + bottom + (m1 > 0 && rest > 0 ? kSplitPenalty : 0.0);
-    if (cost >= inf) continue;  // no kernel tiles the remainder: never a plan
-    if (cost <= best_cost) {  // ties: more rows on the 256x256 kernel
-      best_cost = cost;
-      best = K1Plan{m1, v};
     }
   }
   return best;
 }
 
 // The default dispatch's plan for (M, N, K) (host only; tests and tools).
-NTM_API int ntm_k1_plan(int M, int N, int K, int* top_rows, int* rest_variant) {
-  if (M <= 0 || N <= 0 || K <= 0 || !top_rows || !rest_variant) return (int)hipErrorInvalidValue;
+NTM_API int ntm_k1_plan(int M, int N, int K, int* top_rows, int* top_variant, int* rest_variant) {
+  if (M <= 0 || N <= 0 || K <= 0 || !top_rows || !top_variant || !rest_variant)
+    return (int)hipErrorInvalidValue;
   const K1Plan pl = plan_k1(M, N, K);
   if (!pl.feasible()) return (int)hipErrorInvalidValue;
   *top_rows = pl.top_rows;
+  *top_variant = pl.top_variant;
   *rest_variant = pl.rest_variant;
   return 0;
 }
@@ -136,15 +160,15 @@ NTM_API int ntm_gemm_bf16_variant(int variant, const void* A, const void* B,
   if (variant == 0) {
     const K1Plan pl = plan_k1(M, N, K);
     if (!pl.feasible()) return (int)hipErrorInvalidValue;  // nothing launched
-    const int top = ntm::gemm3::shape_ok3(pl.top_rows, N, K) ? kDefaultVariant : 4;
-    if (pl.top_rows > 0 && pl.top_rows < M) {
-      const int rc = ntm_gemm_bf16_variant(top, A, B, C, pl.top_rows, N, K, lda, ldb, ldc, stream);
+    if (pl.top_rows < M) {
+      const int rc = ntm_gemm_bf16_variant(pl.top_variant, A, B, C, pl.top_rows, N, K, lda, ldb,
+                                           ldc, stream);
       if (rc != 0) return rc;
       return ntm_gemm_bf16_variant(pl.rest_variant, (const __bf16*)A + (size_t)pl.top_rows * lda,
                                    B, (__bf16*)C + (size_t)pl.top_rows * ldc, M - pl.top_rows, N,
                                    K, lda, ldb, ldc, stream);
     }
-    variant = pl.top_rows == M ? top : pl.rest_variant;
+    variant = pl.top_variant;
   }
   ntm::gemm::GemmArgs a;
   a.A = (const __bf16*)A;
