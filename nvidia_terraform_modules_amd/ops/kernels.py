@@ -51,7 +51,14 @@ TILE_SHAPES = {"tile128": (128, 128), "tile256x128": (256, 128), "tile160": (160
                "tile160w4": (160, 160)}
 
 
-def _tile128_shape_ok(m: int, n: int, k: int, tm: int = 128, tn: int = 128) -> bool:
+# wave-specialised tile kernels: any M, N (N % 4 == 0), partial edge tiles masked
+MASKED_TILES = frozenset({"tile128", "tile256x128", "tile160"})
+
+
+def _tile128_shape_ok(m: int, n: int, k: int, tm: int = 128, tn: int = 128,
+                      masked: bool = False) -> bool:
+    if masked:
+        return m > 0 and n > 0 and n % 4 == 0 and k >= 128 and k % 128 == 0
     return m > 0 and n > 0 and m % tm == 0 and n % tn == 0 and k >= 128 and k % 128 == 0
 
 
@@ -78,7 +85,8 @@ def gemm_bf16(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
     (rounds of 256 CUs x tile area / efficiency, ``k1_plan``): "tile128" /
     "tile256x128" / "tile160" / "tile256x160" (128x128 / 256x128 / 160x160 /
     256x160 tiles, K % 128; the first three with 4 LDS-DMA producer + 4 MFMA
-    consumer waves, 256x160 with 4 waves) for small and mid-size C,
+    consumer waves and masked edge tiles (any M, N % 4), 256x160 with 4 waves
+    and whole tiles) for small, mid-size and ragged C,
     else "pingpong8c" when K % 128 == 0, else "pingpong8b" (8 waves, two per SIMD, staggered, balanced 8/4/8/4 LDS read
     schedule; 8c adds parity-alternating B buffers and a tail-free K loop -
     fastest measured), "pingpong8" (the first 12/4/8/0 schedule), or the
@@ -93,8 +101,9 @@ def gemm_bf16(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
         raise ValueError(f"K mismatch: a has {k}, b has {kb}")
     if variant in TILE_SHAPES:
         tm, tn = TILE_SHAPES[variant]
-        if not _tile128_shape_ok(m, n, k, tm, tn):
-            raise ValueError(f"shape ({m},{n},{k}) not tiled by the {tm}x{tn} kernel (K % 128)")
+        if not _tile128_shape_ok(m, n, k, tm, tn, masked=variant in MASKED_TILES):
+            raise ValueError(f"shape ({m},{n},{k}) not tiled by the {tm}x{tn} kernel "
+                             "(K % 128; exact tiles unless masked, N % 4)")
     elif variant == "default":
         k1_plan(m, n, k)        # the native plan is the one authority on what it serves
     elif not gemm_shape_ok(m, n, k):

@@ -20,17 +20,20 @@ def k1_plan():
     (2048, 2048, 2048, 2048, "tile128", None),
     (2560, 2560, 2560, 2560, "tile160", None),       # 256 tiles of 160x160: one full round
     (1920, 1920, 1920, 1920, "tile128", None),
-    (256, 160, 128, 256, "tile256x160", None),
+    (256, 160, 128, 256, "tile128", None),           # 4 masked 128x128 tiles beat one 256x160
     (2816, 2816, 2816, 2816, "tile256x128", None),   # 242 tiles: one round
     (4096, 2048, 4096, 4096, "tile256x128", None),
     (3072, 3072, 3072, 3072, "pingpong8c", None),    # whole rounds: 256x256 only
     (4096, 4096, 4096, 4096, "pingpong8c", None),
     (8192, 8192, 8192, 8192, "pingpong8c", None),
     (8192, 8192, 8128, 8192, "pingpong8b", None),    # K % 128 != 0: the K % 64 kernel
-    (6144, 6144, 6144, 5376, "pingpong8c", "tile256x128"),   # 3 rounds -> 2 + one of 256x128
+    (6144, 6144, 6144, 5376, "pingpong8c", "tile160"),  # 3 rounds -> 2 + one of masked 160x160
     (4352, 4352, 4352, 3840, "pingpong8c", "tile128"),
     (3200, 3200, 3200, 1280, "tile128", "tile160"),  # mixed small tiles: 2 full rounds
-    (416, 1280, 128, 256, "tile128", "tile160"),     # split with a 160-row remainder
+    (416, 1280, 128, 416, "tile128", None),          # masked edge tiles: one launch
+    (1696, 2560, 2560, 1696, "tile160", None),       # 11 x 16 tiles, last row 96/160 full
+    (2400, 3200, 3200, 2400, "tile256x128", None),   # 10 x 25 tiles: one round
+    (8200, 8192, 8192, 8192, "pingpong8c", "tile128"),  # 8 ragged rows on masked tiles
 ])
 def test_plan_matches_cost_model(k1_plan, m, n, k, top, top_variant, rest):
     got = k1_plan(m, n, k)
@@ -48,9 +51,18 @@ def test_plan_is_well_formed(k1_plan, m, n, k):
     assert rest in small
     tm = {"tile128": 128, "tile256x128": 256, "tile160": 160, "tile256x160": 256,
           "pingpong8c": 256}
-    assert top % tm[top_variant] == 0
+    masked = ("tile128", "tile256x128", "tile160")
+    assert top % tm[top_variant] == 0 or (top == m and top_variant in masked)
     if top < m:
-        assert (m - top) % tm[rest] == 0
+        assert (m - top) % tm[rest] == 0 or rest in masked
+
+
+@pytest.mark.parametrize("m,n,k", [(1000, 1000, 1024), (100, 4096, 4096), (8200, 8192, 8192),
+                                   (3000, 5000, 2048), (1, 4, 128)])
+def test_plan_serves_ragged_shapes(k1_plan, m, n, k):
+    """Masked edge tiles: any M and N % 4 == 0 with K % 128 == 0 has a plan."""
+    top, top_variant, _ = k1_plan(m, n, k)
+    assert 0 < top <= m
 
 
 def test_plan_rejects_bad_args(k1_plan):
@@ -58,7 +70,8 @@ def test_plan_rejects_bad_args(k1_plan):
         k1_plan(0, 256, 256)
 
 
-@pytest.mark.parametrize("m,n,k", [(384, 256, 192), (100, 256, 256), (256, 256, 64)])
+@pytest.mark.parametrize("m,n,k", [(384, 256, 192), (100, 256, 192), (256, 256, 64),
+                                   (256, 6, 128)])
 def test_plan_reports_infeasible_shapes(k1_plan, m, n, k):
     """No kernel combination tiles these: the plan says so instead of returning
     a plan whose second launch would fail after the first one wrote C (ADVICE r1:

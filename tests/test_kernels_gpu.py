@@ -317,8 +317,34 @@ def test_gemm_tile128_rejects_bad_shapes(ops):
     with pytest.raises(ValueError):
         ops.gemm_bf16(a, a, variant="tile128")    # K % 128
     a = torch.zeros((192, 128), dtype=torch.bfloat16, device="cuda")
+    b = torch.zeros((6, 128), dtype=torch.bfloat16, device="cuda")
     with pytest.raises(ValueError):
-        ops.gemm_bf16(a, a, variant="tile128")    # M % 128
+        ops.gemm_bf16(a, b, variant="tile128")    # N % 4 (8-byte C stores)
+    with pytest.raises(ValueError):
+        ops.gemm_bf16(a, a, variant="tile256x160")  # whole tiles only (M % 256)
+
+
+@pytest.mark.parametrize("variant", ["tile128", "tile256x128", "tile160", "default"])
+@pytest.mark.parametrize("m,n,k", [(1000, 1000, 1024), (100, 4096, 256), (1696, 2560, 256),
+                                   (2400, 3200, 128), (1, 4, 128), (333, 1004, 384),
+                                   (8200, 260, 128)])
+def test_gemm_masked_edge_tiles(ops, variant, m, n, k):
+    """Wave-specialised tiles on ragged C (any M, N % 4): vs fp32, and nothing
+    written outside C - C is a view into a sentinel-filled buffer with extra
+    rows below and extra columns to the right (ldc > N)."""
+    a = _rand(ops, (m, k), 971 + m)
+    b = _rand(ops, (n, k), 973 + n)
+    big = torch.full((m + 37, n + 12), 3.0, dtype=torch.bfloat16, device="cuda")
+    c = big[:m, :n]
+    ops.gemm_bf16(a, b, c, variant=variant)
+    torch.cuda.synchronize()
+    ref = a.float() @ b.float().T
+    atol, rtol = ops.gemm_tolerance(k)
+    err = (c.float() - ref).abs()
+    assert torch.all(err <= atol + rtol * ref.abs()), float(err.max())
+    assert torch.all(big[m:] == 3.0) and torch.all(big[:, n:] == 3.0)
+    if variant != "default" and m % 256 == 0 and n % 256 == 0:
+        assert torch.equal(c, ops.gemm_bf16(a, b, variant="pingpong8"))
 
 
 def _rand_fp8(shape, seed):

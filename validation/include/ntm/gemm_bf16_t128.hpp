@@ -179,7 +179,9 @@ __device__ __forceinline__ void tile_coords_t(int M, int N, int& tm, int& tn) {
   const int xcd = bid & 7;
   const int q = nwg >> 3, r = nwg & 7;
   const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-  const int tiles_m = M / Cfg<MT, NT>::TM, tiles_n = N / Cfg<MT, NT>::TN;
+  // ceil: the wave-specialised kernel masks a partial last tile row / column
+  const int tiles_m = (M + Cfg<MT, NT>::TM - 1) / Cfg<MT, NT>::TM;
+  const int tiles_n = (N + Cfg<MT, NT>::TN - 1) / Cfg<MT, NT>::TN;
   const int group = kGroupMT * tiles_n;
   const int gid = wgid / group;
   const int first_m = gid * kGroupMT;
@@ -301,6 +303,12 @@ inline hipError_t launch_gemm_bf16_tile(const GemmArgs& a, hipStream_t stream) {
 //   Drain: producers vmcnt(0) before exit; MFMA order per accumulator is the
 //        kernel above's, so results are bitwise equal to it.
 // Same shape rule as the kernel above.
+// Shape rule of the wave-specialised kernel: any M, N with N % 4 == 0 (8-byte
+// C stores); K % 128 as the 4-wave kernel.
+__host__ __device__ inline bool shape_ok_ws(int M, int N, int K) {
+  return M > 0 && N > 0 && (N % 4) == 0 && K >= 2 * TK && (K % (2 * TK)) == 0;
+}
+
 template <int MT, int NT>
 struct CfgWS {
   static_assert(4 * MT * NT + 8 * (MT + NT) <= 232, "256 registers per lane at 2 waves / SIMD");
@@ -320,6 +328,61 @@ template <int MT, int NT, int KNOB>
 __device__ __forceinline__ void read_half(const CtxT& c, FragsT<MT, NT>& f, int kt, int ks, int i) {
   const int r = (KNOB & kWsBFirst) ? (i < NT ? MT + i : i - NT) : i;
   read_frag<MT, NT>(c, f, kt, ks * (MT + NT) + r);
+}
+
+// Edge tiles (M or N not a multiple of the tile): a piece's source row is
+// clamped to the last row of A / B, so every load stays in bounds; the rows
+// and columns of C it feeds beyond M / N are computed but never stored.
+struct Clamp {
+  const __bf16* A;
+  const __bf16* B;
+  int a_row, b_row;  // this lane's first row (tile origin + lane / 4)
+  int a_last, b_last;
+  int lda, ldb, col;  // col: this lane's swizzled 8-element column chunk
+};
+
+template <int MT, int NT>
+__device__ __forceinline__ void issue_piece_clamped(const CtxT& c, const Clamp& q, int kt, int T,
+                                                    int i) {
+  using C = Cfg<MT, NT>;
+  const bool real = kt < T;
+  const bool is_a = i < MT;
+  const int g = is_a ? c.w * MT + i : c.w * NT + (i - MT);
+  const int rb = g >> 1, kh = g & 1;
+  const size_t koff = (size_t)(real ? kt : T - 1) * TK + kh * 32;
+  char* slot = c.lds + (kt % C::S) * C::kSlot;
+  const __bf16* src = is_a ? q.A + (size_t)min(q.a_row + rb * 16, q.a_last) * q.lda
+                           : q.B + (size_t)min(q.b_row + rb * 16, q.b_last) * q.ldb;
+  char* dst = real ? slot + (is_a ? 0 : C::kA) + (rb * 2 + kh) * 1024
+                   : c.lds + C::kScratch + c.w * 1024;
+  glds16(src + q.col + koff, dst);
+}
+
+// Producer loop of the wave-specialised kernel (see below).
+template <int MT, int NT, int KNOB, bool CLAMP>
+__device__ __forceinline__ void ws_produce(const CtxT& c, const Clamp& q, int T) {
+  using C = Cfg<MT, NT>;
+  constexpr int LA = (KNOB & kWsShallow) ? C::S - 2 : C::S - 1;  // tiles issued ahead
+  constexpr int VM = (LA - 1) * C::P;
+  auto issue = [&](int kt, int i) {
+    if constexpr (CLAMP)
+      issue_piece_clamped<MT, NT>(c, q, kt, T, i);
+    else
+      issue_piece<MT, NT>(c, kt, T, i);
+  };
+#pragma unroll
+  for (int s = 0; s < LA; ++s)
+#pragma unroll
+    for (int i = 0; i < C::P; ++i) issue(s, i);
+  wait_vmcnt_n<VM>();  // tile 0 landed
+  raw_barrier();
+  for (int t = 0; t < T; ++t) {
+#pragma unroll
+    for (int i = 0; i < C::P; ++i) issue(t + LA, i);
+    wait_vmcnt_n<VM>();  // tile t+1 landed
+    raw_barrier();
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // dummy pieces drained
 }
 
 template <int MT, int NT = 4, int KNOB = 0>
@@ -350,21 +413,14 @@ __global__ void __launch_bounds__(2 * kThreadsT, 1) gemm_bf16_tile_ws_kernel(Gem
   c.frag_off = (lane & 15) * 64 + ((lane >> 4) ^ ((lane >> 2) & 2)) * 16;
 
   if (wave >= 4) {  // producer
-    constexpr int LA = (KNOB & kWsShallow) ? C::S - 2 : C::S - 1;  // tiles issued ahead
-    constexpr int VM = (LA - 1) * C::P;
-#pragma unroll
-    for (int s = 0; s < LA; ++s)
-#pragma unroll
-      for (int i = 0; i < C::P; ++i) issue_piece<MT, NT>(c, s, T, i);
-    wait_vmcnt_n<VM>();  // tile 0 landed
-    raw_barrier();
-    for (int t = 0; t < T; ++t) {
-#pragma unroll
-      for (int i = 0; i < C::P; ++i) issue_piece<MT, NT>(c, t + LA, T, i);
-      wait_vmcnt_n<VM>();  // tile t+1 landed
-      raw_barrier();
+    if (m0 + C::TM > p.M || n0 + C::TN > p.N) {  // edge tile (uniform branch)
+      const int r = lane >> 2;
+      Clamp q{p.A, p.B, m0 + r, n0 + r, p.M - 1, p.N - 1, p.lda, p.ldb,
+              ((lane & 3) ^ (((r >> 3) & 1) << 1)) * 8};
+      ws_produce<MT, NT, KNOB, true>(c, q, T);
+    } else {
+      ws_produce<MT, NT, KNOB, false>(c, Clamp{}, T);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // dummy pieces drained
     return;
   }
 
@@ -415,16 +471,18 @@ __global__ void __launch_bounds__(2 * kThreadsT, 1) gemm_bf16_tile_ws_kernel(Gem
       o[1] = (__bf16)v[1];
       o[2] = (__bf16)v[2];
       o[3] = (__bf16)v[3];
-      *(bf16x4*)(p.C + (size_t)row * p.ldc + col) = o;
+      if (row < p.M && col < p.N)  // edge tiles: rows / columns past C are not stored
+        *(bf16x4*)(p.C + (size_t)row * p.ldc + col) = o;
     }
 }
 
 template <int MT, int NT = 4, int KNOB = 0>
 inline hipError_t launch_gemm_bf16_tile_ws(const GemmArgs& a, hipStream_t stream) {
-  if (!shape_ok_t<MT, NT>(a.M, a.N, a.K) || a.lda < a.K || a.ldb < a.K || a.ldc < a.N ||
+  if (!shape_ok_ws(a.M, a.N, a.K) || a.lda < a.K || a.ldb < a.K || a.ldc < a.N ||
       (a.lda % 8) || (a.ldb % 8) || (a.ldc % 4))
     return hipErrorInvalidValue;
-  const unsigned grid = (unsigned)((a.M / Cfg<MT, NT>::TM) * (a.N / Cfg<MT, NT>::TN));
+  const unsigned grid = (unsigned)(((a.M + Cfg<MT, NT>::TM - 1) / Cfg<MT, NT>::TM) *
+                                   ((a.N + Cfg<MT, NT>::TN - 1) / Cfg<MT, NT>::TN));
   hipLaunchKernelGGL((gemm_bf16_tile_ws_kernel<MT, NT, KNOB>), dim3(grid), dim3(2 * kThreadsT), 0,
                      stream, a);
   return hipGetLastError();

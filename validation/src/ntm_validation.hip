@@ -74,9 +74,12 @@ constexpr double kCUs = 256.0;
 struct SmallTile {
   int variant, tm, tn;
   double eff;
+  bool masked;  // wave-specialised kernel: any M, N (N % 4), partial edge tiles masked
 };
-constexpr SmallTile kSmallTiles[] = {
-    {15, 128, 128, 0.60}, {16, 256, 128, 0.78}, {17, 160, 160, 0.72}, {18, 256, 160, 0.61}};
+constexpr SmallTile kSmallTiles[] = {{15, 128, 128, 0.60, true},
+                                     {16, 256, 128, 0.78, true},
+                                     {17, 160, 160, 0.72, true},
+                                     {18, 256, 160, 0.61, false}};
 constexpr double kSplitPenalty = 0.25;  // a second launch, in 128x128-tile-round units
 
 struct K1Plan {
@@ -104,18 +107,22 @@ inline K1Plan plan_k1(int M, int N, int K) {
   int best_launches = 3, best_big_rows = -1;
   if (M <= 0 || N <= 0 || K <= 0) return best;
   auto small_ok = [&](const SmallTile& st, int rows) {
-    return rows % st.tm == 0 && N % st.tn == 0 && K % 128 == 0 && K >= 128;
+    const bool mn = st.masked ? N % 4 == 0 : rows % st.tm == 0 && N % st.tn == 0;
+    return mn && K % 128 == 0 && K >= 128;
   };
-  auto small_cost = [&](const SmallTile& st, int rows) {
-    return rounds((double)(rows / st.tm) * (N / st.tn)) * (st.tm * st.tn / 16384.0) / st.eff;
+  auto small_cost = [&](const SmallTile& st, int rows) {  // edge tiles cost a whole tile
+    const double tiles = (double)((rows + st.tm - 1) / st.tm) * ((N + st.tn - 1) / st.tn);
+    return rounds(tiles) * (st.tm * st.tn / 16384.0) / st.eff;
   };
   // top candidates: index -1 = the 256x256 kernel, else kSmallTiles[t]
   const int nsmall = (int)(sizeof(kSmallTiles) / sizeof(kSmallTiles[0]));
   for (int t = -1; t < nsmall; ++t) {
     const int tm = t < 0 ? 256 : kSmallTiles[t].tm;
     if (t < 0 && !big_ok) continue;
-    if (t >= 0 && (N % kSmallTiles[t].tn || K % 128 || K < 128)) continue;
-    for (int m1 = tm; m1 <= M; m1 += tm) {
+    if (t >= 0 && !small_ok(kSmallTiles[t], kSmallTiles[t].tm)) continue;
+    const bool masked = t >= 0 && kSmallTiles[t].masked;
+    for (int m1 = tm; m1 < M + (masked ? tm : 1); m1 += tm) {
+      if (m1 > M) m1 = M;  // masked kernel: the whole of C, last tile row partial
       const double top = t < 0 ? rounds((m1 / 256.0) * (N / 256.0)) * 4.0
                                : small_cost(kSmallTiles[t], m1);
       const int rest = M - m1;
