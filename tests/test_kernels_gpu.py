@@ -63,9 +63,11 @@ def test_gemm_strided_ld(ops, k, ldc_pad):
 
 def test_gemm_rejects_bad_shapes(ops):
     a = torch.zeros((300, 256), dtype=torch.bfloat16, device="cuda")
-    b = torch.zeros((256, 256), dtype=torch.bfloat16, device="cuda")
+    b = torch.zeros((6, 256), dtype=torch.bfloat16, device="cuda")
     with pytest.raises(ValueError):
-        ops.gemm_bf16(a, b)
+        ops.gemm_bf16(a, b)                   # N % 4: no kernel stores it
+    with pytest.raises(ValueError):
+        ops.gemm_bf16(a, a[:256], variant="pingpong8c")  # 256x256 kernel: M % 256
     with pytest.raises(ValueError):
         ops.gemm_bf16(b[:, :64], b[:, :64])  # K < 128
 
@@ -274,9 +276,10 @@ def test_gemm_default_split_plan(ops, m, n, k):
 
 @pytest.mark.parametrize("m,n,k,plan", [
     (2560, 2560, 512, (2560, "tile160")),               # 256 tiles of 160x160: one round
-    (416, 1280, 128, (256, "tile128", "tile160")),      # 160-row remainder after 128x128 rows
-    (1696, 2560, 256, (256, "tile128", "tile160")),
+    (416, 1280, 128, (416, "tile128")),                 # masked edge tiles, one launch
+    (1696, 2560, 256, (1696, "tile160")),               # 11 x 16 tiles, last row partial
     (3200, 3200, 256, (1280, "tile128", "tile160")),    # two full rounds of mixed tiles
+    (2880, 3200, 256, (1024, "tile128", "tile160")),    # 160-row tiles after 128-row ones
 ])
 def test_gemm_default_dispatch_mixed_tiles(ops, m, n, k, plan):
     """Default dispatch where the plan runs small tiles only: one 160x160 launch,
