@@ -27,6 +27,9 @@ SHAPES = [(256, 256, 128), (256, 512, 256), (512, 768, 384), (2304, 1536, 640),
           (4096, 4352, 512), (4096, 4096, 4096), (8192, 8192, 8192)]
 SHAPES_160 = [(160, 160, 128), (1280, 800, 384), (2560, 1600, 640), (2560, 2560, 2560),
               (5120, 5120, 1280)]
+# ragged C for the masked (wave-specialised) tiles and the default dispatch
+SHAPES_RAGGED = [(1000, 1000, 1024), (1696, 2560, 640), (333, 1004, 384), (2400, 3200, 512)]
+MASKED = ("tile128", "tile256x128", "tile160", "default")
 SHAPES_FP8 = [(256, 256, 256), (256, 512, 512), (512, 768, 768), (2304, 1536, 1280),
               (4096, 4352, 1024), (4096, 4096, 4096), (8192, 8192, 8192)]
 
@@ -51,8 +54,9 @@ def main():
             return ops.gemm_fp8(a, b, out) if fp8 else ops.gemm_bf16(a, b, out, variant=v)
 
         tm, tn = ops.kernels.TILE_SHAPES.get(v, (0, 0))
-        for (m, n, k) in (SHAPES_FP8 if fp8 else SHAPES_160 if tn == 160 else SHAPES):
-            if tm and m % tm:
+        shapes = SHAPES_FP8 if fp8 else SHAPES_160 if tn == 160 else SHAPES
+        for (m, n, k) in shapes + (SHAPES_RAGGED if v in MASKED else []):
+            if tm and m % tm and v not in MASKED:
                 continue
             a = ops.fill_uniform_(torch.empty((m, k), dtype=dt, device=dev), 5 + m)
             b = ops.fill_uniform_(torch.empty((n, k), dtype=dt, device=dev), 6 + n)
