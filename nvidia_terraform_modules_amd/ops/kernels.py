@@ -35,7 +35,7 @@ GEMM_VARIANTS = {"default": 0, "pingpong8": 1, "wave128": 2, "wave128d4": 3, "pi
                  "pingpong8ww": 9, "pingpong8cw": 10, "pingpong8cwe": 11,
                  "pingpong8cwn": 12, "pingpong8cwne": 13, "pingpong8pw": 14, "tile128": 15,
                  "tile256x128": 16, "tile160": 17, "tile256x160": 18, "tile128w4": 19,
-                 "tile256x128w4": 20, "tile160w4": 21}
+                 "tile256x128w4": 20, "tile160w4": 21, "pingpong8cm": 22}
 
 
 # variants built only into libntm_experimental.so (tests / tools): never selected
@@ -106,6 +106,9 @@ def gemm_bf16(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
                              "(K % 128; exact tiles unless masked, N % 4)")
     elif variant == "default":
         k1_plan(m, n, k)        # the native plan is the one authority on what it serves
+    elif variant == "pingpong8cm":  # 256x256 with masked edge tiles
+        if not (m > 0 and n > 0 and n % 8 == 0 and k >= 128 and k % 128 == 0):
+            raise ValueError(f"shape ({m},{n},{k}) not served by pingpong8cm (N % 8, K % 128)")
     elif not gemm_shape_ok(m, n, k):
         raise ValueError(f"shape ({m},{n},{k}) not tiled by the 256x256x64 kernel")
     if out is None:

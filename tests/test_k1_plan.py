@@ -29,7 +29,9 @@ def k1_plan():
     (8192, 8192, 8128, 8192, "pingpong8b", None),    # K % 128 != 0: the K % 64 kernel
     (6144, 6144, 6144, 5376, "pingpong8c", "tile160"),  # 3 rounds -> 2 + one of masked 160x160
     (4352, 4352, 4352, 3840, "pingpong8c", "tile128"),
-    (3200, 3200, 3200, 1280, "tile128", "tile160"),  # mixed small tiles: 2 full rounds
+    (3200, 3200, 3200, 3200, "pingpong8cm", None),   # one round of masked 256x256 tiles
+    (2080, 3844, 256, 512, "tile128", "tile160"),    # N % 8 != 0: mixed small tiles
+    (4000, 4000, 4096, 4000, "pingpong8cm", None),
     (416, 1280, 128, 416, "tile128", None),          # masked edge tiles: one launch
     (1696, 2560, 2560, 1696, "tile160", None),       # 11 x 16 tiles, last row 96/160 full
     (2400, 3200, 3200, 2400, "tile256x128", None),   # 10 x 25 tiles: one round
@@ -47,11 +49,11 @@ def test_plan_matches_cost_model(k1_plan, m, n, k, top, top_variant, rest):
 def test_plan_is_well_formed(k1_plan, m, n, k):
     top, top_variant, rest = k1_plan(m, n, k)
     small = ("tile128", "tile256x128", "tile160", "tile256x160")
-    assert 0 < top <= m and top_variant in small + ("pingpong8c",)
+    assert 0 < top <= m and top_variant in small + ("pingpong8c", "pingpong8cm")
     assert rest in small
     tm = {"tile128": 128, "tile256x128": 256, "tile160": 160, "tile256x160": 256,
-          "pingpong8c": 256}
-    masked = ("tile128", "tile256x128", "tile160")
+          "pingpong8c": 256, "pingpong8cm": 256}
+    masked = ("tile128", "tile256x128", "tile160", "pingpong8cm")
     assert top % tm[top_variant] == 0 or (top == m and top_variant in masked)
     if top < m:
         assert (m - top) % tm[rest] == 0 or rest in masked

@@ -278,14 +278,15 @@ def test_gemm_default_split_plan(ops, m, n, k):
     (2560, 2560, 512, (2560, "tile160")),               # 256 tiles of 160x160: one round
     (416, 1280, 128, (416, "tile128")),                 # masked edge tiles, one launch
     (1696, 2560, 256, (1696, "tile160")),               # 11 x 16 tiles, last row partial
-    (3200, 3200, 256, (1280, "tile128", "tile160")),    # two full rounds of mixed tiles
-    (2880, 3200, 256, (1024, "tile128", "tile160")),    # 160-row tiles after 128-row ones
+    (2080, 3844, 256, (512, "tile128", "tile160")),     # mixed small tiles, ragged N
+    (2304, 3844, 256, (768, "tile128", "tile160")),
+    (3200, 3200, 256, (3200, "pingpong8cm")),           # 256x256 with masked edge tiles
 ])
 def test_gemm_default_dispatch_mixed_tiles(ops, m, n, k, plan):
-    """Default dispatch where the plan runs small tiles only: one 160x160 launch,
-    or a row split across two small-tile kernels (A/C row offsets top*lda /
-    top*ldc, 160-row tiles after 128-row ones): vs fp32 and bitwise equal to
-    the explicit variants run on the same row ranges."""
+    """Default dispatch without the exact 256x256 kernel: one 160x160 launch, a
+    row split across two small-tile kernels (A/C row offsets top*lda /
+    top*ldc, 160-row tiles after 128-row ones), or the masked 256x256 kernel:
+    vs fp32 and bitwise equal to the explicit variants on the same row ranges."""
     top, top_variant, rest = ops.kernels.k1_plan(m, n, k)
     assert (top, top_variant) == plan[:2] and (top == m or rest == plan[2])
     a = _rand(ops, (m, k), 571 + k)
@@ -327,17 +328,21 @@ def test_gemm_tile128_rejects_bad_shapes(ops):
         ops.gemm_bf16(a, a, variant="tile256x160")  # whole tiles only (M % 256)
 
 
-@pytest.mark.parametrize("variant", ["tile128", "tile256x128", "tile160", "default"])
+@pytest.mark.parametrize("variant", ["tile128", "tile256x128", "tile160", "pingpong8cm",
+                                     "default"])
 @pytest.mark.parametrize("m,n,k", [(1000, 1000, 1024), (100, 4096, 256), (1696, 2560, 256),
                                    (2400, 3200, 128), (1, 4, 128), (333, 1004, 384),
-                                   (8200, 260, 128)])
+                                   (8200, 260, 128), (4000, 4000, 512)])
 def test_gemm_masked_edge_tiles(ops, variant, m, n, k):
-    """Wave-specialised tiles on ragged C (any M, N % 4): vs fp32, and nothing
-    written outside C - C is a view into a sentinel-filled buffer with extra
-    rows below and extra columns to the right (ldc > N)."""
+    """Masked edge tiles on ragged C (wave-specialised tiles: any M, N % 4; the
+    256x256 kernel "pingpong8cm": N % 8): vs fp32, and nothing written outside
+    C - C is a view into a sentinel-filled buffer with extra rows below and
+    extra columns to the right (ldc > N)."""
+    if variant == "pingpong8cm" and n % 8:
+        pytest.skip("pingpong8cm stores 8-column chunks (N % 8)")
     a = _rand(ops, (m, k), 971 + m)
     b = _rand(ops, (n, k), 973 + n)
-    big = torch.full((m + 37, n + 12), 3.0, dtype=torch.bfloat16, device="cuda")
+    big = torch.full((m + 37, n + 16), 3.0, dtype=torch.bfloat16, device="cuda")
     c = big[:m, :n]
     ops.gemm_bf16(a, b, c, variant=variant)
     torch.cuda.synchronize()

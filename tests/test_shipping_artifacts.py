@@ -18,7 +18,8 @@ EXP = ROOT / "nvidia_terraform_modules_amd" / "ops" / "libntm_experimental.so"
 
 # K1 kernel instantiations the default dispatch may launch: pingpong8c (LDS-staged
 # epilogue when ldc % 8 == 0, register epilogue otherwise; with/without the ABFT
-# row sum; F8 = 3 is K1-fp8), pingpong8b for K % 128 != 0, and the 4 tile shapes
+# row sum; F8 = 3 is K1-fp8; EPI 26 = the masked ragged-C build), pingpong8b for
+# K % 128 != 0, and the 4 tile shapes
 # (128x128 / 256x128 / 160x160 wave-specialised, 256x160 4-wave).
 ALLOWED_K1 = {
     "ntm::gemm3::gemm_bf16_pp3_kernel<false, 8, false, 0, 0, 0>",
@@ -26,6 +27,7 @@ ALLOWED_K1 = {
     "ntm::gemm3::gemm_bf16_pp3_kernel<true, 8, false, 0, 0, 0>",
     "ntm::gemm3::gemm_bf16_pp3_kernel<true, 8, false, 10, 0, 0>",
     "ntm::gemm3::gemm_bf16_pp3_kernel<false, 8, false, 10, 0, 3>",
+    "ntm::gemm3::gemm_bf16_pp3_kernel<false, 8, false, 26, 0, 0>",  # masked edge tiles
     "ntm::gemm2::gemm_bf16_pp2_kernel<false, 0>",
     "ntm::gemm2::gemm_bf16_pp2_kernel<false, 3>",
     "ntm::gemm2::gemm_bf16_pp2_kernel<true, 0>",

@@ -1,6 +1,6 @@
 """Time manual row splits of C against the default dispatch and hipBLASLt
 (developer tool): each split "ROWS:TOPVARIANT:RESTVARIANT" runs rows [0, ROWS)
-on TOPVARIANT and the rest on RESTVARIANT (two launches), interleaved rounds,
+on TOPVARIANT and the rest on RESTVARIANT (two launches; ROWS = M: one), interleaved rounds,
 median TF/s; every split is checked against the default result (fp32 tolerance).
 
     python tools/split_check.py --shape 3200x3200x3200 --splits 1920:tile160:tile128
@@ -49,7 +49,8 @@ def main():
 
         def f(r=r, top=top, rest=rest):
             ops.gemm_bf16(a[:r], b, c[:r], variant=top)
-            ops.gemm_bf16(a[r:], b, c[r:], variant=rest)
+            if r < m:
+                ops.gemm_bf16(a[r:], b, c[r:], variant=rest)
         f()
         torch.cuda.synchronize()
         ok[sp] = bool(torch.all((c.float() - ref).abs() <= atol + rtol * ref.abs()))

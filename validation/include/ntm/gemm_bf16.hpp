@@ -277,7 +277,7 @@ __device__ __forceinline__ void tile_coords_of(int bid, int nwg, int M, int N,
   const int q = nwg >> 3, r = nwg & 7;
   const int wgid =
       (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-  const int tiles_m = M / BM, tiles_n = N / BN;
+  const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;  // ceil: masked edge tiles
   const int group = GROUP_M * tiles_n;
   const int gid = wgid / group;
   const int first_m = gid * GROUP_M;
@@ -401,7 +401,7 @@ __device__ __forceinline__ void store_tile_wide(const GemmArgs& p, const Ctx& c,
 // orders every wave's last fragment read and DMA before the overwrite.
 constexpr int kStagePitch = 528;
 
-template <bool kRowSum, bool NT>
+template <bool kRowSum, bool NT, bool MASK = false>
 __device__ __forceinline__ void store_tile_lds(const GemmArgs& p, const Ctx& c,
                                                const f32x4 (&acc)[2][2][4][2],
                                                int m0, int n0, int lane) {
@@ -437,6 +437,9 @@ __device__ __forceinline__ void store_tile_lds(const GemmArgs& p, const Ctx& c,
     const int chunk = lane & 31;
     const u32x4 val = *(const u32x4*)(c.lds + row * kStagePitch + chunk * 16);
     u32x4* dst = (u32x4*)(p.C + (size_t)(m0 + row) * p.ldc + n0 + chunk * 8);
+    if constexpr (MASK) {  // edge tile: rows >= M / 8-column chunks >= N stay unwritten
+      if (m0 + row >= p.M || n0 + chunk * 8 >= p.N) continue;
+    }
     if constexpr (NT)
       __builtin_nontemporal_store(val, dst);
     else
@@ -446,14 +449,16 @@ __device__ __forceinline__ void store_tile_lds(const GemmArgs& p, const Ctx& c,
 }
 
 // Epilogue selector for the kernels' EPI template bit mask.
-enum : int { kEpiWide = 1, kEpiNT = 2, kEpiEarly = 4, kEpiLds = 8 };
+// kEpiMask: ragged C (M, N not multiples of 256; N % 8): the LDS-staged stores
+// skip rows / column chunks past C (the kernel clamps its loads).
+enum : int { kEpiWide = 1, kEpiNT = 2, kEpiEarly = 4, kEpiLds = 8, kEpiMask = 16 };
 
 template <bool kRowSum, int EPI>
 __device__ __forceinline__ void store_tile_epi(const GemmArgs& p, const Ctx& c,
                                                const f32x4 (&acc)[2][2][4][2],
                                                int m0, int n0, int lane) {
   if constexpr ((EPI & kEpiLds) != 0)
-    store_tile_lds<kRowSum, (EPI & kEpiNT) != 0>(p, c, acc, m0, n0, lane);
+    store_tile_lds<kRowSum, (EPI & kEpiNT) != 0, (EPI & kEpiMask) != 0>(p, c, acc, m0, n0, lane);
   else if constexpr ((EPI & kEpiWide) != 0)
     store_tile_wide<kRowSum, (EPI & kEpiNT) != 0>(p, c, acc, m0, n0, lane);
   else

@@ -112,6 +112,7 @@ template <bool kRowSum, int GROUP_M = kGroupM, bool PRIO = false, int EPI = 0, i
 __global__ void __launch_bounds__(kThreads, 2)
     gemm_bf16_pp3_kernel(GemmArgs p) {
   static_assert(!((EPI & kEpiLds) && (EPI & kEpiEarly)), "LDS staging needs all waves");
+  static_assert(!(EPI & kEpiMask) || ((EPI & kEpiLds) && !kRowSum), "masked: LDS epilogue, no ABFT");
   static_assert(kLdsBytes3 >= BM * kStagePitch, "LDS staging buffer");
   __shared__ __attribute__((aligned(16))) char smem[kLdsBytes3];
 
@@ -128,12 +129,23 @@ __global__ void __launch_bounds__(kThreads, 2)
   {
     const int r = lane >> 2;
     const int cl = (lane & 3) ^ (((r >> 3) & 1) << 1);
-    const __bf16* a0 = p.A + (size_t)(m0 + c.w * 16 + r) * p.lda + cl * 8;
-    const __bf16* b0 = p.B + (size_t)(n0 + c.w * 16 + r) * p.ldb + cl * 8;
-    c.src[kALo] = a0;
-    c.src[kAHi] = a0 + (size_t)128 * p.lda;
-    c.src[kBLo] = b0;
-    c.src[kBHi] = b0 + (size_t)128 * p.ldb;
+    int ra = m0 + c.w * 16 + r, rb = n0 + c.w * 16 + r;
+    if constexpr ((EPI & kEpiMask) != 0) {
+      // Ragged C: each lane's four source rows are fixed for the whole K loop,
+      // so clamping them once keeps every load in bounds at no loop cost; the
+      // clamped rows only feed C rows / columns the epilogue does not store.
+      c.src[kALo] = p.A + (size_t)min(ra, p.M - 1) * p.lda + cl * 8;
+      c.src[kAHi] = p.A + (size_t)min(ra + 128, p.M - 1) * p.lda + cl * 8;
+      c.src[kBLo] = p.B + (size_t)min(rb, p.N - 1) * p.ldb + cl * 8;
+      c.src[kBHi] = p.B + (size_t)min(rb + 128, p.N - 1) * p.ldb + cl * 8;
+    } else {
+      const __bf16* a0 = p.A + (size_t)ra * p.lda + cl * 8;
+      const __bf16* b0 = p.B + (size_t)rb * p.ldb + cl * 8;
+      c.src[kALo] = a0;
+      c.src[kAHi] = a0 + (size_t)128 * p.lda;
+      c.src[kBLo] = b0;
+      c.src[kBHi] = b0 + (size_t)128 * p.ldb;
+    }
   }
   c.frag_off = (lane & 15) * 64 + ((lane >> 4) ^ ((lane >> 2) & 2)) * 16;
 
@@ -208,6 +220,23 @@ inline hipError_t launch_gemm_bf16_pp3(const GemmArgs& a, hipStream_t stream) {
     hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, kGroupM, false, kEpiDefault>), g, b, 0, stream, a);
   else
     hipLaunchKernelGGL(gemm_bf16_pp3_kernel<false>, g, b, 0, stream, a);
+  return hipGetLastError();
+}
+
+// Ragged C on the 256x256 kernel ("pingpong8cm"): any M, N % 8 (16-B row
+// chunks of the LDS-staged epilogue), K % 128; edge tiles clamp their loads
+// and mask their stores. No ABFT row sum.
+inline bool shape_ok3m(int M, int N, int K) {
+  return M > 0 && N > 0 && (N % 8) == 0 && K >= 2 * BK && (K % (2 * BK)) == 0;
+}
+
+inline hipError_t launch_gemm_bf16_pp3_masked(const GemmArgs& a, hipStream_t stream) {
+  if (!shape_ok3m(a.M, a.N, a.K) || a.rowsum || a.lda < a.K || a.ldb < a.K || a.ldc < a.N ||
+      (a.lda % 8) || (a.ldb % 8) || (a.ldc % 8))
+    return hipErrorInvalidValue;
+  const dim3 g((unsigned)(((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN))), b(kThreads);
+  hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, kGroupM, false, kEpiDefault | kEpiMask>), g, b, 0,
+                     stream, a);
   return hipGetLastError();
 }
 

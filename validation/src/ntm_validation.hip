@@ -116,14 +116,17 @@ inline K1Plan plan_k1(int M, int N, int K) {
   };
   // top candidates: index -1 = the 256x256 kernel, else kSmallTiles[t]
   const int nsmall = (int)(sizeof(kSmallTiles) / sizeof(kSmallTiles[0]));
+  // the 256x256 kernel on ragged C: variant 22 (masked edge tiles, N % 8, K % 128)
+  const bool big_masked_ok = N % 8 == 0 && K % 128 == 0 && K >= 128;
   for (int t = -1; t < nsmall; ++t) {
     const int tm = t < 0 ? 256 : kSmallTiles[t].tm;
-    if (t < 0 && !big_ok) continue;
+    if (t < 0 && !big_ok && !big_masked_ok) continue;
     if (t >= 0 && !small_ok(kSmallTiles[t], kSmallTiles[t].tm)) continue;
-    const bool masked = t >= 0 && kSmallTiles[t].masked;
+    const bool masked = t >= 0 ? kSmallTiles[t].masked : big_masked_ok;
     for (int m1 = tm; m1 < M + (masked ? tm : 1); m1 += tm) {
       if (m1 > M) m1 = M;  // masked kernel: the whole of C, last tile row partial
-      const double top = t < 0 ? rounds((m1 / 256.0) * (N / 256.0)) * 4.0
+      const bool big_exact = t < 0 && big_ok && m1 % 256 == 0;
+      const double top = t < 0 ? rounds((double)((m1 + 255) / 256) * ((N + 255) / 256)) * 4.0
                                : small_cost(kSmallTiles[t], m1);
       const int rest = M - m1;
       for (int r = 0; r < nsmall; ++r) {
@@ -140,7 +143,7 @@ inline K1Plan plan_k1(int M, int N, int K) {
           best_cost = cost;
           best_launches = launches;
           best_big_rows = big_rows;
-          best = K1Plan{m1, t < 0 ? big_variant : kSmallTiles[t].variant,
+          best = K1Plan{m1, t < 0 ? (big_exact ? big_variant : 22) : kSmallTiles[t].variant,
                         rest > 0 ? kSmallTiles[r].variant : (t < 0 ? 15 : kSmallTiles[t].variant)};
         }
       }
@@ -196,6 +199,8 @@ NTM_API int ntm_gemm_bf16_variant(int variant, const void* A, const void* B,
     case 16: return (int)ntm::gemmt::launch_gemm_bf16_tile_ws<8>(a, S(stream));
     case 17: return (int)ntm::gemmt::launch_gemm_bf16_tile_ws<5, 5>(a, S(stream));
     case 18: return (int)ntm::gemmt::launch_gemm_bf16_tile<8, 5>(a, S(stream));
+    // 256x256 on ragged C: clamped loads, masked LDS-staged stores
+    case 22: return (int)ntm::gemm3::launch_gemm_bf16_pp3_masked(a, S(stream));
     default: return (int)hipErrorInvalidValue;  // experimental variants: libntm_experimental.so
   }
 }
