@@ -156,7 +156,7 @@ def gemm_fp8(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
     if k != kb:
         raise ValueError(f"K mismatch: a has {k}, b has {kb}")
     if not gemm_fp8_shape_ok(m, n, k):
-        raise ValueError(f"shape ({m},{n},{k}) not tiled by the fp8 kernel (M, N, K % 256)")
+        raise ValueError(f"shape ({m},{n},{k}) not served by the fp8 kernel (K % 256, N % 8)")
     if out is None:
         out = torch.empty((m, n), dtype=torch.bfloat16, device=a.device)
     _require(out, "out", torch.bfloat16)

@@ -407,6 +407,22 @@ def test_gemm_fp8_operand_map_probe(ops):
     assert torch.equal(got, ref)
 
 
+@pytest.mark.parametrize("m,n,k", [(1000, 1000, 512), (300, 2056, 256), (4000, 4000, 256)])
+def test_gemm_fp8_masked_edge_tiles(ops, m, n, k):
+    """K1-fp8 on ragged C (masked build): vs fp32, nothing written outside C."""
+    a = _rand_fp8((m, k), 17 + m)
+    b = _rand_fp8((n, k), 19 + n)
+    big = torch.full((m + 21, n + 16), 3.0, dtype=torch.bfloat16, device="cuda")
+    c = big[:m, :n]
+    ops.gemm_fp8(a, b, c)
+    torch.cuda.synchronize()
+    ref = a.float() @ b.float().T
+    atol, rtol = ops.gemm_tolerance(k)
+    err = (c.float() - ref).abs()
+    assert torch.all(err <= atol + rtol * ref.abs()), float(err.max())
+    assert torch.all(big[m:] == 3.0) and torch.all(big[:, n:] == 3.0)
+
+
 def test_gemm_fp8_rejects_bad_shapes(ops):
     a = torch.zeros((256, 128), dtype=torch.float8_e4m3fn, device="cuda")
     with pytest.raises(ValueError):

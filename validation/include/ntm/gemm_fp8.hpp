@@ -32,10 +32,14 @@ __device__ __forceinline__ f32x4 mfma_f8(const i32x8& a, const i32x8& b, f32x4 c
 // C[M x N] (bf16) = A[M x K] (e4m3) * B[N x K]^T (e4m3), fp32 accumulation,
 // on the pingpong8c schedule (gemm_bf16_pp3.hpp, F8 = true) with its default
 // LDS-staged epilogue. lda / ldb / ldc in elements (fp8 for A/B, bf16 for C).
-// Shape rule: M, N % 256, K % 256 (128-value K-tiles, an even count), 16-byte
-// aligned rows.
-__host__ __device__ inline bool shape_ok(int M, int N, int K) {
+// Shape rule: K % 256 (128-value K-tiles, an even count), 16-byte aligned rows;
+// M, N % 256 run the exact build, any M with N % 8 the masked one (edge tiles
+// clamp their DMA source rows and skip stores past C, gemm_bf16_pp3.hpp).
+__host__ __device__ inline bool shape_exact(int M, int N, int K) {
   return M > 0 && N > 0 && K >= 256 && (M % 256) == 0 && (N % 256) == 0 && (K % 256) == 0;
+}
+__host__ __device__ inline bool shape_ok(int M, int N, int K) {
+  return M > 0 && N > 0 && K >= 256 && (N % 8) == 0 && (K % 256) == 0;
 }
 
 inline hipError_t launch_gemm_fp8(const void* A, const void* B, __bf16* C, int M, int N, int K,
@@ -54,14 +58,19 @@ inline hipError_t launch_gemm_fp8(const void* A, const void* B, __bf16* C, int M
   a.lda = lda / 2;
   a.ldb = ldb / 2;
   a.ldc = ldc;
-  const dim3 g((unsigned)((M / BM) * (N / BN))), b(kThreads);
+  const dim3 g((unsigned)(((M + BM - 1) / BM) * ((N + BN - 1) / BN))), b(kThreads);
   // F8 = 3: the plain v_mfma_f32_16x16x128_f8f6f4 (no v_mfma_ld_scale_b32
   // prefix; the hardware's default scales are 2^0, bit-identical results):
   // +1 % at 8192^3, +2.5 % at 4096^3, +3.6 % at 6144^3 over the scaled form
   // with unit VGPR scales in 15 interleaved rounds (profiles/r1_fp8b/knobs_plain.log).
-  hipLaunchKernelGGL((::ntm::gemm3::gemm_bf16_pp3_kernel<false, kGroupM, false,
-                                                         ::ntm::gemm3::kEpiDefault, 0, 3>),
-                     g, b, 0, stream, a);
+  using ::ntm::gemm3::kEpiDefault;
+  if (shape_exact(M, N, K))
+    hipLaunchKernelGGL((::ntm::gemm3::gemm_bf16_pp3_kernel<false, kGroupM, false, kEpiDefault, 0, 3>),
+                       g, b, 0, stream, a);
+  else
+    hipLaunchKernelGGL((::ntm::gemm3::gemm_bf16_pp3_kernel<false, kGroupM, false,
+                                                           kEpiDefault | kEpiMask, 0, 3>),
+                       g, b, 0, stream, a);
   return hipGetLastError();
 }
 
