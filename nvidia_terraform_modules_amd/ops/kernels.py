@@ -51,14 +51,14 @@ TILE_SHAPES = {"tile128": (128, 128), "tile256x128": (256, 128), "tile160": (160
                "tile160w4": (160, 160)}
 
 
-# wave-specialised tile kernels: any M, N (N % 4 == 0), partial edge tiles masked
+# wave-specialised tile kernels: any M, N % 4, K % 8 (edge tiles and the K tail masked)
 MASKED_TILES = frozenset({"tile128", "tile256x128", "tile160"})
 
 
 def _tile128_shape_ok(m: int, n: int, k: int, tm: int = 128, tn: int = 128,
                       masked: bool = False) -> bool:
     if masked:
-        return m > 0 and n > 0 and n % 4 == 0 and k >= 128 and k % 128 == 0
+        return m > 0 and n > 0 and n % 4 == 0 and k > 0 and k % 8 == 0
     return m > 0 and n > 0 and m % tm == 0 and n % tn == 0 and k >= 128 and k % 128 == 0
 
 
@@ -102,8 +102,8 @@ def gemm_bf16(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
     if variant in TILE_SHAPES:
         tm, tn = TILE_SHAPES[variant]
         if not _tile128_shape_ok(m, n, k, tm, tn, masked=variant in MASKED_TILES):
-            raise ValueError(f"shape ({m},{n},{k}) not tiled by the {tm}x{tn} kernel "
-                             "(K % 128; exact tiles unless masked, N % 4)")
+            raise ValueError(f"shape ({m},{n},{k}) not served by the {tm}x{tn} kernel "
+                             "(masked tiles: N % 4, K % 8; others: whole tiles, K % 128)")
     elif variant == "default":
         k1_plan(m, n, k)        # the native plan is the one authority on what it serves
     elif variant == "pingpong8cm":  # 256x256 with masked edge tiles

@@ -60,9 +60,10 @@ def test_plan_is_well_formed(k1_plan, m, n, k):
 
 
 @pytest.mark.parametrize("m,n,k", [(1000, 1000, 1024), (100, 4096, 4096), (8200, 8192, 8192),
-                                   (3000, 5000, 2048), (1, 4, 128)])
+                                   (3000, 5000, 2048), (1, 4, 128), (384, 256, 192),
+                                   (1000, 1000, 1000), (64, 64, 8)])
 def test_plan_serves_ragged_shapes(k1_plan, m, n, k):
-    """Masked edge tiles: any M and N % 4 == 0 with K % 128 == 0 has a plan."""
+    """Masked edge tiles and K tails: any M, N % 4 == 0 and K % 8 == 0 has a plan."""
     top, top_variant, _ = k1_plan(m, n, k)
     assert 0 < top <= m
 
@@ -72,11 +73,12 @@ def test_plan_rejects_bad_args(k1_plan):
         k1_plan(0, 256, 256)
 
 
-@pytest.mark.parametrize("m,n,k", [(384, 256, 192), (100, 256, 192), (256, 256, 64),
+@pytest.mark.parametrize("m,n,k", [(384, 256, 100), (100, 256, 12), (256, 256, 4),
                                    (256, 6, 128)])
 def test_plan_reports_infeasible_shapes(k1_plan, m, n, k):
-    """No kernel combination tiles these: the plan says so instead of returning
-    a plan whose second launch would fail after the first one wrote C (ADVICE r1:
-    (384,256,192) used to launch 256 rows, then fail)."""
+    """No kernel serves these (K % 8 or N % 4): the plan says so instead of
+    returning a plan whose second launch would fail after the first one wrote C
+    ((384,256,192) used to launch 256 rows, then fail - it is now
+    served whole by the masked 128x128 tiles)."""
     with pytest.raises(ValueError):
         k1_plan(m, n, k)

@@ -69,7 +69,7 @@ def test_gemm_rejects_bad_shapes(ops):
     with pytest.raises(ValueError):
         ops.gemm_bf16(a, a[:256], variant="pingpong8c")  # 256x256 kernel: M % 256
     with pytest.raises(ValueError):
-        ops.gemm_bf16(b[:, :64], b[:, :64])  # K < 128
+        ops.gemm_bf16(b[:, :60], b[:, :60])  # K % 8
 
 
 def test_fill_uniform_distribution(ops):
@@ -302,24 +302,25 @@ def test_gemm_default_dispatch_mixed_tiles(ops, m, n, k, plan):
 
 
 def test_gemm_default_rejects_unplannable_shape_before_launch(ops):
-    """an infeasible plan must fail before anything is written."""
-    a = _rand(ops, (384, 192), 5)
-    b = _rand(ops, (256, 192), 6)
+    """an infeasible plan must fail before anything is written
+    (K % 8 != 0: no kernel can load the rows in 16-byte chunks)."""
+    a = _rand(ops, (384, 104), 5)[:, :100]
+    b = _rand(ops, (256, 104), 6)[:, :100]
     c = torch.full((384, 256), 7.0, dtype=torch.bfloat16, device="cuda")
     with pytest.raises(ValueError):
         ops.gemm_bf16(a, b, c)
     with pytest.raises(RuntimeError):           # the C ABI alone rejects it too
         from nvidia_terraform_modules_amd.ops._lib import check, lib, stream_handle
         check(lib().ntm_gemm_bf16_variant(0, a.data_ptr(), b.data_ptr(), c.data_ptr(), 384, 256,
-                                          192, 192, 192, 256, stream_handle()), "default")
+                                          100, 104, 104, 256, stream_handle()), "default")
     torch.cuda.synchronize()
     assert torch.all(c == 7.0)
 
 
 def test_gemm_tile128_rejects_bad_shapes(ops):
-    a = torch.zeros((128, 192), dtype=torch.bfloat16, device="cuda")
+    a = torch.zeros((128, 192), dtype=torch.bfloat16, device="cuda")[:, :100]
     with pytest.raises(ValueError):
-        ops.gemm_bf16(a, a, variant="tile128")    # K % 128
+        ops.gemm_bf16(a, a, variant="tile128")    # K % 8
     a = torch.zeros((192, 128), dtype=torch.bfloat16, device="cuda")
     b = torch.zeros((6, 128), dtype=torch.bfloat16, device="cuda")
     with pytest.raises(ValueError):
@@ -332,14 +333,16 @@ def test_gemm_tile128_rejects_bad_shapes(ops):
                                      "default"])
 @pytest.mark.parametrize("m,n,k", [(1000, 1000, 1024), (100, 4096, 256), (1696, 2560, 256),
                                    (2400, 3200, 128), (1, 4, 128), (333, 1004, 384),
-                                   (8200, 260, 128), (4000, 4000, 512)])
+                                   (8200, 260, 128), (4000, 4000, 512), (1000, 1000, 1000),
+                                   (333, 1004, 200), (100, 512, 72), (64, 64, 8)])
 def test_gemm_masked_edge_tiles(ops, variant, m, n, k):
-    """Masked edge tiles on ragged C (wave-specialised tiles: any M, N % 4; the
-    256x256 kernel "pingpong8cm": N % 8): vs fp32, and nothing written outside
-    C - C is a view into a sentinel-filled buffer with extra rows below and
-    extra columns to the right (ldc > N)."""
-    if variant == "pingpong8cm" and n % 8:
-        pytest.skip("pingpong8cm stores 8-column chunks (N % 8)")
+    """Masked edge tiles on ragged C (wave-specialised tiles: any M, N % 4 and a
+    zero-filled partial last K-tile for K % 8; the 256x256 kernel "pingpong8cm":
+    N % 8, K % 128): vs fp32, and nothing written outside C - C is a view into
+    a sentinel-filled buffer with extra rows below and extra columns to the
+    right (ldc > N)."""
+    if variant == "pingpong8cm" and (n % 8 or k % 128):
+        pytest.skip("pingpong8cm: N % 8 (8-column store chunks), K % 128")
     a = _rand(ops, (m, k), 971 + m)
     b = _rand(ops, (n, k), 973 + n)
     big = torch.full((m + 37, n + 16), 3.0, dtype=torch.bfloat16, device="cuda")

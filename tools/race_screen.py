@@ -28,7 +28,8 @@ SHAPES = [(256, 256, 128), (256, 512, 256), (512, 768, 384), (2304, 1536, 640),
 SHAPES_160 = [(160, 160, 128), (1280, 800, 384), (2560, 1600, 640), (2560, 2560, 2560),
               (5120, 5120, 1280)]
 # ragged C for the masked (wave-specialised) tiles and the default dispatch
-SHAPES_RAGGED = [(1000, 1000, 1024), (1696, 2560, 640), (333, 1004, 384), (2400, 3200, 512)]
+SHAPES_RAGGED = [(1000, 1000, 1024), (1696, 2560, 640), (333, 1004, 384), (2400, 3200, 512),
+                 (1000, 1000, 1000), (333, 1004, 200)]  # the last two: partial K-tiles
 MASKED = ("tile128", "tile256x128", "tile160", "default")
 SHAPES_FP8 = [(256, 256, 256), (256, 512, 512), (512, 768, 768), (2304, 1536, 1280),
               (4096, 4352, 1024), (4096, 4096, 4096), (8192, 8192, 8192)]

@@ -304,9 +304,10 @@ inline hipError_t launch_gemm_bf16_tile(const GemmArgs& a, hipStream_t stream) {
 //        kernel above's, so results are bitwise equal to it.
 // Same shape rule as the kernel above.
 // Shape rule of the wave-specialised kernel: any M, N with N % 4 == 0 (8-byte
-// C stores); K % 128 as the 4-wave kernel.
+// C stores), any K with K % 8 == 0 (16-byte source chunks; a partial last
+// K-tile reads zeros past K, see issue_piece_ws).
 __host__ __device__ inline bool shape_ok_ws(int M, int N, int K) {
-  return M > 0 && N > 0 && (N % 4) == 0 && K >= 2 * TK && (K % (2 * TK)) == 0;
+  return M > 0 && N > 0 && (N % 4) == 0 && K > 0 && (K % 8) == 0;
 }
 
 template <int MT, int NT>
@@ -333,43 +334,52 @@ __device__ __forceinline__ void read_half(const CtxT& c, FragsT<MT, NT>& f, int 
 // Edge tiles (M or N not a multiple of the tile): a piece's source row is
 // clamped to the last row of A / B, so every load stays in bounds; the rows
 // and columns of C it feeds beyond M / N are computed but never stored.
+// Partial last K-tile (K % 64 != 0): a lane whose 8-element chunk starts at
+// k >= K takes its 16 bytes from a zero block instead, so the LDS image holds
+// zeros past K in both operands - same instruction count, so every counted
+// vmcnt stays exact, and no load leaves the row.
 struct Clamp {
   const __bf16* A;
   const __bf16* B;
   int a_row, b_row;  // this lane's first row (tile origin + lane / 4)
   int a_last, b_last;
   int lda, ldb, col;  // col: this lane's swizzled 8-element column chunk
+  int K;
 };
 
-template <int MT, int NT>
-__device__ __forceinline__ void issue_piece_clamped(const CtxT& c, const Clamp& q, int kt, int T,
-                                                    int i) {
+__device__ __attribute__((aligned(16))) const unsigned kZeroChunk[4] = {0u, 0u, 0u, 0u};
+
+template <int MT, int NT, bool CLAMP, bool TAIL>
+__device__ __forceinline__ void issue_piece_ws(const CtxT& c, const Clamp& q, int kt, int T,
+                                               int i) {
   using C = Cfg<MT, NT>;
   const bool real = kt < T;
   const bool is_a = i < MT;
   const int g = is_a ? c.w * MT + i : c.w * NT + (i - MT);
   const int rb = g >> 1, kh = g & 1;
-  const size_t koff = (size_t)(real ? kt : T - 1) * TK + kh * 32;
+  const int kcol = (real ? kt : T - 1) * TK + kh * 32;
   char* slot = c.lds + (kt % C::S) * C::kSlot;
-  const __bf16* src = is_a ? q.A + (size_t)min(q.a_row + rb * 16, q.a_last) * q.lda
-                           : q.B + (size_t)min(q.b_row + rb * 16, q.b_last) * q.ldb;
+  const __bf16* src;
+  if constexpr (CLAMP)
+    src = (is_a ? q.A + (size_t)min(q.a_row + rb * 16, q.a_last) * q.lda
+                : q.B + (size_t)min(q.b_row + rb * 16, q.b_last) * q.ldb) + q.col + kcol;
+  else
+    src = (is_a ? c.a_src + rb * c.a_rb16 : c.b_src + rb * c.b_rb16) + kcol;
+  if constexpr (TAIL) {
+    if (kcol + q.col >= q.K) src = (const __bf16*)kZeroChunk;
+  }
   char* dst = real ? slot + (is_a ? 0 : C::kA) + (rb * 2 + kh) * 1024
                    : c.lds + C::kScratch + c.w * 1024;
-  glds16(src + q.col + koff, dst);
+  glds16(src, dst);
 }
 
 // Producer loop of the wave-specialised kernel (see below).
-template <int MT, int NT, int KNOB, bool CLAMP>
+template <int MT, int NT, int KNOB, bool CLAMP, bool TAIL>
 __device__ __forceinline__ void ws_produce(const CtxT& c, const Clamp& q, int T) {
   using C = Cfg<MT, NT>;
   constexpr int LA = (KNOB & kWsShallow) ? C::S - 2 : C::S - 1;  // tiles issued ahead
   constexpr int VM = (LA - 1) * C::P;
-  auto issue = [&](int kt, int i) {
-    if constexpr (CLAMP)
-      issue_piece_clamped<MT, NT>(c, q, kt, T, i);
-    else
-      issue_piece<MT, NT>(c, kt, T, i);
-  };
+  auto issue = [&](int kt, int i) { issue_piece_ws<MT, NT, CLAMP, TAIL>(c, q, kt, T, i); };
 #pragma unroll
   for (int s = 0; s < LA; ++s)
 #pragma unroll
@@ -395,7 +405,7 @@ __global__ void __launch_bounds__(2 * kThreadsT, 1) gemm_bf16_tile_ws_kernel(Gem
   const int m0 = tm * C::TM, n0 = tn * C::TN;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int T = p.K / TK;
+  const int T = (p.K + TK - 1) / TK;  // a partial last K-tile reads zeros past K
 
   CtxT c;
   c.lds = smem;
@@ -413,13 +423,19 @@ __global__ void __launch_bounds__(2 * kThreadsT, 1) gemm_bf16_tile_ws_kernel(Gem
   c.frag_off = (lane & 15) * 64 + ((lane >> 4) ^ ((lane >> 2) & 2)) * 16;
 
   if (wave >= 4) {  // producer
-    if (m0 + C::TM > p.M || n0 + C::TN > p.N) {  // edge tile (uniform branch)
-      const int r = lane >> 2;
-      Clamp q{p.A, p.B, m0 + r, n0 + r, p.M - 1, p.N - 1, p.lda, p.ldb,
-              ((lane & 3) ^ (((r >> 3) & 1) << 1)) * 8};
-      ws_produce<MT, NT, KNOB, true>(c, q, T);
+    const int r = lane >> 2;
+    const Clamp q{p.A, p.B, m0 + r, n0 + r, p.M - 1, p.N - 1, p.lda, p.ldb,
+                  ((lane & 3) ^ (((r >> 3) & 1) << 1)) * 8, p.K};
+    const bool edge = m0 + C::TM > p.M || n0 + C::TN > p.N;  // uniform branches
+    if (p.K % TK) {
+      if (edge)
+        ws_produce<MT, NT, KNOB, true, true>(c, q, T);
+      else
+        ws_produce<MT, NT, KNOB, false, true>(c, q, T);
+    } else if (edge) {
+      ws_produce<MT, NT, KNOB, true, false>(c, q, T);
     } else {
-      ws_produce<MT, NT, KNOB, false>(c, Clamp{}, T);
+      ws_produce<MT, NT, KNOB, false, false>(c, q, T);
     }
     return;
   }

@@ -74,7 +74,7 @@ constexpr double kCUs = 256.0;
 struct SmallTile {
   int variant, tm, tn;
   double eff;
-  bool masked;  // wave-specialised kernel: any M, N (N % 4), partial edge tiles masked
+  bool masked;  // wave-specialised kernel: any M, N % 4, K % 8 (edge tiles / K tail masked)
 };
 constexpr SmallTile kSmallTiles[] = {{15, 128, 128, 0.60, true},
                                      {16, 256, 128, 0.78, true},
@@ -106,9 +106,9 @@ inline K1Plan plan_k1(int M, int N, int K) {
   double best_cost = inf;
   int best_launches = 3, best_big_rows = -1;
   if (M <= 0 || N <= 0 || K <= 0) return best;
-  auto small_ok = [&](const SmallTile& st, int rows) {
-    const bool mn = st.masked ? N % 4 == 0 : rows % st.tm == 0 && N % st.tn == 0;
-    return mn && K % 128 == 0 && K >= 128;
+  auto small_ok = [&](const SmallTile& st, int rows) {  // masked: any M, N % 4, K % 8
+    if (st.masked) return N % 4 == 0 && K % 8 == 0;
+    return rows % st.tm == 0 && N % st.tn == 0 && K % 128 == 0 && K >= 128;
   };
   auto small_cost = [&](const SmallTile& st, int rows) {  // edge tiles cost a whole tile
     const double tiles = (double)((rows + st.tm - 1) / st.tm) * ((N + st.tn - 1) / st.tn);
