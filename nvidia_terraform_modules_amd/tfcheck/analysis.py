@@ -51,7 +51,7 @@ import re
 from dataclasses import dataclass
 from pathlib import Path
 
-from .config import Module, load_module, provider_of_type
+from .config import Module, load_module
 from .hcl import (Block, Body, Call, Literal, ObjectExpr, Template, Traversal, iter_calls,
                   iter_strings, key_name, walk_refs)
 

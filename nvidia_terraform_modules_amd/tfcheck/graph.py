@@ -18,7 +18,7 @@ from dataclasses import dataclass, field
 from pathlib import Path
 
 from .analysis import module_exprs
-from .config import Module, load_module, provider_of_type
+from .config import Module, load_module
 from .hcl import Traversal, walk_refs
 
 

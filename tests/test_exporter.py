@@ -1,6 +1,5 @@
 """amdgpu-exporter (validation/src/amdgpu_exporter.cpp): Prometheus text
 format, no-GPU behaviour on CPU, real metrics + HTTP serving on MI355X."""
-import os
 import re
 import signal
 import socket
