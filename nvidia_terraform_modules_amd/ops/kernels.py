@@ -106,9 +106,9 @@ def gemm_bf16(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
                              "(masked tiles: N % 4, K % 8; others: whole tiles, K % 128)")
     elif variant == "default":
         k1_plan(m, n, k)        # the native plan is the one authority on what it serves
-    elif variant == "pingpong8cm":  # 256x256 with masked edge tiles
-        if not (m > 0 and n > 0 and n % 8 == 0 and k >= 128 and k % 128 == 0):
-            raise ValueError(f"shape ({m},{n},{k}) not served by pingpong8cm (N % 8, K % 128)")
+    elif variant == "pingpong8cm":  # 256x256 with masked edge tiles and K tail
+        if not (m > 0 and n > 0 and n % 8 == 0 and k > 0 and k % 8 == 0):
+            raise ValueError(f"shape ({m},{n},{k}) not served by pingpong8cm (N % 8, K % 8)")
     elif not gemm_shape_ok(m, n, k):
         raise ValueError(f"shape ({m},{n},{k}) not tiled by the 256x256x64 kernel")
     if out is None:
@@ -156,7 +156,7 @@ def gemm_fp8(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
     if k != kb:
         raise ValueError(f"K mismatch: a has {k}, b has {kb}")
     if not gemm_fp8_shape_ok(m, n, k):
-        raise ValueError(f"shape ({m},{n},{k}) not served by the fp8 kernel (K % 256, N % 8)")
+        raise ValueError(f"shape ({m},{n},{k}) not served by the fp8 kernel (N % 8, K % 16)")
     if out is None:
         out = torch.empty((m, n), dtype=torch.bfloat16, device=a.device)
     _require(out, "out", torch.bfloat16)

@@ -26,7 +26,7 @@ def k1_plan():
     (3072, 3072, 3072, 3072, "pingpong8c", None),    # whole rounds: 256x256 only
     (4096, 4096, 4096, 4096, "pingpong8c", None),
     (8192, 8192, 8192, 8192, "pingpong8c", None),
-    (8192, 8192, 8128, 8192, "pingpong8b", None),    # K % 128 != 0: the K % 64 kernel
+    (8192, 8192, 8128, 8192, "pingpong8cm", None),   # K % 128 != 0: partial-K build
     (6144, 6144, 6144, 5376, "pingpong8c", "tile160"),  # 3 rounds -> 2 + one of masked 160x160
     (4352, 4352, 4352, 3840, "pingpong8c", "tile128"),
     (3200, 3200, 3200, 3200, "pingpong8cm", None),   # one round of masked 256x256 tiles

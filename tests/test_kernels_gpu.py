@@ -338,11 +338,11 @@ def test_gemm_tile128_rejects_bad_shapes(ops):
 def test_gemm_masked_edge_tiles(ops, variant, m, n, k):
     """Masked edge tiles on ragged C (wave-specialised tiles: any M, N % 4 and a
     zero-filled partial last K-tile for K % 8; the 256x256 kernel "pingpong8cm":
-    N % 8, K % 128): vs fp32, and nothing written outside C - C is a view into
+    N % 8, K % 8): vs fp32, and nothing written outside C - C is a view into
     a sentinel-filled buffer with extra rows below and extra columns to the
     right (ldc > N)."""
-    if variant == "pingpong8cm" and (n % 8 or k % 128):
-        pytest.skip("pingpong8cm: N % 8 (8-column store chunks), K % 128")
+    if variant == "pingpong8cm" and n % 8:
+        pytest.skip("pingpong8cm: N % 8 (8-column store chunks)")
     a = _rand(ops, (m, k), 971 + m)
     b = _rand(ops, (n, k), 973 + n)
     big = torch.full((m + 37, n + 16), 3.0, dtype=torch.bfloat16, device="cuda")
@@ -410,9 +410,11 @@ def test_gemm_fp8_operand_map_probe(ops):
     assert torch.equal(got, ref)
 
 
-@pytest.mark.parametrize("m,n,k", [(1000, 1000, 512), (300, 2056, 256), (4000, 4000, 256)])
+@pytest.mark.parametrize("m,n,k", [(1000, 1000, 512), (300, 2056, 256), (4000, 4000, 256),
+                                   (1000, 1000, 1008), (256, 256, 16), (300, 2056, 400)])
 def test_gemm_fp8_masked_edge_tiles(ops, m, n, k):
-    """K1-fp8 on ragged C (masked build): vs fp32, nothing written outside C."""
+    """K1-fp8 on ragged C (masked build; K % 256 != 0 adds the zero-filled
+    partial last K-tile): vs fp32, nothing written outside C."""
     a = _rand_fp8((m, k), 17 + m)
     b = _rand_fp8((n, k), 19 + n)
     big = torch.full((m + 21, n + 16), 3.0, dtype=torch.bfloat16, device="cuda")
@@ -427,9 +429,9 @@ def test_gemm_fp8_masked_edge_tiles(ops, m, n, k):
 
 
 def test_gemm_fp8_rejects_bad_shapes(ops):
-    a = torch.zeros((256, 128), dtype=torch.float8_e4m3fn, device="cuda")
+    a = torch.zeros((256, 136), dtype=torch.float8_e4m3fn, device="cuda")[:, :120]
     with pytest.raises(ValueError):
-        ops.gemm_fp8(a, a)                       # K % 256
+        ops.gemm_fp8(a, a)                       # K % 16
     with pytest.raises(ValueError):
         ops.gemm_fp8(a.to(torch.bfloat16), a.to(torch.bfloat16))
 

@@ -29,6 +29,8 @@ ALLOWED_K1 = {
     "ntm::gemm3::gemm_bf16_pp3_kernel<false, 8, false, 10, 0, 3>",
     "ntm::gemm3::gemm_bf16_pp3_kernel<false, 8, false, 26, 0, 0>",  # masked edge tiles
     "ntm::gemm3::gemm_bf16_pp3_kernel<false, 8, false, 26, 0, 3>",  # K1-fp8, masked
+    "ntm::gemm3::gemm_bf16_pp3_kernel<false, 8, false, 58, 0, 0>",  # masked + partial K
+    "ntm::gemm3::gemm_bf16_pp3_kernel<false, 8, false, 58, 0, 3>",  # K1-fp8, masked + partial K
     "ntm::gemm2::gemm_bf16_pp2_kernel<false, 0>",
     "ntm::gemm2::gemm_bf16_pp2_kernel<false, 3>",
     "ntm::gemm2::gemm_bf16_pp2_kernel<true, 0>",

@@ -41,12 +41,14 @@ def main():
         c = torch.empty((m, n), dtype=torch.bfloat16, device="cuda")
         fns = {"default": lambda: ops.gemm_bf16(a, b, c),
                "torch": lambda: torch.matmul(a, b.T, out=c)}
+        exact_k = k % 128 == 0
         if m % 128 == 0 and n % 128 == 0:
             fns["tile128"] = lambda: ops.gemm_bf16(a, b, c, variant="tile128")
-        if m % 256 == 0 and n % 256 == 0:
+        if m % 256 == 0 and n % 256 == 0 and exact_k:
             fns["pingpong8c"] = lambda: ops.gemm_bf16(a, b, c, variant="pingpong8c")
         for v, (tm, tn) in ops.kernels.TILE_SHAPES.items():
-            if v != "tile128" and m % tm == 0 and n % tn == 0:
+            if v != "tile128" and m % tm == 0 and n % tn == 0 and (
+                    exact_k or v in ops.kernels.MASKED_TILES):
                 fns[v] = lambda v=v: ops.gemm_bf16(a, b, c, variant=v)
         t = {name: [] for name in fns}
         for _ in range(args.rounds):

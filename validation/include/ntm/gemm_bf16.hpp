@@ -112,6 +112,8 @@ struct Ctx {
   const __bf16* src[4];  // per-lane glds source for each half, K-tile 0
   int frag_off;          // per-lane byte offset of an MFMA fragment read
   int w, wr, wc;         // wave id, wave row (0..1), wave col (0..3)
+  int K;                 // partial-K builds only (kEpiKTail): K, in elements
+  int lane_col;          //   and this lane's 8-element source chunk offset
 };
 
 // Issue the two glds of this wave for half-tile H of K-tile kt into buffer.
@@ -451,7 +453,11 @@ __device__ __forceinline__ void store_tile_lds(const GemmArgs& p, const Ctx& c,
 // Epilogue selector for the kernels' EPI template bit mask.
 // kEpiMask: ragged C (M, N not multiples of 256; N % 8): the LDS-staged stores
 // skip rows / column chunks past C (the kernel clamps its loads).
-enum : int { kEpiWide = 1, kEpiNT = 2, kEpiEarly = 4, kEpiLds = 8, kEpiMask = 16 };
+// kEpiKTail (with kEpiMask): K % 128 != 0 - chunks past K load zeros (a build
+// flag that rides on the EPI mask, like kEpiMask it changes the loads too).
+enum : int { kEpiWide = 1, kEpiNT = 2, kEpiEarly = 4, kEpiLds = 8, kEpiMask = 16, kEpiKTail = 32 };
+
+__device__ __attribute__((aligned(16))) const unsigned kZeroChunk16[4] = {0u, 0u, 0u, 0u};
 
 template <bool kRowSum, int EPI>
 __device__ __forceinline__ void store_tile_epi(const GemmArgs& p, const Ctx& c,

@@ -44,18 +44,25 @@ struct Frags3 {
 };
 
 // Stage half H of K-tile kt into buffer buf, or a dummy piece if kt >= T.
-template <int H>
+// TAIL (partial-K build): a lane chunk starting at k >= K loads 16 zero bytes.
+template <int H, bool TAIL = false>
 __device__ __forceinline__ void issue_half3(const Ctx& c, int kt, int buf, int T) {
   const bool real = kt < T;
   const int k_eff = real ? kt : T - 1;
   const __bf16* s = c.src[H] + (size_t)k_eff * BK;
   const int off = real ? buf * kTileBytes + H * kHalfBytes : kScratch;
   char* d = c.lds + off + (2 * c.w) * 1024;
-  glds16(s, d);
-  glds16(s + 32, d + 1024);
+  if constexpr (TAIL) {
+    const int col = k_eff * BK + c.lane_col;
+    glds16(col < c.K ? s : (const __bf16*)kZeroChunk16, d);
+    glds16(col + 32 < c.K ? s + 32 : (const __bf16*)kZeroChunk16, d + 1024);
+  } else {
+    glds16(s, d);
+    glds16(s + 32, d + 1024);
+  }
 }
 
-template <int P, bool ODD, bool PRIO, int F8 = 0>
+template <int P, bool ODD, bool PRIO, int F8 = 0, bool TAIL = false>
 __device__ __forceinline__ void phase3(const Ctx& c, Frags3& f,
                                        f32x4 (&acc)[2][2][4][2], int t, int T) {
   bf16x8(&bcur)[2][2] = ODD ? f.b1 : f.b0;
@@ -65,10 +72,10 @@ __device__ __forceinline__ void phase3(const Ctx& c, Frags3& f,
   if constexpr (P == 1) read_b<kBHi>(c, both, cur);
   if constexpr (P == 2) read_a<kAHi>(c, f.a, cur);
   if constexpr (P == 3) read_b<kBLo>(c, both, cur ^ 1);  // tile t+1 (junk at t = T-1)
-  if constexpr (P == 0) issue_half3<kAHi>(c, t + 1, cur ^ 1, T);
-  if constexpr (P == 1) issue_half3<kBLo>(c, t + 2, cur, T);
-  if constexpr (P == 2) issue_half3<kALo>(c, t + 2, cur, T);
-  if constexpr (P == 3) issue_half3<kBHi>(c, t + 2, cur, T);
+  if constexpr (P == 0) issue_half3<kAHi, TAIL>(c, t + 1, cur ^ 1, T);
+  if constexpr (P == 1) issue_half3<kBLo, TAIL>(c, t + 2, cur, T);
+  if constexpr (P == 2) issue_half3<kALo, TAIL>(c, t + 2, cur, T);
+  if constexpr (P == 3) issue_half3<kBHi, TAIL>(c, t + 2, cur, T);
   wait_vmcnt<10>();
   raw_barrier();
   if constexpr (F8) {
@@ -85,13 +92,13 @@ __device__ __forceinline__ void phase3(const Ctx& c, Frags3& f,
   raw_barrier();
 }
 
-template <bool ODD, bool PRIO, int F8 = 0>
+template <bool ODD, bool PRIO, int F8 = 0, bool TAIL = false>
 __device__ __forceinline__ void tile3(const Ctx& c, Frags3& f,
                                       f32x4 (&acc)[2][2][4][2], int t, int T) {
-  phase3<0, ODD, PRIO, F8>(c, f, acc, t, T);
-  phase3<1, ODD, PRIO, F8>(c, f, acc, t, T);
-  phase3<2, ODD, PRIO, F8>(c, f, acc, t, T);
-  phase3<3, ODD, PRIO, F8>(c, f, acc, t, T);
+  phase3<0, ODD, PRIO, F8, TAIL>(c, f, acc, t, T);
+  phase3<1, ODD, PRIO, F8, TAIL>(c, f, acc, t, T);
+  phase3<2, ODD, PRIO, F8, TAIL>(c, f, acc, t, T);
+  phase3<3, ODD, PRIO, F8, TAIL>(c, f, acc, t, T);
 }
 
 // GROUP_M / PRIO are tuning knobs (tools/gemm_check.py --variants knobN). The
@@ -113,6 +120,8 @@ __global__ void __launch_bounds__(kThreads, 2)
     gemm_bf16_pp3_kernel(GemmArgs p) {
   static_assert(!((EPI & kEpiLds) && (EPI & kEpiEarly)), "LDS staging needs all waves");
   static_assert(!(EPI & kEpiMask) || ((EPI & kEpiLds) && !kRowSum), "masked: LDS epilogue, no ABFT");
+  static_assert(!(EPI & kEpiKTail) || (EPI & kEpiMask), "partial K rides on the masked build");
+  constexpr bool TAIL = (EPI & kEpiKTail) != 0;
   static_assert(kLdsBytes3 >= BM * kStagePitch, "LDS staging buffer");
   __shared__ __attribute__((aligned(16))) char smem[kLdsBytes3];
 
@@ -160,16 +169,33 @@ __global__ void __launch_bounds__(kThreads, 2)
         for (int n = 0; n < 2; ++n) acc[i][j][m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   Frags3 f;
-  const int T = p.K / BK;
+  // partial-K build: ceil(K / 64) K-tiles rounded up to an even count (the
+  // loop body is two K-tiles); chunks past K load zeros
+  const int T = TAIL ? ((p.K + 2 * BK - 1) / (2 * BK)) * 2 : p.K / BK;
+  if constexpr (TAIL) {
+    c.K = p.K;
+    const int r = lane >> 2;
+    c.lane_col = ((lane & 3) ^ (((r >> 3) & 1) << 1)) * 8;  // as in the source setup above
+  }
 
   // prologue: B-lo0 A-lo0 B-hi0 A-hi0 B-lo1 A-lo1 B-hi1 (virtual phases -7..-1)
-  issue_half<kBLo>(c, 0, 0);
-  issue_half<kALo>(c, 0, 0);
-  issue_half<kBHi>(c, 0, 0);
-  issue_half<kAHi>(c, 0, 0);
-  issue_half<kBLo>(c, 1, 1);
-  issue_half<kALo>(c, 1, 1);
-  issue_half<kBHi>(c, 1, 1);
+  if constexpr (TAIL) {
+    issue_half3<kBLo, true>(c, 0, 0, T);
+    issue_half3<kALo, true>(c, 0, 0, T);
+    issue_half3<kBHi, true>(c, 0, 0, T);
+    issue_half3<kAHi, true>(c, 0, 0, T);
+    issue_half3<kBLo, true>(c, 1, 1, T);
+    issue_half3<kALo, true>(c, 1, 1, T);
+    issue_half3<kBHi, true>(c, 1, 1, T);
+  } else {
+    issue_half<kBLo>(c, 0, 0);
+    issue_half<kALo>(c, 0, 0);
+    issue_half<kBHi>(c, 0, 0);
+    issue_half<kAHi>(c, 0, 0);
+    issue_half<kBLo>(c, 1, 1);
+    issue_half<kALo>(c, 1, 1);
+    issue_half<kBHi>(c, 1, 1);
+  }
   wait_vmcnt<10>();
   raw_barrier();
   read_b<kBLo>(c, f.b0, 0);
@@ -178,9 +204,25 @@ __global__ void __launch_bounds__(kThreads, 2)
     if (c.wr == SPRIO - 1) __builtin_amdgcn_s_setprio(1);
   }
 
-  for (int t = 0; t < T; t += 2) {
-    tile3<false, PRIO, F8>(c, f, acc, t, T);
-    tile3<true, PRIO, F8>(c, f, acc, t + 1, T);
+  if constexpr (TAIL) {
+    // Iteration t issues K-tiles up to t+3; until that reaches the partial
+    // one (ceil(K/64) - 1) the plain issue path runs, so the per-lane zero
+    // selects cost nothing in the bulk of the loop.
+    const int t_real = (p.K + BK - 1) / BK;
+    int t = 0;
+    for (; t + 4 < t_real; t += 2) {
+      tile3<false, PRIO, F8, false>(c, f, acc, t, T);
+      tile3<true, PRIO, F8, false>(c, f, acc, t + 1, T);
+    }
+    for (; t < T; t += 2) {
+      tile3<false, PRIO, F8, true>(c, f, acc, t, T);
+      tile3<true, PRIO, F8, true>(c, f, acc, t + 1, T);
+    }
+  } else {
+    for (int t = 0; t < T; t += 2) {
+      tile3<false, PRIO, F8>(c, f, acc, t, T);
+      tile3<true, PRIO, F8>(c, f, acc, t + 1, T);
+    }
   }
   if constexpr (SPRIO != 0) __builtin_amdgcn_s_setprio(0);
   if constexpr (F8) mfma_drain();  // asm MFMAs: results must land before VALU reads
@@ -224,10 +266,10 @@ inline hipError_t launch_gemm_bf16_pp3(const GemmArgs& a, hipStream_t stream) {
 }
 
 // Ragged C on the 256x256 kernel ("pingpong8cm"): any M, N % 8 (16-B row
-// chunks of the LDS-staged epilogue), K % 128; edge tiles clamp their loads
-// and mask their stores. No ABFT row sum.
+// chunks of the LDS-staged epilogue), K % 8 (K % 128 != 0: the partial-K
+// build); edge tiles clamp their loads and mask their stores. No ABFT row sum.
 inline bool shape_ok3m(int M, int N, int K) {
-  return M > 0 && N > 0 && (N % 8) == 0 && K >= 2 * BK && (K % (2 * BK)) == 0;
+  return M > 0 && N > 0 && (N % 8) == 0 && K > 0 && (K % 8) == 0;
 }
 
 inline hipError_t launch_gemm_bf16_pp3_masked(const GemmArgs& a, hipStream_t stream) {
@@ -235,8 +277,12 @@ inline hipError_t launch_gemm_bf16_pp3_masked(const GemmArgs& a, hipStream_t str
       (a.lda % 8) || (a.ldb % 8) || (a.ldc % 8))
     return hipErrorInvalidValue;
   const dim3 g((unsigned)(((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN))), b(kThreads);
-  hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, kGroupM, false, kEpiDefault | kEpiMask>), g, b, 0,
-                     stream, a);
+  if (a.K % (2 * BK))
+    hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, kGroupM, false, kEpiDefault | kEpiMask | kEpiKTail>),
+                       g, b, 0, stream, a);
+  else
+    hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, kGroupM, false, kEpiDefault | kEpiMask>), g, b, 0,
+                       stream, a);
   return hipGetLastError();
 }
 

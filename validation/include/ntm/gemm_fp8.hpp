@@ -32,14 +32,15 @@ __device__ __forceinline__ f32x4 mfma_f8(const i32x8& a, const i32x8& b, f32x4 c
 // C[M x N] (bf16) = A[M x K] (e4m3) * B[N x K]^T (e4m3), fp32 accumulation,
 // on the pingpong8c schedule (gemm_bf16_pp3.hpp, F8 = true) with its default
 // LDS-staged epilogue. lda / ldb / ldc in elements (fp8 for A/B, bf16 for C).
-// Shape rule: K % 256 (128-value K-tiles, an even count), 16-byte aligned rows;
-// M, N % 256 run the exact build, any M with N % 8 the masked one (edge tiles
-// clamp their DMA source rows and skip stores past C, gemm_bf16_pp3.hpp).
+// Shape rule: 16-byte aligned rows; M, N, K % 256 run the exact build; any M
+// with N % 8 and K % 16 the masked one (edge tiles clamp their DMA source rows
+// and skip stores past C; a partial last K-tile loads zeros past K;
+// gemm_bf16_pp3.hpp).
 __host__ __device__ inline bool shape_exact(int M, int N, int K) {
   return M > 0 && N > 0 && K >= 256 && (M % 256) == 0 && (N % 256) == 0 && (K % 256) == 0;
 }
 __host__ __device__ inline bool shape_ok(int M, int N, int K) {
-  return M > 0 && N > 0 && K >= 256 && (N % 8) == 0 && (K % 256) == 0;
+  return M > 0 && N > 0 && K > 0 && (N % 8) == 0 && (K % 16) == 0;  // K % 256: exact K loop
 }
 
 inline hipError_t launch_gemm_fp8(const void* A, const void* B, __bf16* C, int M, int N, int K,
@@ -66,6 +67,10 @@ inline hipError_t launch_gemm_fp8(const void* A, const void* B, __bf16* C, int M
   using ::ntm::gemm3::kEpiDefault;
   if (shape_exact(M, N, K))
     hipLaunchKernelGGL((::ntm::gemm3::gemm_bf16_pp3_kernel<false, kGroupM, false, kEpiDefault, 0, 3>),
+                       g, b, 0, stream, a);
+  else if (K % 256)  // partial last K-tile: 16-value chunks past K load zeros
+    hipLaunchKernelGGL((::ntm::gemm3::gemm_bf16_pp3_kernel<false, kGroupM, false,
+                                                           kEpiDefault | kEpiMask | kEpiKTail, 0, 3>),
                        g, b, 0, stream, a);
   else
     hipLaunchKernelGGL((::ntm::gemm3::gemm_bf16_pp3_kernel<false, kGroupM, false,

@@ -100,7 +100,13 @@ struct K1Plan {
 inline K1Plan plan_k1(int M, int N, int K) {
   auto rounds = [](double tiles) { return tiles <= 0 ? 0.0 : __builtin_ceil(tiles / kCUs); };
   const double inf = 1e300;
-  const bool big_ok = N % 256 == 0 && K % 64 == 0 && K >= 128;
+  // the 256x256 kernel on whole tiles: pingpong8c (K % 128). K % 128 != 0 goes
+  // to the masked build's partial-K path (22), measured faster than pingpong8b
+  // (8192x8192x8000: 1634 vs 1472 TF/s, profiles/r2_ws/ktail_pp2_vs_cm.log); the
+  // pingpong8b clause below only matters if that build ever cannot serve a shape
+  const bool big_masked_ok = N % 8 == 0 && K % 8 == 0;
+  const bool big_ok = N % 256 == 0 && K >= 128 &&
+                      (K % 128 == 0 || (K % 64 == 0 && !big_masked_ok));
   const int big_variant = K % 128 == 0 ? kDefaultVariant : 4;
   K1Plan best{-1, 15, 15};
   double best_cost = inf;
@@ -116,8 +122,7 @@ inline K1Plan plan_k1(int M, int N, int K) {
   };
   // top candidates: index -1 = the 256x256 kernel, else kSmallTiles[t]
   const int nsmall = (int)(sizeof(kSmallTiles) / sizeof(kSmallTiles[0]));
-  // the 256x256 kernel on ragged C: variant 22 (masked edge tiles, N % 8, K % 128)
-  const bool big_masked_ok = N % 8 == 0 && K % 128 == 0 && K >= 128;
+  // the 256x256 kernel on ragged C: variant 22 (masked edge tiles, N % 8, K % 8)
   for (int t = -1; t < nsmall; ++t) {
     const int tm = t < 0 ? 256 : kSmallTiles[t].tm;
     if (t < 0 && !big_ok && !big_masked_ok) continue;
@@ -126,6 +131,7 @@ inline K1Plan plan_k1(int M, int N, int K) {
     for (int m1 = tm; m1 < M + (masked ? tm : 1); m1 += tm) {
       if (m1 > M) m1 = M;  // masked kernel: the whole of C, last tile row partial
       const bool big_exact = t < 0 && big_ok && m1 % 256 == 0;
+      if (t < 0 && !big_exact && !big_masked_ok) continue;
       const double top = t < 0 ? rounds((double)((m1 + 255) / 256) * ((N + 255) / 256)) * 4.0
                                : small_cost(kSmallTiles[t], m1);
       const int rest = M - m1;
