@@ -33,29 +33,39 @@ def main():
     ap.add_argument("--shapes", default="2048x2048x2048")
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--only-default", action="store_true",
+                    help="time the default dispatch and hipBLASLt only (shape sweeps)")
+    ap.add_argument("--random", type=int, default=0,
+                    help="append N random shapes (M, N % 8, K % 8 in [256, 8192], seeded)")
     args = ap.parse_args()
-    for sh in args.shapes.split(","):
-        m, n, k = (int(x) for x in sh.split("x"))
+    shapes = [tuple(int(x) for x in sh.split("x")) for sh in args.shapes.split(",") if sh]
+    if args.random:
+        import random
+        rng = random.Random(20261016)
+        shapes += [tuple(rng.randrange(256, 8193, 8) for _ in range(3)) for _ in range(args.random)]
+    for m, n, k in shapes:
         a = ops.fill_uniform_(torch.empty((m, k), dtype=torch.bfloat16, device="cuda"), 1)
         b = ops.fill_uniform_(torch.empty((n, k), dtype=torch.bfloat16, device="cuda"), 2)
         c = torch.empty((m, n), dtype=torch.bfloat16, device="cuda")
         fns = {"default": lambda: ops.gemm_bf16(a, b, c),
                "torch": lambda: torch.matmul(a, b.T, out=c)}
         exact_k = k % 128 == 0
-        if m % 128 == 0 and n % 128 == 0:
-            fns["tile128"] = lambda: ops.gemm_bf16(a, b, c, variant="tile128")
-        if m % 256 == 0 and n % 256 == 0 and exact_k:
-            fns["pingpong8c"] = lambda: ops.gemm_bf16(a, b, c, variant="pingpong8c")
-        for v, (tm, tn) in ops.kernels.TILE_SHAPES.items():
-            if v != "tile128" and m % tm == 0 and n % tn == 0 and (
-                    exact_k or v in ops.kernels.MASKED_TILES):
-                fns[v] = lambda v=v: ops.gemm_bf16(a, b, c, variant=v)
+        if not args.only_default:
+            if m % 128 == 0 and n % 128 == 0:
+                fns["tile128"] = lambda: ops.gemm_bf16(a, b, c, variant="tile128")
+            if m % 256 == 0 and n % 256 == 0 and exact_k:
+                fns["pingpong8c"] = lambda: ops.gemm_bf16(a, b, c, variant="pingpong8c")
+            for v, (tm, tn) in ops.kernels.TILE_SHAPES.items():
+                if v != "tile128" and m % tm == 0 and n % tn == 0 and (
+                        exact_k or v in ops.kernels.MASKED_TILES):
+                    fns[v] = lambda v=v: ops.gemm_bf16(a, b, c, variant=v)
         t = {name: [] for name in fns}
         for _ in range(args.rounds):
             for name, fn in fns.items():
                 t[name].append(timed(fn, args.iters))
         fl = 2.0 * m * n * k
-        row = {"shape": [m, n, k], "tiles256": (m // 256) * (n // 256)}
+        row = {"shape": [m, n, k], "tiles256": (m // 256) * (n // 256),
+               "plan": list(ops.kernels.k1_plan(m, n, k))}
         for name, v in t.items():
             v.sort()
             row[f"{name}_tflops"] = round(fl / v[len(v) // 2] / 1e9, 1)
