@@ -44,6 +44,12 @@ def _declare(lib: ctypes.CDLL) -> None:
         "ntm_abft_result_bytes": ([], c_int),
         "ntm_fill_uniform_bf16": ([c_vp, c_size, ctypes.c_ulonglong, c_float, c_vp], c_int),
         "ntm_k1_plan": ([c_int, c_int, c_int, c_vp, c_vp, c_vp], c_int),
+        "ntm_k1_plan_splitk": ([c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp], c_int),
+        "ntm_gemm_bf16_ex": ([c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp,
+                              c_size, c_vp], c_int),
+        "ntm_splitk_ws_bytes": ([c_int, c_int, c_int, c_int], c_size),
+        "ntm_gemm_bf16_splitk": ([c_int, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int,
+                                  c_int, c_int, c_vp, c_size, c_vp], c_int),
         "ntm_fill_uniform_e4m3": ([c_vp, c_size, ctypes.c_ulonglong, c_float, c_vp], c_int),
         "ntm_ref_gemm_f32_e4m3": (
             [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp], c_int),

@@ -76,13 +76,42 @@ def k1_plan(m: int, n: int, k: int) -> tuple[int, str, str]:
     return top.value, names[tv.value], names[rest.value]
 
 
+def k1_splitk_plan(m: int, n: int, k: int) -> tuple[int, str, str, int]:
+    """The default dispatch's plan with split-K allowed (what ``gemm_bf16``
+    runs): ``k1_plan``'s triple plus the number of K slices (1 = unsplit; > 1 =
+    all of C on the top kernel, a masked small tile, in that many K slices)."""
+    top, tv, rest, sp = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    rc = lib().ntm_k1_plan_splitk(m, n, k, ctypes.byref(top), ctypes.byref(tv),
+                                  ctypes.byref(rest), ctypes.byref(sp))
+    if rc != 0:
+        raise ValueError(f"shape ({m},{n},{k}) not tiled by the K1 kernels")
+    names = {v: kname for kname, v in GEMM_VARIANTS.items()}
+    return top.value, names[tv.value], names[rest.value], sp.value
+
+
+# (M, N, K) -> split-K workspace bytes of the default plan (0 = unsplit); a
+# plan is validated once per shape
+_DEFAULT_WS: dict[tuple[int, int, int], int] = {}
+
+
+def _default_ws_bytes(m: int, n: int, k: int) -> int:
+    key = (m, n, k)
+    wsb = _DEFAULT_WS.get(key)
+    if wsb is None:
+        _, _, _, sp = k1_splitk_plan(m, n, k)  # raises if no kernel serves the shape
+        wsb = lib().ntm_splitk_ws_bytes(m, n, k, sp) if sp > 1 else 0
+        _DEFAULT_WS[key] = wsb
+    return wsb
+
+
 def gemm_bf16(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
-              variant: str = "default") -> torch.Tensor:
+              variant: str = "default", splits: int = 1) -> torch.Tensor:
     """K1: ``out = a @ b.T`` in bf16 with fp32 accumulation on MFMA.
 
     a: [M, K] bf16, b: [N, K] bf16 (both K-contiguous), out: [M, N] bf16.
     ``variant``: "default" = the tile shape with the smallest predicted time
-    (rounds of 256 CUs x tile area / efficiency, ``k1_plan``): "tile128" /
+    (rounds of 256 CUs x tile area / efficiency, ``k1_plan``; split-K on a small
+    tile when C cannot fill the chip and K is long, ``k1_splitk_plan``): "tile128" /
     "tile256x128" / "tile160" / "tile256x160" (128x128 / 256x128 / 160x160 /
     256x160 tiles, K % 128; the first three with 4 LDS-DMA producer + 4 MFMA
     consumer waves and masked edge tiles (any M, N % 4), 256x160 with 4 waves
@@ -92,6 +121,8 @@ def gemm_bf16(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
     fastest measured), "pingpong8" (the first 12/4/8/0 schedule), or the
     experimental "wave128"/"wave128d4" (4 waves, 128x128 per wave,
     AGPR-pinned accumulators) - see validation/include.
+    ``splits`` > 1 (masked tiles only): split-K into that many K slices, fp32
+    partials in a workspace from PyTorch's allocator, then one reduction kernel.
     """
     _require(a, "a", torch.bfloat16)
     _require(b, "b", torch.bfloat16)
@@ -105,7 +136,7 @@ def gemm_bf16(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
             raise ValueError(f"shape ({m},{n},{k}) not served by the {tm}x{tn} kernel "
                              "(masked tiles: N % 4, K % 8; others: whole tiles, K % 128)")
     elif variant == "default":
-        k1_plan(m, n, k)        # the native plan is the one authority on what it serves
+        _default_ws_bytes(m, n, k)  # the native plan is the one authority on what it serves
     elif variant == "pingpong8cm":  # 256x256 with masked edge tiles and K tail
         if not (m > 0 and n > 0 and n % 8 == 0 and k > 0 and k % 8 == 0):
             raise ValueError(f"shape ({m},{n},{k}) not served by pingpong8cm (N % 8, K % 8)")
@@ -116,6 +147,16 @@ def gemm_bf16(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
     _require(out, "out", torch.bfloat16)
     if tuple(out.shape) != (m, n):
         raise ValueError("out has the wrong shape")
+    if splits > 1:
+        if variant not in MASKED_TILES:
+            raise ValueError(f"split-K runs on {sorted(MASKED_TILES)}, not {variant}")
+        ws_bytes = lib().ntm_splitk_ws_bytes(m, n, k, splits)
+        ws = torch.empty((ws_bytes + 3) // 4, dtype=torch.float32, device=a.device)
+        rc = lib().ntm_gemm_bf16_splitk(
+            GEMM_VARIANTS[variant], splits, a.data_ptr(), b.data_ptr(), out.data_ptr(), m, n, k,
+            a.stride(0), b.stride(0), out.stride(0), ws.data_ptr(), ws_bytes, stream_handle())
+        check(rc, "ntm_gemm_bf16_splitk")
+        return out
     if variant.startswith("knob"):            # experimental tuning sweep: "knob<N>"
         rc = lib_experimental().ntm_gemm_bf16_knob(
             int(variant[4:]), a.data_ptr(), b.data_ptr(), out.data_ptr(), m, n, k, a.stride(0),
@@ -127,6 +168,14 @@ def gemm_bf16(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
             GEMM_VARIANTS[variant], a.data_ptr(), b.data_ptr(), out.data_ptr(), m, n, k,
             a.stride(0), b.stride(0), out.stride(0), stream_handle())
         check(rc, "ntm_gemm_bf16_experimental")
+        return out
+    if variant == "default" and _default_ws_bytes(m, n, k):
+        wsb = _default_ws_bytes(m, n, k)
+        ws = torch.empty((wsb + 3) // 4, dtype=torch.float32, device=a.device)
+        rc = lib().ntm_gemm_bf16_ex(a.data_ptr(), b.data_ptr(), out.data_ptr(), m, n, k,
+                                    a.stride(0), b.stride(0), out.stride(0), ws.data_ptr(), wsb,
+                                    stream_handle())
+        check(rc, "ntm_gemm_bf16_ex")
         return out
     rc = lib().ntm_gemm_bf16_variant(
         GEMM_VARIANTS[variant], a.data_ptr(), b.data_ptr(), out.data_ptr(), m, n, k,

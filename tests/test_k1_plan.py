@@ -82,3 +82,42 @@ def test_plan_reports_infeasible_shapes(k1_plan, m, n, k):
     served whole by the masked 128x128 tiles)."""
     with pytest.raises(ValueError):
         k1_plan(m, n, k)
+
+
+@pytest.fixture(scope="module")
+def splitk_plan(k1_plan):
+    from nvidia_terraform_modules_amd.ops.kernels import k1_splitk_plan as f
+
+    return f
+
+
+@pytest.mark.parametrize("m,n,k,variant,splits", [
+    (280, 6352, 7568, "tile160", 3),       # 80 tiles of 160x160 -> 240 in one round
+    (256, 8192, 8192, "tile256x128", 4),   # 64 tiles -> 256
+    (128, 8192, 8192, "tile128", 4),
+    (792, 3416, 6104, "tile160", 2),
+])
+def test_splitk_plan_for_skinny_long_k(splitk_plan, m, n, k, variant, splits):
+    """C too small to fill 256 CUs with a long K: split-K on a masked small tile."""
+    assert splitk_plan(m, n, k) == (m, variant, variant, splits)
+
+
+@pytest.mark.parametrize("m,n,k", [(8192, 8192, 8192), (4096, 4096, 4096), (5624, 752, 5880),
+                                   (4672, 1472, 6696), (1000, 3112, 768), (3200, 3200, 3200),
+                                   (6144, 6144, 6144), (2080, 3844, 256)])
+def test_splitk_plan_keeps_unsplit_plan(k1_plan, splitk_plan, m, n, k):
+    """Chip-filling C or short K: split-K is not worth its fp32 partials, and the
+    plan is exactly the unsplit one."""
+    assert splitk_plan(m, n, k) == k1_plan(m, n, k) + (1,)
+
+
+@pytest.mark.parametrize("m,n,k", [(m, n, k) for m in (64, 333, 1000, 2048)
+                                   for n in (256, 1004, 4096) for k in (1024, 4104, 16384)])
+def test_splitk_plan_is_well_formed(k1_plan, splitk_plan, m, n, k):
+    top, tv, rest, splits = splitk_plan(m, n, k)
+    assert 1 <= splits <= 16
+    if splits > 1:   # all of C on one masked small tile; K slices of >= 64
+        assert top == m and tv == rest and tv in ("tile128", "tile256x128", "tile160")
+        assert k // splits >= 32
+    else:
+        assert (top, tv, rest) == k1_plan(m, n, k)

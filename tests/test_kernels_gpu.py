@@ -358,6 +358,58 @@ def test_gemm_masked_edge_tiles(ops, variant, m, n, k):
         assert torch.equal(c, ops.gemm_bf16(a, b, variant="pingpong8"))
 
 
+@pytest.mark.parametrize("variant", ["tile128", "tile256x128", "tile160"])
+@pytest.mark.parametrize("splits", [2, 3, 5, 16])
+@pytest.mark.parametrize("m,n,k", [(280, 636, 7568), (100, 4096, 1000), (333, 1004, 2056),
+                                   (1, 4, 1032), (256, 512, 8192), (64, 64, 136)])
+def test_gemm_splitk(ops, variant, splits, m, n, k):
+    """Split-K on the masked small tiles: K slices of round_up(ceil(K / S), 64)
+    (the last one shorter, its partial K-tile zero-filled), fp32 partials, one
+    reduction: vs fp32, within the unsplit tolerance, nothing written outside C
+    (sentinel rows below and columns right of C, ldc > N)."""
+    a = _rand(ops, (m, k), 1171 + m)
+    b = _rand(ops, (n, k), 1173 + n)
+    big = torch.full((m + 19, n + 12), 3.0, dtype=torch.bfloat16, device="cuda")
+    c = big[:m, :n]
+    ops.gemm_bf16(a, b, c, variant=variant, splits=splits)
+    torch.cuda.synchronize()
+    ref = a.float() @ b.float().T
+    atol, rtol = ops.gemm_tolerance(k)
+    err = (c.float() - ref).abs()
+    assert torch.all(err <= atol + rtol * ref.abs()), float(err.max())
+    assert torch.all(big[m:] == 3.0) and torch.all(big[:, n:] == 3.0)
+
+
+@pytest.mark.parametrize("m,n,k,splits", [(280, 6352, 7568, 3), (128, 8192, 8192, 4),
+                                          (333, 1004, 2056, None)])
+def test_gemm_default_dispatch_splitk(ops, m, n, k, splits):
+    """The default dispatch takes split-K for skinny long-K C (k1_splitk_plan),
+    with a workspace from PyTorch's allocator: vs fp32, and equal to the
+    explicit split of the same tile (same slices, same reduction order)."""
+    top, tv, _, sp = ops.kernels.k1_splitk_plan(m, n, k)
+    assert top == m and sp > 1 and (splits is None or sp == splits)
+    a = _rand(ops, (m, k), 1271 + m)
+    b = _rand(ops, (n, k), 1273 + n)
+    c = ops.gemm_bf16(a, b)
+    ref = a.float() @ b.float().T
+    atol, rtol = ops.gemm_tolerance(k)
+    err = (c.float() - ref).abs()
+    assert torch.all(err <= atol + rtol * ref.abs()), float(err.max())
+    assert torch.equal(c, ops.gemm_bf16(a, b, variant=tv, splits=sp))
+
+
+def test_gemm_splitk_rejects_bad_args(ops):
+    a = torch.zeros((128, 256), dtype=torch.bfloat16, device="cuda")
+    with pytest.raises(ValueError):
+        ops.gemm_bf16(a, a, variant="pingpong8c", splits=2)   # masked small tiles only
+    from nvidia_terraform_modules_amd.ops._lib import lib
+    c = torch.zeros((128, 128), dtype=torch.bfloat16, device="cuda")
+    ws = torch.zeros(16, dtype=torch.float32, device="cuda")   # too small: nothing launched
+    rc = lib().ntm_gemm_bf16_splitk(15, 2, a.data_ptr(), a.data_ptr(), c.data_ptr(), 128, 128, 256,
+                                    256, 256, 128, ws.data_ptr(), 64, 0)
+    assert rc != 0
+
+
 def _rand_fp8(shape, seed):
     g = torch.Generator(device="cuda").manual_seed(seed)
     x = torch.rand(shape, generator=g, device="cuda") * 2 - 1      # uniform [-1, 1)

@@ -65,7 +65,7 @@ def main():
                 t[name].append(timed(fn, args.iters))
         fl = 2.0 * m * n * k
         row = {"shape": [m, n, k], "tiles256": (m // 256) * (n // 256),
-               "plan": list(ops.kernels.k1_plan(m, n, k))}
+               "plan": list(ops.kernels.k1_splitk_plan(m, n, k))}
         for name, v in t.items():
             v.sort()
             row[f"{name}_tflops"] = round(fl / v[len(v) // 2] / 1e9, 1)

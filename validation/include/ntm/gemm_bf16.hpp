@@ -67,6 +67,11 @@ struct GemmArgs {
   // optional ABFT checksum: rowsum[m] += sum_n of the fp32 accumulators of
   // row m (caller zeroes it). nullptr selects the plain kernel.
   float* rowsum = nullptr;
+  // split-K (wave-specialised tiles only): workgroup (tile, blockIdx.y = s)
+  // runs K range [s kc, (s+1) kc) and stores its fp32 partial to
+  // splitk_ws[s][M][N]; splitk_reduce_kernel sums the slices into C.
+  float* splitk_ws = nullptr;
+  int splitk_kc = 0;
 };
 
 // Shapes the fast kernel accepts; the host launcher rejects anything else.

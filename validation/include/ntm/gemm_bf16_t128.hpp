@@ -395,7 +395,7 @@ __device__ __forceinline__ void ws_produce(const CtxT& c, const Clamp& q, int T)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // dummy pieces drained
 }
 
-template <int MT, int NT = 4, int KNOB = 0>
+template <int MT, int NT = 4, int KNOB = 0, bool SPLIT = false>
 __global__ void __launch_bounds__(2 * kThreadsT, 1) gemm_bf16_tile_ws_kernel(GemmArgs p) {
   using C = Cfg<MT, NT>;
   (void)sizeof(CfgWS<MT, NT>);
@@ -405,7 +405,10 @@ __global__ void __launch_bounds__(2 * kThreadsT, 1) gemm_bf16_tile_ws_kernel(Gem
   const int m0 = tm * C::TM, n0 = tn * C::TN;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int T = (p.K + TK - 1) / TK;  // a partial last K-tile reads zeros past K
+  // split-K: this workgroup's K slice [kb, kb + klen); else the whole K
+  const int kb = SPLIT ? (int)blockIdx.y * p.splitk_kc : 0;
+  const int klen = SPLIT ? min(p.splitk_kc, p.K - kb) : p.K;
+  const int T = (klen + TK - 1) / TK;  // a partial last K-tile reads zeros past K
 
   CtxT c;
   c.lds = smem;
@@ -415,8 +418,8 @@ __global__ void __launch_bounds__(2 * kThreadsT, 1) gemm_bf16_tile_ws_kernel(Gem
   {
     const int r = lane >> 2;
     const int cl = (lane & 3) ^ (((r >> 3) & 1) << 1);
-    c.a_src = p.A + (size_t)(m0 + r) * p.lda + cl * 8;
-    c.b_src = p.B + (size_t)(n0 + r) * p.ldb + cl * 8;
+    c.a_src = p.A + (size_t)(m0 + r) * p.lda + cl * 8 + kb;
+    c.b_src = p.B + (size_t)(n0 + r) * p.ldb + cl * 8 + kb;
     c.a_rb16 = (size_t)16 * p.lda;
     c.b_rb16 = (size_t)16 * p.ldb;
   }
@@ -424,10 +427,10 @@ __global__ void __launch_bounds__(2 * kThreadsT, 1) gemm_bf16_tile_ws_kernel(Gem
 
   if (wave >= 4) {  // producer
     const int r = lane >> 2;
-    const Clamp q{p.A, p.B, m0 + r, n0 + r, p.M - 1, p.N - 1, p.lda, p.ldb,
-                  ((lane & 3) ^ (((r >> 3) & 1) << 1)) * 8, p.K};
+    const Clamp q{p.A + kb, p.B + kb, m0 + r, n0 + r, p.M - 1, p.N - 1, p.lda, p.ldb,
+                  ((lane & 3) ^ (((r >> 3) & 1) << 1)) * 8, klen};
     const bool edge = m0 + C::TM > p.M || n0 + C::TN > p.N;  // uniform branches
-    if (p.K % TK) {
+    if (klen % TK) {
       if (edge)
         ws_produce<MT, NT, KNOB, true, true>(c, q, T);
       else
@@ -474,6 +477,18 @@ __global__ void __launch_bounds__(2 * kThreadsT, 1) gemm_bf16_tile_ws_kernel(Gem
   }
 
   ::ntm::gemm::mfma_drain();
+  if constexpr (SPLIT) {  // split-K: the fp32 partial of slice blockIdx.y
+    float* w = p.splitk_ws + (size_t)blockIdx.y * p.M * p.N;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        const int row = m0 + c.wr * (16 * MT) + mt * 16 + (lane & 15);
+        const int col = n0 + c.wc * (16 * NT) + nt * 16 + (lane >> 4) * 4;
+        if (row < p.M && col < p.N) *(f32x4*)(w + (size_t)row * p.N + col) = acc[mt][nt];
+      }
+    return;
+  }
   typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
@@ -492,6 +507,25 @@ __global__ void __launch_bounds__(2 * kThreadsT, 1) gemm_bf16_tile_ws_kernel(Gem
     }
 }
 
+// Split-K reduction: C = bf16(sum over S slices of ws[s][M][N]) (N % 4).
+__global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* ws, __bf16* C, int M,
+                                                            int N, int ldc, int S) {
+  typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+  const size_t n4 = (size_t)M * N / 4, slice = (size_t)M * N;
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (size_t)gridDim.x * 256) {
+    f32x4 v = *(const f32x4*)(ws + i * 4);
+    for (int s = 1; s < S; ++s) v += *(const f32x4*)(ws + s * slice + i * 4);
+    const size_t e = i * 4;
+    const int row = (int)(e / N), col = (int)(e % N);
+    bf16x4 o;
+    o[0] = (__bf16)v[0];
+    o[1] = (__bf16)v[1];
+    o[2] = (__bf16)v[2];
+    o[3] = (__bf16)v[3];
+    *(bf16x4*)(C + (size_t)row * ldc + col) = o;
+  }
+}
+
 template <int MT, int NT = 4, int KNOB = 0>
 inline hipError_t launch_gemm_bf16_tile_ws(const GemmArgs& a, hipStream_t stream) {
   if (!shape_ok_ws(a.M, a.N, a.K) || a.lda < a.K || a.ldb < a.K || a.ldc < a.N ||
@@ -501,6 +535,35 @@ inline hipError_t launch_gemm_bf16_tile_ws(const GemmArgs& a, hipStream_t stream
                                    ((a.N + Cfg<MT, NT>::TN - 1) / Cfg<MT, NT>::TN));
   hipLaunchKernelGGL((gemm_bf16_tile_ws_kernel<MT, NT, KNOB>), dim3(grid), dim3(2 * kThreadsT), 0,
                      stream, a);
+  return hipGetLastError();
+}
+
+// Split-K over S slices of kc = ceil(K / S) rounded up to 64 (the last slice
+// may be shorter; its partial K-tile reads zeros): the wave-specialised tile
+// kernel on a (tiles, S) grid writes fp32 partials to ws (S M N floats), then
+// splitk_reduce_kernel sums them into C. For C too small to fill the chip
+// with a long K (hipBLASLt's GSU kernels serve these shapes the same way).
+inline int splitk_kc(int K, int S) { return ((K + S - 1) / S + TK - 1) / TK * TK; }
+inline int splitk_slices(int K, int S) { const int kc = splitk_kc(K, S); return (K + kc - 1) / kc; }
+
+template <int MT, int NT>
+inline hipError_t launch_gemm_bf16_tile_ws_splitk(const GemmArgs& a, int S, float* ws,
+                                                  hipStream_t stream) {
+  if (!shape_ok_ws(a.M, a.N, a.K) || S < 1 || !ws || a.lda < a.K || a.ldb < a.K ||
+      a.ldc < a.N || (a.lda % 8) || (a.ldb % 8) || (a.ldc % 4))
+    return hipErrorInvalidValue;
+  GemmArgs b = a;
+  b.splitk_ws = ws;
+  b.splitk_kc = splitk_kc(a.K, S);
+  const int slices = splitk_slices(a.K, S);
+  const unsigned tiles = (unsigned)(((a.M + Cfg<MT, NT>::TM - 1) / Cfg<MT, NT>::TM) *
+                                    ((a.N + Cfg<MT, NT>::TN - 1) / Cfg<MT, NT>::TN));
+  hipLaunchKernelGGL((gemm_bf16_tile_ws_kernel<MT, NT, 0, true>), dim3(tiles, (unsigned)slices),
+                     dim3(2 * kThreadsT), 0, stream, b);
+  const size_t n4 = (size_t)a.M * a.N / 4;
+  const unsigned rg = (unsigned)std::min<size_t>(4096, (n4 + 255) / 256);
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(rg), dim3(256), 0, stream, ws, a.C, a.M, a.N,
+                     a.ldc, slices);
   return hipGetLastError();
 }
 

@@ -86,8 +86,20 @@ struct K1Plan {
   int top_rows;      // rows [0, top_rows) on top_variant; -1 = no plan tiles (M,N,K)
   int top_variant;   // 5 / 4 (the 256x256 kernel) or a kSmallTiles variant
   int rest_variant;  // rows [top_rows, M) on a kSmallTiles variant (15..18)
+  int splits = 1;    // > 1: all of C on top_variant (masked tile), split-K in that many slices
   bool feasible() const { return top_rows >= 0; }
 };
+
+// Split-K time model (seconds), fitted on MI355X (tools/splitk_check.py,
+// profiles/r2_splitk/): a round of tm x tn tiles over kc costs
+// 2 tm tn kc / (kPerCU eff); the fp32 partials cost kRedFixed + slices M N 4 /
+// kRedBW (partial stores in the tile epilogue + the reduction kernel, mostly
+// MALL-resident). A split plan must beat the unsplit one by kSplitKMargin.
+constexpr double kPerCU = 1650e12 / 256.0;  // the 256x256 kernel's per-CU bf16 rate
+constexpr double kRedFixed = 4e-6;
+constexpr double kRedBW = 3e12;
+constexpr double kSplitKMargin = 1.1;
+constexpr int kMaxSplits = 16;
 
 // The plan: C split by rows into a top part and a rest part, each on one tile
 // kernel in its own launch (either part may be empty). The top part runs the
@@ -97,7 +109,7 @@ struct K1Plan {
 // 128x128 (250 tiles), two full rounds instead of 1.56 rounds of 160x160
 // (977 vs 924 TF/s, hipBLASLt 948: profiles/r2_ws/split_3200.log).
 // Ties: fewer launches, then more rows on the 256x256 kernel.
-inline K1Plan plan_k1(int M, int N, int K) {
+inline K1Plan plan_k1(int M, int N, int K, bool splitk = false) {
   auto rounds = [](double tiles) { return tiles <= 0 ? 0.0 : __builtin_ceil(tiles / kCUs); };
   const double inf = 1e300;
   // the 256x256 kernel on whole tiles: pingpong8c (K % 128). K % 128 != 0 goes
@@ -155,7 +167,28 @@ inline K1Plan plan_k1(int M, int N, int K) {
       }
     }
   }
-  return best;
+  if (!splitk || !best.feasible()) return best;
+  // Split-K: C too small to fill 256 CUs with a long K (e.g. 280x6352x7568: 80
+  // tiles of 160x160 -> 3 slices of 240 tiles, 631 vs 321 TF/s unsplit).
+  const double unsplit = best_cost * 2.0 * 16384.0 * K / kPerCU;  // cost units -> seconds
+  double best_t = unsplit / kSplitKMargin;
+  K1Plan split = best;
+  for (const SmallTile& st : kSmallTiles) {
+    if (!st.masked || !small_ok(st, M)) continue;
+    const double tiles = (double)((M + st.tm - 1) / st.tm) * ((N + st.tn - 1) / st.tn);
+    for (int sp = 2; sp <= kMaxSplits; ++sp) {
+      const int slices = ntm::gemmt::splitk_slices(K, sp);
+      if (slices != sp) continue;  // the same slicing as a smaller sp
+      const double kc = ntm::gemmt::splitk_kc(K, sp);
+      const double t = rounds(tiles * slices) * 2.0 * st.tm * st.tn * kc / (kPerCU * st.eff) +
+                       kRedFixed + (double)slices * M * N * 4.0 / kRedBW;
+      if (t < best_t) {
+        best_t = t;
+        split = K1Plan{M, st.variant, st.variant, slices};
+      }
+    }
+  }
+  return split;
 }
 
 // The default dispatch's plan for (M, N, K) (host only; tests and tools).
@@ -167,6 +200,21 @@ NTM_API int ntm_k1_plan(int M, int N, int K, int* top_rows, int* top_variant, in
   *top_rows = pl.top_rows;
   *top_variant = pl.top_variant;
   *rest_variant = pl.rest_variant;
+  return 0;
+}
+
+// The same with split-K allowed (a workspace of ntm_splitk_ws_bytes(M, N, K,
+// *splits) bytes when *splits > 1): the plan ntm_gemm_bf16_ex runs.
+NTM_API int ntm_k1_plan_splitk(int M, int N, int K, int* top_rows, int* top_variant,
+                               int* rest_variant, int* splits) {
+  if (M <= 0 || N <= 0 || K <= 0 || !top_rows || !top_variant || !rest_variant || !splits)
+    return (int)hipErrorInvalidValue;
+  const K1Plan pl = plan_k1(M, N, K, true);
+  if (!pl.feasible()) return (int)hipErrorInvalidValue;
+  *top_rows = pl.top_rows;
+  *top_variant = pl.top_variant;
+  *rest_variant = pl.rest_variant;
+  *splits = pl.splits;
   return 0;
 }
 
@@ -209,6 +257,53 @@ NTM_API int ntm_gemm_bf16_variant(int variant, const void* A, const void* B,
     case 22: return (int)ntm::gemm3::launch_gemm_bf16_pp3_masked(a, S(stream));
     default: return (int)hipErrorInvalidValue;  // experimental variants: libntm_experimental.so
   }
+}
+
+// Split-K on a wave-specialised tile (15 / 16 / 17): `splits` K-slices, fp32 partials
+// in the caller's workspace ws (ntm_splitk_ws_bytes; stream-ordered, reused once
+// this call's reduction has run), then one reduction kernel writes C.
+NTM_API size_t ntm_splitk_ws_bytes(int M, int N, int K, int splits) {
+  if (M <= 0 || N <= 0 || K <= 0 || splits < 1) return 0;
+  return sizeof(float) * (size_t)ntm::gemmt::splitk_slices(K, splits) * M * N;
+}
+
+NTM_API int ntm_gemm_bf16_splitk(int variant, int splits, const void* A, const void* B, void* C,
+                                 int M, int N, int K, int lda, int ldb, int ldc, void* ws,
+                                 size_t ws_bytes, void* stream) {
+  if (splits < 1 || !ws || ws_bytes < ntm_splitk_ws_bytes(M, N, K, splits))
+    return (int)hipErrorInvalidValue;
+  ntm::gemm::GemmArgs a;
+  a.A = (const __bf16*)A;
+  a.B = (const __bf16*)B;
+  a.C = (__bf16*)C;
+  a.M = M;
+  a.N = N;
+  a.K = K;
+  a.lda = lda;
+  a.ldb = ldb;
+  a.ldc = ldc;
+  float* w = (float*)ws;
+  using namespace ntm::gemmt;
+  switch (variant) {
+    case 15: return (int)launch_gemm_bf16_tile_ws_splitk<4, 4>(a, splits, w, S(stream));
+    case 16: return (int)launch_gemm_bf16_tile_ws_splitk<8, 4>(a, splits, w, S(stream));
+    case 17: return (int)launch_gemm_bf16_tile_ws_splitk<5, 5>(a, splits, w, S(stream));
+    default: return (int)hipErrorInvalidValue;
+  }
+}
+
+// The default dispatch with split-K allowed: ws (ws_bytes) is the caller's
+// workspace; when the split-K plan needs more than ws_bytes (or ws is null) the
+// unsplit plan runs instead.
+NTM_API int ntm_gemm_bf16_ex(const void* A, const void* B, void* C, int M, int N, int K, int lda,
+                             int ldb, int ldc, void* ws, size_t ws_bytes, void* stream) {
+  if (ws) {
+    const K1Plan pl = plan_k1(M, N, K, true);
+    if (pl.feasible() && pl.splits > 1 && ws_bytes >= ntm_splitk_ws_bytes(M, N, K, pl.splits))
+      return ntm_gemm_bf16_splitk(pl.top_variant, pl.splits, A, B, C, M, N, K, lda, ldb, ldc, ws,
+                                  ws_bytes, stream);
+  }
+  return ntm_gemm_bf16_variant(0, A, B, C, M, N, K, lda, ldb, ldc, stream);
 }
 
 // K1-fp8: C (bf16) = A (e4m3) * B (e4m3)^T, fp32 accumulation (gemm_fp8.hpp).
