@@ -93,7 +93,9 @@ def splitk_plan(k1_plan):
 
 @pytest.mark.parametrize("m,n,k,variant,splits", [
     (280, 6352, 7568, "tile160", 3),       # 80 tiles of 160x160 -> 240 in one round
-    (256, 8192, 8192, "tile256x128", 4),   # 64 tiles -> 256
+    (256, 8192, 8192, "tile128", 2),       # 128 tiles -> 256
+    (512, 4096, 16384, "tile256x128", 4),  # 64 tiles -> 256
+    (1024, 1024, 16384, "tile128", 4),
     (128, 8192, 8192, "tile128", 4),
     (792, 3416, 6104, "tile160", 2),
 ])

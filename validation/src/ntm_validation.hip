@@ -90,14 +90,16 @@ struct K1Plan {
   bool feasible() const { return top_rows >= 0; }
 };
 
-// Split-K time model (seconds), fitted on MI355X (tools/splitk_check.py,
-// profiles/r2_splitk/): a round of tm x tn tiles over kc costs
-// 2 tm tn kc / (kPerCU eff); the fp32 partials cost kRedFixed + slices M N 4 /
-// kRedBW (partial stores in the tile epilogue + the reduction kernel, mostly
-// MALL-resident). A split plan must beat the unsplit one by kSplitKMargin.
+// Split-K time model (seconds), fitted on MI355X (tools/splitk_check.py, 14
+// shapes x 3 tiles x up to 6 slice counts, profiles/r2_splitk/): a round of
+// tm x tn tiles over kc costs 2 tm tn kc / (kPerCU eff); the fp32 partials cost
+// kRedFixed + slices M N 4 / kRedBW (the partial stores in the tile epilogue +
+// the reduction kernel's reads; an effective rate, not HBM's). Its picks are
+// within 3.3 % of the fastest measured split on every fitted shape. A split plan
+// must beat the unsplit one by kSplitKMargin.
 constexpr double kPerCU = 1650e12 / 256.0;  // the 256x256 kernel's per-CU bf16 rate
-constexpr double kRedFixed = 4e-6;
-constexpr double kRedBW = 3e12;
+constexpr double kRedFixed = 2e-6;
+constexpr double kRedBW = 2e12;
 constexpr double kSplitKMargin = 1.1;
 constexpr int kMaxSplits = 16;
 
