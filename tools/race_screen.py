@@ -10,7 +10,8 @@ placed too early (WAR) shows up as a changed tile.
 
     python tools/race_screen.py [--variants pingpong8b] [--repeats 200]
 
-Variant ``fp8`` screens K1-fp8 (ops.gemm_fp8, e4m3 operands, K % 256 shapes).
+Variant ``fp8`` screens K1-fp8 (ops.gemm_fp8, e4m3 operands, K % 256 shapes);
+``<tile>/s<S>`` a masked tile with split-K in S slices (skinny long-K shapes).
 """
 import argparse
 import json
@@ -31,6 +32,8 @@ SHAPES_160 = [(160, 160, 128), (1280, 800, 384), (2560, 1600, 640), (2560, 2560,
 SHAPES_RAGGED = [(1000, 1000, 1024), (1696, 2560, 640), (333, 1004, 384), (2400, 3200, 512),
                  (1000, 1000, 1000), (333, 1004, 200)]  # the last two: partial K-tiles
 MASKED = ("tile128", "tile256x128", "tile160", "pingpong8cm", "default")
+# skinny C with a long K: the default dispatch splits K here (k1_splitk_plan)
+SHAPES_SPLITK = [(280, 6352, 7568), (128, 8192, 8192), (333, 1004, 2056), (256, 2048, 8200)]
 SHAPES_FP8 = [(256, 256, 256), (256, 512, 512), (512, 768, 768), (2304, 1536, 1280),
               (4096, 4352, 1024), (4096, 4096, 4096), (8192, 8192, 8192)]
 
@@ -48,15 +51,23 @@ def main():
     report = {"repeats": args.repeats, "results": []}
     failed = False
     for v in args.variants.split(","):
+        v, _, sp = v.partition("/s")
+        splits = int(sp) if sp else 1
         fp8 = v == "fp8"
         dt = torch.float8_e4m3fn if fp8 else torch.bfloat16
 
-        def gemm(a, b, out=None, v=v, fp8=fp8):
-            return ops.gemm_fp8(a, b, out) if fp8 else ops.gemm_bf16(a, b, out, variant=v)
+        def gemm(a, b, out=None, v=v, fp8=fp8, splits=splits):
+            if fp8:
+                return ops.gemm_fp8(a, b, out)
+            return ops.gemm_bf16(a, b, out, variant=v, splits=splits)
 
         tm, tn = ops.kernels.TILE_SHAPES.get(v, (0, 0))
         shapes = SHAPES_FP8 if fp8 else SHAPES_160 if tn == 160 else SHAPES
-        for (m, n, k) in shapes + (SHAPES_RAGGED if v in MASKED else []):
+        if splits > 1:
+            shapes = SHAPES_SPLITK + SHAPES_RAGGED
+        elif v in MASKED:
+            shapes = shapes + SHAPES_RAGGED + (SHAPES_SPLITK if v == "default" else [])
+        for (m, n, k) in shapes:
             if tm and m % tm and v not in MASKED:
                 continue
             if v == "pingpong8cm" and n % 8:
@@ -80,7 +91,8 @@ def main():
                 if not torch.equal(out, first):
                     mismatches += 1
             torch.cuda.synchronize()
-            row = {"variant": v, "shape": [m, n, k], "repeats": reps, "ref_ok": ok_ref,
+            row = {"variant": v + (f"/s{splits}" if splits > 1 else ""), "shape": [m, n, k],
+                   "repeats": reps, "ref_ok": ok_ref,
                    "bitwise_mismatches": mismatches}
             failed |= (not ok_ref) or mismatches > 0
             report["results"].append(row)
