@@ -35,7 +35,8 @@ GEMM_VARIANTS = {"default": 0, "pingpong8": 1, "wave128": 2, "wave128d4": 3, "pi
                  "pingpong8ww": 9, "pingpong8cw": 10, "pingpong8cwe": 11,
                  "pingpong8cwn": 12, "pingpong8cwne": 13, "pingpong8pw": 14, "tile128": 15,
                  "tile256x128": 16, "tile160": 17, "tile256x160": 18, "tile128w4": 19,
-                 "tile256x128w4": 20, "tile160w4": 21, "pingpong8cm": 22}
+                 "tile256x128w4": 20, "tile160w4": 21, "pingpong8cm": 22, "tile160x128": 23,
+                 "tile128x160": 24}
 
 
 # variants built only into libntm_experimental.so (tests / tools): never selected
@@ -48,11 +49,11 @@ EXPERIMENTAL_VARIANTS = frozenset({"pingpong8", "wave128", "wave128d4", "pingpon
 # (TM, TN) of the 4-wave tile kernels (gemm_bf16_t128.hpp)
 TILE_SHAPES = {"tile128": (128, 128), "tile256x128": (256, 128), "tile160": (160, 160),
                "tile256x160": (256, 160), "tile128w4": (128, 128), "tile256x128w4": (256, 128),
-               "tile160w4": (160, 160)}
+               "tile160w4": (160, 160), "tile160x128": (160, 128), "tile128x160": (128, 160)}
 
 
 # wave-specialised tile kernels: any M, N % 4, K % 8 (edge tiles and the K tail masked)
-MASKED_TILES = frozenset({"tile128", "tile256x128", "tile160"})
+MASKED_TILES = frozenset({"tile128", "tile256x128", "tile160", "tile160x128", "tile128x160"})
 
 
 def _tile128_shape_ok(m: int, n: int, k: int, tm: int = 128, tn: int = 128,

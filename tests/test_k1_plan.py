@@ -27,13 +27,16 @@ def k1_plan():
     (4096, 4096, 4096, 4096, "pingpong8c", None),
     (8192, 8192, 8192, 8192, "pingpong8c", None),
     (8192, 8192, 8128, 8192, "pingpong8cm", None),   # K % 128 != 0: partial-K build
-    (6144, 6144, 6144, 5376, "pingpong8c", "tile160"),  # 3 rounds -> 2 + one of masked 160x160
+    (6144, 6144, 6144, 5376, "pingpong8c", "tile160x128"),  # 3 rounds -> 2 + one of 160x128
     (4352, 4352, 4352, 3840, "pingpong8c", "tile128"),
     (3200, 3200, 3200, 3200, "pingpong8cm", None),   # one round of masked 256x256 tiles
     (2080, 3844, 256, 512, "tile128", "tile160"),    # N % 8 != 0: mixed small tiles
     (4000, 4000, 4096, 4000, "pingpong8cm", None),
     (416, 1280, 128, 416, "tile128", None),          # masked edge tiles: one launch
-    (1696, 2560, 2560, 1696, "tile160", None),       # 11 x 16 tiles, last row 96/160 full
+    (1696, 2560, 2560, 1696, "tile160x128", None),   # 11 x 20 tiles: one round
+    (5624, 752, 5880, 5624, "tile160x128", None),    # 216 tiles vs 180 of 160x160
+    (4072, 1240, 3784, 4072, "tile128x160", None),   # 32 x 8 tiles: one full round
+    (3000, 3000, 3000, 3000, "pingpong8cm", None),   # one-round tiles stay out of 2-round plans
     (2400, 3200, 3200, 2400, "tile256x128", None),   # 10 x 25 tiles: one round
     (8200, 8192, 8192, 8192, "pingpong8c", "tile128"),  # 8 ragged rows on masked tiles
 ])
@@ -48,12 +51,12 @@ def test_plan_matches_cost_model(k1_plan, m, n, k, top, top_variant, rest):
                                    for j in range(1, 33, 5)])
 def test_plan_is_well_formed(k1_plan, m, n, k):
     top, top_variant, rest = k1_plan(m, n, k)
-    small = ("tile128", "tile256x128", "tile160", "tile256x160")
+    small = ("tile128", "tile256x128", "tile160", "tile256x160", "tile160x128", "tile128x160")
     assert 0 < top <= m and top_variant in small + ("pingpong8c", "pingpong8cm")
     assert rest in small
     tm = {"tile128": 128, "tile256x128": 256, "tile160": 160, "tile256x160": 256,
-          "pingpong8c": 256, "pingpong8cm": 256}
-    masked = ("tile128", "tile256x128", "tile160", "pingpong8cm")
+          "tile160x128": 160, "tile128x160": 128, "pingpong8c": 256, "pingpong8cm": 256}
+    masked = ("tile128", "tile256x128", "tile160", "tile160x128", "tile128x160", "pingpong8cm")
     assert top % tm[top_variant] == 0 or (top == m and top_variant in masked)
     if top < m:
         assert (m - top) % tm[rest] == 0 or rest in masked
@@ -119,7 +122,8 @@ def test_splitk_plan_is_well_formed(k1_plan, splitk_plan, m, n, k):
     top, tv, rest, splits = splitk_plan(m, n, k)
     assert 1 <= splits <= 16
     if splits > 1:   # all of C on one masked small tile; K slices of >= 64
-        assert top == m and tv == rest and tv in ("tile128", "tile256x128", "tile160")
+        assert top == m and tv == rest
+        assert tv in ("tile128", "tile256x128", "tile160", "tile160x128", "tile128x160")
         assert k // splits >= 32
     else:
         assert (top, tv, rest) == k1_plan(m, n, k)

@@ -236,13 +236,16 @@ def test_gemm_tile128_vs_torch_fp32(ops, variant, m, n, k):
         assert torch.equal(c, ops.gemm_bf16(a, b, variant=variant[:-2]))
 
 
-@pytest.mark.parametrize("variant", ["tile160", "tile256x160", "tile160w4"])
+@pytest.mark.parametrize("variant", ["tile160", "tile256x160", "tile160w4", "tile160x128",
+                                     "tile128x160"])
 @pytest.mark.parametrize("m,n,k", [(160, 160, 128), (1280, 800, 384), (2560, 2560, 2560),
-                                   (1280, 160, 1024), (2560, 1600, 256), (5120, 320, 128)])
+                                   (1280, 160, 1024), (2560, 1600, 256), (5120, 320, 128),
+                                   (640, 1280, 640)])
 def test_gemm_tile160_vs_torch_fp32(ops, variant, m, n, k):
-    """160-wide tiles (gemm_bf16_t128.hpp with NT = 5; odd MT / NT split the
-    DMA pieces across waves by global piece index): vs fp32, and bitwise equal
-    to the 128-wide tile kernel where both tile the shape (same MFMA order)."""
+    """160-wide tiles (gemm_bf16_t128.hpp with MT or NT = 5; odd MT / NT split
+    the DMA pieces across waves by global piece index): vs fp32, and bitwise
+    equal to the 128-wide tile kernel where both tile the shape (same MFMA
+    order)."""
     tm, tn = ops.kernels.TILE_SHAPES[variant]
     if m % tm or n % tn:
         pytest.skip(f"{variant} needs M % {tm}, N % {tn}")
@@ -277,7 +280,9 @@ def test_gemm_default_split_plan(ops, m, n, k):
 @pytest.mark.parametrize("m,n,k,plan", [
     (2560, 2560, 512, (2560, "tile160")),               # 256 tiles of 160x160: one round
     (416, 1280, 128, (416, "tile128")),                 # masked edge tiles, one launch
-    (1696, 2560, 256, (1696, "tile160")),               # 11 x 16 tiles, last row partial
+    (1696, 2560, 256, (1696, "tile160x128")),           # 11 x 20 tiles: one round
+    (4072, 1240, 256, (4072, "tile128x160")),           # 32 x 8 tiles: one full round
+    (4608, 4608, 128, (3584, "pingpong8c", "tile160x128")),  # one-round tile as the rest
     (2080, 3844, 256, (512, "tile128", "tile160")),     # mixed small tiles, ragged N
     (2304, 3844, 256, (768, "tile128", "tile160")),
     (3200, 3200, 256, (3200, "pingpong8cm")),           # 256x256 with masked edge tiles
@@ -329,8 +334,8 @@ def test_gemm_tile128_rejects_bad_shapes(ops):
         ops.gemm_bf16(a, a, variant="tile256x160")  # whole tiles only (M % 256)
 
 
-@pytest.mark.parametrize("variant", ["tile128", "tile256x128", "tile160", "pingpong8cm",
-                                     "default"])
+@pytest.mark.parametrize("variant", ["tile128", "tile256x128", "tile160", "tile160x128",
+                                     "tile128x160", "pingpong8cm", "default"])
 @pytest.mark.parametrize("m,n,k", [(1000, 1000, 1024), (100, 4096, 256), (1696, 2560, 256),
                                    (2400, 3200, 128), (1, 4, 128), (333, 1004, 384),
                                    (8200, 260, 128), (4000, 4000, 512), (1000, 1000, 1000),
@@ -358,7 +363,8 @@ def test_gemm_masked_edge_tiles(ops, variant, m, n, k):
         assert torch.equal(c, ops.gemm_bf16(a, b, variant="pingpong8"))
 
 
-@pytest.mark.parametrize("variant", ["tile128", "tile256x128", "tile160"])
+@pytest.mark.parametrize("variant", ["tile128", "tile256x128", "tile160", "tile160x128",
+                                     "tile128x160"])
 @pytest.mark.parametrize("splits", [2, 3, 5, 16])
 @pytest.mark.parametrize("m,n,k", [(280, 636, 7568), (100, 4096, 1000), (333, 1004, 2056),
                                    (1, 4, 1032), (256, 512, 8192), (64, 64, 136)])

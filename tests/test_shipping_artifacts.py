@@ -38,10 +38,14 @@ ALLOWED_K1 = {
     "ntm::gemmt::gemm_bf16_tile_ws_kernel<4, 4, 0, false>",
     "ntm::gemmt::gemm_bf16_tile_ws_kernel<8, 4, 0, false>",
     "ntm::gemmt::gemm_bf16_tile_ws_kernel<5, 5, 0, false>",
+    "ntm::gemmt::gemm_bf16_tile_ws_kernel<5, 4, 0, false>",
+    "ntm::gemmt::gemm_bf16_tile_ws_kernel<4, 5, 0, false>",
     # split-K builds of the same tiles (fp32 partials; splitk_reduce_kernel sums them)
     "ntm::gemmt::gemm_bf16_tile_ws_kernel<4, 4, 0, true>",
     "ntm::gemmt::gemm_bf16_tile_ws_kernel<8, 4, 0, true>",
     "ntm::gemmt::gemm_bf16_tile_ws_kernel<5, 5, 0, true>",
+    "ntm::gemmt::gemm_bf16_tile_ws_kernel<5, 4, 0, true>",
+    "ntm::gemmt::gemm_bf16_tile_ws_kernel<4, 5, 0, true>",
     "ntm::gemmt::gemm_bf16_tile_kernel<8, 5>",
 }
 EXPERIMENTAL_ONLY = ("gemm_bf16_w4_kernel", "gemm_bf16_pp4_kernel", "gemm_bf16_pp5_kernel",

@@ -31,7 +31,8 @@ SHAPES_160 = [(160, 160, 128), (1280, 800, 384), (2560, 1600, 640), (2560, 2560,
 # ragged C for the masked (wave-specialised) tiles and the default dispatch
 SHAPES_RAGGED = [(1000, 1000, 1024), (1696, 2560, 640), (333, 1004, 384), (2400, 3200, 512),
                  (1000, 1000, 1000), (333, 1004, 200)]  # the last two: partial K-tiles
-MASKED = ("tile128", "tile256x128", "tile160", "pingpong8cm", "default")
+MASKED = ("tile128", "tile256x128", "tile160", "tile160x128", "tile128x160", "pingpong8cm",
+          "default")
 # skinny C with a long K: the default dispatch splits K here (k1_splitk_plan)
 SHAPES_SPLITK = [(280, 6352, 7568), (128, 8192, 8192), (333, 1004, 2056), (256, 2048, 8200)]
 SHAPES_FP8 = [(256, 256, 256), (256, 512, 512), (512, 768, 768), (2304, 1536, 1280),

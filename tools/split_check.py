@@ -1,7 +1,8 @@
 """Time manual row splits of C against the default dispatch and hipBLASLt
 (developer tool): each split "ROWS:TOPVARIANT:RESTVARIANT" runs rows [0, ROWS)
 on TOPVARIANT and the rest on RESTVARIANT (two launches; ROWS = M: one), interleaved rounds,
-median TF/s; every split is checked against the default result (fp32 tolerance).
+median TF/s; every split is checked against the default result (fp32 tolerance). A variant
+"tile128/s8" runs split-K in 8 K slices.
 
     python tools/split_check.py --shape 3200x3200x3200 --splits 1920:tile160:tile128
 """
@@ -47,10 +48,14 @@ def main():
         rows, top, rest = sp.split(":")
         r = int(rows)
 
+        def run(x, y, z, v):
+            v, _, sk = v.partition("/s")
+            ops.gemm_bf16(x, y, z, variant=v, splits=int(sk) if sk else 1)
+
         def f(r=r, top=top, rest=rest):
-            ops.gemm_bf16(a[:r], b, c[:r], variant=top)
+            run(a[:r], b, c[:r], top)
             if r < m:
-                ops.gemm_bf16(a[r:], b, c[r:], variant=rest)
+                run(a[r:], b, c[r:], rest)
         f()
         torch.cuda.synchronize()
         ok[sp] = bool(torch.all((c.float() - ref).abs() <= atol + rtol * ref.abs()))

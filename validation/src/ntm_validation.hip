@@ -38,10 +38,11 @@ NTM_API int ntm_gemm_shape_ok(int M, int N, int K) {
 // kernel with the balanced 8/4/8/4 LDS read schedule (gemm_bf16_pp2.hpp; K %
 // 64); 5 = pingpong8c, the same schedule with parity-alternating B buffers, a
 // uniform tail-free K loop and the LDS-staged nontemporal epilogue
-// (gemm_bf16_pp3.hpp; K % 128); 15 / 16 / 17 / 18 = 128x128 / 256x128 /
-// 160x160 / 256x160 tiles (gemm_bf16_t128.hpp; K % 128): the first three on
-// the wave-specialised 8-wave kernel, 256x160 on the 4-wave one (its
-// accumulators + one fragment set do not fit 256 registers).
+// (gemm_bf16_pp3.hpp; K % 128); 15 / 16 / 17 / 23 / 24 / 18 = 128x128 /
+// 256x128 / 160x160 / 160x128 / 128x160 / 256x160 tiles (gemm_bf16_t128.hpp):
+// all but the last on the wave-specialised 8-wave kernel (masked: any M, N % 4,
+// K % 8), 256x160 on the 4-wave one (whole tiles, K % 128; its accumulators +
+// one fragment set do not fit 256 registers at two waves per SIMD).
 // 0 = default: the plan below. Variants 1-3 and 6-14 (the first ping-pong,
 // the 4-wave 128x128-per-wave kernel, the persistent kernel, the 32-MFMA
 // segment schedules, epilogue knobs) are experimental: libntm_experimental.so.
@@ -69,23 +70,35 @@ constexpr int kDefaultVariant = 5;
 // rounds). 256x160 (4-wave) is priced from a full round of it against one of
 // 256x256 at 4096x2560x4096 (1121 vs 1146 TF/s, r1_t160/policy_plan.log), not
 // from its 8192x5120 rate (0.72): at 0.72 the plan split 5120^3 and
-// 8192x5120x4096 onto it and lost 2-3 %.
+// 8192x5120x4096 onto it and lost 2-3 %. 160x128 / 128x160 (0.70): 1160 /
+// 1170 TF/s on 8 full rounds (5120x8192x4096 / 8192x5120x4096,
+// profiles/r2_tiles/); they fill a round where the square tiles leave CUs idle
+// (5624x752x5880: 216 tiles of 160x128 vs 180 of 160x160, 677 vs 616 TF/s).
 constexpr double kCUs = 256.0;
 struct SmallTile {
   int variant, tm, tn;
   double eff;
-  bool masked;  // wave-specialised kernel: any M, N % 4, K % 8 (edge tiles / K tail masked)
+  bool masked;     // wave-specialised kernel: any M, N % 4, K % 8 (edge tiles / K tail masked)
+  bool one_round;  // only where its tiles fit in one round of 256 CUs
 };
-constexpr SmallTile kSmallTiles[] = {{15, 128, 128, 0.60, true},
-                                     {16, 256, 128, 0.78, true},
-                                     {17, 160, 160, 0.72, true},
-                                     {18, 256, 160, 0.61, false}};
+// 160x128 / 128x160 are one-round tiles: filling a round the square tiles
+// leave part-idle they win 2-16 % (5624x752x5880, 4072x1240x3784, the rest
+// parts of 4608^3 / 6144^3); over 2+ rounds, in place of the 256x256 kernel's
+// one partial round, they lost 3-22 % (3000^3, 1344x6216x4848, 1616x6208x6504;
+// profiles/r2_tiles/plan_ab_*.log) - there the big kernel's partial round runs
+// faster per tile than the full-chip rate the model prices.
+constexpr SmallTile kSmallTiles[] = {{15, 128, 128, 0.60, true, false},
+                                     {16, 256, 128, 0.78, true, false},
+                                     {17, 160, 160, 0.72, true, false},
+                                     {23, 160, 128, 0.70, true, true},
+                                     {24, 128, 160, 0.70, true, true},
+                                     {18, 256, 160, 0.61, false, false}};
 constexpr double kSplitPenalty = 0.25;  // a second launch, in 128x128-tile-round units
 
 struct K1Plan {
   int top_rows;      // rows [0, top_rows) on top_variant; -1 = no plan tiles (M,N,K)
   int top_variant;   // 5 / 4 (the 256x256 kernel) or a kSmallTiles variant
-  int rest_variant;  // rows [top_rows, M) on a kSmallTiles variant (15..18)
+  int rest_variant;  // rows [top_rows, M) on a kSmallTiles variant
   int splits = 1;    // > 1: all of C on top_variant (masked tile), split-K in that many slices
   bool feasible() const { return top_rows >= 0; }
 };
@@ -132,6 +145,7 @@ inline K1Plan plan_k1(int M, int N, int K, bool splitk = false) {
   };
   auto small_cost = [&](const SmallTile& st, int rows) {  // edge tiles cost a whole tile
     const double tiles = (double)((rows + st.tm - 1) / st.tm) * ((N + st.tn - 1) / st.tn);
+    if (st.one_round && tiles > kCUs) return inf;
     return rounds(tiles) * (st.tm * st.tn / 16384.0) / st.eff;
   };
   // top candidates: index -1 = the 256x256 kernel, else kSmallTiles[t]
@@ -153,6 +167,10 @@ inline K1Plan plan_k1(int M, int N, int K, bool splitk = false) {
         if (rest > 0 && !small_ok(kSmallTiles[r], rest)) continue;
         if (rest == 0 && r > 0) break;  // no rest part: one candidate is enough
         const double cost = top + (rest > 0 ? small_cost(kSmallTiles[r], rest) + kSplitPenalty : 0.0);
+        if (cost >= inf) continue;  // a one-round tile over more than one round
+        // one-round tiles: all of C, or the rest after the 256x256 kernel's rounds
+        if (rest > 0 && t >= 0 && (kSmallTiles[t].one_round || kSmallTiles[r].one_round))
+          continue;
         const int launches = rest > 0 ? 2 : 1;
         const int big_rows = t < 0 ? m1 : 0;
         const bool better = cost < best_cost - 1e-9 ||
@@ -181,6 +199,7 @@ inline K1Plan plan_k1(int M, int N, int K, bool splitk = false) {
     for (int sp = 2; sp <= kMaxSplits; ++sp) {
       const int slices = ntm::gemmt::splitk_slices(K, sp);
       if (slices != sp) continue;  // the same slicing as a smaller sp
+      if (st.one_round && tiles * slices > kCUs) break;
       const double kc = ntm::gemmt::splitk_kc(K, sp);
       const double t = rounds(tiles * slices) * 2.0 * st.tm * st.tn * kc / (kPerCU * st.eff) +
                        kRedFixed + (double)slices * M * N * 4.0 / kRedBW;
@@ -254,6 +273,8 @@ NTM_API int ntm_gemm_bf16_variant(int variant, const void* A, const void* B,
     case 15: return (int)ntm::gemmt::launch_gemm_bf16_tile_ws<4>(a, S(stream));
     case 16: return (int)ntm::gemmt::launch_gemm_bf16_tile_ws<8>(a, S(stream));
     case 17: return (int)ntm::gemmt::launch_gemm_bf16_tile_ws<5, 5>(a, S(stream));
+    case 23: return (int)ntm::gemmt::launch_gemm_bf16_tile_ws<5, 4>(a, S(stream));  // 160x128
+    case 24: return (int)ntm::gemmt::launch_gemm_bf16_tile_ws<4, 5>(a, S(stream));  // 128x160
     case 18: return (int)ntm::gemmt::launch_gemm_bf16_tile<8, 5>(a, S(stream));
     // 256x256 on ragged C: clamped loads, masked LDS-staged stores
     case 22: return (int)ntm::gemm3::launch_gemm_bf16_pp3_masked(a, S(stream));
@@ -261,7 +282,7 @@ NTM_API int ntm_gemm_bf16_variant(int variant, const void* A, const void* B,
   }
 }
 
-// Split-K on a wave-specialised tile (15 / 16 / 17): `splits` K-slices, fp32 partials
+// Split-K on a wave-specialised tile (15-17, 23, 24): `splits` K-slices, fp32 partials
 // in the caller's workspace ws (ntm_splitk_ws_bytes; stream-ordered, reused once
 // this call's reduction has run), then one reduction kernel writes C.
 NTM_API size_t ntm_splitk_ws_bytes(int M, int N, int K, int splits) {
@@ -290,6 +311,8 @@ NTM_API int ntm_gemm_bf16_splitk(int variant, int splits, const void* A, const v
     case 15: return (int)launch_gemm_bf16_tile_ws_splitk<4, 4>(a, splits, w, S(stream));
     case 16: return (int)launch_gemm_bf16_tile_ws_splitk<8, 4>(a, splits, w, S(stream));
     case 17: return (int)launch_gemm_bf16_tile_ws_splitk<5, 5>(a, splits, w, S(stream));
+    case 23: return (int)launch_gemm_bf16_tile_ws_splitk<5, 4>(a, splits, w, S(stream));
+    case 24: return (int)launch_gemm_bf16_tile_ws_splitk<4, 5>(a, splits, w, S(stream));
     default: return (int)hipErrorInvalidValue;
   }
 }
