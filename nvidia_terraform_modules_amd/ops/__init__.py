@@ -1,7 +1,9 @@
 """MI355X (gfx950) HIP kernels used by the post-provision validation Job.
 
-K1 ``gemm_bf16``      - 256x256x64 LDS-DMA + MFMA bf16 GEMM (the headline; small and
-                        mid-size C also on 128x128 / 256x128 tiles, see ``k1_plan``);
+K1 ``gemm_bf16``      - 256x256x64 LDS-DMA + MFMA bf16 GEMM (the headline; small,
+                        mid-size and ragged C also on 128x128 / 256x128 / 160x160 /
+                        160x128 / 128x160 tiles, skinny long-K C split-K; see
+                        ``k1_plan`` / ``k1_splitk_plan``);
    ``gemm_bf16_rowsum`` - same kernel with the fused ABFT row-checksum epilogue;
    ``gemm_fp8``         - the same schedule on OCP e4m3 operands (MX-scaled MFMA).
 K2 ``stream_copy``, ``stream_read`` - tuned float4 HBM streams.
@@ -23,6 +25,8 @@ from .kernels import (  # noqa: F401
     gemm_fp8_shape_ok,
     gemm_shape_ok,
     gemm_tolerance,
+    k1_plan,
+    k1_splitk_plan,
     ref_gemm_f32,
     stream_copy,
     stream_read,
