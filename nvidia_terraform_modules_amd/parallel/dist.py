@@ -11,6 +11,7 @@ multi-node enabler is the all-protocol node<->node security-group rule
 """
 from __future__ import annotations
 
+import datetime
 import os
 from dataclasses import dataclass
 
@@ -40,7 +41,9 @@ def init(backend: str | None = None, device_type: str | None = None) -> DistEnv:
     """Initialise (or reuse) the default process group from the env contract.
 
     ``backend`` defaults to ``nccl`` (RCCL) when GPUs are present, ``gloo``
-    otherwise. world_size == 1 never creates a process group.
+    otherwise. world_size == 1 never creates a process group. Collectives time
+    out after ``NTM_DIST_TIMEOUT_S`` seconds (default 300, not torch's 10 min):
+    a rank that never arrives fails the job quickly instead of holding the node.
     """
     world = env_int("WORLD_SIZE", 1)
     rank = env_int("RANK", 0)
@@ -56,7 +59,7 @@ def init(backend: str | None = None, device_type: str | None = None) -> DistEnv:
     if world > 1 and not tdist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29512")
-        kwargs = {}
+        kwargs = {"timeout": datetime.timedelta(seconds=env_int("NTM_DIST_TIMEOUT_S", 300))}
         if backend == "nccl":
             kwargs["device_id"] = device
         tdist.init_process_group(backend=backend, rank=rank, world_size=world, **kwargs)
