@@ -355,14 +355,16 @@ def verify_bf16(c: torch.Tensor, ref: torch.Tensor, atol: float, rtol: float) ->
 
 # (unroll, policy, grid) of the block-tiled K2 kernels; policy bit0 =
 # nontemporal loads, bit1 = nontemporal stores, bit2 = software-pipelined
-# copy, bit3 = chunked; grid 0 = auto; unroll 1 = the original grid-stride
-# kernel. Chosen by tools/hbm_sweep.py on MI355X, interleaved rounds, two
-# boxes (profiles/r2_k2/): (8, 7, 512) is top-3 at 1, 2 and 4 GiB on both -
-# box 1: 5.82 TB/s at 1 GiB, 5.69 at 4 GiB; box 2: 5.78 / 5.57 at 1 / 2 GiB
-# (torch copy_ 5.23 / 5.08). The previous (4, 7, 256) ranged 5.44-6.00 and
-# fell out of box 2's top 20. Box-to-box spread is ~5 %.
+# copy, bit3 = chunked; grid 0 = one block per tile (no grid-stride loop);
+# unroll 1 = the original grid-stride kernel. Chosen by tools/hbm_sweep.py on
+# MI355X, interleaved rounds (profiles/r2_k2/): (2, 7, 0) - 2 float4 per lane,
+# nontemporal load + store, one 8 KiB tile per block, so the dispatcher keeps
+# every CU's wave slots full - 6.37 TB/s at 2 GiB and 6.05 at 4 GiB, against
+# 5.81 / 5.41 for the earlier (8, 7, 512) grid-stride pipeline and 4.97 / 4.78
+# for a plain grid-stride float4 copy on the same box. Grids <= 1024 blocks
+# (at most 16 waves per CU) were all that the round-1 sweeps tried.
 #   read  (8, 1, 1024) 7.08-7.13 TB/s at 1 GiB (grid-stride 6.11)
-STREAM_COPY_CONFIG: tuple[int, int, int] = (8, 7, 512)
+STREAM_COPY_CONFIG: tuple[int, int, int] = (2, 7, 0)
 STREAM_READ_CONFIG: tuple[int, int, int] = (8, 1, 1024)
 
 

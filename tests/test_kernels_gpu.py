@@ -114,6 +114,12 @@ def test_stream_copy_and_read(ops):
     torch.cuda.synchronize()
     assert torch.equal(src, dst)
     assert torch.count_nonzero(sink) == 0
+    # the default copy launches one block per 8 KiB tile: 8193 blocks + a tail here
+    big = torch.randint(0, 255, ((1 << 26) + 8192 + 48,), dtype=torch.uint8, device="cuda")
+    out = torch.zeros_like(big)
+    ops.stream_copy(big, out)
+    torch.cuda.synchronize()
+    assert torch.equal(big, out)
 
 
 @pytest.mark.parametrize("nbytes", [16, 4096 + 48, (1 << 20) * 3 + 16 * 7])

@@ -72,9 +72,14 @@ def test_rejects_bad_counts():
         simulate_allreduce(ok, one_shot=True, inplace=True)
 
 
-def test_ipc_allreduce_two_processes():
-    """XgmiAllReduce across two PROCESSES (IPC handles + cross-process flags),
-    both on the one GPU of the box; every element checked exactly."""
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_ipc_allreduce_processes(world):
+    """XgmiAllReduce across ``world`` PROCESSES (IPC handles + cross-process
+    flags), all on the one GPU of the box; every element checked exactly. At
+    world 8 this is the bench's N = 8 set-up (7 peers' buffers opened per rank,
+    8-way device-side barriers) minus only the xGMI links. Each worker keeps to
+    one hardware queue, so the 8 ranks' kernels are co-resident rather than
+    time-sliced (the barrier needs them all running)."""
     import json
     import os
     import socket
@@ -87,9 +92,9 @@ def test_ipc_allreduce_two_processes():
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     procs = []
-    for r in range(2):
-        env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT=str(port))
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), GPU_MAX_HW_QUEUES="1")
         procs.append(subprocess.Popen([sys.executable, str(worker)], env=env,
                                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
     outs = []

@@ -1,5 +1,5 @@
-"""Worker for tests/test_xgmi_gpu.py::test_ipc_allreduce_two_processes: one
-rank of XgmiAllReduce. Both ranks share cuda:0 (one-GPU box), so this runs
+"""Worker for tests/test_xgmi_gpu.py::test_ipc_allreduce_processes: one
+rank of XgmiAllReduce. All ranks share cuda:0 (one-GPU box), so this runs
 the real multi-process path - HIP IPC handle exchange, peer-mapped buffers,
 cross-process release/acquire flags - minus only the xGMI link itself."""
 import json

@@ -33,11 +33,18 @@ def main():
     ap.add_argument("--gib", default="1,2", help="comma list of buffer sizes (GiB each)")
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=5, help="interleaved rounds (median reported)")
-    ap.add_argument("--grids", default="256,384,512,768,1024")
+    ap.add_argument("--grids", default="256,384,512,768,1024",
+                    help="comma list; 'tiles' = one block per tile (no grid-stride loop)")
+    ap.add_argument("--unrolls", default="2,4,8")
+    ap.add_argument("--policies", default="3,7,11",
+                    help="copy policy ids (bit0 nt load, bit1 nt store, bit2 pipelined, 8+ chunked)")
+    ap.add_argument("--no-read", action="store_true", help="copies only")
     args = ap.parse_args()
     import statistics
 
-    grids = [int(g) for g in args.grids.split(",")]
+    grids = args.grids.split(",")
+    unrolls = [int(u) for u in args.unrolls.split(",")]
+    policies = [int(p) for p in args.policies.split(",")]
     for gib in [float(x) for x in args.gib.split(",")]:
         nbytes = int(gib * 2**30) // 65536 * 65536
         src = torch.empty(nbytes // 2, dtype=torch.bfloat16, device="cuda")
@@ -45,13 +52,16 @@ def main():
         dst = torch.empty_like(src)
         sink = torch.zeros(1 << 16, dtype=torch.float32, device="cuda")
         copies = {"torch.copy_": lambda: dst.copy_(src),
-                  "tuned-default": lambda: ops.stream_copy(src, dst)}
-        for u, pol, grid in itertools.product((2, 4, 8), (3, 7, 11), grids):
-            copies[f"copy {u},{pol},{grid}"] = lambda c=(u, pol, grid): ops.stream_copy(src, dst, config=c)
+                  "tuned-default": lambda: ops.stream_copy(src, dst),
+                  "copy 1,0,0 (grid-stride baseline)": lambda: ops.stream_copy(src, dst, config=None)}
+        for u, pol, g in itertools.product(unrolls, policies, grids):
+            grid = nbytes // 16 // (256 * u) if g == "tiles" else int(g)
+            copies[f"copy {u},{pol},{g}"] = lambda c=(u, pol, grid): ops.stream_copy(src, dst, config=c)
         reads = {"tuned-default": lambda: ops.stream_read(src, sink)}
         for u, pol, grid in itertools.product((4, 8, 16), (1,), (0, 512, 1024, 2048)):
             reads[f"read {u},{pol},{grid}"] = lambda c=(u, pol, grid): ops.stream_read(src, sink, config=c)
-        for kind, cands, mult in (("copy", copies, 2), ("read", reads, 1)):
+        kinds = (("copy", copies, 2),) if args.no_read else (("copy", copies, 2), ("read", reads, 1))
+        for kind, cands, mult in kinds:
             ts = {k: [] for k in cands}
             for _ in range(args.rounds):
                 for k, fn in cands.items():

@@ -456,7 +456,8 @@ NTM_API int ntm_verify_result_bytes() {
 
 // K2 entry points. unroll in {2,4,8,16} selects the block-tiled kernels
 // (policy bit0 = nontemporal loads, bit1 = nontemporal stores, bit2 (copy
-// only) = software-pipelined; grid 0 = one block per tile capped at 8192);
+// only) = software-pipelined; grid 0 = one block per tile, no grid-stride
+// loop: the hardware dispatcher keeps every CU's wave slots full);
 // unroll 1 selects the first grid-stride kernel (2048 x 256, nt), kept as
 // the sweep baseline. Defaults measured by tools/hbm_sweep.py on MI355X.
 namespace {
@@ -497,7 +498,7 @@ int read_u(const void* src, size_t n4, float* sink, int policy, unsigned grid,
 unsigned tiled_grid(size_t n4, int unroll, int grid) {
   if (grid > 0) return (unsigned)grid;
   const size_t tiles = n4 / (256 * (size_t)unroll);
-  return (unsigned)(tiles < 1 ? 1 : (tiles > 8192 ? 8192 : tiles));
+  return (unsigned)(tiles < 1 ? 1 : (tiles > 0x7fffffffu ? 0x7fffffffu : tiles));
 }
 }  // namespace
 
@@ -539,11 +540,14 @@ NTM_API int ntm_stream_read_ex(const void* src, size_t bytes, float* sink,
   }
 }
 
-// Tuned defaults (= ops.kernels.STREAM_COPY_CONFIG / STREAM_READ_CONFIG; copy
-// 5.6-5.8 TB/s, read 7.1 TB/s on two MI355X boxes, profiles/r2_k2/).
+// Tuned defaults (= ops.kernels.STREAM_COPY_CONFIG / STREAM_READ_CONFIG).
+// Copy: 2 float4 per lane, nontemporal load + store, one 8 KiB tile per block
+// (grid 0): 6.37 TB/s at 2 GiB, 6.05 at 4 GiB against 5.81 / 5.41 for the
+// earlier (8, 7, 512) grid-stride pipeline (interleaved, profiles/r2_k2/).
+// Read 7.1 TB/s on two MI355X boxes.
 NTM_API int ntm_stream_copy(const void* src, void* dst, size_t bytes,
                             void* stream) {
-  return ntm_stream_copy_ex(src, dst, bytes, 8, 7, 512, stream);
+  return ntm_stream_copy_ex(src, dst, bytes, 2, 7, 0, stream);
 }
 
 NTM_API int ntm_stream_read(const void* src, size_t bytes, float* sink,
