@@ -5,7 +5,8 @@ K1 ``gemm_bf16``      - 256x256x64 LDS-DMA + MFMA bf16 GEMM (the headline; small
                         160x128 / 128x160 tiles, skinny long-K C split-K; see
                         ``k1_plan`` / ``k1_splitk_plan``);
    ``gemm_bf16_rowsum`` - same kernel with the fused ABFT row-checksum epilogue;
-   ``gemm_fp8``         - the same schedule on OCP e4m3 operands (MX-scaled MFMA).
+   ``gemm_fp8``         - the same kernels on OCP e4m3 operands (f8f6f4 MFMA; 256x256
+                          and the wave-specialised tiles, ``k1_fp8_plan``).
 K2 ``stream_copy``, ``stream_read`` - tuned float4 HBM streams.
 K3 ``fill_uniform_``, ``ref_gemm_f32``, ``verify_bf16``, ``abft_check`` - synthetic
    data, full fp32 reference check and the O(n^2) checksum check.
@@ -25,6 +26,8 @@ from .kernels import (  # noqa: F401
     gemm_fp8_shape_ok,
     gemm_shape_ok,
     gemm_tolerance,
+    FP8_VARIANTS,
+    k1_fp8_plan,
     k1_plan,
     k1_splitk_plan,
     ref_gemm_f32,

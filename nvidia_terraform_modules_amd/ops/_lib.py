@@ -37,6 +37,9 @@ def _declare(lib: ctypes.CDLL) -> None:
             [c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp], c_int),
         "ntm_gemm_fp8": ([c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp], c_int),
         "ntm_gemm_fp8_shape_ok": ([c_int, c_int, c_int], c_int),
+        "ntm_gemm_fp8_variant": ([c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int,
+                                  c_vp], c_int),
+        "ntm_k1_fp8_plan": ([c_int, c_int, c_int, c_vp, c_vp, c_vp], c_int),
         "ntm_gemm_bf16_rowsum": (
             [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp], c_int),
         "ntm_abft_check": ([c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int,

@@ -189,15 +189,35 @@ def gemm_fp8_shape_ok(m: int, n: int, k: int) -> bool:
     return bool(lib().ntm_gemm_fp8_shape_ok(m, n, k))
 
 
-def gemm_fp8(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
-             knob: int = 0) -> torch.Tensor:
-    """K1-fp8: ``out = a @ b.T`` with OCP e4m3 operands (``torch.float8_e4m3fn``),
-    fp32 accumulation on the MX-scaled MFMA path (unit scales), bf16 output.
+# K1-fp8 variants: the 256x256 kernel and the wave-specialised tiles with the fp8 consumer
+FP8_VARIANTS = ("default", "pingpong8c", "pingpong8cm", "tile128", "tile256x128", "tile160", "tile160x128",
+                "tile128x160")
 
-    a: [M, K], b: [N, K] (K-contiguous, rows 16-byte aligned), out: [M, N] bf16.
-    M, N % 256 and K % 256. Same 8-wave schedule and LDS image as the bf16
-    default; twice the MFMA rate per clock. ``knob`` != 0 selects an
-    experimental schedule variant (gemm_fp8.hpp ``launch_gemm_fp8_knob``).
+
+def k1_fp8_plan(m: int, n: int, k: int) -> tuple[int, str, str]:
+    """K1-fp8's default plan, as ``k1_plan`` (the same tile and row-split model
+    with K counted in pairs of e4m3 values, over the tiles that have an fp8
+    build). Raises ValueError for shapes the fp8 kernels do not serve."""
+    top, tv, rest = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    rc = lib().ntm_k1_fp8_plan(m, n, k, ctypes.byref(top), ctypes.byref(tv), ctypes.byref(rest))
+    if rc != 0:
+        raise ValueError(f"shape ({m},{n},{k}) not served by the fp8 kernels (N % 8, K % 16)")
+    names = {v: kname for kname, v in GEMM_VARIANTS.items()}
+    return top.value, names[tv.value], names[rest.value]
+
+
+def gemm_fp8(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
+             knob: int = 0, variant: str = "default") -> torch.Tensor:
+    """K1-fp8: ``out = a @ b.T`` with OCP e4m3 operands (``torch.float8_e4m3fn``),
+    fp32 accumulation on the f8f6f4 MFMA (unit scales), bf16 output.
+
+    a: [M, K], b: [N, K] (K-contiguous, rows 16-byte aligned), out: [M, N] bf16;
+    N % 8, K % 16. ``variant``: "default" = ``k1_fp8_plan`` (256x256 tiles, or
+    the wave-specialised 128x128 / 256x128 / 160x160 / 160x128 / 128x160 tiles
+    and row splits where they fill the chip better); "pingpong8c" = the 256x256
+    kernel (the bf16 default's schedule and LDS image, twice the MFMA rate per
+    clock); "tile*" = one tile shape. ``knob`` != 0 selects an experimental
+    schedule of the 256x256 kernel (gemm_fp8_diag.hpp).
     """
     _require(a, "a", torch.float8_e4m3fn)
     _require(b, "b", torch.float8_e4m3fn)
@@ -217,8 +237,11 @@ def gemm_fp8(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
                                      a.stride(0), b.stride(0), out.stride(0), int(knob),
                                      stream_handle())
     else:
-        rc = lib().ntm_gemm_fp8(a.data_ptr(), b.data_ptr(), out.data_ptr(), m, n, k,
-                                a.stride(0), b.stride(0), out.stride(0), stream_handle())
+        if variant not in FP8_VARIANTS:
+            raise ValueError(f"fp8 variant {variant!r} not in {FP8_VARIANTS}")
+        rc = lib().ntm_gemm_fp8_variant(GEMM_VARIANTS[variant], a.data_ptr(), b.data_ptr(),
+                                        out.data_ptr(), m, n, k, a.stride(0), b.stride(0),
+                                        out.stride(0), stream_handle())
     check(rc, "ntm_gemm_fp8")
     return out
 

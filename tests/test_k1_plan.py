@@ -127,3 +127,45 @@ def test_splitk_plan_is_well_formed(k1_plan, splitk_plan, m, n, k):
         assert k // splits >= 32
     else:
         assert (top, tv, rest) == k1_plan(m, n, k)
+
+
+@pytest.fixture(scope="module")
+def fp8_plan():
+    from nvidia_terraform_modules_amd.ops import _lib
+
+    if not _lib.LIB_PATH.exists():
+        pytest.skip("native library not built (python -m nvidia_terraform_modules_amd.ops.build)")
+    from nvidia_terraform_modules_amd.ops.kernels import k1_fp8_plan as f
+
+    return f
+
+
+@pytest.mark.parametrize("m,n,k,plan", [
+    (8192, 8192, 8192, (8192, "pingpong8c", "tile128")),   # the Job's fp8 check: 256x256 only
+    (4096, 4096, 4096, (4096, "pingpong8c", "tile128")),
+    (6144, 6144, 6144, (5376, "pingpong8c", "tile160x128")),
+    (2048, 2048, 2048, (2048, "tile128", "tile128")),
+    (2560, 2560, 2560, (2560, "tile160", "tile160")),
+    (1000, 1000, 1008, (1000, "tile128", "tile128")),
+])
+def test_fp8_plan(fp8_plan, k1_plan, m, n, k, plan):
+    """K1-fp8's plan is the bf16 model at K / 2 (a K-tile of 128 e4m3 values
+    costs what one of 64 bf16 values does) over the tiles with an fp8 build."""
+    assert fp8_plan(m, n, k) == plan
+
+
+@pytest.mark.parametrize("m,n,k", [(256, 160, 256), (512, 640, 256), (5120, 5120, 8192),
+                                   (8192, 5120, 8192), (1280, 2560, 1024)])
+def test_fp8_plan_uses_only_fp8_builds(fp8_plan, m, n, k):
+    """No 4-wave 256x160 tile (no fp8 build) and no split-K in an fp8 plan."""
+    top, tv, rv = fp8_plan(m, n, k)
+    assert 0 < top <= m
+    assert tv in ("pingpong8c", "pingpong8cm", "tile128", "tile256x128", "tile160",
+                  "tile160x128", "tile128x160")
+    assert rv != "tile256x160" and tv != "tile256x160"
+
+
+def test_fp8_plan_rejects_bad_shapes(fp8_plan):
+    for m, n, k in [(256, 252, 256), (256, 256, 24), (0, 256, 256)]:
+        with pytest.raises(ValueError):
+            fp8_plan(m, n, k)

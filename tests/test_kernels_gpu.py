@@ -492,6 +492,50 @@ def test_gemm_fp8_masked_edge_tiles(ops, m, n, k):
     assert torch.all(big[m:] == 3.0) and torch.all(big[:, n:] == 3.0)
 
 
+@pytest.mark.parametrize("variant", ["tile128", "tile256x128", "tile160", "tile160x128",
+                                     "tile128x160"])
+@pytest.mark.parametrize("m,n,k", [(256, 256, 256), (1000, 1000, 1008), (300, 2056, 400),
+                                   (640, 520, 2048), (33, 8, 16)])
+def test_gemm_fp8_wave_specialised_tiles(ops, variant, m, n, k):
+    """K1-fp8 on the wave-specialised tiles (fp8 consumer: one f8f6f4 MFMA over
+    both k-halves, fragments refilled after their last MFMA): vs fp32 on whole,
+    ragged and K-tail shapes, nothing written outside C (strided C), and
+    bitwise deterministic."""
+    a = _rand_fp8((m, k), 23 + m + k)
+    b = _rand_fp8((n, k), 29 + n)
+    big = torch.full((m + 7, n + 24), 3.0, dtype=torch.bfloat16, device="cuda")
+    c = big[:m, :n]
+    ops.gemm_fp8(a, b, c, variant=variant)
+    torch.cuda.synchronize()
+    ref = a.float() @ b.float().T
+    atol, rtol = ops.gemm_tolerance(k)
+    err = (c.float() - ref).abs()
+    assert torch.all(err <= atol + rtol * ref.abs()), (variant, float(err.max()))
+    assert torch.all(big[m:] == 3.0) and torch.all(big[:, n:] == 3.0)
+    assert torch.equal(c, ops.gemm_fp8(a, b, variant=variant))
+
+
+@pytest.mark.parametrize("m,n,k,plan", [(4352, 4352, 512, (3840, "pingpong8c", "tile128")),
+                                        (4608, 4608, 256, (3584, "pingpong8c", "tile160x128")),
+                                        (2816, 2816, 512, (2816, "tile256x128", "tile256x128")),
+                                        (1024, 1024, 1024, (1024, "tile128", "tile128"))])
+def test_gemm_fp8_default_plan(ops, m, n, k, plan):
+    """K1-fp8's default dispatch runs k1_fp8_plan: row splits (256x256 rounds +
+    a small-tile rest) and small tiles are bitwise equal to the explicit
+    variants on their rows (same MFMA order per output), and match fp32."""
+    assert ops.k1_fp8_plan(m, n, k) == plan
+    a = _rand_fp8((m, k), 31 + m)
+    b = _rand_fp8((n, k), 37 + n)
+    c = ops.gemm_fp8(a, b)
+    top, tv, rv = plan
+    assert torch.equal(c[:top], ops.gemm_fp8(a[:top], b, variant=tv))
+    if top < m:
+        assert torch.equal(c[top:], ops.gemm_fp8(a[top:].contiguous(), b, variant=rv))
+    ref = a.float() @ b.float().T
+    atol, rtol = ops.gemm_tolerance(k)
+    assert torch.all((c.float() - ref).abs() <= atol + rtol * ref.abs())
+
+
 def test_gemm_fp8_rejects_bad_shapes(ops):
     a = torch.zeros((256, 136), dtype=torch.float8_e4m3fn, device="cuda")[:, :120]
     with pytest.raises(ValueError):

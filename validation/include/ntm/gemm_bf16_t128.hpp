@@ -395,7 +395,63 @@ __device__ __forceinline__ void ws_produce(const CtxT& c, const Clamp& q, int T)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // dummy pieces drained
 }
 
-template <int MT, int NT = 4, int KNOB = 0, bool SPLIT = false>
+// fp8 consumer (K1-fp8 on the wave-specialised tiles, F8 = true). One
+// v_mfma_f32_16x16x128_f8f6f4 per (mt, nt) and K-tile consumes BOTH k-halves of
+// its A and B fragments (the LDS image is the bf16 one: a 128-byte K-tile row is
+// 64 bf16 or 128 e4m3 values, gemm_fp8.hpp), so the bf16 consumer's half-tile
+// ping-pong does not apply; instead each fragment of tile t+1 is read as soon
+// as its last MFMA of tile t has issued (MFMAs read their A/B sources at issue):
+//   row 0 of tile t (NT MFMAs); lgkmcnt(0); barrier t+1 (tile t+1 visible,
+//   every read of tile t retired); rows 1 .. MT-1, with A[r] of tile t+1 read
+//   after the first two MFMAs of row r+1, and in the last row B[nt] after MFMA
+//   (MT-1, nt), A[MT-1] after the last one.
+// Barriers and the RAW / WAR argument are the bf16 consumer's (T + 1 barriers,
+// every read of tile t issued after barrier t and retired before barrier t+1),
+// so the producer loop is unchanged. Next tile's row 0 needs B[nt] about NT
+// 32-cycle MFMAs after its read was issued.
+template <int MT, int NT>
+__device__ __forceinline__ void read_a_f8(const CtxT& c, FragsT<MT, NT>& f, int kt, int i) {
+  read_frag<MT, NT>(c, f, kt, i);
+  read_frag<MT, NT>(c, f, kt, MT + NT + i);
+}
+
+template <int MT, int NT>
+__device__ __forceinline__ void ws_consume_f8(const CtxT& c, FragsT<MT, NT>& f,
+                                              f32x4 (&acc)[MT][NT], int T) {
+  using ::ntm::gemm::cat_f8;
+  using ::ntm::gemm::mfma_f8_agpr_plain;
+  auto mma = [&](int mt, int nt) {
+    mfma_f8_agpr_plain(acc[mt][nt], cat_f8(f.b[nt][0], f.b[nt][1]), cat_f8(f.a[mt][0], f.a[mt][1]));
+  };
+  raw_barrier();  // tile 0 visible
+#pragma unroll
+  for (int i = 0; i < MT + NT; ++i) read_a_f8<MT, NT>(c, f, 0, i);
+  for (int t = 0; t < T; ++t) {
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      mma(0, nt);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    raw_barrier();  // tile t+1 visible; every read of tile t retired
+#pragma unroll
+    for (int mt = 1; mt < MT; ++mt) {
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        mma(mt, nt);
+        // A[mt-1] of tile t+1 (t + 1 == T: stale slot, unused): its last MFMA was row mt-1
+        if (nt == 0) read_frag<MT, NT>(c, f, t + 1, mt - 1);
+        if (nt == 1) read_frag<MT, NT>(c, f, t + 1, MT + NT + mt - 1);
+        if (mt == MT - 1) read_a_f8<MT, NT>(c, f, t + 1, MT + nt);  // B[nt]
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    read_a_f8<MT, NT>(c, f, t + 1, MT - 1);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+template <int MT, int NT = 4, int KNOB = 0, bool SPLIT = false, bool F8 = false>
 __global__ void __launch_bounds__(2 * kThreadsT, 1) gemm_bf16_tile_ws_kernel(GemmArgs p) {
   using C = Cfg<MT, NT>;
   (void)sizeof(CfgWS<MT, NT>);
@@ -451,6 +507,10 @@ __global__ void __launch_bounds__(2 * kThreadsT, 1) gemm_bf16_tile_ws_kernel(Gem
 #pragma unroll
     for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   FragsT<MT, NT> f;
+  if constexpr (F8) {
+    static_assert(!SPLIT && KNOB == 0, "fp8: plain tiles only");
+    ws_consume_f8<MT, NT>(c, f, acc, T);
+  } else {
   raw_barrier();  // tile 0 visible
 #pragma unroll
   for (int i = 0; i < MT + NT; ++i) read_half<MT, NT, KNOB>(c, f, 0, 0, i);
@@ -475,6 +535,7 @@ __global__ void __launch_bounds__(2 * kThreadsT, 1) gemm_bf16_tile_ws_kernel(Gem
       __builtin_amdgcn_sched_barrier(0);
     }
   }
+  }  // bf16 consumer
 
   ::ntm::gemm::mfma_drain();
   if constexpr (SPLIT) {  // split-K: the fp32 partial of slice blockIdx.y
@@ -535,6 +596,33 @@ inline hipError_t launch_gemm_bf16_tile_ws(const GemmArgs& a, hipStream_t stream
                                    ((a.N + Cfg<MT, NT>::TN - 1) / Cfg<MT, NT>::TN));
   hipLaunchKernelGGL((gemm_bf16_tile_ws_kernel<MT, NT, KNOB>), dim3(grid), dim3(2 * kThreadsT), 0,
                      stream, a);
+  return hipGetLastError();
+}
+
+// K1-fp8 on a wave-specialised tile: C (bf16) = A (e4m3) * B (e4m3)^T, M x N x
+// K in fp8 elements (N % 8, K % 16, 16-byte aligned rows); the kernel sees the
+// operands as bf16-sized pairs (K / 2, lda / 2, ldb / 2), exactly like the
+// 256x256 fp8 build (gemm_fp8.hpp).
+template <int MT, int NT>
+inline hipError_t launch_gemm_fp8_tile_ws(const void* A, const void* B, __bf16* C, int M, int N,
+                                          int K, int lda, int ldb, int ldc, hipStream_t stream) {
+  if (M <= 0 || N <= 0 || K <= 0 || (N % 8) || (K % 16) || lda < K || ldb < K || ldc < N ||
+      (lda % 16) || (ldb % 16) || (ldc % 4))
+    return hipErrorInvalidValue;
+  GemmArgs a;
+  a.A = (const __bf16*)A;
+  a.B = (const __bf16*)B;
+  a.C = C;
+  a.M = M;
+  a.N = N;
+  a.K = K / 2;
+  a.lda = lda / 2;
+  a.ldb = ldb / 2;
+  a.ldc = ldc;
+  const unsigned grid = (unsigned)(((M + Cfg<MT, NT>::TM - 1) / Cfg<MT, NT>::TM) *
+                                   ((N + Cfg<MT, NT>::TN - 1) / Cfg<MT, NT>::TN));
+  hipLaunchKernelGGL((gemm_bf16_tile_ws_kernel<MT, NT, 0, false, true>), dim3(grid),
+                     dim3(2 * kThreadsT), 0, stream, a);
   return hipGetLastError();
 }
 

@@ -124,7 +124,10 @@ constexpr int kMaxSplits = 16;
 // 128x128 (250 tiles), two full rounds instead of 1.56 rounds of 160x160
 // (977 vs 924 TF/s, hipBLASLt 948: profiles/r2_ws/split_3200.log).
 // Ties: fewer launches, then more rows on the 256x256 kernel.
-inline K1Plan plan_k1(int M, int N, int K, bool splitk = false) {
+// fp8 (K1-fp8's plan): K counted in bf16-sized pairs of e4m3 values (a K-tile
+// costs the same cycles in both dtypes); only the tiles with an fp8 build - the
+// 256x256 kernel and the wave-specialised ones - and no split-K.
+inline K1Plan plan_k1(int M, int N, int K, bool splitk = false, bool fp8 = false) {
   auto rounds = [](double tiles) { return tiles <= 0 ? 0.0 : __builtin_ceil(tiles / kCUs); };
   const double inf = 1e300;
   // the 256x256 kernel on whole tiles: pingpong8c (K % 128). K % 128 != 0 goes
@@ -140,6 +143,7 @@ inline K1Plan plan_k1(int M, int N, int K, bool splitk = false) {
   int best_launches = 3, best_big_rows = -1;
   if (M <= 0 || N <= 0 || K <= 0) return best;
   auto small_ok = [&](const SmallTile& st, int rows) {  // masked: any M, N % 4, K % 8
+    if (fp8 && !st.masked) return false;
     if (st.masked) return N % 4 == 0 && K % 8 == 0;
     return rows % st.tm == 0 && N % st.tn == 0 && K % 128 == 0 && K >= 128;
   };
@@ -331,10 +335,55 @@ NTM_API int ntm_gemm_bf16_ex(const void* A, const void* B, void* C, int M, int N
   return ntm_gemm_bf16_variant(0, A, B, C, M, N, K, lda, ldb, ldc, stream);
 }
 
-// K1-fp8: C (bf16) = A (e4m3) * B (e4m3)^T, fp32 accumulation (gemm_fp8.hpp).
+// K1-fp8: C (bf16) = A (e4m3) * B (e4m3)^T, fp32 accumulation. Variant 5 / 22:
+// the 256x256 kernel (gemm_fp8.hpp; exact, masked and partial-K builds picked by
+// shape); 15 / 16 / 17 / 23 / 24: the wave-specialised tiles with the fp8
+// consumer (gemm_bf16_t128.hpp); 0: the plan (plan_k1 in fp8 mode: tile shape
+// and row split priced exactly as for bf16).
+NTM_API int ntm_gemm_fp8_variant(int variant, const void* A, const void* B, void* C, int M, int N,
+                                 int K, int lda, int ldb, int ldc, void* stream) {
+  if (!ntm::fp8::shape_ok(M, N, K)) return (int)hipErrorInvalidValue;
+  if (variant == 0) {
+    const K1Plan pl = plan_k1(M, N, K / 2, false, true);
+    if (!pl.feasible()) return (int)hipErrorInvalidValue;  // nothing launched
+    if (pl.top_rows < M) {
+      const int rc = ntm_gemm_fp8_variant(pl.top_variant, A, B, C, pl.top_rows, N, K, lda, ldb,
+                                          ldc, stream);
+      if (rc != 0) return rc;
+      return ntm_gemm_fp8_variant(pl.rest_variant, (const char*)A + (size_t)pl.top_rows * lda, B,
+                                  (__bf16*)C + (size_t)pl.top_rows * ldc, M - pl.top_rows, N, K,
+                                  lda, ldb, ldc, stream);
+    }
+    variant = pl.top_variant;
+  }
+  __bf16* c = (__bf16*)C;
+  using namespace ntm::gemmt;
+  switch (variant) {
+    case 5: case 22: return (int)ntm::fp8::launch_gemm_fp8(A, B, c, M, N, K, lda, ldb, ldc, S(stream));
+    case 15: return (int)launch_gemm_fp8_tile_ws<4, 4>(A, B, c, M, N, K, lda, ldb, ldc, S(stream));
+    case 16: return (int)launch_gemm_fp8_tile_ws<8, 4>(A, B, c, M, N, K, lda, ldb, ldc, S(stream));
+    case 17: return (int)launch_gemm_fp8_tile_ws<5, 5>(A, B, c, M, N, K, lda, ldb, ldc, S(stream));
+    case 23: return (int)launch_gemm_fp8_tile_ws<5, 4>(A, B, c, M, N, K, lda, ldb, ldc, S(stream));
+    case 24: return (int)launch_gemm_fp8_tile_ws<4, 5>(A, B, c, M, N, K, lda, ldb, ldc, S(stream));
+    default: return (int)hipErrorInvalidValue;
+  }
+}
+
+NTM_API int ntm_k1_fp8_plan(int M, int N, int K, int* top_rows, int* top_variant,
+                            int* rest_variant) {
+  if (!ntm::fp8::shape_ok(M, N, K) || !top_rows || !top_variant || !rest_variant)
+    return (int)hipErrorInvalidValue;
+  const K1Plan pl = plan_k1(M, N, K / 2, false, true);
+  if (!pl.feasible()) return (int)hipErrorInvalidValue;
+  *top_rows = pl.top_rows;
+  *top_variant = pl.top_variant;
+  *rest_variant = pl.rest_variant;
+  return 0;
+}
+
 NTM_API int ntm_gemm_fp8(const void* A, const void* B, void* C, int M, int N, int K, int lda,
                          int ldb, int ldc, void* stream) {
-  return (int)ntm::fp8::launch_gemm_fp8(A, B, (__bf16*)C, M, N, K, lda, ldb, ldc, S(stream));
+  return ntm_gemm_fp8_variant(0, A, B, C, M, N, K, lda, ldb, ldc, stream);
 }
 
 NTM_API int ntm_gemm_fp8_shape_ok(int M, int N, int K) {
