@@ -10,7 +10,8 @@ placed too early (WAR) shows up as a changed tile.
 
     python tools/race_screen.py [--variants pingpong8b] [--repeats 200]
 
-Variant ``fp8`` screens K1-fp8 (ops.gemm_fp8, e4m3 operands, K % 256 shapes);
+Variant ``fp8`` screens K1-fp8's default plan (ops.gemm_fp8, e4m3 operands),
+``fp8:<variant>`` one fp8 kernel (``fp8:tile128`` ...; both also on ragged C);
 ``<tile>/s<S>`` a masked tile with split-K in S slices (skinny long-K shapes).
 """
 import argparse
@@ -54,21 +55,24 @@ def main():
     for v in args.variants.split(","):
         v, _, sp = v.partition("/s")
         splits = int(sp) if sp else 1
-        fp8 = v == "fp8"
+        fp8 = v == "fp8" or v.startswith("fp8:")
+        fv = v.partition(":")[2] or "default"
         dt = torch.float8_e4m3fn if fp8 else torch.bfloat16
 
-        def gemm(a, b, out=None, v=v, fp8=fp8, splits=splits):
+        def gemm(a, b, out=None, v=v, fp8=fp8, fv=fv, splits=splits):
             if fp8:
-                return ops.gemm_fp8(a, b, out)
+                return ops.gemm_fp8(a, b, out, variant=fv)
             return ops.gemm_bf16(a, b, out, variant=v, splits=splits)
 
         tm, tn = ops.kernels.TILE_SHAPES.get(v, (0, 0))
-        shapes = SHAPES_FP8 if fp8 else SHAPES_160 if tn == 160 else SHAPES
+        shapes = SHAPES_FP8 + SHAPES_RAGGED if fp8 else SHAPES_160 if tn == 160 else SHAPES
         if splits > 1:
             shapes = SHAPES_SPLITK + SHAPES_RAGGED
         elif v in MASKED:
             shapes = shapes + SHAPES_RAGGED + (SHAPES_SPLITK if v == "default" else [])
         for (m, n, k) in shapes:
+            if fp8 and not ops.gemm_fp8_shape_ok(m, n, k):
+                continue
             if tm and m % tm and v not in MASKED:
                 continue
             if v == "pingpong8cm" and n % 8:
