@@ -20,7 +20,8 @@ EXP = ROOT / "nvidia_terraform_modules_amd" / "ops" / "libntm_experimental.so"
 # epilogue when ldc % 8 == 0, register epilogue otherwise; with/without the ABFT
 # row sum; F8 = 3 is K1-fp8; EPI 26 = the masked ragged-C build), pingpong8b for
 # K % 128 != 0, and the 4 tile shapes
-# (128x128 / 256x128 / 160x160 wave-specialised, 256x160 4-wave).
+# (128x128 / 256x128 / 160x160 / 160x128 / 128x160 wave-specialised, also as K1-fp8,
+# 256x160 4-wave).
 ALLOWED_K1 = {
     "ntm::gemm3::gemm_bf16_pp3_kernel<false, 8, false, 0, 0, 0>",
     "ntm::gemm3::gemm_bf16_pp3_kernel<false, 8, false, 10, 0, 0>",
@@ -35,17 +36,23 @@ ALLOWED_K1 = {
     "ntm::gemm2::gemm_bf16_pp2_kernel<false, 3>",
     "ntm::gemm2::gemm_bf16_pp2_kernel<true, 0>",
     "ntm::gemm2::gemm_bf16_pp2_kernel<true, 3>",
-    "ntm::gemmt::gemm_bf16_tile_ws_kernel<4, 4, 0, false>",
-    "ntm::gemmt::gemm_bf16_tile_ws_kernel<8, 4, 0, false>",
-    "ntm::gemmt::gemm_bf16_tile_ws_kernel<5, 5, 0, false>",
-    "ntm::gemmt::gemm_bf16_tile_ws_kernel<5, 4, 0, false>",
-    "ntm::gemmt::gemm_bf16_tile_ws_kernel<4, 5, 0, false>",
+    "ntm::gemmt::gemm_bf16_tile_ws_kernel<4, 4, 0, false, false>",
+    "ntm::gemmt::gemm_bf16_tile_ws_kernel<8, 4, 0, false, false>",
+    "ntm::gemmt::gemm_bf16_tile_ws_kernel<5, 5, 0, false, false>",
+    "ntm::gemmt::gemm_bf16_tile_ws_kernel<5, 4, 0, false, false>",
+    "ntm::gemmt::gemm_bf16_tile_ws_kernel<4, 5, 0, false, false>",
     # split-K builds of the same tiles (fp32 partials; splitk_reduce_kernel sums them)
-    "ntm::gemmt::gemm_bf16_tile_ws_kernel<4, 4, 0, true>",
-    "ntm::gemmt::gemm_bf16_tile_ws_kernel<8, 4, 0, true>",
-    "ntm::gemmt::gemm_bf16_tile_ws_kernel<5, 5, 0, true>",
-    "ntm::gemmt::gemm_bf16_tile_ws_kernel<5, 4, 0, true>",
-    "ntm::gemmt::gemm_bf16_tile_ws_kernel<4, 5, 0, true>",
+    "ntm::gemmt::gemm_bf16_tile_ws_kernel<4, 4, 0, true, false>",
+    "ntm::gemmt::gemm_bf16_tile_ws_kernel<8, 4, 0, true, false>",
+    "ntm::gemmt::gemm_bf16_tile_ws_kernel<5, 5, 0, true, false>",
+    "ntm::gemmt::gemm_bf16_tile_ws_kernel<5, 4, 0, true, false>",
+    "ntm::gemmt::gemm_bf16_tile_ws_kernel<4, 5, 0, true, false>",
+    # K1-fp8 on the same tiles (fp8 consumer)
+    "ntm::gemmt::gemm_bf16_tile_ws_kernel<4, 4, 0, false, true>",
+    "ntm::gemmt::gemm_bf16_tile_ws_kernel<8, 4, 0, false, true>",
+    "ntm::gemmt::gemm_bf16_tile_ws_kernel<5, 5, 0, false, true>",
+    "ntm::gemmt::gemm_bf16_tile_ws_kernel<5, 4, 0, false, true>",
+    "ntm::gemmt::gemm_bf16_tile_ws_kernel<4, 5, 0, false, true>",
     "ntm::gemmt::gemm_bf16_tile_kernel<8, 5>",
 }
 EXPERIMENTAL_ONLY = ("gemm_bf16_w4_kernel", "gemm_bf16_pp4_kernel", "gemm_bf16_pp5_kernel",
