@@ -28,6 +28,7 @@ from .kernels import (  # noqa: F401
     gemm_tolerance,
     FP8_VARIANTS,
     k1_fp8_plan,
+    k1_fp8_splitk_plan,
     k1_plan,
     k1_splitk_plan,
     ref_gemm_f32,

@@ -40,6 +40,12 @@ def _declare(lib: ctypes.CDLL) -> None:
         "ntm_gemm_fp8_variant": ([c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int,
                                   c_vp], c_int),
         "ntm_k1_fp8_plan": ([c_int, c_int, c_int, c_vp, c_vp, c_vp], c_int),
+        "ntm_k1_fp8_plan_splitk": ([c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp], c_int),
+        "ntm_fp8_splitk_ws_bytes": ([c_int, c_int, c_int, c_int], c_size),
+        "ntm_gemm_fp8_splitk": ([c_int, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int,
+                                 c_int, c_vp, c_size, c_vp], c_int),
+        "ntm_gemm_fp8_ex": ([c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp,
+                             c_size, c_vp], c_int),
         "ntm_gemm_bf16_rowsum": (
             [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp], c_int),
         "ntm_abft_check": ([c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int,

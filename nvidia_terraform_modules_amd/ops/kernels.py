@@ -206,8 +206,33 @@ def k1_fp8_plan(m: int, n: int, k: int) -> tuple[int, str, str]:
     return top.value, names[tv.value], names[rest.value]
 
 
+def k1_fp8_splitk_plan(m: int, n: int, k: int) -> tuple[int, str, str, int]:
+    """K1-fp8's plan with split-K allowed (what ``gemm_fp8`` runs): ``k1_fp8_plan``'s
+    triple plus the number of K slices (> 1: all of C on a masked small tile)."""
+    top, tv, rest, sp = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    rc = lib().ntm_k1_fp8_plan_splitk(m, n, k, ctypes.byref(top), ctypes.byref(tv),
+                                      ctypes.byref(rest), ctypes.byref(sp))
+    if rc != 0:
+        raise ValueError(f"shape ({m},{n},{k}) not served by the fp8 kernels (N % 8, K % 16)")
+    names = {v: kname for kname, v in GEMM_VARIANTS.items()}
+    return top.value, names[tv.value], names[rest.value], sp.value
+
+
+_FP8_WS: dict[tuple[int, int, int], int] = {}
+
+
+def _fp8_ws_bytes(m: int, n: int, k: int) -> int:
+    key = (m, n, k)
+    wsb = _FP8_WS.get(key)
+    if wsb is None:
+        sp = k1_fp8_splitk_plan(m, n, k)[3]
+        wsb = lib().ntm_fp8_splitk_ws_bytes(m, n, k, sp) if sp > 1 else 0
+        _FP8_WS[key] = wsb
+    return wsb
+
+
 def gemm_fp8(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
-             knob: int = 0, variant: str = "default") -> torch.Tensor:
+             knob: int = 0, variant: str = "default", splits: int = 1) -> torch.Tensor:
     """K1-fp8: ``out = a @ b.T`` with OCP e4m3 operands (``torch.float8_e4m3fn``),
     fp32 accumulation on the f8f6f4 MFMA (unit scales), bf16 output.
 
@@ -216,8 +241,11 @@ def gemm_fp8(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
     the wave-specialised 128x128 / 256x128 / 160x160 / 160x128 / 128x160 tiles
     and row splits where they fill the chip better); "pingpong8c" = the 256x256
     kernel (the bf16 default's schedule and LDS image, twice the MFMA rate per
-    clock); "tile*" = one tile shape. ``knob`` != 0 selects an experimental
-    schedule of the 256x256 kernel (gemm_fp8_diag.hpp).
+    clock); "tile*" = one tile shape. The default splits K over a masked small
+    tile for skinny C with a long K (``k1_fp8_splitk_plan``; fp32 partials in a
+    workspace from PyTorch's allocator); ``splits`` > 1 forces that on a "tile*"
+    variant. ``knob`` != 0 selects an experimental schedule of the 256x256
+    kernel (gemm_fp8_diag.hpp).
     """
     _require(a, "a", torch.float8_e4m3fn)
     _require(b, "b", torch.float8_e4m3fn)
@@ -236,6 +264,21 @@ def gemm_fp8(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
         rc = lib_experimental().ntm_gemm_fp8_knob(a.data_ptr(), b.data_ptr(), out.data_ptr(), m, n, k,
                                      a.stride(0), b.stride(0), out.stride(0), int(knob),
                                      stream_handle())
+    elif splits > 1 or (variant == "default" and _fp8_ws_bytes(m, n, k)):
+        if splits > 1 and variant not in MASKED_TILES:
+            raise ValueError(f"fp8 split-K runs on {sorted(MASKED_TILES)}, not {variant}")
+        wsb = (lib().ntm_fp8_splitk_ws_bytes(m, n, k, splits) if splits > 1
+               else _fp8_ws_bytes(m, n, k))
+        ws = torch.empty((wsb + 3) // 4, dtype=torch.float32, device=a.device)
+        if splits > 1:
+            rc = lib().ntm_gemm_fp8_splitk(GEMM_VARIANTS[variant], splits, a.data_ptr(),
+                                           b.data_ptr(), out.data_ptr(), m, n, k, a.stride(0),
+                                           b.stride(0), out.stride(0), ws.data_ptr(), wsb,
+                                           stream_handle())
+        else:
+            rc = lib().ntm_gemm_fp8_ex(a.data_ptr(), b.data_ptr(), out.data_ptr(), m, n, k,
+                                       a.stride(0), b.stride(0), out.stride(0), ws.data_ptr(), wsb,
+                                       stream_handle())
     else:
         if variant not in FP8_VARIANTS:
             raise ValueError(f"fp8 variant {variant!r} not in {FP8_VARIANTS}")

@@ -536,6 +536,37 @@ def test_gemm_fp8_default_plan(ops, m, n, k, plan):
     assert torch.all((c.float() - ref).abs() <= atol + rtol * ref.abs())
 
 
+@pytest.mark.parametrize("variant,splits", [("tile128", 2), ("tile128", 5), ("tile160", 3),
+                                            ("tile256x128", 4), ("tile160x128", 2),
+                                            ("tile128x160", 3)])
+@pytest.mark.parametrize("m,n,k", [(280, 1000, 4112), (128, 256, 2048), (33, 8, 400)])
+def test_gemm_fp8_splitk(ops, variant, splits, m, n, k):
+    """K1-fp8 split-K (fp32 partials of the fp8 consumer, one reduction) vs fp32,
+    on ragged C and partial K-tiles (K % 128 != 0)."""
+    a = _rand_fp8((m, k), 41 + m)
+    b = _rand_fp8((n, k), 43 + n)
+    c = ops.gemm_fp8(a, b, variant=variant, splits=splits)
+    ref = a.float() @ b.float().T
+    atol, rtol = ops.gemm_tolerance(k)
+    err = (c.float() - ref).abs()
+    assert torch.all(err <= atol + rtol * ref.abs()), (variant, splits, float(err.max()))
+
+
+@pytest.mark.parametrize("m,n,k", [(280, 6352, 15136), (256, 2048, 16400), (333, 1008, 4112)])
+def test_gemm_fp8_default_splitk_plan(ops, m, n, k):
+    """Skinny C with a long K: the fp8 default splits K as k1_fp8_splitk_plan says,
+    bitwise equal to the explicit split on that tile."""
+    top, tv, _, sp = ops.k1_fp8_splitk_plan(m, n, k)
+    assert sp > 1 and top == m
+    a = _rand_fp8((m, k), 47 + m)
+    b = _rand_fp8((n, k), 53 + n)
+    c = ops.gemm_fp8(a, b)
+    assert torch.equal(c, ops.gemm_fp8(a, b, variant=tv, splits=sp))
+    ref = a.float() @ b.float().T
+    atol, rtol = ops.gemm_tolerance(k)
+    assert torch.all((c.float() - ref).abs() <= atol + rtol * ref.abs())
+
+
 def test_gemm_fp8_rejects_bad_shapes(ops):
     a = torch.zeros((256, 136), dtype=torch.float8_e4m3fn, device="cuda")[:, :120]
     with pytest.raises(ValueError):

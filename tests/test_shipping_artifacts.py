@@ -53,6 +53,12 @@ ALLOWED_K1 = {
     "ntm::gemmt::gemm_bf16_tile_ws_kernel<5, 5, 0, false, true>",
     "ntm::gemmt::gemm_bf16_tile_ws_kernel<5, 4, 0, false, true>",
     "ntm::gemmt::gemm_bf16_tile_ws_kernel<4, 5, 0, false, true>",
+    # ... and their split-K builds
+    "ntm::gemmt::gemm_bf16_tile_ws_kernel<4, 4, 0, true, true>",
+    "ntm::gemmt::gemm_bf16_tile_ws_kernel<8, 4, 0, true, true>",
+    "ntm::gemmt::gemm_bf16_tile_ws_kernel<5, 5, 0, true, true>",
+    "ntm::gemmt::gemm_bf16_tile_ws_kernel<5, 4, 0, true, true>",
+    "ntm::gemmt::gemm_bf16_tile_ws_kernel<4, 5, 0, true, true>",
     "ntm::gemmt::gemm_bf16_tile_kernel<8, 5>",
 }
 EXPERIMENTAL_ONLY = ("gemm_bf16_w4_kernel", "gemm_bf16_pp4_kernel", "gemm_bf16_pp5_kernel",

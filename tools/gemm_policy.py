@@ -4,6 +4,11 @@ tile256x128), the default
 dispatch and hipBLASLt (torch.matmul) on M x N x K shapes; one JSON line each.
 
     python tools/gemm_policy.py --shapes 2048x2048x2048,4096x2048x4096 [--rounds 7]
+    python tools/gemm_policy.py --dtype fp8 --random 40   # K1-fp8 default vs hipBLASLt fp8
+
+--dtype fp8 times the K1-fp8 default dispatch, its 256x256 kernel alone
+("pingpong8c") and hipBLASLt's fp8 GEMM (torch._scaled_mm, unit scales, bf16
+out) on e4m3 operands; random shapes then use K % 16.
 """
 import argparse
 import json
@@ -37,12 +42,17 @@ def main():
                     help="time the default dispatch and hipBLASLt only (shape sweeps)")
     ap.add_argument("--random", type=int, default=0,
                     help="append N random shapes (M, N % 8, K % 8 in [256, 8192], seeded)")
+    ap.add_argument("--dtype", default="bf16", choices=("bf16", "fp8"))
     args = ap.parse_args()
     shapes = [tuple(int(x) for x in sh.split("x")) for sh in args.shapes.split(",") if sh]
     if args.random:
         import random
         rng = random.Random(20261016)
         shapes += [tuple(rng.randrange(256, 8193, 8) for _ in range(3)) for _ in range(args.random)]
+        if args.dtype == "fp8":   # same draws; N, K rounded up to 16 (torch._scaled_mm's rule)
+            shapes = [(m, (n + 15) // 16 * 16, (k + 15) // 16 * 16) for m, n, k in shapes]
+    if args.dtype == "fp8":
+        return fp8_sweep(shapes, args)
     for m, n, k in shapes:
         a = ops.fill_uniform_(torch.empty((m, k), dtype=torch.bfloat16, device="cuda"), 1)
         b = ops.fill_uniform_(torch.empty((n, k), dtype=torch.bfloat16, device="cuda"), 2)
@@ -70,6 +80,30 @@ def main():
             v.sort()
             row[f"{name}_tflops"] = round(fl / v[len(v) // 2] / 1e9, 1)
         print(json.dumps(row), flush=True)
+
+
+def fp8_sweep(shapes, args):
+    one = torch.ones((), device="cuda")
+    for m, n, k in shapes:
+        a = ops.fill_uniform_(torch.empty((m, k), dtype=torch.float8_e4m3fn, device="cuda"), 1)
+        b = ops.fill_uniform_(torch.empty((n, k), dtype=torch.float8_e4m3fn, device="cuda"), 2)
+        c = torch.empty((m, n), dtype=torch.bfloat16, device="cuda")
+        fns = {"default": lambda: ops.gemm_fp8(a, b, c),
+               "pingpong8c": lambda: ops.gemm_fp8(a, b, c, variant="pingpong8c"),
+               "hipblaslt": lambda: torch._scaled_mm(a, b.T, scale_a=one, scale_b=one,
+                                                     out_dtype=torch.bfloat16)}
+        t = {name: [] for name in fns}
+        for _ in range(args.rounds):
+            for name, fn in fns.items():
+                t[name].append(timed(fn, args.iters))
+        fl = 2.0 * m * n * k
+        row = {"dtype": "fp8", "shape": [m, n, k], "plan": list(ops.k1_fp8_splitk_plan(m, n, k))}
+        for name, v in t.items():
+            v.sort()
+            row[f"{name}_tflops"] = round(fl / v[len(v) // 2] / 1e9, 1)
+        row["default_over_hipblaslt"] = round(row["default_tflops"] / row["hipblaslt_tflops"], 3)
+        print(json.dumps(row), flush=True)
+    return 0
 
 
 if __name__ == "__main__":

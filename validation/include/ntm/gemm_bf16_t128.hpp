@@ -508,7 +508,7 @@ __global__ void __launch_bounds__(2 * kThreadsT, 1) gemm_bf16_tile_ws_kernel(Gem
     for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   FragsT<MT, NT> f;
   if constexpr (F8) {
-    static_assert(!SPLIT && KNOB == 0, "fp8: plain tiles only");
+    static_assert(KNOB == 0, "fp8: default schedule only");
     ws_consume_f8<MT, NT>(c, f, acc, T);
   } else {
   raw_barrier();  // tile 0 visible
@@ -652,6 +652,41 @@ inline hipError_t launch_gemm_bf16_tile_ws_splitk(const GemmArgs& a, int S, floa
   const unsigned rg = (unsigned)std::min<size_t>(4096, (n4 + 255) / 256);
   hipLaunchKernelGGL(splitk_reduce_kernel, dim3(rg), dim3(256), 0, stream, ws, a.C, a.M, a.N,
                      a.ldc, slices);
+  return hipGetLastError();
+}
+
+// Split-K for K1-fp8: the launch above on the fp8 consumer. K, lda, ldb in fp8
+// elements (N % 8, K % 16, 16-byte aligned rows); slices of the K-tile range
+// counted in bf16-sized pairs (128 e4m3 values per K-tile), ws holds
+// splitk_slices(K / 2, S) M N floats.
+template <int MT, int NT>
+inline hipError_t launch_gemm_fp8_tile_ws_splitk(const void* A, const void* B, __bf16* C, int M,
+                                                 int N, int K, int lda, int ldb, int ldc, int S,
+                                                 float* ws, hipStream_t stream) {
+  if (M <= 0 || N <= 0 || K <= 0 || (N % 8) || (K % 16) || lda < K || ldb < K || ldc < N ||
+      (lda % 16) || (ldb % 16) || (ldc % 4) || S < 1 || !ws)
+    return hipErrorInvalidValue;
+  GemmArgs b;
+  b.A = (const __bf16*)A;
+  b.B = (const __bf16*)B;
+  b.C = C;
+  b.M = M;
+  b.N = N;
+  b.K = K / 2;
+  b.lda = lda / 2;
+  b.ldb = ldb / 2;
+  b.ldc = ldc;
+  b.splitk_ws = ws;
+  b.splitk_kc = splitk_kc(b.K, S);
+  const int slices = splitk_slices(b.K, S);
+  const unsigned tiles = (unsigned)(((M + Cfg<MT, NT>::TM - 1) / Cfg<MT, NT>::TM) *
+                                    ((N + Cfg<MT, NT>::TN - 1) / Cfg<MT, NT>::TN));
+  hipLaunchKernelGGL((gemm_bf16_tile_ws_kernel<MT, NT, 0, true, true>), dim3(tiles, (unsigned)slices),
+                     dim3(2 * kThreadsT), 0, stream, b);
+  const size_t n4 = (size_t)M * N / 4;
+  const unsigned rg = (unsigned)std::min<size_t>(4096, (n4 + 255) / 256);
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(rg), dim3(256), 0, stream, ws, C, M, N, ldc,
+                     slices);
   return hipGetLastError();
 }
 

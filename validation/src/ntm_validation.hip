@@ -386,6 +386,57 @@ NTM_API int ntm_gemm_fp8(const void* A, const void* B, void* C, int M, int N, in
   return ntm_gemm_fp8_variant(0, A, B, C, M, N, K, lda, ldb, ldc, stream);
 }
 
+// K1-fp8 split-K on a wave-specialised tile (15-17, 23, 24): `splits` slices of
+// the K-tile range, fp32 partials in ws (ntm_fp8_splitk_ws_bytes), one reduction.
+NTM_API size_t ntm_fp8_splitk_ws_bytes(int M, int N, int K, int splits) {
+  return ntm_splitk_ws_bytes(M, N, K / 2, splits);
+}
+
+NTM_API int ntm_gemm_fp8_splitk(int variant, int splits, const void* A, const void* B, void* C,
+                                int M, int N, int K, int lda, int ldb, int ldc, void* ws,
+                                size_t ws_bytes, void* stream) {
+  if (!ntm::fp8::shape_ok(M, N, K) || splits < 1 || !ws ||
+      ws_bytes < ntm_fp8_splitk_ws_bytes(M, N, K, splits))
+    return (int)hipErrorInvalidValue;
+  __bf16* c = (__bf16*)C;
+  float* w = (float*)ws;
+  using namespace ntm::gemmt;
+  switch (variant) {
+    case 15: return (int)launch_gemm_fp8_tile_ws_splitk<4, 4>(A, B, c, M, N, K, lda, ldb, ldc, splits, w, S(stream));
+    case 16: return (int)launch_gemm_fp8_tile_ws_splitk<8, 4>(A, B, c, M, N, K, lda, ldb, ldc, splits, w, S(stream));
+    case 17: return (int)launch_gemm_fp8_tile_ws_splitk<5, 5>(A, B, c, M, N, K, lda, ldb, ldc, splits, w, S(stream));
+    case 23: return (int)launch_gemm_fp8_tile_ws_splitk<5, 4>(A, B, c, M, N, K, lda, ldb, ldc, splits, w, S(stream));
+    case 24: return (int)launch_gemm_fp8_tile_ws_splitk<4, 5>(A, B, c, M, N, K, lda, ldb, ldc, splits, w, S(stream));
+    default: return (int)hipErrorInvalidValue;
+  }
+}
+
+// K1-fp8's plan with split-K allowed (what ntm_gemm_fp8_ex runs when given a
+// workspace of ntm_fp8_splitk_ws_bytes(M, N, K, *splits) bytes).
+NTM_API int ntm_k1_fp8_plan_splitk(int M, int N, int K, int* top_rows, int* top_variant,
+                                   int* rest_variant, int* splits) {
+  if (!ntm::fp8::shape_ok(M, N, K) || !top_rows || !top_variant || !rest_variant || !splits)
+    return (int)hipErrorInvalidValue;
+  const K1Plan pl = plan_k1(M, N, K / 2, true, true);
+  if (!pl.feasible()) return (int)hipErrorInvalidValue;
+  *top_rows = pl.top_rows;
+  *top_variant = pl.top_variant;
+  *rest_variant = pl.rest_variant;
+  *splits = pl.splits;
+  return 0;
+}
+
+NTM_API int ntm_gemm_fp8_ex(const void* A, const void* B, void* C, int M, int N, int K, int lda,
+                            int ldb, int ldc, void* ws, size_t ws_bytes, void* stream) {
+  if (ws && ntm::fp8::shape_ok(M, N, K)) {
+    const K1Plan pl = plan_k1(M, N, K / 2, true, true);
+    if (pl.feasible() && pl.splits > 1 && ws_bytes >= ntm_fp8_splitk_ws_bytes(M, N, K, pl.splits))
+      return ntm_gemm_fp8_splitk(pl.top_variant, pl.splits, A, B, C, M, N, K, lda, ldb, ldc, ws,
+                                 ws_bytes, stream);
+  }
+  return ntm_gemm_fp8_variant(0, A, B, C, M, N, K, lda, ldb, ldc, stream);
+}
+
 NTM_API int ntm_gemm_fp8_shape_ok(int M, int N, int K) {
   return ntm::fp8::shape_ok(M, N, K) ? 1 : 0;
 }
