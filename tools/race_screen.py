@@ -61,7 +61,7 @@ def main():
 
         def gemm(a, b, out=None, v=v, fp8=fp8, fv=fv, splits=splits):
             if fp8:
-                return ops.gemm_fp8(a, b, out, variant=fv)
+                return ops.gemm_fp8(a, b, out, variant=fv, splits=splits)
             return ops.gemm_bf16(a, b, out, variant=v, splits=splits)
 
         tm, tn = ops.kernels.TILE_SHAPES.get(v, (0, 0))
