@@ -92,6 +92,9 @@ def fp8_sweep(shapes, args):
                "pingpong8c": lambda: ops.gemm_fp8(a, b, c, variant="pingpong8c"),
                "hipblaslt": lambda: torch._scaled_mm(a, b.T, scale_a=one, scale_b=one,
                                                      out_dtype=torch.bfloat16)}
+        if not args.only_default:   # every fp8 tile alone (wave-specialised, masked edges)
+            for v in ("tile256x128", "tile160", "tile128", "tile160x128", "tile128x160"):
+                fns[v] = lambda v=v: ops.gemm_fp8(a, b, c, variant=v)
         t = {name: [] for name in fns}
         for _ in range(args.rounds):
             for name, fn in fns.items():
