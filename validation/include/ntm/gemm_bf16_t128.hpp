@@ -1,7 +1,8 @@
 // K1 tile kernels: bf16 GEMM with (32 MT) x (32 NT) macro tiles for the sizes
 // where the 256x256 kernels cannot fill the chip: "tile128" (MT = NT = 4,
 // 128x128), "tile256x128" (8, 4), "tile160" (5, 5, 160x160) and
-// "tile256x160" (8, 5).
+// "tile256x160" (8, 5); the wave-specialised kernel below also serves
+// K1-fp8's small and mid tiles (F8 = true: its own consumer, same producers).
 //
 //   C[M x N] (bf16) = A[M x K] (bf16) * B[N x K]^T (bf16), fp32 accumulate.
 //
