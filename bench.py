@@ -183,6 +183,17 @@ def run_validation_job(n: int, timeout_s: float = 240.0) -> dict:
     }
 
 
+def pair_busbw(rccl, xgmi) -> list:
+    """C2 against RCCL at the message sizes both sweeps ran (bf16, in place,
+    same timing loop): one row per shared size with both busbw and the ratio."""
+    rccl_at = {r.bytes: r.busbw_GBps for r in rccl}
+    return [{"bytes": r.bytes, "rccl_busbw_GBps": round(rccl_at[r.bytes], 1),
+             "xgmi_busbw_GBps": round(r.busbw_GBps, 1),
+             "xgmi_over_rccl": round(r.busbw_GBps / rccl_at[r.bytes], 3)
+             if rccl_at[r.bytes] > 0 else None}
+            for r in xgmi if r.bytes in rccl_at]
+
+
 def relaunch_distributed(args) -> int:
     """Start torch.distributed.run as a CHILD process (never exec) and return its rc."""
     port = os.environ.get("MASTER_PORT", "29531")
@@ -348,7 +359,10 @@ def main(argv=None) -> int:
             # line still comes out with the error recorded.
             from nvidia_terraform_modules_amd.parallel.xgmi import XgmiAllReduce
 
-            xs = [b for b in coll.sweep_sizes(1 << 10, max_b, 4) if b <= 1 << 30]
+            # the RCCL bf16 sizes from 512 B to 1 GiB (so the two can be paired) that
+            # split into 8-element chunks per rank
+            xs = [b for b in coll.sweep_sizes(8, max_b, 4)
+                  if 512 <= b <= 1 << 30 and (b // 2) % (8 * n) == 0]
             ar, err = None, ""
             try:
                 ar = XgmiAllReduce(env, max_bytes=max(xs), nblk=64)
@@ -365,6 +379,7 @@ def main(argv=None) -> int:
                     {"bytes": r.bytes, "time_us": round(r.time_us, 1),
                      "busbw_GBps": round(r.busbw_GBps, 1), "errors": r.errors} for r in xr]
                 extras["xgmi_peak_busbw_GBps"] = coll.peak_busbw(xr)
+                extras["xgmi_vs_rccl_bf16"] = pair_busbw(res, xr)
                 extras["xgmi_timed_out"] = dist.all_reduce_max(
                     env, 1.0 if ar.timed_out() else 0.0) > 0
                 ar.close()

@@ -108,3 +108,24 @@ def test_bench_on_one_gpu_json_contract(tmp_path):
     assert job["ran"] and job["passed"], job
     assert 0 < d["time_to_gpu_ready_in_node_s"] < 30
     assert json.loads(out.read_text()) == d
+
+
+def test_pair_busbw_pairs_xgmi_with_rccl_sizes():
+    """bench.py's C2-vs-RCCL table: one row per size both sweeps ran; the xGMI
+    sweep's sizes are a subset of the RCCL bf16 sweep's (512 B .. 1 GiB)."""
+    from types import SimpleNamespace as R
+
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+    import bench
+    from nvidia_terraform_modules_amd.parallel import collectives as coll
+
+    rccl = [R(bytes=b, busbw_GBps=100.0 + i) for i, b in enumerate(coll.sweep_sizes(8, 1 << 33, 4))]
+    n = 8
+    xs = [b for b in coll.sweep_sizes(8, 1 << 33, 4) if 512 <= b <= 1 << 30 and (b // 2) % (8 * n) == 0]
+    assert xs and set(xs) <= {r.bytes for r in rccl}
+    xgmi = [R(bytes=b, busbw_GBps=200.0) for b in xs]
+    rows = bench.pair_busbw(rccl, xgmi)
+    assert [r["bytes"] for r in rows] == xs
+    assert all(r["xgmi_over_rccl"] > 1.0 for r in rows)
+    assert bench.pair_busbw([R(bytes=512, busbw_GBps=0.0)], [R(bytes=512, busbw_GBps=1.0)])[0][
+        "xgmi_over_rccl"] is None

@@ -40,6 +40,12 @@ def main():
         exp = ((2.0 ** (i % 4)) * (n * (n + 1) / 2 + 2 * n)).to(torch.bfloat16)
         results.append({"count": count, "wrong": int((buf != exp).sum()),
                         "timeout": ar.timed_out(), "path": "in_place"})
+    # bench.py's C2 sweep, as it runs at N > 1: all_reduce_sweep with the
+    # registered buffer as operand (zero-copy, in place), element check + timing
+    from nvidia_terraform_modules_amd.parallel.collectives import all_reduce_sweep
+    for r in all_reduce_sweep(env, [512, 2048, 1 << 20], dtype="bf16", iters=3, warmup=1, impl=ar):
+        results.append({"count": r.count, "wrong": r.errors, "timeout": ar.timed_out(),
+                        "path": "bench_sweep", "busbw_GBps": r.busbw_GBps})
     ar.close()
     print(json.dumps({"rank": env.rank, "results": results}), flush=True)
     shutdown(env)
