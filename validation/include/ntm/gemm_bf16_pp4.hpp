@@ -98,7 +98,7 @@ __device__ __forceinline__ void read_b_p(const PCtx& c, bf16x8 (&b)[2][2], int h
       b[nt][ks] = *(const bf16x8*)(base + ((c.wc * 2 + nt) * 2 + ks) * 1024);
 }
 
-template <int P, bool ODD>
+template <int P, bool ODD, int F8 = 0>
 __device__ __forceinline__ void phase_p(const PCtx& c, Frags3& f, f32x4 (&acc)[2][2][4][2],
                                         const TileRef& cur, const TileRef& nxt,
                                         bool has_next, int t, int T) {
@@ -115,24 +115,31 @@ __device__ __forceinline__ void phase_p(const PCtx& c, Frags3& f, f32x4 (&acc)[2
   if constexpr (P == 3) issue_p<kBHi>(c, cur, nxt, has_next, t + 2, T, b);
   wait_vmcnt<10>();
   raw_barrier();
-  if constexpr (P == 0) mma_quadrant<false>(acc[0][0], f.a, bcur);
-  if constexpr (P == 1) mma_quadrant<false>(acc[0][1], f.a, both);
-  if constexpr (P == 2) mma_quadrant<false>(acc[1][1], f.a, both);
-  if constexpr (P == 3) mma_quadrant<false>(acc[1][0], f.a, bcur);
+  if constexpr (F8) {  // K1-fp8 (experimental persistent build, gemm_fp8_diag.hpp knob 6)
+    if constexpr (P == 0) mma_quadrant_f8<F8>(acc[0][0], f.a, bcur);
+    if constexpr (P == 1) mma_quadrant_f8<F8>(acc[0][1], f.a, both);
+    if constexpr (P == 2) mma_quadrant_f8<F8>(acc[1][1], f.a, both);
+    if constexpr (P == 3) mma_quadrant_f8<F8>(acc[1][0], f.a, bcur);
+  } else {
+    if constexpr (P == 0) mma_quadrant<false>(acc[0][0], f.a, bcur);
+    if constexpr (P == 1) mma_quadrant<false>(acc[0][1], f.a, both);
+    if constexpr (P == 2) mma_quadrant<false>(acc[1][1], f.a, both);
+    if constexpr (P == 3) mma_quadrant<false>(acc[1][0], f.a, bcur);
+  }
   raw_barrier();
 }
 
-template <bool ODD>
+template <bool ODD, int F8 = 0>
 __device__ __forceinline__ void ktile_p(const PCtx& c, Frags3& f, f32x4 (&acc)[2][2][4][2],
                                         const TileRef& cur, const TileRef& nxt, bool has_next,
                                         int t, int T) {
-  phase_p<0, ODD>(c, f, acc, cur, nxt, has_next, t, T);
-  phase_p<1, ODD>(c, f, acc, cur, nxt, has_next, t, T);
-  phase_p<2, ODD>(c, f, acc, cur, nxt, has_next, t, T);
-  phase_p<3, ODD>(c, f, acc, cur, nxt, has_next, t, T);
+  phase_p<0, ODD, F8>(c, f, acc, cur, nxt, has_next, t, T);
+  phase_p<1, ODD, F8>(c, f, acc, cur, nxt, has_next, t, T);
+  phase_p<2, ODD, F8>(c, f, acc, cur, nxt, has_next, t, T);
+  phase_p<3, ODD, F8>(c, f, acc, cur, nxt, has_next, t, T);
 }
 
-template <bool kRowSum, int EPI = 0>
+template <bool kRowSum, int EPI = 0, int F8 = 0>
 __global__ void __launch_bounds__(kThreads, 2)
     gemm_bf16_pp4_kernel(GemmArgs p) {
   __shared__ __attribute__((aligned(16))) char smem[kLdsBytes3];
@@ -188,9 +195,10 @@ __global__ void __launch_bounds__(kThreads, 2)
 
   while (true) {
     for (int t = 0; t < T; t += 2) {
-      ktile_p<false>(c, f, acc, cur, nxt, has_next, t, T);
-      ktile_p<true>(c, f, acc, cur, nxt, has_next, t + 1, T);
+      ktile_p<false, F8>(c, f, acc, cur, nxt, has_next, t, T);
+      ktile_p<true, F8>(c, f, acc, cur, nxt, has_next, t + 1, T);
     }
+    if constexpr (F8) mfma_drain();  // asm MFMAs: results land before the VALU reads
     // boundary: retire every load in flight BEFORE any store (see header)
     wait_vmcnt<0>();
     store_tile_epi<kRowSum, EPI>(p, Ctx{c.lds, {}, c.frag_off, c.w, c.wr, c.wc}, acc, cur.m0, cur.n0,

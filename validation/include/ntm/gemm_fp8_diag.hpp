@@ -9,6 +9,7 @@
 // with exact integer data").
 #pragma once
 
+#include "ntm/gemm_bf16_pp4.hpp"
 #include "ntm/gemm_fp8.hpp"
 
 namespace ntm {
@@ -52,6 +53,16 @@ inline hipError_t launch_gemm_fp8_knob(const void* A, const void* B, __bf16* C, 
     case 3: hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, kGroupM, false, kEpiDefault, 2, 1>), g, b, 0, s, a); break;
     case 4: hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, kGroupM, false, kEpiWide | kEpiNT, 0, 1>), g, b, 0, s, a); break;
     case 5: hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, kGroupM, false, kEpiDefault, 0, 1>), g, b, 0, s, a); break;
+    case 6: {  // persistent (gemm_bf16_pp4.hpp): DMA pipeline across tiles, register epilogue
+      if (!::ntm::gemm3::shape_ok3(a.M, a.N, a.K)) return hipErrorInvalidValue;
+      const int ntiles = (M / BM) * (N / BN);
+      int gp = ::ntm::gemmp::cu_count();
+      gp -= gp % 8;
+      if (gp <= 0) gp = 8;
+      if (gp > ntiles) gp = ntiles;
+      hipLaunchKernelGGL((::ntm::gemmp::gemm_bf16_pp4_kernel<false, kEpiWide | kEpiNT, 3>), dim3(gp), b, 0, s, a);
+      break;
+    }
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
