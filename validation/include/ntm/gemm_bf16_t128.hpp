@@ -410,8 +410,10 @@ __device__ __forceinline__ void ws_produce(const CtxT& c, const Clamp& q, int T)
 // every read of tile t issued after barrier t and retired before barrier t+1),
 // so the producer loop is unchanged. Next tile's row 0 needs B[nt] about NT
 // 32-cycle MFMAs after its read was issued.
+// Fragment i (A row block i < MT, else B column block i - MT) of K-tile kt,
+// both k-halves: the 32-byte operand of one f8f6f4 MFMA.
 template <int MT, int NT>
-__device__ __forceinline__ void read_a_f8(const CtxT& c, FragsT<MT, NT>& f, int kt, int i) {
+__device__ __forceinline__ void read_both_halves(const CtxT& c, FragsT<MT, NT>& f, int kt, int i) {
   read_frag<MT, NT>(c, f, kt, i);
   read_frag<MT, NT>(c, f, kt, MT + NT + i);
 }
@@ -426,7 +428,7 @@ __device__ __forceinline__ void ws_consume_f8(const CtxT& c, FragsT<MT, NT>& f,
   };
   raw_barrier();  // tile 0 visible
 #pragma unroll
-  for (int i = 0; i < MT + NT; ++i) read_a_f8<MT, NT>(c, f, 0, i);
+  for (int i = 0; i < MT + NT; ++i) read_both_halves<MT, NT>(c, f, 0, i);
   for (int t = 0; t < T; ++t) {
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
@@ -443,11 +445,11 @@ __device__ __forceinline__ void ws_consume_f8(const CtxT& c, FragsT<MT, NT>& f,
         // A[mt-1] of tile t+1 (t + 1 == T: stale slot, unused): its last MFMA was row mt-1
         if (nt == 0) read_frag<MT, NT>(c, f, t + 1, mt - 1);
         if (nt == 1) read_frag<MT, NT>(c, f, t + 1, MT + NT + mt - 1);
-        if (mt == MT - 1) read_a_f8<MT, NT>(c, f, t + 1, MT + nt);  // B[nt]
+        if (mt == MT - 1) read_both_halves<MT, NT>(c, f, t + 1, MT + nt);  // B[nt]
         __builtin_amdgcn_sched_barrier(0);
       }
     }
-    read_a_f8<MT, NT>(c, f, t + 1, MT - 1);
+    read_both_halves<MT, NT>(c, f, t + 1, MT - 1);
     __builtin_amdgcn_sched_barrier(0);
   }
 }
