@@ -169,3 +169,19 @@ def test_fp8_plan_rejects_bad_shapes(fp8_plan):
     for m, n, k in [(256, 252, 256), (256, 256, 24), (0, 256, 256)]:
         with pytest.raises(ValueError):
             fp8_plan(m, n, k)
+
+
+def test_fp8_entry_points_reject_bad_shapes_before_any_launch(fp8_plan):
+    """The fp8 C ABI validates the shape on the host (no GPU touched): N % 8,
+    K % 16, known variants only; split-K needs a masked tile and a big-enough
+    workspace."""
+    from nvidia_terraform_modules_amd.ops._lib import lib
+
+    L = lib()
+    for m, n, k in [(256, 252, 256), (256, 256, 24), (0, 256, 256)]:
+        assert L.ntm_gemm_fp8_variant(0, None, None, None, m, n, k, k, k, n, None) != 0
+        assert L.ntm_gemm_fp8(None, None, None, m, n, k, k, k, n, None) != 0
+    assert L.ntm_gemm_fp8_variant(18, None, None, None, 256, 256, 256, 256, 256, 256, None) != 0
+    assert L.ntm_gemm_fp8_splitk(5, 2, None, None, None, 256, 256, 256, 256, 256, 256, None, 0,
+                                 None) != 0
+    assert L.ntm_fp8_splitk_ws_bytes(280, 6352, 15136, 3) == 4 * 3 * 280 * 6352
