@@ -17,6 +17,7 @@
 #              hipBLASLt at 8192^3 (PMC_DTYPE=fp8: K1-fp8 vs hipBLASLt fp8; PMC_ARGS: extra
 #              tools/gemm_pair.py arguments, e.g. "--variant A --versus B") +
 #              tools/pmc_summary.py -> <tag>/pmc/summary.json
+#   fp8        K1-fp8 vs hipBLASLt fp8: square sizes (gemm_fp8_check) + the 41-shape sweep
 #   py:<file>  python -u <file> (a tool script; its own args via PYARGS)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
@@ -78,6 +79,13 @@ for s in "${STEPS[@]}"; do
       timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$P/trace" -o run \
         -- python3 $pair > "$P/trace.log" 2>&1 || fail "pmc trace" $? "$P/trace.log"
       python3 tools/pmc_summary.py "$P" > "$P/summary.json" && head -c 3000 "$P/summary.json" ;;
+    fp8)
+      timeout -k 10 600 python -u tools/gemm_fp8_check.py --sizes 1024,2048,2560,3072,4096,4608,6144,8192 \
+        --iters 30 --rounds 5 > "$O/fp8_check.log" 2>&1 || fail fp8 $? "$O/fp8_check.log"
+      timeout -k 10 900 python -u tools/gemm_policy.py --dtype fp8 --only-default --shapes 8192x8192x8192 \
+        --random 40 --rounds 5 --iters 20 > "$O/fp8_policy_random.log" 2>&1 \
+        || fail "fp8 policy" $? "$O/fp8_policy_random.log"
+      python3 -c "import json,statistics,sys; r=[json.loads(l)['default_over_hipblaslt'] for l in open(sys.argv[1]) if l.startswith('{')]; print(f'fp8 default ahead of hipBLASLt on {sum(x > 1 for x in r)} of {len(r)}, median {statistics.median(r):.3f}')" "$O/fp8_policy_random.log" ;;
     py:*)
       f=${s#py:}
       timeout -k 10 600 python -u "$f" $PYARGS > "$O/$(basename "$f" .py).log" 2>&1 \
