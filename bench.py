@@ -380,6 +380,7 @@ def main(argv=None) -> int:
                      "busbw_GBps": round(r.busbw_GBps, 1), "errors": r.errors} for r in xr]
                 extras["xgmi_peak_busbw_GBps"] = coll.peak_busbw(xr)
                 extras["xgmi_vs_rccl_bf16"] = pair_busbw(res, xr)
+                extras["xgmi_blocks_per_rank"] = ar.nblk
                 extras["xgmi_timed_out"] = dist.all_reduce_max(
                     env, 1.0 if ar.timed_out() else 0.0) > 0
                 ar.close()
