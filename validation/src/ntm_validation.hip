@@ -6,7 +6,8 @@
 // can be captured in a hipGraph (playbook §6 Guideline 9).
 //
 // Only the kernels the default dispatch can select are instantiated here
-// (pingpong8c / pingpong8b 256x256, the four tile shapes, K1-fp8, K2, K3).
+// (pingpong8c / pingpong8b 256x256, the six tile shapes and split-K, K1-fp8 on
+// the 256x256 kernel and the wave-specialised tiles, K2, K3).
 // The non-default K1 builds, schedule knobs and diagnostics live in
 // ntm_experimental.hip -> libntm_experimental.so (tests and tools only).
 #include "ntm/aux_kernels.hpp"
