@@ -23,6 +23,7 @@ from .kernels import (  # noqa: F401
     gemm_bf16,
     gemm_bf16_rowsum,
     gemm_fp8,
+    gemm_fp8_rowsum,
     gemm_fp8_shape_ok,
     gemm_shape_ok,
     gemm_tolerance,

@@ -51,6 +51,10 @@ def _declare(lib: ctypes.CDLL) -> None:
         "ntm_abft_check": ([c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int,
                             c_vp, c_vp, c_vp], c_int),
         "ntm_abft_result_bytes": ([], c_int),
+        "ntm_gemm_fp8_rowsum": (
+            [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp], c_int),
+        "ntm_abft_check_fp8": ([c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int,
+                                c_vp, c_vp, c_vp], c_int),
         "ntm_fill_uniform_bf16": ([c_vp, c_size, ctypes.c_ulonglong, c_float, c_vp], c_int),
         "ntm_k1_plan": ([c_int, c_int, c_int, c_vp, c_vp, c_vp], c_int),
         "ntm_k1_plan_splitk": ([c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp], c_int),

@@ -315,6 +315,32 @@ def gemm_bf16_rowsum(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None 
     return out, rowsum
 
 
+def gemm_fp8_rowsum(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
+                    rowsum: torch.Tensor | None = None) -> tuple[torch.Tensor, torch.Tensor]:
+    """K1-fp8 with the fused ABFT epilogue (the 256x256 fp8 build, M, N, K %
+    256): returns ``(out, rowsum)`` as ``gemm_bf16_rowsum`` does; check it with
+    ``abft_check`` on the same e4m3 operands."""
+    _require(a, "a", torch.float8_e4m3fn)
+    _require(b, "b", torch.float8_e4m3fn)
+    m, k = a.shape
+    n = b.shape[0]
+    if b.shape[1] != k or m % 256 or n % 256 or k % 256:
+        raise ValueError(f"shape ({m},{n},{k}) not tiled by the 256x256 fp8 kernel (M, N, K % 256)")
+    if out is None:
+        out = torch.empty((m, n), dtype=torch.bfloat16, device=a.device)
+    _require(out, "out", torch.bfloat16)
+    if rowsum is None:
+        rowsum = torch.empty(m, dtype=torch.float32, device=a.device)
+    if rowsum.dtype != torch.float32 or rowsum.numel() < m or not rowsum.is_contiguous():
+        raise ValueError("rowsum must be a contiguous fp32 tensor of >= M entries")
+    rowsum.zero_()
+    rc = lib().ntm_gemm_fp8_rowsum(a.data_ptr(), b.data_ptr(), out.data_ptr(), rowsum.data_ptr(),
+                                   m, n, k, a.stride(0), b.stride(0), out.stride(0),
+                                   stream_handle())
+    check(rc, "ntm_gemm_fp8_rowsum")
+    return out, rowsum
+
+
 @dataclass
 class AbftReport:
     rows: int
@@ -336,16 +362,20 @@ class AbftReport:
 def abft_check(a: torch.Tensor, b: torch.Tensor, c: torch.Tensor,
                rowsum: torch.Tensor) -> AbftReport:
     """K3: O(MK + NK + MN) ABFT check of ``c = a @ b.T`` against the fused
-    row checksum (see aux_kernels.hpp). Synchronises to read the result."""
+    row checksum (see aux_kernels.hpp); ``a`` / ``b`` bf16 (K1) or e4m3
+    (K1-fp8). Synchronises to read the result."""
     m, k = a.shape
     n = b.shape[0]
     if c.shape != (m, n) or c.dtype != torch.bfloat16 or c.stride(1) != 1:
         raise ValueError("c must be [M, N] bf16 with unit inner stride")
+    if a.dtype != b.dtype or a.dtype not in (torch.bfloat16, torch.float8_e4m3fn):
+        raise ValueError("a and b must both be bf16 or both float8_e4m3fn")
+    fn = lib().ntm_abft_check if a.dtype == torch.bfloat16 else lib().ntm_abft_check_fp8
     scratch = torch.empty(k, dtype=torch.float64, device=a.device)
     res = torch.empty(lib().ntm_abft_result_bytes(), dtype=torch.uint8, device=a.device)
-    rc = lib().ntm_abft_check(a.data_ptr(), b.data_ptr(), c.data_ptr(), rowsum.data_ptr(),
-                              m, n, k, a.stride(0), b.stride(0), c.stride(0),
-                              scratch.data_ptr(), res.data_ptr(), stream_handle())
+    rc = fn(a.data_ptr(), b.data_ptr(), c.data_ptr(), rowsum.data_ptr(),
+            m, n, k, a.stride(0), b.stride(0), c.stride(0),
+            scratch.data_ptr(), res.data_ptr(), stream_handle())
     check(rc, "ntm_abft_check")
     raw = res.cpu().numpy().tobytes()
     return AbftReport(

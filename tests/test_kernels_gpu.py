@@ -194,6 +194,40 @@ def test_abft_detects_corruption(ops):
     assert not ops.abft_check(a, b, c3, rs).ok
 
 
+@pytest.mark.parametrize("m,n,k", [(256, 256, 256), (512, 1024, 768), (2048, 2048, 2048),
+                                   (8192, 8192, 8192)])
+def test_abft_fp8_rowsum_and_check(ops, m, n, k):
+    """K1-fp8 with the fused row checksum: the checksum matches the fp64 row sums
+    of the exact e4m3 product, C is bitwise the plain fp8 kernel's, the O(n^2)
+    checker passes, and it flags a stored-output and an accumulator fault."""
+    a = ops.fill_uniform_(torch.empty((m, k), dtype=torch.float8_e4m3fn, device="cuda"), 51 + k)
+    b = ops.fill_uniform_(torch.empty((n, k), dtype=torch.float8_e4m3fn, device="cuda"), 53 + n)
+    c, rs = ops.gemm_fp8_rowsum(a, b)
+    assert torch.equal(c, ops.gemm_fp8(a, b, variant="pingpong8c"))
+    if m * k < 2**27:
+        exact = a.double() @ b.double().sum(0)
+        norm = (a.float() @ b.float().T).double().norm(dim=1)
+        assert torch.all((rs.double() - exact).abs() <= 1e-3 + 2**-14 * norm)
+    rep = ops.abft_check(a, b, c, rs)
+    assert rep.ok, rep.as_dict()
+    c2 = c.clone()
+    c2[m // 2, n // 3] += 64.0
+    rep = ops.abft_check(a, b, c2, rs)
+    assert rep.bad_store == 1 and rep.bad_acc == 0
+    rs2 = rs.clone()
+    rs2[m - 1] += 0.5
+    assert ops.abft_check(a, b, c, rs2).bad_acc == 1
+
+
+def test_gemm_fp8_rowsum_rejects_ragged(ops):
+    a = torch.zeros((256, 272), dtype=torch.float8_e4m3fn, device="cuda")
+    with pytest.raises(ValueError):
+        ops.gemm_fp8_rowsum(a, a)             # K % 256
+    with pytest.raises(ValueError):
+        ops.abft_check(a, a.to(torch.bfloat16), torch.zeros((256, 256), dtype=torch.bfloat16,
+                                                            device="cuda"), torch.zeros(256, device="cuda"))
+
+
 @pytest.mark.parametrize("variant", ["pingpong8", "pingpong8b", "pingpong8c", "pingpong8p",
                                      "pingpong8w", "pingpong8wi", "pingpong8ww", "pingpong8cw",
                                      "pingpong8cwe", "pingpong8cwn", "pingpong8cwne",

@@ -28,6 +28,7 @@ ALLOWED_K1 = {
     "ntm::gemm3::gemm_bf16_pp3_kernel<true, 8, false, 0, 0, 0>",
     "ntm::gemm3::gemm_bf16_pp3_kernel<true, 8, false, 10, 0, 0>",
     "ntm::gemm3::gemm_bf16_pp3_kernel<false, 8, false, 10, 0, 3>",
+    "ntm::gemm3::gemm_bf16_pp3_kernel<true, 8, false, 10, 0, 3>",   # K1-fp8 + ABFT row sum
     "ntm::gemm3::gemm_bf16_pp3_kernel<false, 8, false, 26, 0, 0>",  # masked edge tiles
     "ntm::gemm3::gemm_bf16_pp3_kernel<false, 8, false, 26, 0, 3>",  # K1-fp8, masked
     "ntm::gemm3::gemm_bf16_pp3_kernel<false, 8, false, 58, 0, 0>",  # masked + partial K

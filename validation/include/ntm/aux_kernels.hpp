@@ -194,16 +194,17 @@ struct AbftResult {
   unsigned int max_rel_store_bits;
 };
 
+// T: the operand type (__bf16 for K1, uint8_t = OCP e4m3 for K1-fp8).
+template <typename T>
 __global__ void __launch_bounds__(256)
-    abft_colsum_kernel(const __bf16* __restrict__ B, int N, int K, int ldb,
+    abft_colsum_kernel(const T* __restrict__ B, int N, int K, int ldb,
                        int rows_per_chunk, double* __restrict__ bsum) {
   const int k = blockIdx.x * 256 + threadIdx.x;
   if (k >= K) return;
   const int n0 = blockIdx.y * rows_per_chunk;
   const int n1 = min(N, n0 + rows_per_chunk);
   double s = 0.0;
-  for (int n = n0; n < n1; ++n)
-    s += bf16_bits_to_f32(((const uint16_t*)B)[(size_t)n * ldb + k]);
+  for (int n = n0; n < n1; ++n) s += ref_load(B, (size_t)n * ldb + k);
   unsafeAtomicAdd(bsum + k, s);
 }
 
@@ -222,18 +223,19 @@ __device__ __forceinline__ void atomic_max_nonneg(unsigned int* p, float v) {
   atomicMax(p, bits);
 }
 
+template <typename T>
 __global__ void __launch_bounds__(256)
-    abft_row_check_kernel(const __bf16* __restrict__ A, int lda,
+    abft_row_check_kernel(const T* __restrict__ A, int lda,
                           const __bf16* __restrict__ C, int ldc,
                           const float* __restrict__ rowsum,
                           const double* __restrict__ bsum, int N, int K,
                           AbftResult* __restrict__ out) {
   __shared__ double s_tmp[4];
   const int m = blockIdx.x;
-  const uint16_t* a = (const uint16_t*)A + (size_t)m * lda;
+  const T* a = A + (size_t)m * lda;
   const uint16_t* c = (const uint16_t*)C + (size_t)m * ldc;
   double r = 0.0, sc = 0.0, ss = 0.0;
-  for (int k = threadIdx.x; k < K; k += 256) r += bf16_bits_to_f32(a[k]) * bsum[k];
+  for (int k = threadIdx.x; k < K; k += 256) r += ref_load(a, k) * bsum[k];
   for (int n = threadIdx.x; n < N; n += 256) {
     const double v = bf16_bits_to_f32(c[n]);
     sc += v;

@@ -468,17 +468,42 @@ NTM_API int ntm_gemm_bf16_rowsum(const void* A, const void* B, void* C,
                                         : (int)ntm::gemm2::launch_gemm_bf16_pp2(a, S(stream));
 }
 
-// ABFT check of C = A B^T against the fused rowsum. scratch: K doubles;
-// result: ntm::aux::AbftResult (both zeroed here, stream-ordered).
-NTM_API int ntm_abft_check(const void* A, const void* B, const void* C,
-                           const float* rowsum, int M, int N, int K, int lda,
-                           int ldb, int ldc, double* scratch, void* result,
-                           void* stream) {
+// K1-fp8 with the fused ABFT row checksum: the 256x256 fp8 build with kRowSum
+// (exact shapes: M, N, K % 256); rowsum zeroed by the caller on `stream`.
+NTM_API int ntm_gemm_fp8_rowsum(const void* A, const void* B, void* C, float* rowsum, int M,
+                                int N, int K, int lda, int ldb, int ldc, void* stream) {
+  if (!rowsum || !ntm::fp8::shape_exact(M, N, K) || lda < K || ldb < K || ldc < N ||
+      (lda % 16) || (ldb % 16) || (ldc % 8))
+    return (int)hipErrorInvalidValue;
+  ntm::gemm::GemmArgs a;
+  a.A = (const __bf16*)A;  // byte image: two e4m3 per bf16 slot (gemm_fp8.hpp)
+  a.B = (const __bf16*)B;
+  a.C = (__bf16*)C;
+  a.M = M;
+  a.N = N;
+  a.K = K / 2;
+  a.lda = lda / 2;
+  a.ldb = ldb / 2;
+  a.ldc = ldc;
+  a.rowsum = rowsum;
+  using ntm::gemm3::gemm_bf16_pp3_kernel;
+  using ntm::gemm3::kEpiDefault;
+  hipLaunchKernelGGL((gemm_bf16_pp3_kernel<true, ntm::gemm::kGroupM, false, kEpiDefault, 0, 3>),
+                     dim3((unsigned)((M / ntm::gemm::BM) * (N / ntm::gemm::BN))),
+                     dim3(ntm::gemm::kThreads), 0, S(stream), a);
+  return (int)hipGetLastError();
+}
+
+namespace {
+template <typename T>
+int abft_check_t(const void* A, const void* B, const void* C, const float* rowsum, int M, int N,
+                 int K, int lda, int ldb, int ldc, double* scratch, void* result,
+                 hipStream_t stream) {
   if (M <= 0 || N <= 0 || K <= 0 || !rowsum || !scratch || !result)
     return (int)hipErrorInvalidValue;
-  hipError_t e = hipMemsetAsync(scratch, 0, sizeof(double) * (size_t)K, S(stream));
+  hipError_t e = hipMemsetAsync(scratch, 0, sizeof(double) * (size_t)K, stream);
   if (e != hipSuccess) return (int)e;
-  e = hipMemsetAsync(result, 0, sizeof(ntm::aux::AbftResult), S(stream));
+  e = hipMemsetAsync(result, 0, sizeof(ntm::aux::AbftResult), stream);
   if (e != hipSuccess) return (int)e;
   // ~2048 column blocks x row chunks: enough parallelism for 256 CUs
   const int kb = (K + 255) / 256;
@@ -486,12 +511,31 @@ NTM_API int ntm_abft_check(const void* A, const void* B, const void* C,
   if (chunks > N) chunks = N;
   const int rpc = (N + chunks - 1) / chunks;
   chunks = (N + rpc - 1) / rpc;
-  hipLaunchKernelGGL(ntm::aux::abft_colsum_kernel, dim3(kb, chunks), dim3(256),
-                     0, S(stream), (const __bf16*)B, N, K, ldb, rpc, scratch);
-  hipLaunchKernelGGL(ntm::aux::abft_row_check_kernel, dim3(M), dim3(256), 0,
-                     S(stream), (const __bf16*)A, lda, (const __bf16*)C, ldc,
-                     rowsum, scratch, N, K, (ntm::aux::AbftResult*)result);
+  hipLaunchKernelGGL(ntm::aux::abft_colsum_kernel<T>, dim3(kb, chunks), dim3(256), 0, stream,
+                     (const T*)B, N, K, ldb, rpc, scratch);
+  hipLaunchKernelGGL(ntm::aux::abft_row_check_kernel<T>, dim3(M), dim3(256), 0, stream,
+                     (const T*)A, lda, (const __bf16*)C, ldc, rowsum, scratch, N, K,
+                     (ntm::aux::AbftResult*)result);
   return (int)hipGetLastError();
+}
+}  // namespace
+
+// ABFT check of K1-fp8's C = A B^T (e4m3 operands) against its fused rowsum.
+NTM_API int ntm_abft_check_fp8(const void* A, const void* B, const void* C, const float* rowsum,
+                               int M, int N, int K, int lda, int ldb, int ldc, double* scratch,
+                               void* result, void* stream) {
+  return abft_check_t<uint8_t>(A, B, C, rowsum, M, N, K, lda, ldb, ldc, scratch, result,
+                               S(stream));
+}
+
+// ABFT check of C = A B^T against the fused rowsum. scratch: K doubles;
+// result: ntm::aux::AbftResult (both zeroed here, stream-ordered).
+NTM_API int ntm_abft_check(const void* A, const void* B, const void* C,
+                           const float* rowsum, int M, int N, int K, int lda,
+                           int ldb, int ldc, double* scratch, void* result,
+                           void* stream) {
+  return abft_check_t<__bf16>(A, B, C, rowsum, M, N, K, lda, ldb, ldc, scratch, result,
+                              S(stream));
 }
 
 NTM_API int ntm_abft_result_bytes() {
