@@ -65,6 +65,7 @@ def test_binary_passes_and_writes_sidecar_outputs(tmp_path):
     assert rep["passed"] and rep["gpus"][0]["gemm_wrong"] == 0
     assert rep["gpus"][0]["abft_bad_rows"] == 0
     assert rep["gpus"][0]["gemm_fp8_wrong"] == 0 and rep["gpus"][0]["gemm_fp8_tflops"] > 0
+    assert rep["gpus"][0]["gemm_fp8_abft_bad_rows"] == 0
     assert rep["gpus"][0]["hbm_read_GBps"] > 1000
     assert rep["start_epoch_s"] > 1.6e9 and rep["end_epoch_s"] >= rep["start_epoch_s"]
     t = json.loads(term.read_text())
@@ -79,7 +80,8 @@ def test_binary_passes_and_writes_sidecar_outputs(tmp_path):
 @pytest.mark.gpu
 @pytest.mark.parametrize("kind,needle", [("corrupt_gemm", "GEMM verification failed"),
                                          ("corrupt_abft", "ABFT"),
-                                         ("corrupt_fp8", "fp8 GEMM verification failed")])
+                                         ("corrupt_fp8", "fp8 GEMM verification failed"),
+                                         ("corrupt_fp8_abft", "fp8 GEMM ABFT checksum failed")])
 def test_binary_fault_injection_fails_loudly(tmp_path, kind, needle):
     _have_bin()
     term = tmp_path / "term"
@@ -172,6 +174,7 @@ def test_binary_no_fp8_skips_the_fp8_check():
     assert rc == 0
     g = _last_json(out)["gpus"][0]
     assert g["gemm_fp8_wrong"] is None and g["gemm_fp8_tflops"] == 0
+    assert g["gemm_fp8_abft_bad_rows"] is None
 
 
 # ------------------------------------------------ validation image runtime

@@ -63,6 +63,10 @@ int ntm_gemm_bf16_rowsum(const void*, const void*, void*, float*, int, int, int,
 int ntm_abft_check(const void*, const void*, const void*, const float*, int, int, int, int, int,
                    int, double*, void*, void*);
 int ntm_abft_result_bytes();
+int ntm_gemm_fp8_rowsum(const void*, const void*, void*, float*, int, int, int, int, int, int,
+                        void*);
+int ntm_abft_check_fp8(const void*, const void*, const void*, const float*, int, int, int, int,
+                       int, int, double*, void*, void*);
 int ntm_xgmi_allreduce_bf16(const void* const*, void* const*, unsigned* const*, int, int,
                             int, int, size_t, unsigned, unsigned*, int, void*);
 size_t ntm_xgmi_signal_bytes(int);
@@ -130,8 +134,8 @@ void usage() {
                "       [--termination-log FILE] [--prom-out FILE] [--fault-inject KIND]\n"
                "       [--pushgateway http://host:port]\n"
                "fault-inject (also env NTM_FAULT_INJECT): corrupt_gemm | corrupt_abft |\n"
-               "       corrupt_fp8 | corrupt_p2p | corrupt_allreduce - corrupts the LAST GPU's data\n"
-               "       to prove detection\n");
+               "       corrupt_fp8 | corrupt_fp8_abft | corrupt_p2p | corrupt_allreduce - corrupts\n"
+               "       the LAST GPU's data to prove detection\n");
 }
 
 bool parse(int argc, char** argv, Opts& o) {
@@ -256,6 +260,7 @@ struct GpuResult {
   double fp8_ms = 0, fp8_tflops = 0;
   unsigned long long fp8_bad = ~0ull;  // stays ~0 when --no-fp8
   float fp8_max_err = NAN;
+  unsigned long long fp8_abft_bad = ~0ull;  // rows failing the fp8 fused checksum (~0: not run)
   double hbm_copy_gbps = 0, hbm_read_gbps = 0;
   bool hbm_copy_ok = false;
   double t_init = 0, t_gemm = 0, t_hbm = 0;
@@ -415,6 +420,35 @@ bool run_gpu(int dev, bool last, const Opts& o, GpuResult& r) {
     CK(hipEventElapsedTime(&ms, e0, e1));
     r.fp8_ms = ms / o.iters;
     r.fp8_tflops = 2.0 * n * (double)n * n / (r.fp8_ms * 1e-3) / 1e12;
+    if (n % 256 == 0) {
+      // the fp8 build with the fused ABFT row checksum, checked in O(n^2)
+      float* rowsum;
+      double* scratch;
+      void* ab;
+      CK(hipMalloc(&rowsum, sizeof(float) * n));
+      CK(hipMalloc(&scratch, sizeof(double) * n));
+      CK(hipMalloc(&ab, 64));
+      CK(hipMemsetAsync(rowsum, 0, sizeof(float) * n, s));
+      CK(ntm_gemm_fp8_rowsum(A8, B8, C, rowsum, n, n, n, n, n, n, s));
+      if (last && o.fault == "corrupt_fp8_abft") {
+        uint16_t h;
+        CK(hipMemcpyAsync(&h, (uint16_t*)C + 4242, 2, hipMemcpyDeviceToHost, s));
+        CK(hipStreamSynchronize(s));
+        h ^= 0x4000;  // exponent bit: a large stored-output error
+        CK(hipMemcpyAsync((uint16_t*)C + 4242, &h, 2, hipMemcpyHostToDevice, s));
+      }
+      CK(ntm_abft_check_fp8(A8, B8, C, rowsum, n, n, n, n, n, n, scratch, ab, s));
+      unsigned char abr[64];
+      CK(hipMemcpyAsync(abr, ab, ntm_abft_result_bytes(), hipMemcpyDeviceToHost, s));
+      CK(hipStreamSynchronize(s));
+      unsigned long long bad_acc, bad_store;
+      std::memcpy(&bad_acc, abr, 8);
+      std::memcpy(&bad_store, abr + 8, 8);
+      r.fp8_abft_bad = bad_acc + bad_store;
+      CK(hipFree(rowsum));
+      CK(hipFree(scratch));
+      CK(hipFree(ab));
+    }
     CK(hipFree(A8));
     CK(hipFree(B8));
   }
@@ -962,6 +996,8 @@ int main(int argc, char** argv) {
       fail(d + "fp8 GEMM verification failed (" +
            (r.fp8_bad == ~0ull ? std::string("not run: --size must be a multiple of 256")
                                : std::to_string(r.fp8_bad) + " elements") + ")");
+    if (o.fp8 && r.fp8_abft_bad != 0 && r.fp8_abft_bad != ~0ull)
+      fail(d + "fp8 GEMM ABFT checksum failed (" + std::to_string(r.fp8_abft_bad) + " rows)");
     if (o.fp8 && o.fp8_tflops_floor > 0 && r.fp8_tflops < o.fp8_tflops_floor)
       fail(d + "fp8 GEMM " + jnum(r.fp8_tflops) + " TFLOP/s below floor " + jnum(o.fp8_tflops_floor));
     if (o.min_hbm_gb > 0 && r.total_gb < o.min_hbm_gb)
@@ -1051,6 +1087,8 @@ int main(int argc, char** argv) {
           ",\"gemm_fp8_tflops\":" + jnum(r.fp8_tflops) +
           ",\"gemm_fp8_wrong\":" + (r.fp8_bad == ~0ull ? std::string("null") : std::to_string(r.fp8_bad)) +
           ",\"gemm_fp8_max_abs_err\":" + jnum(r.fp8_max_err) +
+          ",\"gemm_fp8_abft_bad_rows\":" +
+          (r.fp8_abft_bad == ~0ull ? std::string("null") : std::to_string(r.fp8_abft_bad)) +
           ",\"hbm_copy_GBps\":" + jnum(r.hbm_copy_gbps) +
           ",\"hbm_read_GBps\":" + jnum(r.hbm_read_gbps) + "}";
   }
