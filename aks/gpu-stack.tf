@@ -13,6 +13,10 @@ module "amd_gpu_stack" {
   gpu_operator_driver_version = var.gpu_operator_driver_version
   gpu_operator_namespace      = var.gpu_operator_namespace
 
+  driver_enabled              = !var.gpu_driver_preinstalled
+  node_prep_iommu_mode        = var.gpu_node_iommu_passthrough
+  validation_require_iommu_pt = var.gpu_node_iommu_passthrough == "reboot"
+
   gpu_node_selector = { "amd.com/gpu.present" = "true" }
   gpu_node_pool_ids = [azurerm_kubernetes_cluster_node_pool.mi355x.id]
 

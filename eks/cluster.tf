@@ -28,17 +28,29 @@ locals {
   #    argument only takes effect on a boot: "reboot" adds it and reboots once
   #    before the node joins (cloud-init runs user data once per instance, so a
   #    one-shot unit re-runs it after the reboot; the second pass sees iommu=pt
-  #    in /proc/cmdline and proceeds to bootstrap); "image" expects it baked
-  #    into gpu_ami_id and only records what the kernel booted with; "off"
-  #    leaves it alone.
+  #    in /proc/cmdline and proceeds to bootstrap). The reboot happens at most
+  #    ONCE per instance: a sentinel is written before it, and a pass that
+  #    finds the sentinel but still no iommu=pt (no GRUB_CMDLINE_LINUX line, a
+  #    grub.d snippet overriding it, another boot loader) logs a warning and
+  #    bootstraps without it instead of rebooting forever; the grub edit is
+  #    non-fatal under the script's `set -e`. "image" expects it baked into
+  #    gpu_ami_id and only records what the kernel booted with; "off" leaves
+  #    it alone. The validation Job re-checks the result from inside the pod
+  #    (amdgpu-validate --require-host-prep).
   # (Inlined into the node group's bootstrap script, which already runs
   # under `set -e`: no shebang, no shell options of its own.)
   mi355x_host_prep = <<-EOT
     mode="${var.gpu_node_iommu_passthrough}"
+    sentinel=/var/lib/mi355x-iommu-rebooted
+    if [ "$mode" = "reboot" ] && ! grep -qw 'iommu=pt' /proc/cmdline && [ -f "$sentinel" ]; then
+      echo "mi355x: WARNING iommu=pt still absent after one reboot; bootstrapping without it" >&2
+      mode="reboot-failed"
+    fi
     if [ "$mode" = "reboot" ] && ! grep -qw 'iommu=pt' /proc/cmdline; then
-      grep -q 'iommu=pt' /etc/default/grub ||
-        sed -i 's/^GRUB_CMDLINE_LINUX="/&iommu=pt /' /etc/default/grub
-      update-grub
+      { grep -q 'iommu=pt' /etc/default/grub ||
+          sed -i 's/^GRUB_CMDLINE_LINUX="/&iommu=pt /' /etc/default/grub; } || true
+      update-grub || echo "mi355x: WARNING update-grub failed" >&2
+      mkdir -p /var/lib && touch "$sentinel"
       cat > /etc/systemd/system/mi355x-userdata-rerun.service <<'UNIT'
     [Unit]
     Description=Re-run EC2 user data once after the iommu=pt reboot
@@ -235,6 +247,38 @@ module "ebs_csi_irsa_role" {
     this = {
       provider_arn               = module.eks.oidc_provider_arn
       namespace_service_accounts = ["kube-system:ebs-csi-controller-sa"]
+    }
+  }
+}
+
+# State moves for deployments created before the node groups and the EBS CSI
+# add-on left module "eks" (round 2): without them an upgrade would replace
+# both node groups (draining the MI355X nodes) and fail creating an add-on
+# that already exists.
+moved {
+  from = module.eks.module.eks_managed_node_group["gpu_node_pool"]
+  to   = module.gpu_node_pool
+}
+
+moved {
+  from = module.eks.module.eks_managed_node_group["cpu_node_pool"]
+  to   = module.cpu_node_pool
+}
+
+moved {
+  from = module.eks.aws_eks_addon.this["aws-ebs-csi-driver"]
+  to   = aws_eks_addon.ebs_csi
+}
+
+# A preinstalled driver can only come from a pinned image: the default lookup
+# (newest Canonical EKS Ubuntu) has no amdgpu, and the stack would then wait
+# out validation_timeout for GPUs that never appear.
+resource "terraform_data" "driver_preinstalled_guard" {
+  input = var.gpu_driver_preinstalled
+  lifecycle {
+    precondition {
+      condition     = !var.gpu_driver_preinstalled || var.gpu_ami_id != ""
+      error_message = "gpu_driver_preinstalled = true needs gpu_ami_id: an AMI with the amdgpu driver for gfx950 baked in (README \"Preinstalled driver\")."
     }
   }
 }

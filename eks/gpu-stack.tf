@@ -15,6 +15,12 @@ module "amd_gpu_stack" {
   gpu_operator_driver_version = var.gpu_operator_driver_version
   gpu_operator_namespace      = var.gpu_operator_namespace
 
+  driver_enabled = !var.gpu_driver_preinstalled
+  # the pre-bootstrap user data applies the host prep (incl. the iommu=pt
+  # reboot); the DaemonSet re-applies it idempotently and the Job checks it
+  node_prep_iommu_mode        = "check"
+  validation_require_iommu_pt = var.gpu_node_iommu_passthrough != "off"
+
   gpu_node_selector = { "amd.com/gpu.present" = "true" }
   gpu_node_pool_ids = [module.gpu_node_pool.node_group_id]
 

@@ -304,3 +304,9 @@ variable "gpu_validation_tflops_floor" {
   type        = number
   default     = 1000
 }
+
+variable "gpu_driver_preinstalled" {
+  description = "The MI355X node image (gpu_ami_id) already ships the amdgpu driver for gfx950: skip the driver install (operator: no KMM build/load; daemonsets: no DKMS DaemonSet) and run only the device plugin + labeller - the biggest in-cluster phase of time-to-GPU-ready (reference parity: driver.enabled=false, /root/reference/aks/main.tf:89-91). Requires gpu_ami_id; how to bake the driver: README \"Preinstalled driver\"."
+  type        = bool
+  default     = false
+}

@@ -15,6 +15,10 @@ module "amd_gpu_stack" {
   gpu_operator_namespace      = var.gpu_operator_namespace
   critical_pod_quota          = true
 
+  driver_enabled              = !var.gpu_driver_preinstalled
+  node_prep_iommu_mode        = var.gpu_node_iommu_passthrough
+  validation_require_iommu_pt = var.gpu_node_iommu_passthrough == "reboot"
+
   gpu_node_selector = { "amd.com/gpu.present" = "true" }
   gpu_node_pool_ids = [google_container_node_pool.mi355x.id]
 

@@ -219,3 +219,19 @@ variable "gpu_validation_tflops_floor" {
   type        = number
   default     = 1000
 }
+
+variable "gpu_driver_preinstalled" {
+  description = "The MI355X node image already ships the amdgpu driver for gfx950: skip the driver install (operator: no KMM build/load; daemonsets: no DKMS DaemonSet) and run only the device plugin + labeller (reference parity: driver.enabled=false, /root/reference/aks/main.tf:89-91). Only for a node image that really has it - the managed images of this cloud do not today (README \"Preinstalled driver\"); the validation Job fails if no GPU comes up."
+  type        = bool
+  default     = false
+}
+
+variable "gpu_node_iommu_passthrough" {
+  description = "iommu=pt on the MI355X nodes (xGMI / PCIe peer DMA), applied by the module's node-prep DaemonSet: \"check\" (record whether the node image booted with it), \"reboot\" (add it to GRUB and reboot each node once) or \"off\". The managed node images take no kernel arguments, so \"reboot\" is the only in-cluster lever."
+  type        = string
+  default     = "check"
+  validation {
+    condition     = contains(["check", "reboot", "off"], var.gpu_node_iommu_passthrough)
+    error_message = "gpu_node_iommu_passthrough must be check, reboot or off."
+  }
+}

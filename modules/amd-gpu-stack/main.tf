@@ -13,6 +13,16 @@ locals {
   gpu_resource   = "amd.com/gpu"
   node_pool_hash = sha1(join(",", var.gpu_node_pool_ids))
 
+  # CRDs the destroy-time janitor may delete: the KMM CRDs only when this
+  # release installs KMM (driver_enabled), the NFD ones only when it installs
+  # NFD. Otherwise they belong to a separate cluster-wide install, and deleting
+  # a CRD cascades to every CR of that kind in the cluster.
+  crd_cleanup_list = [
+    for crd in var.gpu_operator_crds : crd
+    if (var.driver_enabled || !endswith(crd, ".kmm.sigs.x-k8s.io")) &&
+    (var.install_node_feature_discovery || !endswith(crd, ".nfd.k8s-sigs.io"))
+  ]
+
   gpu_tolerations = [
     { key = var.gpu_node_taint_key, operator = "Exists", effect = "NoSchedule" },
   ]
@@ -136,7 +146,7 @@ resource "helm_release" "crd_janitor" {
   values = [yamlencode({
     name   = "amd-gpu-crd-janitor"
     image  = var.kubectl_image
-    crds   = var.gpu_operator_crds
+    crds   = local.crd_cleanup_list
     labels = local.common_labels
   })]
 

@@ -22,6 +22,14 @@ locals {
     "--fp8-tflops-floor", tostring(var.validation_fp8_tflops_floor),
   ] : ["--no-fp8"], var.validation_p2p_floor_gbps > 0 ? [
     "--p2p-floor-gbps", tostring(var.validation_p2p_floor_gbps),
+  ] : [], var.validation_gpu_count > 1 && var.validation_rccl_busbw_floor_gbps > 0 ? [
+    "--rccl-busbw-floor-gbps", tostring(var.validation_rccl_busbw_floor_gbps),
+  ] : [], var.validation_gpu_count > 1 && var.validation_xgmi_busbw_floor_gbps > 0 ? [
+    "--xgmi-busbw-floor-gbps", tostring(var.validation_xgmi_busbw_floor_gbps),
+  ] : [], var.node_prep_enabled && var.validation_require_host_prep ? [
+    "--require-host-prep",
+  ] : [], var.validation_require_iommu_pt ? [
+    "--require-iommu-pt",
   ] : [], [
     # one-line verdict surfaced as the pod's termination message
     "--termination-log", "/dev/termination-log",
@@ -141,6 +149,7 @@ resource "kubernetes_job_v1" "gpu_validation" {
     helm_release.device_config,
     kubernetes_daemon_set_v1.rocm_device_plugin,
     kubernetes_daemon_set_v1.amdgpu_dkms,
+    kubernetes_daemon_set_v1.node_prep,
   ]
 }
 

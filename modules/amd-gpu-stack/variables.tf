@@ -67,7 +67,7 @@ variable "gpu_operator_chart_name" {
 variable "gpu_operator_crd_cleanup" {
   type        = bool
   default     = true
-  description = "Delete the operator's CRDs (gpu_operator_crds) on destroy, after the operator release is gone (pre-delete hook of a module-local chart). Parity with the reference's operator.cleanupCRD=true (aks/main.tf:89-91)."
+  description = "Delete the operator's CRDs on destroy, after the operator release is gone (pre-delete hook of a module-local chart running kubectl_image). Only the CRDs this release installs are deleted: the KMM ones only with driver_enabled, the NFD ones only with install_node_feature_discovery. Parity with the reference's operator.cleanupCRD=true (aks/main.tf:89-91). Escape hatch: false skips the hook (e.g. when kubectl_image cannot be pulled, which would block destroy)."
 }
 
 variable "gpu_operator_crds" {
@@ -86,8 +86,8 @@ variable "gpu_operator_crds" {
 
 variable "kubectl_image" {
   type        = string
-  default     = "docker.io/bitnami/kubectl:1.31"
-  description = "Image with kubectl for the destroy-time CRD cleanup Job."
+  default     = "registry.k8s.io/kubectl:v1.31.4"
+  description = "Image with kubectl for the destroy-time CRD cleanup Job (the Kubernetes project's own registry; Bitnami stopped publishing versioned tags on docker.io). It is pulled only at destroy time: if the GPU nodes' cluster cannot pull it (air-gapped, registry allow-list), mirror it and set this, or set gpu_operator_crd_cleanup = false - a hook whose image cannot be pulled fails after its 300 s deadline and blocks `terraform destroy` of the operator."
 }
 
 variable "create_namespace" {
@@ -324,4 +324,67 @@ variable "validation_env" {
   type        = map(string)
   default     = {}
   description = "Extra environment for the validation container (e.g. NCCL_DEBUG=INFO)."
+}
+
+/************************
+  MI355X host preparation (node-prep.tf)
+*************************/
+variable "node_prep_enabled" {
+  type        = bool
+  default     = true
+  description = "Run the privileged mi355x-node-prep DaemonSet on the GPU nodes: automatic NUMA balancing off, containerd LimitMEMLOCK=infinity, iommu=pt per node_prep_iommu_mode. Idempotent (EKS user data applies the same settings before the join; here it then only verifies)."
+}
+
+variable "node_prep_iommu_mode" {
+  type        = string
+  default     = "check"
+  description = "iommu=pt handling on the GPU nodes: \"check\" records whether the kernel booted with it, \"reboot\" adds it to GRUB and reboots each node at most once, \"off\" skips it. A kernel argument needs a boot: prefer a node image that has it (EKS gpu_ami_id)."
+
+  validation {
+    condition     = contains(["off", "check", "reboot"], var.node_prep_iommu_mode)
+    error_message = "node_prep_iommu_mode must be \"off\", \"check\" or \"reboot\"."
+  }
+}
+
+variable "node_prep_image" {
+  type        = string
+  default     = "docker.io/library/ubuntu:22.04"
+  description = "Image of the node-prep init container; it only needs nsenter (util-linux): the script runs in the host's namespaces."
+}
+
+variable "validation_require_host_prep" {
+  type        = bool
+  default     = true
+  description = "The validation Job fails (amdgpu-validate --require-host-prep) unless its pod sees kernel.numa_balancing = 0 and an unlimited RLIMIT_MEMLOCK. Only passed while node_prep_enabled."
+}
+
+variable "validation_require_iommu_pt" {
+  type        = bool
+  default     = false
+  description = "The validation Job also fails unless the node kernel booted with iommu=pt (amdgpu-validate --require-iommu-pt)."
+}
+
+/************************
+  Interconnect gates of the validation Job
+*************************/
+variable "validation_rccl_busbw_floor_gbps" {
+  type        = number
+  default     = 0
+  description = "Peak bf16 RCCL all-reduce busbw (GB/s) below which the Job fails; applied when validation_gpu_count > 1. 0 = report only. Set it from the first 8-GPU measurement of the node type (no such number exists yet: BASELINE has none, and the single-GPU development boxes cannot produce one)."
+
+  validation {
+    condition     = var.validation_rccl_busbw_floor_gbps >= 0
+    error_message = "validation_rccl_busbw_floor_gbps must be >= 0."
+  }
+}
+
+variable "validation_xgmi_busbw_floor_gbps" {
+  type        = number
+  default     = 0
+  description = "The same floor for the hand-written xGMI all-reduce (C2); applied when validation_gpu_count > 1. 0 = report only."
+
+  validation {
+    condition     = var.validation_xgmi_busbw_floor_gbps >= 0
+    error_message = "validation_xgmi_busbw_floor_gbps must be >= 0."
+  }
 }

@@ -174,11 +174,13 @@ def cmd_critical_path(a) -> int:
     durations = None
     if a.apply_log:
         durations = durations_from_timeline(parse_apply_json(Path(a.apply_log).read_text().splitlines()))
-    cp = critical_path(g, durations, stack_mode=a.stack_mode)
+    cp = critical_path(g, durations, stack_mode=a.stack_mode,
+                       driver_preinstalled=a.driver_preinstalled)
     if a.json:
         print(json.dumps(cp.as_dict(), indent=1))
         return 0
-    print(f"critical path of {a.root} ({a.stack_mode}): {cp.total_s:.0f} s")
+    drv = ", driver preinstalled" if a.driver_preinstalled else ""
+    print(f"critical path of {a.root} ({a.stack_mode}{drv}): {cp.total_s:.0f} s")
     for addr, s in cp.path:
         print(f"  {s:7.0f} s  {addr}")
     print("by phase: " + ", ".join(f"{k} {v:.0f}s" for k, v in cp.phases.items()))
@@ -204,6 +206,8 @@ def main(argv=None) -> int:
     c.add_argument("root")
     c.add_argument("--stack-mode", default="operator", choices=["operator", "daemonsets"])
     c.add_argument("--apply-log", help="measured durations from an apply -json log")
+    c.add_argument("--driver-preinstalled", action="store_true",
+                   help="the root's gpu_driver_preinstalled = true (no driver install phase)")
     c.add_argument("--json", action="store_true")
     a = ap.parse_args(argv)
     if a.cmd == "record":

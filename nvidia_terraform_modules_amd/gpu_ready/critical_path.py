@@ -74,6 +74,10 @@ PREPULL_MARK = "kubernetes_daemon_set_v1.validation_prepull"
 # completed: driver install (DKMS build or operator KMM), device plugin
 # registration. Attributed to the node that waits on it.
 DRIVER_READY_S = {"operator": 240.0, "daemonsets": 300.0}
+# gpu_driver_preinstalled (node image ships amdgpu; module driver_enabled =
+# false): no KMM build / DKMS compile, only the device plugin registering
+# amd.com/gpu with the kubelet and the labeller - the SURVEY §7.4 lever
+PLUGIN_READY_S = 30.0
 
 PHASE_OF_KIND = [
     ("network", ("module.vpc", "google_compute_network", "google_compute_subnetwork",
@@ -127,7 +131,10 @@ class CriticalPath:
         return {"total_s": self.total_s, "path": self.path, "phases": self.phases}
 
 
-def critical_path(g: Graph, durations: dict | None = None, stack_mode: str = "operator") -> CriticalPath:
+def critical_path(g: Graph, durations: dict | None = None, stack_mode: str = "operator",
+                  driver_preinstalled: bool = False) -> CriticalPath:
+    """``driver_preinstalled``: the root's gpu_driver_preinstalled = true (the
+    driver-install phase drops to device-plugin registration)."""
     dur = dict(DEFAULT_DURATIONS)
     dur.update(durations or {})
 
@@ -140,7 +147,8 @@ def critical_path(g: Graph, durations: dict | None = None, stack_mode: str = "op
         named = f"{t}.{addr.split(t + '.', 1)[1].split('[')[0]}" if (t + ".") in addr else t
         base = dur.get(named, dur.get(t, 0.0))
         if t == "kubernetes_job_v1":
-            driver = DRIVER_READY_S.get(stack_mode, 0.0)  # GPUs allocatable only after the driver
+            # GPUs allocatable only after the driver (or just the plugin, preinstalled)
+            driver = PLUGIN_READY_S if driver_preinstalled else DRIVER_READY_S.get(stack_mode, 0.0)
             pull = dur.get("image_pull", IMAGE_PULL_S)
             if prepull:  # pulled while the driver installed: only the excess remains
                 base -= min(pull, driver)

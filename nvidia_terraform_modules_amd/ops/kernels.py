@@ -36,7 +36,7 @@ GEMM_VARIANTS = {"default": 0, "pingpong8": 1, "wave128": 2, "wave128d4": 3, "pi
                  "pingpong8cwn": 12, "pingpong8cwne": 13, "pingpong8pw": 14, "tile128": 15,
                  "tile256x128": 16, "tile160": 17, "tile256x160": 18, "tile128w4": 19,
                  "tile256x128w4": 20, "tile160w4": 21, "pingpong8cm": 22, "tile160x128": 23,
-                 "tile128x160": 24}
+                 "tile128x160": 24, "regstage4": 25, "regstage4b": 26, "regstage4c": 27}
 
 
 # variants built only into libntm_experimental.so (tests / tools): never selected
@@ -44,7 +44,8 @@ GEMM_VARIANTS = {"default": 0, "pingpong8": 1, "wave128": 2, "wave128d4": 3, "pi
 EXPERIMENTAL_VARIANTS = frozenset({"pingpong8", "wave128", "wave128d4", "pingpong8p",
                                    "pingpong8w", "pingpong8wi", "pingpong8ww", "pingpong8cw",
                                    "pingpong8cwe", "pingpong8cwn", "pingpong8cwne",
-                                   "pingpong8pw", "tile128w4", "tile256x128w4", "tile160w4"})
+                                   "pingpong8pw", "tile128w4", "tile256x128w4", "tile160w4",
+                                   "regstage4", "regstage4b", "regstage4c"})
 
 # (TM, TN) of the 4-wave tile kernels (gemm_bf16_t128.hpp)
 TILE_SHAPES = {"tile128": (128, 128), "tile256x128": (256, 128), "tile160": (160, 160),

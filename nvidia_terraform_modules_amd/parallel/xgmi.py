@@ -113,6 +113,15 @@ class XgmiAllReduce:
     ``ar(t)`` on any other tensor stages it in and out with two stream-ordered
     copies (still no host sync). Messages up to ``one_shot_max_bytes`` take the
     one-shot kernel (one read pass over all peers, 2 barriers instead of 3).
+
+    Failure contract: the device-side barriers are bounded. The entry barrier
+    waits up to ~16x longer than the in-kernel phases (it absorbs host skew
+    between ranks: a checkpoint, a GC pause); a block that still times out
+    fills the part of the output it owns with bf16 NaN and records the phase in
+    a sticky device error word, so a late rank yields NaNs, never a silently
+    partial sum. ``run(..., check=True)`` / ``ar(t, check=True)`` synchronise
+    and raise on a timeout; otherwise poll :meth:`timed_out` (or call
+    :meth:`raise_if_timed_out`) at a convenient sync point.
     """
 
     def __init__(self, env, max_bytes: int, nblk: int = 64, one_shot_max_bytes: int = 256 << 10):
@@ -193,20 +202,24 @@ class XgmiAllReduce:
             1 if one_shot else 0, stream_handle())
         check(rc, "ntm_xgmi_allreduce_bf16")
 
-    def run(self, numel: int) -> torch.Tensor:
-        """Sum over ranks of ``buffer(numel)``, in place, stream-ordered."""
+    def run(self, numel: int, check: bool = False) -> torch.Tensor:
+        """Sum over ranks of ``buffer(numel)``, in place, stream-ordered.
+        ``check``: synchronise and raise if a device barrier timed out."""
         self._check_count(numel)
         if numel * 2 <= self.one_shot_max_bytes:
             self._launch(numel, one_shot=True)
             _copy_d2d(self.ptrs["in"][self.env.rank], self.ptrs["out"][self.env.rank], numel * 2)
         else:
             self._launch(numel, one_shot=False)
+        if check:
+            self.raise_if_timed_out()
         return self.buffer(numel)
 
-    def __call__(self, t: torch.Tensor) -> torch.Tensor:
+    def __call__(self, t: torch.Tensor, check: bool = False) -> torch.Tensor:
         """In-place sum over ranks of bf16 tensor ``t``. Zero-copy when ``t``
         is :meth:`buffer`; otherwise staged in and out with stream-ordered
-        copies. Never synchronises the host."""
+        copies. Never synchronises the host unless ``check`` (then raises on a
+        device barrier timeout)."""
         nbytes = t.numel() * t.element_size()
         if t.dtype != torch.bfloat16 or not t.is_contiguous():
             raise ValueError("contiguous bf16 tensor expected")
@@ -214,16 +227,30 @@ class XgmiAllReduce:
         self._check_count(count)
         mine = self.ptrs["in"][self.env.rank]
         if t.data_ptr() == mine:
-            self.run(count)
+            self.run(count, check=check)
             return t
         _copy_d2d(mine, t.data_ptr(), nbytes)
         one = nbytes <= self.one_shot_max_bytes
         self._launch(count, one_shot=one)
         _copy_d2d(t.data_ptr(), self.ptrs["out" if one else "in"][self.env.rank], nbytes)
+        if check:
+            self.raise_if_timed_out()
         return t
 
+    PHASES = {1: "entry", 2: "reduce-scatter", 3: "exit"}
+
     def timed_out(self) -> bool:
+        """True once any call's device barrier timed out (sticky; syncs)."""
         return bool(self.err.item())
+
+    def raise_if_timed_out(self) -> None:
+        """Synchronise; raise RuntimeError if a device barrier timed out (the
+        affected outputs hold NaN, see the class docstring)."""
+        code = int(self.err.item())
+        if code:
+            raise RuntimeError(f"XgmiAllReduce rank {self.env.rank}: device barrier timed out "
+                               f"in the {self.PHASES.get(code, str(code))} phase "
+                               "(a peer never arrived); outputs of the failed call are NaN")
 
     def close(self) -> None:
         torch.cuda.synchronize()

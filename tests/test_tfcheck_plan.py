@@ -179,3 +179,19 @@ def test_validation_job_args_carry_the_fp8_check():
     assert "--p2p-floor-gbps" not in args
     p2p = _stack_local("validation_args", validation_p2p_floor_gbps=40)
     assert p2p[p2p.index("--p2p-floor-gbps") + 1] == "40"
+
+
+def test_crd_janitor_deletes_only_crds_this_release_installs():
+    """the destroy-time janitor must not delete KMM / NFD CRDs that
+    belong to a separate cluster-wide install (a CRD delete cascades to every CR
+    of that kind in the cluster)."""
+    full = _stack_local("crd_cleanup_list")
+    assert "deviceconfigs.amd.com" in full
+    assert any(c.endswith(".kmm.sigs.x-k8s.io") for c in full)
+    assert any(c.endswith(".nfd.k8s-sigs.io") for c in full)
+    no_kmm = _stack_local("crd_cleanup_list", driver_enabled=False)
+    assert not any(c.endswith(".kmm.sigs.x-k8s.io") for c in no_kmm)
+    assert any(c.endswith(".nfd.k8s-sigs.io") for c in no_kmm)
+    no_nfd = _stack_local("crd_cleanup_list", install_node_feature_discovery=False)
+    assert not any(c.endswith(".nfd.k8s-sigs.io") for c in no_nfd)
+    assert no_nfd[0] == "deviceconfigs.amd.com"

@@ -168,6 +168,67 @@ def test_binary_xgmi_simulated_fault_fails():
 
 
 @pytest.mark.gpu
+def test_binary_busbw_floors_fire():
+    """the readiness gate gates the interconnect. An impossible
+    floor fails the Job on both collectives (N = 1: RCCL busbw is 0 on a
+    one-rank communicator; C2 on 4 simulated ranks); no floor, no failure."""
+    _have_bin()
+    rc, out, _ = _run("--size", "512", "--iters", "2", "--no-fp8", "--rccl", "--no-xgmi",
+                      "--allreduce-max-mib", "1", "--rccl-busbw-floor-gbps", "1")
+    g = _last_json(out)
+    assert rc == 1 and any("RCCL all-reduce peak bf16 busbw" in f for f in g["failures"]), g
+    assert g["rccl_peak_busbw_bf16_GBps"] == 0
+    rc, out, _ = _run("--size", "512", "--iters", "2", "--no-fp8", "--no-rccl", "--xgmi-sim", "4",
+                      "--allreduce-max-mib", "4", "--xgmi-busbw-floor-gbps", "1e9")
+    g = _last_json(out)
+    assert rc == 1 and any("xGMI all-reduce peak bf16 busbw" in f for f in g["failures"]), g
+    assert g["xgmi_peak_busbw_bf16_GBps"] > 0
+    rc, out, _ = _run("--size", "512", "--iters", "2", "--no-fp8", "--no-rccl", "--xgmi-sim", "4",
+                      "--allreduce-max-mib", "4", "--xgmi-busbw-floor-gbps", "0.001")
+    assert rc == 0, _last_json(out)["failures"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nblk,one_shot_max", [(16, 0), (32, 1 << 20), (128, 64 << 10)])
+def test_binary_xgmi_knobs(nblk, one_shot_max):
+    """--xgmi-nblk / --xgmi-one-shot-max (what bench.py sweeps at N > 1): every
+    combination stays exact; 0 sends every size to the two-shot kernel."""
+    _have_bin()
+    rc, out, err = _run("--size", "512", "--iters", "2", "--no-fp8", "--no-rccl", "--xgmi-sim", "4",
+                        "--allreduce-max-mib", "16", "--xgmi-nblk", str(nblk),
+                        "--xgmi-one-shot-max", str(one_shot_max))
+    g = _last_json(out)
+    assert rc == 0, (g["failures"], err[-2000:])
+    assert g["xgmi_nblk"] == nblk and g["xgmi_one_shot_max_bytes"] == one_shot_max
+    rows = g["xgmi_allreduce_bf16"]
+    assert all(r["wrong"] == 0 for r in rows)
+    one = [r["bytes"] for r in rows if r["dtype"] == "bf16-1shot"]
+    assert all(b <= one_shot_max for b in one) and (one_shot_max > 0) == bool(one)
+
+
+@pytest.mark.gpu
+def test_binary_reports_and_enforces_host_prep():
+    """The in-pod host-prep check (--require-host-prep): the report always
+    carries what the pod sees; the flag fails the Job exactly when a setting is
+    missing (the GPU boxes are not prepared nodes, so either outcome is legal -
+    the test pins that the verdict follows the observation)."""
+    _have_bin()
+    rc, out, _ = _run("--size", "512", "--iters", "2", "--no-fp8")
+    hp = _last_json(out)["host_prep"]
+    assert set(hp) == {"numa_balancing", "memlock_unlimited", "iommu_pt"} and rc == 0
+    prepared = hp["numa_balancing"] == 0 and hp["memlock_unlimited"]
+    rc, out, _ = _run("--size", "512", "--iters", "2", "--no-fp8", "--require-host-prep")
+    fails = [f for f in _last_json(out)["failures"] if f.startswith("host prep")]
+    assert (rc == 0 and not fails) if prepared else (rc == 1 and fails)
+
+
+def test_xgmi_knob_arguments_are_checked():
+    _have_bin()
+    rc, _, err = _run("--xgmi-nblk", "0", timeout=60)
+    assert rc == 2 and "--xgmi-nblk" in err
+
+
+@pytest.mark.gpu
 def test_binary_no_fp8_skips_the_fp8_check():
     _have_bin()
     rc, out, _ = _run("--size", "1024", "--iters", "3", "--no-fp8")

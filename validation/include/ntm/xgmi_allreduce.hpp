@@ -48,7 +48,16 @@ namespace xgmi {
 constexpr int kMaxRanks = 8;
 constexpr int kThreads = 256;
 constexpr int kPhases = 3;                 // entry, reduce-scatter done, exit
-constexpr unsigned kSpinLimit = 1u << 24;  // ~ seconds; then report a timeout
+// Spin limits (s_sleep 2 + one uncached load per spin). The ENTRY barrier
+// absorbs host-side skew between ranks (a checkpoint, a GC pause, uneven work
+// before the call): it waits 16x longer (~minutes) than the in-kernel phases,
+// which only wait for peers already running the same kernel (~seconds).
+constexpr unsigned kSpinLimit = 1u << 24;
+constexpr unsigned kEntrySpinLimit = 1u << 28;
+// A block whose barrier times out never leaves a stale sum behind: it fills
+// the part of the output it owns with bf16 NaN (0x7FC0), so a caller that does
+// not read the error word still cannot consume partial sums silently.
+constexpr unsigned short kPoison = 0x7FC0;
 
 struct Peers {
   const __bf16* in[kMaxRanks];
@@ -75,7 +84,8 @@ __device__ __forceinline__ u16x8 pack8(const float (&acc)[8]) {
 __device__ __forceinline__ bool cross_rank_barrier(const Peers& p, int nranks,
                                                    int rank, int b, int nblk,
                                                    int ph, unsigned epoch,
-                                                   unsigned* err) {
+                                                   unsigned* err,
+                                                   unsigned limit = kSpinLimit) {
   __shared__ int s_ok;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave
   __syncthreads();
@@ -92,7 +102,7 @@ __device__ __forceinline__ bool cross_rank_barrier(const Peers& p, int nranks,
       unsigned spins = 0;
       while ((int)(__hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0) {
         __builtin_amdgcn_s_sleep(2);
-        if (++spins > kSpinLimit) {
+        if (++spins > limit) {
           ok = false;
           atomicMax(err, 1u + (unsigned)ph);
           break;
@@ -121,8 +131,21 @@ __global__ void __launch_bounds__(kThreads)
   const size_t v1 = v0 + per_blk < nvec ? v0 + per_blk : nvec;
   const size_t base = (size_t)rank * chunk / 8;  // vector index of chunk `rank`
 
+  // slice b of every chunk of my output: what this block writes (phase 1
+  // writes chunk `rank`, phase 2 the others) - poisoned on a timeout
+  auto poison = [&]() {
+    u16x8 nan8;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) nan8[i] = kPoison;
+    for (int q = 0; q < nranks; ++q)
+      for (size_t v = v0 + threadIdx.x; v < v1; v += kThreads)
+        ((u16x8*)p.out[rank])[(size_t)q * chunk / 8 + v] = nan8;
+  };
   // phase 0 (entry): every peer's input for this epoch is complete
-  if (!cross_rank_barrier(p, nranks, rank, b, nblk, 0, epoch, err)) return;
+  if (!cross_rank_barrier(p, nranks, rank, b, nblk, 0, epoch, err, kEntrySpinLimit)) {
+    poison();
+    return;
+  }
 
   // reduce-scatter - chunk `rank`, slice b, summed over all ranks. Start the
   // sum at a different peer per rank so the 7 links carry load at once.
@@ -135,7 +158,10 @@ __global__ void __launch_bounds__(kThreads)
     }
     ((u16x8*)p.out[rank])[base + v] = pack8(acc);
   }
-  if (!cross_rank_barrier(p, nranks, rank, b, nblk, 1, epoch, err)) return;
+  if (!cross_rank_barrier(p, nranks, rank, b, nblk, 1, epoch, err)) {
+    poison();
+    return;
+  }
 
   // all-gather - copy chunk q, slice b, from rank q's output
   for (int qq = 1; qq < nranks; ++qq) {
@@ -157,7 +183,14 @@ __global__ void __launch_bounds__(kThreads)
   const int rank = rank_base + (int)(blockIdx.x / nblk);
   const int b = (int)(blockIdx.x % nblk);
   const size_t nvec = count / 8;
-  if (!cross_rank_barrier(p, nranks, rank, b, nblk, 0, epoch, err)) return;
+  if (!cross_rank_barrier(p, nranks, rank, b, nblk, 0, epoch, err, kEntrySpinLimit)) {
+    u16x8 nan8;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) nan8[i] = kPoison;
+    for (size_t v = (size_t)b * kThreads + threadIdx.x; v < nvec; v += (size_t)nblk * kThreads)
+      ((u16x8*)p.out[rank])[v] = nan8;
+    return;
+  }
   for (size_t v = (size_t)b * kThreads + threadIdx.x; v < nvec;
        v += (size_t)nblk * kThreads) {
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};

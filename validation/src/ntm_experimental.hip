@@ -12,6 +12,9 @@
 //   7..9   pingpong8w / wi / ww: 32-MFMA segment schedules (gemm_bf16_pp5.hpp)
 //   10..13 pingpong8c epilogue knobs: widened / + early row-0 stores /
 //          nontemporal stores / both (gemm_bf16_pp3.hpp launch_gemm_bf16_pp3_knob)
+//   25..27 regstage4 / regstage4b / regstage4c: 4 waves, 128x128 per wave,
+//          register-staged operands, barrier after phase-1 MFMA 40 / 48 / 34
+//          (gemm_bf16_r4.hpp)
 //   19..21 tile128w4 / tile256x128w4 / tile160w4: the 4-wave (one wave per
 //          SIMD) tile kernels that the wave-specialised ones replaced as
 //          variants 15..17 (gemm_bf16_t128.hpp; profiles/r2_ws)
@@ -22,6 +25,7 @@
 #include "ntm/gemm_bf16_pp3_stamp.hpp"
 #include "ntm/gemm_bf16_pp4.hpp"
 #include "ntm/gemm_bf16_pp5.hpp"
+#include "ntm/gemm_bf16_r4.hpp"
 #include "ntm/gemm_bf16_t128.hpp"
 #include "ntm/gemm_bf16_w4.hpp"
 #include "ntm/gemm_fp8_diag.hpp"
@@ -73,6 +77,9 @@ NTM_API int ntm_gemm_bf16_experimental(int variant, const void* A, const void* B
     case 19: return (int)ntm::gemmt::launch_gemm_bf16_tile<4>(a, S(stream));
     case 20: return (int)ntm::gemmt::launch_gemm_bf16_tile<8>(a, S(stream));
     case 21: return (int)ntm::gemmt::launch_gemm_bf16_tile<5, 5>(a, S(stream));
+    case 25: return (int)ntm::gemmr::launch_gemm_bf16_r4<40>(a, S(stream));
+    case 26: return (int)ntm::gemmr::launch_gemm_bf16_r4<48>(a, S(stream));
+    case 27: return (int)ntm::gemmr::launch_gemm_bf16_r4<34>(a, S(stream));
     default: return (int)hipErrorInvalidValue;
   }
 }

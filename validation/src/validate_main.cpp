@@ -33,6 +33,7 @@
 #include <vector>
 
 #include <netdb.h>
+#include <sys/resource.h>
 #include <sys/socket.h>
 #include <unistd.h>
 
@@ -115,6 +116,12 @@ struct Opts {
   bool p2p_loopback = false;    // C3 code path on one GPU (pair 0 <- 0), for tests
   long p2p_mib = 256;
   double p2p_floor_gbps = 0;
+  double rccl_busbw_floor_gbps = 0;  // C1: peak bf16 busbw floor (0 = off; busbw is 0 at n = 1)
+  double xgmi_busbw_floor_gbps = 0;  // C2: the same for the hand-written all-reduce
+  int xgmi_nblk = 64;                // C2 blocks per rank (bench.py sweeps it at N > 1)
+  long xgmi_one_shot_max = 256 << 10;  // C2: messages <= this take the one-shot kernel
+  bool require_host_prep = false;    // fail unless numa_balancing = 0 and memlock unlimited
+  bool require_iommu_pt = false;     // ... and the kernel booted with iommu=pt
   bool json = true;
   std::string out;
   std::string termination_log;  // k8s terminationMessagePath (<= 4 KiB summary)
@@ -130,6 +137,9 @@ void usage() {
                "       [--allreduce-max-mib MiB] [--rccl | --no-rccl] [--no-xgmi] [--xgmi-sim N]\n"
                "       [--settle-s S] [--no-fp8] [--fp8-tflops-floor TF]\n"
                "       [--no-p2p] [--p2p-mib MiB] [--p2p-floor-gbps GBps] [--p2p-loopback]\n"
+               "       [--rccl-busbw-floor-gbps GBps] [--xgmi-busbw-floor-gbps GBps]\n"
+               "       [--xgmi-nblk N] [--xgmi-one-shot-max BYTES]\n"
+               "       [--require-host-prep] [--require-iommu-pt]\n"
                "       [--json] [--out FILE]\n"
                "       [--termination-log FILE] [--prom-out FILE] [--fault-inject KIND]\n"
                "       [--pushgateway http://host:port]\n"
@@ -166,6 +176,12 @@ bool parse(int argc, char** argv, Opts& o) {
     else if (a == "--p2p-loopback") o.p2p_loopback = true;
     else if (a == "--p2p-mib") { if (!(v = next(a.c_str()))) return false; o.p2p_mib = std::atol(v); }
     else if (a == "--p2p-floor-gbps") { if (!(v = next(a.c_str()))) return false; o.p2p_floor_gbps = std::atof(v); }
+    else if (a == "--rccl-busbw-floor-gbps") { if (!(v = next(a.c_str()))) return false; o.rccl_busbw_floor_gbps = std::atof(v); }
+    else if (a == "--xgmi-busbw-floor-gbps") { if (!(v = next(a.c_str()))) return false; o.xgmi_busbw_floor_gbps = std::atof(v); }
+    else if (a == "--xgmi-nblk") { if (!(v = next(a.c_str()))) return false; o.xgmi_nblk = std::atoi(v); }
+    else if (a == "--xgmi-one-shot-max") { if (!(v = next(a.c_str()))) return false; o.xgmi_one_shot_max = std::atol(v); }
+    else if (a == "--require-host-prep") o.require_host_prep = true;
+    else if (a == "--require-iommu-pt") o.require_iommu_pt = true;
     else if (a == "--fp8-tflops-floor") { if (!(v = next(a.c_str()))) return false; o.fp8_tflops_floor = std::atof(v); }
     else if (a == "--json") o.json = true;
     else if (a == "--out") { if (!(v = next("--out"))) return false; o.out = v; }
@@ -763,8 +779,11 @@ bool run_xgmi(const std::vector<int>& devs, const Opts& o, std::vector<CollRow>&
         hipError_t e = hipDeviceEnablePeerAccess(devs[j], 0);
         if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) CK(e);
       }
-  const int nblk = sim ? std::min(64, 1024 / n) : 64;
-  const size_t one_shot_max = (size_t)256 << 10;
+  // blocks per rank and the one-shot cutoff are knobs (--xgmi-nblk,
+  // --xgmi-one-shot-max): bench.py sweeps them at N > 1, so the first 8-GPU
+  // run says whether the design or the constant is at fault
+  const int nblk = sim ? std::min(o.xgmi_nblk, 1024 / n) : o.xgmi_nblk;
+  const size_t one_shot_max = (size_t)std::max(0L, o.xgmi_one_shot_max);
   std::vector<int> used(devs.begin(), devs.begin() + ndev);
   const size_t maxb = sweep_cap(used, std::min<size_t>((size_t)o.allreduce_max_mib << 20,
                                                        (size_t)1 << 30), sim ? 2 * n : 2);
@@ -955,6 +974,38 @@ std::string push_metrics(const std::string& url, const std::string& body) {
   return "error: " + status.substr(0, status.find('\r'));
 }
 
+// MI355X host preparation as the pod sees it (the node-prep DaemonSet of
+// modules/amd-gpu-stack, or the EKS pre-bootstrap user data, sets it up):
+// automatic NUMA balancing off (a host-wide sysctl, readable in any
+// container), RLIMIT_MEMLOCK unlimited for this process (inherited from
+// containerd's LimitMEMLOCK; RCCL pins host memory) and iommu=pt on the
+// kernel command line (xGMI / PCIe peer DMA).
+struct HostPrep {
+  int numa_balancing = -1;  // -1: unreadable
+  bool memlock_unlimited = false;
+  bool iommu_pt = false;
+};
+
+HostPrep read_host_prep() {
+  HostPrep h;
+  std::ifstream nb("/proc/sys/kernel/numa_balancing");
+  if (nb) nb >> h.numa_balancing;
+  rlimit rl{};
+  h.memlock_unlimited = getrlimit(RLIMIT_MEMLOCK, &rl) == 0 && rl.rlim_cur == RLIM_INFINITY;
+  std::ifstream cl("/proc/cmdline");
+  std::string w;
+  while (cl >> w) h.iommu_pt = h.iommu_pt || w == "iommu=pt";
+  return h;
+}
+
+// peak busbw of the bf16 rows (the floors gate the interconnect, not a size)
+double peak_busbw(const std::vector<CollRow>& rows) {
+  double m = 0;
+  for (auto& r : rows)
+    if (std::strncmp(r.dtype, "bf16", 4) == 0 && std::isfinite(r.busbw)) m = std::max(m, r.busbw);
+  return m;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -964,8 +1015,19 @@ int main(int argc, char** argv) {
     usage();
     return 2;
   }
+  if (o.xgmi_nblk < 1 || o.xgmi_nblk > 1024 || o.xgmi_one_shot_max < 0) {
+    std::fprintf(stderr, "--xgmi-nblk must be in 1..1024, --xgmi-one-shot-max >= 0\n");
+    return 2;
+  }
   if (o.fault.empty())
     if (const char* f = std::getenv("NTM_FAULT_INJECT")) o.fault = f;
+  const HostPrep hp = read_host_prep();
+  if (o.require_host_prep || o.require_iommu_pt) {
+    if (hp.numa_balancing != 0)
+      fail("host prep: kernel.numa_balancing = " + std::to_string(hp.numa_balancing) + " (want 0)");
+    if (!hp.memlock_unlimited) fail("host prep: RLIMIT_MEMLOCK is not unlimited (containerd LimitMEMLOCK)");
+  }
+  if (o.require_iommu_pt && !hp.iommu_pt) fail("host prep: iommu=pt missing from /proc/cmdline");
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
     std::printf("{\"passed\":false,\"failures\":[\"no AMD GPU visible\"]}\n");
@@ -1016,6 +1078,14 @@ int main(int argc, char** argv) {
   P2pResult p2p;
   if (o.p2p && (n > 1 || o.p2p_loopback)) run_p2p(devs, o, p2p);
   const double t_end = wall_now();
+  // interconnect gates (0 = off; set from the first 8-GPU measurement)
+  const double rccl_peak_bf16 = peak_busbw(rccl_rows), xgmi_peak_bf16 = peak_busbw(xgmi_rows);
+  if (o.rccl_busbw_floor_gbps > 0 && !rccl_rows.empty() && rccl_peak_bf16 < o.rccl_busbw_floor_gbps)
+    fail("RCCL all-reduce peak bf16 busbw " + jnum(rccl_peak_bf16) + " GB/s below floor " +
+         jnum(o.rccl_busbw_floor_gbps));
+  if (o.xgmi_busbw_floor_gbps > 0 && !xgmi_rows.empty() && xgmi_peak_bf16 < o.xgmi_busbw_floor_gbps)
+    fail("xGMI all-reduce peak bf16 busbw " + jnum(xgmi_peak_bf16) + " GB/s below floor " +
+         jnum(o.xgmi_busbw_floor_gbps));
 
   double agg = 0;
   for (auto& r : res) agg += r.gemm_tflops;
@@ -1095,6 +1165,13 @@ int main(int argc, char** argv) {
   js += "],\"rccl_allreduce\":" + coll_json(rccl_rows);
   js += ",\"xgmi_allreduce_bf16\":" + coll_json(xgmi_rows);
   js += ",\"xgmi_simulated_ranks\":" + std::to_string(o.xgmi_sim);
+  js += ",\"xgmi_nblk\":" + std::to_string(o.xgmi_nblk) +
+        ",\"xgmi_one_shot_max_bytes\":" + std::to_string(o.xgmi_one_shot_max);
+  js += ",\"rccl_peak_busbw_bf16_GBps\":" + jnum(rccl_peak_bf16) +
+        ",\"xgmi_peak_busbw_bf16_GBps\":" + jnum(xgmi_peak_bf16);
+  js += ",\"host_prep\":{\"numa_balancing\":" + std::to_string(hp.numa_balancing) +
+        ",\"memlock_unlimited\":" + (hp.memlock_unlimited ? "true" : "false") +
+        ",\"iommu_pt\":" + (hp.iommu_pt ? "true" : "false") + "}";
   js += ",\"xgmi_p2p_GBps\":" + p2p_json(p2p) + ",\"xgmi_p2p_min_GBps\":" +
         (p2p.n > 0 ? jnum(p2p.min_gbps) : std::string("null")) +
         ",\"xgmi_p2p_bad_pairs\":" + std::to_string(p2p.bad_pairs);
