@@ -266,10 +266,20 @@ def main(argv=None) -> int:
     sync()
     t1 = time.perf_counter()
     dist.barrier(env)
-    elapsed = dist.all_reduce_max(env, tmr.seconds())
+    my_seconds = tmr.seconds()
+    elapsed = dist.all_reduce_max(env, my_seconds)
     wall_elapsed = dist.all_reduce_max(env, t1 - t0)
     ms_per_step = elapsed / args.steps * 1e3
     total_tflops = n * wl.flops * args.steps / elapsed / 1e12
+    # per-rank view (weak-scaling diagnosis; `value` stays the max-over-ranks
+    # figure): each rank's own TF/s and the shader clock it holds under a dense
+    # MFMA load right after the timed loop (clock_probe_ghz, ~1 ms), so a
+    # power- or thermally-limited GPU is told apart from a slow one
+    clk = None
+    if dev.type == "cuda" and hasattr(backend, "clock_probe_ghz"):
+        clk = backend.clock_probe_ghz(dev)
+    per_rank = dist.all_gather_obj(env, {"tflops": round(wl.flops * args.steps / my_seconds / 1e12, 2),
+                                         "clock": clk})
 
     # ---- after the timed region: verification + context measurements
     extras: dict = {}
@@ -351,6 +361,24 @@ def main(argv=None) -> int:
             extras["p2p_send_GBps"] = pm.as_dict()
             if pm.errors:
                 verified = False
+        if not args.no_xgmi and n <= 8:
+            # C2 knob sweep first: blocks per rank x one-/two-shot at 4 sizes, the
+            # favoured one-shot cutoff (xgmi.tune; a few seconds at N = 8). The
+            # rehearsal runs it over torch.distributed to pin the JSON shape.
+            from nvidia_terraform_modules_amd.parallel import xgmi as xg
+
+            fac = None
+            if args.rehearsal:
+                fac = lambda nb, mb: xg.ReferenceAllReduce(env, mb, nblk=nb)  # noqa: E731
+            t_tune = time.perf_counter()
+            try:
+                tuned = xg.tune(env, factory=fac)
+                tuned["seconds"] = round(time.perf_counter() - t_tune, 2)
+                extras["xgmi_tune"] = tuned
+                if tuned["errors"] or tuned["timed_out"]:
+                    verified = False
+            except Exception as e:  # noqa: BLE001 - recorded; the main sweep still runs
+                extras["xgmi_tune"] = {"error": f"{type(e).__name__}: {e}"[:300]}
         if not args.no_xgmi and not args.rehearsal and n <= 8:
             # C2 next to RCCL: the same sizes, in place on the registered buffer,
             # no host sync / barrier / staging per call (device-side barriers).
@@ -440,6 +468,9 @@ def main(argv=None) -> int:
             if (extras.get("validation_job") or {}).get("passed") else None),
         "bench_process_to_verified_s": round(_CLOCK.elapsed("gemm_verified"), 3),
         "in_node_phases_s": {k: round(v, 4) for k, v in _CLOCK.durations().items()},
+        "per_rank_tflops": [p["tflops"] for p in per_rank],
+        "per_rank_clock_GHz": [p["clock"]["median_GHz"] if p["clock"] else None for p in per_rank],
+        "per_rank_clock_probe": [p["clock"] for p in per_rank],
         "vs_baseline_note": "reference publishes no TFLOP/s or busbw (BASELINE.json published={})",
         **({"rehearsal": True} if args.rehearsal else {}),
         **extras,

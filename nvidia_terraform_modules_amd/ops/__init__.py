@@ -9,7 +9,8 @@ K1 ``gemm_bf16``      - 256x256x64 LDS-DMA + MFMA bf16 GEMM (the headline; small
                           and the wave-specialised tiles, ``k1_fp8_plan``).
 K2 ``stream_copy``, ``stream_read`` - tuned float4 HBM streams.
 K3 ``fill_uniform_``, ``ref_gemm_f32``, ``verify_bf16``, ``abft_check`` - synthetic
-   data, full fp32 reference check and the O(n^2) checksum check.
+   data, full fp32 reference check and the O(n^2) checksum check;
+   ``clock_probe_ghz`` - the shader clock held under a dense MFMA load.
 
 Import is cheap; the native library is loaded on first kernel call and raises
 ``NativeLibraryMissing`` if it was not built (no silent fallback).
@@ -19,6 +20,7 @@ from .kernels import (  # noqa: F401
     AbftReport,
     VerifyReport,
     abft_check,
+    clock_probe_ghz,
     fill_uniform_,
     gemm_bf16,
     gemm_bf16_rowsum,

@@ -36,7 +36,10 @@ GEMM_VARIANTS = {"default": 0, "pingpong8": 1, "wave128": 2, "wave128d4": 3, "pi
                  "pingpong8cwn": 12, "pingpong8cwne": 13, "pingpong8pw": 14, "tile128": 15,
                  "tile256x128": 16, "tile160": 17, "tile256x160": 18, "tile128w4": 19,
                  "tile256x128w4": 20, "tile160w4": 21, "pingpong8cm": 22, "tile160x128": 23,
-                 "tile128x160": 24, "regstage4": 25, "regstage4b": 26, "regstage4c": 27}
+                 "tile128x160": 24, "regstage4": 25, "regstage4b": 26, "regstage4c": 27,
+                 "regstage4_diag_noload": 28, "regstage4_diag_nostage": 29,
+                 "regstage4_diag_noread": 30, "dma4": 31, "dma4_j24": 32, "dma4_j40": 33,
+                 "dma4_pb4": 34, "dma4_d3": 35, "dma4_pb8": 36}
 
 
 # variants built only into libntm_experimental.so (tests / tools): never selected
@@ -45,7 +48,10 @@ EXPERIMENTAL_VARIANTS = frozenset({"pingpong8", "wave128", "wave128d4", "pingpon
                                    "pingpong8w", "pingpong8wi", "pingpong8ww", "pingpong8cw",
                                    "pingpong8cwe", "pingpong8cwn", "pingpong8cwne",
                                    "pingpong8pw", "tile128w4", "tile256x128w4", "tile160w4",
-                                   "regstage4", "regstage4b", "regstage4c"})
+                                   "regstage4", "regstage4b", "regstage4c",
+                                   "regstage4_diag_noload", "regstage4_diag_nostage",
+                                   "regstage4_diag_noread", "dma4", "dma4_j24", "dma4_j40",
+                                   "dma4_pb4", "dma4_d3", "dma4_pb8"})
 
 # (TM, TN) of the 4-wave tile kernels (gemm_bf16_t128.hpp)
 TILE_SHAPES = {"tile128": (128, 128), "tile256x128": (256, 128), "tile160": (160, 160),
@@ -494,3 +500,28 @@ def gemm_tolerance(k: int) -> tuple[float, float]:
     summation-order difference grows ~sqrt(K) * 2^-24 * |terms|."""
     atol = 1e-3 + 4.0 * (k ** 0.5) * 2.0 ** -20
     return atol, 2.0 ** -7
+
+
+def clock_probe_ghz(device=None, iters: int = 20000, grid: int = 256) -> dict:
+    """Shader clock this GPU holds under a dense bf16 MFMA load on random
+    operands (``clock_probe_kernel``: Delta s_memtime / Delta s_memrealtime per
+    wave, one 4-wave block per CU). Returns the median / min / max GHz over
+    waves and the probe's wall time. Run it right after a timed loop: it reads
+    the power / thermal state that loop left, which is what tells a
+    power-limited GPU apart from a slow one in a multi-GPU run."""
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    out = torch.zeros(grid * 4 * 2, dtype=torch.int64, device=dev)
+    sink = torch.zeros(1, dtype=torch.float32, device=dev)
+    t0 = torch.cuda.Event(enable_timing=True)
+    t1 = torch.cuda.Event(enable_timing=True)
+    t0.record()
+    check(lib().ntm_clock_probe(grid, iters, out.data_ptr(), sink.data_ptr(), stream_handle()),
+          "ntm_clock_probe")
+    t1.record()
+    t1.synchronize()
+    v = out.view(-1, 2).double()
+    ghz = (v[:, 0] / v[:, 1] * 0.1)
+    ghz = ghz[torch.isfinite(ghz)]
+    return {"median_GHz": round(float(ghz.median()), 4), "min_GHz": round(float(ghz.min()), 4),
+            "max_GHz": round(float(ghz.max()), 4), "probe_ms": round(t0.elapsed_time(t1), 3),
+            "waves": int(ghz.numel())}

@@ -267,3 +267,90 @@ def _copy_d2d(dst: int, src: int, nbytes: int) -> None:
         check(lib().ntm_stream_copy(src, dst, nbytes, stream_handle()), "ntm_stream_copy")
     else:
         raise ValueError("sizes must be 16-byte multiples")
+
+
+class ReferenceAllReduce:
+    """The knob surface of :class:`XgmiAllReduce` (``nblk``,
+    ``one_shot_max_bytes``, ``timed_out``, ``close``) over
+    ``torch.distributed.all_reduce``: lets CPU/gloo rehearsals run
+    :func:`tune` end to end and pin its JSON shape. Not a measurement."""
+
+    def __init__(self, env, max_bytes: int, nblk: int = 64, one_shot_max_bytes: int = 256 << 10):
+        self.env, self.nblk, self.max_bytes = env, nblk, max_bytes
+        self.one_shot_max_bytes = min(one_shot_max_bytes, max_bytes)
+
+    def __call__(self, t: torch.Tensor, check: bool = False) -> torch.Tensor:
+        import torch.distributed as tdist
+
+        if self.env.world_size > 1:
+            tdist.all_reduce(t)
+        return t
+
+    def timed_out(self) -> bool:
+        return False
+
+    def close(self) -> None:
+        pass
+
+
+# C2 knob sweep (VERDICT r2: the first 8-GPU run must say whether the design or
+# a constant is at fault). Budget at N = 8: 4 communicators (one IPC set-up
+# each, ~0.1-0.5 s) x 4 sizes x <= 2 algorithms x 12 calls of <= ~0.2 ms, plus
+# one full-element check per point - a few seconds in all.
+TUNE_SIZES = (64 << 10, 256 << 10, 1 << 20, 16 << 20)
+TUNE_NBLKS = (16, 32, 64, 128)
+TUNE_CUTOFFS = (64 << 10, 256 << 10, 1 << 20)
+
+
+def tune(env, sizes=TUNE_SIZES, nblks=TUNE_NBLKS, cutoffs=TUNE_CUTOFFS, iters: int = 10,
+         warmup: int = 2, factory=None) -> dict:
+    """Sweep blocks per rank x algorithm (one-shot where a size is <= the
+    largest cutoff, two-shot always) at each size, every element checked.
+    Returns the full table, the best (nblk, algorithm) per size and the
+    one-shot cutoff among ``cutoffs`` that the measurements favour.
+    ``factory(nblk, max_bytes)`` builds the communicator (default
+    :class:`XgmiAllReduce`); set-up is collective, so every rank must call."""
+    from .collectives import all_reduce_sweep
+
+    factory = factory or (lambda nb, mb: XgmiAllReduce(env, max_bytes=mb, nblk=nb))
+    max_b = max(sizes)
+    table, errors, timed_out = [], 0, False
+    for nb in nblks:
+        ar = factory(nb, max_b)
+        try:
+            for size in sizes:
+                for algo in ("1shot", "2shot"):
+                    if algo == "1shot" and size > max(cutoffs):
+                        continue
+                    ar.one_shot_max_bytes = size if algo == "1shot" else 0
+                    r = all_reduce_sweep(env, [size], dtype="bf16", iters=iters, warmup=warmup,
+                                         impl=ar)[0]
+                    errors += r.errors
+                    table.append({"nblk": nb, "bytes": r.bytes, "algo": algo,
+                                  "time_us": round(r.time_us, 2),
+                                  "busbw_GBps": round(r.busbw_GBps, 2), "errors": r.errors})
+            timed_out = timed_out or ar.timed_out()
+        finally:
+            ar.close()
+
+    def best(size, algos):
+        rows = [t for t in table if t["bytes"] == size and t["algo"] in algos]
+        return max(rows, key=lambda t: t["busbw_GBps"]) if rows else None
+
+    best_per_size = [{k: b[k] for k in ("bytes", "nblk", "algo", "busbw_GBps")}
+                     for b in (best(s, ("1shot", "2shot")) for s in sizes) if b]
+    # the cutoff whose implied algorithm choice (one-shot iff size <= cutoff),
+    # each at its best nblk, moves the sizes fastest (sum of per-size times)
+    score = {}
+    for c in cutoffs:
+        tot = 0.0
+        for s in sizes:
+            b = best(s, ("1shot",) if s <= c else ("2shot",))
+            tot += b["time_us"] if b else float("inf")
+        score[c] = tot
+    best_cut = min(score, key=score.get)
+    return {"sizes": list(sizes), "nblks": list(nblks), "cutoffs": list(cutoffs),
+            "table": table, "best_per_size": best_per_size,
+            "best_one_shot_max_bytes": best_cut,
+            "cutoff_total_time_us": {str(c): round(v, 2) for c, v in score.items()},
+            "errors": errors, "timed_out": timed_out}

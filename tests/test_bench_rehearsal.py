@@ -66,6 +66,23 @@ def test_torchrun_launch_one_json_line(nproc):
     job = d["validation_job"]
     assert job["ran"] is False or job["passed"] is False
     assert d["time_to_gpu_ready_in_node_s"] is None
+    # per-rank view of the weak-scaling run: every rank's own TF/s
+    # and its MFMA-load clock (None on the CPU rehearsal)
+    assert len(d["per_rank_tflops"]) == nproc and all(t > 0 for t in d["per_rank_tflops"])
+    assert d["per_rank_clock_GHz"] == [None] * nproc
+    assert len(d["per_rank_clock_probe"]) == nproc
+    if nproc > 1:
+        # C2 knob sweep: blocks per rank x one/two-shot at 4 sizes, best per size and
+        # the favoured one-shot cutoff (over torch.distributed here: shape only)
+        tune = d["xgmi_tune"]
+        assert tune["errors"] == 0 and tune["timed_out"] is False
+        assert tune["nblks"] == [16, 32, 64, 128] and len(tune["sizes"]) == 4
+        assert {r["nblk"] for r in tune["table"]} == set(tune["nblks"])
+        one = [r for r in tune["table"] if r["algo"] == "1shot"]
+        assert one and all(r["bytes"] <= max(tune["cutoffs"]) for r in one)
+        assert len(tune["best_per_size"]) == 4
+        assert tune["best_one_shot_max_bytes"] in tune["cutoffs"]
+        assert set(tune["cutoff_total_time_us"]) == {str(c) for c in tune["cutoffs"]}
     if nproc > 1:
         assert all(r["errors"] == 0 for r in d["allreduce_bf16"] + d["allreduce_fp32"])
         assert d["allreduce_bf16"][0]["bytes"] == 8

@@ -375,3 +375,26 @@ def test_help_exits_zero_without_touching_the_gpu():
     _have_bin()
     rc, out, err = _run("--help", timeout=60)
     assert rc == 0 and "usage" in err
+
+
+def test_cpp_and_python_collective_sweeps_agree():
+    """the Job binary's C1/C2 sweeps (C++) and the torch
+    sweeps bench.py runs (parallel/collectives.py) must not drift: same sizes,
+    same nccl-tests busbw factor (host-only --describe-sweep, no GPU)."""
+    _have_bin()
+    import sys
+    sys.path.insert(0, str(ROOT))
+    from nvidia_terraform_modules_amd.parallel import collectives as coll
+
+    for mib in (1, 64, 8192):
+        rc, out, err = _run("--describe-sweep", "--allreduce-max-mib", str(mib), timeout=60)
+        assert rc == 0, err
+        d = json.loads(out)
+        assert d["rccl_bytes"] == coll.sweep_sizes(8, mib << 20, 4)
+        assert d["bus_factor"] == pytest.approx([coll.bus_factor("all_reduce", n)
+                                                 for n in range(1, 9)])
+        for n in range(1, 9):
+            # bench.py's C2 list (paired with its RCCL rows): same rule, same cap
+            py = [b for b in coll.sweep_sizes(8, mib << 20, 4)
+                  if 512 <= b <= 1 << 30 and (b // 2) % (8 * n) == 0]
+            assert d["xgmi_bytes"][str(n)] == py

@@ -430,5 +430,49 @@ __global__ void __launch_bounds__(256)
   if (s != s || s == __builtin_huge_valf()) sink[blockIdx.x] = s;
 }
 
+// Clock probe: the shader clock a GPU holds under a dense MFMA load, for
+// telling a power- or thermally-limited GPU apart from a slow one in a
+// multi-GPU run (bench.py per_rank_clock_GHz). Each wave runs `iters` x 8
+// back-to-back v_mfma_f32_16x16x32_bf16 on random operands (the clock depends
+// on the data: MI355X_MICROARCH.md "DVFS give-back" items 1, 6) and records
+// Delta s_memtime (shader cycles) and Delta s_memrealtime (100 MHz ticks):
+// clock = cycles / ticks * 0.1 GHz. One block of 4 waves per CU loads every
+// SIMD. out: 2 u64 per wave; sink: one float nobody reads (keeps the MFMAs).
+__global__ void __launch_bounds__(256) clock_probe_kernel(int iters, unsigned seed,
+                                                          unsigned long long* out, float* sink) {
+  typedef int i32x4 __attribute__((ext_vector_type(4)));
+  const int lane = threadIdx.x & 63;
+  i32x4 a, b;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    // bf16 pairs with small exponents: random mantissas, no inf / nan
+    const unsigned h = (unsigned)mix64(((unsigned long long)seed << 32) ^ (lane * 8 + i));
+    a[i] = (int)(h & 0x3F7F3F7Fu);
+    b[i] = (int)((h >> 5) & 0x3F7F3F7Fu);
+  }
+  f32x4 acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+  const unsigned long long r0 = __builtin_amdgcn_s_memrealtime();
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[j]) : "v"(a), "v"(b));
+  }
+  asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");  // MFMA results land before VALU reads
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s += acc[j][0] + acc[j][1] + acc[j][2] + acc[j][3];
+  const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+  const unsigned long long r1 = __builtin_amdgcn_s_memrealtime();
+  if (s == 12345.678f) sink[0] = s;
+  if (lane == 0) {
+    const size_t w = (size_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+    out[2 * w] = t1 - t0;
+    out[2 * w + 1] = r1 - r0;
+  }
+}
+
 }  // namespace aux
 }  // namespace ntm

@@ -63,10 +63,19 @@ constexpr int kGroupM = 8;
 
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
+// K >= 256: the two-tile loop body runs at least once, so the tail is reached
+// by ONE path (a second path - the loop skipped - made the register allocator
+// permute accumulators with v_accvgpr_mov at the join, right before asm
+// MFMAs that read them as srcC: an unpadded hazard, wrong results).
 __host__ __device__ inline bool shape_ok(int M, int N, int K) {
-  return M > 0 && N > 0 && K >= 2 * BK && (M % BM) == 0 && (N % BN) == 0 &&
+  return M > 0 && N > 0 && K >= 4 * BK && (M % BM) == 0 && (N % BN) == 0 &&
          (K % (2 * BK)) == 0;
 }
+
+// Diagnostic builds (timing ablations, results wrong): DIAG 1 = no
+// buffer_loads in the loop (the ds_writes store stale S), 2 = neither loads
+// nor ds_writes, 3 = no fragment reads (MFMAs on stale fragments).
+enum : int { kDiagNone = 0, kDiagNoLoad = 1, kDiagNoStage = 2, kDiagNoRead = 3 };
 
 struct Ctx {
   __amdgpu_buffer_rsrc_t rsa, rsb;  // whole-operand descriptors (wave-uniform)
@@ -120,14 +129,17 @@ __device__ __forceinline__ void mfma(f32x4& acc, const bf16x8& b, const bf16x8& 
 // One K-tile t held in buffer BUF. WRITES: stage tile t+1 (in S) into the other
 // buffer; LOADS: refill S with tile t+2; NEXT: barrier t + F0 reads of tile t+1.
 // JB: the phase-1 MFMA after which the barrier sits.
-template <int BUF, bool WRITES, bool LOADS, bool NEXT, int JB>
+template <int BUF, bool WRITES_, bool LOADS_, bool NEXT, int JB, int DIAG = 0>
 __device__ __forceinline__ void ktile(const Ctx& c, f32x4 (&acc)[8][8], Frags& f0, Frags& f1,
                                       u32x4 (&s)[16], int t) {
   static_assert(JB >= 32 && JB <= 56, "barrier after the write/load pairs, reads after it");
+  constexpr bool WRITES = WRITES_ && DIAG != kDiagNoStage;
+  constexpr bool LOADS = LOADS_ && DIAG != kDiagNoStage && DIAG != kDiagNoLoad;
+  constexpr bool READS = DIAG != kDiagNoRead;
 #pragma unroll
   for (int j = 0; j < 64; ++j) {
     mfma(acc[j >> 3][j & 7], f0.b[j & 7], f0.a[j >> 3]);
-    if ((j & 3) == 0) read_frag<BUF, 1>(c, f1, j >> 2);
+    if (READS && (j & 3) == 0) read_frag<BUF, 1>(c, f1, j >> 2);
     if constexpr (WRITES) {
       if ((j & 7) == 2) write_piece<BUF ^ 1>(c, s[j >> 3], j >> 3);
     }
@@ -153,7 +165,7 @@ __device__ __forceinline__ void ktile(const Ctx& c, f32x4 (&acc)[8][8], Frags& f
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         raw_barrier();
       }
-      if (j >= JB && ((j - JB) * 16) / NR != ((j - JB + 1) * 16) / NR)
+      if (READS && j >= JB && ((j - JB) * 16) / NR != ((j - JB + 1) * 16) / NR)
         read_frag<BUF ^ 1, 0>(c, f0, ((j - JB) * 16) / NR);
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -200,7 +212,7 @@ __device__ __forceinline__ void store_tile(const GemmArgs& p, const Ctx& c, cons
   }
 }
 
-template <int JB = 40, int GROUP_M = kGroupM>
+template <int JB = 40, int GROUP_M = kGroupM, int DIAG = 0>
 __global__ void __launch_bounds__(kThreads, 1) gemm_bf16_r4_kernel(GemmArgs p) {
   __shared__ __attribute__((aligned(16))) char smem[kLds];
   int tm, tn;
@@ -250,14 +262,16 @@ __global__ void __launch_bounds__(kThreads, 1) gemm_bf16_r4_kernel(GemmArgs p) {
 #pragma unroll
   for (int r = 0; r < 16; ++r) read_frag<0, 0>(c, f0, r);
 
-  // T even: one straight two-tile body keeps buffer and register roles fixed
+  // T even, >= 4: one straight two-tile body keeps buffer and register roles
+  // fixed; do-while so that the tail has a single predecessor (shape_ok)
   int t = 0;
-  for (; t < T - 2; t += 2) {
-    ktile<0, true, true, true, JB>(c, acc, f0, f1, s, t);
-    ktile<1, true, true, true, JB>(c, acc, f0, f1, s, t + 1);
-  }
-  ktile<0, true, false, true, JB>(c, acc, f0, f1, s, t);
-  ktile<1, false, false, false, JB>(c, acc, f0, f1, s, t + 1);
+  do {
+    ktile<0, true, true, true, JB, DIAG>(c, acc, f0, f1, s, t);
+    ktile<1, true, true, true, JB, DIAG>(c, acc, f0, f1, s, t + 1);
+    t += 2;
+  } while (t < T - 2);
+  ktile<0, true, false, true, JB, DIAG>(c, acc, f0, f1, s, t);
+  ktile<1, false, false, false, JB, DIAG>(c, acc, f0, f1, s, t + 1);
 
   ::ntm::gemm::mfma_drain();  // asm MFMAs: results land before the epilogue reads them
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -272,11 +286,11 @@ inline bool args_ok(const GemmArgs& a) {
          !a.rowsum;
 }
 
-template <int JB = 40>
+template <int JB = 40, int DIAG = 0>
 inline hipError_t launch_gemm_bf16_r4(const GemmArgs& a, hipStream_t stream) {
   if (!args_ok(a)) return hipErrorInvalidValue;
   const dim3 g((unsigned)((a.M / BM) * (a.N / BN))), b(kThreads);
-  hipLaunchKernelGGL((gemm_bf16_r4_kernel<JB>), g, b, 0, stream, a);
+  hipLaunchKernelGGL((gemm_bf16_r4_kernel<JB, kGroupM, DIAG>), g, b, 0, stream, a);
   return hipGetLastError();
 }
 

@@ -15,6 +15,8 @@
 //   25..27 regstage4 / regstage4b / regstage4c: 4 waves, 128x128 per wave,
 //          register-staged operands, barrier after phase-1 MFMA 40 / 48 / 34
 //          (gemm_bf16_r4.hpp)
+//   31..36 dma4 / _j24 / _j40 / _pb4 / _d3 / _pb8: 4 waves, 128x128 per wave,
+//          LDS-DMA ring of half-K-tile slots (gemm_bf16_r4d.hpp knobs)
 //   19..21 tile128w4 / tile256x128w4 / tile160w4: the 4-wave (one wave per
 //          SIMD) tile kernels that the wave-specialised ones replaced as
 //          variants 15..17 (gemm_bf16_t128.hpp; profiles/r2_ws)
@@ -26,6 +28,7 @@
 #include "ntm/gemm_bf16_pp4.hpp"
 #include "ntm/gemm_bf16_pp5.hpp"
 #include "ntm/gemm_bf16_r4.hpp"
+#include "ntm/gemm_bf16_r4d.hpp"
 #include "ntm/gemm_bf16_t128.hpp"
 #include "ntm/gemm_bf16_w4.hpp"
 #include "ntm/gemm_fp8_diag.hpp"
@@ -80,6 +83,18 @@ NTM_API int ntm_gemm_bf16_experimental(int variant, const void* A, const void* B
     case 25: return (int)ntm::gemmr::launch_gemm_bf16_r4<40>(a, S(stream));
     case 26: return (int)ntm::gemmr::launch_gemm_bf16_r4<48>(a, S(stream));
     case 27: return (int)ntm::gemmr::launch_gemm_bf16_r4<34>(a, S(stream));
+    // timing ablations (wrong results): no loads / no staging / no fragment reads
+    case 28: return (int)ntm::gemmr::launch_gemm_bf16_r4<40, 1>(a, S(stream));
+    case 29: return (int)ntm::gemmr::launch_gemm_bf16_r4<40, 2>(a, S(stream));
+    case 30: return (int)ntm::gemmr::launch_gemm_bf16_r4<40, 3>(a, S(stream));
+    // 4 waves x 128x128, LDS-DMA ring of half-K-tile slots (gemm_bf16_r4d.hpp):
+    // <prefetch distance D, barrier after MFMA JB, DMA pieces before it PB>
+    case 31: return (int)ntm::gemmrd::launch_gemm_bf16_r4d<4, 8, 0>(a, S(stream));
+    case 32: return (int)ntm::gemmrd::launch_gemm_bf16_r4d<4, 24, 0>(a, S(stream));
+    case 33: return (int)ntm::gemmrd::launch_gemm_bf16_r4d<4, 40, 0>(a, S(stream));
+    case 34: return (int)ntm::gemmrd::launch_gemm_bf16_r4d<4, 16, 4>(a, S(stream));
+    case 35: return (int)ntm::gemmrd::launch_gemm_bf16_r4d<3, 8, 0>(a, S(stream));
+    case 36: return (int)ntm::gemmrd::launch_gemm_bf16_r4d<4, 40, 8>(a, S(stream));
     default: return (int)hipErrorInvalidValue;
   }
 }

@@ -595,6 +595,15 @@ NTM_API int ntm_verify_bf16(const void* C, const float* R, size_t n,
   return (int)hipGetLastError();
 }
 
+// Clock probe (aux_kernels.hpp clock_probe_kernel): grid blocks of 4 waves,
+// out = 2 u64 per wave (shader cycles, 100 MHz ticks), sink = 1 float.
+NTM_API int ntm_clock_probe(int grid, int iters, void* out, float* sink, void* stream) {
+  if (grid <= 0 || iters <= 0 || !out || !sink) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(ntm::aux::clock_probe_kernel, dim3(grid), dim3(256), 0, S(stream), iters,
+                     7u, (unsigned long long*)out, sink);
+  return (int)hipGetLastError();
+}
+
 NTM_API int ntm_verify_result_bytes() {
   return (int)sizeof(ntm::aux::VerifyResult);
 }

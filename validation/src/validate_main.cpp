@@ -122,6 +122,7 @@ struct Opts {
   long xgmi_one_shot_max = 256 << 10;  // C2: messages <= this take the one-shot kernel
   bool require_host_prep = false;    // fail unless numa_balancing = 0 and memlock unlimited
   bool require_iommu_pt = false;     // ... and the kernel booted with iommu=pt
+  bool describe_sweep = false;       // print the C1/C2 size lists + busbw factors, no GPU
   bool json = true;
   std::string out;
   std::string termination_log;  // k8s terminationMessagePath (<= 4 KiB summary)
@@ -139,7 +140,7 @@ void usage() {
                "       [--no-p2p] [--p2p-mib MiB] [--p2p-floor-gbps GBps] [--p2p-loopback]\n"
                "       [--rccl-busbw-floor-gbps GBps] [--xgmi-busbw-floor-gbps GBps]\n"
                "       [--xgmi-nblk N] [--xgmi-one-shot-max BYTES]\n"
-               "       [--require-host-prep] [--require-iommu-pt]\n"
+               "       [--require-host-prep] [--require-iommu-pt] [--describe-sweep]\n"
                "       [--json] [--out FILE]\n"
                "       [--termination-log FILE] [--prom-out FILE] [--fault-inject KIND]\n"
                "       [--pushgateway http://host:port]\n"
@@ -182,6 +183,7 @@ bool parse(int argc, char** argv, Opts& o) {
     else if (a == "--xgmi-one-shot-max") { if (!(v = next(a.c_str()))) return false; o.xgmi_one_shot_max = std::atol(v); }
     else if (a == "--require-host-prep") o.require_host_prep = true;
     else if (a == "--require-iommu-pt") o.require_iommu_pt = true;
+    else if (a == "--describe-sweep") o.describe_sweep = true;
     else if (a == "--fp8-tflops-floor") { if (!(v = next(a.c_str()))) return false; o.fp8_tflops_floor = std::atof(v); }
     else if (a == "--json") o.json = true;
     else if (a == "--out") { if (!(v = next("--out"))) return false; o.out = v; }
@@ -526,6 +528,24 @@ struct CollRow {
 
 double bus_factor(int n) { return n > 1 ? 2.0 * (n - 1) / n : 0.0; }
 
+// C1 message sizes up to maxb: nccl-tests style, 8 B .. max, x4 per step (the
+// torch sweep in parallel/collectives.py builds the same list; a CPU test
+// pins the two against each other through --describe-sweep)
+std::vector<size_t> rccl_sizes(size_t maxb) {
+  std::vector<size_t> v;
+  for (size_t b = 8; b <= maxb; b *= 4) v.push_back(b);
+  return v;
+}
+
+// C2 message sizes: the C1 sizes from 512 B that split into 8-element chunks
+// per rank, so every C2 row pairs with a C1 row (bench.py builds the same list)
+std::vector<size_t> xgmi_sizes(size_t maxb, int n) {
+  std::vector<size_t> v;
+  for (const size_t b : rccl_sizes(maxb))
+    if (b >= 512 && (b / 2) % (8 * (size_t)n) == 0) v.push_back(b);
+  return v;
+}
+
 // Largest sweep message: --allreduce-max-mib, capped at 40 % of the smallest
 // free HBM over `devs` and rounded down to a power of two (the sweep doubles).
 size_t sweep_cap(const std::vector<int>& devs, size_t want, int buffers_per_dev) {
@@ -581,7 +601,8 @@ bool run_rccl(const std::vector<int>& devs, const Opts& o, std::vector<CollRow>&
   }
   // nccl-tests style: 8 B .. max, x4 per step, bf16 then fp32
   for (const bool f32 : {false, true}) {
-    for (size_t bytes = 8; bytes <= maxb && ok; bytes *= 4) {
+    for (const size_t bytes : rccl_sizes(maxb)) {
+      if (!ok) break;
       const size_t esz = f32 ? 4 : 2;
       const size_t cnt = bytes / esz;
       const ncclDataType_t dt = f32 ? ncclFloat32 : ncclBfloat16;
@@ -756,9 +777,10 @@ std::string p2p_json(const P2pResult& r) {
 // one launch per GPU). Simulated mode (--xgmi-sim N): all N ranks on devs[0]
 // in one launch (rank = block / nblk), so the whole protocol - entry barrier,
 // reduce-scatter, all-gather, exit barrier, epochs - runs on a one-GPU box
-// through this same driver. Sizes from 1 KiB; <= 256 KiB takes the one-shot
-// kernel. The kernel synchronises the ranks itself (device-side entry
-// barrier), so the timed loop launches back to back with no host sync.
+// through this same driver. Sizes: xgmi_sizes (512 B .. min(max, 1 GiB));
+// <= --xgmi-one-shot-max (256 KiB) takes the one-shot kernel. The kernel
+// synchronises the ranks itself (device-side entry barrier), so the timed
+// loop launches back to back with no host sync.
 bool run_xgmi(const std::vector<int>& devs, const Opts& o, std::vector<CollRow>& rows) {
   const bool sim = o.xgmi_sim > 0;
   const int n = sim ? o.xgmi_sim : (int)devs.size();
@@ -808,9 +830,9 @@ bool run_xgmi(const std::vector<int>& devs, const Opts& o, std::vector<CollRow>&
   }
   unsigned epoch = 0;
   bool ok = true;
-  for (size_t bytes = 1024; bytes <= maxb && ok; bytes *= 4) {
+  for (const size_t bytes : xgmi_sizes(maxb, n)) {
+    if (!ok) break;
     const size_t cnt = bytes / 2;
-    if (cnt % (8 * (size_t)n)) continue;
     const int one_shot = bytes <= one_shot_max ? 1 : 0;
     auto run_once = [&]() -> bool {
       ++epoch;
@@ -1018,6 +1040,22 @@ int main(int argc, char** argv) {
   if (o.xgmi_nblk < 1 || o.xgmi_nblk > 1024 || o.xgmi_one_shot_max < 0) {
     std::fprintf(stderr, "--xgmi-nblk must be in 1..1024, --xgmi-one-shot-max >= 0\n");
     return 2;
+  }
+  if (o.describe_sweep) {
+    // host-only: the sweep definitions the GPU paths use, for CPU tests
+    const size_t maxb = (size_t)o.allreduce_max_mib << 20;
+    auto arr = [](const std::vector<size_t>& v) {
+      std::string t = "[";
+      for (size_t i = 0; i < v.size(); ++i) t += (i ? "," : "") + std::to_string(v[i]);
+      return t + "]";
+    };
+    std::string t = "{\"rccl_bytes\":" + arr(rccl_sizes(maxb)) + ",\"bus_factor\":[";
+    for (int k = 1; k <= 8; ++k) t += (k > 1 ? "," : "") + jnum(bus_factor(k));
+    t += "],\"xgmi_bytes\":{";
+    for (int k = 1; k <= 8; ++k)
+      t += (k > 1 ? ",\"" : "\"") + std::to_string(k) + "\":" + arr(xgmi_sizes(std::min<size_t>(maxb, (size_t)1 << 30), k));
+    std::printf("%s}}\n", t.c_str());
+    return 0;
   }
   if (o.fault.empty())
     if (const char* f = std::getenv("NTM_FAULT_INJECT")) o.fault = f;
