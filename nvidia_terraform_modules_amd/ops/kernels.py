@@ -30,10 +30,9 @@ def _require(t: torch.Tensor, name: str, dtype: torch.dtype) -> None:
         raise ValueError(f"{name} must be 2-D with unit inner stride")
 
 
-GEMM_VARIANTS = {"default": 0, "pingpong8": 1, "wave128": 2, "wave128d4": 3, "pingpong8b": 4,
-                 "pingpong8c": 5, "pingpong8p": 6, "pingpong8w": 7, "pingpong8wi": 8,
-                 "pingpong8ww": 9, "pingpong8cw": 10, "pingpong8cwe": 11,
-                 "pingpong8cwn": 12, "pingpong8cwne": 13, "pingpong8pw": 14, "tile128": 15,
+GEMM_VARIANTS = {"default": 0, "pingpong8": 1, "pingpong8b": 4,
+                 "pingpong8c": 5, "pingpong8cw": 10, "pingpong8cwe": 11,
+                 "pingpong8cwn": 12, "pingpong8cwne": 13, "tile128": 15,
                  "tile256x128": 16, "tile160": 17, "tile256x160": 18, "tile128w4": 19,
                  "tile256x128w4": 20, "tile160w4": 21, "pingpong8cm": 22, "tile160x128": 23,
                  "tile128x160": 24, "regstage4": 25, "regstage4b": 26, "regstage4c": 27,
@@ -44,10 +43,9 @@ GEMM_VARIANTS = {"default": 0, "pingpong8": 1, "wave128": 2, "wave128d4": 3, "pi
 
 # variants built only into libntm_experimental.so (tests / tools): never selected
 # by the default dispatch, not present in the shipping library or Job binary
-EXPERIMENTAL_VARIANTS = frozenset({"pingpong8", "wave128", "wave128d4", "pingpong8p",
-                                   "pingpong8w", "pingpong8wi", "pingpong8ww", "pingpong8cw",
+EXPERIMENTAL_VARIANTS = frozenset({"pingpong8", "pingpong8cw",
                                    "pingpong8cwe", "pingpong8cwn", "pingpong8cwne",
-                                   "pingpong8pw", "tile128w4", "tile256x128w4", "tile160w4",
+                                   "tile128w4", "tile256x128w4", "tile160w4",
                                    "regstage4", "regstage4b", "regstage4c",
                                    "regstage4_diag_noload", "regstage4_diag_nostage",
                                    "regstage4_diag_noread", "dma4", "dma4_j24", "dma4_j40",
@@ -125,10 +123,10 @@ def gemm_bf16(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
     consumer waves and masked edge tiles (any M, N % 4), 256x160 with 4 waves
     and whole tiles) for small, mid-size and ragged C,
     else "pingpong8c" when K % 128 == 0, else "pingpong8b" (8 waves, two per SIMD, staggered, balanced 8/4/8/4 LDS read
-    schedule; 8c adds parity-alternating B buffers and a tail-free K loop -
-    fastest measured), "pingpong8" (the first 12/4/8/0 schedule), or the
-    experimental "wave128"/"wave128d4" (4 waves, 128x128 per wave,
-    AGPR-pinned accumulators) - see validation/include.
+    schedule; 8c adds parity-alternating B buffers and a tail-free K loop),
+    "pingpong8" (the first 12/4/8/0 schedule), or the experimental
+    "regstage4*" / "dma4*" (4 waves, 128x128 per wave, register-staged /
+    LDS-DMA operands) - see validation/include.
     ``splits`` > 1 (masked tiles only): split-K into that many K slices, fp32
     partials in a workspace from PyTorch's allocator, then one reduction kernel.
     """

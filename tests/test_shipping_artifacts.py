@@ -1,6 +1,6 @@
 """What ships: the validation-Job binary and libntm_validation.so carry ONLY
 the kernels the default K1 dispatch (and K1-fp8 / K2 / K3 / C2) can launch.
-The experimental K1 builds, schedule knobs and diagnostics (w4, pp4, pp5,
+The experimental K1 builds, schedule knobs and diagnostics (r4, r4d,
 pp3 knobs and stamps, the first ping-pong, fp8 knobs, MFMA probes) live in
 libntm_experimental.so only (VERDICT r1 "Next round" #8). Host-only check of
 the kernel symbols with nm - no GPU needed."""
@@ -62,7 +62,7 @@ ALLOWED_K1 = {
     "ntm::gemmt::gemm_bf16_tile_ws_kernel<4, 5, 0, true, true>",
     "ntm::gemmt::gemm_bf16_tile_kernel<8, 5>",
 }
-EXPERIMENTAL_ONLY = ("gemm_bf16_w4_kernel", "gemm_bf16_pp4_kernel", "gemm_bf16_pp5_kernel",
+EXPERIMENTAL_ONLY = ("gemm_bf16_r4_kernel", "gemm_bf16_r4d_kernel",
                      "gemm_bf16_pp3_stamp_kernel", "ntm::gemm::gemm_bf16_kernel",
                      "mfma_rate_kernel", "mfma_f8_probe_kernel")
 
@@ -93,6 +93,6 @@ def test_shipping_artifact_has_only_default_dispatch_k1(path):
 
 def test_experimental_library_holds_the_experiments():
     ks = _kernels(EXP)
-    for fam in ("gemm_bf16_w4_kernel", "gemm_bf16_pp4_kernel", "gemm_bf16_pp5_kernel",
+    for fam in ("gemm_bf16_r4_kernel", "gemm_bf16_r4d_kernel",
                 "gemm_bf16_pp3_stamp_kernel", "mfma_rate_kernel", "mfma_f8_probe_kernel"):
         assert any(fam in k for k in ks), fam

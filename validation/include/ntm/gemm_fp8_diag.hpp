@@ -9,7 +9,7 @@
 // with exact integer data").
 #pragma once
 
-#include "ntm/gemm_bf16_pp4.hpp"
+#include "ntm/gemm_bf16_pp3.hpp"
 #include "ntm/gemm_fp8.hpp"
 
 namespace ntm {
@@ -25,10 +25,9 @@ __global__ void __launch_bounds__(64) mfma_f8_probe_kernel(const i32x8* a, const
 // 1 = B-fragment-outer MFMA order (scaled form); 2 = GROUP_M 4; 3 = static s_setprio(1) on
 // wave row 1; 4 = register (widened + nontemporal) epilogue instead of the
 // LDS-staged one; 5 = the scaled MFMA form with unit VGPR scales (the previous default;
-// knobs 1-4 use it too); on the plain form: 6 = persistent (gemm_bf16_pp4.hpp), 7 = register
-// epilogue with wave row 0 storing early, 8 = register epilogue, 9 = GROUP_M 4. Measured
-// (profiles/r2_fp8ws/knobs_6_9.log, persistent_fp8_knob6_rejected.log): 6-8 are 1-2 % slower,
-// 9 ties (+0.5 % at 8192^3 over 15 rounds, -1.4 % at 4096^3), so the default stays.
+// knobs 1-4 use it too). Knobs 6-9 (persistent, early / register epilogues, GROUP_M 4 on
+// the plain form) measured 1-2 % slower or tied (profiles/r2_fp8ws/knobs_6_9.log) and were
+// deleted (git history).
 inline hipError_t launch_gemm_fp8_knob(const void* A, const void* B, __bf16* C, int M, int N,
                                        int K, int lda, int ldb, int ldc, int knob,
                                        hipStream_t s) {
@@ -56,19 +55,6 @@ inline hipError_t launch_gemm_fp8_knob(const void* A, const void* B, __bf16* C, 
     case 3: hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, kGroupM, false, kEpiDefault, 2, 1>), g, b, 0, s, a); break;
     case 4: hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, kGroupM, false, kEpiWide | kEpiNT, 0, 1>), g, b, 0, s, a); break;
     case 5: hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, kGroupM, false, kEpiDefault, 0, 1>), g, b, 0, s, a); break;
-    case 7: hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, kGroupM, false, kEpiWide | kEpiNT | kEpiEarly, 0, 3>), g, b, 0, s, a); break;
-    case 8: hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, kGroupM, false, kEpiWide | kEpiNT, 0, 3>), g, b, 0, s, a); break;
-    case 9: hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, 4, false, kEpiDefault, 0, 3>), g, b, 0, s, a); break;
-    case 6: {  // persistent (gemm_bf16_pp4.hpp): DMA pipeline across tiles, register epilogue
-      if (!::ntm::gemm3::shape_ok3(a.M, a.N, a.K)) return hipErrorInvalidValue;
-      const int ntiles = (M / BM) * (N / BN);
-      int gp = ::ntm::gemmp::cu_count();
-      gp -= gp % 8;
-      if (gp <= 0) gp = 8;
-      if (gp > ntiles) gp = ntiles;
-      hipLaunchKernelGGL((::ntm::gemmp::gemm_bf16_pp4_kernel<false, kEpiWide | kEpiNT, 3>), dim3(gp), b, 0, s, a);
-      break;
-    }
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

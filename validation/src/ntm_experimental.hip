@@ -5,11 +5,6 @@
 //
 // K1 variants (bf16, C = A B^T, the numbering of ops.kernels.GEMM_VARIANTS):
 //   1      pingpong8: the first 8-wave 12/4/8/0 LDS-read schedule (gemm_bf16.hpp)
-//   2, 3   wave128 / wave128d4: 4 waves, 128x128 per wave, AGPR-pinned
-//          accumulators, prefetch distance 3 / 4 k-steps (gemm_bf16_w4.hpp)
-//   6, 14  pingpong8p / pingpong8pw: pingpong8c made persistent (one WG per CU,
-//          DMA pipeline across tiles), + widened epilogue (gemm_bf16_pp4.hpp)
-//   7..9   pingpong8w / wi / ww: 32-MFMA segment schedules (gemm_bf16_pp5.hpp)
 //   10..13 pingpong8c epilogue knobs: widened / + early row-0 stores /
 //          nontemporal stores / both (gemm_bf16_pp3.hpp launch_gemm_bf16_pp3_knob)
 //   25..27 regstage4 / regstage4b / regstage4c: 4 waves, 128x128 per wave,
@@ -20,17 +15,16 @@
 //   19..21 tile128w4 / tile256x128w4 / tile160w4: the 4-wave (one wave per
 //          SIMD) tile kernels that the wave-specialised ones replaced as
 //          variants 15..17 (gemm_bf16_t128.hpp; profiles/r2_ws)
-// Measured: none beats the shipping default (profiles/r1_pp3, r1_pp4, r1_pp3_knobs,
-// r1_pmc2_w4); kept as the record of what was tried and as ablation baselines.
+// Rejected builds are deleted once measured (git history keeps them: the 4-wave
+// wave128 / wave128d4, the persistent pingpong8p / 8pw, the 32-MFMA-segment
+// pingpong8w / wi / ww, fp8 knobs 6-9 - profiles/r1_pmc2_w4, r1_pp4, r2_fp8ws);
+// what stays is used by a test or a tool under tools/.
 #include "ntm/gemm_bf16.hpp"
 #include "ntm/gemm_bf16_pp3.hpp"
 #include "ntm/gemm_bf16_pp3_stamp.hpp"
-#include "ntm/gemm_bf16_pp4.hpp"
-#include "ntm/gemm_bf16_pp5.hpp"
 #include "ntm/gemm_bf16_r4.hpp"
 #include "ntm/gemm_bf16_r4d.hpp"
 #include "ntm/gemm_bf16_t128.hpp"
-#include "ntm/gemm_bf16_w4.hpp"
 #include "ntm/gemm_fp8_diag.hpp"
 #include "ntm/stream_policy_exp.hpp"
 
@@ -62,17 +56,6 @@ NTM_API int ntm_gemm_bf16_experimental(int variant, const void* A, const void* B
   const ntm::gemm::GemmArgs a = args(A, B, C, M, N, K, lda, ldb, ldc);
   switch (variant) {
     case 1: return (int)ntm::gemm::launch_gemm_bf16(a, S(stream));
-    case 2:
-    case 3: {
-      ntm::gemm4::Args w{(const __bf16*)A, (const __bf16*)B, (__bf16*)C, M, N, K, lda, ldb, ldc};
-      return variant == 2 ? (int)ntm::gemm4::launch<3>(w, S(stream))
-                          : (int)ntm::gemm4::launch<4>(w, S(stream));
-    }
-    case 6: return (int)ntm::gemmp::launch_gemm_bf16_pp4(a, S(stream));
-    case 14: return (int)ntm::gemmp::launch_gemm_bf16_pp4(a, S(stream), true);
-    case 7:
-    case 8:
-    case 9: return (int)ntm::gemm5::launch_gemm_bf16_pp5(a, variant - 7, S(stream));
     case 10:
     case 11:
     case 12:
