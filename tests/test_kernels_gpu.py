@@ -667,3 +667,39 @@ def test_gemm_fp8_plain_and_scaled_mfma_forms_agree_bitwise(ops):
     ref = a.float() @ b.float().T
     atol, rtol = ops.gemm_tolerance(k)
     assert ((c0.float() - ref).abs() <= atol + rtol * ref.abs()).all()
+
+
+@pytest.mark.parametrize("variant", ["regstage4", "dma4", "dma4_d3", "dma4_pb8", "knob24", "knob25"])
+@pytest.mark.parametrize("m,n,k", [(256, 256, 256), (512, 768, 384), (1024, 512, 1024),
+                                   (2048, 2048, 4096), (768, 1280, 640)])
+def test_round3_k1_experiments_vs_torch_fp32(ops, variant, m, n, k):
+    """Round-3 K1 experiments (profiles/r3_k1): the 4-wave 128x128-per-wave
+    kernels (register-staged, LDS-DMA ring at prefetch depth 4 / 3, DMA before
+    the barrier) and the 8-wave default with SGPR-addressed DMA (buffer /
+    global saddr forms): every K-tile count from 4 (the peeled tail only) up,
+    vs fp32; the 8-wave builds bitwise equal to the default (same MFMA order)."""
+    if variant.startswith(("regstage4", "dma4")) and (k < 256 or k % 128):
+        pytest.skip("4-wave kernels need K % 128, K >= 256")
+    a = _rand(ops, (m, k), 571 + k)
+    b = _rand(ops, (n, k), 573 + n)
+    c = ops.gemm_bf16(a, b, variant=variant)
+    ref = a.float() @ b.float().T
+    atol, rtol = ops.gemm_tolerance(k)
+    err = (c.float() - ref).abs()
+    assert torch.all(err <= atol + rtol * ref.abs()), float(err.max())
+    if variant.startswith("knob"):
+        assert torch.equal(c, ops.gemm_bf16(a, b, variant="pingpong8c"))
+
+
+@pytest.mark.parametrize("m,n,k", [(256, 256, 512), (512, 768, 1024), (2048, 1024, 4096)])
+def test_fp8_dma4_vs_torch_fp32(ops, m, n, k):
+    """K1-fp8 on the 4-wave LDS-DMA kernel (fp8 knob 10, gemm_fp8_r4d.hpp):
+    vs the fp32 product of the e4m3 values, and bitwise equal to the default
+    8-wave build (per accumulator the same f8f6f4 MFMAs in the same K order)."""
+    a = ops.fill_uniform_(torch.empty((m, k), dtype=torch.float8_e4m3fn, device="cuda"), 21)
+    b = ops.fill_uniform_(torch.empty((n, k), dtype=torch.float8_e4m3fn, device="cuda"), 22)
+    c10 = ops.gemm_fp8(a, b, knob=10)
+    ref = a.float() @ b.float().T
+    atol, rtol = ops.gemm_tolerance(k)
+    assert ((c10.float() - ref).abs() <= atol + rtol * ref.abs()).all()
+    assert torch.equal(c10.view(torch.int16), ops.gemm_fp8(a, b).view(torch.int16))
