@@ -75,15 +75,34 @@ struct Ctx {
 // the k step in the SGPR soffset, the LDS destination in M0 - no per-piece
 // VALU address math and no 64-bit address VGPRs (the global_load_lds form
 // needed 16 of them per half-step pair and spilled).
+// M0SHARE: the 4 pieces of an operand share one M0 (the LDS base of the
+// wave's 4 subtiles) and step the LDS destination with the instruction offset
+// field (it moves the global address too, so soffset takes it back out):
+// one M0 write per 4 pieces instead of one per piece.
+template <bool M0SHARE = false>
 __device__ __forceinline__ void issue_piece(const Ctx& c, int hs, int H, int slot_off, int w,
                                             int i) {
   const int kb = (hs < H ? hs : H - 1) * (BKH * 2);
   const bool is_b = i >= 4;
   const int rbi = i & 3;
-  char* dst = c.lds + slot_off + (is_b ? kHalfOp : 0) + (w * 4 + rbi) * 1024;
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(is_b ? c.rsb : c.rsa, (NTM_AS3 void*)dst, 16,
-                                           is_b ? c.voff_b : c.voff_a,
-                                           kb + rbi * (is_b ? c.rowblk_b : c.rowblk_a), 0, 0);
+  const int row_soff = kb + rbi * (is_b ? c.rowblk_b : c.rowblk_a);
+  if constexpr (M0SHARE) {
+    char* dst = c.lds + slot_off + (is_b ? kHalfOp : 0) + (w * 4) * 1024;
+    // rowblk >= 16 rows x 256 x 2 B > rbi * 1024: soffset stays positive
+    const auto rs = is_b ? c.rsb : c.rsa;
+    const int vo = is_b ? c.voff_b : c.voff_a, so = row_soff - rbi * 1024;
+    NTM_AS3 void* d = (NTM_AS3 void*)dst;
+    switch (rbi) {  // the offset operand must be a literal
+      case 0: __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, d, 16, vo, so, 0, 0); break;
+      case 1: __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, d, 16, vo, so, 1024, 0); break;
+      case 2: __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, d, 16, vo, so, 2048, 0); break;
+      default: __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, d, 16, vo, so, 3072, 0); break;
+    }
+  } else {
+    char* dst = c.lds + slot_off + (is_b ? kHalfOp : 0) + (w * 4 + rbi) * 1024;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(is_b ? c.rsb : c.rsa, (NTM_AS3 void*)dst, 16,
+                                             is_b ? c.voff_b : c.voff_a, row_soff, 0, 0);
+  }
 }
 
 // Fragment read r (0..15): a[0], b[0..7], a[1..7].
@@ -105,7 +124,7 @@ __device__ __forceinline__ void wait_vm() {
 
 // One half-step. fc: fragments consumed; fn: fragments read for hs+1.
 // PB: DMA pieces issued before the barrier (the rest after it).
-template <int D, int JB, int PB>
+template <int D, int JB, int PB, bool M0S = false>
 __device__ __forceinline__ void half_step(const Ctx& c, f32x4 (&acc)[8][8], const Frags& fc,
                                           Frags& fn, int hs, int H, int slot_next, int slot_dma,
                                           int w) {
@@ -117,11 +136,11 @@ __device__ __forceinline__ void half_step(const Ctx& c, f32x4 (&acc)[8][8], cons
     mfma(acc[j >> 3][j & 7], fc.b[j & 7], fc.a[j >> 3]);
     if (j < JB) {
       if (PB > 0 && (j * PB) / JB != ((j + 1) * PB) / JB)
-        issue_piece(c, hs + D, H, slot_dma, w, (j * PB) / JB);
+        issue_piece<M0S>(c, hs + D, H, slot_dma, w, (j * PB) / JB);
     } else {
       const int x = j - JB;
       if (PA > 0 && (x * PA) / NR != ((x + 1) * PA) / NR)
-        issue_piece(c, hs + D, H, slot_dma, w, PB + (x * PA) / NR);
+        issue_piece<M0S>(c, hs + D, H, slot_dma, w, PB + (x * PA) / NR);
       if ((x * 16) / NR != ((x + 1) * 16) / NR) read_frag(c, fn, slot_next, (x * 16) / NR);
     }
     if (j == JB - 1) {
@@ -134,7 +153,7 @@ __device__ __forceinline__ void half_step(const Ctx& c, f32x4 (&acc)[8][8], cons
   }
 }
 
-template <int D = 4, int JB = 8, int PB = 0, int GROUP_M = kGroupM>
+template <int D = 4, int JB = 8, int PB = 0, int GROUP_M = kGroupM, bool M0S = false>
 __global__ void __launch_bounds__(kThreads, 1) gemm_bf16_r4d_kernel(GemmArgs p) {
   using C = Cfg<D>;
   __shared__ __attribute__((aligned(16))) char smem[C::kLds];
@@ -189,18 +208,18 @@ __global__ void __launch_bounds__(kThreads, 1) gemm_bf16_r4d_kernel(GemmArgs p) 
   // iteration)
   int hs = 0;
   do {
-    half_step<D, JB, PB>(c, acc, f0, f1, hs, H, sn * kSlot, sd * kSlot, w);
+    half_step<D, JB, PB, M0S>(c, acc, f0, f1, hs, H, sn * kSlot, sd * kSlot, w);
     sn = sn + 1 == C::S ? 0 : sn + 1;
     sd = sd + 1 == C::S ? 0 : sd + 1;
-    half_step<D, JB, PB>(c, acc, f1, f0, hs + 1, H, sn * kSlot, sd * kSlot, w);
+    half_step<D, JB, PB, M0S>(c, acc, f1, f0, hs + 1, H, sn * kSlot, sd * kSlot, w);
     sn = sn + 1 == C::S ? 0 : sn + 1;
     sd = sd + 1 == C::S ? 0 : sd + 1;
     hs += 2;
   } while (hs < H - 2);
-  half_step<D, JB, PB>(c, acc, f0, f1, hs, H, sn * kSlot, sd * kSlot, w);
+  half_step<D, JB, PB, M0S>(c, acc, f0, f1, hs, H, sn * kSlot, sd * kSlot, w);
   sn = sn + 1 == C::S ? 0 : sn + 1;
   sd = sd + 1 == C::S ? 0 : sd + 1;
-  half_step<D, JB, PB>(c, acc, f1, f0, hs + 1, H, sn * kSlot, sd * kSlot, w);
+  half_step<D, JB, PB, M0S>(c, acc, f1, f0, hs + 1, H, sn * kSlot, sd * kSlot, w);
 
   ::ntm::gemm::mfma_drain();
   wait_vm<0>();  // dummy pieces landed before LDS is reused
@@ -218,11 +237,12 @@ inline bool args_ok(const GemmArgs& a) {
          (long long)a.M * a.lda * 2 < (1ll << 31) && (long long)a.N * a.ldb * 2 < (1ll << 31);
 }
 
-template <int D = 4, int JB = 8, int PB = 0>
+template <int D = 4, int JB = 8, int PB = 0, bool M0S = false>
 inline hipError_t launch_gemm_bf16_r4d(const GemmArgs& a, hipStream_t stream) {
-  if (!args_ok(a)) return hipErrorInvalidValue;
+  if (!args_ok(a) || (M0S && (16 * a.lda * 2 < 4096 || 16 * a.ldb * 2 < 4096)))
+    return hipErrorInvalidValue;
   const dim3 g((unsigned)((a.M / BM) * (a.N / BN))), b(kThreads);
-  hipLaunchKernelGGL((gemm_bf16_r4d_kernel<D, JB, PB>), g, b, 0, stream, a);
+  hipLaunchKernelGGL((gemm_bf16_r4d_kernel<D, JB, PB, kGroupM, M0S>), g, b, 0, stream, a);
   return hipGetLastError();
 }
 

@@ -78,6 +78,7 @@ NTM_API int ntm_gemm_bf16_experimental(int variant, const void* A, const void* B
     case 34: return (int)ntm::gemmrd::launch_gemm_bf16_r4d<4, 16, 4>(a, S(stream));
     case 35: return (int)ntm::gemmrd::launch_gemm_bf16_r4d<3, 8, 0>(a, S(stream));
     case 36: return (int)ntm::gemmrd::launch_gemm_bf16_r4d<4, 40, 8>(a, S(stream));
+    case 37: return (int)ntm::gemmrd::launch_gemm_bf16_r4d<4, 8, 0, true>(a, S(stream));
     default: return (int)hipErrorInvalidValue;
   }
 }
