@@ -38,7 +38,9 @@ GEMM_VARIANTS = {"default": 0, "pingpong8": 1, "pingpong8b": 4,
                  "tile128x160": 24, "regstage4": 25, "regstage4b": 26, "regstage4c": 27,
                  "regstage4_diag_noload": 28, "regstage4_diag_nostage": 29,
                  "regstage4_diag_noread": 30, "dma4": 31, "dma4_j24": 32, "dma4_j40": 33,
-                 "dma4_pb4": 34, "dma4_d3": 35, "dma4_pb8": 36, "dma4_m0": 37}
+                 "dma4_pb4": 34, "dma4_d3": 35, "dma4_pb8": 36, "dma4_m0": 37,
+                 "dma4k": 38, "dma4k_d3": 39,
+                 "ring4": 41, "ring4ab": 44}
 
 
 # variants built only into libntm_experimental.so (tests / tools): never selected
@@ -49,7 +51,9 @@ EXPERIMENTAL_VARIANTS = frozenset({"pingpong8", "pingpong8cw",
                                    "regstage4", "regstage4b", "regstage4c",
                                    "regstage4_diag_noload", "regstage4_diag_nostage",
                                    "regstage4_diag_noread", "dma4", "dma4_j24", "dma4_j40",
-                                   "dma4_pb4", "dma4_d3", "dma4_pb8", "dma4_m0"})
+                                   "dma4_pb4", "dma4_d3", "dma4_pb8", "dma4_m0",
+                                   "dma4k", "dma4k_d3",
+                                   "ring4", "ring4ab"})
 
 # (TM, TN) of the 4-wave tile kernels (gemm_bf16_t128.hpp)
 TILE_SHAPES = {"tile128": (128, 128), "tile256x128": (256, 128), "tile160": (160, 160),

@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--ks", default="1024,2048,4096,8192,16384")
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--variant", default="default")
+    ap.add_argument("--knob", type=int, default=0, help="fp8: experimental K1-fp8 schedule knob")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"])
     args = ap.parse_args()
     fp8 = args.dtype == "fp8"
@@ -45,7 +46,7 @@ def main():
         ours, theirs = [], []
         for _ in range(args.rounds):
             if fp8:
-                ours.append(timed(lambda: ops.gemm_fp8(a, b, c), 20))
+                ours.append(timed(lambda: ops.gemm_fp8(a, b, c, knob=args.knob), 20))
                 theirs.append(timed(lambda: torch._scaled_mm(a, b.T, scale_a=one, scale_b=one,
                                                              out_dtype=torch.bfloat16), 20))
             else:

@@ -26,13 +26,15 @@ def main() -> int:
     ap.add_argument("--versus", default="",
                     help="a second K1 variant to run in place of torch.matmul (e.g. tile256x128w4)")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"])
+    ap.add_argument("--knob", type=int, default=0,
+                    help="fp8: experimental K1-fp8 schedule knob for 'ours' (--which all adds the default)")
     ap.add_argument("--warm-iters", type=int, default=40,
                     help="untimed pairs first, so most profiled dispatches run on a settled chip")
     args = ap.parse_args()
     args.iters += args.warm_iters
     s = args.size
     if args.dtype == "fp8":
-        return fp8_pair(s, args.iters, args.which)
+        return fp8_pair(s, args.iters, args.which, args.knob)
     a = torch.empty((s, s), dtype=torch.bfloat16, device="cuda")
     b = torch.empty((s, s), dtype=torch.bfloat16, device="cuda")
     c = torch.empty((s, s), dtype=torch.bfloat16, device="cuda")
@@ -52,7 +54,7 @@ def main() -> int:
     return 0
 
 
-def fp8_pair(s: int, iters: int, which: str) -> int:
+def fp8_pair(s: int, iters: int, which: str, knob: int = 0) -> int:
     """K1-fp8 vs hipBLASLt's fp8 GEMM (torch._scaled_mm, unit scales, bf16 out)."""
     a = ops.fill_uniform_(torch.empty((s, s), dtype=torch.float8_e4m3fn, device="cuda"), 1)
     b = ops.fill_uniform_(torch.empty((s, s), dtype=torch.float8_e4m3fn, device="cuda"), 2)
@@ -60,6 +62,8 @@ def fp8_pair(s: int, iters: int, which: str) -> int:
     one = torch.ones((), device="cuda")
     for _ in range(iters):
         if which in ("both", "ours", "all"):
+            ops.gemm_fp8(a, b, c, knob=knob)
+        if which == "all" and knob:
             ops.gemm_fp8(a, b, c)
         if which in ("both", "torch", "all"):
             torch._scaled_mm(a, b.T, scale_a=one, scale_b=one, out_dtype=torch.bfloat16)

@@ -12,6 +12,7 @@
 #include "ntm/gemm_bf16_pp3.hpp"
 #include "ntm/gemm_fp8.hpp"
 #include "ntm/gemm_fp8_r4d.hpp"
+#include "ntm/gemm_r4ring.hpp"
 
 namespace ntm {
 namespace fp8 {
@@ -52,7 +53,10 @@ inline hipError_t launch_gemm_fp8_knob(const void* A, const void* B, __bf16* C, 
   switch (knob) {
     case 0: return launch_gemm_fp8(A, B, C, M, N, K, lda, ldb, ldc, s);
     // 10: the 4-wave 128x128-per-wave LDS-DMA kernel (gemm_fp8_r4d.hpp)
-    case 10: return ::ntm::fp8r::launch_gemm_fp8_r4d(A, B, C, M, N, K, lda, ldb, ldc, s);
+    case 10: return ::ntm::fp8r::launch_gemm_fp8_r4d<3>(A, B, C, M, N, K, lda, ldb, ldc, s);
+    case 12: return ::ntm::fp8r::launch_gemm_fp8_r4d<2>(A, B, C, M, N, K, lda, ldb, ldc, s);
+    // 17: the 5-slot operand-split half-K-tile ring (gemm_r4ring.hpp), DMA every 3 MFMAs
+    case 17: return ::ntm::ring::launch_gemm_fp8_ring4<3, true>(A, B, C, M, N, K, lda, ldb, ldc, s);
     case 1: hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, kGroupM, false, kEpiDefault, 0, 2>), g, b, 0, s, a); break;
     case 2: hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, 4, false, kEpiDefault, 0, 1>), g, b, 0, s, a); break;
     case 3: hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, kGroupM, false, kEpiDefault, 2, 1>), g, b, 0, s, a); break;

@@ -65,6 +65,8 @@ struct Frags8 {
 
 // Piece i (0..15) of K-tile kt: i < 8 -> A, else B; row block 4w + ((i >> 1) & 3),
 // half i & 1 (adjacent instructions fetch the two halves of a 128-byte line).
+// (A split-wait build - low k-halves first, two barriers per K-tile - ran
+// 9-14 % slower at 8192^3: profiles/r3_k1/fp8_r4k.log; git history.)
 __device__ __forceinline__ void issue_piece(const Ctx& c, int kt, int T, int buf, int w, int i) {
   const int kb = (kt < T ? kt : T - 1) * 128;
   const bool is_b = i >= 8;
@@ -87,17 +89,30 @@ __device__ __forceinline__ void read_b(const Ctx& c, Frags8& f, int buf, int nt)
   f.b[nt][1] = *(const bf16x8*)(p + 1024);
 }
 
+// One "MFMA slot" of the step: e4m3 -> one 32-cycle f8f6f4 MFMA over the
+// K-tile's 128 values; bf16 (F8 = false, the same image holds 64 bf16 per row)
+// -> two 16-cycle 16x16x32 MFMAs, k-half 0 then 1 (per accumulator the order
+// of the 8-wave default, so results are bitwise equal to it).
+template <bool F8 = true>
 __device__ __forceinline__ void mma(f32x4& acc, const Frags8& f, int mt, int nt) {
-  ::ntm::gemm::mfma_f8_agpr_plain(acc, cat_f8(f.b[nt][0], f.b[nt][1]), cat_f8(f.a[mt][0], f.a[mt][1]));
+  if constexpr (F8) {
+    ::ntm::gemm::mfma_f8_agpr_plain(acc, cat_f8(f.b[nt][0], f.b[nt][1]),
+                                    cat_f8(f.a[mt][0], f.a[mt][1]));
+  } else {
+    ::ntm::gemmr::mfma(acc, f.b[nt][0], f.a[mt][0]);
+    ::ntm::gemmr::mfma(acc, f.b[nt][1], f.a[mt][1]);
+  }
 }
 
 // One K-tile step on buffer BUF (fragments of tile t in f on entry, of t+1 on exit).
-template <int BUF>
+// DI: one DMA piece every DI MFMAs from the barrier on (the last piece's lead
+// to the next barrier is (56 - 16 DI) + 8 MFMAs).
+template <int BUF, int DI = 3, bool F8 = true>
 __device__ __forceinline__ void step(const Ctx& c, f32x4 (&acc)[8][8], Frags8& f, int t, int T,
                                      int w) {
 #pragma unroll
   for (int nt = 0; nt < 8; ++nt) {
-    mma(acc[0][nt], f, 0, nt);
+    mma<F8>(acc[0][nt], f, 0, nt);
     __builtin_amdgcn_sched_barrier(0);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile t+1 landed (this wave's pieces)
@@ -107,10 +122,10 @@ __device__ __forceinline__ void step(const Ctx& c, f32x4 (&acc)[8][8], Frags8& f
   for (int mt = 1; mt < 8; ++mt) {
 #pragma unroll
     for (int nt = 0; nt < 8; ++nt) {
-      mma(acc[mt][nt], f, mt, nt);
+      mma<F8>(acc[mt][nt], f, mt, nt);
       const int j = (mt - 1) * 8 + nt;  // 0..55
-      // 16 DMA pieces of tile t+2 over the first 48 MFMAs of rows 1..7
-      if ((j % 3) == 0 && j / 3 < 16) issue_piece(c, t + 2, T, BUF, w, j / 3);
+      // 16 DMA pieces of tile t+2, one every DI MFMA slots from the barrier
+      if ((j % DI) == 0 && j / DI < 16) issue_piece(c, t + 2, T, BUF, w, j / DI);
       if (nt == 1) read_a(c, f, BUF ^ 1, mt - 1);  // A[mt-1]: its last MFMA was row mt-1
       if (mt == 7) read_b(c, f, BUF ^ 1, nt);      // B[nt] after MFMA (7, nt)
       __builtin_amdgcn_sched_barrier(0);
@@ -120,7 +135,7 @@ __device__ __forceinline__ void step(const Ctx& c, f32x4 (&acc)[8][8], Frags8& f
   __builtin_amdgcn_sched_barrier(0);
 }
 
-template <int GROUP_M = kGroupM>
+template <int GROUP_M = kGroupM, int DI = 3, bool F8 = true>
 __global__ void __launch_bounds__(kThreads, 1) gemm_fp8_r4d_kernel(GemmArgs p) {
   __shared__ __attribute__((aligned(16))) char smem[kLds];
   int tm, tn;
@@ -174,12 +189,12 @@ __global__ void __launch_bounds__(kThreads, 1) gemm_fp8_r4d_kernel(GemmArgs p) {
   // is peeled (a loop exit straight into the epilogue made hipcc spill, r4d)
   int t = 0;
   do {
-    step<0>(c, acc, f, t, T, w);
-    step<1>(c, acc, f, t + 1, T, w);
+    step<0, DI, F8>(c, acc, f, t, T, w);
+    step<1, DI, F8>(c, acc, f, t + 1, T, w);
     t += 2;
   } while (t < T - 2);
-  step<0>(c, acc, f, t, T, w);
-  step<1>(c, acc, f, t + 1, T, w);
+  step<0, DI, F8>(c, acc, f, t, T, w);
+  step<1, DI, F8>(c, acc, f, t + 1, T, w);
 
   ::ntm::gemm::mfma_drain();
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // dummy pieces landed before LDS reuse
@@ -191,6 +206,7 @@ __global__ void __launch_bounds__(kThreads, 1) gemm_fp8_r4d_kernel(GemmArgs p) {
 }
 
 // K, lda, ldb in fp8 elements (the launcher halves them, like launch_gemm_fp8).
+template <int DI = 3>
 inline hipError_t launch_gemm_fp8_r4d(const void* A, const void* B, __bf16* C, int M, int N, int K,
                                       int lda, int ldb, int ldc, hipStream_t stream) {
   if (M <= 0 || N <= 0 || K < 512 || (M % BM) || (N % BN) || (K % 256) || lda < K || ldb < K ||
@@ -208,7 +224,21 @@ inline hipError_t launch_gemm_fp8_r4d(const void* A, const void* B, __bf16* C, i
   a.ldb = ldb / 2;
   a.ldc = ldc;
   const dim3 g((unsigned)((M / BM) * (N / BN))), b(kThreads);
-  hipLaunchKernelGGL(gemm_fp8_r4d_kernel<>, g, b, 0, stream, a);
+  hipLaunchKernelGGL((gemm_fp8_r4d_kernel<kGroupM, DI>), g, b, 0, stream, a);
+  return hipGetLastError();
+}
+
+// The same K-tile step on bf16 operands ("dma4k": one barrier per 128 MFMAs,
+// the DMA ring of gemm_bf16_r4d.hpp had one per 64). Shape rule: M, N % 256,
+// K % 128, K >= 256.
+template <int DI = 2>
+inline hipError_t launch_gemm_bf16_r4k(const GemmArgs& a, hipStream_t stream) {
+  if (a.M <= 0 || a.N <= 0 || a.K < 256 || (a.M % BM) || (a.N % BN) || (a.K % 128) ||
+      a.lda < a.K || a.ldb < a.K || a.ldc < a.N || (a.lda % 8) || (a.ldb % 8) || (a.ldc % 8) ||
+      a.rowsum || (long long)a.M * a.lda * 2 >= (1ll << 31) || (long long)a.N * a.ldb * 2 >= (1ll << 31))
+    return hipErrorInvalidValue;
+  const dim3 g((unsigned)((a.M / BM) * (a.N / BN))), b(kThreads);
+  hipLaunchKernelGGL((gemm_fp8_r4d_kernel<kGroupM, DI, false>), g, b, 0, stream, a);
   return hipGetLastError();
 }
 

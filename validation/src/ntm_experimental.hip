@@ -10,6 +10,10 @@
 //   25..27 regstage4 / regstage4b / regstage4c: 4 waves, 128x128 per wave,
 //          register-staged operands, barrier after phase-1 MFMA 40 / 48 / 34
 //          (gemm_bf16_r4.hpp)
+//   38, 39 dma4k / _d3: 4 waves, one K-tile step per barrier, two
+//          K-tile buffers (gemm_fp8_r4d.hpp on bf16)
+//   41, 44 ring4 / ring4ab: 4 waves, one K-tile step per barrier, 5-slot
+//          half-K-tile LDS-DMA ring, K-split / operand-split slots (gemm_r4ring.hpp)
 //   31..36 dma4 / _j24 / _j40 / _pb4 / _d3 / _pb8: 4 waves, 128x128 per wave,
 //          LDS-DMA ring of half-K-tile slots (gemm_bf16_r4d.hpp knobs)
 //   19..21 tile128w4 / tile256x128w4 / tile160w4: the 4-wave (one wave per
@@ -24,6 +28,9 @@
 #include "ntm/gemm_bf16_pp3_stamp.hpp"
 #include "ntm/gemm_bf16_r4.hpp"
 #include "ntm/gemm_bf16_r4d.hpp"
+#include "ntm/gemm_fp8_r4d.hpp"
+#include "ntm/gemm_r4ring.hpp"
+#include "ntm/gemm_r4k_stamp.hpp"
 #include "ntm/gemm_bf16_t128.hpp"
 #include "ntm/gemm_fp8_diag.hpp"
 #include "ntm/stream_policy_exp.hpp"
@@ -79,6 +86,15 @@ NTM_API int ntm_gemm_bf16_experimental(int variant, const void* A, const void* B
     case 35: return (int)ntm::gemmrd::launch_gemm_bf16_r4d<3, 8, 0>(a, S(stream));
     case 36: return (int)ntm::gemmrd::launch_gemm_bf16_r4d<4, 40, 8>(a, S(stream));
     case 37: return (int)ntm::gemmrd::launch_gemm_bf16_r4d<4, 8, 0, true>(a, S(stream));
+    // 4 waves x 128x128, one K-tile step per barrier, two LDS buffers
+    // (gemm_fp8_r4d.hpp on bf16): DMA piece every 2 / 3 MFMA pairs
+    case 38: return (int)ntm::fp8r::launch_gemm_bf16_r4k<2>(a, S(stream));
+    case 39: return (int)ntm::fp8r::launch_gemm_bf16_r4k<3>(a, S(stream));
+    // 4 waves x 128x128, one barrier per K-tile, 5-slot half-K-tile LDS-DMA
+    // ring (gemm_r4ring.hpp), DMA piece every 3 MFMA pairs: K-split slots
+    // (the two halves of a 128-B line fetched a K-tile apart) / operand-split
+    case 41: return (int)ntm::ring::launch_gemm_bf16_ring4<3>(a, S(stream));
+    case 44: return (int)ntm::ring::launch_gemm_bf16_ring4<3, true>(a, S(stream));
     default: return (int)hipErrorInvalidValue;
   }
 }
@@ -97,6 +113,15 @@ NTM_API int ntm_gemm_bf16_stamp(int mode, const void* A, const void* B, void* C,
                                 int K, int lda, int ldb, int ldc, void* stamps, void* stream) {
   return (int)ntm::gemm3s::launch_gemm_bf16_pp3_stamp(args(A, B, C, M, N, K, lda, ldb, ldc), mode,
                                                       (unsigned long long*)stamps, S(stream));
+}
+
+// dma4k (4 waves, one barrier per K-tile) with per-step wait / barrier stamps
+// (gemm_r4k_stamp.hpp; mode 0 real, 1 no DMA, 2 no reads, 3 no barrier, 4
+// MFMA only). stamps: (M/256)*(N/256)*4*10 u64.
+NTM_API int ntm_gemm_r4k_stamp(int mode, const void* A, const void* B, void* C, int M, int N,
+                               int K, int lda, int ldb, int ldc, void* stamps, void* stream) {
+  return (int)ntm::r4ks::launch_gemm_r4k_stamp(args(A, B, C, M, N, K, lda, ldb, ldc), mode,
+                                               (unsigned long long*)stamps, S(stream));
 }
 
 // Matrix-core issue rate (gemm_fp8_diag.hpp mfma_rate_kernel); out: 2 u64 per
