@@ -87,6 +87,17 @@ def main() -> int:
         wait = [r[2] / steps for r in s]
         bar = [r[3] / steps for r in s]
         ms = statistics.median(times[m])
+        # per-XCD view of the last launch: end of the XCD's last wave after the
+        # kernel's first wave started (s_memrealtime is one 100 MHz clock), and
+        # the XCD's median in-kernel clock
+        t0 = min(r[4] for r in s)
+        xcd_end, xcd_clk = {}, {}
+        for r, cl in zip(s, [sp / (max(r[5] - r[4], 1) * 10.0) for sp, r in zip(span, s)]):
+            x = r[7] & 0xF
+            xcd_end[x] = max(xcd_end.get(x, 0), r[5] - t0)
+            xcd_clk.setdefault(x, []).append(cl)
+        ends = [xcd_end[x] / 100.0 for x in sorted(xcd_end)]  # us
+        clks = [round(statistics.median(xcd_clk[x]), 3) for x in sorted(xcd_clk)]
         print(json.dumps({
             "mode": m, "ms": round(ms, 4), "tflops": round(2 * n ** 3 / ms / 1e9, 1),
             "clock_GHz": round(statistics.median(clk), 3),
@@ -98,7 +109,9 @@ def main() -> int:
             "wait_p90": round(sorted(wait)[int(0.9 * len(wait))], 1),
             "barrier_per_step": round(statistics.median(bar), 1),
             "barrier_p90": round(sorted(bar)[int(0.9 * len(bar))], 1),
-            "mfma_floor_per_step": 2048, "dtype": args.dtype,
+            "mfma_floor_per_step": 2048,
+            "xcd_end_us": [round(e, 1) for e in ends], "xcd_end_spread_us": round(max(ends) - min(ends), 1),
+            "xcd_clock_GHz": clks, "dtype": args.dtype,
             "c_stores": "temporal" if args.temporal else "nontemporal"}), flush=True)
     return 0
 
