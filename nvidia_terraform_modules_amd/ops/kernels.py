@@ -35,25 +35,14 @@ GEMM_VARIANTS = {"default": 0, "pingpong8": 1, "pingpong8b": 4,
                  "pingpong8cwn": 12, "pingpong8cwne": 13, "tile128": 15,
                  "tile256x128": 16, "tile160": 17, "tile256x160": 18, "tile128w4": 19,
                  "tile256x128w4": 20, "tile160w4": 21, "pingpong8cm": 22, "tile160x128": 23,
-                 "tile128x160": 24, "regstage4": 25, "regstage4b": 26, "regstage4c": 27,
-                 "regstage4_diag_noload": 28, "regstage4_diag_nostage": 29,
-                 "regstage4_diag_noread": 30, "dma4": 31, "dma4_j24": 32, "dma4_j40": 33,
-                 "dma4_pb4": 34, "dma4_d3": 35, "dma4_pb8": 36, "dma4_m0": 37,
-                 "dma4k": 38, "dma4k_d3": 39,
-                 "ring4": 41, "ring4ab": 44}
+                 "tile128x160": 24, "dma4k_d3": 39}
 
 
 # variants built only into libntm_experimental.so (tests / tools): never selected
 # by the default dispatch, not present in the shipping library or Job binary
 EXPERIMENTAL_VARIANTS = frozenset({"pingpong8", "pingpong8cw",
                                    "pingpong8cwe", "pingpong8cwn", "pingpong8cwne",
-                                   "tile128w4", "tile256x128w4", "tile160w4",
-                                   "regstage4", "regstage4b", "regstage4c",
-                                   "regstage4_diag_noload", "regstage4_diag_nostage",
-                                   "regstage4_diag_noread", "dma4", "dma4_j24", "dma4_j40",
-                                   "dma4_pb4", "dma4_d3", "dma4_pb8", "dma4_m0",
-                                   "dma4k", "dma4k_d3",
-                                   "ring4", "ring4ab"})
+                                   "tile128w4", "tile256x128w4", "tile160w4", "dma4k_d3"})
 
 # (TM, TN) of the 4-wave tile kernels (gemm_bf16_t128.hpp)
 TILE_SHAPES = {"tile128": (128, 128), "tile256x128": (256, 128), "tile160": (160, 160),
@@ -129,8 +118,8 @@ def gemm_bf16(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
     else "pingpong8c" when K % 128 == 0, else "pingpong8b" (8 waves, two per SIMD, staggered, balanced 8/4/8/4 LDS read
     schedule; 8c adds parity-alternating B buffers and a tail-free K loop),
     "pingpong8" (the first 12/4/8/0 schedule), or the experimental
-    "regstage4*" / "dma4*" (4 waves, 128x128 per wave, register-staged /
-    LDS-DMA operands) - see validation/include.
+    "dma4k_d3" (4 waves, 128x128 per wave, one barrier per K-tile, LDS-DMA
+    operands) - see validation/include.
     ``splits`` > 1 (masked tiles only): split-K into that many K slices, fp32
     partials in a workspace from PyTorch's allocator, then one reduction kernel.
     """

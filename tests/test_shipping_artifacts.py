@@ -62,7 +62,7 @@ ALLOWED_K1 = {
     "ntm::gemmt::gemm_bf16_tile_ws_kernel<4, 5, 0, true, true>",
     "ntm::gemmt::gemm_bf16_tile_kernel<8, 5>",
 }
-EXPERIMENTAL_ONLY = ("gemm_bf16_r4_kernel", "gemm_bf16_r4d_kernel",
+EXPERIMENTAL_ONLY = ("gemm_w4k_kernel", "gemm_r4k_stamp_kernel",
                      "gemm_bf16_pp3_stamp_kernel", "ntm::gemm::gemm_bf16_kernel",
                      "mfma_rate_kernel", "mfma_f8_probe_kernel")
 
@@ -93,6 +93,6 @@ def test_shipping_artifact_has_only_default_dispatch_k1(path):
 
 def test_experimental_library_holds_the_experiments():
     ks = _kernels(EXP)
-    for fam in ("gemm_bf16_r4_kernel", "gemm_bf16_r4d_kernel",
+    for fam in ("gemm_w4k_kernel", "gemm_r4k_stamp_kernel",
                 "gemm_bf16_pp3_stamp_kernel", "mfma_rate_kernel", "mfma_f8_probe_kernel"):
         assert any(fam in k for k in ks), fam

@@ -119,29 +119,7 @@ struct Ctx {
   int w, wr, wc;         // wave id, wave row (0..1), wave col (0..3)
   int K;                 // partial-K builds only (kEpiKTail): K, in elements
   int lane_col;          //   and this lane's 8-element source chunk offset
-  // buffer-DMA builds (kEpiBufDma): SGPR descriptors of A / B, the lane's
-  // byte offset in its row block (VGPR), the halves' row offsets (SGPR)
-  __amdgpu_buffer_rsrc_t rs[2];
-  int voff[2];
-  int hoff[4];
-  // SGPR-address DMA builds (kEpiSaddr): per-operand wave-uniform base
-  // pointers (SGPR pairs) - the lane part is voff[op]
-  const char* sbase[2];
 };
-
-// LDS-DMA piece with an SGPR base + 32-bit VGPR offset (global_load_lds_dwordx4
-// v_off, s[base:base+1]): hipcc (ROCm 7.2) never selects this form for the
-// builtin - it keeps a 64-bit address VGPR per piece and advances it with a
-// v_lshl_add_u64 per issue (the instruction offset field would move the LDS
-// destination as well). Here the K step is SGPR arithmetic. M0 = the piece's
-// LDS byte address; s_nop 0 covers the M0 write -> LDS-DMA hazard. The asm is
-// invisible to hipcc's vmcnt tracking: every wait on these pieces is an
-// explicit s_waitcnt vmcnt(N) (wait_vmcnt), as for the builtin form.
-__device__ __forceinline__ void glds16_saddr(const char* sbase, unsigned voff, char* lds_dst) {
-  const unsigned m = (unsigned)(size_t)(NTM_AS3 char*)lds_dst;
-  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1"
-               ::"v"(voff), "s"(sbase), "s"(m) : "memory");
-}
 
 // Issue the two glds of this wave for half-tile H of K-tile kt into buffer.
 template <int H>
@@ -482,11 +460,7 @@ __device__ __forceinline__ void store_tile_lds(const GemmArgs& p, const Ctx& c,
 // skip rows / column chunks past C (the kernel clamps its loads).
 // kEpiKTail (with kEpiMask): K % 128 != 0 - chunks past K load zeros (a build
 // flag that rides on the EPI mask, like kEpiMask it changes the loads too).
-// kEpiBufDma (whole tiles only): the DMA pieces are buffer_load_dwordx4 ... lds
-// with SGPR descriptors - no 64-bit address VGPRs and no per-piece VALU.
-// kEpiSaddr (whole tiles only): global_load_lds with SGPR base (glds16_saddr).
-enum : int { kEpiWide = 1, kEpiNT = 2, kEpiEarly = 4, kEpiLds = 8, kEpiMask = 16, kEpiKTail = 32,
-             kEpiBufDma = 64, kEpiSaddr = 128 };
+enum : int { kEpiWide = 1, kEpiNT = 2, kEpiEarly = 4, kEpiLds = 8, kEpiMask = 16, kEpiKTail = 32 };
 
 __device__ __attribute__((aligned(16))) const unsigned kZeroChunk16[4] = {0u, 0u, 0u, 0u};
 

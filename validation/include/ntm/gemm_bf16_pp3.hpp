@@ -45,33 +45,10 @@ struct Frags3 {
 
 // Stage half H of K-tile kt into buffer buf, or a dummy piece if kt >= T.
 // TAIL (partial-K build): a lane chunk starting at k >= K loads 16 zero bytes.
-template <int H, bool TAIL = false, bool BUFDMA = false, bool SADDR = false>
+template <int H, bool TAIL = false>
 __device__ __forceinline__ void issue_half3(const Ctx& c, int kt, int buf, int T) {
   const bool real = kt < T;
   const int k_eff = real ? kt : T - 1;
-  if constexpr (SADDR) {
-    static_assert(!TAIL && !BUFDMA, "SGPR-address DMA: whole tiles");
-    const int off = real ? buf * kTileBytes + H * kHalfBytes : kScratch;
-    char* d = c.lds + off + (2 * c.w) * 1024;
-    constexpr int op = H >= kBLo ? 1 : 0;
-    const char* sb = c.sbase[op] + c.hoff[H] + k_eff * (BK * 2);
-    glds16_saddr(sb, (unsigned)c.voff[op], d);
-    glds16_saddr(sb + 64, (unsigned)c.voff[op], d + 1024);
-    return;
-  }
-  if constexpr (BUFDMA) {
-    static_assert(!TAIL, "buffer DMA: whole tiles");
-    const int off = real ? buf * kTileBytes + H * kHalfBytes : kScratch;
-    char* d = c.lds + off + (2 * c.w) * 1024;
-    constexpr int op = H >= kBLo ? 1 : 0;
-    const int so = k_eff * (BK * 2) + c.hoff[H];
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(c.rs[op], (NTM_AS3 void*)d, 16, c.voff[op], so, 0, 0);
-    // (the instruction offset field moves the LDS destination too: the k-half
-    // step goes into soffset, never into `offset`)
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(c.rs[op], (NTM_AS3 void*)(d + 1024), 16, c.voff[op],
-                                             so + 64, 0, 0);
-    return;
-  }
   const __bf16* s = c.src[H] + (size_t)k_eff * BK;
   const int off = real ? buf * kTileBytes + H * kHalfBytes : kScratch;
   char* d = c.lds + off + (2 * c.w) * 1024;
@@ -85,8 +62,7 @@ __device__ __forceinline__ void issue_half3(const Ctx& c, int kt, int buf, int T
   }
 }
 
-template <int P, bool ODD, bool PRIO, int F8 = 0, bool TAIL = false, bool BUFDMA = false,
-          bool SADDR = false>
+template <int P, bool ODD, bool PRIO, int F8 = 0, bool TAIL = false>
 __device__ __forceinline__ void phase3(const Ctx& c, Frags3& f,
                                        f32x4 (&acc)[2][2][4][2], int t, int T) {
   bf16x8(&bcur)[2][2] = ODD ? f.b1 : f.b0;
@@ -96,21 +72,12 @@ __device__ __forceinline__ void phase3(const Ctx& c, Frags3& f,
   if constexpr (P == 1) read_b<kBHi>(c, both, cur);
   if constexpr (P == 2) read_a<kAHi>(c, f.a, cur);
   if constexpr (P == 3) read_b<kBLo>(c, both, cur ^ 1);  // tile t+1 (junk at t = T-1)
-  if constexpr (P == 0) issue_half3<kAHi, TAIL, BUFDMA, SADDR>(c, t + 1, cur ^ 1, T);
-  if constexpr (P == 1) issue_half3<kBLo, TAIL, BUFDMA, SADDR>(c, t + 2, cur, T);
-  if constexpr (P == 2) issue_half3<kALo, TAIL, BUFDMA, SADDR>(c, t + 2, cur, T);
-  if constexpr (P == 3) issue_half3<kBHi, TAIL, BUFDMA, SADDR>(c, t + 2, cur, T);
+  if constexpr (P == 0) issue_half3<kAHi, TAIL>(c, t + 1, cur ^ 1, T);
+  if constexpr (P == 1) issue_half3<kBLo, TAIL>(c, t + 2, cur, T);
+  if constexpr (P == 2) issue_half3<kALo, TAIL>(c, t + 2, cur, T);
+  if constexpr (P == 3) issue_half3<kBHi, TAIL>(c, t + 2, cur, T);
   wait_vmcnt<10>();
   raw_barrier();
-  if constexpr (BUFDMA || SADDR) {
-    // every fragment read of this phase retired before the first MFMA, as in
-    // the builtin-DMA build (where hipcc must wait lgkmcnt(0) because it
-    // counts the LDS-DMA as an LDS op); left alone, hipcc splits the wait
-    // into lgkmcnt(7/5/3/1/0) between MFMAs and reorders them: +4 % wave
-    // cycles (profiles/r3_k1/saddr_pmc.json)
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-  }
   if constexpr (F8) {
     if constexpr (P == 0) mma_quadrant_f8<F8>(acc[0][0], f.a, bcur);
     if constexpr (P == 1) mma_quadrant_f8<F8>(acc[0][1], f.a, both);
@@ -125,14 +92,13 @@ __device__ __forceinline__ void phase3(const Ctx& c, Frags3& f,
   raw_barrier();
 }
 
-template <bool ODD, bool PRIO, int F8 = 0, bool TAIL = false, bool BUFDMA = false,
-          bool SADDR = false>
+template <bool ODD, bool PRIO, int F8 = 0, bool TAIL = false>
 __device__ __forceinline__ void tile3(const Ctx& c, Frags3& f,
                                       f32x4 (&acc)[2][2][4][2], int t, int T) {
-  phase3<0, ODD, PRIO, F8, TAIL, BUFDMA, SADDR>(c, f, acc, t, T);
-  phase3<1, ODD, PRIO, F8, TAIL, BUFDMA, SADDR>(c, f, acc, t, T);
-  phase3<2, ODD, PRIO, F8, TAIL, BUFDMA, SADDR>(c, f, acc, t, T);
-  phase3<3, ODD, PRIO, F8, TAIL, BUFDMA, SADDR>(c, f, acc, t, T);
+  phase3<0, ODD, PRIO, F8, TAIL>(c, f, acc, t, T);
+  phase3<1, ODD, PRIO, F8, TAIL>(c, f, acc, t, T);
+  phase3<2, ODD, PRIO, F8, TAIL>(c, f, acc, t, T);
+  phase3<3, ODD, PRIO, F8, TAIL>(c, f, acc, t, T);
 }
 
 // GROUP_M / PRIO are tuning knobs (tools/gemm_check.py --variants knobN). The
@@ -156,10 +122,6 @@ __global__ void __launch_bounds__(kThreads, 2)
   static_assert(!(EPI & kEpiMask) || ((EPI & kEpiLds) && !kRowSum), "masked: LDS epilogue, no ABFT");
   static_assert(!(EPI & kEpiKTail) || (EPI & kEpiMask), "partial K rides on the masked build");
   constexpr bool TAIL = (EPI & kEpiKTail) != 0;
-  constexpr bool BUFDMA = (EPI & kEpiBufDma) != 0;
-  constexpr bool SADDR = (EPI & kEpiSaddr) != 0;
-  static_assert(!SADDR || !(EPI & (kEpiMask | kEpiBufDma)), "SGPR-address DMA: whole tiles");
-  static_assert(!BUFDMA || !(EPI & kEpiMask), "buffer DMA: whole tiles");
   static_assert(kLdsBytes3 >= BM * kStagePitch, "LDS staging buffer");
   __shared__ __attribute__((aligned(16))) char smem[kLdsBytes3];
 
@@ -185,25 +147,6 @@ __global__ void __launch_bounds__(kThreads, 2)
       c.src[kAHi] = p.A + (size_t)min(ra + 128, p.M - 1) * p.lda + cl * 8;
       c.src[kBLo] = p.B + (size_t)min(rb, p.N - 1) * p.ldb + cl * 8;
       c.src[kBHi] = p.B + (size_t)min(rb + 128, p.N - 1) * p.ldb + cl * 8;
-    } else if constexpr (SADDR) {
-      // wave-uniform bases (SGPRs): the tile's first A / B row; lane part in voff
-      c.sbase[0] = (const char*)(p.A + (size_t)m0 * p.lda);
-      c.sbase[1] = (const char*)(p.B + (size_t)n0 * p.ldb);
-      c.voff[0] = ((c.w * 16 + r) * p.lda + cl * 8) * 2;
-      c.voff[1] = ((c.w * 16 + r) * p.ldb + cl * 8) * 2;
-      c.hoff[kALo] = 0;
-      c.hoff[kAHi] = 128 * p.lda * 2;
-      c.hoff[kBLo] = 0;
-      c.hoff[kBHi] = 128 * p.ldb * 2;
-    } else if constexpr (BUFDMA) {
-      c.rs[0] = __builtin_amdgcn_make_buffer_rsrc((void*)p.A, (short)0, p.M * p.lda * 2, 0x00020000);
-      c.rs[1] = __builtin_amdgcn_make_buffer_rsrc((void*)p.B, (short)0, p.N * p.ldb * 2, 0x00020000);
-      c.voff[0] = (ra * p.lda + cl * 8) * 2;
-      c.voff[1] = (rb * p.ldb + cl * 8) * 2;
-      c.hoff[kALo] = 0;
-      c.hoff[kAHi] = 128 * p.lda * 2;
-      c.hoff[kBLo] = 0;
-      c.hoff[kBHi] = 128 * p.ldb * 2;
     } else {
       const __bf16* a0 = p.A + (size_t)ra * p.lda + cl * 8;
       const __bf16* b0 = p.B + (size_t)rb * p.ldb + cl * 8;
@@ -244,22 +187,6 @@ __global__ void __launch_bounds__(kThreads, 2)
     issue_half3<kBLo, true>(c, 1, 1, T);
     issue_half3<kALo, true>(c, 1, 1, T);
     issue_half3<kBHi, true>(c, 1, 1, T);
-  } else if constexpr (SADDR) {
-    issue_half3<kBLo, false, false, true>(c, 0, 0, T);
-    issue_half3<kALo, false, false, true>(c, 0, 0, T);
-    issue_half3<kBHi, false, false, true>(c, 0, 0, T);
-    issue_half3<kAHi, false, false, true>(c, 0, 0, T);
-    issue_half3<kBLo, false, false, true>(c, 1, 1, T);
-    issue_half3<kALo, false, false, true>(c, 1, 1, T);
-    issue_half3<kBHi, false, false, true>(c, 1, 1, T);
-  } else if constexpr (BUFDMA) {
-    issue_half3<kBLo, false, true>(c, 0, 0, T);
-    issue_half3<kALo, false, true>(c, 0, 0, T);
-    issue_half3<kBHi, false, true>(c, 0, 0, T);
-    issue_half3<kAHi, false, true>(c, 0, 0, T);
-    issue_half3<kBLo, false, true>(c, 1, 1, T);
-    issue_half3<kALo, false, true>(c, 1, 1, T);
-    issue_half3<kBHi, false, true>(c, 1, 1, T);
   } else {
     issue_half<kBLo>(c, 0, 0);
     issue_half<kALo>(c, 0, 0);
@@ -293,8 +220,8 @@ __global__ void __launch_bounds__(kThreads, 2)
     }
   } else {
     for (int t = 0; t < T; t += 2) {
-      tile3<false, PRIO, F8, false, BUFDMA, SADDR>(c, f, acc, t, T);
-      tile3<true, PRIO, F8, false, BUFDMA, SADDR>(c, f, acc, t + 1, T);
+      tile3<false, PRIO, F8>(c, f, acc, t, T);
+      tile3<true, PRIO, F8>(c, f, acc, t + 1, T);
     }
   }
   if constexpr (SPRIO != 0) __builtin_amdgcn_s_setprio(0);
@@ -403,16 +330,6 @@ inline hipError_t launch_gemm_bf16_pp3_knob(const GemmArgs& a, int knob, hipStre
       if (knob == 22) hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, kGroupM, false, kEpiLds>), g, b, 0, s, a);
       break;
     }
-    case 24:  // default build with buffer-DMA pieces (SGPR descriptors, no address VALU)
-      if (a.ldc % 8 || (long long)a.M * a.lda * 2 >= (1ll << 31) || (long long)a.N * a.ldb * 2 >= (1ll << 31))
-        return hipErrorInvalidValue;
-      hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, kGroupM, false, kEpiDefault | kEpiBufDma>), g, b, 0, s, a);
-      break;
-    case 25:  // default build with SGPR-address DMA pieces (glds16_saddr)
-      if (a.ldc % 8 || (long long)a.M * a.lda * 2 >= (1ll << 31) || (long long)a.N * a.ldb * 2 >= (1ll << 31))
-        return hipErrorInvalidValue;
-      hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, kGroupM, false, kEpiDefault | kEpiSaddr>), g, b, 0, s, a);
-      break;
     case 23:  // LDS-staged nontemporal epilogue + GROUP_M 4
       if (a.ldc % 8) return hipErrorInvalidValue;
       hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, 4, false, kEpiLds | kEpiNT>), g, b, 0, s, a);

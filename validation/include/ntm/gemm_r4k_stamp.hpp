@@ -1,5 +1,5 @@
 // DIAGNOSTIC build of the 4-wave one-barrier-per-K-tile kernel ("dma4k",
-// gemm_fp8_r4d.hpp, bf16 operands, DI = 3) with per-step s_memtime stamps, for
+// gemm_w4k.hpp, DI = 3) with per-step s_memtime stamps, for
 // a cycle budget of the step: [row 0 MFMAs] t_a [s_waitcnt lgkmcnt(0) +
 // vmcnt(0)] t_b [s_barrier] t_c [rows 1..7]. Each stamp's value is consumed
 // one step later, after the next barrier's lgkmcnt(0) retired it, so the
@@ -16,12 +16,12 @@
 // over the K loop.
 #pragma once
 
-#include "ntm/gemm_fp8_r4d.hpp"
+#include "ntm/gemm_w4k.hpp"
 
 namespace ntm {
 namespace r4ks {
 
-using namespace ::ntm::fp8r;
+using namespace ::ntm::w4k;
 using ::ntm::gemm::GemmArgs;
 using ::ntm::gemm::raw_barrier;
 
@@ -77,51 +77,19 @@ template <int MODE, bool F8, bool NT>
 __global__ void __launch_bounds__(kThreads, 1) gemm_r4k_stamp_kernel(GemmArgs p,
                                                                      unsigned long long* stamps) {
   __shared__ __attribute__((aligned(16))) char smem[kLds];
-  int tm, tn;
-  ::ntm::gemm::tile_coords<kGroupM>(p.M, p.N, tm, tn);
-  const int m0 = tm * BM, n0 = tn * BN;
-  const int lane = threadIdx.x & 63;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wr = w >> 1, wc = w & 1;
   const unsigned long long ts0 = __builtin_amdgcn_s_memtime();
   const unsigned long long rt0 = __builtin_amdgcn_s_memrealtime();
-
   Ctx c;
-  c.lds = smem;
-  c.rsa = __builtin_amdgcn_make_buffer_rsrc((void*)p.A, (short)0, p.M * p.lda * 2, 0x00020000);
-  c.rsb = __builtin_amdgcn_make_buffer_rsrc((void*)p.B, (short)0, p.N * p.ldb * 2, 0x00020000);
-  {
-    const int r = lane >> 2;
-    const int cl = (lane & 3) ^ (((r >> 3) & 1) << 1);
-    c.voff_a = ((m0 + w * 64 + r) * p.lda + cl * 8) * 2;
-    c.voff_b = ((n0 + w * 64 + r) * p.ldb + cl * 8) * 2;
-    c.rowblk_a = 16 * p.lda * 2;
-    c.rowblk_b = 16 * p.ldb * 2;
-  }
-  {
-    const int fo = (lane & 15) * 64 + ((lane >> 4) ^ ((lane >> 2) & 2)) * 16;
-    c.rd_a = fo + wr * 8 * 2048;
-    c.rd_b = kOp + fo + wc * 8 * 2048;
-  }
+  int m0, n0, lane, w, wr, wc;
+  setup(p, smem, c, m0, n0, lane, w, wr, wc);
   f32x4 acc[8][8];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
   const int T = p.K / 64;
   Frags8 f;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) issue_piece(c, 0, T, 0, w, i);
-#pragma unroll
-  for (int i = 0; i < 16; ++i) issue_piece(c, 1, T, 1, w, i);
-  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-  raw_barrier();
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    read_a(c, f, 0, i);
-    read_b(c, f, 0, i);
-  }
+  prologue(c, f, T, w);
   Stamps s;
   const unsigned long long tl0 = __builtin_amdgcn_s_memtime();
   int t = 0;
@@ -139,9 +107,7 @@ __global__ void __launch_bounds__(kThreads, 1) gemm_r4k_stamp_kernel(GemmArgs p,
   s.bar += s.tc - s.tb;
   const unsigned long long tl1 = __builtin_amdgcn_s_memtime();
   raw_barrier();
-  ::ntm::gemmr::Ctx e;
-  e.lds = smem;
-  ::ntm::gemmr::store_tile<NT>(p, e, acc, m0, n0, w, wr, wc, lane);
+  store_tile<NT>(p, smem, acc, m0, n0, w, wr, wc, lane);
   const unsigned long long ts1 = __builtin_amdgcn_s_memtime();
   const unsigned long long rt1 = __builtin_amdgcn_s_memrealtime();
   if (lane == 0) {
@@ -161,7 +127,7 @@ __global__ void __launch_bounds__(kThreads, 1) gemm_r4k_stamp_kernel(GemmArgs p,
 
 // stamps: (M/256)*(N/256) * 4 waves * kSlots (10) u64. mode + 8: temporal C
 // stores (default nontemporal); mode + 16: e4m3 operands (K, lda, ldb in fp8
-// elements, as launch_gemm_fp8_r4d).
+// elements, as launch_gemm_fp8_w4k).
 template <bool F8, bool NT>
 inline hipError_t launch_stamp(const GemmArgs& a, int mode, unsigned long long* stamps,
                                hipStream_t stream) {

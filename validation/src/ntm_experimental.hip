@@ -7,29 +7,21 @@
 //   1      pingpong8: the first 8-wave 12/4/8/0 LDS-read schedule (gemm_bf16.hpp)
 //   10..13 pingpong8c epilogue knobs: widened / + early row-0 stores /
 //          nontemporal stores / both (gemm_bf16_pp3.hpp launch_gemm_bf16_pp3_knob)
-//   25..27 regstage4 / regstage4b / regstage4c: 4 waves, 128x128 per wave,
-//          register-staged operands, barrier after phase-1 MFMA 40 / 48 / 34
-//          (gemm_bf16_r4.hpp)
-//   38, 39 dma4k / _d3: 4 waves, one K-tile step per barrier, two
-//          K-tile buffers (gemm_fp8_r4d.hpp on bf16)
-//   41, 44 ring4 / ring4ab: 4 waves, one K-tile step per barrier, 5-slot
-//          half-K-tile LDS-DMA ring, K-split / operand-split slots (gemm_r4ring.hpp)
-//   31..36 dma4 / _j24 / _j40 / _pb4 / _d3 / _pb8: 4 waves, 128x128 per wave,
-//          LDS-DMA ring of half-K-tile slots (gemm_bf16_r4d.hpp knobs)
+//   39     dma4k_d3: 4 waves x 128x128, one barrier per K-tile, two K-tile
+//          LDS-DMA buffers (gemm_w4k.hpp; stamp build gemm_r4k_stamp.hpp)
 //   19..21 tile128w4 / tile256x128w4 / tile160w4: the 4-wave (one wave per
 //          SIMD) tile kernels that the wave-specialised ones replaced as
 //          variants 15..17 (gemm_bf16_t128.hpp; profiles/r2_ws)
 // Rejected builds are deleted once measured (git history keeps them: the 4-wave
 // wave128 / wave128d4, the persistent pingpong8p / 8pw, the 32-MFMA-segment
-// pingpong8w / wi / ww, fp8 knobs 6-9 - profiles/r1_pmc2_w4, r1_pp4, r2_fp8ws);
+// pingpong8w / wi / ww, fp8 knobs 6-9 - profiles/r1_pmc2_w4, r1_pp4, r2_fp8ws;
+// round 3's register-staged, half-K-tile-ring, 5-slot-ring and SGPR-DMA
+// builds - profiles/r3_k1);
 // what stays is used by a test or a tool under tools/.
 #include "ntm/gemm_bf16.hpp"
 #include "ntm/gemm_bf16_pp3.hpp"
 #include "ntm/gemm_bf16_pp3_stamp.hpp"
-#include "ntm/gemm_bf16_r4.hpp"
-#include "ntm/gemm_bf16_r4d.hpp"
-#include "ntm/gemm_fp8_r4d.hpp"
-#include "ntm/gemm_r4ring.hpp"
+#include "ntm/gemm_w4k.hpp"
 #include "ntm/gemm_r4k_stamp.hpp"
 #include "ntm/gemm_bf16_t128.hpp"
 #include "ntm/gemm_fp8_diag.hpp"
@@ -70,31 +62,9 @@ NTM_API int ntm_gemm_bf16_experimental(int variant, const void* A, const void* B
     case 19: return (int)ntm::gemmt::launch_gemm_bf16_tile<4>(a, S(stream));
     case 20: return (int)ntm::gemmt::launch_gemm_bf16_tile<8>(a, S(stream));
     case 21: return (int)ntm::gemmt::launch_gemm_bf16_tile<5, 5>(a, S(stream));
-    case 25: return (int)ntm::gemmr::launch_gemm_bf16_r4<40>(a, S(stream));
-    case 26: return (int)ntm::gemmr::launch_gemm_bf16_r4<48>(a, S(stream));
-    case 27: return (int)ntm::gemmr::launch_gemm_bf16_r4<34>(a, S(stream));
-    // timing ablations (wrong results): no loads / no staging / no fragment reads
-    case 28: return (int)ntm::gemmr::launch_gemm_bf16_r4<40, 1>(a, S(stream));
-    case 29: return (int)ntm::gemmr::launch_gemm_bf16_r4<40, 2>(a, S(stream));
-    case 30: return (int)ntm::gemmr::launch_gemm_bf16_r4<40, 3>(a, S(stream));
-    // 4 waves x 128x128, LDS-DMA ring of half-K-tile slots (gemm_bf16_r4d.hpp):
-    // <prefetch distance D, barrier after MFMA JB, DMA pieces before it PB>
-    case 31: return (int)ntm::gemmrd::launch_gemm_bf16_r4d<4, 8, 0>(a, S(stream));
-    case 32: return (int)ntm::gemmrd::launch_gemm_bf16_r4d<4, 24, 0>(a, S(stream));
-    case 33: return (int)ntm::gemmrd::launch_gemm_bf16_r4d<4, 40, 0>(a, S(stream));
-    case 34: return (int)ntm::gemmrd::launch_gemm_bf16_r4d<4, 16, 4>(a, S(stream));
-    case 35: return (int)ntm::gemmrd::launch_gemm_bf16_r4d<3, 8, 0>(a, S(stream));
-    case 36: return (int)ntm::gemmrd::launch_gemm_bf16_r4d<4, 40, 8>(a, S(stream));
-    case 37: return (int)ntm::gemmrd::launch_gemm_bf16_r4d<4, 8, 0, true>(a, S(stream));
-    // 4 waves x 128x128, one K-tile step per barrier, two LDS buffers
-    // (gemm_fp8_r4d.hpp on bf16): DMA piece every 2 / 3 MFMA pairs
-    case 38: return (int)ntm::fp8r::launch_gemm_bf16_r4k<2>(a, S(stream));
-    case 39: return (int)ntm::fp8r::launch_gemm_bf16_r4k<3>(a, S(stream));
-    // 4 waves x 128x128, one barrier per K-tile, 5-slot half-K-tile LDS-DMA
-    // ring (gemm_r4ring.hpp), DMA piece every 3 MFMA pairs: K-split slots
-    // (the two halves of a 128-B line fetched a K-tile apart) / operand-split
-    case 41: return (int)ntm::ring::launch_gemm_bf16_ring4<3>(a, S(stream));
-    case 44: return (int)ntm::ring::launch_gemm_bf16_ring4<3, true>(a, S(stream));
+    // 4 waves x 128x128, one barrier per K-tile, two K-tile LDS-DMA buffers,
+    // a DMA piece every 3 MFMA pairs (gemm_w4k.hpp)
+    case 39: return (int)ntm::w4k::launch_gemm_bf16_w4k<3>(a, S(stream));
     default: return (int)hipErrorInvalidValue;
   }
 }
