@@ -35,7 +35,7 @@ GEMM_VARIANTS = {"default": 0, "pingpong8": 1, "pingpong8b": 4,
                  "pingpong8cwn": 12, "pingpong8cwne": 13, "tile128": 15,
                  "tile256x128": 16, "tile160": 17, "tile256x160": 18, "tile128w4": 19,
                  "tile256x128w4": 20, "tile160w4": 21, "pingpong8cm": 22, "tile160x128": 23,
-                 "tile128x160": 24, "dma4k_d3": 39}
+                 "tile128x160": 24, "dma4k_d3": 39, "pingpong8o": 25}
 
 
 # variants built only into libntm_experimental.so (tests / tools): never selected

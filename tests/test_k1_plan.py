@@ -25,9 +25,12 @@ def k1_plan():
     (4096, 2048, 4096, 4096, "tile256x128", None),
     (3072, 3072, 3072, 3072, "pingpong8c", None),    # whole rounds: 256x256 only
     (4096, 4096, 4096, 4096, "pingpong8c", None),
-    (8192, 8192, 8192, 8192, "pingpong8c", None),
+    (8192, 8192, 8192, 8192, "pingpong8o", None),    # > 256 tiles: the persistent build
+    (4096, 8192, 8192, 4096, "pingpong8o", None),    # 512 tiles
+    (5120, 5120, 256, 5120, "pingpong8o", None),     # 400 tiles, K = 256: the shortest tile
+    (5120, 5120, 128, 5120, "pingpong8c", None),     # K = 128: below the persistent build's K
     (8192, 8192, 8128, 8192, "pingpong8cm", None),   # K % 128 != 0: partial-K build
-    (6144, 6144, 6144, 5376, "pingpong8c", "tile160x128"),  # 3 rounds -> 2 + one of 160x128
+    (6144, 6144, 6144, 5376, "pingpong8o", "tile160x128"),  # 3 rounds -> 2 + one of 160x128
     (4352, 4352, 4352, 3840, "pingpong8c", "tile128"),
     (3200, 3200, 3200, 3200, "pingpong8cm", None),   # one round of masked 256x256 tiles
     (2080, 3844, 256, 512, "tile128", "tile160"),    # N % 8 != 0: mixed small tiles
@@ -38,7 +41,7 @@ def k1_plan():
     (4072, 1240, 3784, 4072, "tile128x160", None),   # 32 x 8 tiles: one full round
     (3000, 3000, 3000, 3000, "pingpong8cm", None),   # one-round tiles stay out of 2-round plans
     (2400, 3200, 3200, 2400, "tile256x128", None),   # 10 x 25 tiles: one round
-    (8200, 8192, 8192, 8192, "pingpong8c", "tile128"),  # 8 ragged rows on masked tiles
+    (8200, 8192, 8192, 8192, "pingpong8o", "tile128"),  # 8 ragged rows on masked tiles
 ])
 def test_plan_matches_cost_model(k1_plan, m, n, k, top, top_variant, rest):
     got = k1_plan(m, n, k)
@@ -52,10 +55,13 @@ def test_plan_matches_cost_model(k1_plan, m, n, k, top, top_variant, rest):
 def test_plan_is_well_formed(k1_plan, m, n, k):
     top, top_variant, rest = k1_plan(m, n, k)
     small = ("tile128", "tile256x128", "tile160", "tile256x160", "tile160x128", "tile128x160")
-    assert 0 < top <= m and top_variant in small + ("pingpong8c", "pingpong8cm")
+    assert 0 < top <= m and top_variant in small + ("pingpong8c", "pingpong8cm", "pingpong8o")
+    if top_variant == "pingpong8o":  # more 256x256 tiles than CUs, else pingpong8c
+        assert (top // 256) * (n // 256) > 256 and k >= 256
     assert rest in small
     tm = {"tile128": 128, "tile256x128": 256, "tile160": 160, "tile256x160": 256,
-          "tile160x128": 160, "tile128x160": 128, "pingpong8c": 256, "pingpong8cm": 256}
+          "tile160x128": 160, "tile128x160": 128, "pingpong8c": 256, "pingpong8cm": 256,
+          "pingpong8o": 256}
     masked = ("tile128", "tile256x128", "tile160", "tile160x128", "tile128x160", "pingpong8cm")
     assert top % tm[top_variant] == 0 or (top == m and top_variant in masked)
     if top < m:

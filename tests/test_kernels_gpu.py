@@ -705,3 +705,35 @@ def test_fp8_dma4_vs_torch_fp32(ops, knob, m, n, k):
     atol, rtol = ops.gemm_tolerance(k)
     assert ((ck.float() - ref).abs() <= atol + rtol * ref.abs()).all()
     assert torch.equal(ck.view(torch.int16), ops.gemm_fp8(a, b).view(torch.int16))
+
+
+@pytest.mark.parametrize("m,n,k", [(256, 256, 256), (1024, 512, 1024), (4608, 4608, 512),
+                                   (8192, 8192, 256), (2304, 1792, 768)])
+def test_persistent_overlap_vs_torch_fp32(ops, m, n, k):
+    """pingpong8o, the persistent pingpong8c whose C stores overlap the next
+    tile's K loop (gemm_bf16_pp6.hpp): 1 to 4 tiles per workgroup (4608^2: 324
+    tiles on 256 workgroups, so both one- and two-tile workgroups), the
+    shortest tile (K = 256, T = 4) included; vs fp32, and bitwise equal to
+    pingpong8c (each accumulator sees the same MFMAs in the same K order)."""
+    a = _rand(ops, (m, k), 601 + k)
+    b = _rand(ops, (n, k), 603 + n)
+    c = ops.gemm_bf16(a, b, variant="pingpong8o")
+    ref = a.float() @ b.float().T
+    atol, rtol = ops.gemm_tolerance(k)
+    err = (c.float() - ref).abs()
+    assert torch.all(err <= atol + rtol * ref.abs()), float(err.max())
+    assert torch.equal(c, ops.gemm_bf16(a, b, variant="pingpong8c"))
+
+
+def test_default_runs_persistent_build_past_one_round(ops):
+    """The default plan puts a multi-round 256x256 part on pingpong8o: same
+    bytes as pingpong8c; strided ldc (% 8 != 0) falls back to pingpong8c."""
+    m, n, k = 5120, 5120, 256
+    a = _rand(ops, (m, k), 621)
+    b = _rand(ops, (n, k), 623)
+    assert ops.k1_plan(m, n, k) == (m, "pingpong8o", "tile128")
+    ref = ops.gemm_bf16(a, b, variant="pingpong8c")
+    assert torch.equal(ops.gemm_bf16(a, b), ref)
+    out = torch.zeros((m, n + 4), dtype=torch.bfloat16, device="cuda")
+    ops.gemm_bf16(a, b, out[:, :n], variant="pingpong8o")
+    assert torch.equal(out[:, :n], ref)

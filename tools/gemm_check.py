@@ -1,6 +1,6 @@
 """K1 numerics + throughput check on one MI355X (developer tool).
 
-    python tools/gemm_check.py [--sizes 4096,8192] [--iters 50] [--variants default,dma4k_d3]
+    python tools/gemm_check.py [--sizes 4096,8192,6144x6144x8192] [--iters 50] [--variants default,dma4k_d3]
 
 For every size: full verification of each variant against the independent
 fp32 reference kernel, then interleaved timing rounds of every variant and of
@@ -41,15 +41,15 @@ def main() -> int:
     variants = args.variants.split(",")
     dev = torch.device("cuda:0")
     print(json.dumps({"device": torch.cuda.get_device_name(0), "lib": ops.version()}), flush=True)
-    for s in [int(x) for x in args.sizes.split(",")]:
-        m = n = k = s
+    for s in args.sizes.split(","):
+        m, n, k = (int(x) for x in s.split("x")) if "x" in s else (int(s),) * 3
         a = torch.empty((m, k), dtype=torch.bfloat16, device=dev)
         b = torch.empty((n, k), dtype=torch.bfloat16, device=dev)
         ops.fill_uniform_(a, seed=1)
         ops.fill_uniform_(b, seed=2)
         atol, rtol = ops.gemm_tolerance(k)
         ref = ops.ref_gemm_f32(a, b)
-        res = {"size": s}
+        res = {"size": int(s) if "x" not in s else s}
         cc = torch.empty((m, n), dtype=torch.bfloat16, device=dev)
         for v in variants:
             cc.fill_(float("nan"))

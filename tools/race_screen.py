@@ -36,6 +36,10 @@ MASKED = ("tile128", "tile256x128", "tile160", "tile160x128", "tile128x160", "pi
           "default")
 # skinny C with a long K: the default dispatch splits K here (k1_splitk_plan)
 SHAPES_SPLITK = [(280, 6352, 7568), (128, 8192, 8192), (333, 1004, 2056), (256, 2048, 8200)]
+# persistent overlap kernel (pingpong8o*, K >= 256): 1-4 tiles per workgroup,
+# one- and two-tile workgroups mixed (4608^2), the shortest tile (K = 256)
+SHAPES_PERSIST = [(256, 256, 256), (1024, 512, 1024), (4608, 4608, 512), (8192, 8192, 256),
+                  (6144, 6144, 2048), (2304, 1792, 768), (8192, 8192, 8192)]
 SHAPES_FP8 = [(256, 256, 256), (256, 512, 512), (512, 768, 768), (2304, 1536, 1280),
               (4096, 4352, 1024), (4096, 4096, 4096), (8192, 8192, 8192)]
 
@@ -66,6 +70,8 @@ def main():
 
         tm, tn = ops.kernels.TILE_SHAPES.get(v, (0, 0))
         shapes = SHAPES_FP8 + SHAPES_RAGGED if fp8 else SHAPES_160 if tn == 160 else SHAPES
+        if v.startswith("pingpong8o"):
+            shapes = SHAPES_PERSIST
         if splits > 1:
             shapes = SHAPES_SPLITK + SHAPES_RAGGED
         elif v in MASKED:

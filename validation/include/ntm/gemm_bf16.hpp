@@ -408,7 +408,18 @@ __device__ __forceinline__ void store_tile_wide(const GemmArgs& p, const Ctx& c,
 // orders every wave's last fragment read and DMA before the overwrite.
 constexpr int kStagePitch = 528;
 
-template <bool kRowSum, bool NT, bool MASK = false>
+// 16-byte C store: POL 0 plain, 1 nontemporal. (Write-through sc1 / nt sc1 /
+// sc0 sc1 forms in asm were measured in round 3 and lost 0-3.5 % at 8192^3:
+// profiles/r3_k1o/sc1_epilogue.log.)
+template <int POL>
+__device__ __forceinline__ void store_c16(void* dst, const unsigned __attribute__((ext_vector_type(4))) & v) {
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  static_assert(POL == 0 || POL == 1, "store policy");
+  if constexpr (POL == 0) *(u32x4*)dst = v;
+  if constexpr (POL == 1) __builtin_nontemporal_store(v, (u32x4*)dst);
+}
+
+template <bool kRowSum, bool NT, bool MASK = false, int POL = NT ? 1 : 0>
 __device__ __forceinline__ void store_tile_lds(const GemmArgs& p, const Ctx& c,
                                                const f32x4 (&acc)[2][2][4][2],
                                                int m0, int n0, int lane) {
@@ -447,10 +458,7 @@ __device__ __forceinline__ void store_tile_lds(const GemmArgs& p, const Ctx& c,
     if constexpr (MASK) {  // edge tile: rows >= M / 8-column chunks >= N stay unwritten
       if (m0 + row >= p.M || n0 + chunk * 8 >= p.N) continue;
     }
-    if constexpr (NT)
-      __builtin_nontemporal_store(val, dst);
-    else
-      *dst = val;
+    store_c16<POL>(dst, val);
   }
   if constexpr (kRowSum) abft_rowsum(p, c, acc, m0, lane);
 }

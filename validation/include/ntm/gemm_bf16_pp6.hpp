@@ -1,0 +1,354 @@
+// K1 "pingpong8o" (variant 25): persistent pingpong8c whose C stores OVERLAP
+// the next tile's K loop. The default plan runs it in place of pingpong8c when
+// the 256x256 part has more tiles than CUs (ntm_validation.hip plan_k1).
+//
+// Why: at 8192^3 every CU runs 4 tiles back to back, and each tile boundary
+// costs ~5 us of wall in the data-parallel kernel (profiles/r2_k1/
+// stamp8192_phase_split.log: prologue 1.5 us, epilogue 2.2-2.5 us, 1.4 us
+// between workgroups), ~3 % of the launch; kfit puts our fixed cost 10 us above
+// hipBLASLt's. The earlier persistent build (pingpong8p, round 1, deleted) kept
+// the LDS-DMA pipeline running across tiles but drained it with vmcnt(0) and
+// then stored the whole tile at the boundary, so every CU still stalled there
+// at the same moment: no gain (profiles/r1_pp4).
+//
+// Here nothing drains at a boundary. The four 64x32 accumulator quadrants of a
+// wave finish one phase apart in the last K-tile (P0: acc[0][0], P1: acc[0][1],
+// P2: acc[1][1], P3: acc[1][0]), and each is first rewritten one phase later in
+// the next tile's first K-tile. So quadrant q is converted to bf16 and stored
+// from registers (4 dwordx4 stores per lane, widened layout of store_tile_wide)
+// in the LOAD segment of the phase after its last MFMA - where the partner wave
+// row runs its MFMAs (ping-pong) - and the next tile's first MFMA on it starts
+// from a zero C operand instead of a zeroing pass:
+//   P1(T-1): q0   P2(T-1): q1   P3(T-1): q2   P0(0 of the next tile): q3
+// The LDS-DMA stream is the uniform one of pingpong8c; pieces that pingpong8c
+// pointed past the tile (dummy pieces) stage the next tile's K-tiles 0 / 1, so
+// the next tile's prologue is absorbed too. Only the CU's last tile drains and
+// stores through the LDS-staged epilogue.
+//
+// vmcnt with stores in the stream: loads, stores and LDS-DMA decrement vmcnt in
+// issue order (MI355X_MICROARCH.md, last paragraph of the cycle constants), so
+// a counted wait stays exact if it counts the stores younger than its target.
+// Each phase issues 2 pieces, then waits, then (conversion phases) 4 stores;
+// the wait of phase j retires the pieces of phase j-5 (RAW distance 6, as in
+// pingpong8c), so it is vmcnt(10 + stores issued in phases j-5 .. j-1):
+//   P1(T-1) 10, P2(T-1) 14, P3(T-1) 18, P0(0) 22, P1(0) 26, P2(0) 26, P3(0) 22,
+//   P0(1) 18, P1(1) 14, P2(1) 10.
+// WAR and the reads are pingpong8c's (gemm_bf16_pp2.hpp proof); the stores
+// touch no LDS. Every wave runs the same barrier count per tile.
+//
+// Measured (tools/gemm_check.py, one process, medians of 13 rounds,
+// profiles/r3_k1o/): 8192^3 1634 vs pingpong8c 1622 TF/s (hipBLASLt 1642),
+// 5120^3 1394 vs 1374, 8192x8192x6144 1611 vs 1590; race screen clean.
+// Rejected variants (deleted): sc1 write-through C stores -3.5 %, plain
+// (L2-allocating) stores -2 %, static priority on wave row 1 a tie.
+//
+// Shape rule: M, N % 256, K % 128, K >= 256 (T = K / 64 even and >= 4), no ABFT
+// row sum. Grid = min(tiles, CUs): workgroup b walks tiles b, b + G, ... in the
+// non-persistent kernel's block order, so with G % 8 == 0 each XCD keeps its
+// 32 lock-step tiles and their shared L2 panels.
+#pragma once
+
+#include "ntm/gemm_bf16_pp3.hpp"
+
+namespace ntm {
+namespace gemm6 {
+
+using namespace ::ntm::gemm;
+using ::ntm::gemm3::Frags3;
+using ::ntm::gemm3::kLdsBytes3;
+using ::ntm::gemm3::kScratch;
+
+__host__ __device__ inline bool shape_ok6(int M, int N, int K) {
+  return M > 0 && N > 0 && (M % BM) == 0 && (N % BN) == 0 && (K % (2 * BK)) == 0 && K >= 4 * BK;
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  static_assert(N >= 0 && N <= 63, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// Where the pieces of K-tile kt (counted from the current tile's start) come
+// from: the current tile (NX false), or (NX true, kt >= T) the next tile when
+// there is one (dA / dB = its element offset from this tile) and otherwise an
+// L2-hot in-bounds dummy slice into the scratch region nobody reads.
+template <int H, bool NX>
+__device__ __forceinline__ void issue6(const Ctx& c, int kt, int buf, int T, bool has_next,
+                                       long dA, long dB) {
+  const __bf16* s;
+  int off = buf * kTileBytes + H * kHalfBytes;
+  if constexpr (!NX) {
+    s = c.src[H] + (size_t)kt * BK;
+  } else {
+    const long d = (H == kALo || H == kAHi) ? dA : dB;
+    s = c.src[H] + (has_next ? d + (long)(kt - T) * BK : (long)(T - 1) * BK);
+    off = has_next ? off : kScratch;
+  }
+  char* d = c.lds + off + (2 * c.w) * 1024;
+  glds16(s, d);
+  glds16(s + 32, d + 1024);
+}
+
+// 16 MFMAs of one quadrant (mma_quadrant without the setprio).
+__device__ __forceinline__ void mma_q(f32x4 (&acc)[4][2], const bf16x8 (&a)[4][2],
+                                      const bf16x8 (&b)[2][2]) {
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt)
+        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[nt][ks], a[mt][ks], acc[mt][nt], 0, 0, 0);
+}
+
+// One quadrant of the previous tile (origin m0, n0) to C, in store_tile_wide's
+// layout: after a permlane16 swap per dword pair every lane holds 8 consecutive
+// columns. c_lane = the lane's element offset inside the tile (one VGPR).
+template <int MH, int NH, int POL>
+__device__ __forceinline__ void store_quadrant(const GemmArgs& p, const f32x4 (&q)[4][2],
+                                               int m0, int n0, int c_lane) {
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) {
+    const f32x4 v0 = q[mt][0], v1 = q[mt][1];
+    unsigned w0[2], w1[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const auto r = __builtin_amdgcn_permlane16_swap(pack_bf16x2(v0[2 * h], v0[2 * h + 1]),
+                                                      pack_bf16x2(v1[2 * h], v1[2 * h + 1]),
+                                                      false, false);
+      w0[h] = r[0];
+      w1[h] = r[1];
+    }
+    __bf16* tile = p.C + (size_t)(m0 + MH * 128 + mt * 16) * p.ldc + (n0 + NH * 128);
+    store_c16<POL>(tile + c_lane, u32x4{w0[0], w0[1], w1[0], w1[1]});
+  }
+}
+
+// Zero a stored quadrant in place (32 v_mov): an MFMA with an inline-zero C
+// operand instead lets hipcc give the result fresh registers, and the copies
+// back at the loop's back edge spilled.
+__device__ __forceinline__ void zero_quadrant(f32x4 (&q)[4][2]) {
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) q[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+}
+
+struct Edge {
+  int pm0, pn0;   // previous tile's origin (its quadrants leave in K-tile 0)
+  bool prev;      // there is a previous tile (not the CU's first)
+  bool has_next;  // there is a next tile (this tile's quadrants leave in K-tile T-1)
+  long dA, dB;    // next tile's element offsets from this one
+  int m0, n0;     // this tile's origin
+};
+
+// One phase. CONV: quadrant stored in this phase's load segment when ON (-1
+// none; 0..3 = q0..q3 in finishing order; q3 belongs to the previous tile, so
+// its origin is e.pm0 / e.pn0); ON: e.prev (K-tiles 0 / 1) or e.has_next
+// (K-tile T-1); VMC: the counted wait when ON (10 otherwise); NX: this phase's
+// piece is past the tile (issue6). A stored quadrant is zeroed for the next tile.
+template <int P, bool ODD, int CONV, int VMC, bool NX, int POL>
+__device__ __forceinline__ void phase6(const GemmArgs& p, const Ctx& c, Frags3& f,
+                                       f32x4 (&acc)[2][2][4][2], int t, int T, const Edge& e,
+                                       bool on, int c_lane) {
+  bf16x8(&bcur)[2][2] = ODD ? f.b1 : f.b0;
+  bf16x8(&both)[2][2] = ODD ? f.b0 : f.b1;
+  const int cur = t & 1;
+  if constexpr (P == 0) read_a<kALo>(c, f.a, cur);
+  if constexpr (P == 1) read_b<kBHi>(c, both, cur);
+  if constexpr (P == 2) read_a<kAHi>(c, f.a, cur);
+  if constexpr (P == 3) read_b<kBLo>(c, both, cur ^ 1);  // K-tile t+1 (next tile's 0 at t = T-1)
+  if constexpr (P == 0) issue6<kAHi, NX>(c, t + 1, cur ^ 1, T, e.has_next, e.dA, e.dB);
+  if constexpr (P == 1) issue6<kBLo, NX>(c, t + 2, cur, T, e.has_next, e.dA, e.dB);
+  if constexpr (P == 2) issue6<kALo, NX>(c, t + 2, cur, T, e.has_next, e.dA, e.dB);
+  if constexpr (P == 3) issue6<kBHi, NX>(c, t + 2, cur, T, e.has_next, e.dA, e.dB);
+  if constexpr (VMC == 10) {
+    wait_vm<10>();
+  } else {
+    if (on)
+      wait_vm<VMC>();
+    else
+      wait_vm<10>();
+  }
+  if constexpr (CONV >= 0) {
+    if (on) {
+      constexpr int MH = (CONV == 2 || CONV == 3) ? 1 : 0;
+      constexpr int NH = (CONV == 1 || CONV == 2) ? 1 : 0;
+      store_quadrant<MH, NH, POL>(p, acc[MH][NH], CONV == 3 ? e.pm0 : e.m0,
+                                  CONV == 3 ? e.pn0 : e.n0, c_lane);
+      zero_quadrant(acc[MH][NH]);
+    }
+  }
+  raw_barrier();
+  if constexpr (P == 0) mma_q(acc[0][0], f.a, bcur);
+  if constexpr (P == 1) mma_q(acc[0][1], f.a, both);
+  if constexpr (P == 2) mma_q(acc[1][1], f.a, both);
+  if constexpr (P == 3) mma_q(acc[1][0], f.a, bcur);
+  raw_barrier();
+}
+
+#define NTM_PH(P, ODD, CV, VMC, NX, ON) \
+  phase6<P, ODD, CV, VMC, NX, POL>(p, c, f, acc, t, T, e, ON, c_lane)
+
+__device__ __forceinline__ void tile_origin(const GemmArgs& p, int tile, int ntiles, int& m0,
+                                            int& n0) {
+  int tm, tn;
+  tile_coords_of<kGroupM>(tile, ntiles, p.M, p.N, tm, tn);
+  m0 = tm * BM;
+  n0 = tn * BN;
+}
+
+// POL: C store policy of store_c16 (1 = nontemporal, the shipping build).
+// An fp8 build of this structure did not fit: pingpong8c's fp8 consumer already
+// holds 128 VGPRs + 128 AGPRs, and the boundary conversion spilled 76 VGPRs.
+template <int POL>
+__global__ void __launch_bounds__(kThreads, 2) gemm_bf16_pp6_kernel(GemmArgs p) {
+  __shared__ __attribute__((aligned(16))) char smem[kLdsBytes3];
+  const int ntiles = (p.M / BM) * (p.N / BN);
+  const int G = (int)gridDim.x;
+  int tile = (int)blockIdx.x;
+
+  Ctx c;
+  c.lds = smem;
+  const int lane = threadIdx.x & 63;
+  c.w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  c.wr = c.w >> 2;
+  c.wc = c.w & 3;
+  Edge e;
+  tile_origin(p, tile, ntiles, e.m0, e.n0);
+  {
+    const int r = lane >> 2;
+    const int cl = (lane & 3) ^ (((r >> 3) & 1) << 1);
+    const __bf16* a0 = p.A + (size_t)(e.m0 + c.w * 16 + r) * p.lda + cl * 8;
+    const __bf16* b0 = p.B + (size_t)(e.n0 + c.w * 16 + r) * p.ldb + cl * 8;
+    c.src[kALo] = a0;
+    c.src[kAHi] = a0 + (size_t)128 * p.lda;
+    c.src[kBLo] = b0;
+    c.src[kBHi] = b0 + (size_t)128 * p.ldb;
+  }
+  c.frag_off = (lane & 15) * 64 + ((lane >> 4) ^ ((lane >> 2) & 2)) * 16;
+  const int c_lane = (c.wr * 64 + (lane & 15)) * p.ldc + c.wc * 32 +
+                     ((lane >> 4) & 1) * 16 + (lane >> 5) * 8;
+
+  f32x4 acc[2][2][4][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) zero_quadrant(acc[i][j]);
+  Frags3 f;
+  const int T = p.K / BK;
+  e.prev = false;
+  e.pm0 = e.pn0 = 0;
+  int nm0 = 0, nn0 = 0;
+  e.has_next = tile + G < ntiles;
+  e.dA = e.dB = 0;
+  if (e.has_next) {
+    tile_origin(p, tile + G, ntiles, nm0, nn0);
+    e.dA = (long)(nm0 - e.m0) * p.lda;
+    e.dB = (long)(nn0 - e.n0) * p.ldb;
+  }
+
+  // prologue of the first tile: B-lo0 A-lo0 B-hi0 A-hi0 B-lo1 A-lo1 B-hi1
+  issue_half<kBLo>(c, 0, 0);
+  issue_half<kALo>(c, 0, 0);
+  issue_half<kBHi>(c, 0, 0);
+  issue_half<kAHi>(c, 0, 0);
+  issue_half<kBLo>(c, 1, 1);
+  issue_half<kALo>(c, 1, 1);
+  issue_half<kBHi>(c, 1, 1);
+  wait_vm<10>();
+  raw_barrier();
+  read_b<kBLo>(c, f.b0, 0);
+  if (c.wr == 1) raw_barrier();  // ping-pong stagger
+
+  // One iteration per tile; the only data-dependent control flow is uniform
+  // branches around the boundary stores / waits, so the accumulators keep
+  // their registers around the back edge.
+  for (;;) {
+    int t = 0;
+    // K-tile 0: q3 of the previous tile leaves in P0
+    NTM_PH(0, false, 3, 22, false, e.prev);
+    NTM_PH(1, false, -1, 26, false, e.prev);
+    NTM_PH(2, false, -1, 26, false, e.prev);
+    NTM_PH(3, false, -1, 22, false, e.prev);
+    t = 1;
+    NTM_PH(0, true, -1, 18, false, e.prev);
+    NTM_PH(1, true, -1, 14, false, e.prev);
+    NTM_PH(2, true, -1, 10, false, e.prev);
+    NTM_PH(3, true, -1, 10, false, e.prev);
+#pragma nounroll
+    for (t = 2; t < T - 2; t += 2) {
+      NTM_PH(0, false, -1, 10, false, false);
+      NTM_PH(1, false, -1, 10, false, false);
+      NTM_PH(2, false, -1, 10, false, false);
+      NTM_PH(3, false, -1, 10, false, false);
+      ++t;
+      NTM_PH(0, true, -1, 10, false, false);
+      NTM_PH(1, true, -1, 10, false, false);
+      NTM_PH(2, true, -1, 10, false, false);
+      NTM_PH(3, true, -1, 10, false, false);
+      --t;
+    }
+    // K-tile T-2 stages the next tile's K-tile 0, K-tile T-1 its K-tile 1 (or
+    // dummies); with a next tile, q0..q2 leave in P1..P3 of K-tile T-1
+    t = T - 2;
+    NTM_PH(0, false, -1, 10, false, false);
+    NTM_PH(1, false, -1, 10, true, false);
+    NTM_PH(2, false, -1, 10, true, false);
+    NTM_PH(3, false, -1, 10, true, false);
+    t = T - 1;
+    NTM_PH(0, true, -1, 10, true, false);
+    NTM_PH(1, true, 0, 10, true, e.has_next);
+    NTM_PH(2, true, 1, 14, true, e.has_next);
+    NTM_PH(3, true, 2, 18, true, e.has_next);
+    if (!e.has_next) break;
+    // advance to the next tile
+#pragma unroll
+    for (int h = 0; h < 4; ++h) c.src[h] += (h == kALo || h == kAHi) ? e.dA : e.dB;
+    e.pm0 = e.m0;
+    e.pn0 = e.n0;
+    e.m0 = nm0;
+    e.n0 = nn0;
+    e.prev = true;
+    tile += G;
+    e.has_next = tile + G < ntiles;
+    if (e.has_next) {
+      tile_origin(p, tile + G, ntiles, nm0, nn0);
+      e.dA = (long)(nm0 - e.m0) * p.lda;
+      e.dB = (long)(nn0 - e.n0) * p.ldb;
+    }
+  }
+  if (c.wr == 0) raw_barrier();  // balance the stagger
+  wait_vm<0>();                  // dummy pieces: nothing may land after the WG exits
+  store_tile_lds<false, POL == 1, false, POL>(p, c, acc, e.m0, e.n0, lane);
+}
+#undef NTM_PH
+
+// Grid: one workgroup per CU (LDS allows no more), fewer if there are fewer tiles.
+inline int pp6_grid(int ntiles) {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    hipDeviceProp_t prop;
+    if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess)
+      cus = 256;
+    else
+      cus = prop.multiProcessorCount;
+  }
+  return ntiles < cus ? ntiles : cus;
+}
+
+template <int POL>
+inline hipError_t launch_gemm_bf16_pp6(const GemmArgs& a, hipStream_t stream) {
+  if (!shape_ok6(a.M, a.N, a.K) || a.rowsum || a.lda < a.K || a.ldb < a.K || a.ldc < a.N ||
+      (a.lda % 8) || (a.ldb % 8) || (a.ldc % 8))
+    return hipErrorInvalidValue;
+  const int ntiles = (a.M / BM) * (a.N / BN);
+  hipLaunchKernelGGL((gemm_bf16_pp6_kernel<POL>), dim3((unsigned)pp6_grid(ntiles)),
+                     dim3(kThreads), 0, stream, a);
+  return hipGetLastError();
+}
+
+}  // namespace gemm6
+}  // namespace ntm

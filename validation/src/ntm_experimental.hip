@@ -16,7 +16,8 @@
 // wave128 / wave128d4, the persistent pingpong8p / 8pw, the 32-MFMA-segment
 // pingpong8w / wi / ww, fp8 knobs 6-9 - profiles/r1_pmc2_w4, r1_pp4, r2_fp8ws;
 // round 3's register-staged, half-K-tile-ring, 5-slot-ring and SGPR-DMA
-// builds - profiles/r3_k1);
+// builds - profiles/r3_k1; the overlap kernel's sc1 / plain-store / static-
+// priority builds and pingpong8c's write-through epilogues - profiles/r3_k1o);
 // what stays is used by a test or a tool under tools/.
 #include "ntm/gemm_bf16.hpp"
 #include "ntm/gemm_bf16_pp3.hpp"

@@ -13,6 +13,7 @@
 #include "ntm/aux_kernels.hpp"
 #include "ntm/gemm_bf16_pp2.hpp"
 #include "ntm/gemm_bf16_pp3.hpp"
+#include "ntm/gemm_bf16_pp6.hpp"
 #include "ntm/gemm_bf16_t128.hpp"
 #include "ntm/gemm_fp8.hpp"
 
@@ -54,7 +55,14 @@ NTM_API int ntm_gemm_shape_ok(int M, int N, int K) {
 // vs hipBLASLt 1632-1648, 4096^3 1536 vs 1532-1544 (same processes).
 // Variants 4 and 5 pass tools/race_screen.py (bitwise-stable under HBM noise).
 // Default: 5 when K % 128 == 0, else 4 (both need K % 64 == 0, K >= 128).
+// 25 = pingpong8o, the persistent build of 5 whose C stores overlap the next
+// tile's K loop (gemm_bf16_pp6.hpp): the plan runs it in place of 5 when the
+// 256x256 part has more tiles than CUs (a CU then crosses a tile boundary) and
+// K >= 256. Measured in one process against 5 (tools/gemm_check.py, medians of
+// 13 rounds, profiles/r3_k1o/): 8192^3 1634 vs 1622 TF/s (+0.8 %), 5120^3
+// 1394 vs 1374 (+1.5 %), 8192x8192x6144 1611 vs 1590 (+1.3 %).
 constexpr int kDefaultVariant = 5;
+constexpr int kPersistentVariant = 25;
 
 // Tile-shape plan of the default dispatch: the smallest predicted time
 // rounds(tiles) x tile_area / efficiency over 256 CUs, where the efficiencies
@@ -192,6 +200,10 @@ inline K1Plan plan_k1(int M, int N, int K, bool splitk = false, bool fp8 = false
       }
     }
   }
+  // whole 256x256 tiles over more than one round: the persistent build
+  if (!fp8 && best.feasible() && best.top_variant == kDefaultVariant && K >= 256 &&
+      (double)(best.top_rows / 256) * (N / 256) > kCUs)
+    best.top_variant = kPersistentVariant;
   if (!splitk || !best.feasible()) return best;
   // Split-K: C too small to fill 256 CUs with a long K (e.g. 280x6352x7568: 80
   // tiles of 160x160 -> 3 slices of 240 tiles, 631 vs 321 TF/s unsplit).
@@ -273,6 +285,12 @@ NTM_API int ntm_gemm_bf16_variant(int variant, const void* A, const void* B,
   switch (variant) {
     case 4: return (int)ntm::gemm2::launch_gemm_bf16_pp2(a, S(stream));
     case 5: return (int)ntm::gemm3::launch_gemm_bf16_pp3(a, S(stream));
+    // persistent pingpong8c with overlapped C stores (needs lda / ldb / ldc % 8,
+    // K >= 256; otherwise the same tiles on pingpong8c)
+    case 25:
+      if (!ntm::gemm6::shape_ok6(M, N, K) || (lda % 8) || (ldb % 8) || (ldc % 8))
+        return (int)ntm::gemm3::launch_gemm_bf16_pp3(a, S(stream));
+      return (int)ntm::gemm6::launch_gemm_bf16_pp6<1>(a, S(stream));
     // gemm_bf16_t128.hpp: 128x128 / 256x128 / 160x160 tiles on the wave-specialised
     // kernel (4 DMA-producer + 4 MFMA-consumer waves), 256x160 on the 4-wave one
     case 15: return (int)ntm::gemmt::launch_gemm_bf16_tile_ws<4>(a, S(stream));
