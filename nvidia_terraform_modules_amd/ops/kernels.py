@@ -35,14 +35,16 @@ GEMM_VARIANTS = {"default": 0, "pingpong8": 1, "pingpong8b": 4,
                  "pingpong8cwn": 12, "pingpong8cwne": 13, "tile128": 15,
                  "tile256x128": 16, "tile160": 17, "tile256x160": 18, "tile128w4": 19,
                  "tile256x128w4": 20, "tile160w4": 21, "pingpong8cm": 22, "tile160x128": 23,
-                 "tile128x160": 24, "dma4k_d3": 39, "pingpong8o": 25}
+                 "tile128x160": 24, "dma4k_d3": 39, "pingpong8o": 25,
+                 "dma4ko": 40}
 
 
 # variants built only into libntm_experimental.so (tests / tools): never selected
 # by the default dispatch, not present in the shipping library or Job binary
 EXPERIMENTAL_VARIANTS = frozenset({"pingpong8", "pingpong8cw",
                                    "pingpong8cwe", "pingpong8cwn", "pingpong8cwne",
-                                   "tile128w4", "tile256x128w4", "tile160w4", "dma4k_d3"})
+                                   "tile128w4", "tile256x128w4", "tile160w4", "dma4k_d3",
+                                   "dma4ko"})
 
 # (TM, TN) of the 4-wave tile kernels (gemm_bf16_t128.hpp)
 TILE_SHAPES = {"tile128": (128, 128), "tile256x128": (256, 128), "tile160": (160, 160),
@@ -119,7 +121,7 @@ def gemm_bf16(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
     schedule; 8c adds parity-alternating B buffers and a tail-free K loop),
     "pingpong8" (the first 12/4/8/0 schedule), or the experimental
     "dma4k_d3" (4 waves, 128x128 per wave, one barrier per K-tile, LDS-DMA
-    operands) - see validation/include.
+    operands) and its persistent overlap build "dma4ko" - see validation/include.
     ``splits`` > 1 (masked tiles only): split-K into that many K slices, fp32
     partials in a workspace from PyTorch's allocator, then one reduction kernel.
     """

@@ -6,7 +6,8 @@ shape) and, when this PyTorch build supports it on the device, hipBLASLt's
 fp8 GEMM through torch._scaled_mm (unit scales, bf16 out). One JSON line per
 size.
 
-    python tools/gemm_fp8_check.py [--sizes 4096,8192] [--iters 50] [--rounds 7]
+    python tools/gemm_fp8_check.py [--sizes 4096,8192,6144x8192x4096] [--iters 50] [--rounds 7]
+        [--knobs 12,22] [--no-bf16]
 """
 from __future__ import annotations
 
@@ -38,26 +39,30 @@ def main() -> int:
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--knobs", default="", help="comma list of experimental fp8 knobs to time too")
+    ap.add_argument("--no-bf16", action="store_true", help="skip the bf16 K1 / hipBLASLt timings")
     args = ap.parse_args()
     knobs = [int(x) for x in args.knobs.split(",") if x]
     dev = torch.device("cuda:0")
     ok_all = True
-    for s in [int(x) for x in args.sizes.split(",")]:
-        g = torch.Generator(device=dev).manual_seed(s)
-        a = (torch.rand((s, s), generator=g, device=dev) * 2 - 1).to(torch.float8_e4m3fn)
-        b = (torch.rand((s, s), generator=g, device=dev) * 2 - 1).to(torch.float8_e4m3fn)
+    for size in args.sizes.split(","):
+        m, n, k = (int(x) for x in size.split("x")) if "x" in size else (int(size),) * 3
+        s = int(size) if "x" not in size else size
+        g = torch.Generator(device=dev).manual_seed(m * 7 + n * 3 + k)
+        a = (torch.rand((m, k), generator=g, device=dev) * 2 - 1).to(torch.float8_e4m3fn)
+        b = (torch.rand((n, k), generator=g, device=dev) * 2 - 1).to(torch.float8_e4m3fn)
         c = ops.gemm_fp8(a, b)
         ref = a.float() @ b.float().T
-        atol, rtol = ops.gemm_tolerance(s)
+        atol, rtol = ops.gemm_tolerance(k)
         err = (c.float() - ref).abs()
         bad = int((err > atol + rtol * ref.abs()).sum())
         del ref, err
         ok_all &= bad == 0
-        ab = ops.fill_uniform_(torch.empty((s, s), dtype=torch.bfloat16, device=dev), 1)
-        bb = ops.fill_uniform_(torch.empty((s, s), dtype=torch.bfloat16, device=dev), 2)
-        cb = torch.empty((s, s), dtype=torch.bfloat16, device=dev)
-        fns = {"ours_fp8": lambda: ops.gemm_fp8(a, b, c),
-               "ours_bf16": lambda: ops.gemm_bf16(ab, bb, cb)}
+        fns = {"ours_fp8": lambda: ops.gemm_fp8(a, b, c)}
+        if not args.no_bf16:
+            ab = ops.fill_uniform_(torch.empty((m, k), dtype=torch.bfloat16, device=dev), 1)
+            bb = ops.fill_uniform_(torch.empty((n, k), dtype=torch.bfloat16, device=dev), 2)
+            cb = torch.empty((m, n), dtype=torch.bfloat16, device=dev)
+            fns["ours_bf16"] = lambda: ops.gemm_bf16(ab, bb, cb)
         for kn in knobs:
             ck = ops.gemm_fp8(a, b, knob=kn)
             kbad = int(((ck.float() - c.float()).abs() > 1e-2 * (1 + c.float().abs())).sum())
@@ -72,16 +77,17 @@ def main() -> int:
             hb_note = "torch._scaled_mm"
         except Exception as exc:  # not every build/device pairs support e4m3fn
             hb_note = f"unavailable: {type(exc).__name__}: {str(exc)[:120]}"
-        fns["hipblaslt_bf16"] = lambda: torch.matmul(ab, bb.T, out=cb)
+        if not args.no_bf16:
+            fns["hipblaslt_bf16"] = lambda: torch.matmul(ab, bb.T, out=cb)
         times = {k: [] for k in fns}
         for _ in range(args.rounds):
-            for k, fn in fns.items():
-                times[k].append(timed(fn, args.iters))
-        flops = 2.0 * s ** 3
+            for name, fn in fns.items():
+                times[name].append(timed(fn, args.iters))
+        flops = 2.0 * m * n * k
         res = {"size": s, "fp8_bad": bad, "hipblaslt_fp8": hb_note}
-        for k, t in times.items():
+        for name, t in times.items():
             t = sorted(t)
-            res[f"{k}_tflops_med"] = round(flops / t[len(t) // 2] / 1e9, 1)
+            res[f"{name}_tflops_med"] = round(flops / t[len(t) // 2] / 1e9, 1)
         print(json.dumps(res), flush=True)
     return 0 if ok_all else 1
 

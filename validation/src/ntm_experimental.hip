@@ -9,6 +9,8 @@
 //          nontemporal stores / both (gemm_bf16_pp3.hpp launch_gemm_bf16_pp3_knob)
 //   39     dma4k_d3: 4 waves x 128x128, one barrier per K-tile, two K-tile
 //          LDS-DMA buffers (gemm_w4k.hpp; stamp build gemm_r4k_stamp.hpp)
+//   40     dma4ko: dma4k_d3 persistent, C stores overlapping the next tile's
+//          K loop (gemm_w4o.hpp)
 //   19..21 tile128w4 / tile256x128w4 / tile160w4: the 4-wave (one wave per
 //          SIMD) tile kernels that the wave-specialised ones replaced as
 //          variants 15..17 (gemm_bf16_t128.hpp; profiles/r2_ws)
@@ -23,6 +25,7 @@
 #include "ntm/gemm_bf16_pp3.hpp"
 #include "ntm/gemm_bf16_pp3_stamp.hpp"
 #include "ntm/gemm_w4k.hpp"
+#include "ntm/gemm_w4o.hpp"
 #include "ntm/gemm_r4k_stamp.hpp"
 #include "ntm/gemm_bf16_t128.hpp"
 #include "ntm/gemm_fp8_diag.hpp"
@@ -66,6 +69,8 @@ NTM_API int ntm_gemm_bf16_experimental(int variant, const void* A, const void* B
     // 4 waves x 128x128, one barrier per K-tile, two K-tile LDS-DMA buffers,
     // a DMA piece every 3 MFMA pairs (gemm_w4k.hpp)
     case 39: return (int)ntm::w4k::launch_gemm_bf16_w4k<3>(a, S(stream));
+    // dma4k made persistent, C stores overlapping the next tile's K loop (gemm_w4o.hpp)
+    case 40: return (int)ntm::w4o::launch_gemm_bf16_w4o<3>(a, S(stream));
     default: return (int)hipErrorInvalidValue;
   }
 }
