@@ -35,7 +35,7 @@ GEMM_VARIANTS = {"default": 0, "pingpong8": 1, "pingpong8b": 4,
                  "pingpong8cwn": 12, "pingpong8cwne": 13, "tile128": 15,
                  "tile256x128": 16, "tile160": 17, "tile256x160": 18, "tile128w4": 19,
                  "tile256x128w4": 20, "tile160w4": 21, "pingpong8cm": 22, "tile160x128": 23,
-                 "tile128x160": 24, "dma4k_d3": 39, "pingpong8o": 25,
+                 "tile128x160": 24, "tile128x256": 26, "dma4k_d3": 39, "pingpong8o": 25,
                  "dma4ko": 40}
 
 
@@ -49,11 +49,13 @@ EXPERIMENTAL_VARIANTS = frozenset({"pingpong8", "pingpong8cw",
 # (TM, TN) of the 4-wave tile kernels (gemm_bf16_t128.hpp)
 TILE_SHAPES = {"tile128": (128, 128), "tile256x128": (256, 128), "tile160": (160, 160),
                "tile256x160": (256, 160), "tile128w4": (128, 128), "tile256x128w4": (256, 128),
-               "tile160w4": (160, 160), "tile160x128": (160, 128), "tile128x160": (128, 160)}
+               "tile160w4": (160, 160), "tile160x128": (160, 128), "tile128x160": (128, 160),
+               "tile128x256": (128, 256)}
 
 
 # wave-specialised tile kernels: any M, N % 4, K % 8 (edge tiles and the K tail masked)
-MASKED_TILES = frozenset({"tile128", "tile256x128", "tile160", "tile160x128", "tile128x160"})
+MASKED_TILES = frozenset({"tile128", "tile256x128", "tile160", "tile160x128", "tile128x160",
+                          "tile128x256"})
 
 
 def _tile128_shape_ok(m: int, n: int, k: int, tm: int = 128, tn: int = 128,
@@ -191,7 +193,7 @@ def gemm_fp8_shape_ok(m: int, n: int, k: int) -> bool:
 
 # K1-fp8 variants: the 256x256 kernel and the wave-specialised tiles with the fp8 consumer
 FP8_VARIANTS = ("default", "pingpong8c", "pingpong8cm", "tile128", "tile256x128", "tile160", "tile160x128",
-                "tile128x160")
+                "tile128x160", "tile128x256")
 
 
 def k1_fp8_plan(m: int, n: int, k: int) -> tuple[int, str, str]:

@@ -21,8 +21,9 @@ def k1_plan():
     (2560, 2560, 2560, 2560, "tile160", None),       # 256 tiles of 160x160: one full round
     (1920, 1920, 1920, 1920, "tile128", None),
     (256, 160, 128, 256, "tile128", None),           # 4 masked 128x128 tiles beat one 256x160
-    (2816, 2816, 2816, 2816, "tile256x128", None),   # 242 tiles: one round
-    (4096, 2048, 4096, 4096, "tile256x128", None),
+    (2816, 2816, 2816, 2816, "tile128x256", None),   # 242 tiles: one round (128x256 2 % above 256x128)
+    (4096, 2048, 4096, 4096, "tile128x256", None),
+    (4672, 1472, 6696, 4672, "tile128x256", None),   # hipBLASLt's MT128x256 there (r2_tiles)
     (3072, 3072, 3072, 3072, "pingpong8c", None),    # whole rounds: 256x256 only
     (4096, 4096, 4096, 4096, "pingpong8c", None),
     (8192, 8192, 8192, 8192, "pingpong8o", None),    # > 256 tiles: the persistent build
@@ -40,7 +41,8 @@ def k1_plan():
     (5624, 752, 5880, 5624, "tile160x128", None),    # 216 tiles vs 180 of 160x160
     (4072, 1240, 3784, 4072, "tile128x160", None),   # 32 x 8 tiles: one full round
     (3000, 3000, 3000, 3000, "pingpong8cm", None),   # one-round tiles stay out of 2-round plans
-    (2400, 3200, 3200, 2400, "tile256x128", None),   # 10 x 25 tiles: one round
+    (2400, 3200, 3200, 2400, "tile128x256", None),   # 19 x 13 tiles: one round
+    (3200, 5104, 3480, 3200, "tile128x256", None),   # 2 full rounds beat 256x256 + a tile128 rest (+2.4 %)
     (8200, 8192, 8192, 8192, "pingpong8o", "tile128"),  # 8 ragged rows on masked tiles
 ])
 def test_plan_matches_cost_model(k1_plan, m, n, k, top, top_variant, rest):
@@ -54,15 +56,18 @@ def test_plan_matches_cost_model(k1_plan, m, n, k, top, top_variant, rest):
                                    for j in range(1, 33, 5)])
 def test_plan_is_well_formed(k1_plan, m, n, k):
     top, top_variant, rest = k1_plan(m, n, k)
-    small = ("tile128", "tile256x128", "tile160", "tile256x160", "tile160x128", "tile128x160")
+    small = ("tile128", "tile256x128", "tile160", "tile256x160", "tile160x128", "tile128x160",
+             "tile128x256")
     assert 0 < top <= m and top_variant in small + ("pingpong8c", "pingpong8cm", "pingpong8o")
     if top_variant == "pingpong8o":  # more 256x256 tiles than CUs, else pingpong8c
         assert (top // 256) * (n // 256) > 256 and k >= 256
     assert rest in small
     tm = {"tile128": 128, "tile256x128": 256, "tile160": 160, "tile256x160": 256,
-          "tile160x128": 160, "tile128x160": 128, "pingpong8c": 256, "pingpong8cm": 256,
+          "tile160x128": 160, "tile128x160": 128, "tile128x256": 128, "pingpong8c": 256,
+          "pingpong8cm": 256,
           "pingpong8o": 256}
-    masked = ("tile128", "tile256x128", "tile160", "tile160x128", "tile128x160", "pingpong8cm")
+    masked = ("tile128", "tile256x128", "tile160", "tile160x128", "tile128x160", "tile128x256",
+              "pingpong8cm")
     assert top % tm[top_variant] == 0 or (top == m and top_variant in masked)
     if top < m:
         assert (m - top) % tm[rest] == 0 or rest in masked

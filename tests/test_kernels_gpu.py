@@ -372,7 +372,7 @@ def test_gemm_tile128_rejects_bad_shapes(ops):
 
 
 @pytest.mark.parametrize("variant", ["tile128", "tile256x128", "tile160", "tile160x128",
-                                     "tile128x160", "pingpong8cm", "default"])
+                                     "tile128x160", "tile128x256", "pingpong8cm", "default"])
 @pytest.mark.parametrize("m,n,k", [(1000, 1000, 1024), (100, 4096, 256), (1696, 2560, 256),
                                    (2400, 3200, 128), (1, 4, 128), (333, 1004, 384),
                                    (8200, 260, 128), (4000, 4000, 512), (1000, 1000, 1000),
@@ -401,7 +401,7 @@ def test_gemm_masked_edge_tiles(ops, variant, m, n, k):
 
 
 @pytest.mark.parametrize("variant", ["tile128", "tile256x128", "tile160", "tile160x128",
-                                     "tile128x160"])
+                                     "tile128x160", "tile128x256"])
 @pytest.mark.parametrize("splits", [2, 3, 5, 16])
 @pytest.mark.parametrize("m,n,k", [(280, 636, 7568), (100, 4096, 1000), (333, 1004, 2056),
                                    (1, 4, 1032), (256, 512, 8192), (64, 64, 136)])
@@ -524,7 +524,7 @@ def test_gemm_fp8_masked_edge_tiles(ops, m, n, k):
 
 
 @pytest.mark.parametrize("variant", ["tile128", "tile256x128", "tile160", "tile160x128",
-                                     "tile128x160"])
+                                     "tile128x160", "tile128x256"])
 @pytest.mark.parametrize("m,n,k", [(256, 256, 256), (1000, 1000, 1008), (300, 2056, 400),
                                    (640, 520, 2048), (33, 8, 16)])
 def test_gemm_fp8_wave_specialised_tiles(ops, variant, m, n, k):
@@ -569,7 +569,7 @@ def test_gemm_fp8_default_plan(ops, m, n, k, plan):
 
 @pytest.mark.parametrize("variant,splits", [("tile128", 2), ("tile128", 5), ("tile160", 3),
                                             ("tile256x128", 4), ("tile160x128", 2),
-                                            ("tile128x160", 3)])
+                                            ("tile128x160", 3), ("tile128x256", 2)])
 @pytest.mark.parametrize("m,n,k", [(280, 1000, 4112), (128, 256, 2048), (33, 8, 400)])
 def test_gemm_fp8_splitk(ops, variant, splits, m, n, k):
     """K1-fp8 split-K (fp32 partials of the fp8 consumer, one reduction) vs fp32,

@@ -5,6 +5,7 @@ dispatch and hipBLASLt (torch.matmul) on M x N x K shapes; one JSON line each.
 
     python tools/gemm_policy.py --shapes 2048x2048x2048,4096x2048x4096 [--rounds 7]
     python tools/gemm_policy.py --dtype fp8 --random 40   # K1-fp8 default vs hipBLASLt fp8
+    python tools/gemm_policy.py --shapes 4672x1472x6696 --variants tile256x128,tile128x256
 
 --dtype fp8 times the K1-fp8 default dispatch, its 256x256 kernel alone
 ("pingpong8c") and hipBLASLt's fp8 GEMM (torch._scaled_mm, unit scales, bf16
@@ -43,6 +44,9 @@ def main():
     ap.add_argument("--random", type=int, default=0,
                     help="append N random shapes (M, N % 8, K % 8 in [256, 8192], seeded)")
     ap.add_argument("--dtype", default="bf16", choices=("bf16", "fp8"))
+    ap.add_argument("--variants", default="",
+                    help="time exactly these variants (masked tiles on any shape) besides "
+                         "the default and hipBLASLt")
     args = ap.parse_args()
     shapes = [tuple(int(x) for x in sh.split("x")) for sh in args.shapes.split(",") if sh]
     if args.random:
@@ -60,7 +64,10 @@ def main():
         fns = {"default": lambda: ops.gemm_bf16(a, b, c),
                "torch": lambda: torch.matmul(a, b.T, out=c)}
         exact_k = k % 128 == 0
-        if not args.only_default:
+        if args.variants:
+            for v in args.variants.split(","):
+                fns[v] = lambda v=v: ops.gemm_bf16(a, b, c, variant=v)
+        elif not args.only_default:
             if m % 128 == 0 and n % 128 == 0:
                 fns["tile128"] = lambda: ops.gemm_bf16(a, b, c, variant="tile128")
             if m % 256 == 0 and n % 256 == 0 and exact_k:
@@ -92,8 +99,12 @@ def fp8_sweep(shapes, args):
                "pingpong8c": lambda: ops.gemm_fp8(a, b, c, variant="pingpong8c"),
                "hipblaslt": lambda: torch._scaled_mm(a, b.T, scale_a=one, scale_b=one,
                                                      out_dtype=torch.bfloat16)}
-        if not args.only_default:   # every fp8 tile alone (wave-specialised, masked edges)
-            for v in ("tile256x128", "tile160", "tile128", "tile160x128", "tile128x160"):
+        if args.variants:
+            for v in args.variants.split(","):
+                fns[v] = lambda v=v: ops.gemm_fp8(a, b, c, variant=v)
+        elif not args.only_default:   # every fp8 tile alone (wave-specialised, masked edges)
+            for v in ("tile256x128", "tile160", "tile128", "tile160x128", "tile128x160",
+                      "tile128x256"):
                 fns[v] = lambda v=v: ops.gemm_fp8(a, b, c, variant=v)
         t = {name: [] for name in fns}
         for _ in range(args.rounds):

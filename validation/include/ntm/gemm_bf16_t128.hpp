@@ -54,7 +54,8 @@ constexpr int kGroupMT = 8;
 
 template <int MT, int NT = 4>
 struct Cfg {
-  static_assert(MT >= 4 && MT <= 8 && NT >= 4 && NT <= 5, "tile shapes 128..256 x 128..160");
+  static_assert(MT >= 4 && MT <= 8 && NT >= 4 && (NT <= 5 || (MT == 4 && NT == 8)),
+                "tile shapes 128..256 x 128..160, and 128x256");
   static constexpr int TM = 32 * MT;
   static constexpr int TN = 32 * NT;
   static constexpr int kA = TM * TK * 2;             // A bytes of a slot

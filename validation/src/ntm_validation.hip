@@ -83,12 +83,18 @@ constexpr int kPersistentVariant = 25;
 // 1170 TF/s on 8 full rounds (5120x8192x4096 / 8192x5120x4096,
 // profiles/r2_tiles/); they fill a round where the square tiles leave CUs idle
 // (5624x752x5880: 216 tiles of 160x128 vs 180 of 160x160, 677 vs 616 TF/s).
+// 128x256 (round 3, hipBLASLt's MT128x256 on 4672x1472x6696,
+// profiles/r2_tiles/hipblaslt_kernels_stats.csv): 2 % above 256x128 on full
+// rounds (8192x8192x4096 / 4096x8192x4096 / 8192x4096x4096: 1300 / 1289 / 1282
+// vs 1279 / 1258 / 1253 TF/s, profiles/r3_tiles/), so 0.80 against 0.78; it
+// wastes fewer edge rows where M is ragged and N a multiple of 256.
 constexpr double kCUs = 256.0;
 struct SmallTile {
   int variant, tm, tn;
   double eff;
   bool masked;     // wave-specialised kernel: any M, N % 4, K % 8 (edge tiles / K tail masked)
   bool one_round;  // only where its tiles fit in one round of 256 CUs
+  bool splitk;     // a split-K candidate (the split model was fitted without 128x256)
 };
 // 160x128 / 128x160 are one-round tiles: filling a round the square tiles
 // leave part-idle they win 2-16 % (5624x752x5880, 4072x1240x3784, the rest
@@ -96,12 +102,13 @@ struct SmallTile {
 // one partial round, they lost 3-22 % (3000^3, 1344x6216x4848, 1616x6208x6504;
 // profiles/r2_tiles/plan_ab_*.log) - there the big kernel's partial round runs
 // faster per tile than the full-chip rate the model prices.
-constexpr SmallTile kSmallTiles[] = {{15, 128, 128, 0.60, true, false},
-                                     {16, 256, 128, 0.78, true, false},
-                                     {17, 160, 160, 0.72, true, false},
-                                     {23, 160, 128, 0.70, true, true},
-                                     {24, 128, 160, 0.70, true, true},
-                                     {18, 256, 160, 0.61, false, false}};
+constexpr SmallTile kSmallTiles[] = {{15, 128, 128, 0.60, true, false, true},
+                                     {16, 256, 128, 0.78, true, false, true},
+                                     {17, 160, 160, 0.72, true, false, true},
+                                     {23, 160, 128, 0.70, true, true, true},
+                                     {24, 128, 160, 0.70, true, true, true},
+                                     {26, 128, 256, 0.80, true, false, false},
+                                     {18, 256, 160, 0.61, false, false, false}};
 constexpr double kSplitPenalty = 0.25;  // a second launch, in 128x128-tile-round units
 
 struct K1Plan {
@@ -211,7 +218,7 @@ inline K1Plan plan_k1(int M, int N, int K, bool splitk = false, bool fp8 = false
   double best_t = unsplit / kSplitKMargin;
   K1Plan split = best;
   for (const SmallTile& st : kSmallTiles) {
-    if (!st.masked || !small_ok(st, M)) continue;
+    if (!st.masked || !st.splitk || !small_ok(st, M)) continue;
     const double tiles = (double)((M + st.tm - 1) / st.tm) * ((N + st.tn - 1) / st.tn);
     for (int sp = 2; sp <= kMaxSplits; ++sp) {
       const int slices = ntm::gemmt::splitk_slices(K, sp);
@@ -298,6 +305,7 @@ NTM_API int ntm_gemm_bf16_variant(int variant, const void* A, const void* B,
     case 17: return (int)ntm::gemmt::launch_gemm_bf16_tile_ws<5, 5>(a, S(stream));
     case 23: return (int)ntm::gemmt::launch_gemm_bf16_tile_ws<5, 4>(a, S(stream));  // 160x128
     case 24: return (int)ntm::gemmt::launch_gemm_bf16_tile_ws<4, 5>(a, S(stream));  // 128x160
+    case 26: return (int)ntm::gemmt::launch_gemm_bf16_tile_ws<4, 8>(a, S(stream));  // 128x256
     case 18: return (int)ntm::gemmt::launch_gemm_bf16_tile<8, 5>(a, S(stream));
     // 256x256 on ragged C: clamped loads, masked LDS-staged stores
     case 22: return (int)ntm::gemm3::launch_gemm_bf16_pp3_masked(a, S(stream));
@@ -305,7 +313,7 @@ NTM_API int ntm_gemm_bf16_variant(int variant, const void* A, const void* B,
   }
 }
 
-// Split-K on a wave-specialised tile (15-17, 23, 24): `splits` K-slices, fp32 partials
+// Split-K on a wave-specialised tile (15-17, 23, 24, 26): `splits` K-slices, fp32 partials
 // in the caller's workspace ws (ntm_splitk_ws_bytes; stream-ordered, reused once
 // this call's reduction has run), then one reduction kernel writes C.
 NTM_API size_t ntm_splitk_ws_bytes(int M, int N, int K, int splits) {
@@ -336,6 +344,7 @@ NTM_API int ntm_gemm_bf16_splitk(int variant, int splits, const void* A, const v
     case 17: return (int)launch_gemm_bf16_tile_ws_splitk<5, 5>(a, splits, w, S(stream));
     case 23: return (int)launch_gemm_bf16_tile_ws_splitk<5, 4>(a, splits, w, S(stream));
     case 24: return (int)launch_gemm_bf16_tile_ws_splitk<4, 5>(a, splits, w, S(stream));
+    case 26: return (int)launch_gemm_bf16_tile_ws_splitk<4, 8>(a, splits, w, S(stream));
     default: return (int)hipErrorInvalidValue;
   }
 }
@@ -356,7 +365,7 @@ NTM_API int ntm_gemm_bf16_ex(const void* A, const void* B, void* C, int M, int N
 
 // K1-fp8: C (bf16) = A (e4m3) * B (e4m3)^T, fp32 accumulation. Variant 5 / 22:
 // the 256x256 kernel (gemm_fp8.hpp; exact, masked and partial-K builds picked by
-// shape); 15 / 16 / 17 / 23 / 24: the wave-specialised tiles with the fp8
+// shape); 15 / 16 / 17 / 23 / 24 / 26: the wave-specialised tiles with the fp8
 // consumer (gemm_bf16_t128.hpp); 0: the plan (plan_k1 in fp8 mode: tile shape
 // and row split priced exactly as for bf16).
 NTM_API int ntm_gemm_fp8_variant(int variant, const void* A, const void* B, void* C, int M, int N,
@@ -384,6 +393,7 @@ NTM_API int ntm_gemm_fp8_variant(int variant, const void* A, const void* B, void
     case 17: return (int)launch_gemm_fp8_tile_ws<5, 5>(A, B, c, M, N, K, lda, ldb, ldc, S(stream));
     case 23: return (int)launch_gemm_fp8_tile_ws<5, 4>(A, B, c, M, N, K, lda, ldb, ldc, S(stream));
     case 24: return (int)launch_gemm_fp8_tile_ws<4, 5>(A, B, c, M, N, K, lda, ldb, ldc, S(stream));
+    case 26: return (int)launch_gemm_fp8_tile_ws<4, 8>(A, B, c, M, N, K, lda, ldb, ldc, S(stream));
     default: return (int)hipErrorInvalidValue;
   }
 }
@@ -405,7 +415,7 @@ NTM_API int ntm_gemm_fp8(const void* A, const void* B, void* C, int M, int N, in
   return ntm_gemm_fp8_variant(0, A, B, C, M, N, K, lda, ldb, ldc, stream);
 }
 
-// K1-fp8 split-K on a wave-specialised tile (15-17, 23, 24): `splits` slices of
+// K1-fp8 split-K on a wave-specialised tile (15-17, 23, 24, 26): `splits` slices of
 // the K-tile range, fp32 partials in ws (ntm_fp8_splitk_ws_bytes), one reduction.
 NTM_API size_t ntm_fp8_splitk_ws_bytes(int M, int N, int K, int splits) {
   return ntm_splitk_ws_bytes(M, N, K / 2, splits);
@@ -426,6 +436,7 @@ NTM_API int ntm_gemm_fp8_splitk(int variant, int splits, const void* A, const vo
     case 17: return (int)launch_gemm_fp8_tile_ws_splitk<5, 5>(A, B, c, M, N, K, lda, ldb, ldc, splits, w, S(stream));
     case 23: return (int)launch_gemm_fp8_tile_ws_splitk<5, 4>(A, B, c, M, N, K, lda, ldb, ldc, splits, w, S(stream));
     case 24: return (int)launch_gemm_fp8_tile_ws_splitk<4, 5>(A, B, c, M, N, K, lda, ldb, ldc, splits, w, S(stream));
+    case 26: return (int)launch_gemm_fp8_tile_ws_splitk<4, 8>(A, B, c, M, N, K, lda, ldb, ldc, splits, w, S(stream));
     default: return (int)hipErrorInvalidValue;
   }
 }
