@@ -548,7 +548,7 @@ def test_gemm_fp8_wave_specialised_tiles(ops, variant, m, n, k):
 
 @pytest.mark.parametrize("m,n,k,plan", [(4352, 4352, 512, (3840, "pingpong8c", "tile128")),
                                         (4608, 4608, 256, (3584, "pingpong8c", "tile160x128")),
-                                        (2816, 2816, 512, (2816, "tile256x128", "tile256x128")),
+                                        (2816, 2816, 512, (2816, "tile128x256", "tile128x256")),
                                         (1024, 1024, 1024, (1024, "tile128", "tile128"))])
 def test_gemm_fp8_default_plan(ops, m, n, k, plan):
     """K1-fp8's default dispatch runs k1_fp8_plan: row splits (256x256 rounds +

@@ -43,27 +43,31 @@ ALLOWED_K1 = {
     "ntm::gemmt::gemm_bf16_tile_ws_kernel<5, 5, 0, false, false>",
     "ntm::gemmt::gemm_bf16_tile_ws_kernel<5, 4, 0, false, false>",
     "ntm::gemmt::gemm_bf16_tile_ws_kernel<4, 5, 0, false, false>",
+    "ntm::gemmt::gemm_bf16_tile_ws_kernel<4, 8, 0, false, false>",
     # split-K builds of the same tiles (fp32 partials; splitk_reduce_kernel sums them)
     "ntm::gemmt::gemm_bf16_tile_ws_kernel<4, 4, 0, true, false>",
     "ntm::gemmt::gemm_bf16_tile_ws_kernel<8, 4, 0, true, false>",
     "ntm::gemmt::gemm_bf16_tile_ws_kernel<5, 5, 0, true, false>",
     "ntm::gemmt::gemm_bf16_tile_ws_kernel<5, 4, 0, true, false>",
     "ntm::gemmt::gemm_bf16_tile_ws_kernel<4, 5, 0, true, false>",
+    "ntm::gemmt::gemm_bf16_tile_ws_kernel<4, 8, 0, true, false>",
     # K1-fp8 on the same tiles (fp8 consumer)
     "ntm::gemmt::gemm_bf16_tile_ws_kernel<4, 4, 0, false, true>",
     "ntm::gemmt::gemm_bf16_tile_ws_kernel<8, 4, 0, false, true>",
     "ntm::gemmt::gemm_bf16_tile_ws_kernel<5, 5, 0, false, true>",
     "ntm::gemmt::gemm_bf16_tile_ws_kernel<5, 4, 0, false, true>",
     "ntm::gemmt::gemm_bf16_tile_ws_kernel<4, 5, 0, false, true>",
+    "ntm::gemmt::gemm_bf16_tile_ws_kernel<4, 8, 0, false, true>",
     # ... and their split-K builds
     "ntm::gemmt::gemm_bf16_tile_ws_kernel<4, 4, 0, true, true>",
     "ntm::gemmt::gemm_bf16_tile_ws_kernel<8, 4, 0, true, true>",
     "ntm::gemmt::gemm_bf16_tile_ws_kernel<5, 5, 0, true, true>",
     "ntm::gemmt::gemm_bf16_tile_ws_kernel<5, 4, 0, true, true>",
     "ntm::gemmt::gemm_bf16_tile_ws_kernel<4, 5, 0, true, true>",
+    "ntm::gemmt::gemm_bf16_tile_ws_kernel<4, 8, 0, true, true>",
     "ntm::gemmt::gemm_bf16_tile_kernel<8, 5>",
 }
-EXPERIMENTAL_ONLY = ("gemm_w4k_kernel", "gemm_r4k_stamp_kernel",
+EXPERIMENTAL_ONLY = ("gemm_w4k_kernel", "gemm_w4o_kernel", "gemm_r4k_stamp_kernel",
                      "gemm_bf16_pp3_stamp_kernel", "ntm::gemm::gemm_bf16_kernel",
                      "mfma_rate_kernel", "mfma_f8_probe_kernel")
 

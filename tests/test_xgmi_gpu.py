@@ -8,14 +8,18 @@ pytestmark = pytest.mark.gpu
 
 @pytest.mark.parametrize("nranks", [1, 2, 4, 8])
 @pytest.mark.parametrize("one_shot", [False, True])
-def test_simulated_allreduce_matches_fp32_sum(nranks, one_shot):
+@pytest.mark.parametrize("nblk", [16, 32, 64, 128])   # xgmi.TUNE_NBLKS: every swept value
+def test_simulated_allreduce_matches_fp32_sum(nranks, one_shot, nblk):
     from nvidia_terraform_modules_amd import ops
-    from nvidia_terraform_modules_amd.parallel.xgmi import simulate_allreduce
+    from nvidia_terraform_modules_amd.parallel.xgmi import TUNE_NBLKS, simulate_allreduce
 
+    assert nblk in TUNE_NBLKS
+    if nranks * nblk > 1024:
+        pytest.skip("all ranks' blocks must be co-resident on the one GPU")
     count = 8 * nranks * 4096 + 8 * nranks * 3   # uneven per-block slices
     ins = [ops.fill_uniform_(torch.empty(count, dtype=torch.bfloat16, device="cuda"), seed=r + 1)
            for r in range(nranks)]
-    outs, err = simulate_allreduce(ins, nblk=16, one_shot=one_shot)
+    outs, err = simulate_allreduce(ins, nblk=nblk, one_shot=one_shot)
     assert err == 0
     ref = torch.stack([t.float() for t in ins]).sum(0)
     for o in outs:   # every rank holds the full, identical result
@@ -111,6 +115,11 @@ def test_ipc_allreduce_processes(world):
         for r in rep["results"]:
             assert not r["timeout"], rep
             assert r["wrong"] == 0, rep
+        # bench.py's N > 1 C2 knob sweep (xgmi.tune), every co-resident nblk
+        tune = rep["tune"]
+        assert tune["errors"] == 0 and not tune["timed_out"], tune
+        assert {t["nblk"] for t in tune["table"]} == {nb for nb in (16, 32, 64, 128)
+                                                      if nb * world <= 1024}
 
 
 @pytest.mark.parametrize("nranks", [2, 8])

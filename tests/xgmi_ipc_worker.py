@@ -47,7 +47,14 @@ def main():
         results.append({"count": r.count, "wrong": r.errors, "timeout": ar.timed_out(),
                         "path": "bench_sweep", "busbw_GBps": r.busbw_GBps})
     ar.close()
-    print(json.dumps({"rank": env.rank, "results": results}), flush=True)
+    # bench.py's N > 1 knob sweep (nblk x one-shot / two-shot x cutoff), each
+    # point element-checked; on one GPU only the nblk whose blocks of all ranks
+    # are co-resident
+    from nvidia_terraform_modules_amd.parallel.xgmi import TUNE_NBLKS, tune
+    tr = tune(env, sizes=(64 << 10, 1 << 20), nblks=[nb for nb in TUNE_NBLKS if nb * n <= 1024],
+              iters=2, warmup=1)
+    print(json.dumps({"rank": env.rank, "results": results,
+                      "tune": {k: tr[k] for k in ("table", "errors", "timed_out")}}), flush=True)
     shutdown(env)
 
 
