@@ -32,7 +32,7 @@ SHAPES_160 = [(160, 160, 128), (1280, 800, 384), (2560, 1600, 640), (2560, 2560,
 # ragged C for the masked (wave-specialised) tiles and the default dispatch
 SHAPES_RAGGED = [(1000, 1000, 1024), (1696, 2560, 640), (333, 1004, 384), (2400, 3200, 512),
                  (1000, 1000, 1000), (333, 1004, 200)]  # the last two: partial K-tiles
-MASKED = ("tile128", "tile256x128", "tile160", "tile160x128", "tile128x160", "pingpong8cm",
+MASKED = ("tile128", "tile256x128", "tile160", "tile160x128", "tile128x160", "tile128x256", "pingpong8cm",
           "default")
 # skinny C with a long K: the default dispatch splits K here (k1_splitk_plan)
 SHAPES_SPLITK = [(280, 6352, 7568), (128, 8192, 8192), (333, 1004, 2056), (256, 2048, 8200)]
@@ -70,7 +70,7 @@ def main():
 
         tm, tn = ops.kernels.TILE_SHAPES.get(v, (0, 0))
         shapes = SHAPES_FP8 + SHAPES_RAGGED if fp8 else SHAPES_160 if tn == 160 else SHAPES
-        if v.startswith("pingpong8o"):
+        if v.startswith("pingpong8o") or v == "dma4ko":
             shapes = SHAPES_PERSIST
         if splits > 1:
             shapes = SHAPES_SPLITK + SHAPES_RAGGED
