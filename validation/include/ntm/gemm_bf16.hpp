@@ -468,7 +468,8 @@ __device__ __forceinline__ void store_tile_lds(const GemmArgs& p, const Ctx& c,
 // skip rows / column chunks past C (the kernel clamps its loads).
 // kEpiKTail (with kEpiMask): K % 128 != 0 - chunks past K load zeros (a build
 // flag that rides on the EPI mask, like kEpiMask it changes the loads too).
-enum : int { kEpiWide = 1, kEpiNT = 2, kEpiEarly = 4, kEpiLds = 8, kEpiMask = 16, kEpiKTail = 32 };
+enum : int { kEpiWide = 1, kEpiNT = 2, kEpiEarly = 4, kEpiLds = 8, kEpiMask = 16, kEpiKTail = 32,
+             kEpiSkip = 64 };  // kEpiSkip: ablation (experimental library only), C not stored
 
 __device__ __attribute__((aligned(16))) const unsigned kZeroChunk16[4] = {0u, 0u, 0u, 0u};
 
@@ -476,7 +477,12 @@ template <bool kRowSum, int EPI>
 __device__ __forceinline__ void store_tile_epi(const GemmArgs& p, const Ctx& c,
                                                const f32x4 (&acc)[2][2][4][2],
                                                int m0, int n0, int lane) {
-  if constexpr ((EPI & kEpiLds) != 0)
+  if constexpr ((EPI & kEpiSkip) != 0) {
+    // timing ablation: the store happens only for an impossible ldc, so the
+    // accumulators (and every MFMA) stay live but no byte of C leaves
+    if (p.ldc < 0)
+      store_tile_lds<kRowSum, (EPI & kEpiNT) != 0, false>(p, c, acc, m0, n0, lane);
+  } else if constexpr ((EPI & kEpiLds) != 0)
     store_tile_lds<kRowSum, (EPI & kEpiNT) != 0, (EPI & kEpiMask) != 0>(p, c, acc, m0, n0, lane);
   else if constexpr ((EPI & kEpiWide) != 0)
     store_tile_wide<kRowSum, (EPI & kEpiNT) != 0>(p, c, acc, m0, n0, lane);
