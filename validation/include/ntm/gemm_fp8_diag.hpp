@@ -13,6 +13,7 @@
 #include "ntm/gemm_fp8.hpp"
 #include "ntm/gemm_w4k.hpp"
 #include "ntm/gemm_w4o.hpp"
+#include "ntm/gemm_desync.hpp"
 
 namespace ntm {
 namespace fp8 {
@@ -70,6 +71,8 @@ inline hipError_t launch_gemm_fp8_knob(const void* A, const void* B, __bf16* C, 
     case 26: hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, kGroupM, false, kEpiDefault, 0, 3, 8000>), g, b, 0, s, a); break;
     case 27: hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, kGroupM, false, kEpiDefault, 0, 3, 500>), g, b, 0, s, a); break;
     case 28: hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, kGroupM, false, kEpiDefault, 0, 3, 1000>), g, b, 0, s, a); break;
+    // 29: XCD-desynchronised split first tiles, timing only (gemm_desync.hpp)
+    case 29: return ::ntm::gdsync::launch_gemm_desync<3>(a, s);
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
