@@ -23,17 +23,17 @@ EXP = ROOT / "nvidia_terraform_modules_amd" / "ops" / "libntm_experimental.so"
 # (128x128 / 256x128 / 160x160 / 160x128 / 128x160 wave-specialised, also as K1-fp8,
 # 256x160 4-wave).
 ALLOWED_K1 = {
-    "ntm::gemm3::gemm_bf16_pp3_kernel<false, 8, false, 0, 0, 0, 0>",
-    "ntm::gemm3::gemm_bf16_pp3_kernel<false, 8, false, 10, 0, 0, 0>",
-    "ntm::gemm3::gemm_bf16_pp3_kernel<true, 8, false, 0, 0, 0, 0>",
-    "ntm::gemm3::gemm_bf16_pp3_kernel<true, 8, false, 10, 0, 0, 0>",
-    "ntm::gemm3::gemm_bf16_pp3_kernel<false, 8, false, 10, 0, 3, 0>",
-    "ntm::gemm3::gemm_bf16_pp3_kernel<true, 8, false, 10, 0, 3, 0>",   # K1-fp8 + ABFT row sum
-    "ntm::gemm3::gemm_bf16_pp3_kernel<false, 8, false, 26, 0, 0, 0>",  # masked edge tiles
-    "ntm::gemm3::gemm_bf16_pp3_kernel<false, 8, false, 26, 0, 3, 0>",  # K1-fp8, masked
-    "ntm::gemm3::gemm_bf16_pp3_kernel<false, 8, false, 58, 0, 0, 0>",  # masked + partial K
-    "ntm::gemm3::gemm_bf16_pp3_kernel<false, 8, false, 58, 0, 3, 0>",  # K1-fp8, masked + partial K
-    "ntm::gemm6::gemm_bf16_pp6_kernel<1, 0>",  # pingpong8o: > 256 tiles of 256x256
+    "ntm::gemm3::gemm_bf16_pp3_kernel<false, 8, false, 0, 0, 0>",
+    "ntm::gemm3::gemm_bf16_pp3_kernel<false, 8, false, 10, 0, 0>",
+    "ntm::gemm3::gemm_bf16_pp3_kernel<true, 8, false, 0, 0, 0>",
+    "ntm::gemm3::gemm_bf16_pp3_kernel<true, 8, false, 10, 0, 0>",
+    "ntm::gemm3::gemm_bf16_pp3_kernel<false, 8, false, 10, 0, 3>",
+    "ntm::gemm3::gemm_bf16_pp3_kernel<true, 8, false, 10, 0, 3>",   # K1-fp8 + ABFT row sum
+    "ntm::gemm3::gemm_bf16_pp3_kernel<false, 8, false, 26, 0, 0>",  # masked edge tiles
+    "ntm::gemm3::gemm_bf16_pp3_kernel<false, 8, false, 26, 0, 3>",  # K1-fp8, masked
+    "ntm::gemm3::gemm_bf16_pp3_kernel<false, 8, false, 58, 0, 0>",  # masked + partial K
+    "ntm::gemm3::gemm_bf16_pp3_kernel<false, 8, false, 58, 0, 3>",  # K1-fp8, masked + partial K
+    "ntm::gemm6::gemm_bf16_pp6_kernel<1>",  # pingpong8o: > 256 tiles of 256x256
     "ntm::gemm2::gemm_bf16_pp2_kernel<false, 0>",
     "ntm::gemm2::gemm_bf16_pp2_kernel<false, 3>",
     "ntm::gemm2::gemm_bf16_pp2_kernel<true, 0>",

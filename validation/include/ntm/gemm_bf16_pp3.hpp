@@ -114,20 +114,10 @@ __device__ __forceinline__ void tile3(const Ctx& c, Frags3& f,
 // F8 (nonzero): the operands are OCP e4m3 (K1-fp8, gemm_fp8.hpp); p's K / lda /
 // ldb are then counted in bf16-sized pairs of fp8 values (the LDS image is the
 // same); the value is mma_quadrant_f8's MFMA order (1 = default).
-// DLY (experimental, 0 in every shipping build): first-round workgroups of XCD
-// group x = blockIdx & 7 start x * DLY shader cycles late, so the XCDs' tile
-// boundaries - and their C store bursts - no longer coincide.
 template <bool kRowSum, int GROUP_M = kGroupM, bool PRIO = false, int EPI = 0, int SPRIO = 0,
-          int F8 = 0, int DLY = 0>
+          int F8 = 0>
 __global__ void __launch_bounds__(kThreads, 2)
     gemm_bf16_pp3_kernel(GemmArgs p) {
-  if constexpr (DLY > 0) {
-    if (blockIdx.x < 256u) {
-      const unsigned long long wait = (unsigned long long)(blockIdx.x & 7u) * DLY;
-      const unsigned long long t0 = __builtin_amdgcn_s_memtime();
-      while (__builtin_amdgcn_s_memtime() - t0 < wait) __builtin_amdgcn_s_sleep(2);
-    }
-  }
   static_assert(!((EPI & kEpiLds) && (EPI & kEpiEarly)), "LDS staging needs all waves");
   static_assert(!(EPI & kEpiMask) || ((EPI & kEpiLds) && !kRowSum), "masked: LDS epilogue, no ABFT");
   static_assert(!(EPI & kEpiKTail) || (EPI & kEpiMask), "partial K rides on the masked build");
@@ -344,14 +334,6 @@ inline hipError_t launch_gemm_bf16_pp3_knob(const GemmArgs& a, int knob, hipStre
       if (a.ldc % 8) return hipErrorInvalidValue;
       hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, kGroupM, false, kEpiDefault | kEpiSkip>), g, b, 0, s, a);
       break;
-    case 25: case 26: case 27: {  // XCD-staggered start (DLY 2000 / 4000 / 8000 cycles)
-      if (a.ldc % 8) return hipErrorInvalidValue;
-      constexpr int D = kEpiDefault;
-      if (knob == 25) hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, kGroupM, false, D, 0, 0, 2000>), g, b, 0, s, a);
-      if (knob == 26) hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, kGroupM, false, D, 0, 0, 4000>), g, b, 0, s, a);
-      if (knob == 27) hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, kGroupM, false, D, 0, 0, 8000>), g, b, 0, s, a);
-      break;
-    }
     case 23:  // LDS-staged nontemporal epilogue + GROUP_M 4
       if (a.ldc % 8) return hipErrorInvalidValue;
       hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, 4, false, kEpiLds | kEpiNT>), g, b, 0, s, a);

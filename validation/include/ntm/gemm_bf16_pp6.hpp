@@ -202,16 +202,9 @@ __device__ __forceinline__ void tile_origin(const GemmArgs& p, int tile, int nti
 // POL: C store policy of store_c16 (1 = nontemporal, the shipping build).
 // An fp8 build of this structure did not fit: pingpong8c's fp8 consumer already
 // holds 128 VGPRs + 128 AGPRs, and the boundary conversion spilled 76 VGPRs.
-// DLY (experimental, 0 in the shipping build): workgroups of XCD group
-// x = blockIdx & 7 start x * DLY shader cycles late (gemm_bf16_pp3.hpp).
-template <int POL, int DLY = 0>
+template <int POL>
 __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_pp6_kernel(GemmArgs p) {
   __shared__ __attribute__((aligned(16))) char smem[kLdsBytes3];
-  if constexpr (DLY > 0) {
-    const unsigned long long wait = (unsigned long long)(blockIdx.x & 7u) * DLY;
-    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
-    while (__builtin_amdgcn_s_memtime() - t0 < wait) __builtin_amdgcn_s_sleep(2);
-  }
   const int ntiles = (p.M / BM) * (p.N / BN);
   const int G = (int)gridDim.x;
   int tile = (int)blockIdx.x;
@@ -346,13 +339,13 @@ inline int pp6_grid(int ntiles) {
   return ntiles < cus ? ntiles : cus;
 }
 
-template <int POL, int DLY = 0>
+template <int POL>
 inline hipError_t launch_gemm_bf16_pp6(const GemmArgs& a, hipStream_t stream) {
   if (!shape_ok6(a.M, a.N, a.K) || a.rowsum || a.lda < a.K || a.ldb < a.K || a.ldc < a.N ||
       (a.lda % 8) || (a.ldb % 8) || (a.ldc % 8))
     return hipErrorInvalidValue;
   const int ntiles = (a.M / BM) * (a.N / BN);
-  hipLaunchKernelGGL((gemm_bf16_pp6_kernel<POL, DLY>), dim3((unsigned)pp6_grid(ntiles)),
+  hipLaunchKernelGGL((gemm_bf16_pp6_kernel<POL>), dim3((unsigned)pp6_grid(ntiles)),
                      dim3(kThreads), 0, stream, a);
   return hipGetLastError();
 }

@@ -13,7 +13,6 @@
 #include "ntm/gemm_fp8.hpp"
 #include "ntm/gemm_w4k.hpp"
 #include "ntm/gemm_w4o.hpp"
-#include "ntm/gemm_desync.hpp"
 
 namespace ntm {
 namespace fp8 {
@@ -65,14 +64,6 @@ inline hipError_t launch_gemm_fp8_knob(const void* A, const void* B, __bf16* C, 
     case 5: hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, kGroupM, false, kEpiDefault, 0, 1>), g, b, 0, s, a); break;
     // 23: ablation - the default fp8 build with C not stored (timing only, wrong C)
     case 23: hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, kGroupM, false, kEpiDefault | kEpiSkip, 0, 3>), g, b, 0, s, a); break;
-    // 24-26: the default fp8 build with XCD-staggered first-round starts (2000 / 4000 / 8000 cycles)
-    case 24: hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, kGroupM, false, kEpiDefault, 0, 3, 2000>), g, b, 0, s, a); break;
-    case 25: hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, kGroupM, false, kEpiDefault, 0, 3, 4000>), g, b, 0, s, a); break;
-    case 26: hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, kGroupM, false, kEpiDefault, 0, 3, 8000>), g, b, 0, s, a); break;
-    case 27: hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, kGroupM, false, kEpiDefault, 0, 3, 500>), g, b, 0, s, a); break;
-    case 28: hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, kGroupM, false, kEpiDefault, 0, 3, 1000>), g, b, 0, s, a); break;
-    // 29: XCD-desynchronised split first tiles, timing only (gemm_desync.hpp)
-    case 29: return ::ntm::gdsync::launch_gemm_desync<3>(a, s);
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

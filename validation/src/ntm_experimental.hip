@@ -24,8 +24,6 @@
 #include "ntm/gemm_bf16.hpp"
 #include "ntm/gemm_bf16_pp3.hpp"
 #include "ntm/gemm_bf16_pp3_stamp.hpp"
-#include "ntm/gemm_bf16_pp6.hpp"
-#include "ntm/gemm_desync.hpp"
 #include "ntm/gemm_w4k.hpp"
 #include "ntm/gemm_w4o.hpp"
 #include "ntm/gemm_r4k_stamp.hpp"
@@ -73,12 +71,6 @@ NTM_API int ntm_gemm_bf16_experimental(int variant, const void* A, const void* B
     case 39: return (int)ntm::w4k::launch_gemm_bf16_w4k<3>(a, S(stream));
     // dma4k made persistent, C stores overlapping the next tile's K loop (gemm_w4o.hpp)
     case 40: return (int)ntm::w4o::launch_gemm_bf16_w4o<3>(a, S(stream));
-    // pingpong8o with XCD-staggered starts (DLY 500 / 1000 / 2000 cycles per XCD group)
-    case 41: return (int)ntm::gemm6::launch_gemm_bf16_pp6<1, 500>(a, S(stream));
-    case 42: return (int)ntm::gemm6::launch_gemm_bf16_pp6<1, 1000>(a, S(stream));
-    case 43: return (int)ntm::gemm6::launch_gemm_bf16_pp6<1, 2000>(a, S(stream));
-    // XCD-desynchronised split first tiles, timing only (gemm_desync.hpp)
-    case 44: return (int)ntm::gdsync::launch_gemm_desync<0>(a, S(stream));
     default: return (int)hipErrorInvalidValue;
   }
 }
