@@ -175,8 +175,14 @@ __device__ __forceinline__ void phase6(const GemmArgs& p, const Ctx& c, Frags3& 
     if (on) {
       constexpr int MH = (CONV == 2 || CONV == 3) ? 1 : 0;
       constexpr int NH = (CONV == 1 || CONV == 2) ? 1 : 0;
-      store_quadrant<MH, NH, POL>(p, acc[MH][NH], CONV == 3 ? e.pm0 : e.m0,
-                                  CONV == 3 ? e.pn0 : e.n0, c_lane);
+      if constexpr (POL == 2) {  // ablation (experimental library): C not stored
+        if (p.ldc < 0)
+          store_quadrant<MH, NH, 1>(p, acc[MH][NH], CONV == 3 ? e.pm0 : e.m0,
+                                    CONV == 3 ? e.pn0 : e.n0, c_lane);
+      } else {
+        store_quadrant<MH, NH, POL>(p, acc[MH][NH], CONV == 3 ? e.pm0 : e.m0,
+                                    CONV == 3 ? e.pn0 : e.n0, c_lane);
+      }
       zero_quadrant(acc[MH][NH]);
     }
   }
@@ -321,7 +327,8 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_pp6_kernel(GemmArgs p) 
   }
   if (c.wr == 0) raw_barrier();  // balance the stagger
   wait_vm<0>();                  // dummy pieces: nothing may land after the WG exits
-  store_tile_lds<false, POL == 1, false, POL>(p, c, acc, e.m0, e.n0, lane);
+  if (POL != 2 || p.ldc < 0)
+    store_tile_lds<false, POL != 0, false, POL == 0 ? 0 : 1>(p, c, acc, e.m0, e.n0, lane);
 }
 #undef NTM_PH
 
@@ -337,6 +344,18 @@ inline int pp6_grid(int ntiles) {
       cus = prop.multiProcessorCount;
   }
   return ntiles < cus ? ntiles : cus;
+}
+
+// Experimental: an explicit grid (a multiple of 8, at most the tile count) and
+// POL 2 (C not stored) - the store-bandwidth study of profiles/r3_stores.
+template <int POL>
+inline hipError_t launch_gemm_bf16_pp6_grid(const GemmArgs& a, int grid, hipStream_t stream) {
+  if (!shape_ok6(a.M, a.N, a.K) || a.rowsum || a.lda < a.K || a.ldb < a.K || a.ldc < a.N ||
+      (a.lda % 8) || (a.ldb % 8) || (a.ldc % 8) || grid <= 0 || grid % 8 ||
+      grid > (a.M / BM) * (a.N / BN))
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL((gemm_bf16_pp6_kernel<POL>), dim3((unsigned)grid), dim3(kThreads), 0, stream, a);
+  return hipGetLastError();
 }
 
 template <int POL>

@@ -24,6 +24,7 @@
 #include "ntm/gemm_bf16.hpp"
 #include "ntm/gemm_bf16_pp3.hpp"
 #include "ntm/gemm_bf16_pp3_stamp.hpp"
+#include "ntm/gemm_bf16_pp6.hpp"
 #include "ntm/gemm_w4k.hpp"
 #include "ntm/gemm_w4o.hpp"
 #include "ntm/gemm_r4k_stamp.hpp"
@@ -71,6 +72,11 @@ NTM_API int ntm_gemm_bf16_experimental(int variant, const void* A, const void* B
     case 39: return (int)ntm::w4k::launch_gemm_bf16_w4k<3>(a, S(stream));
     // dma4k made persistent, C stores overlapping the next tile's K loop (gemm_w4o.hpp)
     case 40: return (int)ntm::w4o::launch_gemm_bf16_w4o<3>(a, S(stream));
+    // store-bandwidth study (profiles/r3_stores): pingpong8o on 128 workgroups,
+    // and with C not stored on 128 / 256 workgroups
+    case 41: return (int)ntm::gemm6::launch_gemm_bf16_pp6_grid<1>(a, 128, S(stream));
+    case 42: return (int)ntm::gemm6::launch_gemm_bf16_pp6_grid<2>(a, 128, S(stream));
+    case 43: return (int)ntm::gemm6::launch_gemm_bf16_pp6_grid<2>(a, 256, S(stream));
     default: return (int)hipErrorInvalidValue;
   }
 }
