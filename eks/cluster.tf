@@ -251,24 +251,11 @@ module "ebs_csi_irsa_role" {
   }
 }
 
-# State moves for deployments created before the node groups and the EBS CSI
-# add-on left module "eks" (round 2): without them an upgrade would replace
-# both node groups (draining the MI355X nodes) and fail creating an add-on
-# that already exists.
-moved {
-  from = module.eks.module.eks_managed_node_group["gpu_node_pool"]
-  to   = module.gpu_node_pool
-}
-
-moved {
-  from = module.eks.module.eks_managed_node_group["cpu_node_pool"]
-  to   = module.cpu_node_pool
-}
-
-moved {
-  from = module.eks.aws_eks_addon.this["aws-ebs-csi-driver"]
-  to   = aws_eks_addon.ebs_csi
-}
+# Deployments created before the node groups and the EBS CSI add-on left
+# module "eks" (round 2) keep their objects with a one-time `terraform state
+# mv` (eks/README.md "Upgrading"). A `moved` block cannot do it: module "eks"
+# is a registry package, and Terraform rejects moves across module packages
+# at plan time (tfcheck rule moved-cross-package).
 
 # A preinstalled driver can only come from a pinned image: the default lookup
 # (newest Canonical EKS Ubuntu) has no amdgpu, and the stack would then wait

@@ -43,6 +43,14 @@ namespace-order    a namespaced kubernetes_* / helm_release resource in a module
 gpu-toleration     a pod spec (or operator component) placed on the GPU nodes through
                    the GPU node selector does not tolerate the GPU node taint, so it
                    would never schedule and `apply` would wait out validation_timeout
+moved-cross-package a moved/removed address that reaches INSIDE a module call whose source
+                   is not a local path (a registry / git / remote package): Terraform only
+                   moves objects within one module package and rejects the whole
+                   configuration at plan time ("Cross-package move statement")
+moved-from-exists  a moved `from` that is still declared in the configuration ("Moved
+                   object still exists")
+moved-kind         a moved block between a resource and a module call (both ends must be
+                   the same kind)
 fmt                tabs / trailing whitespace (terraform fmt would rewrite)
 """
 from __future__ import annotations
@@ -327,6 +335,7 @@ def analyze(mod: Module, *, strict_unused: bool = True, vendor_lint: bool = True
     out.extend(practice_findings(mod))
     out.extend(namespace_findings(mod))
     out.extend(eks_node_group_findings(mod))
+    out.extend(moved_findings(mod, callee_loader))
     if check_fmt:
         out.extend(fmt_findings(mod.path))
     return out
@@ -546,6 +555,80 @@ def eks_node_group_findings(mod: Module) -> list[Finding]:
                                f"{label}: post_bootstrap_user_data is ignored without a custom "
                                "ami_id and enable_bootstrap_user_data = true - use "
                                "pre_bootstrap_user_data"))
+    return out
+
+
+def _address_steps(t: Traversal) -> list:
+    """A moved/removed address as (kind, value) steps, root included."""
+    return [("attr", t.root)] + list(t.ops)
+
+
+def _cross_package(t: Traversal, mod: Module, loader):
+    """The first module call with a non-local source that `t` reaches inside
+    of (a different module package), or None. The address of a whole call
+    (`module.x`, `module.x["k"]`) stays in the caller's package."""
+    steps = _address_steps(t)
+    cur, i = mod, 0
+    while i + 1 < len(steps) and steps[i] == ("attr", "module") and steps[i + 1][0] == "attr":
+        mc = cur.modules.get(steps[i + 1][1]) if cur is not None else None
+        i += 2
+        if i < len(steps) and steps[i][0] == "index":
+            i += 1
+        if i >= len(steps) or mc is None:
+            return None
+        if not mc.is_local:
+            return mc
+        p = (cur.path / mc.source).resolve()
+        cur = loader(p) if p.is_dir() else None
+    return None
+
+
+def _declared(t: Traversal, mod: Module) -> bool:
+    """A local (this-module) resource or module-call address is declared."""
+    steps = [v for k, v in _address_steps(t) if k == "attr"]
+    if steps[:1] == ["module"]:
+        return len(steps) == 2 and steps[1] in mod.modules
+    if steps[:1] == ["data"]:
+        return len(steps) == 3 and f"data.{steps[1]}.{steps[2]}" in mod.resources
+    return len(steps) == 2 and f"{steps[0]}.{steps[1]}" in mod.resources
+
+
+def _is_module_addr(t: Traversal) -> bool:
+    """The address names a module call (its last named step is module.X)."""
+    names = [v for k, v in _address_steps(t) if k == "attr"]
+    return len(names) >= 2 and names[-2] == "module"
+
+
+def moved_findings(mod: Module, loader=load_module) -> list[Finding]:
+    """moved-cross-package / moved-from-exists / moved-kind (Terraform's own
+    plan-time checks on refactoring blocks, which an offline parser would
+    otherwise pass: round 3 shipped moves out of the registry module "eks")."""
+    from .docs import render
+
+    out = []
+    blocks = [(b, f, "moved", ("from", "to")) for b, f in mod.moved] + \
+             [(b, f, "removed", ("from",)) for b, f in mod.removed]
+    for b, f, kind, keys in blocks:
+        where = f"{f}:{b.line}"
+        ends = {k: b.body.attr(k) for k in keys}
+        for key, t in ends.items():
+            if not isinstance(t, Traversal):
+                continue
+            mc = _cross_package(t, mod, loader)
+            if mc is not None:
+                out.append(Finding("moved-cross-package", "error", where,
+                                   f"{kind} {key} = {render(t)} reaches inside module.{mc.name} "
+                                   f"(source {mc.source!r}), another module package: Terraform "
+                                   "rejects cross-package moves - use `terraform state mv`"))
+        frm, to = ends.get("from"), ends.get("to")
+        if kind == "moved" and isinstance(frm, Traversal) and isinstance(to, Traversal):
+            if _declared(frm, mod):
+                out.append(Finding("moved-from-exists", "error", where,
+                                   f"moved from {render(frm)} is still declared"))
+            if _is_module_addr(frm) != _is_module_addr(to):
+                out.append(Finding("moved-kind", "error", where,
+                                   f"moved {render(frm)} -> {render(to)}: one end is a module "
+                                   "call, the other a resource"))
     return out
 
 

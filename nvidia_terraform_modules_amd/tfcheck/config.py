@@ -118,7 +118,9 @@ class Module:
     required_providers: dict = field(default_factory=dict)  # local name -> {source, version}
     required_version: str | None = None
     checks: list = field(default_factory=list)
-    moved: list = field(default_factory=list)
+    moved: list = field(default_factory=list)            # (Block, file) of moved blocks
+    removed: list = field(default_factory=list)          # (Block, file) of removed blocks
+    imports: list = field(default_factory=list)          # (Block, file) of import blocks
     tfvars: dict = field(default_factory=dict)           # filename -> Body
     errors: list = field(default_factory=list)
 
@@ -200,9 +202,11 @@ def _index(mod: Module, body: Body, fname: str) -> None:
         elif b.type == "check":
             mod.checks.append(b)
         elif b.type == "moved":
-            mod.moved.append(b)
-        elif b.type in ("import", "removed"):
-            pass
+            mod.moved.append((b, fname))
+        elif b.type == "removed":
+            mod.removed.append((b, fname))
+        elif b.type == "import":
+            mod.imports.append((b, fname))
         else:
             mod.errors.append(f"{fname}:{b.line}: unknown top-level block {b.type!r}")
 

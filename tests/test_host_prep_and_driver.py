@@ -121,12 +121,17 @@ def test_eks_iommu_reboot_is_bounded():
     assert "iommu=pt still absent after one reboot" in prep
 
 
-def test_eks_moved_blocks_keep_existing_node_groups():
-    text = (ROOT / "eks" / "cluster.tf").read_text()
+def test_eks_has_no_cross_package_moves_and_documents_the_state_mv():
+    """moves out of the registry module "eks" fail every plan.
+    The rule runs on the real root; the upgrade path is `terraform state mv`."""
+    from nvidia_terraform_modules_amd.tfcheck.analysis import moved_findings
+
+    assert moved_findings(load_module(ROOT / "eks")) == []
+    readme = (ROOT / "eks" / "README.md").read_text()
     for frm, to in (('module.eks.module.eks_managed_node_group["gpu_node_pool"]', "module.gpu_node_pool"),
                     ('module.eks.module.eks_managed_node_group["cpu_node_pool"]', "module.cpu_node_pool"),
                     ('module.eks.aws_eks_addon.this["aws-ebs-csi-driver"]', "aws_eks_addon.ebs_csi")):
-        assert f"from = {frm}\n  to   = {to}" in text
+        assert f"terraform state mv '{frm}' '{to}'" in readme
 
 
 # ------------------------------------------------------- preinstalled driver

@@ -387,3 +387,48 @@ module "optimized_post" {
 ''')
     fs = [f for f in analyze(load_module(tmp_path)) if f.rule == "eks-ignored-input"]
     assert len(fs) == 1 and "module.optimized_post" in fs[0].message
+
+
+def test_moved_rules(tmp_path):
+    """moved-cross-package / moved-from-exists / moved-kind:
+    the round-3 EKS moves out of the registry module "eks" fire; a move of a
+    whole registry call, or into a local child module, does not."""
+    from nvidia_terraform_modules_amd.tfcheck.analysis import moved_findings
+
+    child = tmp_path / "child"
+    child.mkdir()
+    (child / "c.tf").write_text(
+        'module "inner" {\n  source = "terraform-aws-modules/eks/aws"\n}\n'
+        'resource "null_resource" "r" {}\n')
+    (tmp_path / "main.tf").write_text(
+        'module "eks" {\n  source  = "terraform-aws-modules/eks/aws"\n  version = "~> 20.31"\n}\n'
+        'module "local" {\n  source = "./child"\n}\n'
+        'module "ng" {\n  source = "terraform-aws-modules/eks/aws//modules/eks-managed-node-group"\n}\n'
+        'resource "aws_eks_addon" "ebs" {}\n'
+        # bad: inside a registry package
+        'moved {\n  from = module.eks.module.eks_managed_node_group["gpu"]\n  to   = module.ng\n}\n'
+        'moved {\n  from = module.eks.aws_eks_addon.this["ebs"]\n  to   = aws_eks_addon.ebs\n}\n'
+        # bad: through a local child into its registry call
+        'moved {\n  from = module.local.module.inner.aws_iam_role.x\n  to   = aws_eks_addon.ebs\n}\n'
+        # good: whole call rename, and into a local child package
+        'moved {\n  from = module.old_ng\n  to   = module.ng\n}\n'
+        'moved {\n  from = null_resource.r\n  to   = module.local.null_resource.r\n}\n'
+        # bad: from still declared; resource -> module
+        'moved {\n  from = aws_eks_addon.ebs\n  to   = aws_eks_addon.ebs2\n}\n'
+        'moved {\n  from = null_resource.gone\n  to   = module.ng\n}\n'
+        'removed {\n  from = module.eks.aws_kms_key.this\n}\n')
+    fs = moved_findings(load_module(tmp_path))
+    text = (tmp_path / "main.tf").read_text().splitlines()
+
+    def froms(rule):
+        return sorted(text[int(f.where.split(":")[1])].strip() for f in fs if f.rule == rule)
+
+    assert froms("moved-cross-package") == [
+        "from = module.eks.aws_eks_addon.this[\"ebs\"]", "from = module.eks.aws_kms_key.this",
+        "from = module.eks.module.eks_managed_node_group[\"gpu\"]",
+        "from = module.local.module.inner.aws_iam_role.x"], fs
+    assert froms("moved-from-exists") == ["from = aws_eks_addon.ebs"]
+    assert froms("moved-kind") == ["from = null_resource.gone"]
+    # ...and the real roots are clean (test_every_module_is_clean runs it too)
+    for d in _modules(Path(__file__).resolve().parents[1]):
+        assert moved_findings(load_module(d)) == [], d
