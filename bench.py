@@ -272,14 +272,25 @@ def main(argv=None) -> int:
     ms_per_step = elapsed / args.steps * 1e3
     total_tflops = n * wl.flops * args.steps / elapsed / 1e12
     # per-rank view (weak-scaling diagnosis; `value` stays the max-over-ranks
-    # figure): each rank's own TF/s and the shader clock it holds under a dense
-    # MFMA load right after the timed loop (clock_probe_ghz, ~1 ms), so a
-    # power- or thermally-limited GPU is told apart from a slow one
-    clk = None
-    if dev.type == "cuda" and hasattr(backend, "clock_probe_ghz"):
-        clk = backend.clock_probe_ghz(dev)
+    # figure), right after the timed loop, in the power / thermal state it left:
+    # each rank's own TF/s, the clock K1 ITSELF runs at (the shipping pingpong8o
+    # build with start / end clock stamps per workgroup, gemm_clock_ghz; a few
+    # launches on the same operands) and the clock a dense MFMA-only load holds
+    # (clock_probe_ghz, ~1 ms). The two differ: the GEMM also drives LDS and HBM.
+    # A failure is recorded, never raised: every rank must reach the gather.
+    def _probe(name, *a, **kw):
+        fn = getattr(backend, name, None)
+        if dev.type != "cuda" or fn is None:
+            return None
+        try:
+            return fn(*a, **kw)
+        except Exception as e:  # noqa: BLE001 - reported per rank
+            return {"median_GHz": None, "error": f"{type(e).__name__}: {e}"[:200]}
+
+    gclk = _probe("gemm_clock_ghz", wl.a, wl.b, wl.c, steps=min(max(args.steps, 1), 20))
+    clk = _probe("clock_probe_ghz", dev)
     per_rank = dist.all_gather_obj(env, {"tflops": round(wl.flops * args.steps / my_seconds / 1e12, 2),
-                                         "clock": clk})
+                                         "clock": clk, "gemm_clock": gclk})
 
     # ---- after the timed region: verification + context measurements
     extras: dict = {}
@@ -469,7 +480,10 @@ def main(argv=None) -> int:
         "bench_process_to_verified_s": round(_CLOCK.elapsed("gemm_verified"), 3),
         "in_node_phases_s": {k: round(v, 4) for k, v in _CLOCK.durations().items()},
         "per_rank_tflops": [p["tflops"] for p in per_rank],
-        "per_rank_clock_GHz": [p["clock"]["median_GHz"] if p["clock"] else None for p in per_rank],
+        "per_rank_gemm_clock_GHz": [(p["gemm_clock"] or {}).get("median_GHz") for p in per_rank],
+        "per_rank_gemm_clock_p10_GHz": [(p["gemm_clock"] or {}).get("p10_GHz") for p in per_rank],
+        "per_rank_gemm_clock": [p["gemm_clock"] for p in per_rank],
+        "per_rank_clock_GHz": [(p["clock"] or {}).get("median_GHz") for p in per_rank],
         "per_rank_clock_probe": [p["clock"] for p in per_rank],
         "vs_baseline_note": "reference publishes no TFLOP/s or busbw (BASELINE.json published={})",
         **({"rehearsal": True} if args.rehearsal else {}),

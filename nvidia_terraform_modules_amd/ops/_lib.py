@@ -70,6 +70,9 @@ def _declare(lib: ctypes.CDLL) -> None:
         "ntm_verify_bf16": ([c_vp, c_vp, c_size, c_float, c_float, c_vp, c_vp], c_int),
         "ntm_verify_result_bytes": ([], c_int),
         "ntm_clock_probe": ([c_int, c_int, c_vp, c_vp, c_vp], c_int),
+        "ntm_gemm_bf16_clock_grid": ([c_int, c_int], c_int),
+        "ntm_gemm_bf16_clock": ([c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp,
+                                 c_vp], c_int),
         "ntm_stream_copy": ([c_vp, c_vp, c_size, c_vp], c_int),
         "ntm_stream_read": ([c_vp, c_size, c_vp, c_vp], c_int),
         "ntm_stream_copy_ex": ([c_vp, c_vp, c_size, c_int, c_int, c_int, c_vp], c_int),

@@ -36,7 +36,8 @@ GEMM_VARIANTS = {"default": 0, "pingpong8": 1, "pingpong8b": 4,
                  "tile256x128": 16, "tile160": 17, "tile256x160": 18, "tile128w4": 19,
                  "tile256x128w4": 20, "tile160w4": 21, "pingpong8cm": 22, "tile160x128": 23,
                  "tile128x160": 24, "tile128x256": 26, "dma4k_d3": 39, "pingpong8o": 25,
-                 "dma4ko": 40, "pp8o_g128": 41, "pp8o_g128_nostore": 42, "pp8o_nostore": 43}
+                 "dma4ko": 40, "pp8o_g128": 41, "pp8o_g128_nostore": 42, "pp8o_nostore": 43,
+                 "pingpong8ol": 44, "pp8ol_nostore": 45}
 
 
 # variants built only into libntm_experimental.so (tests / tools): never selected
@@ -44,7 +45,8 @@ GEMM_VARIANTS = {"default": 0, "pingpong8": 1, "pingpong8b": 4,
 EXPERIMENTAL_VARIANTS = frozenset({"pingpong8", "pingpong8cw",
                                    "pingpong8cwe", "pingpong8cwn", "pingpong8cwne",
                                    "tile128w4", "tile256x128w4", "tile160w4", "dma4k_d3",
-                                   "dma4ko", "pp8o_g128", "pp8o_g128_nostore", "pp8o_nostore"})
+                                   "dma4ko", "pp8o_g128", "pp8o_g128_nostore", "pp8o_nostore",
+                                   "pingpong8ol", "pp8ol_nostore"})
 
 # (TM, TN) of the 4-wave tile kernels (gemm_bf16_t128.hpp)
 TILE_SHAPES = {"tile128": (128, 128), "tile256x128": (256, 128), "tile160": (160, 160),
@@ -515,8 +517,59 @@ def clock_probe_ghz(device=None, iters: int = 20000, grid: int = 256) -> dict:
     t1.record()
     t1.synchronize()
     v = out.view(-1, 2).double()
-    ghz = (v[:, 0] / v[:, 1] * 0.1)
-    ghz = ghz[torch.isfinite(ghz)]
-    return {"median_GHz": round(float(ghz.median()), 4), "min_GHz": round(float(ghz.min()), 4),
-            "max_GHz": round(float(ghz.max()), 4), "probe_ms": round(t0.elapsed_time(t1), 3),
-            "waves": int(ghz.numel())}
+    res = _ghz_summary(v[:, 0] / v[:, 1] * 0.1)
+    res["probe_ms"] = round(t0.elapsed_time(t1), 3)
+    res["waves"] = res.pop("n")
+    return res
+
+
+def _ghz_summary(ghz: torch.Tensor) -> dict:
+    """median / p10 / min / max of per-wave (or per-workgroup) clocks; None
+    fields when no finite sample is left (a caller in a collective must not
+    raise on one rank)."""
+    ghz = ghz[torch.isfinite(ghz) & (ghz > 0)]
+    if ghz.numel() == 0:
+        return {"median_GHz": None, "p10_GHz": None, "min_GHz": None, "max_GHz": None, "n": 0}
+    q = torch.quantile(ghz, torch.tensor([0.1, 0.5], dtype=ghz.dtype, device=ghz.device))
+    return {"median_GHz": round(float(q[1]), 4), "p10_GHz": round(float(q[0]), 4),
+            "min_GHz": round(float(ghz.min()), 4), "max_GHz": round(float(ghz.max()), 4),
+            "n": int(ghz.numel())}
+
+
+def gemm_clock_ghz(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
+                   steps: int = 1) -> dict:
+    """K1's OWN clock: ``steps`` back-to-back launches of the
+    shipping pingpong8o build with a start / end s_memtime + s_memrealtime
+    stamp per workgroup (gemm_bf16_pp6.hpp STAMP 1; C is the real product).
+    Per workgroup and launch, clock = d(shader cycles) / d(100 MHz ticks);
+    returns median / p10 / min / max GHz over all of them and the wall time of
+    the launches. Needs whole 256x256 tiles, K % 128, K >= 256. The MFMA-only
+    ``clock_probe_ghz`` reads the clock of a different load (no LDS or HBM
+    traffic): under shared power the two can differ by 15-20 %."""
+    _require(a, "a", torch.bfloat16)
+    _require(b, "b", torch.bfloat16)
+    m, k = a.shape
+    n = b.shape[0]
+    grid = lib().ntm_gemm_bf16_clock_grid(m, n)
+    if grid <= 0 or k % 128 or k < 256 or b.shape[1] != k:
+        raise ValueError(f"shape ({m},{n},{k}) not served by the clock build (M, N % 256, K % 128, K >= 256)")
+    if out is None:
+        out = torch.empty((m, n), dtype=torch.bfloat16, device=a.device)
+    _require(out, "out", torch.bfloat16)
+    stamps = torch.zeros((steps, grid, 4), dtype=torch.int64, device=a.device)
+    t0 = torch.cuda.Event(enable_timing=True)
+    t1 = torch.cuda.Event(enable_timing=True)
+    t0.record()
+    for i in range(steps):
+        check(lib().ntm_gemm_bf16_clock(a.data_ptr(), b.data_ptr(), out.data_ptr(), m, n, k,
+                                        a.stride(0), b.stride(0), out.stride(0),
+                                        stamps[i].data_ptr(), stream_handle()),
+              "ntm_gemm_bf16_clock")
+    t1.record()
+    t1.synchronize()
+    v = stamps.view(-1, 4).double()
+    res = _ghz_summary((v[:, 2] - v[:, 0]) / (v[:, 3] - v[:, 1]) * 0.1)
+    res["workgroups"] = res.pop("n")
+    res["ms_per_launch"] = round(t0.elapsed_time(t1) / steps, 4)
+    res["launches"] = steps
+    return res

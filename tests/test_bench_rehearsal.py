@@ -66,11 +66,14 @@ def test_torchrun_launch_one_json_line(nproc):
     job = d["validation_job"]
     assert job["ran"] is False or job["passed"] is False
     assert d["time_to_gpu_ready_in_node_s"] is None
-    # per-rank view of the weak-scaling run: every rank's own TF/s
-    # and its MFMA-load clock (None on the CPU rehearsal)
+    # per-rank view of the weak-scaling run: every rank's own
+    # TF/s, the clock its GEMM ran at and its MFMA-load clock (None on the CPU rehearsal)
     assert len(d["per_rank_tflops"]) == nproc and all(t > 0 for t in d["per_rank_tflops"])
     assert d["per_rank_clock_GHz"] == [None] * nproc
     assert len(d["per_rank_clock_probe"]) == nproc
+    assert d["per_rank_gemm_clock_GHz"] == [None] * nproc
+    assert d["per_rank_gemm_clock_p10_GHz"] == [None] * nproc
+    assert len(d["per_rank_gemm_clock"]) == nproc
     if nproc > 1:
         # C2 knob sweep: blocks per rank x one/two-shot at 4 sizes, best per size and
         # the favoured one-shot cutoff (over torch.distributed here: shape only)
@@ -121,6 +124,11 @@ def test_bench_on_one_gpu_json_contract(tmp_path):
     cmp_ = d["interleaved_compare_rank0"]       # K1 vs hipBLASLt, ABAB rounds
     assert cmp_["rounds"] == len(cmp_["k1_tflops_rounds"]) == len(cmp_["hipblaslt_tflops_rounds"])
     assert cmp_["k1_over_hipblaslt"] > 0.5 and d["prewarm_s"] >= 0.5
+    # the GEMM's own clock (stamped build) and the MFMA-only probe's, both plausible
+    g = d["per_rank_gemm_clock"][0]
+    assert 0.5 < d["per_rank_gemm_clock_GHz"][0] < 3.0, g
+    assert g["p10_GHz"] <= g["median_GHz"] and g["workgroups"] > 0
+    assert 0.5 < d["per_rank_clock_GHz"][0] < 3.0
     job = d["validation_job"]
     assert job["ran"] and job["passed"], job
     assert 0 < d["time_to_gpu_ready_in_node_s"] < 30

@@ -713,22 +713,41 @@ def test_fp8_dma4_vs_torch_fp32(ops, knob, m, n, k):
     assert torch.equal(ck.view(torch.int16), ops.gemm_fp8(a, b).view(torch.int16))
 
 
+@pytest.mark.parametrize("variant", ["pingpong8o", "pingpong8ol"])
 @pytest.mark.parametrize("m,n,k", [(256, 256, 256), (1024, 512, 1024), (4608, 4608, 512),
                                    (8192, 8192, 256), (2304, 1792, 768)])
-def test_persistent_overlap_vs_torch_fp32(ops, m, n, k):
+def test_persistent_overlap_vs_torch_fp32(ops, variant, m, n, k):
     """pingpong8o, the persistent pingpong8c whose C stores overlap the next
-    tile's K loop (gemm_bf16_pp6.hpp): 1 to 4 tiles per workgroup (4608^2: 324
-    tiles on 256 workgroups, so both one- and two-tile workgroups), the
-    shortest tile (K = 256, T = 4) included; vs fp32, and bitwise equal to
-    pingpong8c (each accumulator sees the same MFMAs in the same K order)."""
+    tile's K loop (gemm_bf16_pp6.hpp), and its whole-line C layout build
+    pingpong8ol (B rows restaged so a wave owns 64 adjacent columns): 1 to 4
+    tiles per workgroup (4608^2: 324 tiles on 256 workgroups, so both one- and
+    two-tile workgroups), the shortest tile (K = 256, T = 4) included; vs fp32,
+    and bitwise equal to pingpong8c (each accumulator sees the same MFMAs in
+    the same K order)."""
     a = _rand(ops, (m, k), 601 + k)
     b = _rand(ops, (n, k), 603 + n)
-    c = ops.gemm_bf16(a, b, variant="pingpong8o")
+    c = ops.gemm_bf16(a, b, variant=variant)
     ref = a.float() @ b.float().T
     atol, rtol = ops.gemm_tolerance(k)
     err = (c.float() - ref).abs()
     assert torch.all(err <= atol + rtol * ref.abs()), float(err.max())
     assert torch.equal(c, ops.gemm_bf16(a, b, variant="pingpong8c"))
+
+
+@pytest.mark.parametrize("m,n,k", [(8192, 8192, 1024), (2048, 2048, 256)])
+def test_gemm_clock_build(ops, m, n, k):
+    """The GEMM's own clock: the shipping pingpong8o with a
+    start / end clock stamp per workgroup writes the same C as the default
+    build, and every workgroup reports a plausible shader clock."""
+    a = _rand(ops, (m, k), 631)
+    b = _rand(ops, (n, k), 633)
+    c = torch.empty((m, n), dtype=torch.bfloat16, device="cuda")
+    r = ops.gemm_clock_ghz(a, b, c, steps=3)
+    assert torch.equal(c, ops.gemm_bf16(a, b, variant="pingpong8o"))
+    assert r["launches"] == 3 and r["workgroups"] == 3 * min(256, (m // 256) * (n // 256))
+    assert 0.5 < r["p10_GHz"] <= r["median_GHz"] <= r["max_GHz"] < 3.0, r
+    with pytest.raises(ValueError):
+        ops.gemm_clock_ghz(a[:, :200], b[:, :200])
 
 
 def test_default_runs_persistent_build_past_one_round(ops):

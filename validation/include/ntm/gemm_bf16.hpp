@@ -72,6 +72,8 @@ struct GemmArgs {
   // splitk_ws[s][M][N]; splitk_reduce_kernel sums the slices into C.
   float* splitk_ws = nullptr;
   int splitk_kc = 0;
+  // clock-stamp builds only (gemm_bf16_pp6.hpp STAMP): 4 u64 per workgroup
+  unsigned long long* stamps = nullptr;
 };
 
 // Shapes the fast kernel accepts; the host launcher rejects anything else.
@@ -419,7 +421,10 @@ __device__ __forceinline__ void store_c16(void* dst, const unsigned __attribute_
   if constexpr (POL == 1) __builtin_nontemporal_store(v, (u32x4*)dst);
 }
 
-template <bool kRowSum, bool NT, bool MASK = false, int POL = NT ? 1 : 0>
+// LINE: the quadrant -> column map of pingpong8o's whole-line layout
+// (gemm_bf16_pp6.hpp): wave column wc owns columns 64 wc .. 64 wc + 63, quadrant
+// nh the 32 at 64 wc + 32 nh (default: 32 wc + 128 nh).
+template <bool kRowSum, bool NT, bool MASK = false, int POL = NT ? 1 : 0, bool LINE = false>
 __device__ __forceinline__ void store_tile_lds(const GemmArgs& p, const Ctx& c,
                                                const f32x4 (&acc)[2][2][4][2],
                                                int m0, int n0, int lane) {
@@ -434,7 +439,7 @@ __device__ __forceinline__ void store_tile_lds(const GemmArgs& p, const Ctx& c,
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt) {
         const int row = mh * 128 + c.wr * 64 + mt * 16 + (lane & 15);
-        const int col = nh * 128 + c.wc * 32 + coff;
+        const int col = LINE ? c.wc * 64 + nh * 32 + coff : nh * 128 + c.wc * 32 + coff;
         const f32x4 v0 = acc[mh][nh][mt][0], v1 = acc[mh][nh][mt][1];
         unsigned w0[2], w1[2];
 #pragma unroll

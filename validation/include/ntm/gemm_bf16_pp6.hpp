@@ -104,7 +104,7 @@ __device__ __forceinline__ void mma_q(f32x4 (&acc)[4][2], const bf16x8 (&a)[4][2
 // One quadrant of the previous tile (origin m0, n0) to C, in store_tile_wide's
 // layout: after a permlane16 swap per dword pair every lane holds 8 consecutive
 // columns. c_lane = the lane's element offset inside the tile (one VGPR).
-template <int MH, int NH, int POL>
+template <int MH, int NH, int POL, bool LINE = false>
 __device__ __forceinline__ void store_quadrant(const GemmArgs& p, const f32x4 (&q)[4][2],
                                                int m0, int n0, int c_lane) {
   typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
@@ -120,8 +120,35 @@ __device__ __forceinline__ void store_quadrant(const GemmArgs& p, const f32x4 (&
       w0[h] = r[0];
       w1[h] = r[1];
     }
-    __bf16* tile = p.C + (size_t)(m0 + MH * 128 + mt * 16) * p.ldc + (n0 + NH * 128);
+    __bf16* tile = p.C + (size_t)(m0 + MH * 128 + mt * 16) * p.ldc + (n0 + NH * (LINE ? 32 : 128));
     store_c16<POL>(tile + c_lane, u32x4{w0[0], w0[1], w1[0], w1[1]});
+  }
+}
+
+// LINE layout: both quadrants of row half MH, one 16-row block at a time, so a
+// wave's two adjacent 64-B half-lines of a row leave in consecutive store
+// instructions (a whole 128-B line per row and block).
+template <int MH, int POL>
+__device__ __forceinline__ void store_pair(const GemmArgs& p, const f32x4 (&q)[2][4][2], int m0,
+                                           int n0, int c_lane) {
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) {
+    __bf16* tile = p.C + (size_t)(m0 + MH * 128 + mt * 16) * p.ldc + n0 + c_lane;
+#pragma unroll
+    for (int nh = 0; nh < 2; ++nh) {
+      const f32x4 v0 = q[nh][mt][0], v1 = q[nh][mt][1];
+      unsigned w0[2], w1[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const auto r = __builtin_amdgcn_permlane16_swap(pack_bf16x2(v0[2 * h], v0[2 * h + 1]),
+                                                        pack_bf16x2(v1[2 * h], v1[2 * h + 1]),
+                                                        false, false);
+        w0[h] = r[0];
+        w1[h] = r[1];
+      }
+      store_c16<POL>(tile + nh * 32, u32x4{w0[0], w0[1], w1[0], w1[1]});
+    }
   }
 }
 
@@ -145,10 +172,12 @@ struct Edge {
 
 // One phase. CONV: quadrant stored in this phase's load segment when ON (-1
 // none; 0..3 = q0..q3 in finishing order; q3 belongs to the previous tile, so
-// its origin is e.pm0 / e.pn0); ON: e.prev (K-tiles 0 / 1) or e.has_next
-// (K-tile T-1); VMC: the counted wait when ON (10 otherwise); NX: this phase's
-// piece is past the tile (issue6). A stored quadrant is zeroed for the next tile.
-template <int P, bool ODD, int CONV, int VMC, bool NX, int POL>
+// its origin is e.pm0 / e.pn0; LINE layout: 4 = both quadrants of row half 0 of
+// this tile, 5 = both of row half 1 of the previous tile); ON: e.prev (K-tiles
+// 0 / 1) or e.has_next (K-tile T-1); VMC: the counted wait when ON (10
+// otherwise); NX: this phase's piece is past the tile (issue6). A stored
+// quadrant is zeroed for the next tile.
+template <int P, bool ODD, int CONV, int VMC, bool NX, int POL, bool LINE>
 __device__ __forceinline__ void phase6(const GemmArgs& p, const Ctx& c, Frags3& f,
                                        f32x4 (&acc)[2][2][4][2], int t, int T, const Edge& e,
                                        bool on, int c_lane) {
@@ -171,7 +200,19 @@ __device__ __forceinline__ void phase6(const GemmArgs& p, const Ctx& c, Frags3& 
     else
       wait_vm<10>();
   }
-  if constexpr (CONV >= 0) {
+  if constexpr (CONV >= 4) {
+    if (on) {
+      constexpr int MH = CONV - 4;
+      const int m0 = MH == 1 ? e.pm0 : e.m0, n0 = MH == 1 ? e.pn0 : e.n0;
+      if constexpr (POL == 2) {  // ablation (experimental library): C not stored
+        if (p.ldc < 0) store_pair<MH, 1>(p, acc[MH], m0, n0, c_lane);
+      } else {
+        store_pair<MH, POL>(p, acc[MH], m0, n0, c_lane);
+      }
+      zero_quadrant(acc[MH][0]);
+      zero_quadrant(acc[MH][1]);
+    }
+  } else if constexpr (CONV >= 0) {
     if (on) {
       constexpr int MH = (CONV == 2 || CONV == 3) ? 1 : 0;
       constexpr int NH = (CONV == 1 || CONV == 2) ? 1 : 0;
@@ -195,7 +236,7 @@ __device__ __forceinline__ void phase6(const GemmArgs& p, const Ctx& c, Frags3& 
 }
 
 #define NTM_PH(P, ODD, CV, VMC, NX, ON) \
-  phase6<P, ODD, CV, VMC, NX, POL>(p, c, f, acc, t, T, e, ON, c_lane)
+  phase6<P, ODD, CV, VMC, NX, POL, LINE>(p, c, f, acc, t, T, e, ON, c_lane)
 
 __device__ __forceinline__ void tile_origin(const GemmArgs& p, int tile, int ntiles, int& m0,
                                             int& n0) {
@@ -205,12 +246,40 @@ __device__ __forceinline__ void tile_origin(const GemmArgs& p, int tile, int nti
   n0 = tn * BN;
 }
 
+// Clock stamp (STAMP builds): shader-clock and 100 MHz real-time counters read
+// together, the wait inside the statement (cdna_hip_programming.md §7).
+__device__ __forceinline__ void clock_stamp(unsigned long long& t, unsigned long long& rt) {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_memrealtime %1\n\ts_waitcnt lgkmcnt(0)"
+               : "=s"(t), "=s"(rt)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
 // POL: C store policy of store_c16 (1 = nontemporal, the shipping build).
+// LINE: whole-line C layout. The B-lo / B-hi LDS halves stage B rows
+// n0 + 64 j + [0, 32) / n0 + 64 j + 32 + [0, 32) for row group pair j = 0..3
+// (only each staging wave's global B row changes; the LDS image and every read
+// stay), so wave column wc's two N-quadrants are the adjacent columns
+// 64 wc .. 64 wc + 63 = one 128-B line per row. A row half's two quadrants leave
+// together (store_pair) in the phase after the second of them finished:
+//   P2(T-1): row half 0 of this tile   P0(0 of the next tile): row half 1
+// With 8 stores per lane in each of those phases the counted waits become
+// (vmcnt = 10 + stores issued in phases j-5 .. j-1):
+//   P2(T-1) 10, P3(T-1) 18, P0(0) 18, P1(0) 26, P2(0) 26, P3(0) 26, P0(1) 18,
+//   P1(1) 18, P2(1) 10.
+// Row half 0 is first rewritten in P0 / P1 of the next tile's K-tile 0, row
+// half 1 in P2 / P3, both after their store phase.
+// STAMP 1 (diagnostic build, never in the default dispatch): lane 0 of wave 0
+// records s_memtime / s_memrealtime at kernel start and after the last store
+// into p.stamps[4 * blockIdx.x ..]: the GEMM's own clock = d(memtime) /
+// d(realtime) x 100 MHz.
 // An fp8 build of this structure did not fit: pingpong8c's fp8 consumer already
 // holds 128 VGPRs + 128 AGPRs, and the boundary conversion spilled 76 VGPRs.
-template <int POL>
+template <int POL, bool LINE = false, int STAMP = 0>
 __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_pp6_kernel(GemmArgs p) {
   __shared__ __attribute__((aligned(16))) char smem[kLdsBytes3];
+  unsigned long long t0 = 0, rt0 = 0;
+  if constexpr (STAMP != 0) clock_stamp(t0, rt0);
   const int ntiles = (p.M / BM) * (p.N / BN);
   const int G = (int)gridDim.x;
   int tile = (int)blockIdx.x;
@@ -226,15 +295,16 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_pp6_kernel(GemmArgs p) 
   {
     const int r = lane >> 2;
     const int cl = (lane & 3) ^ (((r >> 3) & 1) << 1);
+    const int rb = LINE ? (c.w >> 1) * 64 + (c.w & 1) * 16 + r : c.w * 16 + r;
     const __bf16* a0 = p.A + (size_t)(e.m0 + c.w * 16 + r) * p.lda + cl * 8;
-    const __bf16* b0 = p.B + (size_t)(e.n0 + c.w * 16 + r) * p.ldb + cl * 8;
+    const __bf16* b0 = p.B + (size_t)(e.n0 + rb) * p.ldb + cl * 8;
     c.src[kALo] = a0;
     c.src[kAHi] = a0 + (size_t)128 * p.lda;
     c.src[kBLo] = b0;
-    c.src[kBHi] = b0 + (size_t)128 * p.ldb;
+    c.src[kBHi] = b0 + (size_t)(LINE ? 32 : 128) * p.ldb;
   }
   c.frag_off = (lane & 15) * 64 + ((lane >> 4) ^ ((lane >> 2) & 2)) * 16;
-  const int c_lane = (c.wr * 64 + (lane & 15)) * p.ldc + c.wc * 32 +
+  const int c_lane = (c.wr * 64 + (lane & 15)) * p.ldc + c.wc * (LINE ? 64 : 32) +
                      ((lane >> 4) & 1) * 16 + (lane >> 5) * 8;
 
   f32x4 acc[2][2][4][2];
@@ -273,14 +343,14 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_pp6_kernel(GemmArgs p) 
   // their registers around the back edge.
   for (;;) {
     int t = 0;
-    // K-tile 0: q3 of the previous tile leaves in P0
-    NTM_PH(0, false, 3, 22, false, e.prev);
+    // K-tile 0: q3 (LINE: row half 1) of the previous tile leaves in P0
+    NTM_PH(0, false, LINE ? 5 : 3, LINE ? 18 : 22, false, e.prev);
     NTM_PH(1, false, -1, 26, false, e.prev);
     NTM_PH(2, false, -1, 26, false, e.prev);
-    NTM_PH(3, false, -1, 22, false, e.prev);
+    NTM_PH(3, false, -1, LINE ? 26 : 22, false, e.prev);
     t = 1;
     NTM_PH(0, true, -1, 18, false, e.prev);
-    NTM_PH(1, true, -1, 14, false, e.prev);
+    NTM_PH(1, true, -1, LINE ? 18 : 14, false, e.prev);
     NTM_PH(2, true, -1, 10, false, e.prev);
     NTM_PH(3, true, -1, 10, false, e.prev);
 #pragma nounroll
@@ -297,7 +367,8 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_pp6_kernel(GemmArgs p) 
       --t;
     }
     // K-tile T-2 stages the next tile's K-tile 0, K-tile T-1 its K-tile 1 (or
-    // dummies); with a next tile, q0..q2 leave in P1..P3 of K-tile T-1
+    // dummies); with a next tile, q0..q2 leave in P1..P3 of K-tile T-1 (LINE:
+    // row half 0 in P2)
     t = T - 2;
     NTM_PH(0, false, -1, 10, false, false);
     NTM_PH(1, false, -1, 10, true, false);
@@ -305,9 +376,9 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_pp6_kernel(GemmArgs p) 
     NTM_PH(3, false, -1, 10, true, false);
     t = T - 1;
     NTM_PH(0, true, -1, 10, true, false);
-    NTM_PH(1, true, 0, 10, true, e.has_next);
-    NTM_PH(2, true, 1, 14, true, e.has_next);
-    NTM_PH(3, true, 2, 18, true, e.has_next);
+    NTM_PH(1, true, LINE ? -1 : 0, 10, true, e.has_next);
+    NTM_PH(2, true, LINE ? 4 : 1, LINE ? 10 : 14, true, e.has_next);
+    NTM_PH(3, true, LINE ? -1 : 2, 18, true, e.has_next);
     if (!e.has_next) break;
     // advance to the next tile
 #pragma unroll
@@ -328,7 +399,18 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_pp6_kernel(GemmArgs p) 
   if (c.wr == 0) raw_barrier();  // balance the stagger
   wait_vm<0>();                  // dummy pieces: nothing may land after the WG exits
   if (POL != 2 || p.ldc < 0)
-    store_tile_lds<false, POL != 0, false, POL == 0 ? 0 : 1>(p, c, acc, e.m0, e.n0, lane);
+    store_tile_lds<false, POL != 0, false, POL == 0 ? 0 : 1, LINE>(p, c, acc, e.m0, e.n0, lane);
+  if constexpr (STAMP != 0) {
+    unsigned long long t1, rt1;
+    clock_stamp(t1, rt1);
+    if (threadIdx.x == 0) {
+      unsigned long long* o = p.stamps + 4 * (size_t)blockIdx.x;
+      o[0] = t0;
+      o[1] = rt0;
+      o[2] = t1;
+      o[3] = rt1;
+    }
+  }
 }
 #undef NTM_PH
 
@@ -348,23 +430,23 @@ inline int pp6_grid(int ntiles) {
 
 // Experimental: an explicit grid (a multiple of 8, at most the tile count) and
 // POL 2 (C not stored) - the store-bandwidth study of profiles/r3_stores.
-template <int POL>
+template <int POL, bool LINE = false>
 inline hipError_t launch_gemm_bf16_pp6_grid(const GemmArgs& a, int grid, hipStream_t stream) {
   if (!shape_ok6(a.M, a.N, a.K) || a.rowsum || a.lda < a.K || a.ldb < a.K || a.ldc < a.N ||
       (a.lda % 8) || (a.ldb % 8) || (a.ldc % 8) || grid <= 0 || grid % 8 ||
       grid > (a.M / BM) * (a.N / BN))
     return hipErrorInvalidValue;
-  hipLaunchKernelGGL((gemm_bf16_pp6_kernel<POL>), dim3((unsigned)grid), dim3(kThreads), 0, stream, a);
+  hipLaunchKernelGGL((gemm_bf16_pp6_kernel<POL, LINE>), dim3((unsigned)grid), dim3(kThreads), 0, stream, a);
   return hipGetLastError();
 }
 
-template <int POL>
+template <int POL, bool LINE = false, int STAMP = 0>
 inline hipError_t launch_gemm_bf16_pp6(const GemmArgs& a, hipStream_t stream) {
   if (!shape_ok6(a.M, a.N, a.K) || a.rowsum || a.lda < a.K || a.ldb < a.K || a.ldc < a.N ||
-      (a.lda % 8) || (a.ldb % 8) || (a.ldc % 8))
+      (a.lda % 8) || (a.ldb % 8) || (a.ldc % 8) || (STAMP != 0 && a.stamps == nullptr))
     return hipErrorInvalidValue;
   const int ntiles = (a.M / BM) * (a.N / BN);
-  hipLaunchKernelGGL((gemm_bf16_pp6_kernel<POL>), dim3((unsigned)pp6_grid(ntiles)),
+  hipLaunchKernelGGL((gemm_bf16_pp6_kernel<POL, LINE, STAMP>), dim3((unsigned)pp6_grid(ntiles)),
                      dim3(kThreads), 0, stream, a);
   return hipGetLastError();
 }

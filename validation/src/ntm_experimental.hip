@@ -77,6 +77,10 @@ NTM_API int ntm_gemm_bf16_experimental(int variant, const void* A, const void* B
     case 41: return (int)ntm::gemm6::launch_gemm_bf16_pp6_grid<1>(a, 128, S(stream));
     case 42: return (int)ntm::gemm6::launch_gemm_bf16_pp6_grid<2>(a, 128, S(stream));
     case 43: return (int)ntm::gemm6::launch_gemm_bf16_pp6_grid<2>(a, 256, S(stream));
+    // pingpong8o with the whole-line C layout (gemm_bf16_pp6.hpp LINE), and the
+    // same with C not stored
+    case 44: return (int)ntm::gemm6::launch_gemm_bf16_pp6<1, true>(a, S(stream));
+    case 45: return (int)ntm::gemm6::launch_gemm_bf16_pp6_grid<2, true>(a, 256, S(stream));
     default: return (int)hipErrorInvalidValue;
   }
 }

@@ -63,6 +63,8 @@ NTM_API int ntm_gemm_shape_ok(int M, int N, int K) {
 // 1394 vs 1374 (+1.5 %), 8192x8192x6144 1611 vs 1590 (+1.3 %).
 constexpr int kDefaultVariant = 5;
 constexpr int kPersistentVariant = 25;
+// C layout of the shipping pingpong8o build (gemm_bf16_pp6.hpp LINE)
+constexpr bool kPp6Line = false;
 
 // Tile-shape plan of the default dispatch: the smallest predicted time
 // rounds(tiles) x tile_area / efficiency over 256 CUs, where the efficiencies
@@ -297,7 +299,7 @@ NTM_API int ntm_gemm_bf16_variant(int variant, const void* A, const void* B,
     case 25:
       if (!ntm::gemm6::shape_ok6(M, N, K) || (lda % 8) || (ldb % 8) || (ldc % 8))
         return (int)ntm::gemm3::launch_gemm_bf16_pp3(a, S(stream));
-      return (int)ntm::gemm6::launch_gemm_bf16_pp6<1>(a, S(stream));
+      return (int)ntm::gemm6::launch_gemm_bf16_pp6<1, kPp6Line>(a, S(stream));
     // gemm_bf16_t128.hpp: 128x128 / 256x128 / 160x160 tiles on the wave-specialised
     // kernel (4 DMA-producer + 4 MFMA-consumer waves), 256x160 on the 4-wave one
     case 15: return (int)ntm::gemmt::launch_gemm_bf16_tile_ws<4>(a, S(stream));
@@ -631,6 +633,32 @@ NTM_API int ntm_clock_probe(int grid, int iters, void* out, float* sink, void* s
   hipLaunchKernelGGL(ntm::aux::clock_probe_kernel, dim3(grid), dim3(256), 0, S(stream), iters,
                      7u, (unsigned long long*)out, sink);
   return (int)hipGetLastError();
+}
+
+// GEMM clock: the shipping pingpong8o build with a start / end
+// s_memtime + s_memrealtime stamp per workgroup (gemm_bf16_pp6.hpp STAMP 1).
+// Whole 256x256 tiles, more tiles than CUs; stamps = 4 u64 per workgroup
+// (ntm_gemm_bf16_clock_grid workgroups). C is the real product.
+NTM_API int ntm_gemm_bf16_clock_grid(int M, int N) {
+  if (M <= 0 || N <= 0 || M % 256 || N % 256) return 0;
+  return ntm::gemm6::pp6_grid((M / 256) * (N / 256));
+}
+
+NTM_API int ntm_gemm_bf16_clock(const void* A, const void* B, void* C, int M, int N, int K,
+                                int lda, int ldb, int ldc, void* stamps, void* stream) {
+  if (!stamps) return (int)hipErrorInvalidValue;
+  ntm::gemm::GemmArgs a;
+  a.A = (const __bf16*)A;
+  a.B = (const __bf16*)B;
+  a.C = (__bf16*)C;
+  a.M = M;
+  a.N = N;
+  a.K = K;
+  a.lda = lda;
+  a.ldb = ldb;
+  a.ldc = ldc;
+  a.stamps = (unsigned long long*)stamps;
+  return (int)ntm::gemm6::launch_gemm_bf16_pp6<1, kPp6Line, 1>(a, S(stream));
 }
 
 NTM_API int ntm_verify_result_bytes() {
