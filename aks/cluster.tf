@@ -56,7 +56,9 @@ resource "azurerm_kubernetes_cluster_node_pool" "mi355x" {
   node_count            = var.gpu_node_pool_count
   min_count             = var.gpu_node_pool_min_count
   max_count             = var.gpu_node_pool_max_count
-  node_taints           = ["amd.com/gpu=present:NoSchedule"]
+  # + the startup taint the node-prep DaemonSet removes after a verified prep
+  node_taints = concat(["amd.com/gpu=present:NoSchedule"],
+  var.gpu_node_prep_taint ? ["${local.prep_taint_key}=pending:NoSchedule"] : [])
   tags                  = local.tags
   node_labels = {
     "node.kubernetes.io/pool" = "gpu"

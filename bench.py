@@ -372,10 +372,14 @@ def main(argv=None) -> int:
             extras["p2p_send_GBps"] = pm.as_dict()
             if pm.errors:
                 verified = False
+        tuned = None
         if not args.no_xgmi and n <= 8:
-            # C2 knob sweep first: blocks per rank x one-/two-shot at 4 sizes, the
-            # favoured one-shot cutoff (xgmi.tune; a few seconds at N = 8). The
-            # rehearsal runs it over torch.distributed to pin the JSON shape.
+            # C2 knob sweep first: blocks per rank (16 .. 256) x one-/two-shot at 6
+            # sizes up to 256 MiB (capped by free HBM), the favoured one-shot cutoff
+            # and the best single nblk (xgmi.tune; ~5-10 s at N = 8, bounded by
+            # xgmi.TUNE_BUDGET_S). The main sweep below then runs THAT
+            # configuration. The rehearsal runs both over torch.distributed to pin
+            # the JSON shape and the hand-over.
             from nvidia_terraform_modules_amd.parallel import xgmi as xg
 
             fac = None
@@ -383,28 +387,36 @@ def main(argv=None) -> int:
                 fac = lambda nb, mb: xg.ReferenceAllReduce(env, mb, nblk=nb)  # noqa: E731
             t_tune = time.perf_counter()
             try:
-                tuned = xg.tune(env, factory=fac)
+                tuned = xg.tune(env, factory=fac, max_bytes=max_b)
                 tuned["seconds"] = round(time.perf_counter() - t_tune, 2)
                 extras["xgmi_tune"] = tuned
                 if tuned["errors"] or tuned["timed_out"]:
                     verified = False
             except Exception as e:  # noqa: BLE001 - recorded; the main sweep still runs
                 extras["xgmi_tune"] = {"error": f"{type(e).__name__}: {e}"[:300]}
-        if not args.no_xgmi and not args.rehearsal and n <= 8:
+                tuned = None
+        if not args.no_xgmi and n <= 8:
             # C2 next to RCCL: the same sizes, in place on the registered buffer,
-            # no host sync / barrier / staging per call (device-side barriers).
+            # no host sync / barrier / staging per call (device-side barriers),
+            # in the tuned configuration (the defaults if the tune failed).
             # Set-up failures (IPC, peer mapping) are agreed on collectively so no
             # rank is left waiting in a collective the others skipped; the JSON
             # line still comes out with the error recorded.
-            from nvidia_terraform_modules_amd.parallel.xgmi import XgmiAllReduce
+            from nvidia_terraform_modules_amd.parallel import xgmi as xg
 
+            nblk, cut, src = 64, 256 << 10, "default"
+            if tuned and not tuned["errors"] and not tuned["timed_out"]:
+                nblk, cut, src = tuned["best_nblk"], tuned["best_one_shot_max_bytes"], "xgmi_tune"
             # the RCCL bf16 sizes from 512 B to 1 GiB (so the two can be paired) that
             # split into 8-element chunks per rank
             xs = [b for b in coll.sweep_sizes(8, max_b, 4)
                   if 512 <= b <= 1 << 30 and (b // 2) % (8 * n) == 0]
             ar, err = None, ""
             try:
-                ar = XgmiAllReduce(env, max_bytes=max(xs), nblk=64)
+                if args.rehearsal:
+                    ar = xg.ReferenceAllReduce(env, max(xs), nblk=nblk, one_shot_max_bytes=cut)
+                else:
+                    ar = xg.XgmiAllReduce(env, max_bytes=max(xs), nblk=nblk, one_shot_max_bytes=cut)
             except Exception as e:  # noqa: BLE001 - reported, and agreed on below
                 err = f"{type(e).__name__}: {e}"[:300]
             if dist.all_reduce_max(env, 1.0 if err else 0.0) > 0:
@@ -420,6 +432,8 @@ def main(argv=None) -> int:
                 extras["xgmi_peak_busbw_GBps"] = coll.peak_busbw(xr)
                 extras["xgmi_vs_rccl_bf16"] = pair_busbw(res, xr)
                 extras["xgmi_blocks_per_rank"] = ar.nblk
+                extras["xgmi_one_shot_max_bytes"] = ar.one_shot_max_bytes
+                extras["xgmi_config_source"] = src
                 extras["xgmi_timed_out"] = dist.all_reduce_max(
                     env, 1.0 if ar.timed_out() else 0.0) > 0
                 ar.close()

@@ -15,7 +15,8 @@ resource "terraform_data" "gpu_instance_type_guard" {
 }
 
 locals {
-  node_sgs = local.byo_network ? var.additional_security_group_ids : []
+  prep_taint_key = "amd.com/mi355x-prep"
+  node_sgs       = local.byo_network ? var.additional_security_group_ids : []
   node_key = var.ssh_key == "" ? null : var.ssh_key
 
   # Host preparation for MI355X nodes, BEFORE the EKS bootstrap (kubelet and
@@ -170,9 +171,13 @@ module "gpu_node_pool" {
     "amd.com/gpu.arch"        = "gfx950"
     "node.kubernetes.io/pool" = "gpu"
   }
-  taints = {
+  # + the startup taint the node-prep DaemonSet removes once the host prep is
+  # verified on the node (the validation Job does not tolerate it)
+  taints = merge({
     amd_gpu = { key = "amd.com/gpu", value = "present", effect = "NO_SCHEDULE" }
-  }
+    }, var.gpu_node_prep_taint ? {
+    mi355x_prep = { key = local.prep_taint_key, value = "pending", effect = "NO_SCHEDULE" }
+  } : {})
   block_device_mappings = {
     root = {
       device_name = data.aws_ami.lookup.root_device_name

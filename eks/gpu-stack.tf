@@ -21,6 +21,10 @@ module "amd_gpu_stack" {
   node_prep_iommu_mode        = "check"
   validation_require_iommu_pt = var.gpu_node_iommu_passthrough != "off"
 
+  # the pools' startup taint: the Job schedules only on verified-prepared nodes
+  node_prep_startup_taint = var.gpu_node_prep_taint
+  node_prep_taint_key     = local.prep_taint_key
+
   gpu_node_selector = { "amd.com/gpu.present" = "true" }
   gpu_node_pool_ids = [module.gpu_node_pool.node_group_id]
 

@@ -35,6 +35,8 @@ locals {
   "https://www.googleapis.com/auth/${s}"]
   base_labels = { part_of = var.cluster_name, env = var.project_id, managed_by = "terraform" }
   base_tags   = ["tf-managed", var.cluster_name]
+
+  prep_taint_key = "amd.com/mi355x-prep"
 }
 
 resource "google_container_cluster" "this" {
@@ -133,6 +135,15 @@ resource "google_container_node_pool" "mi355x" {
       key    = "amd.com/gpu"
       value  = "present"
       effect = "NO_SCHEDULE"
+    }
+    # startup taint, removed by the node-prep DaemonSet after a verified prep
+    dynamic "taint" {
+      for_each = var.gpu_node_prep_taint ? [local.prep_taint_key] : []
+      content {
+        key    = taint.value
+        value  = "pending"
+        effect = "NO_SCHEDULE"
+      }
     }
     workload_metadata_config {
       mode = "GKE_METADATA"

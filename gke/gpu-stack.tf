@@ -19,6 +19,10 @@ module "amd_gpu_stack" {
   node_prep_iommu_mode        = var.gpu_node_iommu_passthrough
   validation_require_iommu_pt = var.gpu_node_iommu_passthrough == "reboot"
 
+  # the pools' startup taint: the Job schedules only on verified-prepared nodes
+  node_prep_startup_taint = var.gpu_node_prep_taint
+  node_prep_taint_key     = local.prep_taint_key
+
   gpu_node_selector = { "amd.com/gpu.present" = "true" }
   gpu_node_pool_ids = [google_container_node_pool.mi355x.id]
 

@@ -60,6 +60,14 @@ resource "kubernetes_daemon_set_v1" "amdgpu_dkms" {
           operator = "Exists"
           effect   = "NoSchedule"
         }
+        dynamic "toleration" {
+          for_each = local.prep_tolerations
+          content {
+            key      = toleration.value.key
+            operator = toleration.value.operator
+            effect   = toleration.value.effect
+          }
+        }
         init_container {
           name    = "install"
           image   = var.amdgpu_dkms_image
@@ -106,6 +114,14 @@ resource "kubernetes_daemon_set_v1" "rocm_device_plugin" {
           key      = var.gpu_node_taint_key
           operator = "Exists"
           effect   = "NoSchedule"
+        }
+        dynamic "toleration" {
+          for_each = local.prep_tolerations
+          content {
+            key      = toleration.value.key
+            operator = toleration.value.operator
+            effect   = toleration.value.effect
+          }
         }
         container {
           name  = "device-plugin"
@@ -211,6 +227,14 @@ resource "kubernetes_daemon_set_v1" "node_labeller" {
           operator = "Exists"
           effect   = "NoSchedule"
         }
+        dynamic "toleration" {
+          for_each = local.prep_tolerations
+          content {
+            key      = toleration.value.key
+            operator = toleration.value.operator
+            effect   = toleration.value.effect
+          }
+        }
         container {
           name  = "labeller"
           image = var.node_labeller_image
@@ -284,6 +308,14 @@ resource "kubernetes_daemon_set_v1" "metrics_exporter" {
           key      = var.gpu_node_taint_key
           operator = "Exists"
           effect   = "NoSchedule"
+        }
+        dynamic "toleration" {
+          for_each = local.prep_tolerations
+          content {
+            key      = toleration.value.key
+            operator = toleration.value.operator
+            effect   = toleration.value.effect
+          }
         }
         container {
           name  = "exporter"

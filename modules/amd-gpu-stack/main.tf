@@ -23,9 +23,15 @@ locals {
     (var.install_node_feature_discovery || !endswith(crd, ".nfd.k8s-sigs.io"))
   ]
 
-  gpu_tolerations = [
+  # the startup taint of not-yet-prepared GPU nodes (node-prep.tf): tolerated
+  # by the GPU stack's own components (they install beside the prep), never by
+  # the validation Job
+  prep_tolerations = var.node_prep_enabled && var.node_prep_startup_taint ? [
+    { key = var.node_prep_taint_key, operator = "Exists", effect = "NoSchedule" },
+  ] : []
+  gpu_tolerations = concat([
     { key = var.gpu_node_taint_key, operator = "Exists", effect = "NoSchedule" },
-  ]
+  ], local.prep_tolerations)
 
   # One typed map, one code path, AMD only: rendered once with yamlencode.
   operator_values = {

@@ -26,6 +26,10 @@ locals {
     "--rccl-busbw-floor-gbps", tostring(var.validation_rccl_busbw_floor_gbps),
   ] : [], var.validation_gpu_count > 1 && var.validation_xgmi_busbw_floor_gbps > 0 ? [
     "--xgmi-busbw-floor-gbps", tostring(var.validation_xgmi_busbw_floor_gbps),
+  ] : [], var.validation_gpu_count > 1 ? [
+    # the hand-written all-reduce runs in the configuration a mini-sweep picks
+    # (blocks per rank x one-shot cutoff, well under 2 s at 8 GPUs)
+    "--xgmi-tune",
   ] : [], var.node_prep_enabled && var.validation_require_host_prep ? [
     "--require-host-prep",
   ] : [], var.validation_require_iommu_pt ? [
@@ -71,6 +75,10 @@ resource "kubernetes_job_v1" "gpu_validation" {
         host_ipc       = true # RCCL peer-to-peer IPC between the ranks' GPU buffers
         node_selector  = var.gpu_node_selector
 
+        # The GPU taint only: NOT the node-prep startup taint
+        # (node_prep_startup_taint), so the Job schedules on a node only after
+        # the prep has been verified there and containerd restarted with
+        # LimitMEMLOCK=infinity - no race with the prep, no fail-and-retry.
         toleration {
           key      = var.gpu_node_taint_key
           operator = "Exists"
@@ -190,6 +198,14 @@ resource "kubernetes_daemon_set_v1" "validation_prepull" {
           key      = var.gpu_node_taint_key
           operator = "Exists"
           effect   = "NoSchedule"
+        }
+        dynamic "toleration" {
+          for_each = local.prep_tolerations
+          content {
+            key      = toleration.value.key
+            operator = toleration.value.operator
+            effect   = toleration.value.effect
+          }
         }
         init_container {
           name    = "pull-and-link-check"

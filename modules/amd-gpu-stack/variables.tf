@@ -335,6 +335,18 @@ variable "node_prep_enabled" {
   description = "Run the privileged mi355x-node-prep DaemonSet on the GPU nodes: automatic NUMA balancing off, containerd LimitMEMLOCK=infinity, iommu=pt per node_prep_iommu_mode. Idempotent (EKS user data applies the same settings before the join; here it then only verifies)."
 }
 
+variable "node_prep_startup_taint" {
+  type        = bool
+  default     = false
+  description = "The GPU node pools carry the startup taint node_prep_taint_key=pending:NoSchedule (the eks / gke / aks roots set it with gpu_node_prep_taint). The node-prep DaemonSet removes it from a node once the host prep is verified there (NUMA balancing off, containerd running with LimitMEMLOCK=infinity, so every pod created afterwards inherits it); only the GPU-stack DaemonSets tolerate it, never the validation Job, which therefore lands on prepared nodes only. Needs kubectl_image at node-join time and a ClusterRole that may get / patch nodes."
+}
+
+variable "node_prep_taint_key" {
+  type        = string
+  default     = "amd.com/mi355x-prep"
+  description = "Key of the GPU node pools' startup taint (node_prep_startup_taint)."
+}
+
 variable "node_prep_iommu_mode" {
   type        = string
   default     = "check"

@@ -33,6 +33,10 @@ def _declare() -> ctypes.CDLL:
     L.ntm_xgmi_allreduce_bf16.argtypes = [pp, pp, pp, c_int, c_int, c_int, c_int, c_size,
                                           ctypes.c_uint, c_vp, c_int, c_vp]
     L.ntm_xgmi_allreduce_bf16.restype = c_int
+    L.ntm_xgmi_allreduce_bf16_ex.argtypes = [pp, pp, pp, c_int, c_int, c_int, c_int, c_size,
+                                             ctypes.c_uint, c_vp, c_int, ctypes.c_uint,
+                                             ctypes.c_uint, c_vp]
+    L.ntm_xgmi_allreduce_bf16_ex.restype = c_int
     L.ntm_xgmi_signal_bytes.argtypes = [c_int]
     L.ntm_xgmi_signal_bytes.restype = c_size
     L.ntm_malloc.argtypes = [ctypes.POINTER(c_vp), c_size, c_int]
@@ -59,15 +63,23 @@ def _ptrs(xs) -> "ctypes.Array":
 
 def simulate_allreduce(inputs: list[torch.Tensor], nblk: int = 16, one_shot: bool = False,
                        epoch: int = 1, inplace: bool = False,
-                       sigs: list[torch.Tensor] | None = None) -> tuple[list[torch.Tensor], int]:
+                       sigs: list[torch.Tensor] | None = None, nranks_here: int | None = None,
+                       spin_limit: int = 0, entry_spin_limit: int = 0,
+                       ) -> tuple[list[torch.Tensor], int]:
     """All-reduce (sum) N same-shaped bf16 tensors living on ONE device, as N
     simulated ranks. Returns (outputs, timeout_code) - 0 means no barrier
     timed out. ``inplace`` (two-shot only) reduces into the inputs themselves;
-    ``sigs`` reuses signal buffers across calls (epochs must then grow)."""
+    ``sigs`` reuses signal buffers across calls (epochs must then grow).
+    ``nranks_here`` < N launches only ranks 0 .. nranks_here-1: the others
+    never arrive (the failure path), so pass small ``spin_limit`` /
+    ``entry_spin_limit`` (0 = the kernel defaults, minutes)."""
     n = len(inputs)
+    here = n if nranks_here is None else nranks_here
+    if not 1 <= here <= n:
+        raise ValueError("1 <= nranks_here <= len(inputs)")
     if not 1 <= n <= MAX_RANKS:
         raise ValueError("1..8 ranks")
-    if n * nblk > 1024:
+    if here * nblk > 1024:
         raise ValueError("nranks * nblk must be <= 1024 (all blocks co-resident)")
     if inplace and one_shot:
         raise ValueError("one-shot cannot run in place")
@@ -84,10 +96,10 @@ def simulate_allreduce(inputs: list[torch.Tensor], nblk: int = 16, one_shot: boo
         sig_bytes = L.ntm_xgmi_signal_bytes(nblk)
         sigs = [torch.zeros(sig_bytes // 4, dtype=torch.int32, device=dev) for _ in range(n)]
     err = torch.zeros(1, dtype=torch.int32, device=dev)
-    rc = L.ntm_xgmi_allreduce_bf16(
+    rc = L.ntm_xgmi_allreduce_bf16_ex(
         _ptrs([t.data_ptr() for t in inputs]), _ptrs([t.data_ptr() for t in outs]),
-        _ptrs([s.data_ptr() for s in sigs]), n, 0, n, nblk, count, epoch, err.data_ptr(),
-        1 if one_shot else 0, stream_handle())
+        _ptrs([s.data_ptr() for s in sigs]), n, 0, here, nblk, count, epoch, err.data_ptr(),
+        1 if one_shot else 0, spin_limit, entry_spin_limit, stream_handle())
     check(rc, "ntm_xgmi_allreduce_bf16")
     torch.cuda.synchronize(dev)
     return outs, int(err.item())
@@ -114,17 +126,21 @@ class XgmiAllReduce:
     copies (still no host sync). Messages up to ``one_shot_max_bytes`` take the
     one-shot kernel (one read pass over all peers, 2 barriers instead of 3).
 
-    Failure contract: the device-side barriers are bounded. The entry barrier
-    waits up to ~16x longer than the in-kernel phases (it absorbs host skew
-    between ranks: a checkpoint, a GC pause); a block that still times out
-    fills the part of the output it owns with bf16 NaN and records the phase in
-    a sticky device error word, so a late rank yields NaNs, never a silently
-    partial sum. ``run(..., check=True)`` / ``ar(t, check=True)`` synchronise
-    and raise on a timeout; otherwise poll :meth:`timed_out` (or call
+    Failure contract: the device-side barriers are bounded (``spin_limit`` /
+    ``entry_spin_limit``, 0 = the kernel defaults). The entry barrier waits
+    up to ~16x longer than the in-kernel phases (it absorbs host skew between
+    ranks: a checkpoint, a GC pause); a block that times out at the entry or
+    reduce-scatter barrier fills the part of the output it owns with bf16 NaN
+    and records the phase in a sticky device error word, so a late rank yields
+    NaNs, never a silently partial sum. A timeout at the EXIT barrier leaves a
+    complete result; only the buffers may still be read by the late peer.
+    ``run(..., check=True)`` / ``ar(t, check=True)`` synchronise and raise on a
+    timeout; otherwise poll :meth:`timed_out` (or call
     :meth:`raise_if_timed_out`) at a convenient sync point.
     """
 
-    def __init__(self, env, max_bytes: int, nblk: int = 64, one_shot_max_bytes: int = 256 << 10):
+    def __init__(self, env, max_bytes: int, nblk: int = 64, one_shot_max_bytes: int = 256 << 10,
+                 spin_limit: int = 0, entry_spin_limit: int = 0):
         from .dist import all_gather_obj
 
         if env.world_size > MAX_RANKS:
@@ -133,6 +149,7 @@ class XgmiAllReduce:
             raise ValueError("nblk must be in 1..1024")
         self.env, self.nblk, self.max_bytes = env, nblk, max_bytes
         self.one_shot_max_bytes = min(one_shot_max_bytes, max_bytes)
+        self.spin_limit, self.entry_spin_limit = spin_limit, entry_spin_limit
         self.L = L = _declare()
         self._own, self._opened = [], []
         # Collective-safe set-up: every rank reaches both all_gathers whatever
@@ -196,10 +213,10 @@ class XgmiAllReduce:
         self.epoch += 1
         n = self.env.world_size
         out = self.ptrs["out"] if one_shot else self.ptrs["in"]
-        rc = self.L.ntm_xgmi_allreduce_bf16(
+        rc = self.L.ntm_xgmi_allreduce_bf16_ex(
             _ptrs(self.ptrs["in"]), _ptrs(out), _ptrs(self.ptrs["sig"]), n,
             self.env.rank, 1, self.nblk, count, self.epoch, self.err.data_ptr(),
-            1 if one_shot else 0, stream_handle())
+            1 if one_shot else 0, self.spin_limit, self.entry_spin_limit, stream_handle())
         check(rc, "ntm_xgmi_allreduce_bf16")
 
     def run(self, numel: int, check: bool = False) -> torch.Tensor:
@@ -244,13 +261,16 @@ class XgmiAllReduce:
         return bool(self.err.item())
 
     def raise_if_timed_out(self) -> None:
-        """Synchronise; raise RuntimeError if a device barrier timed out (the
-        affected outputs hold NaN, see the class docstring)."""
+        """Synchronise; raise RuntimeError if a device barrier timed out (see
+        the class docstring for what the outputs then hold)."""
         code = int(self.err.item())
         if code:
+            what = ("the result is complete, but a peer may still read this rank's buffers: "
+                    "do not overwrite them before the peers are known to be done"
+                    if code == 3 else "the outputs this rank owns in the failed call are NaN")
             raise RuntimeError(f"XgmiAllReduce rank {self.env.rank}: device barrier timed out "
                                f"in the {self.PHASES.get(code, str(code))} phase "
-                               "(a peer never arrived); outputs of the failed call are NaN")
+                               f"(a peer never arrived); {what}")
 
     def close(self) -> None:
         torch.cuda.synchronize()
@@ -293,29 +313,51 @@ class ReferenceAllReduce:
         pass
 
 
-# C2 knob sweep (the first 8-GPU run must say whether the design or
-# a constant is at fault). Budget at N = 8: 4 communicators (one IPC set-up
-# each, ~0.1-0.5 s) x 4 sizes x <= 2 algorithms x 12 calls of <= ~0.2 ms, plus
-# one full-element check per point - a few seconds in all.
-TUNE_SIZES = (64 << 10, 256 << 10, 1 << 20, 16 << 20)
-TUNE_NBLKS = (16, 32, 64, 128)
+# C2 knob sweep (the first 8-GPU run must say whether the
+# design or a constant is at fault, and run the tuned configuration). Sizes
+# reach the bandwidth regime (64 / 256 MiB) and blocks per rank one per CU.
+# Budget at N = 8: 5 communicators (one IPC set-up each, ~0.1-0.5 s) x 6
+# sizes x <= 2 algorithms x 12 calls (256 MiB two-shot: ~1-3 ms a call at
+# 200-600 GB/s busbw), plus one full-element check per point - ~5-10 s in all.
+# TUNE_BUDGET_S bounds it: once the slowest rank has spent that long, the
+# remaining nblk values are skipped (agreed collectively, recorded).
+TUNE_SIZES = (64 << 10, 256 << 10, 1 << 20, 16 << 20, 64 << 20, 256 << 20)
+TUNE_NBLKS = (16, 32, 64, 128, 256)
 TUNE_CUTOFFS = (64 << 10, 256 << 10, 1 << 20)
+TUNE_BUDGET_S = 30.0
 
 
 def tune(env, sizes=TUNE_SIZES, nblks=TUNE_NBLKS, cutoffs=TUNE_CUTOFFS, iters: int = 10,
-         warmup: int = 2, factory=None) -> dict:
+         warmup: int = 2, factory=None, max_bytes: int | None = None,
+         budget_s: float = TUNE_BUDGET_S) -> dict:
     """Sweep blocks per rank x algorithm (one-shot where a size is <= the
     largest cutoff, two-shot always) at each size, every element checked.
-    Returns the full table, the best (nblk, algorithm) per size and the
-    one-shot cutoff among ``cutoffs`` that the measurements favour.
+    Returns the full table, the best (nblk, algorithm) per size, the one-shot
+    cutoff among ``cutoffs`` that the measurements favour and ``best_nblk``:
+    the one blocks-per-rank value that, with that cutoff, moves the swept
+    sizes fastest (what the main sweep / a communicator should use).
+    ``max_bytes`` drops larger sizes; ``budget_s`` stops after the nblk value
+    during which the slowest rank passed it (collective decision).
     ``factory(nblk, max_bytes)`` builds the communicator (default
     :class:`XgmiAllReduce`); set-up is collective, so every rank must call."""
-    from .collectives import all_reduce_sweep
+    import time
 
+    from .collectives import all_reduce_sweep
+    from .dist import all_reduce_max
+
+    if max_bytes is not None:
+        sizes = tuple(s for s in sizes if s <= max_bytes)
+    if not sizes:
+        raise ValueError("no tune size fits max_bytes")
     factory = factory or (lambda nb, mb: XgmiAllReduce(env, max_bytes=mb, nblk=nb))
     max_b = max(sizes)
     table, errors, timed_out = [], 0, False
+    t0 = time.perf_counter()
+    swept = []
     for nb in nblks:
+        if swept and all_reduce_max(env, time.perf_counter() - t0) > budget_s:
+            break
+        swept.append(nb)
         ar = factory(nb, max_b)
         try:
             for size in sizes:
@@ -349,8 +391,21 @@ def tune(env, sizes=TUNE_SIZES, nblks=TUNE_NBLKS, cutoffs=TUNE_CUTOFFS, iters: i
             tot += b["time_us"] if b else float("inf")
         score[c] = tot
     best_cut = min(score, key=score.get)
-    return {"sizes": list(sizes), "nblks": list(nblks), "cutoffs": list(cutoffs),
-            "table": table, "best_per_size": best_per_size,
-            "best_one_shot_max_bytes": best_cut,
+    # one nblk for the communicator: with the chosen cutoff, the smallest sum
+    # of per-size times (ties: fewer blocks)
+    per_nblk = {}
+    for nb in swept:
+        tot = 0.0
+        for s in sizes:
+            algo = "1shot" if s <= best_cut else "2shot"
+            rows = [t for t in table if t["nblk"] == nb and t["bytes"] == s and t["algo"] == algo]
+            tot += rows[0]["time_us"] if rows else float("inf")
+        per_nblk[nb] = tot
+    best_nblk = min(per_nblk, key=lambda nb: (per_nblk[nb], nb))
+    return {"sizes": list(sizes), "nblks": list(swept), "nblks_skipped": [nb for nb in nblks
+                                                                          if nb not in swept],
+            "cutoffs": list(cutoffs), "table": table, "best_per_size": best_per_size,
+            "best_one_shot_max_bytes": best_cut, "best_nblk": best_nblk,
             "cutoff_total_time_us": {str(c): round(v, 2) for c, v in score.items()},
-            "errors": errors, "timed_out": timed_out}
+            "nblk_total_time_us": {str(nb): round(v, 2) for nb, v in per_nblk.items()},
+            "budget_s": budget_s, "errors": errors, "timed_out": timed_out}

@@ -75,17 +75,29 @@ def test_torchrun_launch_one_json_line(nproc):
     assert d["per_rank_gemm_clock_p10_GHz"] == [None] * nproc
     assert len(d["per_rank_gemm_clock"]) == nproc
     if nproc > 1:
-        # C2 knob sweep: blocks per rank x one/two-shot at 4 sizes, best per size and
-        # the favoured one-shot cutoff (over torch.distributed here: shape only)
+        # C2 knob sweep: blocks per rank 16..256 x one/two-shot at the
+        # tune sizes that fit the sweep cap (1 MiB here; 64 / 256 MiB on a real node),
+        # best per size, the favoured cutoff and ONE best nblk (over torch.distributed
+        # here: shape only) - and the main C2 sweep runs exactly that configuration
+        from nvidia_terraform_modules_amd.parallel.xgmi import TUNE_NBLKS, TUNE_SIZES
+
         tune = d["xgmi_tune"]
         assert tune["errors"] == 0 and tune["timed_out"] is False
-        assert tune["nblks"] == [16, 32, 64, 128] and len(tune["sizes"]) == 4
+        assert tune["nblks"] == list(TUNE_NBLKS) and tune["nblks_skipped"] == []
+        assert max(TUNE_SIZES) == 256 << 20 and max(TUNE_NBLKS) == 256
+        assert tune["sizes"] == [s for s in TUNE_SIZES if s <= 1 << 20]
         assert {r["nblk"] for r in tune["table"]} == set(tune["nblks"])
         one = [r for r in tune["table"] if r["algo"] == "1shot"]
         assert one and all(r["bytes"] <= max(tune["cutoffs"]) for r in one)
-        assert len(tune["best_per_size"]) == 4
+        assert len(tune["best_per_size"]) == len(tune["sizes"])
         assert tune["best_one_shot_max_bytes"] in tune["cutoffs"]
         assert set(tune["cutoff_total_time_us"]) == {str(c) for c in tune["cutoffs"]}
+        assert tune["best_nblk"] in tune["nblks"]
+        assert d["xgmi_config_source"] == "xgmi_tune"
+        assert d["xgmi_blocks_per_rank"] == tune["best_nblk"]
+        assert d["xgmi_one_shot_max_bytes"] == min(tune["best_one_shot_max_bytes"],
+                                                   max(r["bytes"] for r in d["xgmi_allreduce_bf16"]))
+        assert all(r["errors"] == 0 for r in d["xgmi_allreduce_bf16"])
     if nproc > 1:
         assert all(r["errors"] == 0 for r in d["allreduce_bf16"] + d["allreduce_fp32"])
         assert d["allreduce_bf16"][0]["bytes"] == 8

@@ -188,6 +188,127 @@ def test_busbw_floors_only_apply_with_more_than_one_gpu():
                          validation_xgmi_busbw_floor_gbps=400, validation_gpu_count=8)
     assert eight[eight.index("--rccl-busbw-floor-gbps") + 1] == "300"
     assert eight[eight.index("--xgmi-busbw-floor-gbps") + 1] == "400"
+    # the Job's C2 runs tuned at N > 1, never at N = 1
+    assert "--xgmi-tune" in eight and "--xgmi-tune" not in one
     m = load_module(ROOT / "modules" / "amd-gpu-stack")
     for v in ("validation_rccl_busbw_floor_gbps", "validation_xgmi_busbw_floor_gbps"):
         assert m.variables[v].default == 0 and m.variables[v].validations
+
+
+# ------------------------------------------------- startup-taint gate
+def _eval(mdir, expr, **overrides):
+    """Evaluate an expression of module ``mdir`` with variable defaults + overrides."""
+    from nvidia_terraform_modules_amd.tfcheck.evaluate import Evaluator, Scope, convert
+
+    mod = load_module(mdir)
+    ev = Evaluator()
+    variables = {}
+    for vn, v in mod.variables.items():
+        if vn in overrides:
+            variables[vn] = overrides[vn]
+        elif not v.required:
+            variables[vn] = convert(ev.eval(v.block.body.attr("default"), Scope({}, {})),
+                                    v.type_expr)
+    return ev.eval(expr, Scope(variables, {n: e for n, (e, _, _) in mod.locals.items()},
+                               str(mod.path)))
+
+
+def _blocks(body, btype):
+    return [b for b in body.blocks if b.type == btype]
+
+
+def _pod_spec(res):
+    spec = _blocks(res.block.body, "spec")[0]
+    tmpl = _blocks(spec.body, "template")[0]
+    return _blocks(tmpl.body, "spec")[0].body
+
+
+PREP = "amd.com/mi355x-prep"
+
+
+@pytest.mark.parametrize("root", ["eks", "gke", "aks"])
+def test_gpu_pools_join_with_the_prep_startup_taint(root, tmp_path):
+    m = load_module(ROOT / root)
+    if root == "eks":
+        expr = m.modules["gpu_node_pool"].block.body.attr("taints")
+        on, off = _eval(ROOT / root, expr), _eval(ROOT / root, expr, gpu_node_prep_taint=False)
+        assert on["mi355x_prep"] == {"key": PREP, "value": "pending", "effect": "NO_SCHEDULE"}
+        assert set(off) == {"amd_gpu"} and on["amd_gpu"]["key"] == "amd.com/gpu"
+    elif root == "gke":
+        ncfg = _blocks(m.resources["google_container_node_pool.mi355x"].block.body, "node_config")[0]
+        dyn = [b for b in _blocks(ncfg.body, "dynamic") if b.labels == ["taint"]][0]
+        assert _eval(ROOT / root, dyn.body.attr("for_each")) == [PREP]
+        assert _eval(ROOT / root, dyn.body.attr("for_each"), gpu_node_prep_taint=False) == []
+        content = _blocks(dyn.body, "content")[0].body
+        assert render(content.attr("value")) == '"pending"'
+        assert render(content.attr("effect")) == '"NO_SCHEDULE"'
+    else:
+        expr = m.resources["azurerm_kubernetes_cluster_node_pool.mi355x"].block.body.attr("node_taints")
+        assert _eval(ROOT / root, expr) == ["amd.com/gpu=present:NoSchedule",
+                                             f"{PREP}=pending:NoSchedule"]
+        assert _eval(ROOT / root, expr, gpu_node_prep_taint=False) == ["amd.com/gpu=present:NoSchedule"]
+    # the stack gets the same key and the switch; its gate RBAC is planned
+    body = m.modules["amd_gpu_stack"].block.body
+    assert render(body.attr("node_prep_startup_taint")) == "var.gpu_node_prep_taint"
+    assert _eval(ROOT / root, body.attr("node_prep_taint_key")) == PREP
+    r = _plan(root, tmp_path)
+    assert r.ok, r.errors
+    for res in ("kubernetes_service_account_v1.node_prep[0]",
+                "kubernetes_cluster_role_v1.node_prep[0]",
+                "kubernetes_cluster_role_binding_v1.node_prep[0]"):
+        assert STACK + res in r.resources
+    off = _plan(root, tmp_path, "gpu_node_prep_taint=false")
+    assert off.ok and STACK + "kubernetes_cluster_role_v1.node_prep[0]" not in off.resources
+
+
+def test_only_the_gpu_stack_tolerates_the_startup_taint():
+    """Every GPU-node DaemonSet of the stack (and every operator component)
+    tolerates the prep taint; the validation Job does not, so it cannot land
+    on a node whose prep is not verified."""
+    stack = load_module(ROOT / "modules" / "amd-gpu-stack")
+    ds = [r for r in stack.managed if r.type == "kubernetes_daemon_set_v1"]
+    assert len(ds) >= 6
+    for r in ds:
+        dyn = [b for b in _blocks(_pod_spec(r), "dynamic") if b.labels == ["toleration"]]
+        assert dyn and render(dyn[0].body.attr("for_each")) == "local.prep_tolerations", r.address
+    job = _pod_spec(stack.resources["kubernetes_job_v1.gpu_validation"])
+    assert not [b for b in _blocks(job, "dynamic") if b.labels == ["toleration"]]
+    tols = [render(b.body.attr("key")) for b in _blocks(job, "toleration")]
+    assert tols == ["var.gpu_node_taint_key"]
+    on = _stack_local("gpu_tolerations", node_prep_startup_taint=True)
+    assert {"key": PREP, "operator": "Exists", "effect": "NoSchedule"} in on
+    assert len(_stack_local("gpu_tolerations")) == 1          # off by default in the module
+    # operator mode: every component carries gpu_tolerations (gpu-toleration rule)
+    assert not [f for f in analyze(stack) if f.rule == "gpu-toleration"]
+
+
+def test_prep_gate_init_chain_and_rbac():
+    stack = load_module(ROOT / "modules" / "amd-gpu-stack")
+    spec = _pod_spec(stack.resources["kubernetes_daemon_set_v1.node_prep"])
+    names = [render(b.body.attr("name")) for b in _blocks(spec, "init_container")]
+    dyn = [b for b in _blocks(spec, "dynamic") if b.labels == ["init_container"]]
+    assert names == ['"prep"'] and len(dyn) == 2
+    assert _stack_local("prep_gate", node_prep_startup_taint=True) is True
+    verify_fe = _eval(ROOT / "modules" / "amd-gpu-stack", dyn[0].body.attr("for_each"),
+                      node_prep_startup_taint=True)
+    taint_fe = _eval(ROOT / "modules" / "amd-gpu-stack", dyn[1].body.attr("for_each"),
+                     node_prep_startup_taint=True)
+    assert verify_fe == ["verify"]
+    # ensure-then-remove, in that (lexical) order; both single kubectl calls
+    assert list(taint_fe) == ["taint", "untaint"]
+    assert taint_fe["taint"] == f"{PREP}=pending:NoSchedule"
+    assert taint_fe["untaint"] == f"{PREP}=pending:NoSchedule-"
+    cmd = render(_blocks(dyn[1].body, "content")[0].body.attr("command"))
+    assert '"kubectl", "taint", "node", "$(NODE_NAME)"' in cmd and '"--overwrite"' in cmd
+    # verify reads what the Job checks: NUMA balancing and the running containerd's memlock
+    v = "".join(p for p in stack.locals["node_prep_verify_script"][0].parts if isinstance(p, str))
+    assert "/proc/sys/kernel/numa_balancing" in v and "Max locked memory *unlimited" in v
+    # the reboot path waits for the reboot instead of letting the chain untaint first
+    s = "".join(p for p in stack.locals["node_prep_script"][0].parts if isinstance(p, str))
+    assert s.index("systemctl --no-block reboot") < s.index("sleep 600") < s.index("exit 1")
+    # RBAC: get + patch on nodes, nothing else
+    role = stack.resources["kubernetes_cluster_role_v1.node_prep"].block.body
+    rules = _blocks(role, "rule")
+    assert len(rules) == 1
+    assert render(rules[0].body.attr("resources")) == '["nodes"]'
+    assert render(rules[0].body.attr("verbs")) == '["get", "patch"]'

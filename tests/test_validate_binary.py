@@ -207,6 +207,36 @@ def test_binary_xgmi_knobs(nblk, one_shot_max):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("nsim", [2, 4])
+def test_binary_xgmi_tune(nsim):
+    """--xgmi-tune (what the Job passes at N > 1): a mini-sweep
+    of blocks per rank x one-shot cutoff picks the configuration the main C2
+    sweep then runs; every swept point and every main-sweep element exact, and
+    the whole tune a small fraction of the Job's time."""
+    _have_bin()
+    rc, out, err = _run("--size", "512", "--iters", "2", "--no-fp8", "--no-rccl", "--xgmi-sim",
+                        str(nsim), "--allreduce-max-mib", "128", "--xgmi-tune")
+    g = _last_json(out)
+    assert rc == 0, (g["failures"], err[-2000:])
+    t = g["xgmi_tune"]
+    assert t["ran"] is True and t["seconds"] < 10
+    swept = {r["nblk"] for r in t["table"]}
+    assert swept == {nb for nb in (32, 64, 128, 256) if nb * nsim <= 1024}
+    assert {r["bytes"] for r in t["table"]} == {256 << 10, 1 << 20, 64 << 20}
+    assert g["xgmi_nblk"] in swept and g["xgmi_one_shot_max_bytes"] in (0, 256 << 10, 1 << 20)
+    # the chosen point is the fastest total over the three sizes
+    def total(nb, cut):
+        tt = {(r["bytes"], r["algo"]): r["time_us"] for r in t["table"] if r["nblk"] == nb}
+        return sum(tt[(b, "1shot" if b <= cut else "2shot")] for b in (256 << 10, 1 << 20, 64 << 20))
+    best = min(total(nb, c) for nb in swept for c in (0, 256 << 10, 1 << 20))
+    assert total(g["xgmi_nblk"], g["xgmi_one_shot_max_bytes"]) == pytest.approx(best)
+    rows = g["xgmi_allreduce_bf16"]
+    assert rows and all(r["wrong"] == 0 for r in rows)
+    one = [r["bytes"] for r in rows if r["dtype"] == "bf16-1shot"]
+    assert all(b <= g["xgmi_one_shot_max_bytes"] for b in one)
+
+
+@pytest.mark.gpu
 def test_binary_reports_and_enforces_host_prep():
     """The in-pod host-prep check (--require-host-prep): the report always
     carries what the pod sees; the flag fails the Job exactly when a setting is

@@ -8,7 +8,7 @@ pytestmark = pytest.mark.gpu
 
 @pytest.mark.parametrize("nranks", [1, 2, 4, 8])
 @pytest.mark.parametrize("one_shot", [False, True])
-@pytest.mark.parametrize("nblk", [16, 32, 64, 128])   # xgmi.TUNE_NBLKS: every swept value
+@pytest.mark.parametrize("nblk", [16, 32, 64, 128, 256])   # xgmi.TUNE_NBLKS: every swept value
 def test_simulated_allreduce_matches_fp32_sum(nranks, one_shot, nblk):
     from nvidia_terraform_modules_amd import ops
     from nvidia_terraform_modules_amd.parallel.xgmi import TUNE_NBLKS, simulate_allreduce
@@ -118,8 +118,66 @@ def test_ipc_allreduce_processes(world):
         # bench.py's N > 1 C2 knob sweep (xgmi.tune), every co-resident nblk
         tune = rep["tune"]
         assert tune["errors"] == 0 and not tune["timed_out"], tune
-        assert {t["nblk"] for t in tune["table"]} == {nb for nb in (16, 32, 64, 128)
-                                                      if nb * world <= 1024}
+        from nvidia_terraform_modules_amd.parallel.xgmi import TUNE_NBLKS
+
+        assert {t["nblk"] for t in tune["table"]} == {nb for nb in TUNE_NBLKS if nb * world <= 1024}
+        assert tune["best_nblk"] in {t["nblk"] for t in tune["table"]}
+
+
+@pytest.mark.parametrize("one_shot", [False, True])
+@pytest.mark.parametrize("nranks", [2, 8])
+def test_missing_rank_times_out_with_nan(nranks, one_shot):
+    """Failure contract: a rank that never launches. The others'
+    entry barrier gives up after the (short, per-call) spin limit, reports
+    phase 1 and fills every output element they own with NaN - never a
+    silently partial sum. The limits are kernel arguments, so this takes
+    milliseconds instead of the default minutes."""
+    from nvidia_terraform_modules_amd.parallel.xgmi import simulate_allreduce
+
+    count = 8 * nranks * 1024
+    ins = [torch.ones(count, dtype=torch.bfloat16, device="cuda") for _ in range(nranks)]
+    outs, err = simulate_allreduce(ins, nblk=8, one_shot=one_shot, nranks_here=nranks - 1,
+                                   spin_limit=4096, entry_spin_limit=4096)
+    assert err == 1                                   # the entry barrier
+    for o in outs[:nranks - 1]:                       # the ranks that ran
+        assert torch.isnan(o.float()).all()
+
+
+def test_ipc_missing_rank_raises():
+    """The same across two PROCESSES (IPC): rank 1 never calls; rank 0's
+    ``ar(t, check=True)`` raises, names the entry phase, and its tensor is NaN."""
+    import json
+    import os
+    import socket
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    worker = Path(__file__).with_name("xgmi_timeout_worker.py")
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = [subprocess.Popen([sys.executable, str(worker)],
+                              env=dict(os.environ, RANK=str(r), WORLD_SIZE="2",
+                                       MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                                       GPU_MAX_HW_QUEUES="1"),
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+             for r in range(2)]
+    outs = []
+    try:
+        for p in procs:
+            o, e = p.communicate(timeout=120)
+            assert p.returncode == 0, e[-3000:]
+            outs.append(json.loads(o.strip().splitlines()[-1]))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    r0 = next(r for r in outs if r["rank"] == 0)
+    for k in ("0", "1"):
+        assert "entry phase" in r0["raised_" + k] and "NaN" in r0["raised_" + k], r0
+        assert r0["all_nan_" + k], r0
+    assert r0["timed_out"] is True
 
 
 @pytest.mark.parametrize("nranks", [2, 8])

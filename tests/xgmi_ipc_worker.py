@@ -54,7 +54,7 @@ def main():
     tr = tune(env, sizes=(64 << 10, 1 << 20), nblks=[nb for nb in TUNE_NBLKS if nb * n <= 1024],
               iters=2, warmup=1)
     print(json.dumps({"rank": env.rank, "results": results,
-                      "tune": {k: tr[k] for k in ("table", "errors", "timed_out")}}), flush=True)
+                      "tune": {k: tr[k] for k in ("table", "errors", "timed_out", "best_nblk")}}), flush=True)
     shutdown(env)
 
 

@@ -152,6 +152,53 @@ __device__ __forceinline__ void store_pair(const GemmArgs& p, const f32x4 (&q)[2
   }
 }
 
+// STG (LINE layout only): the same two quadrants leave through a per-wave 2 KiB
+// LDS slot past the kernel's 144 KiB (kStgBase: LDS is 160 KiB per CU), so
+// each 16-lane store pass writes two WHOLE 128-B lines instead of 16 rows x
+// 16 B. Register-stored C wrote 154-157 MB per 8192^3 call against the
+// LDS-staged epilogue's exact 128 MB (profiles/r3_pmc, r4_line). Per 16-row
+// block: 2 ds_write_b128 (the lane's NH 0 / 1 pieces of row lane & 15), 2
+// ds_read_b128 (lane l: row l >> 3 (+8), 16-B chunk l & 7), 2 global stores;
+// rows are XOR-swizzled by (row & 7) << 4. A wave only touches its own slot,
+// in program order, so no barrier is needed.
+constexpr int kStgBase = kLdsBytes3;          // 144 KiB
+constexpr int kStgBytes = kStgBase + 8 * 2048;  // 160 KiB: the whole LDS of a CU
+
+template <int MH, int POL>
+__device__ __forceinline__ void store_pair_lds(const GemmArgs& p, char* slot,
+                                               const f32x4 (&q)[2][4][2], int m0, int n0,
+                                               int c_lane2, int lane) {
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  const int r = lane & 15, g = lane >> 4;
+  const int wsw = (r & 7) << 4;
+  const int w0 = r * 128 + ((((g & 1) * 32 + (g >> 1) * 16)) ^ wsw);
+  const int rr = lane >> 3, ch = (lane & 7) * 16;
+  const int r0 = rr * 128 + (ch ^ ((rr & 7) << 4));
+  const int r1 = (rr + 8) * 128 + (ch ^ (((rr + 8) & 7) << 4));
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) {
+#pragma unroll
+    for (int nh = 0; nh < 2; ++nh) {
+      const f32x4 v0 = q[nh][mt][0], v1 = q[nh][mt][1];
+      unsigned a[2], b[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const auto x = __builtin_amdgcn_permlane16_swap(pack_bf16x2(v0[2 * h], v0[2 * h + 1]),
+                                                        pack_bf16x2(v1[2 * h], v1[2 * h + 1]),
+                                                        false, false);
+        a[h] = x[0];
+        b[h] = x[1];
+      }
+      *(u32x4*)(slot + (w0 ^ (nh * 64))) = u32x4{a[0], a[1], b[0], b[1]};
+    }
+    const u32x4 lo = *(const u32x4*)(slot + r0);
+    const u32x4 hi = *(const u32x4*)(slot + r1);
+    __bf16* tile = p.C + (size_t)(m0 + MH * 128 + mt * 16) * p.ldc + n0 + c_lane2;
+    store_c16<POL>(tile, lo);
+    store_c16<POL>(tile + (size_t)8 * p.ldc, hi);
+  }
+}
+
 // Zero a stored quadrant in place (32 v_mov): an MFMA with an inline-zero C
 // operand instead lets hipcc give the result fresh registers, and the copies
 // back at the loop's back edge spilled.
@@ -177,10 +224,10 @@ struct Edge {
 // 0 / 1) or e.has_next (K-tile T-1); VMC: the counted wait when ON (10
 // otherwise); NX: this phase's piece is past the tile (issue6). A stored
 // quadrant is zeroed for the next tile.
-template <int P, bool ODD, int CONV, int VMC, bool NX, int POL, bool LINE>
+template <int P, bool ODD, int CONV, int VMC, bool NX, int POL, bool LINE, bool STG = false>
 __device__ __forceinline__ void phase6(const GemmArgs& p, const Ctx& c, Frags3& f,
                                        f32x4 (&acc)[2][2][4][2], int t, int T, const Edge& e,
-                                       bool on, int c_lane) {
+                                       bool on, int c_lane, int c_lane2 = 0, int lane = 0) {
   bf16x8(&bcur)[2][2] = ODD ? f.b1 : f.b0;
   bf16x8(&both)[2][2] = ODD ? f.b0 : f.b1;
   const int cur = t & 1;
@@ -206,6 +253,8 @@ __device__ __forceinline__ void phase6(const GemmArgs& p, const Ctx& c, Frags3& 
       const int m0 = MH == 1 ? e.pm0 : e.m0, n0 = MH == 1 ? e.pn0 : e.n0;
       if constexpr (POL == 2) {  // ablation (experimental library): C not stored
         if (p.ldc < 0) store_pair<MH, 1>(p, acc[MH], m0, n0, c_lane);
+      } else if constexpr (STG) {
+        store_pair_lds<MH, POL>(p, c.lds + kStgBase + c.w * 2048, acc[MH], m0, n0, c_lane2, lane);
       } else {
         store_pair<MH, POL>(p, acc[MH], m0, n0, c_lane);
       }
@@ -236,7 +285,7 @@ __device__ __forceinline__ void phase6(const GemmArgs& p, const Ctx& c, Frags3& 
 }
 
 #define NTM_PH(P, ODD, CV, VMC, NX, ON) \
-  phase6<P, ODD, CV, VMC, NX, POL, LINE>(p, c, f, acc, t, T, e, ON, c_lane)
+  phase6<P, ODD, CV, VMC, NX, POL, LINE, STG>(p, c, f, acc, t, T, e, ON, c_lane, c_lane2, lane)
 
 __device__ __forceinline__ void tile_origin(const GemmArgs& p, int tile, int ntiles, int& m0,
                                             int& n0) {
@@ -275,9 +324,11 @@ __device__ __forceinline__ void clock_stamp(unsigned long long& t, unsigned long
 // d(realtime) x 100 MHz.
 // An fp8 build of this structure did not fit: pingpong8c's fp8 consumer already
 // holds 128 VGPRs + 128 AGPRs, and the boundary conversion spilled 76 VGPRs.
-template <int POL, bool LINE = false, int STAMP = 0>
+// STG (LINE only): boundary stores staged through LDS in whole lines (store_pair_lds).
+template <int POL, bool LINE = false, int STAMP = 0, bool STG = false>
 __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_pp6_kernel(GemmArgs p) {
-  __shared__ __attribute__((aligned(16))) char smem[kLdsBytes3];
+  static_assert(!STG || LINE, "LDS-staged boundary stores need the whole-line layout");
+  __shared__ __attribute__((aligned(16))) char smem[STG ? kStgBytes : kLdsBytes3];
   unsigned long long t0 = 0, rt0 = 0;
   if constexpr (STAMP != 0) clock_stamp(t0, rt0);
   const int ntiles = (p.M / BM) * (p.N / BN);
@@ -306,6 +357,8 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_pp6_kernel(GemmArgs p) 
   c.frag_off = (lane & 15) * 64 + ((lane >> 4) ^ ((lane >> 2) & 2)) * 16;
   const int c_lane = (c.wr * 64 + (lane & 15)) * p.ldc + c.wc * (LINE ? 64 : 32) +
                      ((lane >> 4) & 1) * 16 + (lane >> 5) * 8;
+  // STG: row lane >> 3 of the 16-row block, 8-column chunk lane & 7
+  const int c_lane2 = (c.wr * 64 + (lane >> 3)) * p.ldc + c.wc * 64 + (lane & 7) * 8;
 
   f32x4 acc[2][2][4][2];
 #pragma unroll
@@ -440,13 +493,13 @@ inline hipError_t launch_gemm_bf16_pp6_grid(const GemmArgs& a, int grid, hipStre
   return hipGetLastError();
 }
 
-template <int POL, bool LINE = false, int STAMP = 0>
+template <int POL, bool LINE = false, int STAMP = 0, bool STG = false>
 inline hipError_t launch_gemm_bf16_pp6(const GemmArgs& a, hipStream_t stream) {
   if (!shape_ok6(a.M, a.N, a.K) || a.rowsum || a.lda < a.K || a.ldb < a.K || a.ldc < a.N ||
       (a.lda % 8) || (a.ldb % 8) || (a.ldc % 8) || (STAMP != 0 && a.stamps == nullptr))
     return hipErrorInvalidValue;
   const int ntiles = (a.M / BM) * (a.N / BN);
-  hipLaunchKernelGGL((gemm_bf16_pp6_kernel<POL, LINE, STAMP>), dim3((unsigned)pp6_grid(ntiles)),
+  hipLaunchKernelGGL((gemm_bf16_pp6_kernel<POL, LINE, STAMP, STG>), dim3((unsigned)pp6_grid(ntiles)),
                      dim3(kThreads), 0, stream, a);
   return hipGetLastError();
 }

@@ -48,12 +48,19 @@ namespace xgmi {
 constexpr int kMaxRanks = 8;
 constexpr int kThreads = 256;
 constexpr int kPhases = 3;                 // entry, reduce-scatter done, exit
-// Spin limits (s_sleep 2 + one uncached load per spin). The ENTRY barrier
-// absorbs host-side skew between ranks (a checkpoint, a GC pause, uneven work
-// before the call): it waits 16x longer (~minutes) than the in-kernel phases,
-// which only wait for peers already running the same kernel (~seconds).
+// Default spin limits (s_sleep 2 + one uncached load per spin). The ENTRY
+// barrier absorbs host-side skew between ranks (a checkpoint, a GC pause,
+// uneven work before the call): it waits 16x longer (~minutes) than the
+// in-kernel phases, which only wait for peers already running the same kernel
+// (~seconds). Both are kernel arguments (0 = these defaults), so a test can
+// time a missing rank out in milliseconds.
 constexpr unsigned kSpinLimit = 1u << 24;
 constexpr unsigned kEntrySpinLimit = 1u << 28;
+
+struct Limits {
+  unsigned spin;   // reduce-scatter / exit barriers
+  unsigned entry;  // entry barrier
+};
 // A block whose barrier times out never leaves a stale sum behind: it fills
 // the part of the output it owns with bf16 NaN (0x7FC0), so a caller that does
 // not read the error word still cannot consume partial sums silently.
@@ -121,7 +128,7 @@ __device__ __forceinline__ bool cross_rank_barrier(const Peers& p, int nranks,
 // grid = nranks_here * nblk blocks; rank = rank_base + blockIdx.x / nblk.
 __global__ void __launch_bounds__(kThreads)
     allreduce_2shot_kernel(Peers p, int nranks, int rank_base, int nblk,
-                           size_t count, unsigned epoch, unsigned* err) {
+                           size_t count, unsigned epoch, unsigned* err, Limits lim) {
   const int rank = rank_base + (int)(blockIdx.x / nblk);
   const int b = (int)(blockIdx.x % nblk);
   const size_t chunk = count / nranks;        // elements per rank chunk
@@ -142,7 +149,7 @@ __global__ void __launch_bounds__(kThreads)
         ((u16x8*)p.out[rank])[(size_t)q * chunk / 8 + v] = nan8;
   };
   // phase 0 (entry): every peer's input for this epoch is complete
-  if (!cross_rank_barrier(p, nranks, rank, b, nblk, 0, epoch, err, kEntrySpinLimit)) {
+  if (!cross_rank_barrier(p, nranks, rank, b, nblk, 0, epoch, err, lim.entry)) {
     poison();
     return;
   }
@@ -158,7 +165,7 @@ __global__ void __launch_bounds__(kThreads)
     }
     ((u16x8*)p.out[rank])[base + v] = pack8(acc);
   }
-  if (!cross_rank_barrier(p, nranks, rank, b, nblk, 1, epoch, err)) {
+  if (!cross_rank_barrier(p, nranks, rank, b, nblk, 1, epoch, err, lim.spin)) {
     poison();
     return;
   }
@@ -170,8 +177,10 @@ __global__ void __launch_bounds__(kThreads)
     for (size_t v = v0 + threadIdx.x; v < v1; v += kThreads)
       ((u16x8*)p.out[rank])[qb + v] = ((const u16x8*)p.out[q])[qb + v];
   }
-  // phase 2 (exit): nobody may overwrite its buffers before all peers copied
-  cross_rank_barrier(p, nranks, rank, b, nblk, 2, epoch, err);
+  // phase 2 (exit): nobody may overwrite its buffers before all peers copied.
+  // A timeout here leaves a COMPLETE output (error code 3): only the buffers
+  // may still be read by a late peer, so nothing is poisoned.
+  cross_rank_barrier(p, nranks, rank, b, nblk, 2, epoch, err, lim.spin);
 }
 
 // One-shot all-reduce (small messages): every rank reads ALL of every peer's
@@ -179,11 +188,11 @@ __global__ void __launch_bounds__(kThreads)
 // are complete; exit barrier: no peer still reads my input when I return.
 __global__ void __launch_bounds__(kThreads)
     allreduce_1shot_kernel(Peers p, int nranks, int rank_base, int nblk,
-                           size_t count, unsigned epoch, unsigned* err) {
+                           size_t count, unsigned epoch, unsigned* err, Limits lim) {
   const int rank = rank_base + (int)(blockIdx.x / nblk);
   const int b = (int)(blockIdx.x % nblk);
   const size_t nvec = count / 8;
-  if (!cross_rank_barrier(p, nranks, rank, b, nblk, 0, epoch, err, kEntrySpinLimit)) {
+  if (!cross_rank_barrier(p, nranks, rank, b, nblk, 0, epoch, err, lim.entry)) {
     u16x8 nan8;
 #pragma unroll
     for (int i = 0; i < 8; ++i) nan8[i] = kPoison;
@@ -198,7 +207,7 @@ __global__ void __launch_bounds__(kThreads)
     for (int q = 0; q < nranks; ++q) add8(acc, ((const u16x8*)p.in[q])[v]);
     ((u16x8*)p.out[rank])[v] = pack8(acc);
   }
-  cross_rank_barrier(p, nranks, rank, b, nblk, 2, epoch, err);
+  cross_rank_barrier(p, nranks, rank, b, nblk, 2, epoch, err, lim.spin);
 }
 
 // bytes of one rank's signal area for `nblk` blocks per rank

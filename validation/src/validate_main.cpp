@@ -120,6 +120,7 @@ struct Opts {
   double xgmi_busbw_floor_gbps = 0;  // C2: the same for the hand-written all-reduce
   int xgmi_nblk = 64;                // C2 blocks per rank (bench.py sweeps it at N > 1)
   long xgmi_one_shot_max = 256 << 10;  // C2: messages <= this take the one-shot kernel
+  bool xgmi_tune = false;            // C2: mini-sweep nblk x cutoff first, then run the best
   bool require_host_prep = false;    // fail unless numa_balancing = 0 and memlock unlimited
   bool require_iommu_pt = false;     // ... and the kernel booted with iommu=pt
   bool describe_sweep = false;       // print the C1/C2 size lists + busbw factors, no GPU
@@ -139,7 +140,7 @@ void usage() {
                "       [--settle-s S] [--no-fp8] [--fp8-tflops-floor TF]\n"
                "       [--no-p2p] [--p2p-mib MiB] [--p2p-floor-gbps GBps] [--p2p-loopback]\n"
                "       [--rccl-busbw-floor-gbps GBps] [--xgmi-busbw-floor-gbps GBps]\n"
-               "       [--xgmi-nblk N] [--xgmi-one-shot-max BYTES]\n"
+               "       [--xgmi-nblk N] [--xgmi-one-shot-max BYTES] [--xgmi-tune]\n"
                "       [--require-host-prep] [--require-iommu-pt] [--describe-sweep]\n"
                "       [--json] [--out FILE]\n"
                "       [--termination-log FILE] [--prom-out FILE] [--fault-inject KIND]\n"
@@ -181,6 +182,7 @@ bool parse(int argc, char** argv, Opts& o) {
     else if (a == "--xgmi-busbw-floor-gbps") { if (!(v = next(a.c_str()))) return false; o.xgmi_busbw_floor_gbps = std::atof(v); }
     else if (a == "--xgmi-nblk") { if (!(v = next(a.c_str()))) return false; o.xgmi_nblk = std::atoi(v); }
     else if (a == "--xgmi-one-shot-max") { if (!(v = next(a.c_str()))) return false; o.xgmi_one_shot_max = std::atol(v); }
+    else if (a == "--xgmi-tune") o.xgmi_tune = true;
     else if (a == "--require-host-prep") o.require_host_prep = true;
     else if (a == "--require-iommu-pt") o.require_iommu_pt = true;
     else if (a == "--describe-sweep") o.describe_sweep = true;
@@ -781,7 +783,17 @@ std::string p2p_json(const P2pResult& r) {
 // <= --xgmi-one-shot-max (256 KiB) takes the one-shot kernel. The kernel
 // synchronises the ranks itself (device-side entry barrier), so the timed
 // loop launches back to back with no host sync.
-bool run_xgmi(const std::vector<int>& devs, const Opts& o, std::vector<CollRow>& rows) {
+// --xgmi-tune: what the mini-sweep chose (and its table) for the JSON report.
+struct XgmiTune {
+  bool ran = false;
+  int nblk = 0;
+  size_t one_shot_max = 0;
+  double seconds = 0;
+  std::string table = "[]";
+};
+
+bool run_xgmi(const std::vector<int>& devs, const Opts& o, std::vector<CollRow>& rows,
+              XgmiTune& tune) {
   const bool sim = o.xgmi_sim > 0;
   const int n = sim ? o.xgmi_sim : (int)devs.size();
   if (n < 1 || n > ntm::xgmi::kMaxRanks) return true;
@@ -804,8 +816,16 @@ bool run_xgmi(const std::vector<int>& devs, const Opts& o, std::vector<CollRow>&
   // blocks per rank and the one-shot cutoff are knobs (--xgmi-nblk,
   // --xgmi-one-shot-max): bench.py sweeps them at N > 1, so the first 8-GPU
   // run says whether the design or the constant is at fault
-  const int nblk = sim ? std::min(o.xgmi_nblk, 1024 / n) : o.xgmi_nblk;
-  const size_t one_shot_max = (size_t)std::max(0L, o.xgmi_one_shot_max);
+  // --xgmi-tune: a mini-sweep (blocks per rank 32..256 x one-/two-shot at
+  // 256 KiB, 1 MiB and 64 MiB, a few calls each, well under 2 s at N = 8)
+  // picks both before the main sweep, like bench.py's xgmi.tune does at N > 1.
+  // One signal area sized for the largest candidate serves every nblk: slots
+  // only alias across calls, and epochs only grow.
+  constexpr int kTuneNblk[] = {32, 64, 128, 256};
+  const int nblk_cap = sim ? 1024 / n : 1024;
+  int nblk = std::min(o.xgmi_nblk, nblk_cap);
+  size_t one_shot_max = (size_t)std::max(0L, o.xgmi_one_shot_max);
+  const int sig_nblk = o.xgmi_tune ? std::max(nblk, std::min(256, nblk_cap)) : nblk;
   std::vector<int> used(devs.begin(), devs.begin() + ndev);
   const size_t maxb = sweep_cap(used, std::min<size_t>((size_t)o.allreduce_max_mib << 20,
                                                        (size_t)1 << 30), sim ? 2 * n : 2);
@@ -825,11 +845,80 @@ bool run_xgmi(const std::vector<int>& devs, const Opts& o, std::vector<CollRow>&
     CK(hipMalloc(&in[r], maxb));
     CK(hipMalloc(&out[r], maxb));
     CK(hipMalloc(&bad[r], 8));
-    CK(hipExtMallocWithFlags((void**)&sig[r], ntm_xgmi_signal_bytes(nblk), hipDeviceMallocUncached));
-    CK(hipMemset(sig[r], 0, ntm_xgmi_signal_bytes(nblk)));
+    CK(hipExtMallocWithFlags((void**)&sig[r], ntm_xgmi_signal_bytes(sig_nblk), hipDeviceMallocUncached));
+    CK(hipMemset(sig[r], 0, ntm_xgmi_signal_bytes(sig_nblk)));
   }
   unsigned epoch = 0;
   bool ok = true;
+  if (o.xgmi_tune) {
+    // time `calls` back-to-back launches at (nb, bytes, one-shot); < 0 on failure
+    auto time_point = [&](int nb, size_t bytes, int os, int calls) -> double {
+      const size_t cnt = bytes / 2;
+      auto launch = [&]() -> bool {
+        ++epoch;
+        for (int i = 0; i < ndev; ++i)
+          if (hipSetDevice(devs[i]) != hipSuccess ||
+              ntm_xgmi_allreduce_bf16((const void* const*)in.data(), os ? out.data() : (void* const*)in.data(),
+                                      sig.data(), n, sim ? 0 : i, sim ? n : 1, nb, cnt, epoch,
+                                      err[i], os, st[i]) != 0)
+            return false;
+        return true;
+      };
+      auto sync = [&]() -> bool {
+        for (int i = 0; i < ndev; ++i)
+          if (hipSetDevice(devs[i]) != hipSuccess || hipStreamSynchronize(st[i]) != hipSuccess)
+            return false;
+        return true;
+      };
+      if (!launch() || !sync()) return -1;
+      const auto t0 = Clock::now();
+      for (int c = 0; c < calls; ++c)
+        if (!launch()) return -1;
+      if (!sync()) return -1;
+      return std::chrono::duration<double>(Clock::now() - t0).count() / calls;
+    };
+    const auto t_tune = Clock::now();
+    std::vector<size_t> tsizes;
+    for (const size_t b : {(size_t)256 << 10, (size_t)1 << 20, (size_t)64 << 20})
+      if (b <= maxb && (b / 2) % (8 * (size_t)n) == 0) tsizes.push_back(b);
+    const size_t cuts[] = {0, (size_t)256 << 10, (size_t)1 << 20};
+    double best_t = 1e300;
+    std::string tab = "[";
+    for (const int nb : kTuneNblk) {
+      if (nb > nblk_cap || !ok) continue;
+      double t1[3] = {1e300, 1e300, 1e300}, t2[3] = {1e300, 1e300, 1e300};
+      for (size_t k = 0; k < tsizes.size() && ok; ++k)
+        for (const int os : {1, 2}) {
+          if (os == 1 && tsizes[k] > ((size_t)1 << 20)) continue;
+          const double t = time_point(nb, tsizes[k], os == 1, 3);
+          if (t < 0) { fail("xGMI tune launch failed"); ok = false; break; }
+          (os == 1 ? t1 : t2)[k] = t;
+          tab += std::string(tab.size() > 1 ? "," : "") + "{\"nblk\":" + std::to_string(nb) +
+                 ",\"bytes\":" + std::to_string(tsizes[k]) + ",\"algo\":\"" +
+                 (os == 1 ? "1shot" : "2shot") + "\",\"time_us\":" + jnum(t * 1e6) + "}";
+        }
+      for (const size_t c : cuts) {
+        double tot = 0;
+        for (size_t k = 0; k < tsizes.size(); ++k) tot += tsizes[k] <= c ? t1[k] : t2[k];
+        if (tot < best_t) {
+          best_t = tot;
+          nblk = nb;
+          one_shot_max = c;
+        }
+      }
+    }
+    tune.table = tab + "]";
+    tune.ran = ok && !tsizes.empty();
+    tune.seconds = std::chrono::duration<double>(Clock::now() - t_tune).count();
+    for (int i = 0; i < ndev && ok; ++i) {   // a tune call that timed out fails the run
+      unsigned e = 0;
+      CK(hipSetDevice(devs[i]));
+      CK(hipMemcpy(&e, err[i], 4, hipMemcpyDeviceToHost));
+      if (e) { fail("xGMI tune: barrier timed out (code " + std::to_string(e) + ")"); ok = false; }
+    }
+  }
+  tune.nblk = nblk;
+  tune.one_shot_max = one_shot_max;
   for (const size_t bytes : xgmi_sizes(maxb, n)) {
     if (!ok) break;
     const size_t cnt = bytes / 2;
@@ -1112,7 +1201,8 @@ int main(int argc, char** argv) {
   // same code path; its ~2 s RCCL init is not worth paying in a 1-GPU Job)
   if (o.rccl == 1 || (o.rccl < 0 && n > 1)) run_rccl(devs, o, rccl_rows);
   const double t_rccl = wall_now();
-  if (o.xgmi && (n > 1 || o.xgmi_sim > 0)) run_xgmi(devs, o, xgmi_rows);
+  XgmiTune xtune;
+  if (o.xgmi && (n > 1 || o.xgmi_sim > 0)) run_xgmi(devs, o, xgmi_rows, xtune);
   P2pResult p2p;
   if (o.p2p && (n > 1 || o.p2p_loopback)) run_p2p(devs, o, p2p);
   const double t_end = wall_now();
@@ -1203,8 +1293,11 @@ int main(int argc, char** argv) {
   js += "],\"rccl_allreduce\":" + coll_json(rccl_rows);
   js += ",\"xgmi_allreduce_bf16\":" + coll_json(xgmi_rows);
   js += ",\"xgmi_simulated_ranks\":" + std::to_string(o.xgmi_sim);
-  js += ",\"xgmi_nblk\":" + std::to_string(o.xgmi_nblk) +
-        ",\"xgmi_one_shot_max_bytes\":" + std::to_string(o.xgmi_one_shot_max);
+  js += ",\"xgmi_nblk\":" + std::to_string(xtune.nblk ? xtune.nblk : o.xgmi_nblk) +
+        ",\"xgmi_one_shot_max_bytes\":" +
+        std::to_string(xtune.nblk ? (long)xtune.one_shot_max : o.xgmi_one_shot_max);
+  js += ",\"xgmi_tune\":{\"ran\":" + std::string(xtune.ran ? "true" : "false") +
+        ",\"seconds\":" + jnum(xtune.seconds) + ",\"table\":" + xtune.table + "}";
   js += ",\"rccl_peak_busbw_bf16_GBps\":" + jnum(rccl_peak_bf16) +
         ",\"xgmi_peak_busbw_bf16_GBps\":" + jnum(xgmi_peak_bf16);
   js += ",\"host_prep\":{\"numa_balancing\":" + std::to_string(hp.numa_balancing) +

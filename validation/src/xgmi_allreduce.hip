@@ -14,12 +14,15 @@
 // one-shot needs in != out. Every call on a communicator uses a fresh, larger
 // epoch and the same nblk on all ranks. The kernel synchronises the ranks on
 // the device (entry barrier), so callers need no host sync or host barrier.
-NTM_API int ntm_xgmi_allreduce_bf16(const void* const* in_ptrs,
-                                    void* const* out_ptrs,
-                                    unsigned* const* sig_ptrs, int nranks,
-                                    int rank_base, int nranks_here, int nblk,
-                                    size_t count, unsigned epoch, unsigned* err,
-                                    int one_shot, void* stream) {
+// ntm_xgmi_allreduce_bf16_ex: the same with the barrier spin limits as
+// arguments (0 = the defaults of xgmi_allreduce.hpp): a missing rank then
+// times out in milliseconds (tests), and error code 1 / 2 poisons the owned
+// output with NaN while 3 (exit barrier) leaves a complete result.
+NTM_API int ntm_xgmi_allreduce_bf16_ex(const void* const* in_ptrs, void* const* out_ptrs,
+                                       unsigned* const* sig_ptrs, int nranks, int rank_base,
+                                       int nranks_here, int nblk, size_t count, unsigned epoch,
+                                       unsigned* err, int one_shot, unsigned spin_limit,
+                                       unsigned entry_spin_limit, void* stream) {
   using namespace ntm::xgmi;
   if (nranks < 1 || nranks > kMaxRanks || nranks_here < 1 || rank_base < 0 ||
       rank_base + nranks_here > nranks || nblk < 1 || nranks_here * nblk > 1024 || epoch == 0 ||
@@ -35,15 +38,25 @@ NTM_API int ntm_xgmi_allreduce_bf16(const void* const* in_ptrs,
     p.sig[r] = sig_ptrs[r];
   }
   const dim3 grid((unsigned)(nranks_here * nblk));
+  const Limits lim{spin_limit ? spin_limit : kSpinLimit,
+                   entry_spin_limit ? entry_spin_limit : kEntrySpinLimit};
   if (one_shot) {
     hipLaunchKernelGGL(allreduce_1shot_kernel, grid, dim3(kThreads), 0,
-                       (hipStream_t)stream, p, nranks, rank_base, nblk, count, epoch, err);
+                       (hipStream_t)stream, p, nranks, rank_base, nblk, count, epoch, err, lim);
   } else {
     hipLaunchKernelGGL(allreduce_2shot_kernel, grid, dim3(kThreads), 0,
                        (hipStream_t)stream, p, nranks, rank_base, nblk, count,
-                       epoch, err);
+                       epoch, err, lim);
   }
   return (int)hipGetLastError();
+}
+
+NTM_API int ntm_xgmi_allreduce_bf16(const void* const* in_ptrs, void* const* out_ptrs,
+                                    unsigned* const* sig_ptrs, int nranks, int rank_base,
+                                    int nranks_here, int nblk, size_t count, unsigned epoch,
+                                    unsigned* err, int one_shot, void* stream) {
+  return ntm_xgmi_allreduce_bf16_ex(in_ptrs, out_ptrs, sig_ptrs, nranks, rank_base, nranks_here,
+                                    nblk, count, epoch, err, one_shot, 0u, 0u, stream);
 }
 
 NTM_API size_t ntm_xgmi_signal_bytes(int nblk) {
