@@ -110,8 +110,6 @@ def _declare_experimental(lib: ctypes.CDLL) -> None:
         "ntm_gemm_bf16_ws_knob": ([c_int] + gemm, c_int),
         "ntm_gemm_bf16_stamp": (
             [c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp], c_int),
-        "ntm_gemm_r4k_stamp": (
-            [c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp], c_int),
         "ntm_mfma_f8_probe": ([c_vp, c_vp, c_vp, c_vp], c_int),
         "ntm_mfma_rate": ([c_int, c_int, c_int, c_vp, c_vp, c_vp], c_int),
         "ntm_gemm_fp8_knob": ([c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int,

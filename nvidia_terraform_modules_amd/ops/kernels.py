@@ -36,7 +36,7 @@ GEMM_VARIANTS = {"default": 0, "pingpong8": 1, "pingpong8b": 4,
                  "tile256x128": 16, "tile160": 17, "tile256x160": 18, "tile128w4": 19,
                  "tile256x128w4": 20, "tile160w4": 21, "pingpong8cm": 22, "tile160x128": 23,
                  "tile128x160": 24, "tile128x256": 26, "dma4k_d3": 39, "pingpong8o": 25,
-                 "dma4ko": 40, "pp8o_g128": 41, "pp8o_g128_nostore": 42, "pp8o_nostore": 43,
+                 "pp8o_g128": 41, "pp8o_g128_nostore": 42, "pp8o_nostore": 43,
                  "pingpong8ol": 44, "pp8ol_nostore": 45, "pingpong8ols": 46}
 
 
@@ -45,7 +45,7 @@ GEMM_VARIANTS = {"default": 0, "pingpong8": 1, "pingpong8b": 4,
 EXPERIMENTAL_VARIANTS = frozenset({"pingpong8", "pingpong8cw",
                                    "pingpong8cwe", "pingpong8cwn", "pingpong8cwne",
                                    "tile128w4", "tile256x128w4", "tile160w4", "dma4k_d3",
-                                   "dma4ko", "pp8o_g128", "pp8o_g128_nostore", "pp8o_nostore",
+                                   "pp8o_g128", "pp8o_g128_nostore", "pp8o_nostore",
                                    "pingpong8ol", "pp8ol_nostore", "pingpong8ols"})
 
 # (TM, TN) of the 4-wave tile kernels (gemm_bf16_t128.hpp)
@@ -125,7 +125,7 @@ def gemm_bf16(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
     schedule; 8c adds parity-alternating B buffers and a tail-free K loop),
     "pingpong8" (the first 12/4/8/0 schedule), or the experimental
     "dma4k_d3" (4 waves, 128x128 per wave, one barrier per K-tile, LDS-DMA
-    operands) and its persistent overlap build "dma4ko" - see validation/include.
+    operands) - see validation/include.
     ``splits`` > 1 (masked tiles only): split-K into that many K slices, fp32
     partials in a workspace from PyTorch's allocator, then one reduction kernel.
     """

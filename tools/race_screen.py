@@ -70,7 +70,7 @@ def main():
 
         tm, tn = ops.kernels.TILE_SHAPES.get(v, (0, 0))
         shapes = SHAPES_FP8 + SHAPES_RAGGED if fp8 else SHAPES_160 if tn == 160 else SHAPES
-        if v.startswith("pingpong8o") or v == "dma4ko":
+        if v.startswith("pingpong8o"):
             shapes = SHAPES_PERSIST
         if splits > 1:
             shapes = SHAPES_SPLITK + SHAPES_RAGGED

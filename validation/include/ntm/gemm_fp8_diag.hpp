@@ -12,7 +12,6 @@
 #include "ntm/gemm_bf16_pp3.hpp"
 #include "ntm/gemm_fp8.hpp"
 #include "ntm/gemm_w4k.hpp"
-#include "ntm/gemm_w4o.hpp"
 
 namespace ntm {
 namespace fp8 {
@@ -55,8 +54,6 @@ inline hipError_t launch_gemm_fp8_knob(const void* A, const void* B, __bf16* C, 
     case 0: return launch_gemm_fp8(A, B, C, M, N, K, lda, ldb, ldc, s);
     // 12: the 4-wave one-barrier-per-K-tile kernel, DMA every 2 MFMAs (gemm_w4k.hpp)
     case 12: return ::ntm::w4k::launch_gemm_fp8_w4k<2>(A, B, C, M, N, K, lda, ldb, ldc, s);
-    // 22: knob 12 made persistent, C stores overlapping the next tile's K loop (gemm_w4o.hpp)
-    case 22: return ::ntm::w4o::launch_gemm_fp8_w4o<2>(A, B, C, M, N, K, lda, ldb, ldc, s);
     case 1: hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, kGroupM, false, kEpiDefault, 0, 2>), g, b, 0, s, a); break;
     case 2: hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, 4, false, kEpiDefault, 0, 1>), g, b, 0, s, a); break;
     case 3: hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, kGroupM, false, kEpiDefault, 2, 1>), g, b, 0, s, a); break;

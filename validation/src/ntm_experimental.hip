@@ -8,9 +8,9 @@
 //   10..13 pingpong8c epilogue knobs: widened / + early row-0 stores /
 //          nontemporal stores / both (gemm_bf16_pp3.hpp launch_gemm_bf16_pp3_knob)
 //   39     dma4k_d3: 4 waves x 128x128, one barrier per K-tile, two K-tile
-//          LDS-DMA buffers (gemm_w4k.hpp; stamp build gemm_r4k_stamp.hpp)
-//   40     dma4ko: dma4k_d3 persistent, C stores overlapping the next tile's
-//          K loop (gemm_w4o.hpp)
+//          LDS-DMA buffers (gemm_w4k.hpp)
+//   41..46 pingpong8o studies: 128 workgroups, C not stored, whole-line C
+//          layout (44), LDS-staged whole-line boundary stores (46)
 //   19..21 tile128w4 / tile256x128w4 / tile160w4: the 4-wave (one wave per
 //          SIMD) tile kernels that the wave-specialised ones replaced as
 //          variants 15..17 (gemm_bf16_t128.hpp; profiles/r2_ws)
@@ -19,15 +19,15 @@
 // pingpong8w / wi / ww, fp8 knobs 6-9 - profiles/r1_pmc2_w4, r1_pp4, r2_fp8ws;
 // round 3's register-staged, half-K-tile-ring, 5-slot-ring and SGPR-DMA
 // builds - profiles/r3_k1; the overlap kernel's sc1 / plain-store / static-
-// priority builds and pingpong8c's write-through epilogues - profiles/r3_k1o);
+// priority builds and pingpong8c's write-through epilogues - profiles/r3_k1o;
+// round 4: the 4-wave persistent overlap dma4ko / fp8 knob 22 (gemm_w4o.hpp,
+// profiles/r3_w4o) and the dma4k stamp build (gemm_r4k_stamp.hpp));
 // what stays is used by a test or a tool under tools/.
 #include "ntm/gemm_bf16.hpp"
 #include "ntm/gemm_bf16_pp3.hpp"
 #include "ntm/gemm_bf16_pp3_stamp.hpp"
 #include "ntm/gemm_bf16_pp6.hpp"
 #include "ntm/gemm_w4k.hpp"
-#include "ntm/gemm_w4o.hpp"
-#include "ntm/gemm_r4k_stamp.hpp"
 #include "ntm/gemm_bf16_t128.hpp"
 #include "ntm/gemm_fp8_diag.hpp"
 #include "ntm/stream_policy_exp.hpp"
@@ -70,8 +70,6 @@ NTM_API int ntm_gemm_bf16_experimental(int variant, const void* A, const void* B
     // 4 waves x 128x128, one barrier per K-tile, two K-tile LDS-DMA buffers,
     // a DMA piece every 3 MFMA pairs (gemm_w4k.hpp)
     case 39: return (int)ntm::w4k::launch_gemm_bf16_w4k<3>(a, S(stream));
-    // dma4k made persistent, C stores overlapping the next tile's K loop (gemm_w4o.hpp)
-    case 40: return (int)ntm::w4o::launch_gemm_bf16_w4o<3>(a, S(stream));
     // store-bandwidth study (profiles/r3_stores): pingpong8o on 128 workgroups,
     // and with C not stored on 128 / 256 workgroups
     case 41: return (int)ntm::gemm6::launch_gemm_bf16_pp6_grid<1>(a, 128, S(stream));
@@ -101,15 +99,6 @@ NTM_API int ntm_gemm_bf16_stamp(int mode, const void* A, const void* B, void* C,
                                 int K, int lda, int ldb, int ldc, void* stamps, void* stream) {
   return (int)ntm::gemm3s::launch_gemm_bf16_pp3_stamp(args(A, B, C, M, N, K, lda, ldb, ldc), mode,
                                                       (unsigned long long*)stamps, S(stream));
-}
-
-// dma4k (4 waves, one barrier per K-tile) with per-step wait / barrier stamps
-// (gemm_r4k_stamp.hpp; mode 0 real, 1 no DMA, 2 no reads, 3 no barrier, 4
-// MFMA only). stamps: (M/256)*(N/256)*4*10 u64.
-NTM_API int ntm_gemm_r4k_stamp(int mode, const void* A, const void* B, void* C, int M, int N,
-                               int K, int lda, int ldb, int ldc, void* stamps, void* stream) {
-  return (int)ntm::r4ks::launch_gemm_r4k_stamp(args(A, B, C, M, N, K, lda, ldb, ldc), mode,
-                                               (unsigned long long*)stamps, S(stream));
 }
 
 // Matrix-core issue rate (gemm_fp8_diag.hpp mfma_rate_kernel); out: 2 u64 per
