@@ -173,7 +173,7 @@ variable "gpu_driver_preinstalled" {
 }
 
 variable "gpu_node_iommu_passthrough" {
-  description = "iommu=pt on the MI355X nodes (xGMI / PCIe peer DMA), applied by the module's node-prep DaemonSet: \"check\" (record whether the node image booted with it), \"reboot\" (add it to GRUB and reboot each node once) or \"off\". The managed node images take no kernel arguments, so \"reboot\" is the only in-cluster lever."
+  description = "iommu=pt on the MI355X nodes (xGMI / PCIe peer DMA), applied by the module's node-prep DaemonSet: \"check\" (record whether the node image booted with it), \"reboot\" (add it to GRUB and reboot each node once) or \"off\". The managed node images take no kernel arguments, so \"reboot\" is the only in-cluster lever. WARNING: switching an EXISTING cluster to \"reboot\" reboots every GPU node that lacks iommu=pt at the same moment, without cordon or drain, killing the workloads on them; new nodes are safe (they join behind the gpu_node_prep_taint startup taint, so nothing runs on them yet). Roll it out by replacing nodes (e.g. a new node pool) rather than in place."
   type        = string
   default     = "check"
   validation {

@@ -350,7 +350,7 @@ variable "node_prep_taint_key" {
 variable "node_prep_iommu_mode" {
   type        = string
   default     = "check"
-  description = "iommu=pt handling on the GPU nodes: \"check\" records whether the kernel booted with it, \"reboot\" adds it to GRUB and reboots each node at most once, \"off\" skips it. A kernel argument needs a boot: prefer a node image that has it (EKS gpu_ami_id)."
+  description = "iommu=pt handling on the GPU nodes: \"check\" records whether the kernel booted with it, \"reboot\" adds it to GRUB and reboots each node at most once, \"off\" skips it. A kernel argument needs a boot: prefer a node image that has it (EKS gpu_ami_id). WARNING: applying \"reboot\" to nodes that already run workloads reboots all of them at once (no cordon / drain); nodes that join behind the node_prep_startup_taint carry no workloads yet, so for them it is safe."
 
   validation {
     condition     = contains(["off", "check", "reboot"], var.node_prep_iommu_mode)
