@@ -37,7 +37,8 @@ GEMM_VARIANTS = {"default": 0, "pingpong8": 1, "pingpong8b": 4,
                  "tile256x128w4": 20, "tile160w4": 21, "pingpong8cm": 22, "tile160x128": 23,
                  "tile128x160": 24, "tile128x256": 26, "dma4k_d3": 39, "pingpong8o": 25,
                  "pp8o_g128": 41, "pp8o_g128_nostore": 42, "pp8o_nostore": 43,
-                 "pingpong8ol": 44, "pp8ol_nostore": 45, "pingpong8ols": 46}
+                 "pingpong8ol": 44, "pp8ol_nostore": 45, "pingpong8ols": 46,
+                 "pingpong8om": 47}
 
 
 # variants built only into libntm_experimental.so (tests / tools): never selected
@@ -142,9 +143,9 @@ def gemm_bf16(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
                              "(masked tiles: N % 4, K % 8; others: whole tiles, K % 128)")
     elif variant == "default":
         _default_ws_bytes(m, n, k)  # the native plan is the one authority on what it serves
-    elif variant == "pingpong8cm":  # 256x256 with masked edge tiles and K tail
+    elif variant in ("pingpong8cm", "pingpong8om"):  # 256x256, masked edge tiles (+ K tail)
         if not (m > 0 and n > 0 and n % 8 == 0 and k > 0 and k % 8 == 0):
-            raise ValueError(f"shape ({m},{n},{k}) not served by pingpong8cm (N % 8, K % 8)")
+            raise ValueError(f"shape ({m},{n},{k}) not served by {variant} (N % 8, K % 8)")
     elif not gemm_shape_ok(m, n, k):
         raise ValueError(f"shape ({m},{n},{k}) not tiled by the 256x256x64 kernel")
     if out is None:

@@ -196,3 +196,24 @@ def test_fp8_entry_points_reject_bad_shapes_before_any_launch(fp8_plan):
     assert L.ntm_gemm_fp8_splitk(5, 2, None, None, None, 256, 256, 256, 256, 256, 256, None, 0,
                                  None) != 0
     assert L.ntm_fp8_splitk_ws_bytes(280, 6352, 15136, 3) == 4 * 3 * 280 * 6352
+
+
+def test_k1_boxes_reports_median_over_boxes(tmp_path):
+    """tools/k1_boxes.py: per-box K1 / hipBLASLt ratios and their median (a +-1 %
+    claim is a distribution over boxes)."""
+    import json
+    import sys
+    from pathlib import Path
+
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1] / "tools"))
+    import k1_boxes
+
+    logs = []
+    for i, (ours, hb) in enumerate([(1600, 1620), (1650, 1630), (1640, 1640)]):
+        p = tmp_path / f"box{i}.log"
+        p.write_text('{"device": "x"}\n' + json.dumps(
+            {"size": 8192, "pingpong8o_tflops_med": ours, "torch_tflops_med": hb}) + "\n")
+        logs.append(str(p))
+    r = k1_boxes.ratios(logs)
+    rs = r[("8192", "pingpong8o")]
+    assert len(rs) == 3 and abs(sorted(rs)[1] - 1.0) < 1e-12

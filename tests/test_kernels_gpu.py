@@ -731,6 +731,26 @@ def test_persistent_overlap_vs_torch_fp32(ops, variant, m, n, k):
     assert torch.equal(c, ops.gemm_bf16(a, b, variant="pingpong8c"))
 
 
+@pytest.mark.parametrize("m,n,k", [(1000, 1000, 256), (4472, 5688, 640), (4608, 4360, 512),
+                                   (8192, 8192, 256), (333, 1000, 384), (5000, 4104, 768)])
+def test_persistent_masked_vs_torch_fp32(ops, m, n, k):
+    """pingpong8om (round 4): the persistent overlap kernel on ragged C - edge
+    tiles with clamped sources and masked stores, 1-2 tiles per workgroup
+    (4472x5688: 414 tiles on 256 workgroups), rows / columns past C never
+    written (the guard columns of a wider out stay untouched), and bitwise
+    equal to pingpong8cm (same MFMAs in the same K order)."""
+    a = _rand(ops, (m, k), 641 + k)
+    b = _rand(ops, (n, k), 643 + n)
+    out = torch.full((m, n + 8), 7.0, dtype=torch.bfloat16, device="cuda")
+    c = ops.gemm_bf16(a, b, out[:, :n], variant="pingpong8om")
+    ref = a.float() @ b.float().T
+    atol, rtol = ops.gemm_tolerance(k)
+    err = (c.float() - ref).abs()
+    assert torch.all(err <= atol + rtol * ref.abs()), float(err.max())
+    assert torch.equal(c, ops.gemm_bf16(a, b, variant="pingpong8cm"))
+    assert torch.all(out[:, n:] == 7.0)
+
+
 @pytest.mark.parametrize("m,n,k", [(8192, 8192, 1024), (2048, 2048, 256)])
 def test_gemm_clock_build(ops, m, n, k):
     """The GEMM's own clock: the shipping pingpong8o with a

@@ -1,0 +1,93 @@
+"""The GEMM's own clock two ways (VERDICT r3 #4 acceptance check).
+
+Runs the shipping pingpong8o clock-stamp build (ops.gemm_clock_ghz: per
+workgroup d(s_memtime) / d(s_memrealtime) x 100 MHz) for --launches
+back-to-back 8192^3 launches after a wall-time warm-up, prints the in-kernel
+clock as JSON, and leaves the dispatches for a profiler. Under
+
+    rocprofv3 --pmc GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d <dir> -o run \
+        -- python3 tools/clock_check.py
+
+the PMC-derived clock of the same kernel is GRBM_GUI_ACTIVE / 8 XCDs / its
+duration (tools/pmc_summary.py eff_clock_GHz); --compare <dir> prints both and
+their ratio.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+import time
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+
+
+def measure(size: int, launches: int, warm_s: float) -> dict:
+    import torch
+
+    from nvidia_terraform_modules_amd import ops
+
+    a = ops.fill_uniform_(torch.empty((size, size), dtype=torch.bfloat16, device="cuda"), 1)
+    b = ops.fill_uniform_(torch.empty((size, size), dtype=torch.bfloat16, device="cuda"), 2)
+    c = torch.empty((size, size), dtype=torch.bfloat16, device="cuda")
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < warm_s:        # clock settle on the same kernel
+        ops.gemm_clock_ghz(a, b, c, steps=8)
+    r = ops.gemm_clock_ghz(a, b, c, steps=launches)
+    r["size"] = size
+    return r
+
+
+def compare(prof_dir: str, inkernel: dict) -> dict:
+    """PMC clock of the stamped kernel's dispatches in ``prof_dir`` (counter and
+    kernel-trace CSVs of ONE rocprofv3 run): GRBM_GUI_ACTIVE / 8 XCDs / the
+    dispatch's own duration, median over dispatches - the same dispatches whose
+    in-kernel clock the tool printed (a profiled run's clock differs from an
+    unprofiled one's, so the two are compared inside one run)."""
+    import csv
+    import glob
+    import statistics
+
+    key = "pp6_kernel<1, false, 1"
+    grbm, dur = {}, {}
+    for f in glob.glob(str(Path(prof_dir) / "**" / "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if key in r["Kernel_Name"] and r["Counter_Name"] == "GRBM_GUI_ACTIVE":
+                grbm[r.get("Dispatch_Id", len(grbm))] = float(r["Counter_Value"])
+    for f in glob.glob(str(Path(prof_dir) / "**" / "*kernel_trace.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if key in r["Kernel_Name"]:
+                dur[r.get("Dispatch_Id", len(dur))] = (float(r["End_Timestamp"]) -
+                                                      float(r["Start_Timestamp"]))
+    ids = [i for i in grbm if i in dur and dur[i] > 0]
+    if not ids:
+        raise SystemExit(f"no stamped-kernel dispatches with both counters and trace in {prof_dir}")
+    pmc = statistics.median(grbm[i] / 8 / dur[i] for i in ids)
+    return {"dispatches": len(ids), "pmc_clock_GHz": round(pmc, 4),
+            "inkernel_median_GHz": inkernel["median_GHz"],
+            "inkernel_over_pmc": round(inkernel["median_GHz"] / pmc, 4)}
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--size", type=int, default=8192)
+    ap.add_argument("--launches", type=int, default=40)
+    ap.add_argument("--warm-s", type=float, default=2.0)
+    ap.add_argument("--out", default="", help="write the in-kernel JSON here")
+    ap.add_argument("--compare", default="", help="profiler output dir of a run of this tool")
+    ap.add_argument("--inkernel", default="", help="with --compare: the JSON --out wrote")
+    args = ap.parse_args()
+    if args.compare:
+        print(json.dumps(compare(args.compare, json.loads(Path(args.inkernel).read_text()))))
+        return 0
+    r = measure(args.size, args.launches, args.warm_s)
+    s = json.dumps(r)
+    print(s, flush=True)
+    if args.out:
+        Path(args.out).write_text(s + "\n")
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -20,6 +20,7 @@ from nvidia_terraform_modules_amd import ops  # noqa: E402
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--size", type=int, default=8192)
+    ap.add_argument("--shape", default="", help="MxNxK instead of --size (e.g. 8192x8192x4096)")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--which", default="both", choices=["both", "ours", "torch", "all"])
     ap.add_argument("--variant", default="default")
@@ -32,12 +33,12 @@ def main() -> int:
                     help="untimed pairs first, so most profiled dispatches run on a settled chip")
     args = ap.parse_args()
     args.iters += args.warm_iters
-    s = args.size
+    m, n, k = (int(x) for x in args.shape.split("x")) if args.shape else (args.size,) * 3
     if args.dtype == "fp8":
-        return fp8_pair(s, args.iters, args.which, args.knob)
-    a = torch.empty((s, s), dtype=torch.bfloat16, device="cuda")
-    b = torch.empty((s, s), dtype=torch.bfloat16, device="cuda")
-    c = torch.empty((s, s), dtype=torch.bfloat16, device="cuda")
+        return fp8_pair((m, n, k), args.iters, args.which, args.knob)
+    a = torch.empty((m, k), dtype=torch.bfloat16, device="cuda")
+    b = torch.empty((n, k), dtype=torch.bfloat16, device="cuda")
+    c = torch.empty((m, n), dtype=torch.bfloat16, device="cuda")
     ops.fill_uniform_(a, 1)
     ops.fill_uniform_(b, 2)
     for _ in range(args.iters):
@@ -54,11 +55,12 @@ def main() -> int:
     return 0
 
 
-def fp8_pair(s: int, iters: int, which: str, knob: int = 0) -> int:
+def fp8_pair(shape, iters: int, which: str, knob: int = 0) -> int:
     """K1-fp8 vs hipBLASLt's fp8 GEMM (torch._scaled_mm, unit scales, bf16 out)."""
-    a = ops.fill_uniform_(torch.empty((s, s), dtype=torch.float8_e4m3fn, device="cuda"), 1)
-    b = ops.fill_uniform_(torch.empty((s, s), dtype=torch.float8_e4m3fn, device="cuda"), 2)
-    c = torch.empty((s, s), dtype=torch.bfloat16, device="cuda")
+    m, n, k = shape
+    a = ops.fill_uniform_(torch.empty((m, k), dtype=torch.float8_e4m3fn, device="cuda"), 1)
+    b = ops.fill_uniform_(torch.empty((n, k), dtype=torch.float8_e4m3fn, device="cuda"), 2)
+    c = torch.empty((m, n), dtype=torch.bfloat16, device="cuda")
     one = torch.ones((), device="cuda")
     for _ in range(iters):
         if which in ("both", "ours", "all"):

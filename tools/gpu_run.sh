@@ -15,8 +15,11 @@
 #   prof       rocprofv3 --kernel-trace --stats of a short bench
 #   pmc        PMC passes (counters in their own runs, --kernel-trace only) of K1 vs
 #              hipBLASLt at 8192^3 (PMC_DTYPE=fp8: K1-fp8 vs hipBLASLt fp8; PMC_ARGS: extra
-#              tools/gemm_pair.py arguments, e.g. "--variant A --versus B") +
+#              tools/gemm_pair.py arguments, e.g. "--variant A --versus B"; PMC_SHAPE:
+#              MxNxK instead of 8192^3) +
 #              tools/pmc_summary.py -> <tag>/pmc/summary.json
+#   clock      the GEMM's in-kernel clock (stamped pingpong8o) vs GRBM_GUI_ACTIVE of the
+#              same dispatches (one rocprofv3 --pmc pass)
 #   fp8        K1-fp8 vs hipBLASLt fp8: square sizes (gemm_fp8_check) + the 41-shape sweep
 #   py:<file>  python -u <file> (a tool script; its own args via PYARGS)
 set -o pipefail
@@ -68,10 +71,12 @@ for s in "${STEPS[@]}"; do
       P="$O/pmc"
       mkdir -p "$P"
       pair="tools/gemm_pair.py --size 8192 --iters 10 --dtype ${PMC_DTYPE:-bf16} ${PMC_ARGS:-}"
+      [ -n "${PMC_SHAPE:-}" ] && pair="$pair --shape $PMC_SHAPE"
       for pass in "sq1:SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE" \
                   "sq2:SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_WAIT_INST_LDS" \
                   "sq3:SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM SQ_LDS_IDX_ACTIVE" \
-                  "tcc:TCC_HIT_sum TCC_MISS_sum" "fetch:FETCH_SIZE" "write:WRITE_SIZE"; do
+                  "tcc:TCC_HIT_sum TCC_MISS_sum" "fetch:FETCH_SIZE" "write:WRITE_SIZE" \
+                  "wrreq:TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum"; do
         name=${pass%%:*}
         timeout -s KILL 120 rocprofv3 --pmc ${pass#*:} --kernel-trace --output-format csv \
           -d "$P/$name" -o run -- python3 $pair > "$P/$name.log" 2>&1 || fail "pmc $name" $? "$P/$name.log"
@@ -79,6 +84,13 @@ for s in "${STEPS[@]}"; do
       timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$P/trace" -o run \
         -- python3 $pair > "$P/trace.log" 2>&1 || fail "pmc trace" $? "$P/trace.log"
       python3 tools/pmc_summary.py "$P" > "$P/summary.json" && head -c 3000 "$P/summary.json" ;;
+    clock)
+      # the GEMM's own clock (stamped build) vs its PMC clock, same dispatches
+      timeout -s KILL 180 rocprofv3 --pmc GRBM_GUI_ACTIVE --kernel-trace --output-format csv \
+        -d "$O/clock_pmc" -o run -- python3 tools/clock_check.py --out "$O/clock_inkernel.json" \
+        > "$O/clock.log" 2>&1 || fail clock $? "$O/clock.log"
+      python3 tools/clock_check.py --compare "$O/clock_pmc" --inkernel "$O/clock_inkernel.json" \
+        | tee "$O/clock_compare.json" ;;
     fp8)
       timeout -k 10 600 python -u tools/gemm_fp8_check.py --sizes 1024,2048,2560,3072,4096,4608,6144,8192 \
         --iters 30 --rounds 5 > "$O/fp8_check.log" 2>&1 || fail fp8 $? "$O/fp8_check.log"

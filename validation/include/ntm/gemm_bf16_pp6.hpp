@@ -62,6 +62,12 @@ __host__ __device__ inline bool shape_ok6(int M, int N, int K) {
   return M > 0 && N > 0 && (M % BM) == 0 && (N % BN) == 0 && (K % (2 * BK)) == 0 && K >= 4 * BK;
 }
 
+// Masked build ("pingpong8om"): ragged C (any M, N % 8) on whole K-tile pairs
+// (K % 128, K >= 256); edge tiles clamp their source rows and mask their stores.
+__host__ __device__ inline bool shape_ok6m(int M, int N, int K) {
+  return M > 0 && N > 0 && (N % 8) == 0 && (K % (2 * BK)) == 0 && K >= 4 * BK;
+}
+
 template <int N>
 __device__ __forceinline__ void wait_vm() {
   static_assert(N >= 0 && N <= 63, "vmcnt range");
@@ -72,13 +78,33 @@ __device__ __forceinline__ void wait_vm() {
 // from: the current tile (NX false), or (NX true, kt >= T) the next tile when
 // there is one (dA / dB = its element offset from this tile) and otherwise an
 // L2-hot in-bounds dummy slice into the scratch region nobody reads.
-template <int H, bool NX>
-__device__ __forceinline__ void issue6(const Ctx& c, int kt, int buf, int T, bool has_next,
-                                       long dA, long dB) {
+// Source of half H of a tile at (m0, n0) for this lane, rows clamped to the
+// matrix (masked build): the clamped rows only feed C rows / columns that the
+// masked stores skip. (Whole-tile builds step c.src by per-tile deltas instead.)
+template <int H>
+__device__ __forceinline__ const __bf16* src_clamped(const GemmArgs& p, int m0, int n0, int w,
+                                                     int lane) {
+  const int r = lane >> 2;
+  const int cl = (lane & 3) ^ (((r >> 3) & 1) << 1);
+  const int hi = (H == kAHi || H == kBHi) ? 128 : 0;
+  if constexpr (H == kALo || H == kAHi)
+    return p.A + (size_t)min(m0 + hi + w * 16 + r, p.M - 1) * p.lda + cl * 8;
+  else
+    return p.B + (size_t)min(n0 + hi + w * 16 + r, p.N - 1) * p.ldb + cl * 8;
+}
+
+template <int H, bool NX, bool MASK = false>
+__device__ __forceinline__ void issue6(const GemmArgs& p, const Ctx& c, int kt, int buf, int T,
+                                       bool has_next, long dA, long dB, int nm0, int nn0,
+                                       int lane) {
   const __bf16* s;
   int off = buf * kTileBytes + H * kHalfBytes;
   if constexpr (!NX) {
     s = c.src[H] + (size_t)kt * BK;
+  } else if constexpr (MASK) {
+    s = has_next ? src_clamped<H>(p, nm0, nn0, c.w, lane) + (long)(kt - T) * BK
+                 : c.src[H] + (long)(T - 1) * BK;
+    off = has_next ? off : kScratch;
   } else {
     const long d = (H == kALo || H == kAHi) ? dA : dB;
     s = c.src[H] + (has_next ? d + (long)(kt - T) * BK : (long)(T - 1) * BK);
@@ -104,9 +130,12 @@ __device__ __forceinline__ void mma_q(f32x4 (&acc)[4][2], const bf16x8 (&a)[4][2
 // One quadrant of the previous tile (origin m0, n0) to C, in store_tile_wide's
 // layout: after a permlane16 swap per dword pair every lane holds 8 consecutive
 // columns. c_lane = the lane's element offset inside the tile (one VGPR).
-template <int MH, int NH, int POL, bool LINE = false>
+// MASK: store only rows < M and 8-column chunks < N (lrow / lcol = the lane's
+// row / column inside the quadrant's 16-row block origin, tile-relative).
+template <int MH, int NH, int POL, bool LINE = false, bool MASK = false>
 __device__ __forceinline__ void store_quadrant(const GemmArgs& p, const f32x4 (&q)[4][2],
-                                               int m0, int n0, int c_lane) {
+                                               int m0, int n0, int c_lane, int lrow = 0,
+                                               int lcol = 0) {
   typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt) {
@@ -121,6 +150,10 @@ __device__ __forceinline__ void store_quadrant(const GemmArgs& p, const f32x4 (&
       w1[h] = r[1];
     }
     __bf16* tile = p.C + (size_t)(m0 + MH * 128 + mt * 16) * p.ldc + (n0 + NH * (LINE ? 32 : 128));
+    if constexpr (MASK) {
+      if (m0 + MH * 128 + mt * 16 + lrow >= p.M || n0 + NH * (LINE ? 32 : 128) + lcol >= p.N)
+        continue;
+    }
     store_c16<POL>(tile + c_lane, u32x4{w0[0], w0[1], w1[0], w1[1]});
   }
 }
@@ -214,6 +247,7 @@ struct Edge {
   bool prev;      // there is a previous tile (not the CU's first)
   bool has_next;  // there is a next tile (this tile's quadrants leave in K-tile T-1)
   long dA, dB;    // next tile's element offsets from this one
+  int nm0, nn0;   // next tile's origin (masked build: its sources are clamped per tile)
   int m0, n0;     // this tile's origin
 };
 
@@ -224,10 +258,12 @@ struct Edge {
 // 0 / 1) or e.has_next (K-tile T-1); VMC: the counted wait when ON (10
 // otherwise); NX: this phase's piece is past the tile (issue6). A stored
 // quadrant is zeroed for the next tile.
-template <int P, bool ODD, int CONV, int VMC, bool NX, int POL, bool LINE, bool STG = false>
+template <int P, bool ODD, int CONV, int VMC, bool NX, int POL, bool LINE, bool STG = false,
+          bool MASK = false>
 __device__ __forceinline__ void phase6(const GemmArgs& p, const Ctx& c, Frags3& f,
                                        f32x4 (&acc)[2][2][4][2], int t, int T, const Edge& e,
-                                       bool on, int c_lane, int c_lane2 = 0, int lane = 0) {
+                                       bool on, int c_lane, int c_lane2 = 0, int lane = 0,
+                                       int lrow = 0, int lcol = 0) {
   bf16x8(&bcur)[2][2] = ODD ? f.b1 : f.b0;
   bf16x8(&both)[2][2] = ODD ? f.b0 : f.b1;
   const int cur = t & 1;
@@ -235,10 +271,10 @@ __device__ __forceinline__ void phase6(const GemmArgs& p, const Ctx& c, Frags3& 
   if constexpr (P == 1) read_b<kBHi>(c, both, cur);
   if constexpr (P == 2) read_a<kAHi>(c, f.a, cur);
   if constexpr (P == 3) read_b<kBLo>(c, both, cur ^ 1);  // K-tile t+1 (next tile's 0 at t = T-1)
-  if constexpr (P == 0) issue6<kAHi, NX>(c, t + 1, cur ^ 1, T, e.has_next, e.dA, e.dB);
-  if constexpr (P == 1) issue6<kBLo, NX>(c, t + 2, cur, T, e.has_next, e.dA, e.dB);
-  if constexpr (P == 2) issue6<kALo, NX>(c, t + 2, cur, T, e.has_next, e.dA, e.dB);
-  if constexpr (P == 3) issue6<kBHi, NX>(c, t + 2, cur, T, e.has_next, e.dA, e.dB);
+  if constexpr (P == 0) issue6<kAHi, NX, MASK>(p, c, t + 1, cur ^ 1, T, e.has_next, e.dA, e.dB, e.nm0, e.nn0, lane);
+  if constexpr (P == 1) issue6<kBLo, NX, MASK>(p, c, t + 2, cur, T, e.has_next, e.dA, e.dB, e.nm0, e.nn0, lane);
+  if constexpr (P == 2) issue6<kALo, NX, MASK>(p, c, t + 2, cur, T, e.has_next, e.dA, e.dB, e.nm0, e.nn0, lane);
+  if constexpr (P == 3) issue6<kBHi, NX, MASK>(p, c, t + 2, cur, T, e.has_next, e.dA, e.dB, e.nm0, e.nn0, lane);
   if constexpr (VMC == 10) {
     wait_vm<10>();
   } else {
@@ -270,8 +306,8 @@ __device__ __forceinline__ void phase6(const GemmArgs& p, const Ctx& c, Frags3& 
           store_quadrant<MH, NH, 1>(p, acc[MH][NH], CONV == 3 ? e.pm0 : e.m0,
                                     CONV == 3 ? e.pn0 : e.n0, c_lane);
       } else {
-        store_quadrant<MH, NH, POL>(p, acc[MH][NH], CONV == 3 ? e.pm0 : e.m0,
-                                    CONV == 3 ? e.pn0 : e.n0, c_lane);
+        store_quadrant<MH, NH, POL, false, MASK>(p, acc[MH][NH], CONV == 3 ? e.pm0 : e.m0,
+                                                 CONV == 3 ? e.pn0 : e.n0, c_lane, lrow, lcol);
       }
       zero_quadrant(acc[MH][NH]);
     }
@@ -285,7 +321,8 @@ __device__ __forceinline__ void phase6(const GemmArgs& p, const Ctx& c, Frags3& 
 }
 
 #define NTM_PH(P, ODD, CV, VMC, NX, ON) \
-  phase6<P, ODD, CV, VMC, NX, POL, LINE, STG>(p, c, f, acc, t, T, e, ON, c_lane, c_lane2, lane)
+  phase6<P, ODD, CV, VMC, NX, POL, LINE, STG, MASK>(p, c, f, acc, t, T, e, ON, c_lane, c_lane2, \
+                                                    lane, lrow, lcol)
 
 __device__ __forceinline__ void tile_origin(const GemmArgs& p, int tile, int ntiles, int& m0,
                                             int& n0) {
@@ -325,13 +362,16 @@ __device__ __forceinline__ void clock_stamp(unsigned long long& t, unsigned long
 // An fp8 build of this structure did not fit: pingpong8c's fp8 consumer already
 // holds 128 VGPRs + 128 AGPRs, and the boundary conversion spilled 76 VGPRs.
 // STG (LINE only): boundary stores staged through LDS in whole lines (store_pair_lds).
-template <int POL, bool LINE = false, int STAMP = 0, bool STG = false>
+// MASK ("pingpong8om", default layout only): ragged C - ceil(M/256) x
+// ceil(N/256) tiles, sources clamped per tile (src_clamped), stores masked.
+template <int POL, bool LINE = false, int STAMP = 0, bool STG = false, bool MASK = false>
 __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_pp6_kernel(GemmArgs p) {
   static_assert(!STG || LINE, "LDS-staged boundary stores need the whole-line layout");
+  static_assert(!MASK || (!LINE && !STG), "the masked build uses the default C layout");
   __shared__ __attribute__((aligned(16))) char smem[STG ? kStgBytes : kLdsBytes3];
   unsigned long long t0 = 0, rt0 = 0;
   if constexpr (STAMP != 0) clock_stamp(t0, rt0);
-  const int ntiles = (p.M / BM) * (p.N / BN);
+  const int ntiles = MASK ? ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN) : (p.M / BM) * (p.N / BN);
   const int G = (int)gridDim.x;
   int tile = (int)blockIdx.x;
 
@@ -353,7 +393,16 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_pp6_kernel(GemmArgs p) 
     c.src[kAHi] = a0 + (size_t)128 * p.lda;
     c.src[kBLo] = b0;
     c.src[kBHi] = b0 + (size_t)(LINE ? 32 : 128) * p.ldb;
+    if constexpr (MASK) {
+      c.src[kALo] = src_clamped<kALo>(p, e.m0, e.n0, c.w, lane);
+      c.src[kAHi] = src_clamped<kAHi>(p, e.m0, e.n0, c.w, lane);
+      c.src[kBLo] = src_clamped<kBLo>(p, e.m0, e.n0, c.w, lane);
+      c.src[kBHi] = src_clamped<kBHi>(p, e.m0, e.n0, c.w, lane);
+    }
   }
+  // masked stores: the lane's row / column inside a quadrant's 16-row block
+  const int lrow = c.wr * 64 + (lane & 15);
+  const int lcol = c.wc * 32 + ((lane >> 4) & 1) * 16 + (lane >> 5) * 8;
   c.frag_off = (lane & 15) * 64 + ((lane >> 4) ^ ((lane >> 2) & 2)) * 16;
   const int c_lane = (c.wr * 64 + (lane & 15)) * p.ldc + c.wc * (LINE ? 64 : 32) +
                      ((lane >> 4) & 1) * 16 + (lane >> 5) * 8;
@@ -377,6 +426,8 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_pp6_kernel(GemmArgs p) 
     e.dA = (long)(nm0 - e.m0) * p.lda;
     e.dB = (long)(nn0 - e.n0) * p.ldb;
   }
+  e.nm0 = nm0;
+  e.nn0 = nn0;
 
   // prologue of the first tile: B-lo0 A-lo0 B-hi0 A-hi0 B-lo1 A-lo1 B-hi1
   issue_half<kBLo>(c, 0, 0);
@@ -434,8 +485,15 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_pp6_kernel(GemmArgs p) 
     NTM_PH(3, true, LINE ? -1 : 2, 18, true, e.has_next);
     if (!e.has_next) break;
     // advance to the next tile
+    if constexpr (MASK) {
+      c.src[kALo] = src_clamped<kALo>(p, nm0, nn0, c.w, lane);
+      c.src[kAHi] = src_clamped<kAHi>(p, nm0, nn0, c.w, lane);
+      c.src[kBLo] = src_clamped<kBLo>(p, nm0, nn0, c.w, lane);
+      c.src[kBHi] = src_clamped<kBHi>(p, nm0, nn0, c.w, lane);
+    } else {
 #pragma unroll
-    for (int h = 0; h < 4; ++h) c.src[h] += (h == kALo || h == kAHi) ? e.dA : e.dB;
+      for (int h = 0; h < 4; ++h) c.src[h] += (h == kALo || h == kAHi) ? e.dA : e.dB;
+    }
     e.pm0 = e.m0;
     e.pn0 = e.n0;
     e.m0 = nm0;
@@ -448,11 +506,13 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_pp6_kernel(GemmArgs p) 
       e.dA = (long)(nm0 - e.m0) * p.lda;
       e.dB = (long)(nn0 - e.n0) * p.ldb;
     }
+    e.nm0 = nm0;
+    e.nn0 = nn0;
   }
   if (c.wr == 0) raw_barrier();  // balance the stagger
   wait_vm<0>();                  // dummy pieces: nothing may land after the WG exits
   if (POL != 2 || p.ldc < 0)
-    store_tile_lds<false, POL != 0, false, POL == 0 ? 0 : 1, LINE>(p, c, acc, e.m0, e.n0, lane);
+    store_tile_lds<false, POL != 0, MASK, POL == 0 ? 0 : 1, LINE>(p, c, acc, e.m0, e.n0, lane);
   if constexpr (STAMP != 0) {
     unsigned long long t1, rt1;
     clock_stamp(t1, rt1);
@@ -501,6 +561,18 @@ inline hipError_t launch_gemm_bf16_pp6(const GemmArgs& a, hipStream_t stream) {
   const int ntiles = (a.M / BM) * (a.N / BN);
   hipLaunchKernelGGL((gemm_bf16_pp6_kernel<POL, LINE, STAMP, STG>), dim3((unsigned)pp6_grid(ntiles)),
                      dim3(kThreads), 0, stream, a);
+  return hipGetLastError();
+}
+
+// pingpong8om: ragged C (any M, N % 8), K % 128, K >= 256.
+template <int POL>
+inline hipError_t launch_gemm_bf16_pp6_masked(const GemmArgs& a, hipStream_t stream) {
+  if (!shape_ok6m(a.M, a.N, a.K) || a.rowsum || a.lda < a.K || a.ldb < a.K || a.ldc < a.N ||
+      (a.lda % 8) || (a.ldb % 8) || (a.ldc % 8))
+    return hipErrorInvalidValue;
+  const int ntiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
+  hipLaunchKernelGGL((gemm_bf16_pp6_kernel<POL, false, 0, false, true>),
+                     dim3((unsigned)pp6_grid(ntiles)), dim3(kThreads), 0, stream, a);
   return hipGetLastError();
 }
 

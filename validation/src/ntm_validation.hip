@@ -300,6 +300,12 @@ NTM_API int ntm_gemm_bf16_variant(int variant, const void* A, const void* B,
       if (!ntm::gemm6::shape_ok6(M, N, K) || (lda % 8) || (ldb % 8) || (ldc % 8))
         return (int)ntm::gemm3::launch_gemm_bf16_pp3(a, S(stream));
       return (int)ntm::gemm6::launch_gemm_bf16_pp6<1, kPp6Line>(a, S(stream));
+    // persistent + masked (pingpong8om): ragged C over more than one round of
+    // 256x256 tiles (K % 128, K >= 256; otherwise pingpong8cm)
+    case 47:
+      if (!ntm::gemm6::shape_ok6m(M, N, K) || (lda % 8) || (ldb % 8) || (ldc % 8))
+        return (int)ntm::gemm3::launch_gemm_bf16_pp3_masked(a, S(stream));
+      return (int)ntm::gemm6::launch_gemm_bf16_pp6_masked<1>(a, S(stream));
     // gemm_bf16_t128.hpp: 128x128 / 256x128 / 160x160 tiles on the wave-specialised
     // kernel (4 DMA-producer + 4 MFMA-consumer waves), 256x160 on the 4-wave one
     case 15: return (int)ntm::gemmt::launch_gemm_bf16_tile_ws<4>(a, S(stream));
