@@ -732,13 +732,18 @@ def test_persistent_overlap_vs_torch_fp32(ops, variant, m, n, k):
 
 
 @pytest.mark.parametrize("m,n,k", [(1000, 1000, 256), (4472, 5688, 640), (4608, 4360, 512),
-                                   (8192, 8192, 256), (333, 1000, 384), (5000, 4104, 768)])
+                                   (8192, 8192, 256), (333, 1000, 384), (5000, 4104, 768),
+                                   # partial K (K % 128 != 0): 4, 6, 8 K-tiles, the last
+                                   # pair partial or all past K
+                                   (4472, 5688, 200), (1000, 4104, 328), (4608, 4360, 456),
+                                   (2056, 3000, 1000), (4472, 5688, 5832)])
 def test_persistent_masked_vs_torch_fp32(ops, m, n, k):
     """pingpong8om (round 4): the persistent overlap kernel on ragged C - edge
     tiles with clamped sources and masked stores, 1-2 tiles per workgroup
-    (4472x5688: 414 tiles on 256 workgroups), rows / columns past C never
-    written (the guard columns of a wider out stay untouched), and bitwise
-    equal to pingpong8cm (same MFMAs in the same K order)."""
+    (4472x5688: 414 tiles on 256 workgroups), K % 128 != 0 on the partial-K
+    build (chunks past K load zeros), rows / columns past C never written
+    (the guard columns of a wider out stay untouched), and bitwise equal to
+    pingpong8cm (same MFMAs in the same K order)."""
     a = _rand(ops, (m, k), 641 + k)
     b = _rand(ops, (n, k), 643 + n)
     out = torch.full((m, n + 8), 7.0, dtype=torch.bfloat16, device="cuda")

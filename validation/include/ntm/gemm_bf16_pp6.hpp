@@ -64,8 +64,11 @@ __host__ __device__ inline bool shape_ok6(int M, int N, int K) {
 
 // Masked build ("pingpong8om"): ragged C (any M, N % 8) on whole K-tile pairs
 // (K % 128, K >= 256); edge tiles clamp their source rows and mask their stores.
+// With TAIL (K % 128 != 0): K % 8 and K > 128 (ceil(K / 128) * 2 >= 4 K-tiles);
+// 16-B chunks past K load zeros, so the partial K-tile pair adds nothing.
 __host__ __device__ inline bool shape_ok6m(int M, int N, int K) {
-  return M > 0 && N > 0 && (N % 8) == 0 && (K % (2 * BK)) == 0 && K >= 4 * BK;
+  return M > 0 && N > 0 && (N % 8) == 0 && K > 2 * BK && (K % 8) == 0 &&
+         ((K % (2 * BK)) != 0 || K >= 4 * BK);
 }
 
 template <int N>
@@ -78,6 +81,18 @@ __device__ __forceinline__ void wait_vm() {
 // from: the current tile (NX false), or (NX true, kt >= T) the next tile when
 // there is one (dA / dB = its element offset from this tile) and otherwise an
 // L2-hot in-bounds dummy slice into the scratch region nobody reads.
+// Lane id recomputed where it is used (2 VALU). The masked builds need lane-
+// derived values (clamped source rows, store masks, the K-tail column) only
+// at tile boundaries; kept live through the K loop they push the kernel past
+// 256 VGPRs, and hipcc then reloads spills with vmcnt(0) inside the loop,
+// draining the LDS-DMA pipeline. The asm is volatile, so it is neither hoisted
+// nor shared across uses.
+__device__ __forceinline__ int opaque_lane() {
+  int l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return l;
+}
+
 // Source of half H of a tile at (m0, n0) for this lane, rows clamped to the
 // matrix (masked build): the clamped rows only feed C rows / columns that the
 // masked stores skip. (Whole-tile builds step c.src by per-tile deltas instead.)
@@ -93,7 +108,9 @@ __device__ __forceinline__ const __bf16* src_clamped(const GemmArgs& p, int m0, 
     return p.B + (size_t)min(n0 + hi + w * 16 + r, p.N - 1) * p.ldb + cl * 8;
 }
 
-template <int H, bool NX, bool MASK = false>
+// TL (partial-K builds, only where a piece can reach past K): a 16-B chunk
+// starting at k >= K loads zeros (as pingpong8cm's TAIL build).
+template <int H, bool NX, bool MASK = false, bool TL = false>
 __device__ __forceinline__ void issue6(const GemmArgs& p, const Ctx& c, int kt, int buf, int T,
                                        bool has_next, long dA, long dB, int nm0, int nn0,
                                        int lane) {
@@ -102,7 +119,7 @@ __device__ __forceinline__ void issue6(const GemmArgs& p, const Ctx& c, int kt, 
   if constexpr (!NX) {
     s = c.src[H] + (size_t)kt * BK;
   } else if constexpr (MASK) {
-    s = has_next ? src_clamped<H>(p, nm0, nn0, c.w, lane) + (long)(kt - T) * BK
+    s = has_next ? src_clamped<H>(p, nm0, nn0, c.w, opaque_lane()) + (long)(kt - T) * BK
                  : c.src[H] + (long)(T - 1) * BK;
     off = has_next ? off : kScratch;
   } else {
@@ -111,8 +128,15 @@ __device__ __forceinline__ void issue6(const GemmArgs& p, const Ctx& c, int kt, 
     off = has_next ? off : kScratch;
   }
   char* d = c.lds + off + (2 * c.w) * 1024;
-  glds16(s, d);
-  glds16(s + 32, d + 1024);
+  if constexpr (TL && !NX) {
+    const int l = opaque_lane();
+    const int col = kt * BK + ((l & 3) ^ (((l >> 5) & 1) << 1)) * 8;
+    glds16(col < c.K ? s : (const __bf16*)kZeroChunk16, d);
+    glds16(col + 32 < c.K ? s + 32 : (const __bf16*)kZeroChunk16, d + 1024);
+  } else {
+    glds16(s, d);
+    glds16(s + 32, d + 1024);
+  }
 }
 
 // 16 MFMAs of one quadrant (mma_quadrant without the setprio).
@@ -151,7 +175,10 @@ __device__ __forceinline__ void store_quadrant(const GemmArgs& p, const f32x4 (&
     }
     __bf16* tile = p.C + (size_t)(m0 + MH * 128 + mt * 16) * p.ldc + (n0 + NH * (LINE ? 32 : 128));
     if constexpr (MASK) {
-      if (m0 + MH * 128 + mt * 16 + lrow >= p.M || n0 + NH * (LINE ? 32 : 128) + lcol >= p.N)
+      const int l = opaque_lane();
+      const int lr = lrow + (l & 15);                              // lrow = 64 wr
+      const int lc = lcol + ((l >> 4) & 1) * 16 + (l >> 5) * 8;    // lcol = 32 wc
+      if (m0 + MH * 128 + mt * 16 + lr >= p.M || n0 + NH * (LINE ? 32 : 128) + lc >= p.N)
         continue;
     }
     store_c16<POL>(tile + c_lane, u32x4{w0[0], w0[1], w1[0], w1[1]});
@@ -259,7 +286,7 @@ struct Edge {
 // otherwise); NX: this phase's piece is past the tile (issue6). A stored
 // quadrant is zeroed for the next tile.
 template <int P, bool ODD, int CONV, int VMC, bool NX, int POL, bool LINE, bool STG = false,
-          bool MASK = false>
+          bool MASK = false, bool TL = false>
 __device__ __forceinline__ void phase6(const GemmArgs& p, const Ctx& c, Frags3& f,
                                        f32x4 (&acc)[2][2][4][2], int t, int T, const Edge& e,
                                        bool on, int c_lane, int c_lane2 = 0, int lane = 0,
@@ -271,10 +298,10 @@ __device__ __forceinline__ void phase6(const GemmArgs& p, const Ctx& c, Frags3& 
   if constexpr (P == 1) read_b<kBHi>(c, both, cur);
   if constexpr (P == 2) read_a<kAHi>(c, f.a, cur);
   if constexpr (P == 3) read_b<kBLo>(c, both, cur ^ 1);  // K-tile t+1 (next tile's 0 at t = T-1)
-  if constexpr (P == 0) issue6<kAHi, NX, MASK>(p, c, t + 1, cur ^ 1, T, e.has_next, e.dA, e.dB, e.nm0, e.nn0, lane);
-  if constexpr (P == 1) issue6<kBLo, NX, MASK>(p, c, t + 2, cur, T, e.has_next, e.dA, e.dB, e.nm0, e.nn0, lane);
-  if constexpr (P == 2) issue6<kALo, NX, MASK>(p, c, t + 2, cur, T, e.has_next, e.dA, e.dB, e.nm0, e.nn0, lane);
-  if constexpr (P == 3) issue6<kBHi, NX, MASK>(p, c, t + 2, cur, T, e.has_next, e.dA, e.dB, e.nm0, e.nn0, lane);
+  if constexpr (P == 0) issue6<kAHi, NX, MASK, TL>(p, c, t + 1, cur ^ 1, T, e.has_next, e.dA, e.dB, e.nm0, e.nn0, lane);
+  if constexpr (P == 1) issue6<kBLo, NX, MASK, TL>(p, c, t + 2, cur, T, e.has_next, e.dA, e.dB, e.nm0, e.nn0, lane);
+  if constexpr (P == 2) issue6<kALo, NX, MASK, TL>(p, c, t + 2, cur, T, e.has_next, e.dA, e.dB, e.nm0, e.nn0, lane);
+  if constexpr (P == 3) issue6<kBHi, NX, MASK, TL>(p, c, t + 2, cur, T, e.has_next, e.dA, e.dB, e.nm0, e.nn0, lane);
   if constexpr (VMC == 10) {
     wait_vm<10>();
   } else {
@@ -320,9 +347,10 @@ __device__ __forceinline__ void phase6(const GemmArgs& p, const Ctx& c, Frags3& 
   raw_barrier();
 }
 
-#define NTM_PH(P, ODD, CV, VMC, NX, ON) \
-  phase6<P, ODD, CV, VMC, NX, POL, LINE, STG, MASK>(p, c, f, acc, t, T, e, ON, c_lane, c_lane2, \
-                                                    lane, lrow, lcol)
+#define NTM_PHT(P, ODD, CV, VMC, NX, ON, TL) \
+  phase6<P, ODD, CV, VMC, NX, POL, LINE, STG, MASK, TL>(p, c, f, acc, t, T, e, ON, c_lane, \
+                                                        c_lane2, lane, lrow, lcol)
+#define NTM_PH(P, ODD, CV, VMC, NX, ON) NTM_PHT(P, ODD, CV, VMC, NX, ON, false)
 
 __device__ __forceinline__ void tile_origin(const GemmArgs& p, int tile, int ntiles, int& m0,
                                             int& n0) {
@@ -364,10 +392,15 @@ __device__ __forceinline__ void clock_stamp(unsigned long long& t, unsigned long
 // STG (LINE only): boundary stores staged through LDS in whole lines (store_pair_lds).
 // MASK ("pingpong8om", default layout only): ragged C - ceil(M/256) x
 // ceil(N/256) tiles, sources clamped per tile (src_clamped), stores masked.
-template <int POL, bool LINE = false, int STAMP = 0, bool STG = false, bool MASK = false>
+// TAIL (with MASK): K % 128 != 0 - T = ceil(K / 128) * 2 K-tiles; the pieces
+// that can reach past K (K-tiles T-2 / T-1, issued from K-tiles T-4 .. T-2, or
+// from K-tiles 0 / 1 when T = 4) zero-fill their chunks past K.
+template <int POL, bool LINE = false, int STAMP = 0, bool STG = false, bool MASK = false,
+          bool TAIL = false>
 __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_pp6_kernel(GemmArgs p) {
   static_assert(!STG || LINE, "LDS-staged boundary stores need the whole-line layout");
   static_assert(!MASK || (!LINE && !STG), "the masked build uses the default C layout");
+  static_assert(!TAIL || MASK, "partial K rides on the masked build");
   __shared__ __attribute__((aligned(16))) char smem[STG ? kStgBytes : kLdsBytes3];
   unsigned long long t0 = 0, rt0 = 0;
   if constexpr (STAMP != 0) clock_stamp(t0, rt0);
@@ -400,9 +433,10 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_pp6_kernel(GemmArgs p) 
       c.src[kBHi] = src_clamped<kBHi>(p, e.m0, e.n0, c.w, lane);
     }
   }
-  // masked stores: the lane's row / column inside a quadrant's 16-row block
-  const int lrow = c.wr * 64 + (lane & 15);
-  const int lcol = c.wc * 32 + ((lane >> 4) & 1) * 16 + (lane >> 5) * 8;
+  // masked stores: the wave's row / column offset inside a quadrant (uniform;
+  // the lane part is recomputed at the store, opaque_lane)
+  const int lrow = c.wr * 64;
+  const int lcol = c.wc * 32;
   c.frag_off = (lane & 15) * 64 + ((lane >> 4) ^ ((lane >> 2) & 2)) * 16;
   const int c_lane = (c.wr * 64 + (lane & 15)) * p.ldc + c.wc * (LINE ? 64 : 32) +
                      ((lane >> 4) & 1) * 16 + (lane >> 5) * 8;
@@ -415,7 +449,8 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_pp6_kernel(GemmArgs p) 
 #pragma unroll
     for (int j = 0; j < 2; ++j) zero_quadrant(acc[i][j]);
   Frags3 f;
-  const int T = p.K / BK;
+  const int T = TAIL ? ((p.K + 2 * BK - 1) / (2 * BK)) * 2 : p.K / BK;
+  if constexpr (TAIL) c.K = p.K;
   e.prev = false;
   e.pm0 = e.pn0 = 0;
   int nm0 = 0, nn0 = 0;
@@ -448,17 +483,17 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_pp6_kernel(GemmArgs p) 
   for (;;) {
     int t = 0;
     // K-tile 0: q3 (LINE: row half 1) of the previous tile leaves in P0
-    NTM_PH(0, false, LINE ? 5 : 3, LINE ? 18 : 22, false, e.prev);
-    NTM_PH(1, false, -1, 26, false, e.prev);
-    NTM_PH(2, false, -1, 26, false, e.prev);
-    NTM_PH(3, false, -1, LINE ? 26 : 22, false, e.prev);
+    NTM_PHT(0, false, LINE ? 5 : 3, LINE ? 18 : 22, false, e.prev, TAIL);
+    NTM_PHT(1, false, -1, 26, false, e.prev, TAIL);
+    NTM_PHT(2, false, -1, 26, false, e.prev, TAIL);
+    NTM_PHT(3, false, -1, LINE ? 26 : 22, false, e.prev, TAIL);
     t = 1;
-    NTM_PH(0, true, -1, 18, false, e.prev);
-    NTM_PH(1, true, -1, LINE ? 18 : 14, false, e.prev);
-    NTM_PH(2, true, -1, 10, false, e.prev);
-    NTM_PH(3, true, -1, 10, false, e.prev);
+    NTM_PHT(0, true, -1, 18, false, e.prev, TAIL);
+    NTM_PHT(1, true, -1, LINE ? 18 : 14, false, e.prev, TAIL);
+    NTM_PHT(2, true, -1, 10, false, e.prev, TAIL);
+    NTM_PHT(3, true, -1, 10, false, e.prev, TAIL);
 #pragma nounroll
-    for (t = 2; t < T - 2; t += 2) {
+    for (t = 2; t < T - (TAIL ? 4 : 2); t += 2) {
       NTM_PH(0, false, -1, 10, false, false);
       NTM_PH(1, false, -1, 10, false, false);
       NTM_PH(2, false, -1, 10, false, false);
@@ -470,11 +505,26 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_pp6_kernel(GemmArgs p) 
       NTM_PH(3, true, -1, 10, false, false);
       --t;
     }
+    if constexpr (TAIL) {
+      // the K-tile pair T-4 / T-3 issues K-tiles T-3 .. T-1: zero-fill past K
+      if (T >= 6) {
+        t = T - 4;
+        NTM_PHT(0, false, -1, 10, false, false, true);
+        NTM_PHT(1, false, -1, 10, false, false, true);
+        NTM_PHT(2, false, -1, 10, false, false, true);
+        NTM_PHT(3, false, -1, 10, false, false, true);
+        ++t;
+        NTM_PHT(0, true, -1, 10, false, false, true);
+        NTM_PHT(1, true, -1, 10, false, false, true);
+        NTM_PHT(2, true, -1, 10, false, false, true);
+        NTM_PHT(3, true, -1, 10, false, false, true);
+      }
+    }
     // K-tile T-2 stages the next tile's K-tile 0, K-tile T-1 its K-tile 1 (or
     // dummies); with a next tile, q0..q2 leave in P1..P3 of K-tile T-1 (LINE:
     // row half 0 in P2)
     t = T - 2;
-    NTM_PH(0, false, -1, 10, false, false);
+    NTM_PHT(0, false, -1, 10, false, false, TAIL);
     NTM_PH(1, false, -1, 10, true, false);
     NTM_PH(2, false, -1, 10, true, false);
     NTM_PH(3, false, -1, 10, true, false);
@@ -486,10 +536,11 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_pp6_kernel(GemmArgs p) 
     if (!e.has_next) break;
     // advance to the next tile
     if constexpr (MASK) {
-      c.src[kALo] = src_clamped<kALo>(p, nm0, nn0, c.w, lane);
-      c.src[kAHi] = src_clamped<kAHi>(p, nm0, nn0, c.w, lane);
-      c.src[kBLo] = src_clamped<kBLo>(p, nm0, nn0, c.w, lane);
-      c.src[kBHi] = src_clamped<kBHi>(p, nm0, nn0, c.w, lane);
+      const int l = opaque_lane();
+      c.src[kALo] = src_clamped<kALo>(p, nm0, nn0, c.w, l);
+      c.src[kAHi] = src_clamped<kAHi>(p, nm0, nn0, c.w, l);
+      c.src[kBLo] = src_clamped<kBLo>(p, nm0, nn0, c.w, l);
+      c.src[kBHi] = src_clamped<kBHi>(p, nm0, nn0, c.w, l);
     } else {
 #pragma unroll
       for (int h = 0; h < 4; ++h) c.src[h] += (h == kALo || h == kAHi) ? e.dA : e.dB;
@@ -526,6 +577,7 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_pp6_kernel(GemmArgs p) 
   }
 }
 #undef NTM_PH
+#undef NTM_PHT
 
 // Grid: one workgroup per CU (LDS allows no more), fewer if there are fewer tiles.
 inline int pp6_grid(int ntiles) {
@@ -564,15 +616,19 @@ inline hipError_t launch_gemm_bf16_pp6(const GemmArgs& a, hipStream_t stream) {
   return hipGetLastError();
 }
 
-// pingpong8om: ragged C (any M, N % 8), K % 128, K >= 256.
+// pingpong8om: ragged C (any M, N % 8), K % 8 and K > 128 (K % 128 != 0 on
+// the partial-K build).
 template <int POL>
 inline hipError_t launch_gemm_bf16_pp6_masked(const GemmArgs& a, hipStream_t stream) {
   if (!shape_ok6m(a.M, a.N, a.K) || a.rowsum || a.lda < a.K || a.ldb < a.K || a.ldc < a.N ||
       (a.lda % 8) || (a.ldb % 8) || (a.ldc % 8))
     return hipErrorInvalidValue;
   const int ntiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
-  hipLaunchKernelGGL((gemm_bf16_pp6_kernel<POL, false, 0, false, true>),
-                     dim3((unsigned)pp6_grid(ntiles)), dim3(kThreads), 0, stream, a);
+  const dim3 g((unsigned)pp6_grid(ntiles)), b(kThreads);
+  if (a.K % (2 * BK))
+    hipLaunchKernelGGL((gemm_bf16_pp6_kernel<POL, false, 0, false, true, true>), g, b, 0, stream, a);
+  else
+    hipLaunchKernelGGL((gemm_bf16_pp6_kernel<POL, false, 0, false, true>), g, b, 0, stream, a);
   return hipGetLastError();
 }
 
