@@ -78,6 +78,13 @@ DRIVER_READY_S = {"operator": 240.0, "daemonsets": 300.0}
 # false): no KMM build / DKMS compile, only the device plugin registering
 # amd.com/gpu with the kubelet and the labeller - the SURVEY §7.4 lever
 PLUGIN_READY_S = 30.0
+# the host-prep gate (node-prep DaemonSet with the startup taint): prep script,
+# the queued containerd restart, the verify step's kubelet retry (10 s
+# backoff) and two kubectl calls incl. the kubectl image pull. It runs beside
+# the driver install, so the Job waits for the LONGER of the two: off the
+# path with a driver to install, on it with a preinstalled driver.
+PREP_GATE_S = 45.0
+PREP_GATE_MARK = "kubernetes_cluster_role_v1.node_prep"
 
 PHASE_OF_KIND = [
     ("network", ("module.vpc", "google_compute_network", "google_compute_subnetwork",
@@ -139,6 +146,7 @@ def critical_path(g: Graph, durations: dict | None = None, stack_mode: str = "op
     dur.update(durations or {})
 
     prepull = any(PREPULL_MARK in n for n in g.topo_order())
+    gated = any(PREP_GATE_MARK in n for n in g.topo_order())
 
     def d(addr: str) -> float:
         if addr in dur:
@@ -152,7 +160,8 @@ def critical_path(g: Graph, durations: dict | None = None, stack_mode: str = "op
             pull = dur.get("image_pull", IMAGE_PULL_S)
             if prepull:  # pulled while the driver installed: only the excess remains
                 base -= min(pull, driver)
-            base += driver
+            # the Job schedules once GPUs are allocatable AND the prep gate lifted
+            base += max(driver, dur.get("prep_gate", PREP_GATE_S)) if gated else driver
         return base
 
     finish: dict = {}

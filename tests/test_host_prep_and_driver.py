@@ -312,3 +312,20 @@ def test_prep_gate_init_chain_and_rbac():
     assert len(rules) == 1
     assert render(rules[0].body.attr("resources")) == '["nodes"]'
     assert render(rules[0].body.attr("verbs")) == '["get", "patch"]'
+
+
+@pytest.mark.parametrize("root", ["eks", "gke", "aks"])
+def test_prep_gate_in_the_critical_path(root):
+    """The Job waits for the longer of the driver install and the prep gate:
+    invisible with a driver to install, the in-node wait with a preinstalled
+    driver (the gate's priors: critical_path.PREP_GATE_S)."""
+    from nvidia_terraform_modules_amd.gpu_ready.critical_path import PREP_GATE_S
+
+    g = build_graph(ROOT / root)
+    assert any("kubernetes_cluster_role_v1.node_prep" in n for n in g.topo_order())
+    full = critical_path(g)
+    fast = critical_path(g, driver_preinstalled=True)
+    slow_gate = critical_path(g, durations={"prep_gate": PREP_GATE_S + 100},
+                              driver_preinstalled=True)
+    assert abs((slow_gate.total_s - fast.total_s) - 100) < 1e-6
+    assert critical_path(g, durations={"prep_gate": 1.0}).total_s == full.total_s

@@ -65,6 +65,11 @@ constexpr int kDefaultVariant = 5;
 constexpr int kPersistentVariant = 25;
 // C layout of the shipping pingpong8o build (gemm_bf16_pp6.hpp LINE)
 constexpr bool kPp6Line = false;
+// 47 = pingpong8om, the persistent overlap kernel on ragged C (masked edge
+// tiles, partial K): the plan runs it in place of 22 when the masked 256x256
+// part has more tiles than CUs (round 4, profiles/r4_om/)
+constexpr int kPersistentMaskedVariant = 47;
+constexpr bool kPlanMaskedPersistent = false;
 
 // Tile-shape plan of the default dispatch: the smallest predicted time
 // rounds(tiles) x tile_area / efficiency over 256 CUs, where the efficiencies
@@ -213,6 +218,11 @@ inline K1Plan plan_k1(int M, int N, int K, bool splitk = false, bool fp8 = false
   if (!fp8 && best.feasible() && best.top_variant == kDefaultVariant && K >= 256 &&
       (double)(best.top_rows / 256) * (N / 256) > kCUs)
     best.top_variant = kPersistentVariant;
+  // ... and on ragged C (masked edge tiles; K > 128, K % 8)
+  if (kPlanMaskedPersistent && !fp8 && best.feasible() && best.top_variant == 22 &&
+      ntm::gemm6::shape_ok6m(best.top_rows, N, K) &&
+      (double)((best.top_rows + 255) / 256) * ((N + 255) / 256) > kCUs)
+    best.top_variant = kPersistentMaskedVariant;
   if (!splitk || !best.feasible()) return best;
   // Split-K: C too small to fill 256 CUs with a long K (e.g. 280x6352x7568: 80
   // tiles of 160x160 -> 3 slices of 240 tiles, 631 vs 321 TF/s unsplit).
