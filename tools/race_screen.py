@@ -33,13 +33,15 @@ SHAPES_160 = [(160, 160, 128), (1280, 800, 384), (2560, 1600, 640), (2560, 2560,
 SHAPES_RAGGED = [(1000, 1000, 1024), (1696, 2560, 640), (333, 1004, 384), (2400, 3200, 512),
                  (1000, 1000, 1000), (333, 1004, 200)]  # the last two: partial K-tiles
 MASKED = ("tile128", "tile256x128", "tile160", "tile160x128", "tile128x160", "tile128x256", "pingpong8cm",
-          "default")
+          "pingpong8om", "default")
 # skinny C with a long K: the default dispatch splits K here (k1_splitk_plan)
 SHAPES_SPLITK = [(280, 6352, 7568), (128, 8192, 8192), (333, 1004, 2056), (256, 2048, 8200)]
 # persistent overlap kernel (pingpong8o*, K >= 256): 1-4 tiles per workgroup,
 # one- and two-tile workgroups mixed (4608^2), the shortest tile (K = 256)
 SHAPES_PERSIST = [(256, 256, 256), (1024, 512, 1024), (4608, 4608, 512), (8192, 8192, 256),
                   (6144, 6144, 2048), (2304, 1792, 768), (8192, 8192, 8192)]
+# ... on ragged C with multi-round tiles and partial K (pingpong8om)
+SHAPES_PERSIST_RAGGED = [(4472, 5688, 5832), (4608, 4360, 456), (5000, 4104, 768), (1000, 4104, 328)]
 SHAPES_FP8 = [(256, 256, 256), (256, 512, 512), (512, 768, 768), (2304, 1536, 1280),
               (4096, 4352, 1024), (4096, 4096, 4096), (8192, 8192, 8192)]
 
@@ -71,7 +73,7 @@ def main():
         tm, tn = ops.kernels.TILE_SHAPES.get(v, (0, 0))
         shapes = SHAPES_FP8 + SHAPES_RAGGED if fp8 else SHAPES_160 if tn == 160 else SHAPES
         if v.startswith("pingpong8o"):
-            shapes = SHAPES_PERSIST
+            shapes = SHAPES_PERSIST + (SHAPES_PERSIST_RAGGED if v == "pingpong8om" else [])
         if splits > 1:
             shapes = SHAPES_SPLITK + SHAPES_RAGGED
         elif v in MASKED:
@@ -81,7 +83,7 @@ def main():
                 continue
             if tm and m % tm and v not in MASKED:
                 continue
-            if v == "pingpong8cm" and n % 8:
+            if v in ("pingpong8cm", "pingpong8om") and n % 8:
                 continue
             a = ops.fill_uniform_(torch.empty((m, k), dtype=dt, device=dev), 5 + m)
             b = ops.fill_uniform_(torch.empty((n, k), dtype=dt, device=dev), 6 + n)
