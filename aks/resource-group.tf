@@ -15,6 +15,6 @@ resource "azurerm_resource_group" "this" {
 
 locals {
   tags           = { group = "amd-instinct", managed_by = "Terraform" }
-  prep_taint_key = "amd.com/mi355x-prep"
+  prep_taint_key = "startup-taint.cluster-autoscaler.kubernetes.io/amd-mi355x-prep"
   rg             = var.existing_resource_group_name == null ? azurerm_resource_group.this[0] : data.azurerm_resource_group.existing[0]
 }

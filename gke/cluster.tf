@@ -36,7 +36,7 @@ locals {
   base_labels = { part_of = var.cluster_name, env = var.project_id, managed_by = "terraform" }
   base_tags   = ["tf-managed", var.cluster_name]
 
-  prep_taint_key = "amd.com/mi355x-prep"
+  prep_taint_key = "startup-taint.cluster-autoscaler.kubernetes.io/amd-mi355x-prep"
 }
 
 resource "google_container_cluster" "this" {

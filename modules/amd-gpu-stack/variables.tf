@@ -343,8 +343,8 @@ variable "node_prep_startup_taint" {
 
 variable "node_prep_taint_key" {
   type        = string
-  default     = "amd.com/mi355x-prep"
-  description = "Key of the GPU node pools' startup taint (node_prep_startup_taint)."
+  default     = "startup-taint.cluster-autoscaler.kubernetes.io/amd-mi355x-prep"
+  description = "Key of the GPU node pools' startup taint (node_prep_startup_taint). The cluster-autoscaler prefix marks it as a startup taint: the autoscaler ignores it when it simulates whether a pending pod (the validation Job) fits a new node, so the gate never blocks a scale-up."
 }
 
 variable "node_prep_iommu_mode" {

@@ -223,7 +223,7 @@ def _pod_spec(res):
     return _blocks(tmpl.body, "spec")[0].body
 
 
-PREP = "amd.com/mi355x-prep"
+PREP = "startup-taint.cluster-autoscaler.kubernetes.io/amd-mi355x-prep"
 
 
 @pytest.mark.parametrize("root", ["eks", "gke", "aks"])
