@@ -710,7 +710,7 @@ def test_fp8_dma4_vs_torch_fp32(ops, knob, m, n, k):
     assert torch.equal(ck.view(torch.int16), ops.gemm_fp8(a, b).view(torch.int16))
 
 
-@pytest.mark.parametrize("variant", ["pingpong8o", "pingpong8ol", "pingpong8ols"])
+@pytest.mark.parametrize("variant", ["pingpong8o", "pingpong8ol", "pingpong8ols", "pingpong8od"])
 @pytest.mark.parametrize("m,n,k", [(256, 256, 256), (1024, 512, 1024), (4608, 4608, 512),
                                    (8192, 8192, 256), (2304, 1792, 768)])
 def test_persistent_overlap_vs_torch_fp32(ops, variant, m, n, k):

@@ -185,6 +185,43 @@ __device__ __forceinline__ void store_quadrant(const GemmArgs& p, const f32x4 (&
   }
 }
 
+// One 16-row block (mt) of a quadrant: the SPREAD build's unit of store.
+template <int MH, int NH, int MT, int POL>
+__device__ __forceinline__ void store_block(const GemmArgs& p, const f32x4 (&q)[4][2], int m0,
+                                            int n0, int c_lane) {
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  const f32x4 v0 = q[MT][0], v1 = q[MT][1];
+  unsigned w0[2], w1[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const auto r = __builtin_amdgcn_permlane16_swap(pack_bf16x2(v0[2 * h], v0[2 * h + 1]),
+                                                    pack_bf16x2(v1[2 * h], v1[2 * h + 1]),
+                                                    false, false);
+    w0[h] = r[0];
+    w1[h] = r[1];
+  }
+  __bf16* tile = p.C + (size_t)(m0 + MH * 128 + MT * 16) * p.ldc + (n0 + NH * 128);
+  store_c16<POL>(tile + c_lane, u32x4{w0[0], w0[1], w1[0], w1[1]});
+}
+
+__device__ __forceinline__ void zero_quadrant(f32x4 (&q)[4][2]);
+
+// SPREAD: the store unit of boundary phase O (0 = P1 of K-tile T-1 .. 6 = P3
+// of the next tile's K-tile 0) for quadrant Q (finishing order q0..q3): block
+// mt = O - Q, zeroing the quadrant after its last block. q0..q2's blocks in
+// O <= 2 belong to this tile, everything from O = 3 on to the previous one.
+template <int O, int Q, int POL>
+__device__ __forceinline__ void spread_unit(const GemmArgs& p, f32x4 (&acc)[2][2][4][2],
+                                            int m0, int n0, int pm0, int pn0, int c_lane) {
+  constexpr int MT = O - Q;
+  if constexpr (MT >= 0 && MT <= 3) {
+    constexpr int MH = (Q == 2 || Q == 3) ? 1 : 0;
+    constexpr int NH = (Q == 1 || Q == 2) ? 1 : 0;
+    store_block<MH, NH, MT, POL>(p, acc[MH][NH], O >= 3 ? pm0 : m0, O >= 3 ? pn0 : n0, c_lane);
+    if constexpr (MT == 3) zero_quadrant(acc[MH][NH]);
+  }
+}
+
 // LINE layout: both quadrants of row half MH, one 16-row block at a time, so a
 // wave's two adjacent 64-B half-lines of a row leave in consecutive store
 // instructions (a whole 128-B line per row and block).
@@ -310,7 +347,15 @@ __device__ __forceinline__ void phase6(const GemmArgs& p, const Ctx& c, Frags3& 
     else
       wait_vm<10>();
   }
-  if constexpr (CONV >= 4) {
+  if constexpr (CONV >= 10) {  // SPREAD build: boundary phase O = CONV - 10
+    if (on) {
+      constexpr int O = CONV - 10;
+      spread_unit<O, 0, POL>(p, acc, e.m0, e.n0, e.pm0, e.pn0, c_lane);
+      spread_unit<O, 1, POL>(p, acc, e.m0, e.n0, e.pm0, e.pn0, c_lane);
+      spread_unit<O, 2, POL>(p, acc, e.m0, e.n0, e.pm0, e.pn0, c_lane);
+      spread_unit<O, 3, POL>(p, acc, e.m0, e.n0, e.pm0, e.pn0, c_lane);
+    }
+  } else if constexpr (CONV >= 4) {
     if (on) {
       constexpr int MH = CONV - 4;
       const int m0 = MH == 1 ? e.pm0 : e.m0, n0 = MH == 1 ? e.pn0 : e.n0;
@@ -395,9 +440,17 @@ __device__ __forceinline__ void clock_stamp(unsigned long long& t, unsigned long
 // TAIL (with MASK): K % 128 != 0 - T = ceil(K / 128) * 2 K-tiles; the pieces
 // that can reach past K (K-tiles T-2 / T-1, issued from K-tiles T-4 .. T-2, or
 // from K-tiles 0 / 1 when T = 4) zero-fill their chunks past K.
+// SPREAD (experimental, default layout): each boundary quadrant's 4 store
+// blocks go out one per phase over the 4 phases it has before its reuse
+// (stores per phase 1,2,3,4,3,2,1 from P1 of K-tile T-1 to P3 of the next
+// tile's K-tile 0, instead of 4,4,4,4); counted waits 10 + stores in phases
+// j-5 .. j-1: P1(T-1) 10, P2 11, P3 13, P0(0) 16, P1 20, P2 23, P3 24,
+// P0(1) 23, P1 20, P2 16, P3 13 (P0(2) needs 11; the loop's 10 over-waits by
+// one store issued 5 phases earlier).
 template <int POL, bool LINE = false, int STAMP = 0, bool STG = false, bool MASK = false,
-          bool TAIL = false>
+          bool TAIL = false, bool SPREAD = false>
 __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_pp6_kernel(GemmArgs p) {
+  static_assert(!SPREAD || (!LINE && !MASK), "SPREAD: default layout, whole tiles");
   static_assert(!STG || LINE, "LDS-staged boundary stores need the whole-line layout");
   static_assert(!MASK || (!LINE && !STG), "the masked build uses the default C layout");
   static_assert(!TAIL || MASK, "partial K rides on the masked build");
@@ -483,15 +536,15 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_pp6_kernel(GemmArgs p) 
   for (;;) {
     int t = 0;
     // K-tile 0: q3 (LINE: row half 1) of the previous tile leaves in P0
-    NTM_PHT(0, false, LINE ? 5 : 3, LINE ? 18 : 22, false, e.prev, TAIL);
-    NTM_PHT(1, false, -1, 26, false, e.prev, TAIL);
-    NTM_PHT(2, false, -1, 26, false, e.prev, TAIL);
-    NTM_PHT(3, false, -1, LINE ? 26 : 22, false, e.prev, TAIL);
+    NTM_PHT(0, false, SPREAD ? 13 : LINE ? 5 : 3, SPREAD ? 16 : LINE ? 18 : 22, false, e.prev, TAIL);
+    NTM_PHT(1, false, SPREAD ? 14 : -1, SPREAD ? 20 : 26, false, e.prev, TAIL);
+    NTM_PHT(2, false, SPREAD ? 15 : -1, SPREAD ? 23 : 26, false, e.prev, TAIL);
+    NTM_PHT(3, false, SPREAD ? 16 : -1, SPREAD ? 24 : LINE ? 26 : 22, false, e.prev, TAIL);
     t = 1;
-    NTM_PHT(0, true, -1, 18, false, e.prev, TAIL);
-    NTM_PHT(1, true, -1, LINE ? 18 : 14, false, e.prev, TAIL);
-    NTM_PHT(2, true, -1, 10, false, e.prev, TAIL);
-    NTM_PHT(3, true, -1, 10, false, e.prev, TAIL);
+    NTM_PHT(0, true, -1, SPREAD ? 23 : 18, false, e.prev, TAIL);
+    NTM_PHT(1, true, -1, SPREAD ? 20 : LINE ? 18 : 14, false, e.prev, TAIL);
+    NTM_PHT(2, true, -1, SPREAD ? 16 : 10, false, e.prev, TAIL);
+    NTM_PHT(3, true, -1, SPREAD ? 13 : 10, false, e.prev, TAIL);
 #pragma nounroll
     for (t = 2; t < T - (TAIL ? 4 : 2); t += 2) {
       NTM_PH(0, false, -1, 10, false, false);
@@ -530,9 +583,9 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_pp6_kernel(GemmArgs p) 
     NTM_PH(3, false, -1, 10, true, false);
     t = T - 1;
     NTM_PH(0, true, -1, 10, true, false);
-    NTM_PH(1, true, LINE ? -1 : 0, 10, true, e.has_next);
-    NTM_PH(2, true, LINE ? 4 : 1, LINE ? 10 : 14, true, e.has_next);
-    NTM_PH(3, true, LINE ? -1 : 2, 18, true, e.has_next);
+    NTM_PH(1, true, SPREAD ? 10 : LINE ? -1 : 0, 10, true, e.has_next);
+    NTM_PH(2, true, SPREAD ? 11 : LINE ? 4 : 1, SPREAD ? 11 : LINE ? 10 : 14, true, e.has_next);
+    NTM_PH(3, true, SPREAD ? 12 : LINE ? -1 : 2, SPREAD ? 13 : 18, true, e.has_next);
     if (!e.has_next) break;
     // advance to the next tile
     if constexpr (MASK) {
@@ -605,13 +658,14 @@ inline hipError_t launch_gemm_bf16_pp6_grid(const GemmArgs& a, int grid, hipStre
   return hipGetLastError();
 }
 
-template <int POL, bool LINE = false, int STAMP = 0, bool STG = false>
+template <int POL, bool LINE = false, int STAMP = 0, bool STG = false, bool SPREAD = false>
 inline hipError_t launch_gemm_bf16_pp6(const GemmArgs& a, hipStream_t stream) {
   if (!shape_ok6(a.M, a.N, a.K) || a.rowsum || a.lda < a.K || a.ldb < a.K || a.ldc < a.N ||
       (a.lda % 8) || (a.ldb % 8) || (a.ldc % 8) || (STAMP != 0 && a.stamps == nullptr))
     return hipErrorInvalidValue;
   const int ntiles = (a.M / BM) * (a.N / BN);
-  hipLaunchKernelGGL((gemm_bf16_pp6_kernel<POL, LINE, STAMP, STG>), dim3((unsigned)pp6_grid(ntiles)),
+  hipLaunchKernelGGL((gemm_bf16_pp6_kernel<POL, LINE, STAMP, STG, false, false, SPREAD>),
+                     dim3((unsigned)pp6_grid(ntiles)),
                      dim3(kThreads), 0, stream, a);
   return hipGetLastError();
 }

@@ -81,6 +81,8 @@ NTM_API int ntm_gemm_bf16_experimental(int variant, const void* A, const void* B
     case 45: return (int)ntm::gemm6::launch_gemm_bf16_pp6_grid<2, true>(a, 256, S(stream));
     // whole-line layout with the boundary stores staged through LDS in whole lines
     case 46: return (int)ntm::gemm6::launch_gemm_bf16_pp6<1, true, 0, true>(a, S(stream));
+    // boundary stores spread one block per phase (SPREAD)
+    case 48: return (int)ntm::gemm6::launch_gemm_bf16_pp6<1, false, 0, false, true>(a, S(stream));
     default: return (int)hipErrorInvalidValue;
   }
 }
