@@ -114,6 +114,8 @@ def _declare_experimental(lib: ctypes.CDLL) -> None:
         "ntm_mfma_rate": ([c_int, c_int, c_int, c_vp, c_vp, c_vp], c_int),
         "ntm_gemm_fp8_knob": ([c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                                c_vp], c_int),
+        "ntm_gemm_bf16_pp6_stamp": ([c_int, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int,
+                                     c_int, c_int, c_vp, c_vp], c_int),
     }
     for name, (argt, rest) in sig.items():
         fn = getattr(lib, name)

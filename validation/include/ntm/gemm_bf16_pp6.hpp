@@ -339,7 +339,9 @@ __device__ __forceinline__ void phase6(const GemmArgs& p, const Ctx& c, Frags3& 
   if constexpr (P == 1) issue6<kBLo, NX, MASK, TL>(p, c, t + 2, cur, T, e.has_next, e.dA, e.dB, e.nm0, e.nn0, lane);
   if constexpr (P == 2) issue6<kALo, NX, MASK, TL>(p, c, t + 2, cur, T, e.has_next, e.dA, e.dB, e.nm0, e.nn0, lane);
   if constexpr (P == 3) issue6<kBHi, NX, MASK, TL>(p, c, t + 2, cur, T, e.has_next, e.dA, e.dB, e.nm0, e.nn0, lane);
-  if constexpr (VMC == 10) {
+  // POL 2 (C not stored): no stores in the stream, so the pieces-only count
+  // (round 3's ablation kept the store-counting waits, which then under-waited)
+  if constexpr (VMC == 10 || POL == 2) {
     wait_vm<10>();
   } else {
     if (on)
@@ -396,6 +398,17 @@ __device__ __forceinline__ void phase6(const GemmArgs& p, const Ctx& c, Frags3& 
   phase6<P, ODD, CV, VMC, NX, POL, LINE, STG, MASK, TL>(p, c, f, acc, t, T, e, ON, c_lane, \
                                                         c_lane2, lane, lrow, lcol)
 #define NTM_PH(P, ODD, CV, VMC, NX, ON) NTM_PHT(P, ODD, CV, VMC, NX, ON, false)
+// STAMP 2: shader-clock stamp I of wave 0 at a phase start of the workgroup's
+// first tile boundary (K-tiles T-2 / T-1 of its first tile: I = 0..7, K-tiles
+// 0 / 1 of its second: I = 8..15, 16 = after K-tile 1), into p.stamps[17 b + I]
+#define NTM_ST(I, FIRST)                                                          \
+  if constexpr (STAMP == 2) {                                                     \
+    if (tile == (int)blockIdx.x + ((FIRST) ? 0 : G)) {                            \
+      unsigned long long st_t, st_rt;                                             \
+      clock_stamp(st_t, st_rt);                                                   \
+      if (threadIdx.x == 0) p.stamps[17 * (size_t)blockIdx.x + (I)] = st_t;       \
+    }                                                                             \
+  }
 
 __device__ __forceinline__ void tile_origin(const GemmArgs& p, int tile, int ntiles, int& m0,
                                             int& n0) {
@@ -456,7 +469,7 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_pp6_kernel(GemmArgs p) 
   static_assert(!TAIL || MASK, "partial K rides on the masked build");
   __shared__ __attribute__((aligned(16))) char smem[STG ? kStgBytes : kLdsBytes3];
   unsigned long long t0 = 0, rt0 = 0;
-  if constexpr (STAMP != 0) clock_stamp(t0, rt0);
+  if constexpr (STAMP == 1) clock_stamp(t0, rt0);
   const int ntiles = MASK ? ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN) : (p.M / BM) * (p.N / BN);
   const int G = (int)gridDim.x;
   int tile = (int)blockIdx.x;
@@ -536,15 +549,24 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_pp6_kernel(GemmArgs p) 
   for (;;) {
     int t = 0;
     // K-tile 0: q3 (LINE: row half 1) of the previous tile leaves in P0
+    NTM_ST(8, false);
     NTM_PHT(0, false, SPREAD ? 13 : LINE ? 5 : 3, SPREAD ? 16 : LINE ? 18 : 22, false, e.prev, TAIL);
+    NTM_ST(9, false);
     NTM_PHT(1, false, SPREAD ? 14 : -1, SPREAD ? 20 : 26, false, e.prev, TAIL);
+    NTM_ST(10, false);
     NTM_PHT(2, false, SPREAD ? 15 : -1, SPREAD ? 23 : 26, false, e.prev, TAIL);
+    NTM_ST(11, false);
     NTM_PHT(3, false, SPREAD ? 16 : -1, SPREAD ? 24 : LINE ? 26 : 22, false, e.prev, TAIL);
     t = 1;
+    NTM_ST(12, false);
     NTM_PHT(0, true, -1, SPREAD ? 23 : 18, false, e.prev, TAIL);
+    NTM_ST(13, false);
     NTM_PHT(1, true, -1, SPREAD ? 20 : LINE ? 18 : 14, false, e.prev, TAIL);
+    NTM_ST(14, false);
     NTM_PHT(2, true, -1, SPREAD ? 16 : 10, false, e.prev, TAIL);
+    NTM_ST(15, false);
     NTM_PHT(3, true, -1, SPREAD ? 13 : 10, false, e.prev, TAIL);
+    NTM_ST(16, false);
 #pragma nounroll
     for (t = 2; t < T - (TAIL ? 4 : 2); t += 2) {
       NTM_PH(0, false, -1, 10, false, false);
@@ -577,14 +599,22 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_pp6_kernel(GemmArgs p) 
     // dummies); with a next tile, q0..q2 leave in P1..P3 of K-tile T-1 (LINE:
     // row half 0 in P2)
     t = T - 2;
+    NTM_ST(0, true);
     NTM_PHT(0, false, -1, 10, false, false, TAIL);
+    NTM_ST(1, true);
     NTM_PH(1, false, -1, 10, true, false);
+    NTM_ST(2, true);
     NTM_PH(2, false, -1, 10, true, false);
+    NTM_ST(3, true);
     NTM_PH(3, false, -1, 10, true, false);
     t = T - 1;
+    NTM_ST(4, true);
     NTM_PH(0, true, -1, 10, true, false);
+    NTM_ST(5, true);
     NTM_PH(1, true, SPREAD ? 10 : LINE ? -1 : 0, 10, true, e.has_next);
+    NTM_ST(6, true);
     NTM_PH(2, true, SPREAD ? 11 : LINE ? 4 : 1, SPREAD ? 11 : LINE ? 10 : 14, true, e.has_next);
+    NTM_ST(7, true);
     NTM_PH(3, true, SPREAD ? 12 : LINE ? -1 : 2, SPREAD ? 13 : 18, true, e.has_next);
     if (!e.has_next) break;
     // advance to the next tile
@@ -617,7 +647,7 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_pp6_kernel(GemmArgs p) 
   wait_vm<0>();                  // dummy pieces: nothing may land after the WG exits
   if (POL != 2 || p.ldc < 0)
     store_tile_lds<false, POL != 0, MASK, POL == 0 ? 0 : 1, LINE>(p, c, acc, e.m0, e.n0, lane);
-  if constexpr (STAMP != 0) {
+  if constexpr (STAMP == 1) {
     unsigned long long t1, rt1;
     clock_stamp(t1, rt1);
     if (threadIdx.x == 0) {
@@ -631,6 +661,7 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_pp6_kernel(GemmArgs p) 
 }
 #undef NTM_PH
 #undef NTM_PHT
+#undef NTM_ST
 
 // Grid: one workgroup per CU (LDS allows no more), fewer if there are fewer tiles.
 inline int pp6_grid(int ntiles) {
@@ -648,13 +679,15 @@ inline int pp6_grid(int ntiles) {
 
 // Experimental: an explicit grid (a multiple of 8, at most the tile count) and
 // POL 2 (C not stored) - the store-bandwidth study of profiles/r3_stores.
-template <int POL, bool LINE = false>
+template <int POL, bool LINE = false, int STAMP = 0>
 inline hipError_t launch_gemm_bf16_pp6_grid(const GemmArgs& a, int grid, hipStream_t stream) {
   if (!shape_ok6(a.M, a.N, a.K) || a.rowsum || a.lda < a.K || a.ldb < a.K || a.ldc < a.N ||
       (a.lda % 8) || (a.ldb % 8) || (a.ldc % 8) || grid <= 0 || grid % 8 ||
       grid > (a.M / BM) * (a.N / BN))
     return hipErrorInvalidValue;
-  hipLaunchKernelGGL((gemm_bf16_pp6_kernel<POL, LINE>), dim3((unsigned)grid), dim3(kThreads), 0, stream, a);
+  if (STAMP != 0 && a.stamps == nullptr) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((gemm_bf16_pp6_kernel<POL, LINE, STAMP>), dim3((unsigned)grid), dim3(kThreads), 0,
+                     stream, a);
   return hipGetLastError();
 }
 

@@ -87,6 +87,19 @@ NTM_API int ntm_gemm_bf16_experimental(int variant, const void* A, const void* B
   }
 }
 
+// pingpong8o boundary-phase stamps (gemm_bf16_pp6.hpp STAMP 2): grid 128 or 256
+// workgroups (a multiple of 8, <= tiles, each workgroup >= 2 tiles), store 1 =
+// C stored (nontemporal) / 0 = not stored; stamps: 17 u64 per workgroup.
+NTM_API int ntm_gemm_bf16_pp6_stamp(int grid, int store, const void* A, const void* B, void* C,
+                                    int M, int N, int K, int lda, int ldb, int ldc, void* stamps,
+                                    void* stream) {
+  ntm::gemm::GemmArgs a = args(A, B, C, M, N, K, lda, ldb, ldc);
+  a.stamps = (unsigned long long*)stamps;
+  if (grid * 2 > (M / 256) * (N / 256)) return (int)hipErrorInvalidValue;
+  return store ? (int)ntm::gemm6::launch_gemm_bf16_pp6_grid<1, false, 2>(a, grid, S(stream))
+               : (int)ntm::gemm6::launch_gemm_bf16_pp6_grid<2, false, 2>(a, grid, S(stream));
+}
+
 // pingpong8c tuning knobs (see launch_gemm_bf16_pp3_knob).
 NTM_API int ntm_gemm_bf16_knob(int knob, const void* A, const void* B, void* C, int M, int N,
                                int K, int lda, int ldb, int ldc, void* stream) {
