@@ -570,8 +570,15 @@ def gemm_clock_ghz(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = 
     t1.record()
     t1.synchronize()
     v = stamps.view(-1, 4).double()
-    res = _ghz_summary((v[:, 2] - v[:, 0]) / (v[:, 3] - v[:, 1]) * 0.1)
+    ghz = (v[:, 2] - v[:, 0]) / (v[:, 3] - v[:, 1]) * 0.1
+    res = _ghz_summary(ghz)
     res["workgroups"] = res.pop("n")
+    # workgroups b with the same b & 7 share an XCD (the dispatcher's round
+    # robin; a label, not the XCD's id): the spread of the group medians is
+    # the per-XCD clock spread under this load
+    g = ghz.view(steps, grid)
+    groups = [g[:, x::8].reshape(-1) for x in range(min(8, grid))]
+    res["per_xcd_group_median_GHz"] = [_ghz_summary(x)["median_GHz"] for x in groups]
     res["ms_per_launch"] = round(t0.elapsed_time(t1) / steps, 4)
     res["launches"] = steps
     return res

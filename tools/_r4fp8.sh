@@ -1,4 +1,6 @@
-# round-4 fp8 store-path study + GEMM clock check (one gpurun call)
+# round-4: race screens of the new K1 builds, the GEMM clock check, and the
+# fp8 store-path PMC (K1-fp8 vs hipBLASLt fp8 at the Job's three shapes)
+PYARGS="--variants pingpong8om,pingpong8ol,pingpong8ols,pingpong8od --repeats 100" bash tools/gpu_run.sh r4_race py:tools/race_screen.py && \
 bash tools/gpu_run.sh r4_clock clock && \
 PMC_DTYPE=fp8 bash tools/gpu_run.sh r4_fp8pmc_8192 pmc && \
 PMC_DTYPE=fp8 PMC_SHAPE=8192x8192x4096 bash tools/gpu_run.sh r4_fp8pmc_8k8k4k pmc && \
