@@ -4,4 +4,5 @@ PYARGS="--variants pingpong8om,pingpong8ol,pingpong8ols,pingpong8od --repeats 10
 bash tools/gpu_run.sh r4_clock clock && \
 PMC_DTYPE=fp8 bash tools/gpu_run.sh r4_fp8pmc_8192 pmc && \
 PMC_DTYPE=fp8 PMC_SHAPE=8192x8192x4096 bash tools/gpu_run.sh r4_fp8pmc_8k8k4k pmc && \
-PMC_DTYPE=fp8 PMC_SHAPE=4096x4096x4096 bash tools/gpu_run.sh r4_fp8pmc_4096 pmc
+PMC_DTYPE=fp8 PMC_SHAPE=4096x4096x4096 bash tools/gpu_run.sh r4_fp8pmc_4096 pmc && \
+PYARGS="--sizes 4096,8192,8192x8192x4096 --variants tile256x128,tile128x256 --no-bf16 --rounds 7 --iters 30" bash tools/gpu_run.sh r4_fp8tiles py:tools/gemm_fp8_check.py

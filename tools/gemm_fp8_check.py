@@ -7,7 +7,7 @@ fp8 GEMM through torch._scaled_mm (unit scales, bf16 out). One JSON line per
 size.
 
     python tools/gemm_fp8_check.py [--sizes 4096,8192,6144x8192x4096] [--iters 50] [--rounds 7]
-        [--knobs 12,22] [--no-bf16]
+        [--knobs 12] [--variants tile256x128,tile128x256] [--no-bf16]
 """
 from __future__ import annotations
 
@@ -40,8 +40,12 @@ def main() -> int:
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--knobs", default="", help="comma list of experimental fp8 knobs to time too")
     ap.add_argument("--no-bf16", action="store_true", help="skip the bf16 K1 / hipBLASLt timings")
+    ap.add_argument("--variants", default="",
+                    help="comma list of K1-fp8 variants (ops.FP8_VARIANTS) to time next to the "
+                         "default plan, each verified bitwise-equal-or-within-tolerance first")
     args = ap.parse_args()
     knobs = [int(x) for x in args.knobs.split(",") if x]
+    variants = [v for v in args.variants.split(",") if v]
     dev = torch.device("cuda:0")
     ok_all = True
     for size in args.sizes.split(","):
@@ -69,6 +73,12 @@ def main() -> int:
             ok_all &= kbad == 0
             print(json.dumps({"size": s, "knob": kn, "mismatch_vs_default": kbad}), flush=True)
             fns[f"knob{kn}_fp8"] = (lambda kn=kn: ops.gemm_fp8(a, b, c, knob=kn))
+        for v in variants:
+            cv = ops.gemm_fp8(a, b, variant=v)
+            vbad = int(((cv.float() - c.float()).abs() > 1e-2 * (1 + c.float().abs())).sum())
+            ok_all &= vbad == 0
+            print(json.dumps({"size": s, "variant": v, "mismatch_vs_default": vbad}), flush=True)
+            fns[f"{v}_fp8"] = (lambda v=v: ops.gemm_fp8(a, b, c, variant=v))
         one = torch.ones((), device=dev)
         try:
             torch._scaled_mm(a, b.T, scale_a=one, scale_b=one, out_dtype=torch.bfloat16)
