@@ -731,6 +731,22 @@ def test_persistent_overlap_vs_torch_fp32(ops, variant, m, n, k):
     assert torch.equal(c, ops.gemm_bf16(a, b, variant="pingpong8c"))
 
 
+@pytest.mark.parametrize("m,n,k", [(256, 256, 512), (2048, 1024, 1024), (4608, 4608, 512),
+                                   (8192, 8192, 2048), (8192, 8192, 256)])
+def test_fp8_persistent_overlap_vs_torch_fp32(ops, m, n, k):
+    """K1-fp8 on the persistent overlap kernel (fp8 knob 30: pingpong8o with
+    f8f6f4 MFMAs on VGPR accumulators, round 4): 1-4 tiles per workgroup, vs
+    the fp32 product of the e4m3 values, and bitwise equal to the default fp8
+    build (per accumulator the same MFMAs in the same K order)."""
+    a = ops.fill_uniform_(torch.empty((m, k), dtype=torch.float8_e4m3fn, device="cuda"), 31)
+    b = ops.fill_uniform_(torch.empty((n, k), dtype=torch.float8_e4m3fn, device="cuda"), 32)
+    ck = ops.gemm_fp8(a, b, knob=30)
+    ref = a.float() @ b.float().T
+    atol, rtol = ops.gemm_tolerance(k)
+    assert ((ck.float() - ref).abs() <= atol + rtol * ref.abs()).all()
+    assert torch.equal(ck.view(torch.int16), ops.gemm_fp8(a, b).view(torch.int16))
+
+
 @pytest.mark.parametrize("m,n,k", [(1000, 1000, 256), (4472, 5688, 640), (4608, 4360, 512),
                                    (8192, 8192, 256), (333, 1000, 384), (5000, 4104, 768),
                                    # partial K (K % 128 != 0): 4, 6, 8 K-tiles, the last

@@ -53,3 +53,21 @@ def test_shipping_library_isa_is_clean():
     dirty = {n: scan.scan_kernel(b) for n, b in ks.items()
              if not scan.EXEMPT.search(n) and scan.scan_kernel(b) != (0, 0)}
     assert not dirty, dirty
+
+
+VMFMA = "v_mfma_f32_16x16x128_f8f6f4 v[200:203], v[40:47], v[8:15], v[200:203]"
+
+
+def test_vgpr_accumulator_asm_mfma_hazards():
+    """Inline-asm MFMAs with VGPR accumulators (the fp8 persistent build): a
+    VALU write of srcC right before, an unpadded VALU read of the result right
+    after; only MFMAs inside ;;#ASMSTART / ;;#ASMEND count (hipcc pads its own)."""
+    asm = [";;#ASMSTART", VMFMA, ";;#ASMEND"]
+    assert scan.scan_kernel(["v_mov_b32_e32 v201, 0", "s_nop 0"] + asm) == (1, 0)
+    assert scan.scan_kernel(asm + ["v_cvt_pk_bf16_f32 v10, v200, v201"]) == (0, 1)
+    assert scan.scan_kernel(asm + ["s_nop 15", "s_nop 7", "v_cvt_pk_bf16_f32 v10, v200, v201"]) \
+        == (0, 0)
+    # the next MFMA accumulating into the same registers needs no padding
+    assert scan.scan_kernel(asm + asm) == (0, 0)
+    # a compiler-emitted (builtin) MFMA of the same form is not scanned
+    assert scan.scan_kernel(["v_mov_b32_e32 v201, 0", VMFMA]) == (0, 0)

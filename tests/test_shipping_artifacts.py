@@ -33,11 +33,11 @@ ALLOWED_K1 = {
     "ntm::gemm3::gemm_bf16_pp3_kernel<false, 8, false, 26, 0, 3>",  # K1-fp8, masked
     "ntm::gemm3::gemm_bf16_pp3_kernel<false, 8, false, 58, 0, 0>",  # masked + partial K
     "ntm::gemm3::gemm_bf16_pp3_kernel<false, 8, false, 58, 0, 3>",  # K1-fp8, masked + partial K
-    # pingpong8o <POL, LINE, STAMP, STG, MASK, TAIL, SPREAD>: > 256 tiles of 256x256
-    "ntm::gemm6::gemm_bf16_pp6_kernel<1, false, 0, false, false, false, false>",
-    "ntm::gemm6::gemm_bf16_pp6_kernel<1, false, 1, false, false, false, false>",  # clock stamps
-    "ntm::gemm6::gemm_bf16_pp6_kernel<1, false, 0, false, true, false, false>",   # pingpong8om
-    "ntm::gemm6::gemm_bf16_pp6_kernel<1, false, 0, false, true, true, false>",    # + partial K
+    # pingpong8o <POL, LINE, STAMP, STG, MASK, TAIL, SPREAD, F8>: > 256 tiles of 256x256
+    "ntm::gemm6::gemm_bf16_pp6_kernel<1, false, 0, false, false, false, false, false>",
+    "ntm::gemm6::gemm_bf16_pp6_kernel<1, false, 1, false, false, false, false, false>",  # clock stamps
+    "ntm::gemm6::gemm_bf16_pp6_kernel<1, false, 0, false, true, false, false, false>",   # pingpong8om
+    "ntm::gemm6::gemm_bf16_pp6_kernel<1, false, 0, false, true, true, false, false>",    # + partial K
     "ntm::gemm2::gemm_bf16_pp2_kernel<false, 0>",
     "ntm::gemm2::gemm_bf16_pp2_kernel<false, 3>",
     "ntm::gemm2::gemm_bf16_pp2_kernel<true, 0>",

@@ -13,7 +13,12 @@ For every kernel with an MFMA this reports the number of
     as srcC, and
   * VALU accesses of an MFMA's destination AGPRs fewer than MFMA_TO_VALU_WS
     wait states after it (the other direction; s_nop N counts N + 1, an MFMA
-    4).
+    4);
+and, for inline-asm MFMAs with VGPR accumulators (the fp8 persistent build,
+gemm_bf16_pp6.hpp mfma_f8_vgpr; only asm ones - hipcc pads its own), the same
+two counts over VGPRs: non-MFMA writes of a srcC VGPR within WINDOW
+instructions before, any non-MFMA access of a dst VGPR within MFMA_TO_VALU_WS
+wait states after.
 The scan is linear over the listing and stops at an unconditional branch
 (the next block is then reached from elsewhere). Exit status 1 if a GEMM kernel (not the rate probes, whose values are unused)
 has a hit.
@@ -39,6 +44,8 @@ WINDOW = 12
 MFMA_TO_VALU_WS = 19
 
 _MFMA = re.compile(r"v_mfma\S* a\[(\d+):(\d+)\], v\[\d+:\d+\], v\[\d+:\d+\], a\[(\d+):(\d+)\]")
+_MFMA_V = re.compile(r"v_mfma\S* v\[(\d+):(\d+)\], v\[\d+:\d+\], v\[\d+:\d+\], v\[(\d+):(\d+)\]")
+_VREF = re.compile(r"\bv\[(\d+):(\d+)\]|\bv(\d+)\b")
 _AWRITE = re.compile(r"v_accvgpr_(?:write|mov)_b32 a(\d+)")
 _AREAD = re.compile(r"v_accvgpr_read_b32 \S+, a(\d+)")
 _NOFALL = re.compile(r"^\s*(s_branch|s_endpgm|s_setpc_b64)\b")
@@ -48,9 +55,68 @@ def _regs(lo: str, hi: str) -> set[int]:
     return set(range(int(lo), int(hi) + 1))
 
 
-def scan_kernel(lines: list[str]) -> tuple[int, int]:
-    lines = [ln for ln in lines if ln.strip() and not ln.strip().startswith(";")]
+def _vregs(text: str) -> list[set[int]]:
+    """Register sets of every VGPR operand in an instruction, in order."""
+    out = []
+    for m in _VREF.finditer(text):
+        out.append(_regs(m.group(1), m.group(2)) if m.group(1) else {int(m.group(3))})
+    return out
+
+
+def _strip(lines: list[str]) -> tuple[list[str], list[bool]]:
+    """Instruction lines and whether each sits between ;;#ASMSTART / ;;#ASMEND."""
+    out, in_asm, inside = [], [], False
+    for ln in lines:
+        t = ln.strip()
+        if t.startswith(";;#ASMSTART"):
+            inside = True
+        elif t.startswith(";;#ASMEND"):
+            inside = False
+        if t and not t.startswith(";"):
+            out.append(ln)
+            in_asm.append(inside)
+    return out, in_asm
+
+
+def scan_kernel_vgpr(lines: list[str]) -> tuple[int, int]:
+    """The two hazard counts for inline-asm MFMAs with VGPR accumulators."""
+    lines, in_asm = _strip(lines)
     before = after = 0
+    for i, ln in enumerate(lines):
+        m = _MFMA_V.search(ln)
+        if not m or not in_asm[i]:
+            continue
+        dst, src = _regs(m.group(1), m.group(2)), _regs(m.group(3), m.group(4))
+        for j in range(i - 1, max(-1, i - 1 - WINDOW), -1):
+            if _NOFALL.search(lines[j]):
+                break
+            if "v_mfma" in lines[j]:
+                continue
+            ops = _vregs(lines[j].split(";")[0])
+            op = lines[j].split()[0] if lines[j].split() else ""
+            writes = op.startswith("v_") and ops and ops[0] & src
+            if writes:
+                before += 1
+        ws = 0
+        for j in range(i + 1, len(lines)):
+            nop = re.search(r"s_nop (\d+)", lines[j])
+            ws += int(nop.group(1)) + 1 if nop else 1
+            if "v_mfma" in lines[j]:
+                ws += 3
+                continue  # the next MFMA taking the result whole as srcC: no wait
+            if ws >= MFMA_TO_VALU_WS:
+                break
+            if any(r & dst for r in _vregs(lines[j].split(";")[0])):
+                after += 1
+            if _NOFALL.search(lines[j]):
+                break
+    return before, after
+
+
+def scan_kernel(lines: list[str]) -> tuple[int, int]:
+    vb, va = scan_kernel_vgpr(lines)
+    lines = [ln for ln in lines if ln.strip() and not ln.strip().startswith(";")]
+    before, after = vb, va
     for i, ln in enumerate(lines):
         m = _MFMA.search(ln)
         if not m:

@@ -139,16 +139,43 @@ __device__ __forceinline__ void issue6(const GemmArgs& p, const Ctx& c, int kt, 
   }
 }
 
-// 16 MFMAs of one quadrant (mma_quadrant without the setprio).
+// fp8 (F8 builds): v_mfma_f32_16x16x128_f8f6f4 (e4m3 x e4m3, default unit
+// scales) updating a VGPR accumulator in place. K1-fp8's pingpong8c keeps its
+// accumulators in AGPRs (gemm_bf16.hpp mfma_f8_agpr), which caps its VGPRs at
+// 128 at two waves per SIMD and left no room for the boundary conversion; in
+// VGPRs the fp8 kernel has the bf16 kernel's register shape. hipcc pads nothing
+// inside the asm: the accumulators are written by VALU only at tile boundaries
+// (zero_quadrant, >= 1 barrier before their next MFMA) and read by VALU only
+// after mfma_wait_states.
+__device__ __forceinline__ void mfma_f8_vgpr(f32x4& acc, const i32x8& a, const i32x8& b) {
+  asm("v_mfma_f32_16x16x128_f8f6f4 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b));
+}
+
+// MFMA result -> VALU read of it (the 16-pass f8f6f4 needs passes + 3 = 19).
+__device__ __forceinline__ void mfma_wait_states() {
+  asm volatile("s_nop 15\n\ts_nop 7" ::: "memory");
+}
+
+// 16 MFMAs of one quadrant (mma_quadrant without the setprio); F8: 8 f8f6f4
+// MFMAs over the same LDS image (K1-fp8's order: mt outer, nt inner).
+template <bool F8 = false>
 __device__ __forceinline__ void mma_q(f32x4 (&acc)[4][2], const bf16x8 (&a)[4][2],
                                       const bf16x8 (&b)[2][2]) {
-#pragma unroll
-  for (int ks = 0; ks < 2; ++ks)
+  if constexpr (F8) {
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt)
-        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[nt][ks], a[mt][ks], acc[mt][nt], 0, 0, 0);
+        mfma_f8_vgpr(acc[mt][nt], cat_f8(b[nt][0], b[nt][1]), cat_f8(a[mt][0], a[mt][1]));
+  } else {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt)
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[nt][ks], a[mt][ks], acc[mt][nt], 0, 0, 0);
+  }
 }
 
 // One quadrant of the previous tile (origin m0, n0) to C, in store_tile_wide's
@@ -323,7 +350,7 @@ struct Edge {
 // otherwise); NX: this phase's piece is past the tile (issue6). A stored
 // quadrant is zeroed for the next tile.
 template <int P, bool ODD, int CONV, int VMC, bool NX, int POL, bool LINE, bool STG = false,
-          bool MASK = false, bool TL = false>
+          bool MASK = false, bool TL = false, bool F8 = false>
 __device__ __forceinline__ void phase6(const GemmArgs& p, const Ctx& c, Frags3& f,
                                        f32x4 (&acc)[2][2][4][2], int t, int T, const Edge& e,
                                        bool on, int c_lane, int c_lane2 = 0, int lane = 0,
@@ -348,6 +375,9 @@ __device__ __forceinline__ void phase6(const GemmArgs& p, const Ctx& c, Frags3& 
       wait_vm<VMC>();
     else
       wait_vm<10>();
+  }
+  if constexpr (F8 && CONV >= 0) {
+    if (on) mfma_wait_states();
   }
   if constexpr (CONV >= 10) {  // SPREAD build: boundary phase O = CONV - 10
     if (on) {
@@ -387,16 +417,16 @@ __device__ __forceinline__ void phase6(const GemmArgs& p, const Ctx& c, Frags3& 
     }
   }
   raw_barrier();
-  if constexpr (P == 0) mma_q(acc[0][0], f.a, bcur);
-  if constexpr (P == 1) mma_q(acc[0][1], f.a, both);
-  if constexpr (P == 2) mma_q(acc[1][1], f.a, both);
-  if constexpr (P == 3) mma_q(acc[1][0], f.a, bcur);
+  if constexpr (P == 0) mma_q<F8>(acc[0][0], f.a, bcur);
+  if constexpr (P == 1) mma_q<F8>(acc[0][1], f.a, both);
+  if constexpr (P == 2) mma_q<F8>(acc[1][1], f.a, both);
+  if constexpr (P == 3) mma_q<F8>(acc[1][0], f.a, bcur);
   raw_barrier();
 }
 
 #define NTM_PHT(P, ODD, CV, VMC, NX, ON, TL) \
-  phase6<P, ODD, CV, VMC, NX, POL, LINE, STG, MASK, TL>(p, c, f, acc, t, T, e, ON, c_lane, \
-                                                        c_lane2, lane, lrow, lcol)
+  phase6<P, ODD, CV, VMC, NX, POL, LINE, STG, MASK, TL, F8>(p, c, f, acc, t, T, e, ON, c_lane, \
+                                                            c_lane2, lane, lrow, lcol)
 #define NTM_PH(P, ODD, CV, VMC, NX, ON) NTM_PHT(P, ODD, CV, VMC, NX, ON, false)
 // STAMP 2: shader-clock stamp I of wave 0 at a phase start of the workgroup's
 // first tile boundary (K-tiles T-2 / T-1 of its first tile: I = 0..7, K-tiles
@@ -460,8 +490,10 @@ __device__ __forceinline__ void clock_stamp(unsigned long long& t, unsigned long
 // j-5 .. j-1: P1(T-1) 10, P2 11, P3 13, P0(0) 16, P1 20, P2 23, P3 24,
 // P0(1) 23, P1 20, P2 16, P3 13 (P0(2) needs 11; the loop's 10 over-waits by
 // one store issued 5 phases earlier).
+// F8: OCP e4m3 operands (K / lda / ldb in bf16-sized pairs, as K1-fp8's
+// pingpong8c), f8f6f4 MFMAs on VGPR accumulators (mfma_f8_vgpr).
 template <int POL, bool LINE = false, int STAMP = 0, bool STG = false, bool MASK = false,
-          bool TAIL = false, bool SPREAD = false>
+          bool TAIL = false, bool SPREAD = false, bool F8 = false>
 __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_pp6_kernel(GemmArgs p) {
   static_assert(!SPREAD || (!LINE && !MASK), "SPREAD: default layout, whole tiles");
   static_assert(!STG || LINE, "LDS-staged boundary stores need the whole-line layout");
@@ -645,6 +677,7 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_pp6_kernel(GemmArgs p) 
   }
   if (c.wr == 0) raw_barrier();  // balance the stagger
   wait_vm<0>();                  // dummy pieces: nothing may land after the WG exits
+  if constexpr (F8) mfma_wait_states();  // asm MFMAs: results land before VALU reads
   if (POL != 2 || p.ldc < 0)
     store_tile_lds<false, POL != 0, MASK, POL == 0 ? 0 : 1, LINE>(p, c, acc, e.m0, e.n0, lane);
   if constexpr (STAMP == 1) {
@@ -700,6 +733,30 @@ inline hipError_t launch_gemm_bf16_pp6(const GemmArgs& a, hipStream_t stream) {
   hipLaunchKernelGGL((gemm_bf16_pp6_kernel<POL, LINE, STAMP, STG, false, false, SPREAD>),
                      dim3((unsigned)pp6_grid(ntiles)),
                      dim3(kThreads), 0, stream, a);
+  return hipGetLastError();
+}
+
+// K1-fp8 on the persistent overlap kernel (experimental): whole 256x256 tiles,
+// fp8 K % 256 (bf16-pair K % 128); A / B are e4m3 byte images, K / lda / ldb in
+// fp8 elements here.
+inline hipError_t launch_gemm_fp8_pp6(const void* A, const void* B, __bf16* C, int M, int N,
+                                      int K, int lda, int ldb, int ldc, hipStream_t stream) {
+  GemmArgs a;
+  a.A = (const __bf16*)A;
+  a.B = (const __bf16*)B;
+  a.C = C;
+  a.M = M;
+  a.N = N;
+  a.K = K / 2;
+  a.lda = lda / 2;
+  a.ldb = ldb / 2;
+  a.ldc = ldc;
+  if ((K % 2) || (lda % 16) || (ldb % 16) || !shape_ok6(a.M, a.N, a.K) || a.lda < a.K ||
+      a.ldb < a.K || a.ldc < a.N || (a.ldc % 8))
+    return hipErrorInvalidValue;
+  const int ntiles = (a.M / BM) * (a.N / BN);
+  hipLaunchKernelGGL((gemm_bf16_pp6_kernel<1, false, 0, false, false, false, false, true>),
+                     dim3((unsigned)pp6_grid(ntiles)), dim3(kThreads), 0, stream, a);
   return hipGetLastError();
 }
 

@@ -11,6 +11,7 @@
 
 #include "ntm/gemm_bf16_pp3.hpp"
 #include "ntm/gemm_fp8.hpp"
+#include "ntm/gemm_bf16_pp6.hpp"
 #include "ntm/gemm_w4k.hpp"
 
 namespace ntm {
@@ -52,6 +53,9 @@ inline hipError_t launch_gemm_fp8_knob(const void* A, const void* B, __bf16* C, 
   const dim3 g((unsigned)((M / BM) * (N / BN))), b(kThreads);
   switch (knob) {
     case 0: return launch_gemm_fp8(A, B, C, M, N, K, lda, ldb, ldc, s);
+    // 30: the persistent overlap kernel (pingpong8o) with f8f6f4 MFMAs on VGPR
+    // accumulators (gemm_bf16_pp6.hpp F8)
+    case 30: return ::ntm::gemm6::launch_gemm_fp8_pp6(A, B, C, M, N, K, lda, ldb, ldc, s);
     // 12: the 4-wave one-barrier-per-K-tile kernel, DMA every 2 MFMAs (gemm_w4k.hpp)
     case 12: return ::ntm::w4k::launch_gemm_fp8_w4k<2>(A, B, C, M, N, K, lda, ldb, ldc, s);
     case 1: hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, kGroupM, false, kEpiDefault, 0, 2>), g, b, 0, s, a); break;
