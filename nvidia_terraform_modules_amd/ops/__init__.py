@@ -37,6 +37,7 @@ from .kernels import (  # noqa: F401
     k1_plan,
     k1_splitk_plan,
     ref_gemm_f32,
+    sk_ws_bytes,
     stream_copy,
     stream_read,
     verify_bf16,

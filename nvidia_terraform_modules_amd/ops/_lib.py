@@ -61,6 +61,9 @@ def _declare(lib: ctypes.CDLL) -> None:
         "ntm_gemm_bf16_ex": ([c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp,
                               c_size, c_vp], c_int),
         "ntm_splitk_ws_bytes": ([c_int, c_int, c_int, c_int], c_size),
+        "ntm_sk_ws_bytes": ([c_int, c_int, c_int], c_size),
+        "ntm_gemm_bf16_sk": ([c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp,
+                              c_size, c_vp], c_int),
         "ntm_gemm_bf16_splitk": ([c_int, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int,
                                   c_int, c_int, c_vp, c_size, c_vp], c_int),
         "ntm_fill_uniform_e4m3": ([c_vp, c_size, ctypes.c_ulonglong, c_float, c_vp], c_int),
@@ -101,7 +104,7 @@ def lib() -> ctypes.CDLL:
 
 
 def _declare_experimental(lib: ctypes.CDLL) -> None:
-    c_int, c_vp = ctypes.c_int, ctypes.c_void_p
+    c_int, c_vp, c_size = ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t
     gemm = [c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp]
     sig = {
         "ntm_experimental_version": ([], ctypes.c_char_p),
@@ -114,6 +117,10 @@ def _declare_experimental(lib: ctypes.CDLL) -> None:
         "ntm_mfma_rate": ([c_int, c_int, c_int, c_vp, c_vp, c_vp], c_int),
         "ntm_gemm_fp8_knob": ([c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                                c_vp], c_int),
+        "ntm_gemm_bf16_sk_rev": ([c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int,
+                                  c_vp, c_size, c_vp], c_int),
+        "ntm_gemm_bf16_sk_stamp": ([c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int,
+                                    c_vp, c_size, c_vp, c_vp], c_int),
         "ntm_gemm_bf16_pp6_stamp": ([c_int, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int,
                                      c_int, c_int, c_vp, c_vp], c_int),
     }

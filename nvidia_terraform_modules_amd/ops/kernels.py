@@ -144,6 +144,10 @@ def gemm_bf16(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
                              "(masked tiles: N % 4, K % 8; others: whole tiles, K % 128)")
     elif variant == "default":
         _default_ws_bytes(m, n, k)  # the native plan is the one authority on what it serves
+    elif variant in ("pingpong8s", "pingpong8s_rev"):  # stream-K: > 1 round of 256x256 tiles
+        if not sk_ws_bytes(m, n, k):
+            raise ValueError(f"shape ({m},{n},{k}) not served by stream-K (N % 8, K % 8, K >= 128, "
+                             "more 256x256 tiles than CUs and not a multiple of them)")
     elif variant in ("pingpong8cm", "pingpong8om"):  # 256x256, masked edge tiles (+ K tail)
         if not (m > 0 and n > 0 and n % 8 == 0 and k > 0 and k % 8 == 0):
             raise ValueError(f"shape ({m},{n},{k}) not served by {variant} (N % 8, K % 8)")
@@ -154,6 +158,8 @@ def gemm_bf16(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
     _require(out, "out", torch.bfloat16)
     if tuple(out.shape) != (m, n):
         raise ValueError("out has the wrong shape")
+    if variant in ("pingpong8s", "pingpong8s_rev"):
+        return _gemm_bf16_sk(a, b, out, rev=variant == "pingpong8s_rev")
     if splits > 1:
         if variant not in MASKED_TILES:
             raise ValueError(f"split-K runs on {sorted(MASKED_TILES)}, not {variant}")
@@ -188,6 +194,45 @@ def gemm_bf16(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
         GEMM_VARIANTS[variant], a.data_ptr(), b.data_ptr(), out.data_ptr(), m, n, k,
         a.stride(0), b.stride(0), out.stride(0), stream_handle())
     check(rc, "ntm_gemm_bf16")
+    return out
+
+
+def sk_ws_bytes(m: int, n: int, k: int) -> int:
+    """Workspace of the stream-K build ("pingpong8s") for (M, N, K) on this
+    device; 0 when it does not serve the shape (the 256x256 tile count is at
+    most one round of CUs or a multiple of them)."""
+    if m <= 0 or n <= 0 or k <= 0:
+        return 0
+    return int(lib().ntm_sk_ws_bytes(m, n, k))
+
+
+# (device index, stream handle) -> the stream-K workspace of that stream: its
+# counter block is zeroed once here and every completed launch leaves it zero,
+# so calls on one stream reuse it with no memset dispatch
+_SK_WS: dict[tuple[int, int], torch.Tensor] = {}
+
+
+def _sk_workspace(dev: torch.device, nbytes: int) -> torch.Tensor:
+    key = (dev.index if dev.index is not None else torch.cuda.current_device(),
+           int(stream_handle() or 0))
+    ws = _SK_WS.get(key)
+    if ws is None or ws.numel() * 4 < nbytes:
+        ws = torch.zeros((nbytes + 3) // 4, dtype=torch.float32, device=dev)
+        _SK_WS[key] = ws
+    return ws
+
+
+def _gemm_bf16_sk(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, rev: bool = False) -> torch.Tensor:
+    """Stream-K (gemm_bf16_sk.hpp): fp32 partials of the split tiles and one
+    counter per split in this stream's cached workspace (_sk_workspace)."""
+    m, k = a.shape
+    n = b.shape[0]
+    wsb = sk_ws_bytes(m, n, k)
+    ws = _sk_workspace(a.device, wsb)
+    fn = lib_experimental().ntm_gemm_bf16_sk_rev if rev else lib().ntm_gemm_bf16_sk
+    rc = fn(a.data_ptr(), b.data_ptr(), out.data_ptr(), m, n, k, a.stride(0), b.stride(0),
+            out.stride(0), ws.data_ptr(), wsb, stream_handle())
+    check(rc, "ntm_gemm_bf16_sk")
     return out
 
 

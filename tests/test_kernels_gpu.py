@@ -805,3 +805,66 @@ def test_default_runs_persistent_build_past_one_round(ops):
     out = torch.zeros((m, n + 4), dtype=torch.bfloat16, device="cuda")
     ops.gemm_bf16(a, b, out[:, :n], variant="pingpong8o")
     assert torch.equal(out[:, :n], ref)
+
+
+SK_SHAPES = [(4472, 5688, 5832),   # 414 tiles: stream-K over all of them, K % 128 = 72
+             (4608, 4608, 1024),   # 324 whole tiles
+             (6144, 6144, 2048),   # 576 tiles: 256 whole, then stream-K over 320
+             (4472, 5688, 200),    # two K-tile pairs per tile, the second partial
+             (8192, 2304, 128),    # one pair per tile: nothing to split, balanced tiles only
+             (5000, 4104, 4096),
+             (1000, 17000, 384)]
+
+
+@pytest.mark.parametrize("m,n,k", SK_SHAPES)
+def test_stream_k_vs_torch_fp32(ops, m, n, k):
+    """pingpong8s (round 4, gemm_bf16_sk.hpp): the last two rounds of 256x256
+    tiles dealt out as K-tile pairs per XCD, split tiles fixed up through fp32
+    partials and a counter. vs the fp32 product; rows / columns past C never
+    written; a second launch gives the same bytes (counters were left at 0);
+    the REV build (segments last-first: heads usually reach the fix-up first,
+    the protocol's other branches) is bitwise equal."""
+    a = _rand(ops, (m, k), 651 + k)
+    b = _rand(ops, (n, k), 653 + n)
+    out = torch.full((m, n + 8), 7.0, dtype=torch.bfloat16, device="cuda")
+    c = ops.gemm_bf16(a, b, out[:, :n], variant="pingpong8s")
+    ref = a.float() @ b.float().T
+    atol, rtol = ops.gemm_tolerance(k)
+    err = (c.float() - ref).abs()
+    assert torch.all(err <= atol + rtol * ref.abs()), float(err.max())
+    assert torch.all(out[:, n:] == 7.0)
+    first = c.clone()
+    assert torch.equal(ops.gemm_bf16(a, b, variant="pingpong8s"), first)
+    assert torch.equal(ops.gemm_bf16(a, b, variant="pingpong8s_rev"), first)
+
+
+def test_stream_k_counters_left_zero_and_refusals(ops):
+    """The fix-up counters are zero after a launch (the combiner resets them), so
+    a workspace zeroed once serves every later launch on its stream; partial
+    slots may hold anything. Shapes stream-K does not serve are refused before
+    anything launches."""
+    from nvidia_terraform_modules_amd.ops._lib import lib, stream_handle
+
+    m, n, k = 4472, 5688, 5832
+    a = _rand(ops, (m, k), 661)
+    b = _rand(ops, (n, k), 663)
+    c = torch.empty((m, n), dtype=torch.bfloat16, device="cuda")
+    wsb = ops.sk_ws_bytes(m, n, k)
+    ws = torch.full(((wsb + 3) // 4,), -1.0, dtype=torch.float32, device="cuda")
+    ws[:1024].zero_()  # the counter block: zero on entry (the caller's contract)
+    assert lib().ntm_gemm_bf16_sk(a.data_ptr(), b.data_ptr(), c.data_ptr(), m, n, k, k, k, n,
+                                  ws.data_ptr(), wsb, stream_handle()) == 0
+    torch.cuda.synchronize()
+    assert torch.all(ws[:1024].view(torch.int32) == 0)
+    assert torch.equal(c, ops.gemm_bf16(a, b, variant="pingpong8s"))
+    c2 = torch.empty_like(c)  # the same workspace again, no re-zeroing
+    assert lib().ntm_gemm_bf16_sk(a.data_ptr(), b.data_ptr(), c2.data_ptr(), m, n, k, k, k, n,
+                                  ws.data_ptr(), wsb, stream_handle()) == 0
+    assert torch.equal(c2, c)
+    # too small a workspace, and shapes without a partial second round
+    assert lib().ntm_gemm_bf16_sk(a.data_ptr(), b.data_ptr(), c.data_ptr(), m, n, k, k, k, n,
+                                  ws.data_ptr(), wsb - 4, stream_handle()) != 0
+    assert ops.sk_ws_bytes(8192, 8192, 8192) == 0     # 1024 tiles: whole rounds
+    assert ops.sk_ws_bytes(4096, 4096, 4096) == 0     # 256 tiles: one round
+    with pytest.raises(ValueError):
+        ops.gemm_bf16(a[:, :4096], b[:256, :4096], variant="pingpong8s")

@@ -42,6 +42,10 @@ SHAPES_PERSIST = [(256, 256, 256), (1024, 512, 1024), (4608, 4608, 512), (8192, 
                   (6144, 6144, 2048), (2304, 1792, 768), (8192, 8192, 8192)]
 # ... on ragged C with multi-round tiles and partial K (pingpong8om)
 SHAPES_PERSIST_RAGGED = [(4472, 5688, 5832), (4608, 4360, 456), (5000, 4104, 768), (1000, 4104, 328)]
+# stream-K (pingpong8s / pingpong8s_rev): more 256x256 tiles than CUs, not a
+# multiple of them - one and two rounds, ragged C, partial K, one-pair tiles
+SHAPES_SK = [(4472, 5688, 5832), (4608, 4608, 1024), (6144, 6144, 2048), (4472, 5688, 200),
+             (8192, 2304, 128), (5000, 4104, 4096), (1000, 17000, 384)]
 SHAPES_FP8 = [(256, 256, 256), (256, 512, 512), (512, 768, 768), (2304, 1536, 1280),
               (4096, 4352, 1024), (4096, 4096, 4096), (8192, 8192, 8192)]
 
@@ -74,6 +78,8 @@ def main():
         shapes = SHAPES_FP8 + SHAPES_RAGGED if fp8 else SHAPES_160 if tn == 160 else SHAPES
         if v.startswith("pingpong8o"):
             shapes = SHAPES_PERSIST + (SHAPES_PERSIST_RAGGED if v == "pingpong8om" else [])
+        if v.startswith("pingpong8s"):
+            shapes = SHAPES_SK
         if splits > 1:
             shapes = SHAPES_SPLITK + SHAPES_RAGGED
         elif v in MASKED:

@@ -27,6 +27,7 @@
 #include "ntm/gemm_bf16_pp3.hpp"
 #include "ntm/gemm_bf16_pp3_stamp.hpp"
 #include "ntm/gemm_bf16_pp6.hpp"
+#include "ntm/gemm_bf16_sk.hpp"
 #include "ntm/gemm_w4k.hpp"
 #include "ntm/gemm_bf16_t128.hpp"
 #include "ntm/gemm_fp8_diag.hpp"
@@ -85,6 +86,44 @@ NTM_API int ntm_gemm_bf16_experimental(int variant, const void* A, const void* B
     case 48: return (int)ntm::gemm6::launch_gemm_bf16_pp6<1, false, 0, false, true>(a, S(stream));
     default: return (int)hipErrorInvalidValue;
   }
+}
+
+// Stream-K test build (gemm_bf16_sk.hpp REV): each workgroup runs its segments
+// in range order, so tails usually reach the fix-up before heads; C must be
+// bitwise equal to ntm_gemm_bf16_sk's.
+NTM_API int ntm_gemm_bf16_sk_rev(const void* A, const void* B, void* C, int M, int N, int K,
+                                 int lda, int ldb, int ldc, void* ws, size_t ws_bytes,
+                                 void* stream) {
+  ntm::gemm::GemmArgs a;
+  a.A = (const __bf16*)A;
+  a.B = (const __bf16*)B;
+  a.C = (__bf16*)C;
+  a.M = M;
+  a.N = N;
+  a.K = K;
+  a.lda = lda;
+  a.ldb = ldb;
+  a.ldc = ldc;
+  return (int)ntm::gemmsk::launch_gemm_bf16_sk<true>(a, ntm::gemm6::pp6_grid(1 << 30), ws,
+                                                     ws_bytes, S(stream));
+}
+
+// Stream-K stamp build (gemm_bf16_sk.hpp STAMP): 16 u64 per workgroup.
+NTM_API int ntm_gemm_bf16_sk_stamp(const void* A, const void* B, void* C, int M, int N, int K,
+                                   int lda, int ldb, int ldc, void* ws, size_t ws_bytes,
+                                   void* stamps, void* stream) {
+  ntm::gemm::GemmArgs a;
+  a.A = (const __bf16*)A;
+  a.B = (const __bf16*)B;
+  a.C = (__bf16*)C;
+  a.M = M;
+  a.N = N;
+  a.K = K;
+  a.lda = lda;
+  a.ldb = ldb;
+  a.ldc = ldc;
+  return (int)ntm::gemmsk::launch_gemm_bf16_sk<false, true>(
+      a, ntm::gemm6::pp6_grid(1 << 30), ws, ws_bytes, S(stream), (unsigned long long*)stamps);
 }
 
 // pingpong8o boundary-phase stamps (gemm_bf16_pp6.hpp STAMP 2): grid 128 or 256

@@ -14,6 +14,7 @@
 #include "ntm/gemm_bf16_pp2.hpp"
 #include "ntm/gemm_bf16_pp3.hpp"
 #include "ntm/gemm_bf16_pp6.hpp"
+#include "ntm/gemm_bf16_sk.hpp"
 #include "ntm/gemm_bf16_t128.hpp"
 #include "ntm/gemm_fp8.hpp"
 
@@ -365,6 +366,34 @@ NTM_API int ntm_gemm_bf16_splitk(int variant, int splits, const void* A, const v
     case 26: return (int)launch_gemm_bf16_tile_ws_splitk<4, 8>(a, splits, w, S(stream));
     default: return (int)hipErrorInvalidValue;
   }
+}
+
+// Stream-K on the 256x256 kernel ("pingpong8s", gemm_bf16_sk.hpp): the last two
+// rounds of tiles dealt out as K-tile pairs over every CU, fp32 partials of the
+// split tiles in ws. ntm_sk_ws_bytes = 0: stream-K does not serve (M, N, K) on
+// this device (the tile count is a multiple of the CUs, or at most one round).
+NTM_API size_t ntm_sk_ws_bytes(int M, int N, int K) {
+  ntm::gemmsk::SkArgs s;
+  if (!ntm::gemmsk::shape_ok_sk(M, N, K) ||
+      !ntm::gemmsk::sk_decompose(M, N, K, ntm::gemm6::pp6_grid(1 << 30), s))
+    return 0;
+  return ntm::gemmsk::sk_ws_bytes(s.G);
+}
+
+NTM_API int ntm_gemm_bf16_sk(const void* A, const void* B, void* C, int M, int N, int K, int lda,
+                             int ldb, int ldc, void* ws, size_t ws_bytes, void* stream) {
+  ntm::gemm::GemmArgs a;
+  a.A = (const __bf16*)A;
+  a.B = (const __bf16*)B;
+  a.C = (__bf16*)C;
+  a.M = M;
+  a.N = N;
+  a.K = K;
+  a.lda = lda;
+  a.ldb = ldb;
+  a.ldc = ldc;
+  return (int)ntm::gemmsk::launch_gemm_bf16_sk(a, ntm::gemm6::pp6_grid(1 << 30), ws, ws_bytes,
+                                               S(stream));
 }
 
 // The default dispatch with split-K allowed: ws (ws_bytes) is the caller's
