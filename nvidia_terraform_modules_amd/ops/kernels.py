@@ -38,7 +38,7 @@ GEMM_VARIANTS = {"default": 0, "pingpong8": 1, "pingpong8b": 4,
                  "tile128x160": 24, "tile128x256": 26, "dma4k_d3": 39, "pingpong8o": 25,
                  "pp8o_g128": 41, "pp8o_g128_nostore": 42, "pp8o_nostore": 43,
                  "pingpong8ol": 44, "pp8ol_nostore": 45, "pingpong8ols": 46,
-                 "pingpong8om": 47, "pingpong8od": 48}
+                 "pingpong8om": 47, "pingpong8od": 48, "pingpong8s": 49}
 
 
 # variants built only into libntm_experimental.so (tests / tools): never selected
@@ -102,11 +102,13 @@ _DEFAULT_WS: dict[tuple[int, int, int], int] = {}
 
 
 def _default_ws_bytes(m: int, n: int, k: int) -> int:
+    """Split-K workspace bytes of the default plan; -1 when the plan is stream-K
+    (its workspace is the per-stream cached one, ``_sk_workspace``)."""
     key = (m, n, k)
     wsb = _DEFAULT_WS.get(key)
     if wsb is None:
-        _, _, _, sp = k1_splitk_plan(m, n, k)  # raises if no kernel serves the shape
-        wsb = lib().ntm_splitk_ws_bytes(m, n, k, sp) if sp > 1 else 0
+        _, top, _, sp = k1_splitk_plan(m, n, k)  # raises if no kernel serves the shape
+        wsb = -1 if top == "pingpong8s" else lib().ntm_splitk_ws_bytes(m, n, k, sp) if sp > 1 else 0
         _DEFAULT_WS[key] = wsb
     return wsb
 
@@ -182,6 +184,8 @@ def gemm_bf16(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
             a.stride(0), b.stride(0), out.stride(0), stream_handle())
         check(rc, "ntm_gemm_bf16_experimental")
         return out
+    if variant == "default" and _default_ws_bytes(m, n, k) < 0:
+        return _gemm_bf16_sk(a, b, out)
     if variant == "default" and _default_ws_bytes(m, n, k):
         wsb = _default_ws_bytes(m, n, k)
         ws = torch.empty((wsb + 3) // 4, dtype=torch.float32, device=a.device)

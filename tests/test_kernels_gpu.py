@@ -868,3 +868,18 @@ def test_stream_k_counters_left_zero_and_refusals(ops):
     assert ops.sk_ws_bytes(4096, 4096, 4096) == 0     # 256 tiles: one round
     with pytest.raises(ValueError):
         ops.gemm_bf16(a[:, :4096], b[:256, :4096], variant="pingpong8s")
+
+
+@pytest.mark.parametrize("m,n,k", [(4864, 3608, 5696), (6496, 2752, 5416)])
+def test_default_plan_runs_stream_k(ops, m, n, k):
+    """Where the split-K plan prices stream-K below the unsplit plan (a small
+    partial second round at long K), the default dispatch runs it: same bytes
+    as pingpong8s, within tolerance of the fp32 product."""
+    assert ops.k1_splitk_plan(m, n, k)[1] == "pingpong8s"
+    a = _rand(ops, (m, k), 671)
+    b = _rand(ops, (n, k), 673)
+    c = ops.gemm_bf16(a, b)
+    assert torch.equal(c, ops.gemm_bf16(a, b, variant="pingpong8s"))
+    ref = a.float() @ b.float().T
+    atol, rtol = ops.gemm_tolerance(k)
+    assert torch.all((c.float() - ref).abs() <= atol + rtol * ref.abs())

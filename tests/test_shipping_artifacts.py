@@ -38,9 +38,9 @@ ALLOWED_K1 = {
     "ntm::gemm6::gemm_bf16_pp6_kernel<1, false, 1, false, false, false, false, false>",  # clock stamps
     "ntm::gemm6::gemm_bf16_pp6_kernel<1, false, 0, false, true, false, false, false>",   # pingpong8om
     "ntm::gemm6::gemm_bf16_pp6_kernel<1, false, 0, false, true, true, false, false>",    # + partial K
-    # stream-K over the last two rounds of 256x256 tiles (pingpong8s <TAIL, REV>)
-    "ntm::gemmsk::gemm_bf16_sk_kernel<false, false>",
-    "ntm::gemmsk::gemm_bf16_sk_kernel<true, false>",
+    # stream-K over the last two rounds of 256x256 tiles (pingpong8s <TAIL, REV, STAMP>)
+    "ntm::gemmsk::gemm_bf16_sk_kernel<false, false, false>",
+    "ntm::gemmsk::gemm_bf16_sk_kernel<true, false, false>",
     "ntm::gemm2::gemm_bf16_pp2_kernel<false, 0>",
     "ntm::gemm2::gemm_bf16_pp2_kernel<false, 3>",
     "ntm::gemm2::gemm_bf16_pp2_kernel<true, 0>",

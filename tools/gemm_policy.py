@@ -66,6 +66,8 @@ def main():
         exact_k = k % 128 == 0
         if args.variants:
             for v in args.variants.split(","):
+                if v.startswith("pingpong8s") and not ops.sk_ws_bytes(m, n, k):
+                    continue  # stream-K serves only a partial round past the first
                 fns[v] = lambda v=v: ops.gemm_bf16(a, b, c, variant=v)
         elif not args.only_default:
             if m % 128 == 0 and n % 128 == 0:

@@ -124,6 +124,7 @@ struct K1Plan {
   int top_variant;   // 5 / 4 (the 256x256 kernel) or a kSmallTiles variant
   int rest_variant;  // rows [top_rows, M) on a kSmallTiles variant
   int splits = 1;    // > 1: all of C on top_variant (masked tile), split-K in that many slices
+  bool sk = false;   // all of C on the stream-K kernel (top_variant kStreamKVariant)
   bool feasible() const { return top_rows >= 0; }
 };
 
@@ -139,6 +140,23 @@ constexpr double kRedFixed = 2e-6;
 constexpr double kRedBW = 2e12;
 constexpr double kSplitKMargin = 1.1;
 constexpr int kMaxSplits = 16;
+
+// Stream-K ("pingpong8s", gemm_bf16_sk.hpp; needs the caller's workspace, so
+// only in the split-K plan). Time model, from its stamps (profiles/r4_sk/
+// sk_stamps.log): the K loop runs 5 % slower per K-tile pair than the
+// data-parallel kernel's (two K offsets per XCD instead of one), over
+// ntiles / G tiles per CU, plus ~30 us per workgroup for the fix-ups, the
+// extra C store and the imbalance between 2- and 3-segment workgroups. It is
+// within +-5 % of the measured time on 29 of 30 shapes (profiles/r4_sk/
+// plan_calibration.log). The unsplit plan's model leaves out per-tile fixed
+// costs, so it is optimistic; stream-K is chosen whenever its predicted time is
+// below the unsplit plan's (4 of 41 random shapes: measured +1 to +12 %).
+constexpr int kStreamKVariant = 49;
+// the last split-K plan's predicted unsplit / stream-K seconds (ntm_k1_plan_times)
+static thread_local double g_plan_debug_unsplit_s = 0.0, g_plan_debug_sk_s = 0.0;
+constexpr double kSkLoopFactor = 1.05;
+constexpr double kSkFixed = 30e-6;
+constexpr double kSkMargin = 1.0;
 
 // The plan: C split by rows into a top part and a rest part, each on one tile
 // kernel in its own launch (either part may be empty). The top part runs the
@@ -227,9 +245,24 @@ inline K1Plan plan_k1(int M, int N, int K, bool splitk = false, bool fp8 = false
   if (!splitk || !best.feasible()) return best;
   // Split-K: C too small to fill 256 CUs with a long K (e.g. 280x6352x7568: 80
   // tiles of 160x160 -> 3 slices of 240 tiles, 631 vs 321 TF/s unsplit).
-  const double unsplit = best_cost * 2.0 * 16384.0 * K / kPerCU;  // cost units -> seconds
+  const double unit_s = 2.0 * 16384.0 * K / kPerCU;  // cost units -> seconds
+  const double unsplit = best_cost * unit_s;
   double best_t = unsplit / kSplitKMargin;
   K1Plan split = best;
+  // Stream-K: a partial last round of 256x256 tiles spread over every CU
+  ntm::gemmsk::SkArgs sk;
+  g_plan_debug_unsplit_s = unsplit;
+  g_plan_debug_sk_s = 0.0;
+  if (!fp8 && ntm::gemmsk::shape_ok_sk(M, N, K) && ntm::gemmsk::sk_decompose(M, N, K, (int)kCUs, sk)) {
+    const double rounds_sk = (double)(sk.ntiles - sk.D) / kCUs + sk.D / kCUs;
+    const double t_sk = kSkLoopFactor * rounds_sk * 4.0 * unit_s * (2.0 * sk.Tp * ntm::gemm::BK / K) + kSkFixed;
+    g_plan_debug_sk_s = t_sk;
+    if (t_sk * kSkMargin < unsplit) {
+      split = K1Plan{M, kStreamKVariant, kStreamKVariant, 1};
+      split.sk = true;
+      best_t = t_sk * kSkMargin / kSplitKMargin;  // a split-K plan must beat stream-K too
+    }
+  }
   for (const SmallTile& st : kSmallTiles) {
     if (!st.masked || !st.splitk || !small_ok(st, M)) continue;
     const double tiles = (double)((M + st.tm - 1) / st.tm) * ((N + st.tn - 1) / st.tn);
@@ -247,6 +280,15 @@ inline K1Plan plan_k1(int M, int N, int K, bool splitk = false, bool fp8 = false
     }
   }
   return split;
+}
+
+// The split-K plan's predicted seconds for (M, N, K): the best unsplit plan and
+// stream-K (0 when it does not serve the shape). Host only; tools.
+NTM_API int ntm_k1_plan_times(int M, int N, int K, double* unsplit_s, double* sk_s) {
+  if (!unsplit_s || !sk_s || !plan_k1(M, N, K, true).feasible()) return (int)hipErrorInvalidValue;
+  *unsplit_s = g_plan_debug_unsplit_s;
+  *sk_s = g_plan_debug_sk_s;
+  return 0;
 }
 
 // The default dispatch's plan for (M, N, K) (host only; tests and tools).
@@ -406,6 +448,13 @@ NTM_API int ntm_gemm_bf16_ex(const void* A, const void* B, void* C, int M, int N
     if (pl.feasible() && pl.splits > 1 && ws_bytes >= ntm_splitk_ws_bytes(M, N, K, pl.splits))
       return ntm_gemm_bf16_splitk(pl.top_variant, pl.splits, A, B, C, M, N, K, lda, ldb, ldc, ws,
                                   ws_bytes, stream);
+    // stream-K: this entry takes any caller workspace, so it zeroes the counter
+    // block first (a caller that keeps a zeroed workspace per stream calls
+    // ntm_gemm_bf16_sk directly and saves that dispatch)
+    if (pl.feasible() && pl.sk && ws_bytes >= ntm_sk_ws_bytes(M, N, K) &&
+        hipMemsetAsync(ws, 0, ntm::gemmsk::kCounterBytes, S(stream)) == hipSuccess &&
+        ntm_gemm_bf16_sk(A, B, C, M, N, K, lda, ldb, ldc, ws, ws_bytes, stream) == 0)
+      return 0;
   }
   return ntm_gemm_bf16_variant(0, A, B, C, M, N, K, lda, ldb, ldc, stream);
 }
