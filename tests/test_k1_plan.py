@@ -152,9 +152,11 @@ def fp8_plan():
 
 
 @pytest.mark.parametrize("m,n,k,plan", [
-    (8192, 8192, 8192, (8192, "pingpong8c", "tile128")),   # the Job's fp8 check: 256x256 only
-    (4096, 4096, 4096, (4096, "pingpong8c", "tile128")),
-    (6144, 6144, 6144, (5376, "pingpong8c", "tile160x128")),
+    # whole 256x256 tiles (fp8 K % 256, K >= 512) run the persistent build
+    (8192, 8192, 8192, (8192, "pingpong8o", "tile128")),   # the Job's fp8 check: 256x256 only
+    (4096, 4096, 4096, (4096, "pingpong8o", "tile128")),
+    (6144, 6144, 6144, (5376, "pingpong8o", "tile160x128")),
+    (4096, 4096, 256, (4096, "pingpong8c", "tile128")),    # K below the persistent build's 512
     (2048, 2048, 2048, (2048, "tile128", "tile128")),
     (2560, 2560, 2560, (2560, "tile160", "tile160")),
     (1000, 1000, 1008, (1000, "tile128", "tile128")),
@@ -171,7 +173,7 @@ def test_fp8_plan_uses_only_fp8_builds(fp8_plan, m, n, k):
     """No 4-wave 256x160 tile (no fp8 build) and no split-K in an fp8 plan."""
     top, tv, rv = fp8_plan(m, n, k)
     assert 0 < top <= m
-    assert tv in ("pingpong8c", "pingpong8cm", "tile128", "tile256x128", "tile160",
+    assert tv in ("pingpong8c", "pingpong8o", "pingpong8cm", "tile128", "tile256x128", "tile160",
                   "tile160x128", "tile128x160")
     assert rv != "tile256x160" and tv != "tile256x160"
 

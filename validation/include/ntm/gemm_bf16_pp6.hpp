@@ -739,6 +739,11 @@ inline hipError_t launch_gemm_bf16_pp6(const GemmArgs& a, hipStream_t stream) {
 // K1-fp8 on the persistent overlap kernel (experimental): whole 256x256 tiles,
 // fp8 K % 256 (bf16-pair K % 128); A / B are e4m3 byte images, K / lda / ldb in
 // fp8 elements here.
+inline bool fp8_pp6_ok(int M, int N, int K, int lda, int ldb, int ldc) {
+  return (K % 2) == 0 && (lda % 16) == 0 && (ldb % 16) == 0 && shape_ok6(M, N, K / 2) &&
+         lda >= K && ldb >= K && ldc >= N && (ldc % 8) == 0;
+}
+
 inline hipError_t launch_gemm_fp8_pp6(const void* A, const void* B, __bf16* C, int M, int N,
                                       int K, int lda, int ldb, int ldc, hipStream_t stream) {
   GemmArgs a;

@@ -66,6 +66,19 @@ constexpr int kDefaultVariant = 5;
 constexpr int kPersistentVariant = 25;
 // C layout of the shipping pingpong8o build (gemm_bf16_pp6.hpp LINE)
 constexpr bool kPp6Line = false;
+// Boundary stores of the shipping build spread over the 7 phases the quadrants
+// allow (gemm_bf16_pp6.hpp SPREAD, "pingpong8od"), round 4: median over 3
+// boxes vs hipBLASLt 8192^3 0.998 (plain 0.996), 8192x8192x4096 1.008
+// (0.992), 5120^3 1.022 (1.009), 8192x8192x6144 1.005 (0.998); never below
+// the plain build on any box (profiles/r4_ab/). Bitwise equal; race screen
+// clean (profiles/r4_race/).
+constexpr bool kPp6Spread = true;
+// K1-fp8 runs the persistent overlap kernel with f8f6f4 MFMAs on VGPR
+// accumulators (gemm_bf16_pp6.hpp F8, experimental fp8 knob 30 until round 4)
+// on whole 256x256 tiles, one round or more: +0.8 to +3.0 % over the fp8
+// pingpong8c at 4096^3, 8192^3, 8192x8192x4096, 8192x4096x8192 and
+// 4096x8192x8192 on each of 3 boxes (profiles/r4_fp8/, r4_ab/); bitwise equal.
+constexpr bool kFp8Persistent = true;
 // 47 = pingpong8om, the persistent overlap kernel on ragged C (masked edge
 // tiles, partial K): the plan runs it in place of 22 when the masked 256x256
 // part has more tiles than CUs (round 4, profiles/r4_om/)
@@ -234,8 +247,12 @@ inline K1Plan plan_k1(int M, int N, int K, bool splitk = false, bool fp8 = false
     }
   }
   // whole 256x256 tiles over more than one round: the persistent build
+  // (K1-fp8: from one round on, K in bf16-sized pairs)
   if (!fp8 && best.feasible() && best.top_variant == kDefaultVariant && K >= 256 &&
       (double)(best.top_rows / 256) * (N / 256) > kCUs)
+    best.top_variant = kPersistentVariant;
+  if (fp8 && kFp8Persistent && best.feasible() && best.top_variant == kDefaultVariant &&
+      ntm::gemm6::shape_ok6(best.top_rows, N, K))
     best.top_variant = kPersistentVariant;
   // ... and on ragged C (masked edge tiles; K > 128, K % 8)
   if (kPlanMaskedPersistent && !fp8 && best.feasible() && best.top_variant == 22 &&
@@ -352,7 +369,7 @@ NTM_API int ntm_gemm_bf16_variant(int variant, const void* A, const void* B,
     case 25:
       if (!ntm::gemm6::shape_ok6(M, N, K) || (lda % 8) || (ldb % 8) || (ldc % 8))
         return (int)ntm::gemm3::launch_gemm_bf16_pp3(a, S(stream));
-      return (int)ntm::gemm6::launch_gemm_bf16_pp6<1, kPp6Line>(a, S(stream));
+      return (int)ntm::gemm6::launch_gemm_bf16_pp6<1, kPp6Line, 0, false, kPp6Spread>(a, S(stream));
     // persistent + masked (pingpong8om): ragged C over more than one round of
     // 256x256 tiles (K % 128, K >= 256; otherwise pingpong8cm)
     case 47:
@@ -484,6 +501,12 @@ NTM_API int ntm_gemm_fp8_variant(int variant, const void* A, const void* B, void
   using namespace ntm::gemmt;
   switch (variant) {
     case 5: case 22: return (int)ntm::fp8::launch_gemm_fp8(A, B, c, M, N, K, lda, ldb, ldc, S(stream));
+    // the persistent overlap build (whole 256x256 tiles, K % 256, K >= 512;
+    // otherwise the same tiles on pingpong8c)
+    case 25:
+      if (ntm::gemm6::fp8_pp6_ok(M, N, K, lda, ldb, ldc))
+        return (int)ntm::gemm6::launch_gemm_fp8_pp6(A, B, c, M, N, K, lda, ldb, ldc, S(stream));
+      return (int)ntm::fp8::launch_gemm_fp8(A, B, c, M, N, K, lda, ldb, ldc, S(stream));
     case 15: return (int)launch_gemm_fp8_tile_ws<4, 4>(A, B, c, M, N, K, lda, ldb, ldc, S(stream));
     case 16: return (int)launch_gemm_fp8_tile_ws<8, 4>(A, B, c, M, N, K, lda, ldb, ldc, S(stream));
     case 17: return (int)launch_gemm_fp8_tile_ws<5, 5>(A, B, c, M, N, K, lda, ldb, ldc, S(stream));
@@ -752,7 +775,7 @@ NTM_API int ntm_gemm_bf16_clock(const void* A, const void* B, void* C, int M, in
   a.ldb = ldb;
   a.ldc = ldc;
   a.stamps = (unsigned long long*)stamps;
-  return (int)ntm::gemm6::launch_gemm_bf16_pp6<1, kPp6Line, 1>(a, S(stream));
+  return (int)ntm::gemm6::launch_gemm_bf16_pp6<1, kPp6Line, 1, false, kPp6Spread>(a, S(stream));
 }
 
 NTM_API int ntm_verify_result_bytes() {
