@@ -245,8 +245,8 @@ def gemm_fp8_shape_ok(m: int, n: int, k: int) -> bool:
 
 
 # K1-fp8 variants: the 256x256 kernel and the wave-specialised tiles with the fp8 consumer
-FP8_VARIANTS = ("default", "pingpong8c", "pingpong8cm", "tile128", "tile256x128", "tile160", "tile160x128",
-                "tile128x160", "tile128x256")
+FP8_VARIANTS = ("default", "pingpong8c", "pingpong8o", "pingpong8cm", "tile128", "tile256x128",
+                "tile160", "tile160x128", "tile128x160", "tile128x256")
 
 
 def k1_fp8_plan(m: int, n: int, k: int) -> tuple[int, str, str]:
@@ -296,7 +296,9 @@ def gemm_fp8(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
     the wave-specialised 128x128 / 256x128 / 160x160 / 160x128 / 128x160 tiles
     and row splits where they fill the chip better); "pingpong8c" = the 256x256
     kernel (the bf16 default's schedule and LDS image, twice the MFMA rate per
-    clock); "tile*" = one tile shape. The default splits K over a masked small
+    clock); "pingpong8o" = its persistent build with the C stores of one tile
+    overlapping the next tile's K loop, on VGPR accumulators (whole 256x256
+    tiles, K % 256, K >= 512; the plan's choice there); "tile*" = one tile shape. The default splits K over a masked small
     tile for skinny C with a long K (``k1_fp8_splitk_plan``; fp32 partials in a
     workspace from PyTorch's allocator); ``splits`` > 1 forces that on a "tile*"
     variant. ``knob`` != 0 selects an experimental schedule of the 256x256
