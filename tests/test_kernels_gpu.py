@@ -745,6 +745,10 @@ def test_fp8_persistent_overlap_vs_torch_fp32(ops, m, n, k):
     atol, rtol = ops.gemm_tolerance(k)
     assert ((ck.float() - ref).abs() <= atol + rtol * ref.abs()).all()
     assert torch.equal(ck.view(torch.int16), ops.gemm_fp8(a, b).view(torch.int16))
+    # knob 31 = the spread-store build the plan ships (padded asm-MFMA srcC)
+    assert torch.equal(ops.gemm_fp8(a, b, knob=31).view(torch.int16), ck.view(torch.int16))
+    assert torch.equal(ops.gemm_fp8(a, b, variant="pingpong8c").view(torch.int16),
+                       ck.view(torch.int16))
     if k == 512:  # 4 K-tiles of 128 e4m3 is the build's minimum: shorter K is refused
         with pytest.raises(RuntimeError):
             ops.gemm_fp8(a[:, :256], b[:, :256], knob=30)

@@ -37,7 +37,7 @@ ALLOWED_K1 = {
     # (the shipping bf16 build spreads its boundary stores: SPREAD, "pingpong8od")
     "ntm::gemm6::gemm_bf16_pp6_kernel<1, false, 0, false, false, false, true, false>",
     "ntm::gemm6::gemm_bf16_pp6_kernel<1, false, 1, false, false, false, true, false>",  # clock stamps
-    "ntm::gemm6::gemm_bf16_pp6_kernel<1, false, 0, false, false, false, false, true>",   # K1-fp8
+    "ntm::gemm6::gemm_bf16_pp6_kernel<1, false, 0, false, false, false, true, true>",    # K1-fp8
     "ntm::gemm6::gemm_bf16_pp6_kernel<1, false, 0, false, true, false, false, false>",   # pingpong8om
     "ntm::gemm6::gemm_bf16_pp6_kernel<1, false, 0, false, true, true, false, false>",    # + partial K
     # stream-K over the last two rounds of 256x256 tiles (pingpong8s <TAIL, REV, STAMP>)

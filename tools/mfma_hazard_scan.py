@@ -19,6 +19,8 @@ gemm_bf16_pp6.hpp mfma_f8_vgpr; only asm ones - hipcc pads its own), the same
 two counts over VGPRs: non-MFMA writes of a srcC VGPR within WINDOW
 instructions before, any non-MFMA access of a dst VGPR within MFMA_TO_VALU_WS
 wait states after.
+Windows are counted in wait states (an s_nop N is N + 1, any other
+instruction 1), so a deliberate pad in front of an asm MFMA clears it.
 The scan is linear over the listing and stops at an unconditional branch
 (the next block is then reached from elsewhere). Exit status 1 if a GEMM kernel (not the rate probes, whose values are unused)
 has a hit.
@@ -87,16 +89,17 @@ def scan_kernel_vgpr(lines: list[str]) -> tuple[int, int]:
         if not m or not in_asm[i]:
             continue
         dst, src = _regs(m.group(1), m.group(2)), _regs(m.group(3), m.group(4))
-        for j in range(i - 1, max(-1, i - 1 - WINDOW), -1):
-            if _NOFALL.search(lines[j]):
+        ws = 0  # wait states strictly between line j and the MFMA (s_nop N = N + 1)
+        for j in range(i - 1, -1, -1):
+            if _NOFALL.search(lines[j]) or ws >= WINDOW:
                 break
-            if "v_mfma" in lines[j]:
-                continue
-            ops = _vregs(lines[j].split(";")[0])
-            op = lines[j].split()[0] if lines[j].split() else ""
-            writes = op.startswith("v_") and ops and ops[0] & src
-            if writes:
-                before += 1
+            nop = re.search(r"s_nop (\d+)", lines[j])
+            if "v_mfma" not in lines[j]:
+                ops = _vregs(lines[j].split(";")[0])
+                op = lines[j].split()[0] if lines[j].split() else ""
+                if op.startswith("v_") and ops and ops[0] & src:
+                    before += 1
+            ws += int(nop.group(1)) + 1 if nop else 1
         ws = 0
         for j in range(i + 1, len(lines)):
             nop = re.search(r"s_nop (\d+)", lines[j])
@@ -122,12 +125,15 @@ def scan_kernel(lines: list[str]) -> tuple[int, int]:
         if not m:
             continue
         dst, src = _regs(m.group(1), m.group(2)), _regs(m.group(3), m.group(4))
-        for j in range(i - 1, max(-1, i - 1 - WINDOW), -1):
-            if _NOFALL.search(lines[j]):
-                break  # the code above is not this MFMA's fall-through predecessor
+        ws = 0
+        for j in range(i - 1, -1, -1):
+            if _NOFALL.search(lines[j]) or ws >= WINDOW:
+                break  # above: not this MFMA's fall-through predecessor, or far enough
             w = _AWRITE.search(lines[j])
             if w and int(w.group(1)) in src:
                 before += 1
+            nop = re.search(r"s_nop (\d+)", lines[j])
+            ws += int(nop.group(1)) + 1 if nop else 1
         ws = 0  # wait states since the MFMA issued (s_nop N = N + 1)
         for j in range(i + 1, len(lines)):
             nop = re.search(r"s_nop (\d+)", lines[j])

@@ -417,6 +417,11 @@ __device__ __forceinline__ void phase6(const GemmArgs& p, const Ctx& c, Frags3& 
     }
   }
   raw_barrier();
+  // F8 + SPREAD: a quadrant zeroed in this phase's load segment (its last store
+  // block, boundary phase O >= 3) is srcC of this segment's asm MFMAs, which
+  // hipcc does not pad; hipcc may sink the zeroing to the barrier, so the pad
+  // goes after it (unconditionally: 16 cycles in 4 phases per tile)
+  if constexpr (F8 && CONV >= 13) asm volatile("s_nop 15" ::: "memory");
   if constexpr (P == 0) mma_q<F8>(acc[0][0], f.a, bcur);
   if constexpr (P == 1) mma_q<F8>(acc[0][1], f.a, both);
   if constexpr (P == 2) mma_q<F8>(acc[1][1], f.a, both);
@@ -744,6 +749,7 @@ inline bool fp8_pp6_ok(int M, int N, int K, int lda, int ldb, int ldc) {
          lda >= K && ldb >= K && ldc >= N && (ldc % 8) == 0;
 }
 
+template <bool SPREAD = false>
 inline hipError_t launch_gemm_fp8_pp6(const void* A, const void* B, __bf16* C, int M, int N,
                                       int K, int lda, int ldb, int ldc, hipStream_t stream) {
   GemmArgs a;
@@ -760,7 +766,7 @@ inline hipError_t launch_gemm_fp8_pp6(const void* A, const void* B, __bf16* C, i
       a.ldb < a.K || a.ldc < a.N || (a.ldc % 8))
     return hipErrorInvalidValue;
   const int ntiles = (a.M / BM) * (a.N / BN);
-  hipLaunchKernelGGL((gemm_bf16_pp6_kernel<1, false, 0, false, false, false, false, true>),
+  hipLaunchKernelGGL((gemm_bf16_pp6_kernel<1, false, 0, false, false, false, SPREAD, true>),
                      dim3((unsigned)pp6_grid(ntiles)), dim3(kThreads), 0, stream, a);
   return hipGetLastError();
 }

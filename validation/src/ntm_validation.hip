@@ -78,6 +78,9 @@ constexpr bool kPp6Spread = true;
 // on whole 256x256 tiles, one round or more: +0.8 to +3.0 % over the fp8
 // pingpong8c at 4096^3, 8192^3, 8192x8192x4096, 8192x4096x8192 and
 // 4096x8192x8192 on each of 3 boxes (profiles/r4_fp8/, r4_ab/); bitwise equal.
+// With the spread boundary stores too (kPp6Spread; fp8 knob 31): another +1.3
+// to +2.0 % at 8192^3 and +2.6 to +4.4 % at 8192x8192x4096 over knob 30 on
+// each of 3 boxes (profiles/r4_ab/fp8_spread_*), never below it.
 constexpr bool kFp8Persistent = true;
 // 47 = pingpong8om, the persistent overlap kernel on ragged C (masked edge
 // tiles, partial K): the plan runs it in place of 22 when the masked 256x256
@@ -505,7 +508,8 @@ NTM_API int ntm_gemm_fp8_variant(int variant, const void* A, const void* B, void
     // otherwise the same tiles on pingpong8c)
     case 25:
       if (ntm::gemm6::fp8_pp6_ok(M, N, K, lda, ldb, ldc))
-        return (int)ntm::gemm6::launch_gemm_fp8_pp6(A, B, c, M, N, K, lda, ldb, ldc, S(stream));
+        return (int)ntm::gemm6::launch_gemm_fp8_pp6<kPp6Spread>(A, B, c, M, N, K, lda, ldb, ldc,
+                                                               S(stream));
       return (int)ntm::fp8::launch_gemm_fp8(A, B, c, M, N, K, lda, ldb, ldc, S(stream));
     case 15: return (int)launch_gemm_fp8_tile_ws<4, 4>(A, B, c, M, N, K, lda, ldb, ldc, S(stream));
     case 16: return (int)launch_gemm_fp8_tile_ws<8, 4>(A, B, c, M, N, K, lda, ldb, ldc, S(stream));
