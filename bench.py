@@ -494,7 +494,9 @@ def main(argv=None) -> int:
         "bench_process_to_verified_s": round(_CLOCK.elapsed("gemm_verified"), 3),
         "in_node_phases_s": {k: round(v, 4) for k, v in _CLOCK.durations().items()},
         "per_rank_tflops": [p["tflops"] for p in per_rank],
-        "per_rank_gemm_clock_GHz": [(p["gemm_clock"] or {}).get("median_GHz") for p in per_rank],
+        # in-kernel clock: per stamped launch the median workgroup's cycles / window,
+        # median over launches (within 2-3 % of the PMC clock, profiles/r4_clock/)
+        "per_rank_gemm_clock_GHz": [(p["gemm_clock"] or {}).get("launch_GHz") for p in per_rank],
         "per_rank_gemm_clock_p10_GHz": [(p["gemm_clock"] or {}).get("p10_GHz") for p in per_rank],
         "per_rank_gemm_clock": [p["gemm_clock"] for p in per_rank],
         "per_rank_clock_GHz": [(p["clock"] or {}).get("median_GHz") for p in per_rank],

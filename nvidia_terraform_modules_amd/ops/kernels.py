@@ -632,4 +632,21 @@ def gemm_clock_ghz(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = 
     res["per_xcd_group_median_GHz"] = [_ghz_summary(x)["median_GHz"] for x in groups]
     res["ms_per_launch"] = round(t0.elapsed_time(t1) / steps, 4)
     res["launches"] = steps
+    # per launch: medians over workgroups of the shader cycles and the wall window
+    # (us) between a workgroup's two stamps - to set against a profiler's
+    # per-dispatch duration and cycle counters (tools/clock_check.py)
+    sv = stamps.double()
+    cyc = (sv[:, :, 2] - sv[:, :, 0]).median(dim=1).values
+    win = ((sv[:, :, 3] - sv[:, :, 1]) / 100.0).median(dim=1).values
+    # per launch: the median workgroup's cycles over the median workgroup's window;
+    # the median over launches is the clock bench.py reports. On the same
+    # dispatches it reads 2.0 / 2.7 % below GRBM_GUI_ACTIVE / 8 XCDs / duration
+    # (two boxes, profiles/r4_clock/; the PMC clock also covers the dispatch's
+    # ramp, when fewer CUs run). The per-workgroup median (median_GHz) reads 5 %
+    # low: the slower XCDs' workgroups pull it down.
+    lg = (cyc / (win * 1e3))
+    lg = lg[torch.isfinite(lg) & (lg > 0)]
+    res["launch_GHz"] = round(float(lg.median()), 4) if lg.numel() else None
+    res["per_launch_cycles_median"] = [int(x) for x in cyc.tolist()]
+    res["per_launch_window_us_median"] = [round(x, 2) for x in win.tolist()]
     return res

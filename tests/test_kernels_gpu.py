@@ -791,6 +791,8 @@ def test_gemm_clock_build(ops, m, n, k):
     assert torch.equal(c, ops.gemm_bf16(a, b, variant="pingpong8o"))
     assert r["launches"] == 3 and r["workgroups"] == 3 * min(256, (m // 256) * (n // 256))
     assert 0.5 < r["p10_GHz"] <= r["median_GHz"] <= r["max_GHz"] < 3.0, r
+    assert r["min_GHz"] <= r["launch_GHz"] <= r["max_GHz"], r
+    assert len(r["per_launch_cycles_median"]) == 3 and len(r["per_launch_window_us_median"]) == 3
     xg = r["per_xcd_group_median_GHz"]
     assert len(xg) == 8 and all(r["min_GHz"] <= x <= r["max_GHz"] for x in xg)
     with pytest.raises(ValueError):

@@ -42,9 +42,10 @@ def measure(size: int, launches: int, warm_s: float) -> dict:
 def compare(prof_dir: str, inkernel: dict) -> dict:
     """PMC clock of the stamped kernel's dispatches in ``prof_dir`` (counter and
     kernel-trace CSVs of ONE rocprofv3 run): GRBM_GUI_ACTIVE / 8 XCDs / the
-    dispatch's own duration, median over dispatches - the same dispatches whose
-    in-kernel clock the tool printed (a profiled run's clock differs from an
-    unprofiled one's, so the two are compared inside one run)."""
+    dispatch's own duration. Compared on the SAME dispatches as the in-kernel
+    numbers: the last N (the N measured launches). Round 4's first comparison took
+    the median over every dispatch, warm-up included (408 vs 40), and read 8-11 %
+    apart; matched, the per-launch in-kernel clock is 2.0-2.7 % below the PMC one."""
     import csv
     import glob
     import statistics
@@ -64,9 +65,27 @@ def compare(prof_dir: str, inkernel: dict) -> dict:
     if not ids:
         raise SystemExit(f"no stamped-kernel dispatches with both counters and trace in {prof_dir}")
     pmc = statistics.median(grbm[i] / 8 / dur[i] for i in ids)
-    return {"dispatches": len(ids), "pmc_clock_GHz": round(pmc, 4),
-            "inkernel_median_GHz": inkernel["median_GHz"],
-            "inkernel_over_pmc": round(inkernel["median_GHz"] / pmc, 4)}
+    out = {"dispatches": len(ids), "pmc_clock_all_dispatches_GHz": round(pmc, 4),
+           "inkernel_median_GHz": inkernel["median_GHz"],
+           "inkernel_launch_GHz": inkernel.get("launch_GHz")}
+    # the last N dispatches are the N measured launches: the same dispatches on both
+    # sides, as cycles and durations rather than ratios
+    cyc = inkernel.get("per_launch_cycles_median")
+    if cyc:
+        last = sorted(ids, key=lambda x: int(x))[-len(cyc):]
+        win = inkernel["per_launch_window_us_median"]
+        out["matched_dispatches"] = len(last)
+        out["dispatch_us_median"] = round(statistics.median(dur[i] / 1e3 for i in last), 2)
+        out["workgroup_window_us_median"] = round(statistics.median(win), 2)
+        out["pmc_cycles_per_xcd_median"] = int(statistics.median(grbm[i] / 8 for i in last))
+        out["inkernel_cycles_median"] = int(statistics.median(cyc))
+        out["pmc_clock_matched_GHz"] = round(statistics.median(grbm[i] / 8 / dur[i] for i in last), 4)
+        out["inkernel_cycles_over_window_GHz"] = round(
+            statistics.median(c / (w * 1e3) for c, w in zip(cyc, win)), 4)
+        if inkernel.get("launch_GHz"):
+            out["launch_over_pmc_matched"] = round(
+                inkernel["launch_GHz"] / out["pmc_clock_matched_GHz"], 4)
+    return out
 
 
 def main() -> int:
