@@ -110,24 +110,13 @@ __device__ __forceinline__ const __bf16* src_clamped(const GemmArgs& p, int m0, 
 
 // TL (partial-K builds, only where a piece can reach past K): a 16-B chunk
 // starting at k >= K loads zeros (as pingpong8cm's TAIL build).
-// ALT (whole tiles only): the current tile walks K in direction dir (+1: K-tile
-// 0 first, c.src at K-tile 0; -1: K-tile T-1 first, c.src at K-tile T-1) and the
-// next tile walks it the other way, so its first K-tiles are the ones this XCD
-// just read for the panel both tiles share.
-template <int H, bool NX, bool MASK = false, bool TL = false, bool ALT = false>
+template <int H, bool NX, bool MASK = false, bool TL = false>
 __device__ __forceinline__ void issue6(const GemmArgs& p, const Ctx& c, int kt, int buf, int T,
                                        bool has_next, long dA, long dB, int nm0, int nn0,
-                                       int lane, int dir = 1) {
+                                       int lane) {
   const __bf16* s;
   int off = buf * kTileBytes + H * kHalfBytes;
-  if constexpr (ALT && !NX) {
-    s = c.src[H] + (long)kt * BK * dir;
-  } else if constexpr (ALT) {
-    const long d = (H == kALo || H == kAHi) ? dA : dB;
-    const long last = (long)dir * (T - 1) * BK;  // this tile's last K-tile in its order
-    s = c.src[H] + (has_next ? d + last - (long)dir * (kt - T) * BK : last);
-    off = has_next ? off : kScratch;
-  } else if constexpr (!NX) {
+  if constexpr (!NX) {
     s = c.src[H] + (size_t)kt * BK;
   } else if constexpr (MASK) {
     s = has_next ? src_clamped<H>(p, nm0, nn0, c.w, opaque_lane()) + (long)(kt - T) * BK
@@ -351,7 +340,6 @@ struct Edge {
   long dA, dB;    // next tile's element offsets from this one
   int nm0, nn0;   // next tile's origin (masked build: its sources are clamped per tile)
   int m0, n0;     // this tile's origin
-  int dir;        // ALT: this tile's K direction (+1 / -1)
 };
 
 // One phase. CONV: quadrant stored in this phase's load segment when ON (-1
@@ -362,7 +350,7 @@ struct Edge {
 // otherwise); NX: this phase's piece is past the tile (issue6). A stored
 // quadrant is zeroed for the next tile.
 template <int P, bool ODD, int CONV, int VMC, bool NX, int POL, bool LINE, bool STG = false,
-          bool MASK = false, bool TL = false, bool F8 = false, bool ALT = false>
+          bool MASK = false, bool TL = false, bool F8 = false>
 __device__ __forceinline__ void phase6(const GemmArgs& p, const Ctx& c, Frags3& f,
                                        f32x4 (&acc)[2][2][4][2], int t, int T, const Edge& e,
                                        bool on, int c_lane, int c_lane2 = 0, int lane = 0,
@@ -374,10 +362,10 @@ __device__ __forceinline__ void phase6(const GemmArgs& p, const Ctx& c, Frags3& 
   if constexpr (P == 1) read_b<kBHi>(c, both, cur);
   if constexpr (P == 2) read_a<kAHi>(c, f.a, cur);
   if constexpr (P == 3) read_b<kBLo>(c, both, cur ^ 1);  // K-tile t+1 (next tile's 0 at t = T-1)
-  if constexpr (P == 0) issue6<kAHi, NX, MASK, TL, ALT>(p, c, t + 1, cur ^ 1, T, e.has_next, e.dA, e.dB, e.nm0, e.nn0, lane, e.dir);
-  if constexpr (P == 1) issue6<kBLo, NX, MASK, TL, ALT>(p, c, t + 2, cur, T, e.has_next, e.dA, e.dB, e.nm0, e.nn0, lane, e.dir);
-  if constexpr (P == 2) issue6<kALo, NX, MASK, TL, ALT>(p, c, t + 2, cur, T, e.has_next, e.dA, e.dB, e.nm0, e.nn0, lane, e.dir);
-  if constexpr (P == 3) issue6<kBHi, NX, MASK, TL, ALT>(p, c, t + 2, cur, T, e.has_next, e.dA, e.dB, e.nm0, e.nn0, lane, e.dir);
+  if constexpr (P == 0) issue6<kAHi, NX, MASK, TL>(p, c, t + 1, cur ^ 1, T, e.has_next, e.dA, e.dB, e.nm0, e.nn0, lane);
+  if constexpr (P == 1) issue6<kBLo, NX, MASK, TL>(p, c, t + 2, cur, T, e.has_next, e.dA, e.dB, e.nm0, e.nn0, lane);
+  if constexpr (P == 2) issue6<kALo, NX, MASK, TL>(p, c, t + 2, cur, T, e.has_next, e.dA, e.dB, e.nm0, e.nn0, lane);
+  if constexpr (P == 3) issue6<kBHi, NX, MASK, TL>(p, c, t + 2, cur, T, e.has_next, e.dA, e.dB, e.nm0, e.nn0, lane);
   // POL 2 (C not stored): no stores in the stream, so the pieces-only count
   // (round 3's ablation kept the store-counting waits, which then under-waited)
   if constexpr (VMC == 10 || POL == 2) {
@@ -442,7 +430,7 @@ __device__ __forceinline__ void phase6(const GemmArgs& p, const Ctx& c, Frags3& 
 }
 
 #define NTM_PHT(P, ODD, CV, VMC, NX, ON, TL) \
-  phase6<P, ODD, CV, VMC, NX, POL, LINE, STG, MASK, TL, F8, ALT>(p, c, f, acc, t, T, e, ON, c_lane, \
+  phase6<P, ODD, CV, VMC, NX, POL, LINE, STG, MASK, TL, F8>(p, c, f, acc, t, T, e, ON, c_lane, \
                                                             c_lane2, lane, lrow, lcol)
 #define NTM_PH(P, ODD, CV, VMC, NX, ON) NTM_PHT(P, ODD, CV, VMC, NX, ON, false)
 // STAMP 2: shader-clock stamp I of wave 0 at a phase start of the workgroup's
@@ -510,10 +498,9 @@ __device__ __forceinline__ void clock_stamp(unsigned long long& t, unsigned long
 // F8: OCP e4m3 operands (K / lda / ldb in bf16-sized pairs, as K1-fp8's
 // pingpong8c), f8f6f4 MFMAs on VGPR accumulators (mfma_f8_vgpr).
 template <int POL, bool LINE = false, int STAMP = 0, bool STG = false, bool MASK = false,
-          bool TAIL = false, bool SPREAD = false, bool F8 = false, bool ALT = false>
+          bool TAIL = false, bool SPREAD = false, bool F8 = false>
 __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_pp6_kernel(GemmArgs p) {
   static_assert(!SPREAD || (!LINE && !MASK), "SPREAD: default layout, whole tiles");
-  static_assert(!ALT || (!MASK && !LINE), "ALT: whole tiles, default layout");
   static_assert(!STG || LINE, "LDS-staged boundary stores need the whole-line layout");
   static_assert(!MASK || (!LINE && !STG), "the masked build uses the default C layout");
   static_assert(!TAIL || MASK, "partial K rides on the masked build");
@@ -568,7 +555,6 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_pp6_kernel(GemmArgs p) 
   const int T = TAIL ? ((p.K + 2 * BK - 1) / (2 * BK)) * 2 : p.K / BK;
   if constexpr (TAIL) c.K = p.K;
   e.prev = false;
-  e.dir = 1;
   e.pm0 = e.pn0 = 0;
   int nm0 = 0, nn0 = 0;
   e.has_next = tile + G < ntiles;
@@ -676,10 +662,8 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_pp6_kernel(GemmArgs p) 
       c.src[kBLo] = src_clamped<kBLo>(p, nm0, nn0, c.w, l);
       c.src[kBHi] = src_clamped<kBHi>(p, nm0, nn0, c.w, l);
     } else {
-      const long turn = ALT ? (long)e.dir * (T - 1) * BK : 0;  // to the next tile's first K-tile
 #pragma unroll
-      for (int h = 0; h < 4; ++h) c.src[h] += ((h == kALo || h == kAHi) ? e.dA : e.dB) + turn;
-      if constexpr (ALT) e.dir = -e.dir;
+      for (int h = 0; h < 4; ++h) c.src[h] += (h == kALo || h == kAHi) ? e.dA : e.dB;
     }
     e.pm0 = e.m0;
     e.pn0 = e.n0;
@@ -745,14 +729,13 @@ inline hipError_t launch_gemm_bf16_pp6_grid(const GemmArgs& a, int grid, hipStre
   return hipGetLastError();
 }
 
-template <int POL, bool LINE = false, int STAMP = 0, bool STG = false, bool SPREAD = false,
-          bool ALT = false>
+template <int POL, bool LINE = false, int STAMP = 0, bool STG = false, bool SPREAD = false>
 inline hipError_t launch_gemm_bf16_pp6(const GemmArgs& a, hipStream_t stream) {
   if (!shape_ok6(a.M, a.N, a.K) || a.rowsum || a.lda < a.K || a.ldb < a.K || a.ldc < a.N ||
       (a.lda % 8) || (a.ldb % 8) || (a.ldc % 8) || (STAMP != 0 && a.stamps == nullptr))
     return hipErrorInvalidValue;
   const int ntiles = (a.M / BM) * (a.N / BN);
-  hipLaunchKernelGGL((gemm_bf16_pp6_kernel<POL, LINE, STAMP, STG, false, false, SPREAD, false, ALT>),
+  hipLaunchKernelGGL((gemm_bf16_pp6_kernel<POL, LINE, STAMP, STG, false, false, SPREAD>),
                      dim3((unsigned)pp6_grid(ntiles)),
                      dim3(kThreads), 0, stream, a);
   return hipGetLastError();
@@ -766,7 +749,7 @@ inline bool fp8_pp6_ok(int M, int N, int K, int lda, int ldb, int ldc) {
          lda >= K && ldb >= K && ldc >= N && (ldc % 8) == 0;
 }
 
-template <bool SPREAD = false, bool ALT = false>
+template <bool SPREAD = false>
 inline hipError_t launch_gemm_fp8_pp6(const void* A, const void* B, __bf16* C, int M, int N,
                                       int K, int lda, int ldb, int ldc, hipStream_t stream) {
   GemmArgs a;
@@ -783,7 +766,7 @@ inline hipError_t launch_gemm_fp8_pp6(const void* A, const void* B, __bf16* C, i
       a.ldb < a.K || a.ldc < a.N || (a.ldc % 8))
     return hipErrorInvalidValue;
   const int ntiles = (a.M / BM) * (a.N / BN);
-  hipLaunchKernelGGL((gemm_bf16_pp6_kernel<1, false, 0, false, false, false, SPREAD, true, ALT>),
+  hipLaunchKernelGGL((gemm_bf16_pp6_kernel<1, false, 0, false, false, false, SPREAD, true>),
                      dim3((unsigned)pp6_grid(ntiles)), dim3(kThreads), 0, stream, a);
   return hipGetLastError();
 }

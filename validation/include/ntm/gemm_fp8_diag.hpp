@@ -59,8 +59,6 @@ inline hipError_t launch_gemm_fp8_knob(const void* A, const void* B, __bf16* C, 
     // 31: the same with the boundary stores spread over 7 phases (SPREAD, as the
     // shipping bf16 build)
     case 31: return ::ntm::gemm6::launch_gemm_fp8_pp6<true>(A, B, C, M, N, K, lda, ldb, ldc, s);
-    // 32: 31 with the K direction alternating per tile (ALT)
-    case 32: return ::ntm::gemm6::launch_gemm_fp8_pp6<true, true>(A, B, C, M, N, K, lda, ldb, ldc, s);
     // 12: the 4-wave one-barrier-per-K-tile kernel, DMA every 2 MFMAs (gemm_w4k.hpp)
     case 12: return ::ntm::w4k::launch_gemm_fp8_w4k<2>(A, B, C, M, N, K, lda, ldb, ldc, s);
     case 1: hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, kGroupM, false, kEpiDefault, 0, 2>), g, b, 0, s, a); break;
