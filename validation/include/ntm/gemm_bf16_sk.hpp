@@ -61,7 +61,6 @@ using ::ntm::gemm3::kEpiDefault;
 using ::ntm::gemm3::kLdsBytes3;
 using ::ntm::gemm3::tile3;
 
-constexpr int kAcc4 = 32;                               // f32x4 accumulators per lane
 constexpr size_t kPartialBytes = (size_t)BM * BN * 4;  // one fp32 256x256 partial
 constexpr size_t kCounterBytes = 4096;                 // counter block at the workspace start
 
@@ -78,7 +77,9 @@ struct SkArgs {
 // Tiles, pairs and the whole-tile prefix for (M, N, K) on `cus` CUs. Stream-K
 // needs more tiles than CUs and a CU count that is a multiple of 8.
 __host__ __device__ inline bool sk_decompose(int M, int N, int K, int cus, SkArgs& s) {
-  if (M <= 0 || N <= 0 || K <= 0 || cus < 8 || (cus % 8) != 0) return false;
+  // one 4-byte counter per workgroup slot in the kCounterBytes block
+  if (M <= 0 || N <= 0 || K <= 0 || cus < 8 || (cus % 8) != 0 || cus > (int)(kCounterBytes / 4))
+    return false;
   s.ntiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   s.G = cus;
   if (s.ntiles <= s.G || (s.ntiles % s.G) == 0) return false;
