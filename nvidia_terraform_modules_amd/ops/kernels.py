@@ -38,7 +38,8 @@ GEMM_VARIANTS = {"default": 0, "pingpong8": 1, "pingpong8b": 4,
                  "tile128x160": 24, "tile128x256": 26, "dma4k_d3": 39, "pingpong8o": 25,
                  "pp8o_g128": 41, "pp8o_g128_nostore": 42, "pp8o_nostore": 43,
                  "pingpong8ol": 44, "pp8ol_nostore": 45, "pingpong8ols": 46,
-                 "pingpong8om": 47, "pingpong8od": 48, "pingpong8s": 49}
+                 "pingpong8om": 47, "pingpong8od": 48, "pingpong8s": 49,
+                 "pingpong8omd": 51}
 
 
 # variants built only into libntm_experimental.so (tests / tools): never selected
@@ -48,7 +49,7 @@ EXPERIMENTAL_VARIANTS = frozenset({"pingpong8", "pingpong8cw",
                                    "tile128w4", "tile256x128w4", "tile160w4", "dma4k_d3",
                                    "pp8o_g128", "pp8o_g128_nostore", "pp8o_nostore",
                                    "pingpong8ol", "pp8ol_nostore", "pingpong8ols",
-                                   "pingpong8od"})
+                                   "pingpong8od", "pingpong8omd"})
 
 # (TM, TN) of the 4-wave tile kernels (gemm_bf16_t128.hpp)
 TILE_SHAPES = {"tile128": (128, 128), "tile256x128": (256, 128), "tile160": (160, 160),
@@ -150,7 +151,7 @@ def gemm_bf16(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
         if not sk_ws_bytes(m, n, k):
             raise ValueError(f"shape ({m},{n},{k}) not served by stream-K (N % 8, K % 8, K >= 128, "
                              "more 256x256 tiles than CUs and not a multiple of them)")
-    elif variant in ("pingpong8cm", "pingpong8om"):  # 256x256, masked edge tiles (+ K tail)
+    elif variant in ("pingpong8cm", "pingpong8om", "pingpong8omd"):  # 256x256, masked edges (+ K tail)
         if not (m > 0 and n > 0 and n % 8 == 0 and k > 0 and k % 8 == 0):
             raise ValueError(f"shape ({m},{n},{k}) not served by {variant} (N % 8, K % 8)")
     elif not gemm_shape_ok(m, n, k):

@@ -71,3 +71,18 @@ def test_vgpr_accumulator_asm_mfma_hazards():
     assert scan.scan_kernel(asm + asm) == (0, 0)
     # a compiler-emitted (builtin) MFMA of the same form is not scanned
     assert scan.scan_kernel(["v_mov_b32_e32 v201, 0", VMFMA]) == (0, 0)
+
+
+def test_windows_count_wait_states():
+    """Windows are wait states, not lines: an s_nop N pad (N + 1 states) between
+    a write of srcC and the asm MFMA clears it - the form the spread fp8 build
+    uses after its barrier - while the same writes with only 3 instructions
+    between are reported."""
+    asm = [";;#ASMSTART", VMFMA, ";;#ASMEND"]
+    near = ["v_mov_b32_e32 v201, v178", ".LBB0_18:", "s_barrier", "s_waitcnt lgkmcnt(0)"]
+    assert scan.scan_kernel(near + asm) == (1, 0)
+    padded = ["v_mov_b32_e32 v201, v178", ".LBB0_18:", "s_barrier", "s_nop 15",
+              "s_waitcnt lgkmcnt(0)"]
+    assert scan.scan_kernel(padded + asm) == (0, 0)
+    # AGPR accumulators the same way
+    assert scan.scan_kernel(["v_accvgpr_write_b32 a196, v212", "s_nop 15", MFMA]) == (0, 0)

@@ -33,7 +33,7 @@ SHAPES_160 = [(160, 160, 128), (1280, 800, 384), (2560, 1600, 640), (2560, 2560,
 SHAPES_RAGGED = [(1000, 1000, 1024), (1696, 2560, 640), (333, 1004, 384), (2400, 3200, 512),
                  (1000, 1000, 1000), (333, 1004, 200)]  # the last two: partial K-tiles
 MASKED = ("tile128", "tile256x128", "tile160", "tile160x128", "tile128x160", "tile128x256", "pingpong8cm",
-          "pingpong8om", "default")
+          "pingpong8om", "pingpong8omd", "default")
 # skinny C with a long K: the default dispatch splits K here (k1_splitk_plan)
 SHAPES_SPLITK = [(280, 6352, 7568), (128, 8192, 8192), (333, 1004, 2056), (256, 2048, 8200)]
 # persistent overlap kernel (pingpong8o*, K >= 256): 1-4 tiles per workgroup,
@@ -77,7 +77,7 @@ def main():
         tm, tn = ops.kernels.TILE_SHAPES.get(v, (0, 0))
         shapes = SHAPES_FP8 + SHAPES_RAGGED if fp8 else SHAPES_160 if tn == 160 else SHAPES
         if v.startswith("pingpong8o"):
-            shapes = SHAPES_PERSIST + (SHAPES_PERSIST_RAGGED if v == "pingpong8om" else [])
+            shapes = SHAPES_PERSIST + (SHAPES_PERSIST_RAGGED if v in ("pingpong8om", "pingpong8omd") else [])
         if v.startswith("pingpong8s"):
             shapes = SHAPES_SK
         if splits > 1:
@@ -89,7 +89,7 @@ def main():
                 continue
             if tm and m % tm and v not in MASKED:
                 continue
-            if v in ("pingpong8cm", "pingpong8om") and n % 8:
+            if v in ("pingpong8cm", "pingpong8om", "pingpong8omd") and n % 8:
                 continue
             a = ops.fill_uniform_(torch.empty((m, k), dtype=dt, device=dev), 5 + m)
             b = ops.fill_uniform_(torch.empty((n, k), dtype=dt, device=dev), 6 + n)

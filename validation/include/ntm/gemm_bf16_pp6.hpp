@@ -178,6 +178,20 @@ __device__ __forceinline__ void mma_q(f32x4 (&acc)[4][2], const bf16x8 (&a)[4][2
   }
 }
 
+// Masked 16-B C store that is always issued: a lane outside C gets an offset
+// past the buffer's range, which the buffer store's range check drops. A
+// branch around the store (hipcc's s_cbranch_execz when a whole wave is
+// outside C, at ragged edges) would issue fewer stores than the counted vmcnt
+// waits assume, and they would then release before their LDS-DMA pieces land.
+// blk = the 16-row block's origin (wave-uniform), off = the lane's element offset.
+template <int POL>
+__device__ __forceinline__ void store_c16_masked(const __bf16* blk, int off, bool ok,
+                                                 const unsigned __attribute__((ext_vector_type(4))) & v) {
+  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<__bf16*>(blk), 0, 0x7FFFFFFF,
+                                                      0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, ok ? off * 2 : (int)0x80000000, 0, POL == 1 ? 2 : 0);
+}
+
 // One quadrant of the previous tile (origin m0, n0) to C, in store_tile_wide's
 // layout: after a permlane16 swap per dword pair every lane holds 8 consecutive
 // columns. c_lane = the lane's element offset inside the tile (one VGPR).
@@ -205,17 +219,19 @@ __device__ __forceinline__ void store_quadrant(const GemmArgs& p, const f32x4 (&
       const int l = opaque_lane();
       const int lr = lrow + (l & 15);                              // lrow = 64 wr
       const int lc = lcol + ((l >> 4) & 1) * 16 + (l >> 5) * 8;    // lcol = 32 wc
-      if (m0 + MH * 128 + mt * 16 + lr >= p.M || n0 + NH * (LINE ? 32 : 128) + lc >= p.N)
-        continue;
+      const bool ok = m0 + MH * 128 + mt * 16 + lr < p.M && n0 + NH * (LINE ? 32 : 128) + lc < p.N;
+      store_c16_masked<POL>(tile, c_lane, ok, u32x4{w0[0], w0[1], w1[0], w1[1]});
+      continue;
     }
     store_c16<POL>(tile + c_lane, u32x4{w0[0], w0[1], w1[0], w1[1]});
   }
 }
 
-// One 16-row block (mt) of a quadrant: the SPREAD build's unit of store.
-template <int MH, int NH, int MT, int POL>
+// One 16-row block (mt) of a quadrant: the SPREAD build's unit of store
+// (MASK: rows < M and 8-column chunks < N only, as store_quadrant).
+template <int MH, int NH, int MT, int POL, bool MASK = false>
 __device__ __forceinline__ void store_block(const GemmArgs& p, const f32x4 (&q)[4][2], int m0,
-                                            int n0, int c_lane) {
+                                            int n0, int c_lane, int lrow = 0, int lcol = 0) {
   typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
   const f32x4 v0 = q[MT][0], v1 = q[MT][1];
   unsigned w0[2], w1[2];
@@ -228,7 +244,15 @@ __device__ __forceinline__ void store_block(const GemmArgs& p, const f32x4 (&q)[
     w1[h] = r[1];
   }
   __bf16* tile = p.C + (size_t)(m0 + MH * 128 + MT * 16) * p.ldc + (n0 + NH * 128);
-  store_c16<POL>(tile + c_lane, u32x4{w0[0], w0[1], w1[0], w1[1]});
+  if constexpr (MASK) {
+    const int l = opaque_lane();
+    const int lr = lrow + (l & 15);
+    const int lc = lcol + ((l >> 4) & 1) * 16 + (l >> 5) * 8;
+    const bool ok = m0 + MH * 128 + MT * 16 + lr < p.M && n0 + NH * 128 + lc < p.N;
+    store_c16_masked<POL>(tile, c_lane, ok, u32x4{w0[0], w0[1], w1[0], w1[1]});
+  } else {
+    store_c16<POL>(tile + c_lane, u32x4{w0[0], w0[1], w1[0], w1[1]});
+  }
 }
 
 __device__ __forceinline__ void zero_quadrant(f32x4 (&q)[4][2]);
@@ -237,14 +261,16 @@ __device__ __forceinline__ void zero_quadrant(f32x4 (&q)[4][2]);
 // of the next tile's K-tile 0) for quadrant Q (finishing order q0..q3): block
 // mt = O - Q, zeroing the quadrant after its last block. q0..q2's blocks in
 // O <= 2 belong to this tile, everything from O = 3 on to the previous one.
-template <int O, int Q, int POL>
+template <int O, int Q, int POL, bool MASK = false>
 __device__ __forceinline__ void spread_unit(const GemmArgs& p, f32x4 (&acc)[2][2][4][2],
-                                            int m0, int n0, int pm0, int pn0, int c_lane) {
+                                            int m0, int n0, int pm0, int pn0, int c_lane,
+                                            int lrow = 0, int lcol = 0) {
   constexpr int MT = O - Q;
   if constexpr (MT >= 0 && MT <= 3) {
     constexpr int MH = (Q == 2 || Q == 3) ? 1 : 0;
     constexpr int NH = (Q == 1 || Q == 2) ? 1 : 0;
-    store_block<MH, NH, MT, POL>(p, acc[MH][NH], O >= 3 ? pm0 : m0, O >= 3 ? pn0 : n0, c_lane);
+    store_block<MH, NH, MT, POL, MASK>(p, acc[MH][NH], O >= 3 ? pm0 : m0, O >= 3 ? pn0 : n0,
+                                       c_lane, lrow, lcol);
     if constexpr (MT == 3) zero_quadrant(acc[MH][NH]);
   }
 }
@@ -382,10 +408,10 @@ __device__ __forceinline__ void phase6(const GemmArgs& p, const Ctx& c, Frags3& 
   if constexpr (CONV >= 10) {  // SPREAD build: boundary phase O = CONV - 10
     if (on) {
       constexpr int O = CONV - 10;
-      spread_unit<O, 0, POL>(p, acc, e.m0, e.n0, e.pm0, e.pn0, c_lane);
-      spread_unit<O, 1, POL>(p, acc, e.m0, e.n0, e.pm0, e.pn0, c_lane);
-      spread_unit<O, 2, POL>(p, acc, e.m0, e.n0, e.pm0, e.pn0, c_lane);
-      spread_unit<O, 3, POL>(p, acc, e.m0, e.n0, e.pm0, e.pn0, c_lane);
+      spread_unit<O, 0, POL, MASK>(p, acc, e.m0, e.n0, e.pm0, e.pn0, c_lane, lrow, lcol);
+      spread_unit<O, 1, POL, MASK>(p, acc, e.m0, e.n0, e.pm0, e.pn0, c_lane, lrow, lcol);
+      spread_unit<O, 2, POL, MASK>(p, acc, e.m0, e.n0, e.pm0, e.pn0, c_lane, lrow, lcol);
+      spread_unit<O, 3, POL, MASK>(p, acc, e.m0, e.n0, e.pm0, e.pn0, c_lane, lrow, lcol);
     }
   } else if constexpr (CONV >= 4) {
     if (on) {
@@ -500,7 +526,7 @@ __device__ __forceinline__ void clock_stamp(unsigned long long& t, unsigned long
 template <int POL, bool LINE = false, int STAMP = 0, bool STG = false, bool MASK = false,
           bool TAIL = false, bool SPREAD = false, bool F8 = false>
 __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_pp6_kernel(GemmArgs p) {
-  static_assert(!SPREAD || (!LINE && !MASK), "SPREAD: default layout, whole tiles");
+  static_assert(!SPREAD || !LINE, "SPREAD: default layout");
   static_assert(!STG || LINE, "LDS-staged boundary stores need the whole-line layout");
   static_assert(!MASK || (!LINE && !STG), "the masked build uses the default C layout");
   static_assert(!TAIL || MASK, "partial K rides on the masked build");
@@ -773,7 +799,7 @@ inline hipError_t launch_gemm_fp8_pp6(const void* A, const void* B, __bf16* C, i
 
 // pingpong8om: ragged C (any M, N % 8), K % 8 and K > 128 (K % 128 != 0 on
 // the partial-K build).
-template <int POL>
+template <int POL, bool SPREAD = false>
 inline hipError_t launch_gemm_bf16_pp6_masked(const GemmArgs& a, hipStream_t stream) {
   if (!shape_ok6m(a.M, a.N, a.K) || a.rowsum || a.lda < a.K || a.ldb < a.K || a.ldc < a.N ||
       (a.lda % 8) || (a.ldb % 8) || (a.ldc % 8))
@@ -781,9 +807,9 @@ inline hipError_t launch_gemm_bf16_pp6_masked(const GemmArgs& a, hipStream_t str
   const int ntiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
   const dim3 g((unsigned)pp6_grid(ntiles)), b(kThreads);
   if (a.K % (2 * BK))
-    hipLaunchKernelGGL((gemm_bf16_pp6_kernel<POL, false, 0, false, true, true>), g, b, 0, stream, a);
+    hipLaunchKernelGGL((gemm_bf16_pp6_kernel<POL, false, 0, false, true, true, SPREAD>), g, b, 0, stream, a);
   else
-    hipLaunchKernelGGL((gemm_bf16_pp6_kernel<POL, false, 0, false, true>), g, b, 0, stream, a);
+    hipLaunchKernelGGL((gemm_bf16_pp6_kernel<POL, false, 0, false, true, false, SPREAD>), g, b, 0, stream, a);
   return hipGetLastError();
 }
 

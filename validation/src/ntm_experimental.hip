@@ -84,6 +84,8 @@ NTM_API int ntm_gemm_bf16_experimental(int variant, const void* A, const void* B
     case 46: return (int)ntm::gemm6::launch_gemm_bf16_pp6<1, true, 0, true>(a, S(stream));
     // boundary stores spread one block per phase (SPREAD)
     case 48: return (int)ntm::gemm6::launch_gemm_bf16_pp6<1, false, 0, false, true>(a, S(stream));
+    // 51: pingpong8om (ragged C) with the spread boundary stores
+    case 51: return (int)ntm::gemm6::launch_gemm_bf16_pp6_masked<1, true>(a, S(stream));
     default: return (int)hipErrorInvalidValue;
   }
 }
