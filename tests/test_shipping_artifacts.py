@@ -33,13 +33,13 @@ ALLOWED_K1 = {
     "ntm::gemm3::gemm_bf16_pp3_kernel<false, 8, false, 26, 0, 3>",  # K1-fp8, masked
     "ntm::gemm3::gemm_bf16_pp3_kernel<false, 8, false, 58, 0, 0>",  # masked + partial K
     "ntm::gemm3::gemm_bf16_pp3_kernel<false, 8, false, 58, 0, 3>",  # K1-fp8, masked + partial K
-    # pingpong8o <POL, LINE, STAMP, STG, MASK, TAIL, SPREAD, F8>: > 256 tiles of 256x256
+    # pingpong8o <POL, STAMP, MASK, TAIL, SPREAD, F8>: > 256 tiles of 256x256
     # (the shipping bf16 build spreads its boundary stores: SPREAD, "pingpong8od")
-    "ntm::gemm6::gemm_bf16_pp6_kernel<1, false, 0, false, false, false, true, false>",
-    "ntm::gemm6::gemm_bf16_pp6_kernel<1, false, 1, false, false, false, true, false>",  # clock stamps
-    "ntm::gemm6::gemm_bf16_pp6_kernel<1, false, 0, false, false, false, true, true>",    # K1-fp8
-    "ntm::gemm6::gemm_bf16_pp6_kernel<1, false, 0, false, true, false, false, false>",   # pingpong8om
-    "ntm::gemm6::gemm_bf16_pp6_kernel<1, false, 0, false, true, true, false, false>",    # + partial K
+    "ntm::gemm6::gemm_bf16_pp6_kernel<1, 0, false, false, true, false>",
+    "ntm::gemm6::gemm_bf16_pp6_kernel<1, 1, false, false, true, false>",  # clock stamps
+    "ntm::gemm6::gemm_bf16_pp6_kernel<1, 0, false, false, true, true>",   # K1-fp8
+    "ntm::gemm6::gemm_bf16_pp6_kernel<1, 0, true, false, false, false>",  # pingpong8om
+    "ntm::gemm6::gemm_bf16_pp6_kernel<1, 0, true, true, false, false>",   # + partial K
     # stream-K over the last two rounds of 256x256 tiles (pingpong8s <TAIL, REV, STAMP>)
     "ntm::gemmsk::gemm_bf16_sk_kernel<false, false, false>",
     "ntm::gemmsk::gemm_bf16_sk_kernel<true, false, false>",

@@ -50,7 +50,7 @@ def compare(prof_dir: str, inkernel: dict) -> dict:
     import glob
     import statistics
 
-    key = "pp6_kernel<1, false, 1"
+    key = "pp6_kernel<1, 1,"
     grbm, dur = {}, {}
     for f in glob.glob(str(Path(prof_dir) / "**" / "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):

@@ -4,7 +4,7 @@ workgroup; prints the count of differing elements per run and, for the first
 bad run, the count per accumulator row (16-row group of a wave's 128 rows) -
 the fingerprint that located the asm-MFMA hazard in profiles/r3_w4o/.
 
-    python tools/overlap_bitwise_check.py [--variants pingpong8o,pingpong8ol] [--repeats 5]
+    python tools/overlap_bitwise_check.py [--variants pingpong8o,pingpong8od] [--repeats 5]
 """
 from __future__ import annotations
 
@@ -21,7 +21,7 @@ from nvidia_terraform_modules_amd import ops  # noqa: E402
 
 def main() -> int:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--variants", default="pingpong8o,pingpong8ol")
+    ap.add_argument("--variants", default="pingpong8o,pingpong8od")
     ap.add_argument("--shapes", default="256x256x256,2048x2048x1024,8192x8192x512")
     ap.add_argument("--repeats", type=int, default=5)
     args = ap.parse_args()

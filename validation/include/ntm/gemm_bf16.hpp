@@ -421,10 +421,7 @@ __device__ __forceinline__ void store_c16(void* dst, const unsigned __attribute_
   if constexpr (POL == 1) __builtin_nontemporal_store(v, (u32x4*)dst);
 }
 
-// LINE: the quadrant -> column map of pingpong8o's whole-line layout
-// (gemm_bf16_pp6.hpp): wave column wc owns columns 64 wc .. 64 wc + 63, quadrant
-// nh the 32 at 64 wc + 32 nh (default: 32 wc + 128 nh).
-template <bool kRowSum, bool NT, bool MASK = false, int POL = NT ? 1 : 0, bool LINE = false>
+template <bool kRowSum, bool NT, bool MASK = false, int POL = NT ? 1 : 0>
 __device__ __forceinline__ void store_tile_lds(const GemmArgs& p, const Ctx& c,
                                                const f32x4 (&acc)[2][2][4][2],
                                                int m0, int n0, int lane) {
@@ -439,7 +436,7 @@ __device__ __forceinline__ void store_tile_lds(const GemmArgs& p, const Ctx& c,
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt) {
         const int row = mh * 128 + c.wr * 64 + mt * 16 + (lane & 15);
-        const int col = LINE ? c.wc * 64 + nh * 32 + coff : nh * 128 + c.wc * 32 + coff;
+        const int col = nh * 128 + c.wc * 32 + coff;
         const f32x4 v0 = acc[mh][nh][mt][0], v1 = acc[mh][nh][mt][1];
         unsigned w0[2], w1[2];
 #pragma unroll

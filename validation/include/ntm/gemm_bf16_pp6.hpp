@@ -197,7 +197,7 @@ __device__ __forceinline__ void store_c16_masked(const __bf16* blk, int off, boo
 // columns. c_lane = the lane's element offset inside the tile (one VGPR).
 // MASK: store only rows < M and 8-column chunks < N (lrow / lcol = the lane's
 // row / column inside the quadrant's 16-row block origin, tile-relative).
-template <int MH, int NH, int POL, bool LINE = false, bool MASK = false>
+template <int MH, int NH, int POL, bool MASK = false>
 __device__ __forceinline__ void store_quadrant(const GemmArgs& p, const f32x4 (&q)[4][2],
                                                int m0, int n0, int c_lane, int lrow = 0,
                                                int lcol = 0) {
@@ -214,12 +214,12 @@ __device__ __forceinline__ void store_quadrant(const GemmArgs& p, const f32x4 (&
       w0[h] = r[0];
       w1[h] = r[1];
     }
-    __bf16* tile = p.C + (size_t)(m0 + MH * 128 + mt * 16) * p.ldc + (n0 + NH * (LINE ? 32 : 128));
+    __bf16* tile = p.C + (size_t)(m0 + MH * 128 + mt * 16) * p.ldc + (n0 + NH * 128);
     if constexpr (MASK) {
       const int l = opaque_lane();
       const int lr = lrow + (l & 15);                              // lrow = 64 wr
       const int lc = lcol + ((l >> 4) & 1) * 16 + (l >> 5) * 8;    // lcol = 32 wc
-      const bool ok = m0 + MH * 128 + mt * 16 + lr < p.M && n0 + NH * (LINE ? 32 : 128) + lc < p.N;
+      const bool ok = m0 + MH * 128 + mt * 16 + lr < p.M && n0 + NH * 128 + lc < p.N;
       store_c16_masked<POL>(tile, c_lane, ok, u32x4{w0[0], w0[1], w1[0], w1[1]});
       continue;
     }
@@ -275,80 +275,6 @@ __device__ __forceinline__ void spread_unit(const GemmArgs& p, f32x4 (&acc)[2][2
   }
 }
 
-// LINE layout: both quadrants of row half MH, one 16-row block at a time, so a
-// wave's two adjacent 64-B half-lines of a row leave in consecutive store
-// instructions (a whole 128-B line per row and block).
-template <int MH, int POL>
-__device__ __forceinline__ void store_pair(const GemmArgs& p, const f32x4 (&q)[2][4][2], int m0,
-                                           int n0, int c_lane) {
-  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-#pragma unroll
-  for (int mt = 0; mt < 4; ++mt) {
-    __bf16* tile = p.C + (size_t)(m0 + MH * 128 + mt * 16) * p.ldc + n0 + c_lane;
-#pragma unroll
-    for (int nh = 0; nh < 2; ++nh) {
-      const f32x4 v0 = q[nh][mt][0], v1 = q[nh][mt][1];
-      unsigned w0[2], w1[2];
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const auto r = __builtin_amdgcn_permlane16_swap(pack_bf16x2(v0[2 * h], v0[2 * h + 1]),
-                                                        pack_bf16x2(v1[2 * h], v1[2 * h + 1]),
-                                                        false, false);
-        w0[h] = r[0];
-        w1[h] = r[1];
-      }
-      store_c16<POL>(tile + nh * 32, u32x4{w0[0], w0[1], w1[0], w1[1]});
-    }
-  }
-}
-
-// STG (LINE layout only): the same two quadrants leave through a per-wave 2 KiB
-// LDS slot past the kernel's 144 KiB (kStgBase: LDS is 160 KiB per CU), so
-// each 16-lane store pass writes two WHOLE 128-B lines instead of 16 rows x
-// 16 B. Register-stored C wrote 154-157 MB per 8192^3 call against the
-// LDS-staged epilogue's exact 128 MB (profiles/r3_pmc, r4_line). Per 16-row
-// block: 2 ds_write_b128 (the lane's NH 0 / 1 pieces of row lane & 15), 2
-// ds_read_b128 (lane l: row l >> 3 (+8), 16-B chunk l & 7), 2 global stores;
-// rows are XOR-swizzled by (row & 7) << 4. A wave only touches its own slot,
-// in program order, so no barrier is needed.
-constexpr int kStgBase = kLdsBytes3;          // 144 KiB
-constexpr int kStgBytes = kStgBase + 8 * 2048;  // 160 KiB: the whole LDS of a CU
-
-template <int MH, int POL>
-__device__ __forceinline__ void store_pair_lds(const GemmArgs& p, char* slot,
-                                               const f32x4 (&q)[2][4][2], int m0, int n0,
-                                               int c_lane2, int lane) {
-  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-  const int r = lane & 15, g = lane >> 4;
-  const int wsw = (r & 7) << 4;
-  const int w0 = r * 128 + ((((g & 1) * 32 + (g >> 1) * 16)) ^ wsw);
-  const int rr = lane >> 3, ch = (lane & 7) * 16;
-  const int r0 = rr * 128 + (ch ^ ((rr & 7) << 4));
-  const int r1 = (rr + 8) * 128 + (ch ^ (((rr + 8) & 7) << 4));
-#pragma unroll
-  for (int mt = 0; mt < 4; ++mt) {
-#pragma unroll
-    for (int nh = 0; nh < 2; ++nh) {
-      const f32x4 v0 = q[nh][mt][0], v1 = q[nh][mt][1];
-      unsigned a[2], b[2];
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const auto x = __builtin_amdgcn_permlane16_swap(pack_bf16x2(v0[2 * h], v0[2 * h + 1]),
-                                                        pack_bf16x2(v1[2 * h], v1[2 * h + 1]),
-                                                        false, false);
-        a[h] = x[0];
-        b[h] = x[1];
-      }
-      *(u32x4*)(slot + (w0 ^ (nh * 64))) = u32x4{a[0], a[1], b[0], b[1]};
-    }
-    const u32x4 lo = *(const u32x4*)(slot + r0);
-    const u32x4 hi = *(const u32x4*)(slot + r1);
-    __bf16* tile = p.C + (size_t)(m0 + MH * 128 + mt * 16) * p.ldc + n0 + c_lane2;
-    store_c16<POL>(tile, lo);
-    store_c16<POL>(tile + (size_t)8 * p.ldc, hi);
-  }
-}
-
 // Zero a stored quadrant in place (32 v_mov): an MFMA with an inline-zero C
 // operand instead lets hipcc give the result fresh registers, and the copies
 // back at the loop's back edge spilled.
@@ -370,17 +296,16 @@ struct Edge {
 
 // One phase. CONV: quadrant stored in this phase's load segment when ON (-1
 // none; 0..3 = q0..q3 in finishing order; q3 belongs to the previous tile, so
-// its origin is e.pm0 / e.pn0; LINE layout: 4 = both quadrants of row half 0 of
-// this tile, 5 = both of row half 1 of the previous tile); ON: e.prev (K-tiles
-// 0 / 1) or e.has_next (K-tile T-1); VMC: the counted wait when ON (10
-// otherwise); NX: this phase's piece is past the tile (issue6). A stored
-// quadrant is zeroed for the next tile.
-template <int P, bool ODD, int CONV, int VMC, bool NX, int POL, bool LINE, bool STG = false,
-          bool MASK = false, bool TL = false, bool F8 = false>
+// its origin is e.pm0 / e.pn0; 10 + O = boundary phase O of the SPREAD build);
+// ON: e.prev (K-tiles 0 / 1) or e.has_next (K-tile T-1); VMC: the counted wait
+// when ON (10 otherwise); NX: this phase's piece is past the tile (issue6). A
+// stored quadrant is zeroed for the next tile.
+template <int P, bool ODD, int CONV, int VMC, bool NX, int POL, bool MASK = false, bool TL = false,
+          bool F8 = false>
 __device__ __forceinline__ void phase6(const GemmArgs& p, const Ctx& c, Frags3& f,
                                        f32x4 (&acc)[2][2][4][2], int t, int T, const Edge& e,
-                                       bool on, int c_lane, int c_lane2 = 0, int lane = 0,
-                                       int lrow = 0, int lcol = 0) {
+                                       bool on, int c_lane, int lane = 0, int lrow = 0,
+                                       int lcol = 0) {
   bf16x8(&bcur)[2][2] = ODD ? f.b1 : f.b0;
   bf16x8(&both)[2][2] = ODD ? f.b0 : f.b1;
   const int cur = t & 1;
@@ -413,20 +338,6 @@ __device__ __forceinline__ void phase6(const GemmArgs& p, const Ctx& c, Frags3& 
       spread_unit<O, 2, POL, MASK>(p, acc, e.m0, e.n0, e.pm0, e.pn0, c_lane, lrow, lcol);
       spread_unit<O, 3, POL, MASK>(p, acc, e.m0, e.n0, e.pm0, e.pn0, c_lane, lrow, lcol);
     }
-  } else if constexpr (CONV >= 4) {
-    if (on) {
-      constexpr int MH = CONV - 4;
-      const int m0 = MH == 1 ? e.pm0 : e.m0, n0 = MH == 1 ? e.pn0 : e.n0;
-      if constexpr (POL == 2) {  // ablation (experimental library): C not stored
-        if (p.ldc < 0) store_pair<MH, 1>(p, acc[MH], m0, n0, c_lane);
-      } else if constexpr (STG) {
-        store_pair_lds<MH, POL>(p, c.lds + kStgBase + c.w * 2048, acc[MH], m0, n0, c_lane2, lane);
-      } else {
-        store_pair<MH, POL>(p, acc[MH], m0, n0, c_lane);
-      }
-      zero_quadrant(acc[MH][0]);
-      zero_quadrant(acc[MH][1]);
-    }
   } else if constexpr (CONV >= 0) {
     if (on) {
       constexpr int MH = (CONV == 2 || CONV == 3) ? 1 : 0;
@@ -436,8 +347,8 @@ __device__ __forceinline__ void phase6(const GemmArgs& p, const Ctx& c, Frags3& 
           store_quadrant<MH, NH, 1>(p, acc[MH][NH], CONV == 3 ? e.pm0 : e.m0,
                                     CONV == 3 ? e.pn0 : e.n0, c_lane);
       } else {
-        store_quadrant<MH, NH, POL, false, MASK>(p, acc[MH][NH], CONV == 3 ? e.pm0 : e.m0,
-                                                 CONV == 3 ? e.pn0 : e.n0, c_lane, lrow, lcol);
+        store_quadrant<MH, NH, POL, MASK>(p, acc[MH][NH], CONV == 3 ? e.pm0 : e.m0,
+                                          CONV == 3 ? e.pn0 : e.n0, c_lane, lrow, lcol);
       }
       zero_quadrant(acc[MH][NH]);
     }
@@ -456,8 +367,7 @@ __device__ __forceinline__ void phase6(const GemmArgs& p, const Ctx& c, Frags3& 
 }
 
 #define NTM_PHT(P, ODD, CV, VMC, NX, ON, TL) \
-  phase6<P, ODD, CV, VMC, NX, POL, LINE, STG, MASK, TL, F8>(p, c, f, acc, t, T, e, ON, c_lane, \
-                                                            c_lane2, lane, lrow, lcol)
+  phase6<P, ODD, CV, VMC, NX, POL, MASK, TL, F8>(p, c, f, acc, t, T, e, ON, c_lane, lane, lrow, lcol)
 #define NTM_PH(P, ODD, CV, VMC, NX, ON) NTM_PHT(P, ODD, CV, VMC, NX, ON, false)
 // STAMP 2: shader-clock stamp I of wave 0 at a phase start of the workgroup's
 // first tile boundary (K-tiles T-2 / T-1 of its first tile: I = 0..7, K-tiles
@@ -489,32 +399,16 @@ __device__ __forceinline__ void clock_stamp(unsigned long long& t, unsigned long
 }
 
 // POL: C store policy of store_c16 (1 = nontemporal, the shipping build).
-// LINE: whole-line C layout. The B-lo / B-hi LDS halves stage B rows
-// n0 + 64 j + [0, 32) / n0 + 64 j + 32 + [0, 32) for row group pair j = 0..3
-// (only each staging wave's global B row changes; the LDS image and every read
-// stay), so wave column wc's two N-quadrants are the adjacent columns
-// 64 wc .. 64 wc + 63 = one 128-B line per row. A row half's two quadrants leave
-// together (store_pair) in the phase after the second of them finished:
-//   P2(T-1): row half 0 of this tile   P0(0 of the next tile): row half 1
-// With 8 stores per lane in each of those phases the counted waits become
-// (vmcnt = 10 + stores issued in phases j-5 .. j-1):
-//   P2(T-1) 10, P3(T-1) 18, P0(0) 18, P1(0) 26, P2(0) 26, P3(0) 26, P0(1) 18,
-//   P1(1) 18, P2(1) 10.
-// Row half 0 is first rewritten in P0 / P1 of the next tile's K-tile 0, row
-// half 1 in P2 / P3, both after their store phase.
 // STAMP 1 (diagnostic build, never in the default dispatch): lane 0 of wave 0
 // records s_memtime / s_memrealtime at kernel start and after the last store
 // into p.stamps[4 * blockIdx.x ..]: the GEMM's own clock = d(memtime) /
 // d(realtime) x 100 MHz.
-// An fp8 build of this structure did not fit: pingpong8c's fp8 consumer already
-// holds 128 VGPRs + 128 AGPRs, and the boundary conversion spilled 76 VGPRs.
-// STG (LINE only): boundary stores staged through LDS in whole lines (store_pair_lds).
-// MASK ("pingpong8om", default layout only): ragged C - ceil(M/256) x
+// MASK ("pingpong8om"): ragged C - ceil(M/256) x
 // ceil(N/256) tiles, sources clamped per tile (src_clamped), stores masked.
 // TAIL (with MASK): K % 128 != 0 - T = ceil(K / 128) * 2 K-tiles; the pieces
 // that can reach past K (K-tiles T-2 / T-1, issued from K-tiles T-4 .. T-2, or
 // from K-tiles 0 / 1 when T = 4) zero-fill their chunks past K.
-// SPREAD (experimental, default layout): each boundary quadrant's 4 store
+// SPREAD (the shipping build, "pingpong8od"): each boundary quadrant's 4 store
 // blocks go out one per phase over the 4 phases it has before its reuse
 // (stores per phase 1,2,3,4,3,2,1 from P1 of K-tile T-1 to P3 of the next
 // tile's K-tile 0, instead of 4,4,4,4); counted waits 10 + stores in phases
@@ -522,15 +416,17 @@ __device__ __forceinline__ void clock_stamp(unsigned long long& t, unsigned long
 // P0(1) 23, P1 20, P2 16, P3 13 (P0(2) needs 11; the loop's 10 over-waits by
 // one store issued 5 phases earlier).
 // F8: OCP e4m3 operands (K / lda / ldb in bf16-sized pairs, as K1-fp8's
-// pingpong8c), f8f6f4 MFMAs on VGPR accumulators (mfma_f8_vgpr).
-template <int POL, bool LINE = false, int STAMP = 0, bool STG = false, bool MASK = false,
-          bool TAIL = false, bool SPREAD = false, bool F8 = false>
+// pingpong8c), f8f6f4 MFMAs on VGPR accumulators (mfma_f8_vgpr; pingpong8c's
+// fp8 build keeps them in AGPRs, and with 128 + 128 registers there its
+// boundary conversion spilled).
+// (Round 4 also measured a whole-128-B-line C layout, with and without LDS
+// staging of the boundary stores: exactly 128 MB written instead of 157 MB,
+// no faster. Removed after measurement, profiles/r4_stg/; git history has it.)
+template <int POL, int STAMP = 0, bool MASK = false, bool TAIL = false, bool SPREAD = false,
+          bool F8 = false>
 __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_pp6_kernel(GemmArgs p) {
-  static_assert(!SPREAD || !LINE, "SPREAD: default layout");
-  static_assert(!STG || LINE, "LDS-staged boundary stores need the whole-line layout");
-  static_assert(!MASK || (!LINE && !STG), "the masked build uses the default C layout");
   static_assert(!TAIL || MASK, "partial K rides on the masked build");
-  __shared__ __attribute__((aligned(16))) char smem[STG ? kStgBytes : kLdsBytes3];
+  __shared__ __attribute__((aligned(16))) char smem[kLdsBytes3];
   unsigned long long t0 = 0, rt0 = 0;
   if constexpr (STAMP == 1) clock_stamp(t0, rt0);
   const int ntiles = MASK ? ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN) : (p.M / BM) * (p.N / BN);
@@ -548,13 +444,13 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_pp6_kernel(GemmArgs p) 
   {
     const int r = lane >> 2;
     const int cl = (lane & 3) ^ (((r >> 3) & 1) << 1);
-    const int rb = LINE ? (c.w >> 1) * 64 + (c.w & 1) * 16 + r : c.w * 16 + r;
+    const int rb = c.w * 16 + r;
     const __bf16* a0 = p.A + (size_t)(e.m0 + c.w * 16 + r) * p.lda + cl * 8;
     const __bf16* b0 = p.B + (size_t)(e.n0 + rb) * p.ldb + cl * 8;
     c.src[kALo] = a0;
     c.src[kAHi] = a0 + (size_t)128 * p.lda;
     c.src[kBLo] = b0;
-    c.src[kBHi] = b0 + (size_t)(LINE ? 32 : 128) * p.ldb;
+    c.src[kBHi] = b0 + (size_t)128 * p.ldb;
     if constexpr (MASK) {
       c.src[kALo] = src_clamped<kALo>(p, e.m0, e.n0, c.w, lane);
       c.src[kAHi] = src_clamped<kAHi>(p, e.m0, e.n0, c.w, lane);
@@ -567,10 +463,8 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_pp6_kernel(GemmArgs p) 
   const int lrow = c.wr * 64;
   const int lcol = c.wc * 32;
   c.frag_off = (lane & 15) * 64 + ((lane >> 4) ^ ((lane >> 2) & 2)) * 16;
-  const int c_lane = (c.wr * 64 + (lane & 15)) * p.ldc + c.wc * (LINE ? 64 : 32) +
+  const int c_lane = (c.wr * 64 + (lane & 15)) * p.ldc + c.wc * 32 +
                      ((lane >> 4) & 1) * 16 + (lane >> 5) * 8;
-  // STG: row lane >> 3 of the 16-row block, 8-column chunk lane & 7
-  const int c_lane2 = (c.wr * 64 + (lane >> 3)) * p.ldc + c.wc * 64 + (lane & 7) * 8;
 
   f32x4 acc[2][2][4][2];
 #pragma unroll
@@ -611,20 +505,20 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_pp6_kernel(GemmArgs p) 
   // their registers around the back edge.
   for (;;) {
     int t = 0;
-    // K-tile 0: q3 (LINE: row half 1) of the previous tile leaves in P0
+    // K-tile 0: q3 of the previous tile leaves in P0 (SPREAD: blocks of q0..q3 in P0..P3)
     NTM_ST(8, false);
-    NTM_PHT(0, false, SPREAD ? 13 : LINE ? 5 : 3, SPREAD ? 16 : LINE ? 18 : 22, false, e.prev, TAIL);
+    NTM_PHT(0, false, SPREAD ? 13 : 3, SPREAD ? 16 : 22, false, e.prev, TAIL);
     NTM_ST(9, false);
     NTM_PHT(1, false, SPREAD ? 14 : -1, SPREAD ? 20 : 26, false, e.prev, TAIL);
     NTM_ST(10, false);
     NTM_PHT(2, false, SPREAD ? 15 : -1, SPREAD ? 23 : 26, false, e.prev, TAIL);
     NTM_ST(11, false);
-    NTM_PHT(3, false, SPREAD ? 16 : -1, SPREAD ? 24 : LINE ? 26 : 22, false, e.prev, TAIL);
+    NTM_PHT(3, false, SPREAD ? 16 : -1, SPREAD ? 24 : 22, false, e.prev, TAIL);
     t = 1;
     NTM_ST(12, false);
     NTM_PHT(0, true, -1, SPREAD ? 23 : 18, false, e.prev, TAIL);
     NTM_ST(13, false);
-    NTM_PHT(1, true, -1, SPREAD ? 20 : LINE ? 18 : 14, false, e.prev, TAIL);
+    NTM_PHT(1, true, -1, SPREAD ? 20 : 14, false, e.prev, TAIL);
     NTM_ST(14, false);
     NTM_PHT(2, true, -1, SPREAD ? 16 : 10, false, e.prev, TAIL);
     NTM_ST(15, false);
@@ -674,11 +568,11 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_pp6_kernel(GemmArgs p) 
     NTM_ST(4, true);
     NTM_PH(0, true, -1, 10, true, false);
     NTM_ST(5, true);
-    NTM_PH(1, true, SPREAD ? 10 : LINE ? -1 : 0, 10, true, e.has_next);
+    NTM_PH(1, true, SPREAD ? 10 : 0, 10, true, e.has_next);
     NTM_ST(6, true);
-    NTM_PH(2, true, SPREAD ? 11 : LINE ? 4 : 1, SPREAD ? 11 : LINE ? 10 : 14, true, e.has_next);
+    NTM_PH(2, true, SPREAD ? 11 : 1, SPREAD ? 11 : 14, true, e.has_next);
     NTM_ST(7, true);
-    NTM_PH(3, true, SPREAD ? 12 : LINE ? -1 : 2, SPREAD ? 13 : 18, true, e.has_next);
+    NTM_PH(3, true, SPREAD ? 12 : 2, SPREAD ? 13 : 18, true, e.has_next);
     if (!e.has_next) break;
     // advance to the next tile
     if constexpr (MASK) {
@@ -710,7 +604,7 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_pp6_kernel(GemmArgs p) 
   wait_vm<0>();                  // dummy pieces: nothing may land after the WG exits
   if constexpr (F8) mfma_wait_states();  // asm MFMAs: results land before VALU reads
   if (POL != 2 || p.ldc < 0)
-    store_tile_lds<false, POL != 0, MASK, POL == 0 ? 0 : 1, LINE>(p, c, acc, e.m0, e.n0, lane);
+    store_tile_lds<false, POL != 0, MASK, POL == 0 ? 0 : 1>(p, c, acc, e.m0, e.n0, lane);
   if constexpr (STAMP == 1) {
     unsigned long long t1, rt1;
     clock_stamp(t1, rt1);
@@ -743,25 +637,25 @@ inline int pp6_grid(int ntiles) {
 
 // Experimental: an explicit grid (a multiple of 8, at most the tile count) and
 // POL 2 (C not stored) - the store-bandwidth study of profiles/r3_stores.
-template <int POL, bool LINE = false, int STAMP = 0>
+template <int POL, int STAMP = 0>
 inline hipError_t launch_gemm_bf16_pp6_grid(const GemmArgs& a, int grid, hipStream_t stream) {
   if (!shape_ok6(a.M, a.N, a.K) || a.rowsum || a.lda < a.K || a.ldb < a.K || a.ldc < a.N ||
       (a.lda % 8) || (a.ldb % 8) || (a.ldc % 8) || grid <= 0 || grid % 8 ||
       grid > (a.M / BM) * (a.N / BN))
     return hipErrorInvalidValue;
   if (STAMP != 0 && a.stamps == nullptr) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((gemm_bf16_pp6_kernel<POL, LINE, STAMP>), dim3((unsigned)grid), dim3(kThreads), 0,
+  hipLaunchKernelGGL((gemm_bf16_pp6_kernel<POL, STAMP>), dim3((unsigned)grid), dim3(kThreads), 0,
                      stream, a);
   return hipGetLastError();
 }
 
-template <int POL, bool LINE = false, int STAMP = 0, bool STG = false, bool SPREAD = false>
+template <int POL, int STAMP = 0, bool SPREAD = false>
 inline hipError_t launch_gemm_bf16_pp6(const GemmArgs& a, hipStream_t stream) {
   if (!shape_ok6(a.M, a.N, a.K) || a.rowsum || a.lda < a.K || a.ldb < a.K || a.ldc < a.N ||
       (a.lda % 8) || (a.ldb % 8) || (a.ldc % 8) || (STAMP != 0 && a.stamps == nullptr))
     return hipErrorInvalidValue;
   const int ntiles = (a.M / BM) * (a.N / BN);
-  hipLaunchKernelGGL((gemm_bf16_pp6_kernel<POL, LINE, STAMP, STG, false, false, SPREAD>),
+  hipLaunchKernelGGL((gemm_bf16_pp6_kernel<POL, STAMP, false, false, SPREAD>),
                      dim3((unsigned)pp6_grid(ntiles)),
                      dim3(kThreads), 0, stream, a);
   return hipGetLastError();
@@ -792,7 +686,7 @@ inline hipError_t launch_gemm_fp8_pp6(const void* A, const void* B, __bf16* C, i
       a.ldb < a.K || a.ldc < a.N || (a.ldc % 8))
     return hipErrorInvalidValue;
   const int ntiles = (a.M / BM) * (a.N / BN);
-  hipLaunchKernelGGL((gemm_bf16_pp6_kernel<1, false, 0, false, false, false, SPREAD, true>),
+  hipLaunchKernelGGL((gemm_bf16_pp6_kernel<1, 0, false, false, SPREAD, true>),
                      dim3((unsigned)pp6_grid(ntiles)), dim3(kThreads), 0, stream, a);
   return hipGetLastError();
 }
@@ -807,9 +701,9 @@ inline hipError_t launch_gemm_bf16_pp6_masked(const GemmArgs& a, hipStream_t str
   const int ntiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
   const dim3 g((unsigned)pp6_grid(ntiles)), b(kThreads);
   if (a.K % (2 * BK))
-    hipLaunchKernelGGL((gemm_bf16_pp6_kernel<POL, false, 0, false, true, true, SPREAD>), g, b, 0, stream, a);
+    hipLaunchKernelGGL((gemm_bf16_pp6_kernel<POL, 0, true, true, SPREAD>), g, b, 0, stream, a);
   else
-    hipLaunchKernelGGL((gemm_bf16_pp6_kernel<POL, false, 0, false, true, false, SPREAD>), g, b, 0, stream, a);
+    hipLaunchKernelGGL((gemm_bf16_pp6_kernel<POL, 0, true, false, SPREAD>), g, b, 0, stream, a);
   return hipGetLastError();
 }
 

@@ -76,14 +76,10 @@ NTM_API int ntm_gemm_bf16_experimental(int variant, const void* A, const void* B
     case 41: return (int)ntm::gemm6::launch_gemm_bf16_pp6_grid<1>(a, 128, S(stream));
     case 42: return (int)ntm::gemm6::launch_gemm_bf16_pp6_grid<2>(a, 128, S(stream));
     case 43: return (int)ntm::gemm6::launch_gemm_bf16_pp6_grid<2>(a, 256, S(stream));
-    // pingpong8o with the whole-line C layout (gemm_bf16_pp6.hpp LINE), and the
-    // same with C not stored
-    case 44: return (int)ntm::gemm6::launch_gemm_bf16_pp6<1, true>(a, S(stream));
-    case 45: return (int)ntm::gemm6::launch_gemm_bf16_pp6_grid<2, true>(a, 256, S(stream));
-    // whole-line layout with the boundary stores staged through LDS in whole lines
-    case 46: return (int)ntm::gemm6::launch_gemm_bf16_pp6<1, true, 0, true>(a, S(stream));
-    // boundary stores spread one block per phase (SPREAD)
-    case 48: return (int)ntm::gemm6::launch_gemm_bf16_pp6<1, false, 0, false, true>(a, S(stream));
+    // 44-46 (round 4: whole-line C layouts, with and without LDS-staged boundary
+    // stores) were removed after measurement (profiles/r4_stg/).
+    // 48: boundary stores spread one block per phase (SPREAD) = the shipping 25
+    case 48: return (int)ntm::gemm6::launch_gemm_bf16_pp6<1, 0, true>(a, S(stream));
     // 51: pingpong8om (ragged C) with the spread boundary stores
     case 51: return (int)ntm::gemm6::launch_gemm_bf16_pp6_masked<1, true>(a, S(stream));
     default: return (int)hipErrorInvalidValue;
@@ -137,8 +133,8 @@ NTM_API int ntm_gemm_bf16_pp6_stamp(int grid, int store, const void* A, const vo
   ntm::gemm::GemmArgs a = args(A, B, C, M, N, K, lda, ldb, ldc);
   a.stamps = (unsigned long long*)stamps;
   if (grid * 2 > (M / 256) * (N / 256)) return (int)hipErrorInvalidValue;
-  return store ? (int)ntm::gemm6::launch_gemm_bf16_pp6_grid<1, false, 2>(a, grid, S(stream))
-               : (int)ntm::gemm6::launch_gemm_bf16_pp6_grid<2, false, 2>(a, grid, S(stream));
+  return store ? (int)ntm::gemm6::launch_gemm_bf16_pp6_grid<1, 2>(a, grid, S(stream))
+               : (int)ntm::gemm6::launch_gemm_bf16_pp6_grid<2, 2>(a, grid, S(stream));
 }
 
 // pingpong8c tuning knobs (see launch_gemm_bf16_pp3_knob).

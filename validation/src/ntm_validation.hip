@@ -64,8 +64,6 @@ NTM_API int ntm_gemm_shape_ok(int M, int N, int K) {
 // 1394 vs 1374 (+1.5 %), 8192x8192x6144 1611 vs 1590 (+1.3 %).
 constexpr int kDefaultVariant = 5;
 constexpr int kPersistentVariant = 25;
-// C layout of the shipping pingpong8o build (gemm_bf16_pp6.hpp LINE)
-constexpr bool kPp6Line = false;
 // Boundary stores of the shipping build spread over the 7 phases the quadrants
 // allow (gemm_bf16_pp6.hpp SPREAD, "pingpong8od"), round 4: median over 3
 // boxes vs hipBLASLt 8192^3 0.998 (plain 0.996), 8192x8192x4096 1.008
@@ -372,7 +370,7 @@ NTM_API int ntm_gemm_bf16_variant(int variant, const void* A, const void* B,
     case 25:
       if (!ntm::gemm6::shape_ok6(M, N, K) || (lda % 8) || (ldb % 8) || (ldc % 8))
         return (int)ntm::gemm3::launch_gemm_bf16_pp3(a, S(stream));
-      return (int)ntm::gemm6::launch_gemm_bf16_pp6<1, kPp6Line, 0, false, kPp6Spread>(a, S(stream));
+      return (int)ntm::gemm6::launch_gemm_bf16_pp6<1, 0, kPp6Spread>(a, S(stream));
     // persistent + masked (pingpong8om): ragged C over more than one round of
     // 256x256 tiles (K % 128, K >= 256; otherwise pingpong8cm)
     case 47:
@@ -779,7 +777,7 @@ NTM_API int ntm_gemm_bf16_clock(const void* A, const void* B, void* C, int M, in
   a.ldb = ldb;
   a.ldc = ldc;
   a.stamps = (unsigned long long*)stamps;
-  return (int)ntm::gemm6::launch_gemm_bf16_pp6<1, kPp6Line, 1, false, kPp6Spread>(a, S(stream));
+  return (int)ntm::gemm6::launch_gemm_bf16_pp6<1, 1, kPp6Spread>(a, S(stream));
 }
 
 NTM_API int ntm_verify_result_bytes() {
