@@ -53,7 +53,7 @@ def parse(argv=None):
     ap.add_argument("--size", type=int, default=8192, help="M = N = K of the per-GPU GEMM")
     ap.add_argument("--prewarm-s", type=float, default=0.5,
                     help="untimed clock-settle pre-warm before the W warmup steps (wall seconds)")
-    ap.add_argument("--compare-rounds", type=int, default=7,
+    ap.add_argument("--compare-rounds", type=int, default=15,
                     help="ABAB rounds of the interleaved K1 vs hipBLASLt comparison")
     ap.add_argument("--no-check", action="store_true", help="skip full-matrix verification")
     ap.add_argument("--no-extras", action="store_true",
@@ -124,13 +124,16 @@ def prewarm_settle(fn, sync, min_s: float, chunk: int = 16) -> dict:
 
 
 def interleaved_compare(fns: dict, dev, rounds: int, launches: int) -> dict:
-    """ABAB timing: in each round every callable runs ``launches`` times under
-    its own events; per-callable median over rounds (seconds per launch)."""
+    """ABBA timing: in each round every callable runs ``launches`` times under
+    its own events, in the given order on even rounds and reversed on odd ones
+    (neither side always follows the other); per-callable median over rounds
+    (seconds per launch)."""
     import statistics
 
     per: dict = {k: [] for k in fns}
-    for _ in range(rounds):
-        for k, fn in fns.items():
+    order = list(fns.items())
+    for r in range(rounds):
+        for k, fn in (order if r % 2 == 0 else order[::-1]):
             tm = StepTimer(dev)
             tm.start()
             for _ in range(launches):
@@ -324,6 +327,7 @@ def main(argv=None) -> int:
             "hipblaslt_tflops_rounds": [round(wl.flops / s / 1e12, 1)
                                         for s in cmp_["hipblaslt"]["rounds_s"]]}
         extras["hipblaslt_tflops_per_gpu_rank0"] = hb_tf
+        extras["k1_over_hipblaslt"] = round(k1_tf / hb_tf, 4)  # rank 0, interleaved medians
         extras["ours_tflops_per_gpu"] = total_tflops / n
         # same K1 with the fused ABFT row-checksum epilogue, then its O(n^2) check
         tm = StepTimer(dev)
