@@ -51,6 +51,10 @@ moved-from-exists  a moved `from` that is still declared in the configuration ("
                    object still exists")
 moved-kind         a moved block between a resource and a module call (both ends must be
                    the same kind)
+import-target      an import block whose `to` is not a managed resource declared in the
+                   configuration (a module call, a data source, or an address nothing
+                   declares: "Configuration for import target does not exist"), or an import
+                   block in a module that is not a root (Terraform accepts them only there)
 fmt                tabs / trailing whitespace (terraform fmt would rewrite)
 """
 from __future__ import annotations
@@ -336,6 +340,7 @@ def analyze(mod: Module, *, strict_unused: bool = True, vendor_lint: bool = True
     out.extend(namespace_findings(mod))
     out.extend(eks_node_group_findings(mod))
     out.extend(moved_findings(mod, callee_loader))
+    out.extend(import_findings(mod, callee_loader))
     if check_fmt:
         out.extend(fmt_findings(mod.path))
     return out
@@ -629,6 +634,64 @@ def moved_findings(mod: Module, loader=load_module) -> list[Finding]:
                 out.append(Finding("moved-kind", "error", where,
                                    f"moved {render(frm)} -> {render(to)}: one end is a module "
                                    "call, the other a resource"))
+    return out
+
+
+def _resolve_target(t: Traversal, mod: Module, loader):
+    """(module holding the resource, "type.name", is_data) for a resource address
+    through local module calls; module None when the path enters another package
+    (unverifiable offline), or when the address names no resource."""
+    steps = _address_steps(t)
+    cur, i = mod, 0
+    while i + 1 < len(steps) and steps[i] == ("attr", "module") and steps[i + 1][0] == "attr":
+        mc = cur.modules.get(steps[i + 1][1])
+        if mc is None:
+            return cur, f"module.{steps[i + 1][1]}", False  # an undeclared call: not found below
+        i += 2
+        if i < len(steps) and steps[i][0] == "index":
+            i += 1
+        if not mc.is_local:
+            return None, "", False
+        p = (cur.path / mc.source).resolve()
+        if not p.is_dir():
+            return None, "", False
+        cur = loader(p)
+    names = [v for k, v in steps[i:] if k == "attr"]
+    if names[:1] == ["data"]:
+        return cur, ".".join(names[1:3]), True
+    return cur, ".".join(names[:2]), False
+
+
+def import_findings(mod: Module, loader=load_module) -> list[Finding]:
+    """import-target: Terraform's plan-time checks on import blocks."""
+    from .docs import render
+
+    out = []
+    non_root = "modules" in mod.path.parts
+    for b, f in mod.imports:
+        where = f"{f}:{b.line}"
+        if non_root:
+            out.append(Finding("import-target", "error", where,
+                               "import block in a non-root module (Terraform allows them only "
+                               "in the root module)"))
+        to = b.body.attr("to")
+        if not isinstance(to, Traversal):
+            out.append(Finding("import-target", "error", where, "import without a `to` address"))
+            continue
+        if _is_module_addr(to):
+            out.append(Finding("import-target", "error", where,
+                               f"import to = {render(to)}: a module call, not a resource"))
+            continue
+        holder, addr, is_data = _resolve_target(to, mod, loader)
+        if holder is None:
+            continue  # inside another package: not checkable offline
+        if is_data:
+            out.append(Finding("import-target", "error", where,
+                               f"import to = {render(to)}: a data source cannot be imported"))
+        elif addr not in holder.resources:
+            out.append(Finding("import-target", "error", where,
+                               f"import to = {render(to)}: no resource {addr} is declared "
+                               "there (\"Configuration for import target does not exist\")"))
     return out
 
 

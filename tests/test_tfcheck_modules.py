@@ -432,3 +432,41 @@ def test_moved_rules(tmp_path):
     # ...and the real roots are clean (test_every_module_is_clean runs it too)
     for d in _modules(Path(__file__).resolve().parents[1]):
         assert moved_findings(load_module(d)) == [], d
+
+
+def test_import_target_rule(tmp_path):
+    """import-target: an import must land on a managed resource the
+    configuration declares (through local child modules too), never on a module
+    call or a data source, and only in a root module."""
+    from nvidia_terraform_modules_amd.tfcheck.analysis import import_findings
+
+    child = tmp_path / "child"
+    child.mkdir()
+    (child / "c.tf").write_text('resource "aws_iam_role" "r" {}\n')
+    (tmp_path / "main.tf").write_text(
+        'module "local" {\n  source = "./child"\n}\n'
+        'module "eks" {\n  source = "terraform-aws-modules/eks/aws"\n}\n'
+        'resource "aws_kms_key" "k" {}\n'
+        'data "aws_caller_identity" "me" {}\n'
+        # good: a declared resource, one in a local child, one inside a registry package
+        'import {\n  to = aws_kms_key.k\n  id = "key-1"\n}\n'
+        'import {\n  to = module.local.aws_iam_role.r\n  id = "role"\n}\n'
+        'import {\n  to = module.eks.aws_iam_role.this[0]\n  id = "role"\n}\n'
+        # bad: undeclared, undeclared in the child, a module call, a data source
+        'import {\n  to = aws_kms_key.gone\n  id = "x"\n}\n'
+        'import {\n  to = module.local.aws_iam_role.nope\n  id = "x"\n}\n'
+        'import {\n  to = module.local\n  id = "x"\n}\n'
+        'import {\n  to = data.aws_caller_identity.me\n  id = "x"\n}\n')
+    fs = import_findings(load_module(tmp_path))
+    text = (tmp_path / "main.tf").read_text().splitlines()
+    bad = sorted(text[int(f.where.split(":")[1])].strip() for f in fs)
+    assert bad == ["to = aws_kms_key.gone", "to = data.aws_caller_identity.me",
+                   "to = module.local", "to = module.local.aws_iam_role.nope"], fs
+    nonroot = tmp_path / "modules" / "m"
+    nonroot.mkdir(parents=True)
+    (nonroot / "m.tf").write_text('resource "aws_kms_key" "k" {}\n'
+                                  'import {\n  to = aws_kms_key.k\n  id = "x"\n}\n')
+    fs = import_findings(load_module(nonroot))
+    assert [f.rule for f in fs] == ["import-target"] and "non-root" in fs[0].message
+    for d in _modules(Path(__file__).resolve().parents[1]):
+        assert import_findings(load_module(d)) == [], d
