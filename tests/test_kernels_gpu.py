@@ -875,8 +875,8 @@ def test_stream_k_counters_left_zero_and_refusals(ops):
                                   ws.data_ptr(), wsb - 4, stream_handle()) != 0
     assert ops.sk_ws_bytes(8192, 8192, 8192) == 0     # 1024 tiles: whole rounds
     assert ops.sk_ws_bytes(4096, 4096, 4096) == 0     # 256 tiles: one round
-    with pytest.raises(ValueError):
-        ops.gemm_bf16(a[:, :4096], b[:256, :4096], variant="pingpong8s")
+    with pytest.raises(ValueError):  # exactly one round of 256x256 tiles: neither mode
+        ops.gemm_bf16(a[:4096, :4096], b[:4096, :4096], variant="pingpong8s")
 
 
 @pytest.mark.parametrize("m,n,k", [(4864, 3608, 5696), (6496, 2752, 5416)])
@@ -892,3 +892,32 @@ def test_default_plan_runs_stream_k(ops, m, n, k):
     ref = a.float() @ b.float().T
     atol, rtol = ops.gemm_tolerance(k)
     assert torch.all((c.float() - ref).abs() <= atol + rtol * ref.abs())
+
+
+SKS_SHAPES = [(4672, 1472, 6696),   # 114 tiles: 2 K slices each
+              (2048, 2048, 4096),   # 64 tiles: 4 slices
+              (280, 6352, 7568),    # 50 tiles: 4 slices, K % 128 != 0
+              (1000, 1000, 1000),   # 16 tiles: 8 slices of one pair, partial K
+              (256, 256, 256)]      # 1 tile: 2 slices of one pair
+
+
+@pytest.mark.parametrize("m,n,k", SKS_SHAPES)
+def test_stream_k_split_mode_vs_torch_fp32(ops, m, n, k):
+    """pingpong8s on at most half a round of 256x256 tiles (round 4, split
+    mode): every tile in S K slices at once, the slice that completes the
+    counter sums all S partials in slice order. vs the fp32 product; no row /
+    column past C written; a second launch gives the same bytes (counters left
+    at 0, combiner-independent sum)."""
+    assert ops.sk_ws_bytes(m, n, k) > 0
+    a = _rand(ops, (m, k), 681 + k)
+    b = _rand(ops, (n, k), 683 + n)
+    out = torch.full((m, n + 8), 7.0, dtype=torch.bfloat16, device="cuda")
+    c = ops.gemm_bf16(a, b, out[:, :n], variant="pingpong8s")
+    ref = a.float() @ b.float().T
+    atol, rtol = ops.gemm_tolerance(k)
+    err = (c.float() - ref).abs()
+    assert torch.all(err <= atol + rtol * ref.abs()), float(err.max())
+    assert torch.all(out[:, n:] == 7.0)
+    first = c.clone()
+    for _ in range(3):
+        assert torch.equal(ops.gemm_bf16(a, b, variant="pingpong8s"), first)

@@ -45,7 +45,9 @@ SHAPES_PERSIST_RAGGED = [(4472, 5688, 5832), (4608, 4360, 456), (5000, 4104, 768
 # stream-K (pingpong8s / pingpong8s_rev): more 256x256 tiles than CUs, not a
 # multiple of them - one and two rounds, ragged C, partial K, one-pair tiles
 SHAPES_SK = [(4472, 5688, 5832), (4608, 4608, 1024), (6144, 6144, 2048), (4472, 5688, 200),
-             (8192, 2304, 128), (5000, 4104, 4096), (1000, 17000, 384)]
+             (8192, 2304, 128), (5000, 4104, 4096), (1000, 17000, 384),
+             # split mode (at most half a round of tiles)
+             (4672, 1472, 6696), (2048, 2048, 4096), (280, 6352, 7568), (1000, 1000, 1000)]
 SHAPES_FP8 = [(256, 256, 256), (256, 512, 512), (512, 768, 768), (2304, 1536, 1280),
               (4096, 4352, 1024), (4096, 4096, 4096), (8192, 8192, 8192)]
 
@@ -79,7 +81,7 @@ def main():
         if v.startswith("pingpong8o"):
             shapes = SHAPES_PERSIST + (SHAPES_PERSIST_RAGGED if v in ("pingpong8om", "pingpong8omd") else [])
         if v.startswith("pingpong8s"):
-            shapes = SHAPES_SK
+            shapes = SHAPES_SK if v == "pingpong8s" else SHAPES_SK[:7]  # REV: two-round mode
         if splits > 1:
             shapes = SHAPES_SPLITK + SHAPES_RAGGED
         elif v in MASKED:

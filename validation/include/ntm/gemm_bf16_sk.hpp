@@ -71,20 +71,38 @@ struct SkArgs {
   int D;          // tiles run whole
   int Tp;         // K-tile pairs per tile
   int ntiles;
+  int S = 0;      // split mode (at most half a round of tiles): K slices per tile, else 0
   unsigned long long* stamps = nullptr;  // STAMP builds: 16 per workgroup
 };
 
-// Tiles, pairs and the whole-tile prefix for (M, N, K) on `cus` CUs. Stream-K
-// needs more tiles than CUs and a CU count that is a multiple of 8.
+// Tiles, pairs and the whole-tile prefix for (M, N, K) on `cus` CUs.
+// Two-round mode (S = 0): more tiles than CUs, not a multiple of them.
+// Split mode (S >= 2, gemm_bf16_sks_kernel): every XCD's tiles fit its CUs at
+// least twice over, so each tile is cut into S equal K slices and every slice
+// runs at once on its own CU (one round, slices at the same K offsets in
+// lockstep); S = the most slices that fit, at most kMaxSlices and one pair each.
+constexpr int kMaxSlices = 8;
+
 __host__ __device__ inline bool sk_decompose(int M, int N, int K, int cus, SkArgs& s) {
-  // one 4-byte counter per workgroup slot in the kCounterBytes block
+  // one 4-byte counter per workgroup slot (or per tile) in the kCounterBytes block
   if (M <= 0 || N <= 0 || K <= 0 || cus < 8 || (cus % 8) != 0 || cus > (int)(kCounterBytes / 4))
     return false;
   s.ntiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   s.G = cus;
-  if (s.ntiles <= s.G || (s.ntiles % s.G) == 0) return false;
-  s.D = (s.ntiles / s.G - 1) * s.G;
   s.Tp = (K + 2 * BK - 1) / (2 * BK);
+  s.S = 0;
+  if (s.ntiles <= s.G) {
+    const int per_xcd = (s.ntiles + 7) / 8, W = s.G / 8;
+    int S = W / per_xcd;
+    if (S > kMaxSlices) S = kMaxSlices;
+    if (S > s.Tp) S = s.Tp;
+    if (S < 2) return false;
+    s.S = S;
+    s.D = 0;
+    return true;
+  }
+  if ((s.ntiles % s.G) == 0) return false;
+  s.D = (s.ntiles / s.G - 1) * s.G;
   return true;
 }
 
@@ -353,6 +371,60 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_sk_kernel(GemmArgs p, S
   }
 }
 
+// Split mode ("pingpong8s" on at most half a round of tiles): XCD x's tiles
+// v = x + 8k (k < n_x), each in S K slices [s Tp / S, (s + 1) Tp / S) pairs;
+// workgroup j of the XCD runs slice j / n_x of tile k = j % n_x (the rest of
+// the XCD's workgroups exit at once). Every slice writes its fp32 partial
+// (write-through) and adds 1 to the tile's counter; the one that draws S - 1
+// sums the other S - 1 partials into its registers, stores C and resets the
+// counter. Nobody waits. C is the same whoever combines: it sums all S
+// partials from memory in slice order.
+template <bool TAIL>
+__global__ void __launch_bounds__(kThreads, 2) gemm_bf16_sks_kernel(GemmArgs p, SkArgs s) {
+  __shared__ __attribute__((aligned(16))) char smem[kLdsBytes3 + 16];  // ONE __shared__ array
+  int* bcast = (int*)(smem + kLdsBytes3);
+  const int b = (int)blockIdx.x;
+  const int x = b & 7, j = b >> 3;
+  const int nx = (s.ntiles - x + 7) >> 3;
+  if (nx <= 0 || j >= nx * s.S) return;  // uniform: the whole workgroup leaves
+  const int slice = j / nx, k = j - slice * nx;
+  const int tile = x + 8 * k;
+  Ctx c;
+  c.lds = smem;
+  const int lane = threadIdx.x & 63;
+  c.w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  c.wr = c.w >> 2;
+  c.wc = c.w & 3;
+  c.frag_off = (lane & 15) * 64 + ((lane >> 4) ^ ((lane >> 2) & 2)) * 16;
+  if constexpr (TAIL) {
+    c.K = p.K;
+    const int r = lane >> 2;
+    c.lane_col = ((lane & 3) ^ (((r >> 3) & 1) << 1)) * 8;
+  }
+  int tm, tn;
+  tile_coords_of<kGroupM>(tile, s.ntiles, p.M, p.N, tm, tn);
+  const int m0 = __builtin_amdgcn_readfirstlane(tm * BM);
+  const int n0 = __builtin_amdgcn_readfirstlane(tn * BN);
+  set_sources(p, c, m0, n0, lane_now());
+  Frags3 f;
+  f32x4 acc[2][2][4][2];
+  zero_acc(acc);
+  const int pa = slice * s.Tp / s.S, pb = (slice + 1) * s.Tp / s.S;
+  k_range<TAIL>(p, c, f, acc, 2 * pa, 2 * pb);
+  float* part = s.ws + (kCounterBytes + (size_t)tile * s.S * kPartialBytes) / 4;
+  unsigned* cnt = s.cnt + tile;
+  write_partial(part + (size_t)slice * (kPartialBytes / 4), acc);
+  const unsigned o = counter_add<true>(cnt, 1u, bcast);
+  if (o != (unsigned)(s.S - 1)) return;  // uniform
+  acquire_all();
+  // every slice's partial (its own too, already written) summed in slice order,
+  // so C does not depend on which slice combines (no second accumulator set)
+  zero_acc(acc);
+  for (int q = 0; q < s.S; ++q) add_partial(part + (size_t)q * (kPartialBytes / 4), acc);
+  reset_counter(cnt);
+  store_tile_epi<false, kEpiSk>(p, c, acc, m0, n0, lane_now());
+}
+
 // Launch on `cus` workgroups with the caller's workspace (sk_ws_bytes(cus)).
 // Its first kCounterBytes (the counters) must be zero on entry, and a completed
 // launch leaves them zero, so a caller zeroes a workspace once and then reuses
@@ -372,6 +444,14 @@ inline hipError_t launch_gemm_bf16_sk(const GemmArgs& a, int cus, void* ws, size
   s.stamps = stamps;
   if (STAMP && stamps == nullptr) return hipErrorInvalidValue;
   const dim3 g((unsigned)s.G), blk(kThreads);
+  if (s.S >= 2) {  // split mode (REV / STAMP do not apply)
+    if (REV || STAMP) return hipErrorInvalidValue;
+    if (a.K % (2 * BK))
+      hipLaunchKernelGGL((gemm_bf16_sks_kernel<true>), g, blk, 0, stream, a, s);
+    else
+      hipLaunchKernelGGL((gemm_bf16_sks_kernel<false>), g, blk, 0, stream, a, s);
+    return hipGetLastError();
+  }
   if (a.K % (2 * BK))
     hipLaunchKernelGGL((gemm_bf16_sk_kernel<true, REV, STAMP>), g, blk, 0, stream, a, s);
   else

@@ -171,6 +171,10 @@ static thread_local double g_plan_debug_unsplit_s = 0.0, g_plan_debug_sk_s = 0.0
 constexpr double kSkLoopFactor = 1.05;
 constexpr double kSkFixed = 30e-6;
 constexpr double kSkMargin = 1.0;
+// split mode (at most half a round of tiles, gemm_bf16_sks_kernel): every slice
+// writes a 256 KiB partial and the combiner reads all S of them
+constexpr double kSkSplitFixed = 12e-6;
+constexpr double kSkSplitPerSlice = 4e-6;
 
 // The plan: C split by rows into a top part and a rest part, each on one tile
 // kernel in its own launch (either part may be empty). The top part runs the
@@ -272,8 +276,14 @@ inline K1Plan plan_k1(int M, int N, int K, bool splitk = false, bool fp8 = false
   g_plan_debug_unsplit_s = unsplit;
   g_plan_debug_sk_s = 0.0;
   if (!fp8 && ntm::gemmsk::shape_ok_sk(M, N, K) && ntm::gemmsk::sk_decompose(M, N, K, (int)kCUs, sk)) {
-    const double rounds_sk = (double)(sk.ntiles - sk.D) / kCUs + sk.D / kCUs;
-    const double t_sk = kSkLoopFactor * rounds_sk * 4.0 * unit_s * (2.0 * sk.Tp * ntm::gemm::BK / K) + kSkFixed;
+    const double tile_s = 4.0 * unit_s * (2.0 * sk.Tp * ntm::gemm::BK / K);  // one 256x256 tile, K in pairs
+    double t_sk;
+    if (sk.S >= 2) {  // split mode: one slice of ceil(Tp / S) pairs per CU, one round
+      const double pairs = (double)((sk.Tp + sk.S - 1) / sk.S);
+      t_sk = kSkLoopFactor * pairs / sk.Tp * tile_s + kSkSplitFixed + kSkSplitPerSlice * sk.S;
+    } else {
+      t_sk = kSkLoopFactor * ((double)sk.ntiles / kCUs) * tile_s + kSkFixed;
+    }
     g_plan_debug_sk_s = t_sk;
     if (t_sk * kSkMargin < unsplit) {
       split = K1Plan{M, kStreamKVariant, kStreamKVariant, 1};
