@@ -132,7 +132,9 @@ def test_splitk_plan_keeps_unsplit_plan(k1_plan, splitk_plan, m, n, k):
 def test_splitk_plan_is_well_formed(k1_plan, splitk_plan, m, n, k):
     top, tv, rest, splits = splitk_plan(m, n, k)
     assert 1 <= splits <= 16
-    if splits > 1:   # all of C on one masked small tile; K slices of >= 64
+    if tv == "pingpong8s":   # stream-K (split mode here): all of C on the 256x256 kernel
+        assert top == m and rest == tv and splits == 1
+    elif splits > 1:   # all of C on one masked small tile; K slices of >= 64
         assert top == m and tv == rest
         assert tv in ("tile128", "tile256x128", "tile160", "tile160x128", "tile128x160")
         assert k // splits >= 32

@@ -43,6 +43,9 @@ ALLOWED_K1 = {
     # stream-K over the last two rounds of 256x256 tiles (pingpong8s <TAIL, REV, STAMP>)
     "ntm::gemmsk::gemm_bf16_sk_kernel<false, false, false>",
     "ntm::gemmsk::gemm_bf16_sk_kernel<true, false, false>",
+    # its split mode (at most half a round of tiles) <TAIL>
+    "ntm::gemmsk::gemm_bf16_sks_kernel<false>",
+    "ntm::gemmsk::gemm_bf16_sks_kernel<true>",
     "ntm::gemm2::gemm_bf16_pp2_kernel<false, 0>",
     "ntm::gemm2::gemm_bf16_pp2_kernel<false, 3>",
     "ntm::gemm2::gemm_bf16_pp2_kernel<true, 0>",
