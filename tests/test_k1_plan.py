@@ -118,13 +118,22 @@ def test_splitk_plan_for_skinny_long_k(splitk_plan, m, n, k, variant, splits):
     assert splitk_plan(m, n, k) == (m, variant, variant, splits)
 
 
-@pytest.mark.parametrize("m,n,k", [(8192, 8192, 8192), (4096, 4096, 4096), (5624, 752, 5880),
-                                   (4672, 1472, 6696), (1000, 3112, 768), (3200, 3200, 3200),
-                                   (6144, 6144, 6144), (2080, 3844, 256)])
+@pytest.mark.parametrize("m,n,k", [(8192, 8192, 8192), (4096, 4096, 4096), (1000, 3112, 768),
+                                   (3200, 3200, 3200), (6144, 6144, 6144), (2080, 3844, 256),
+                                   (2048, 2048, 4096), (3072, 2048, 6144), (8008, 536, 2896)])
 def test_splitk_plan_keeps_unsplit_plan(k1_plan, splitk_plan, m, n, k):
     """Chip-filling C or short K: split-K is not worth its fp32 partials, and the
     plan is exactly the unsplit one."""
     assert splitk_plan(m, n, k) == k1_plan(m, n, k) + (1,)
+
+
+@pytest.mark.parametrize("m,n,k", [(5624, 752, 5880), (4672, 1472, 6696), (1456, 2696, 10744),
+                                   (1872, 2224, 5208)])
+def test_splitk_plan_takes_stream_k_on_ragged_one_round_c(k1_plan, splitk_plan, m, n, k):
+    """One round of a small tile on ragged C runs 1.1-1.5x its modelled time;
+    stream-K's split mode measured 9-39 % faster there (profiles/r4_sks/)."""
+    assert k1_plan(m, n, k)[1].startswith("tile")
+    assert splitk_plan(m, n, k) == (m, "pingpong8s", "pingpong8s", 1)
 
 
 @pytest.mark.parametrize("m,n,k", [(m, n, k) for m in (64, 333, 1000, 2048)

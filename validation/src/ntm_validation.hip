@@ -117,6 +117,7 @@ struct SmallTile {
   bool masked;     // wave-specialised kernel: any M, N % 4, K % 8 (edge tiles / K tail masked)
   bool one_round;  // only where its tiles fit in one round of 256 CUs
   bool splitk;     // a split-K candidate (the split model was fitted without 128x256)
+  double ragged;   // measured / modelled time of one round on ragged C (stream-K pricing only)
 };
 // 160x128 / 128x160 are one-round tiles: filling a round the square tiles
 // leave part-idle they win 2-16 % (5624x752x5880, 4072x1240x3784, the rest
@@ -124,13 +125,17 @@ struct SmallTile {
 // one partial round, they lost 3-22 % (3000^3, 1344x6216x4848, 1616x6208x6504;
 // profiles/r2_tiles/plan_ab_*.log) - there the big kernel's partial round runs
 // faster per tile than the full-chip rate the model prices.
-constexpr SmallTile kSmallTiles[] = {{15, 128, 128, 0.60, true, false, true},
-                                     {16, 256, 128, 0.78, true, false, true},
-                                     {17, 160, 160, 0.72, true, false, true},
-                                     {23, 160, 128, 0.70, true, true, true},
-                                     {24, 128, 160, 0.70, true, true, true},
-                                     {26, 128, 256, 0.80, true, false, false},
-                                     {18, 256, 160, 0.61, false, false, false}};
+// `ragged`: one round of the tile on C with an edge tile row / column or K % 128
+// != 0 took 1.1-1.5x the modelled time on MI355X (20 one-round shapes,
+// profiles/r4_sks/split_sweep.log; exact shapes were within 0.93-1.02x). Only
+// the stream-K choice uses it: the tile choice itself was tuned with the model.
+constexpr SmallTile kSmallTiles[] = {{15, 128, 128, 0.60, true, false, true, 1.13},
+                                     {16, 256, 128, 0.78, true, false, true, 1.0},
+                                     {17, 160, 160, 0.72, true, false, true, 1.12},
+                                     {23, 160, 128, 0.70, true, true, true, 1.37},
+                                     {24, 128, 160, 0.70, true, true, true, 1.37},
+                                     {26, 128, 256, 0.80, true, false, false, 1.30},
+                                     {18, 256, 160, 0.61, false, false, false, 1.0}};
 constexpr double kSplitPenalty = 0.25;  // a second launch, in 128x128-tile-round units
 
 struct K1Plan {
@@ -285,7 +290,17 @@ inline K1Plan plan_k1(int M, int N, int K, bool splitk = false, bool fp8 = false
       t_sk = kSkLoopFactor * ((double)sk.ntiles / kCUs) * tile_s + kSkFixed;
     }
     g_plan_debug_sk_s = t_sk;
-    if (t_sk * kSkMargin < unsplit) {
+    // a single launch of one small tile in one round on ragged C runs slower
+    // than the model (SmallTile::ragged): price stream-K against the measured-ish time
+    double unsplit_vs_sk = unsplit;
+    if (best.top_rows == M && best.top_variant == best.rest_variant)
+      for (const SmallTile& st : kSmallTiles)
+        if (st.variant == best.top_variant &&
+            (double)((M + st.tm - 1) / st.tm) * ((N + st.tn - 1) / st.tn) <= kCUs &&
+            (M % st.tm != 0 || N % st.tn != 0 || K % 128 != 0))
+          unsplit_vs_sk *= st.ragged;
+    g_plan_debug_unsplit_s = unsplit_vs_sk;
+    if (t_sk * kSkMargin < unsplit_vs_sk) {
       split = K1Plan{M, kStreamKVariant, kStreamKVariant, 1};
       split.sk = true;
       best_t = t_sk * kSkMargin / kSplitKMargin;  // a split-K plan must beat stream-K too
