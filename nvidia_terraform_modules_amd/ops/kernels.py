@@ -35,7 +35,7 @@ GEMM_VARIANTS = {"default": 0, "pingpong8": 1, "pingpong8b": 4,
                  "pingpong8cwn": 12, "pingpong8cwne": 13, "tile128": 15,
                  "tile256x128": 16, "tile160": 17, "tile256x160": 18, "tile128w4": 19,
                  "tile256x128w4": 20, "tile160w4": 21, "pingpong8cm": 22, "tile160x128": 23,
-                 "tile128x160": 24, "tile128x256": 26, "dma4k_d3": 39, "pingpong8o": 25,
+                 "tile128x160": 24, "tile128x256": 26, "pingpong8o": 25,
                  "pp8o_g128": 41, "pp8o_g128_nostore": 42, "pp8o_nostore": 43,
                  "pingpong8om": 47, "pingpong8od": 48, "pingpong8s": 49,
                  "pingpong8omd": 51}
@@ -45,7 +45,7 @@ GEMM_VARIANTS = {"default": 0, "pingpong8": 1, "pingpong8b": 4,
 # by the default dispatch, not present in the shipping library or Job binary
 EXPERIMENTAL_VARIANTS = frozenset({"pingpong8", "pingpong8cw",
                                    "pingpong8cwe", "pingpong8cwn", "pingpong8cwne",
-                                   "tile128w4", "tile256x128w4", "tile160w4", "dma4k_d3",
+                                   "tile128w4", "tile256x128w4", "tile160w4",
                                    "pp8o_g128", "pp8o_g128_nostore", "pp8o_nostore",
                                    "pingpong8od", "pingpong8omd"})
 
@@ -126,9 +126,7 @@ def gemm_bf16(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
     and whole tiles) for small, mid-size and ragged C,
     else "pingpong8c" when K % 128 == 0, else "pingpong8b" (8 waves, two per SIMD, staggered, balanced 8/4/8/4 LDS read
     schedule; 8c adds parity-alternating B buffers and a tail-free K loop),
-    "pingpong8" (the first 12/4/8/0 schedule), or the experimental
-    "dma4k_d3" (4 waves, 128x128 per wave, one barrier per K-tile, LDS-DMA
-    operands) - see validation/include.
+    "pingpong8" (the first 12/4/8/0 schedule) - see validation/include.
     ``splits`` > 1 (masked tiles only): split-K into that many K slices, fp32
     partials in a workspace from PyTorch's allocator, then one reduction kernel.
     """

@@ -669,47 +669,6 @@ def test_gemm_fp8_plain_and_scaled_mfma_forms_agree_bitwise(ops):
     assert ((c0.float() - ref).abs() <= atol + rtol * ref.abs()).all()
 
 
-@pytest.mark.parametrize("variant", ["dma4k_d3"])
-@pytest.mark.parametrize("m,n,k", [(256, 256, 256), (512, 768, 384), (1024, 512, 1024),
-                                   (2048, 2048, 4096), (768, 1280, 640), (4608, 4608, 512),
-                                   (8192, 8192, 256), (2304, 1792, 768)])
-def test_round3_k1_experiments_vs_torch_fp32(ops, variant, m, n, k):
-    """Round-3 K1 experiment kept (profiles/r3_k1): the 4-wave 128x128-per-wave
-    kernel with one barrier per K-tile and two LDS-DMA K-tile buffers
-    (gemm_w4k.hpp): every even K-tile count from 4 (the peeled tail only) up,
-    vs fp32, and bitwise equal to the 8-wave default (same MFMA K order). Its
-    persistent overlap build (dma4ko) tied and was deleted in round 4."""
-    if k < 256 or k % 128:
-        pytest.skip("4-wave kernel: K % 128, K >= 256")
-    a = _rand(ops, (m, k), 571 + k)
-    b = _rand(ops, (n, k), 573 + n)
-    c = ops.gemm_bf16(a, b, variant=variant)
-    ref = a.float() @ b.float().T
-    atol, rtol = ops.gemm_tolerance(k)
-    err = (c.float() - ref).abs()
-    assert torch.all(err <= atol + rtol * ref.abs()), float(err.max())
-    assert torch.equal(c, ops.gemm_bf16(a, b, variant="pingpong8c"))
-
-
-@pytest.mark.parametrize("knob", [12])
-@pytest.mark.parametrize("m,n,k", [(256, 256, 512), (512, 768, 1024), (2048, 1024, 4096),
-                                   (4608, 4608, 512), (8192, 8192, 1024)])
-def test_fp8_dma4_vs_torch_fp32(ops, knob, m, n, k):
-    """K1-fp8 on the 4-wave one-barrier-per-K-tile kernel (knob 12, DMA every
-    2 MFMAs, gemm_w4k.hpp): vs the fp32 product of the e4m3 values, and
-    bitwise equal to the default 8-wave build (per accumulator the same f8f6f4
-    MFMAs in the same K order)."""
-    if k < 512 or k % 256:
-        pytest.skip("4-wave fp8 kernel: K % 256, K >= 512")
-    a = ops.fill_uniform_(torch.empty((m, k), dtype=torch.float8_e4m3fn, device="cuda"), 21)
-    b = ops.fill_uniform_(torch.empty((n, k), dtype=torch.float8_e4m3fn, device="cuda"), 22)
-    ck = ops.gemm_fp8(a, b, knob=knob)
-    ref = a.float() @ b.float().T
-    atol, rtol = ops.gemm_tolerance(k)
-    assert ((ck.float() - ref).abs() <= atol + rtol * ref.abs()).all()
-    assert torch.equal(ck.view(torch.int16), ops.gemm_fp8(a, b).view(torch.int16))
-
-
 @pytest.mark.parametrize("variant", ["pingpong8o", "pingpong8od"])
 @pytest.mark.parametrize("m,n,k", [(256, 256, 256), (1024, 512, 1024), (4608, 4608, 512),
                                    (8192, 8192, 256), (2304, 1792, 768)])

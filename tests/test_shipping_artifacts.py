@@ -110,6 +110,6 @@ def test_shipping_artifact_has_only_default_dispatch_k1(path):
 
 def test_experimental_library_holds_the_experiments():
     ks = _kernels(EXP)
-    for fam in ("gemm_w4k_kernel", "gemm_bf16_pp3_stamp_kernel", "mfma_rate_kernel",
+    for fam in ("gemm_bf16_pp3_stamp_kernel", "gemm_bf16_sk_kernel<false, true, false>", "mfma_rate_kernel",
                 "mfma_f8_probe_kernel"):
         assert any(fam in k for k in ks), fam

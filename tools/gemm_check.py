@@ -1,6 +1,6 @@
 """K1 numerics + throughput check on one MI355X (developer tool).
 
-    python tools/gemm_check.py [--sizes 4096,8192,6144x6144x8192] [--iters 50] [--variants default,dma4k_d3]
+    python tools/gemm_check.py [--sizes 4096,8192,6144x6144x8192] [--iters 50] [--variants default,pingpong8o]
 
 For every size: full verification of each variant against the independent
 fp32 reference kernel, then interleaved timing rounds of every variant and of
@@ -36,7 +36,7 @@ def main() -> int:
     ap.add_argument("--sizes", default="4096,8192")
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--rounds", type=int, default=5)
-    ap.add_argument("--variants", default="default,dma4k_d3")
+    ap.add_argument("--variants", default="default,pingpong8o")
     args = ap.parse_args()
     variants = args.variants.split(",")
     dev = torch.device("cuda:0")

@@ -7,7 +7,7 @@ fp8 GEMM through torch._scaled_mm (unit scales, bf16 out). One JSON line per
 size.
 
     python tools/gemm_fp8_check.py [--sizes 4096,8192,6144x8192x4096] [--iters 50] [--rounds 7]
-        [--knobs 12] [--variants tile256x128,tile128x256] [--no-bf16]
+        [--knobs 31] [--variants tile256x128,tile128x256] [--no-bf16]
 """
 from __future__ import annotations
 

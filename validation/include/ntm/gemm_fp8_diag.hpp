@@ -12,7 +12,6 @@
 #include "ntm/gemm_bf16_pp3.hpp"
 #include "ntm/gemm_fp8.hpp"
 #include "ntm/gemm_bf16_pp6.hpp"
-#include "ntm/gemm_w4k.hpp"
 
 namespace ntm {
 namespace fp8 {
@@ -27,7 +26,7 @@ __global__ void __launch_bounds__(64) mfma_f8_probe_kernel(const i32x8* a, const
 // 1 = B-fragment-outer MFMA order (scaled form); 2 = GROUP_M 4; 3 = static s_setprio(1) on
 // wave row 1; 4 = register (widened + nontemporal) epilogue instead of the
 // LDS-staged one; 5 = the scaled MFMA form with unit VGPR scales (the previous default;
-// knobs 1-4 use it too); 12 = the 4-wave one-barrier-per-K-tile kernel (gemm_w4k.hpp).
+// knobs 1-4 use it too). Knob 12 (the 4-wave dma4k kernel) was deleted in round 4.
 // Knobs 6-9 (persistent, early / register epilogues, GROUP_M 4 on
 // the plain form) measured 1-2 % slower or tied (profiles/r2_fp8ws/knobs_6_9.log) and were
 // deleted (git history).
@@ -59,8 +58,6 @@ inline hipError_t launch_gemm_fp8_knob(const void* A, const void* B, __bf16* C, 
     // 31: the same with the boundary stores spread over 7 phases (SPREAD, as the
     // shipping bf16 build)
     case 31: return ::ntm::gemm6::launch_gemm_fp8_pp6<true>(A, B, C, M, N, K, lda, ldb, ldc, s);
-    // 12: the 4-wave one-barrier-per-K-tile kernel, DMA every 2 MFMAs (gemm_w4k.hpp)
-    case 12: return ::ntm::w4k::launch_gemm_fp8_w4k<2>(A, B, C, M, N, K, lda, ldb, ldc, s);
     case 1: hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, kGroupM, false, kEpiDefault, 0, 2>), g, b, 0, s, a); break;
     case 2: hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, 4, false, kEpiDefault, 0, 1>), g, b, 0, s, a); break;
     case 3: hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, kGroupM, false, kEpiDefault, 2, 1>), g, b, 0, s, a); break;

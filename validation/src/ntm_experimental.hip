@@ -7,8 +7,6 @@
 //   1      pingpong8: the first 8-wave 12/4/8/0 LDS-read schedule (gemm_bf16.hpp)
 //   10..13 pingpong8c epilogue knobs: widened / + early row-0 stores /
 //          nontemporal stores / both (gemm_bf16_pp3.hpp launch_gemm_bf16_pp3_knob)
-//   39     dma4k_d3: 4 waves x 128x128, one barrier per K-tile, two K-tile
-//          LDS-DMA buffers (gemm_w4k.hpp)
 //   41..46 pingpong8o studies: 128 workgroups, C not stored, whole-line C
 //          layout (44), LDS-staged whole-line boundary stores (46)
 //   19..21 tile128w4 / tile256x128w4 / tile160w4: the 4-wave (one wave per
@@ -21,14 +19,15 @@
 // builds - profiles/r3_k1; the overlap kernel's sc1 / plain-store / static-
 // priority builds and pingpong8c's write-through epilogues - profiles/r3_k1o;
 // round 4: the 4-wave persistent overlap dma4ko / fp8 knob 22 (gemm_w4o.hpp,
-// profiles/r3_w4o) and the dma4k stamp build (gemm_r4k_stamp.hpp));
+// profiles/r3_w4o), the dma4k stamp build (gemm_r4k_stamp.hpp) and dma4k itself
+// (variant 39 / fp8 knob 12, gemm_w4k.hpp: 4 waves x 128x128 per wave, one
+// barrier per K-tile; it tied the 8-wave default, profiles/r3_k1));
 // what stays is used by a test or a tool under tools/.
 #include "ntm/gemm_bf16.hpp"
 #include "ntm/gemm_bf16_pp3.hpp"
 #include "ntm/gemm_bf16_pp3_stamp.hpp"
 #include "ntm/gemm_bf16_pp6.hpp"
 #include "ntm/gemm_bf16_sk.hpp"
-#include "ntm/gemm_w4k.hpp"
 #include "ntm/gemm_bf16_t128.hpp"
 #include "ntm/gemm_fp8_diag.hpp"
 #include "ntm/stream_policy_exp.hpp"
@@ -68,9 +67,6 @@ NTM_API int ntm_gemm_bf16_experimental(int variant, const void* A, const void* B
     case 19: return (int)ntm::gemmt::launch_gemm_bf16_tile<4>(a, S(stream));
     case 20: return (int)ntm::gemmt::launch_gemm_bf16_tile<8>(a, S(stream));
     case 21: return (int)ntm::gemmt::launch_gemm_bf16_tile<5, 5>(a, S(stream));
-    // 4 waves x 128x128, one barrier per K-tile, two K-tile LDS-DMA buffers,
-    // a DMA piece every 3 MFMA pairs (gemm_w4k.hpp)
-    case 39: return (int)ntm::w4k::launch_gemm_bf16_w4k<3>(a, S(stream));
     // store-bandwidth study (profiles/r3_stores): pingpong8o on 128 workgroups,
     // and with C not stored on 128 / 256 workgroups
     case 41: return (int)ntm::gemm6::launch_gemm_bf16_pp6_grid<1>(a, 128, S(stream));
