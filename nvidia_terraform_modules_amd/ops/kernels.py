@@ -143,10 +143,11 @@ def gemm_bf16(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
                              "(masked tiles: N % 4, K % 8; others: whole tiles, K % 128)")
     elif variant == "default":
         _default_ws_bytes(m, n, k)  # the native plan is the one authority on what it serves
-    elif variant in ("pingpong8s", "pingpong8s_rev"):  # stream-K: > 1 round of 256x256 tiles
+    elif variant in ("pingpong8s", "pingpong8s_rev"):  # stream-K (two-round or split mode)
         if not sk_ws_bytes(m, n, k):
-            raise ValueError(f"shape ({m},{n},{k}) not served by stream-K (N % 8, K % 8, K >= 128, "
-                             "more 256x256 tiles than CUs and not a multiple of them)")
+            raise ValueError(f"shape ({m},{n},{k}) not served by stream-K (N % 8, K % 8, K >= 128; "
+                             "256x256 tiles: more than the CUs and not a multiple of them, or "
+                             "few enough for >= 2 K slices per tile in one round)")
     elif variant in ("pingpong8cm", "pingpong8om", "pingpong8omd"):  # 256x256, masked edges (+ K tail)
         if not (m > 0 and n > 0 and n % 8 == 0 and k > 0 and k % 8 == 0):
             raise ValueError(f"shape ({m},{n},{k}) not served by {variant} (N % 8, K % 8)")
@@ -200,8 +201,9 @@ def gemm_bf16(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
 
 def sk_ws_bytes(m: int, n: int, k: int) -> int:
     """Workspace of the stream-K build ("pingpong8s") for (M, N, K) on this
-    device; 0 when it does not serve the shape (the 256x256 tile count is at
-    most one round of CUs or a multiple of them)."""
+    device; 0 when it does not serve the shape. It serves two-round mode (more
+    256x256 tiles than CUs, not a multiple of them) and split mode (each XCD's
+    tiles fit its CUs at least twice: S >= 2 K slices per tile, one round)."""
     if m <= 0 or n <= 0 or k <= 0:
         return 0
     return int(lib().ntm_sk_ws_bytes(m, n, k))
