@@ -1,4 +1,5 @@
-// K1 "pingpong8s": stream-K over the last two rounds of 256x256 tiles.
+// K1 "pingpong8s": stream-K over the last two rounds of 256x256 tiles, and
+// (split mode, gemm_bf16_sks_kernel below) over at most half a round of them.
 //
 // Why: a 256x256 part whose tile count is not a multiple of the 256 CUs leaves
 // CUs idle in its last round. At 4472 x 5688 x 5832 (18 x 23 = 414 tiles) the
@@ -429,8 +430,8 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_sks_kernel(GemmArgs p, 
 // Its first kCounterBytes (the counters) must be zero on entry, and a completed
 // launch leaves them zero, so a caller zeroes a workspace once and then reuses
 // it for every stream-K launch on one stream (no per-call memset dispatch). Returns hipErrorInvalidValue
-// for shapes stream-K does not serve (tiles a multiple of the CUs, or at most
-// one round of them).
+// for shapes stream-K does not serve (sk_decompose: tiles a multiple of the
+// CUs, or one round of them with fewer than 2 K slices per tile).
 template <bool REV = false, bool STAMP = false>
 inline hipError_t launch_gemm_bf16_sk(const GemmArgs& a, int cus, void* ws, size_t ws_bytes,
                                       hipStream_t stream, unsigned long long* stamps = nullptr) {

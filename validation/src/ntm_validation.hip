@@ -170,6 +170,10 @@ constexpr int kMaxSplits = 16;
 // plan_calibration.log). The unsplit plan's model leaves out per-tile fixed
 // costs, so it is optimistic; stream-K is chosen whenever its predicted time is
 // below the unsplit plan's (4 of 41 random shapes: measured +1 to +12 %).
+// Split mode (at most half a round of tiles, S K slices each): ceil(Tp / S)
+// pairs per CU plus the fix-up terms below, priced against the unsplit plan
+// scaled by SmallTile::ragged (profiles/r4_sks: 6 of 15 sweep shapes, +9 to
+// +39 % over the small tile).
 constexpr int kStreamKVariant = 49;
 // the last split-K plan's predicted unsplit / stream-K seconds (ntm_k1_plan_times)
 static thread_local double g_plan_debug_unsplit_s = 0.0, g_plan_debug_sk_s = 0.0;
