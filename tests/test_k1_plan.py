@@ -230,3 +230,11 @@ def test_k1_boxes_reports_median_over_boxes(tmp_path):
     r = k1_boxes.ratios(logs)
     rs = r[("8192", "pingpong8o")]
     assert len(rs) == 3 and abs(sorted(rs)[1] - 1.0) < 1e-12
+
+
+@pytest.mark.parametrize("m,n,k", [(8008, 536, 2896), (4152, 1096, 16056), (1456, 2696, 10744)])
+def test_plan_tie_prefers_fewer_tiles(k1_plan, m, n, k):
+    """160x128 and 128x160 have the same modelled one-round cost; the one whose
+    tiles span less of C won on every measured shape where the counts differ
+    (profiles/r4_tiles: 8008x536x2896 34.8 vs 39.4 us)."""
+    assert k1_plan(m, n, k) == (m, "tile128x160", "tile128x160")

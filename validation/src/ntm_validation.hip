@@ -192,7 +192,11 @@ constexpr double kSkSplitPerSlice = 4e-6;
 // shape cannot: 3200^3 = 1920 rows of 160x160 (240 tiles) + 1280 rows of
 // 128x128 (250 tiles), two full rounds instead of 1.56 rounds of 160x160
 // (977 vs 924 TF/s, hipBLASLt 948: profiles/r2_ws/split_3200.log).
-// Ties: fewer launches, then more rows on the 256x256 kernel.
+// Ties: fewer launches, then more rows on the 256x256 kernel, then (one
+// launch) less of C covered by tiles (edge waste): in one round, 128x160 beat 160x128 (equal
+// modelled cost) wherever it had fewer tiles, by 2-13 % (8008x536x2896: 252 vs
+// 255 tiles, 34.8 vs 39.4 us; 4152x1096x16056, 1456x2696x10744), and tied
+// where the counts were equal (profiles/r4_tiles).
 // fp8 (K1-fp8's plan): K counted in bf16-sized pairs of e4m3 values (a K-tile
 // costs the same cycles in both dtypes); only the tiles with an fp8 build - the
 // 256x256 kernel and the wave-specialised ones - and no split-K.
@@ -210,6 +214,7 @@ inline K1Plan plan_k1(int M, int N, int K, bool splitk = false, bool fp8 = false
   K1Plan best{-1, 15, 15};
   double best_cost = inf;
   int best_launches = 3, best_big_rows = -1;
+  double best_cover = inf;
   if (M <= 0 || N <= 0 || K <= 0) return best;
   auto small_ok = [&](const SmallTile& st, int rows) {  // masked: any M, N % 4, K % 8
     if (fp8 && !st.masked) return false;
@@ -246,14 +251,22 @@ inline K1Plan plan_k1(int M, int N, int K, bool splitk = false, bool fp8 = false
           continue;
         const int launches = rest > 0 ? 2 : 1;
         const int big_rows = t < 0 ? m1 : 0;
+        auto cover = [&](int tmc, int tnc, int rows) {  // elements of C the tiles span
+          return rows <= 0 ? 0.0 : (double)((rows + tmc - 1) / tmc) * ((N + tnc - 1) / tnc) * tmc * tnc;
+        };
+        const double cov = (t < 0 ? cover(256, 256, m1) : cover(tm, kSmallTiles[t].tn, m1)) +
+                           (rest > 0 ? cover(kSmallTiles[r].tm, kSmallTiles[r].tn, rest) : 0.0);
         const bool better = cost < best_cost - 1e-9 ||
                             (cost <= best_cost + 1e-9 &&
                              (launches < best_launches ||
-                              (launches == best_launches && big_rows > best_big_rows)));
+                              (launches == best_launches &&
+                               (big_rows > best_big_rows ||
+                                (big_rows == best_big_rows && launches == 1 && cov < best_cover)))));
         if (better) {
           best_cost = cost;
           best_launches = launches;
           best_big_rows = big_rows;
+          best_cover = cov;
           best = K1Plan{m1, t < 0 ? (big_exact ? big_variant : 22) : kSmallTiles[t].variant,
                         rest > 0 ? kSmallTiles[r].variant : (t < 0 ? 15 : kSmallTiles[t].variant)};
         }
