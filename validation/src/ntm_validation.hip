@@ -131,7 +131,7 @@ struct SmallTile {
 // the stream-K choice uses it: the tile choice itself was tuned with the model.
 constexpr SmallTile kSmallTiles[] = {{15, 128, 128, 0.60, true, false, true, 1.13},
                                      {16, 256, 128, 0.78, true, false, true, 1.0},
-                                     {17, 160, 160, 0.72, true, false, true, 1.12},
+                                     {17, 160, 160, 0.72, true, false, true, 1.17},
                                      {23, 160, 128, 0.70, true, true, true, 1.37},
                                      {24, 128, 160, 0.70, true, true, true, 1.37},
                                      {26, 128, 256, 0.80, true, false, false, 1.30},
@@ -180,10 +180,15 @@ static thread_local double g_plan_debug_unsplit_s = 0.0, g_plan_debug_sk_s = 0.0
 constexpr double kSkLoopFactor = 1.05;
 constexpr double kSkFixed = 30e-6;
 constexpr double kSkMargin = 1.0;
-// split mode (at most half a round of tiles, gemm_bf16_sks_kernel): every slice
-// writes a 256 KiB partial and the combiner reads all S of them
-constexpr double kSkSplitFixed = 12e-6;
-constexpr double kSkSplitPerSlice = 4e-6;
+// split mode (at most half a round of tiles, gemm_bf16_sks_kernel): the K loop
+// of ceil(Tp / S) pairs at the data-parallel rate, plus the fix-up. Every one of
+// the P = tiles x S slices writes a 256 KiB partial (the write phase grows with
+// P) and each combiner reads S of them (grows with S): fitted over 16 measured
+// shapes, S = 2..8, P = 128..256, rms 4 us (profiles/r4_sks, r4_tiles).
+constexpr double kSkSplitFixed = -18e-6;
+constexpr double kSkSplitPerPartial = 0.15e-6;
+constexpr double kSkSplitPerSlice = 3.4e-6;
+constexpr double kSkSplitMinFixup = 8e-6;
 
 // The plan: C split by rows into a top part and a rest part, each on one tile
 // kernel in its own launch (either part may be empty). The top part runs the
@@ -302,7 +307,8 @@ inline K1Plan plan_k1(int M, int N, int K, bool splitk = false, bool fp8 = false
     double t_sk;
     if (sk.S >= 2) {  // split mode: one slice of ceil(Tp / S) pairs per CU, one round
       const double pairs = (double)((sk.Tp + sk.S - 1) / sk.S);
-      t_sk = kSkLoopFactor * pairs / sk.Tp * tile_s + kSkSplitFixed + kSkSplitPerSlice * sk.S;
+      const double fixup = kSkSplitFixed + kSkSplitPerPartial * sk.ntiles * sk.S + kSkSplitPerSlice * sk.S;
+      t_sk = pairs / sk.Tp * tile_s + (fixup > kSkSplitMinFixup ? fixup : kSkSplitMinFixup);
     } else {
       t_sk = kSkLoopFactor * ((double)sk.ntiles / kCUs) * tile_s + kSkFixed;
     }
