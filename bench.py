@@ -427,7 +427,7 @@ def main(argv=None) -> int:
                 extras["xgmi_error"] = err or "set-up failed on another rank"
                 verified = False
                 if ar is not None:
-                    ar.close()
+                    ar.close(sync_peers=False)  # peers without a communicator do not call
             else:
                 xr = coll.all_reduce_sweep(env, xs, dtype="bf16", iters=10, warmup=2, impl=ar)
                 extras["xgmi_allreduce_bf16"] = [

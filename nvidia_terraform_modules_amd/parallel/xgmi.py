@@ -272,13 +272,25 @@ class XgmiAllReduce:
                                f"in the {self.PHASES.get(code, str(code))} phase "
                                f"(a peer never arrived); {what}")
 
-    def close(self) -> None:
+    def close(self, sync_peers: bool = True) -> None:
+        """Release the peers' mappings, then this rank's buffers. Collective
+        (``sync_peers``): no rank frees an exported buffer before every peer has
+        closed its mapping of it. Freeing early let the next set-up's
+        hipIpcGetMemHandle fail ("invalid argument") on a rank whose new
+        allocation reused a still-imported range (tune's back-to-back
+        communicators at world 8). ``sync_peers=False`` only on error paths
+        where the peers may not all call close."""
+        from .dist import barrier
+
         torch.cuda.synchronize()
         for p in self._opened:
             self.L.ntm_ipc_close(p)
+        self._opened = []
+        if sync_peers and self.env.world_size > 1:
+            barrier(self.env)
         for p in self._own:
             self.L.ntm_free(p)
-        self._opened, self._own = [], []
+        self._own = []
 
 
 def _copy_d2d(dst: int, src: int, nbytes: int) -> None:
@@ -309,7 +321,7 @@ class ReferenceAllReduce:
     def timed_out(self) -> bool:
         return False
 
-    def close(self) -> None:
+    def close(self, sync_peers: bool = True) -> None:
         pass
 
 
