@@ -838,11 +838,13 @@ def test_stream_k_counters_left_zero_and_refusals(ops):
         ops.gemm_bf16(a[:4096, :4096], b[:4096, :4096], variant="pingpong8s")
 
 
-@pytest.mark.parametrize("m,n,k", [(4864, 3608, 5696), (6496, 2752, 5416)])
+@pytest.mark.parametrize("m,n,k", [(4864, 3608, 5696), (6496, 2752, 5416),
+                                   (4672, 1472, 6696), (976, 5712, 9680)])
 def test_default_plan_runs_stream_k(ops, m, n, k):
     """Where the split-K plan prices stream-K below the unsplit plan (a small
-    partial second round at long K), the default dispatch runs it: same bytes
-    as pingpong8s, within tolerance of the fp32 product."""
+    partial second round at long K; split mode on ragged one-round C, the last
+    two shapes), the default dispatch runs it: same bytes as pingpong8s, within
+    tolerance of the fp32 product."""
     assert ops.k1_splitk_plan(m, n, k)[1] == "pingpong8s"
     a = _rand(ops, (m, k), 671)
     b = _rand(ops, (n, k), 673)
