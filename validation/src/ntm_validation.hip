@@ -323,7 +323,11 @@ inline K1Plan plan_k1(int M, int N, int K, bool splitk = false, bool fp8 = false
             (M % st.tm != 0 || N % st.tn != 0 || K % 128 != 0))
           // rows of A / B at least 64-byte aligned (K % 32 == 0): a third of it
           // (4704, 6240, 10720: 1.00-1.16 where 16 / 32-byte rows gave 1.1-1.5)
-          unsplit_vs_sk *= K % 32 == 0 ? 1.0 + (st.ragged - 1.0) * 0.4 : st.ragged;
+          // and 16-byte rows (K % 16 == 8) at least 1.25 (128x128 1.26 / 1.27,
+          // 160x160 1.11 / 1.35 measured)
+          unsplit_vs_sk *= K % 32 == 0   ? 1.0 + (st.ragged - 1.0) * 0.4
+                           : K % 16 == 8 ? (st.ragged > 1.0 && st.ragged < 1.25 ? 1.25 : st.ragged)
+                                         : st.ragged;
     g_plan_debug_unsplit_s = unsplit_vs_sk;
     if (t_sk * kSkMargin < unsplit_vs_sk) {
       split = K1Plan{M, kStreamKVariant, kStreamKVariant, 1};
