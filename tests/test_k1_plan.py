@@ -238,3 +238,22 @@ def test_plan_tie_prefers_fewer_tiles(k1_plan, m, n, k):
     tiles span less of C won on every measured shape where the counts differ
     (profiles/r4_tiles: 8008x536x2896 34.8 vs 39.4 us)."""
     assert k1_plan(m, n, k) == (m, "tile128x160", "tile128x160")
+
+
+@pytest.mark.parametrize("m,n,k,served", [
+    (4472, 5688, 5832, True),    # 414 tiles: two-round mode (1.6 rounds)
+    (4672, 1472, 6696, True),    # 114 tiles: split mode, 2 K slices
+    (1000, 1000, 1000, True),    # 16 tiles: split mode, 8 slices of one pair
+    (256, 256, 256, True),       # 1 tile: 2 slices of one pair
+    (4096, 4096, 4096, False),   # 256 tiles: exactly one round, nothing to balance
+    (8192, 8192, 8192, False),   # 1024 tiles: a multiple of the CUs
+    (7472, 1280, 6024, False),   # 150 tiles: under 2 slices per tile fit one round
+    (256, 256, 128, False),      # one K pair: cannot split
+    (4096, 4100, 4096, False),   # N % 8 != 0
+])
+def test_stream_k_decomposition_serves(k1_plan, m, n, k, served):
+    """sk_decompose (gemm_bf16_sk.hpp), seen through the host-side workspace
+    query: which shapes stream-K's two-round and split modes serve."""
+    from nvidia_terraform_modules_amd import ops
+
+    assert (ops.sk_ws_bytes(m, n, k) > 0) == served
