@@ -48,6 +48,10 @@ SHAPES_SK = [(4472, 5688, 5832), (4608, 4608, 1024), (6144, 6144, 2048), (4472, 
              (8192, 2304, 128), (5000, 4104, 4096), (1000, 17000, 384),
              # split mode (at most half a round of tiles)
              (4672, 1472, 6696), (2048, 2048, 4096), (280, 6352, 7568), (1000, 1000, 1000)]
+# shapes where the default plan runs stream-K (two-round / split mode) or a
+# split-K small tile picked by the ragged-C pricing (profiles/r4_sks)
+SHAPES_DEFAULT_SK = [(4672, 1472, 6696), (976, 5712, 9680), (4064, 1312, 5448),
+                     (1360, 2216, 6328), (384, 7648, 6744)]
 SHAPES_FP8 = [(256, 256, 256), (256, 512, 512), (512, 768, 768), (2304, 1536, 1280),
               (4096, 4352, 1024), (4096, 4096, 4096), (8192, 8192, 8192)]
 
@@ -85,7 +89,7 @@ def main():
         if splits > 1:
             shapes = SHAPES_SPLITK + SHAPES_RAGGED
         elif v in MASKED:
-            shapes = shapes + SHAPES_RAGGED + (SHAPES_SPLITK if v == "default" else [])
+            shapes = shapes + SHAPES_RAGGED + (SHAPES_SPLITK + SHAPES_DEFAULT_SK if v == "default" else [])
         for (m, n, k) in shapes:
             if fp8 and not ops.gemm_fp8_shape_ok(m, n, k):
                 continue
