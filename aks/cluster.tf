@@ -59,7 +59,7 @@ resource "azurerm_kubernetes_cluster_node_pool" "mi355x" {
   # + the startup taint the node-prep DaemonSet removes after a verified prep
   node_taints = concat(["amd.com/gpu=present:NoSchedule"],
   var.gpu_node_prep_taint ? ["${local.prep_taint_key}=pending:NoSchedule"] : [])
-  tags                  = local.tags
+  tags = local.tags
   node_labels = {
     "node.kubernetes.io/pool" = "gpu"
     "amd.com/gpu.present"     = "true"

@@ -185,5 +185,5 @@ variable "gpu_node_iommu_passthrough" {
 variable "gpu_node_prep_taint" {
   type        = bool
   default     = true
-  description = "GPU nodes join with the startup taint startup-taint.cluster-autoscaler.kubernetes.io/amd-mi355x-prep=pending:NoSchedule, which the node-prep DaemonSet removes once the MI355X host prep is verified on the node (NUMA balancing off, containerd running with LimitMEMLOCK=infinity). The GPU stack tolerates it, the validation Job does not, so the Job never races the prep. A cloud operation that re-applies node-pool taints to existing nodes re-gates them: delete the node's mi355x-node-prep pod to run the gate again."
+  description = "GPU nodes join with the startup taint startup-taint.cluster-autoscaler.kubernetes.io/amd-mi355x-prep=pending:NoSchedule, which the node-prep DaemonSet removes once the MI355X host prep is verified on the node (NUMA balancing off, containerd running with LimitMEMLOCK=infinity). The GPU stack tolerates it, the validation Job does not, so the Job never races the prep. A cloud operation that re-applies the taint to a running node is undone by the prep pod's gate reconciler within 30 s, after the same verification."
 }

@@ -17,7 +17,7 @@ resource "terraform_data" "gpu_instance_type_guard" {
 locals {
   prep_taint_key = "startup-taint.cluster-autoscaler.kubernetes.io/amd-mi355x-prep"
   node_sgs       = local.byo_network ? var.additional_security_group_ids : []
-  node_key = var.ssh_key == "" ? null : var.ssh_key
+  node_key       = var.ssh_key == "" ? null : var.ssh_key
 
   # Host preparation for MI355X nodes, BEFORE the EKS bootstrap (kubelet and
   # every pod start with it in effect):

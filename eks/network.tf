@@ -28,11 +28,9 @@ module "vpc" {
 }
 
 locals {
-  byo_network = var.existing_vpc_details != null
-  vpc_id      = local.byo_network ? var.existing_vpc_details.vpc_id : module.vpc[0].vpc_id
-  node_subnets = (local.byo_network
-    ? var.existing_vpc_details.subnet_ids
-    : module.vpc[0].private_subnets)
+  byo_network  = var.existing_vpc_details != null
+  vpc_id       = local.byo_network ? var.existing_vpc_details.vpc_id : module.vpc[0].vpc_id
+  node_subnets = local.byo_network ? var.existing_vpc_details.subnet_ids : module.vpc[0].private_subnets
 
   # Nodes talk to each other on every protocol (RCCL's socket transport
   # between nodes when no RDMA fabric is attached; within one node the

@@ -19,8 +19,10 @@ locals {
   # a CRD cascades to every CR of that kind in the cluster.
   crd_cleanup_list = [
     for crd in var.gpu_operator_crds : crd
-    if (var.driver_enabled || !endswith(crd, ".kmm.sigs.x-k8s.io")) &&
-    (var.install_node_feature_discovery || !endswith(crd, ".nfd.k8s-sigs.io"))
+    if alltrue([
+      var.driver_enabled || !endswith(crd, ".kmm.sigs.x-k8s.io"),
+      var.install_node_feature_discovery || !endswith(crd, ".nfd.k8s-sigs.io"),
+    ])
   ]
 
   # the startup taint of not-yet-prepared GPU nodes (node-prep.tf): tolerated

@@ -23,21 +23,26 @@
   effect fails the readiness gate instead of passing it.
 
   Gate (node_prep_startup_taint): the GPU pools join with the startup taint
-  node_prep_taint_key=pending:NoSchedule. The prep pod's init chain is
-    prep    the script below (host namespaces);
-    verify  this pod sees the host PIDs: NUMA balancing is 0 and the RUNNING
-            containerd has "Max locked memory unlimited" - i.e. its queued
-            restart with the drop-in has happened, so every pod created from
-            now on inherits the limit. Fails (kubelet retries it with backoff)
-            until then;
-    taint   kubectl taint ... --overwrite (idempotent: makes the removal below
-            valid on a pod restart, when the taint is already gone);
-    untaint kubectl taint ... - (removes it).
+  node_prep_taint_key=pending:NoSchedule. The prep pod runs
+    prep    the script below (init container, host namespaces);
+    gate    a reconciler (main container, node_prep_gate_image: sh + kubectl)
+            that checks the node every node_prep_gate_interval_s seconds. When
+            the node carries the startup taint it verifies the prep - this
+            pod sees the host PIDs: NUMA balancing is 0 and the RUNNING
+            containerd has "Max locked memory unlimited", i.e. its restart
+            with the drop-in has happened, so every pod created from now on
+            inherits the limit - and only then removes the taint. A taint that
+            comes back (an EKS node-group update, AKS / GKE pool-taint
+            reconciliation) is removed again at the next check, after the same
+            verification: no human has to delete the pod.
   Only the GPU stack's own DaemonSets tolerate the startup taint, so the
   validation Job lands on a node only after a verified prep: no race with the
   containerd restart or the iommu reboot, no fail-and-retry. In "reboot" mode
   the prep step waits for the reboot it requested instead of exiting, so the
-  chain never reaches untaint before the reboot.
+  gate never starts before the reboot.
+  API access: the gate container alone mounts a (projected, short-lived)
+  service-account token - get + patch on nodes; the privileged prep container
+  gets none (automount is off for the pod).
 ********************************************/
 locals {
   node_prep_script = <<-EOT
@@ -50,13 +55,19 @@ locals {
     # 2. containerd LimitMEMLOCK=infinity (inherited by every container)
     dropin=/etc/systemd/system/containerd.service.d/60-memlock.conf
     want="$(printf '[Service]\nLimitMEMLOCK=infinity')"
-    restart=0
     if [ "$(cat "$dropin" 2>/dev/null || true)" != "$want" ]; then
       mkdir -p "$(dirname "$dropin")"
       printf '%s\n' "$want" > "$dropin"
-      systemctl daemon-reload
-      restart=1
     fi
+    # restart decided from the RUNNING containerd (what the gate checks), not
+    # from the file: a run that wrote the drop-in and lost its queued restart
+    # (killed pod, failed reload) must not leave the node gated forever
+    restart=0
+    for c in /proc/[0-9]*/comm; do
+      [ "$(cat "$c" 2>/dev/null)" = containerd ] || continue
+      grep -q '^Max locked memory *unlimited' "$${c%/comm}/limits" 2>/dev/null || restart=1
+    done
+    if [ "$restart" = 1 ]; then systemctl daemon-reload; fi
     # 3. iommu=pt (boot-time kernel argument)
     sentinel=/var/lib/mi355x-iommu-rebooted
     if grep -qw 'iommu=pt' /proc/cmdline; then
@@ -68,7 +79,7 @@ locals {
       mkdir -p /var/lib && touch "$sentinel"
       echo "mi355x: adding iommu=pt, rebooting once" >> "$log"
       systemctl --no-block reboot
-      # wait for the reboot: the init chain must not go on (and untaint the
+      # wait for the reboot: the gate must not start (and untaint the
       # node) before it; a reboot that never comes fails this step (retried)
       sleep 600
       exit 1
@@ -84,27 +95,47 @@ locals {
     if [ "$restart" = 1 ]; then systemctl --no-block restart containerd; fi
   EOT
 
-  # verify step (in the prep pod, hostPID): what the Job's --require-host-prep
-  # checks, read from the host - NUMA balancing, and the memlock limit of the
-  # containerd that creates the next pods
-  node_prep_verify_script = <<-EOT
+  # gate reconciler (the prep pod's main container, hostPID, sh + kubectl):
+  # what the Job's --require-host-prep checks, read from the host - NUMA
+  # balancing, and the memlock limit of the containerd that creates the next
+  # pods - gates the removal of the startup taint, re-checked every
+  # GATE_INTERVAL_S. PROC_ROOT / GATE_ONCE exist for the offline test
+  # (tests/test_node_prep_gate.py: fake /proc, stub kubectl).
+  node_prep_gate_script = <<-EOT
     set -u
-    nb="$(cat /proc/sys/kernel/numa_balancing 2>/dev/null || echo missing)"
-    if [ "$nb" != 0 ]; then echo "mi355x gate: kernel.numa_balancing=$nb, waiting"; exit 1; fi
-    found=0
-    for c in /proc/[0-9]*/comm; do
-      [ "$(cat "$c" 2>/dev/null)" = containerd ] || continue
-      found=1
-      d=$${c%/comm}
-      if ! grep -q '^Max locked memory *unlimited' "$d/limits" 2>/dev/null; then
-        echo "mi355x gate: containerd ($d) not yet running with LimitMEMLOCK=infinity, waiting"
-        exit 1
+    proc="$${PROC_ROOT:-/proc}"
+    verify() {
+      nb="$(cat "$proc/sys/kernel/numa_balancing" 2>/dev/null || echo missing)"
+      if [ "$nb" != 0 ]; then echo "mi355x gate: kernel.numa_balancing=$nb, waiting"; return 1; fi
+      found=0
+      for c in "$proc"/[0-9]*/comm; do
+        [ "$(cat "$c" 2>/dev/null)" = containerd ] || continue
+        found=1
+        d="$${c%/comm}"
+        if ! grep -q '^Max locked memory *unlimited' "$d/limits" 2>/dev/null; then
+          echo "mi355x gate: containerd ($d) not yet running with LimitMEMLOCK=infinity, waiting"
+          return 1
+        fi
+      done
+      if [ "$found" = 0 ]; then echo "mi355x gate: no containerd process visible, waiting"; return 1; fi
+      return 0
+    }
+    while :; do
+      if keys="$(kubectl get node "$NODE_NAME" -o jsonpath='{range .spec.taints[*]}{.key}{"\n"}{end}')"; then
+        if printf '%s\n' "$keys" | grep -qxF "$TAINT_KEY"; then
+          if verify; then
+            kubectl taint node "$NODE_NAME" "$TAINT_KEY:NoSchedule-" &&
+              echo "mi355x gate: host prep verified, $TAINT_KEY removed from $NODE_NAME"
+          fi
+        fi
+      else
+        echo "mi355x gate: cannot read node $NODE_NAME, retrying"
       fi
+      [ -n "$${GATE_ONCE:-}" ] && exit 0
+      sleep "$GATE_INTERVAL_S"
     done
-    if [ "$found" = 0 ]; then echo "mi355x gate: no containerd process visible, waiting"; exit 1; fi
-    echo "mi355x gate: host prep verified"
   EOT
-  prep_gate = var.node_prep_enabled && var.node_prep_startup_taint
+  prep_gate             = var.node_prep_enabled && var.node_prep_startup_taint
 }
 
 # The gate's API access: get + patch on Node objects, nothing else.
@@ -174,7 +205,7 @@ resource "kubernetes_daemon_set_v1" "node_prep" {
         priority_class_name             = "system-node-critical"
         node_selector                   = var.gpu_node_selector
         service_account_name            = local.prep_gate ? kubernetes_service_account_v1.node_prep[0].metadata[0].name : "default"
-        automount_service_account_token = local.prep_gate
+        automount_service_account_token = false
         toleration {
           key      = var.gpu_node_taint_key
           operator = "Exists"
@@ -196,31 +227,12 @@ resource "kubernetes_daemon_set_v1" "node_prep" {
             privileged = true
           }
         }
-        dynamic "init_container" {
-          for_each = local.prep_gate ? ["verify"] : []
+        dynamic "container" {
+          for_each = local.prep_gate ? ["gate"] : []
           content {
-            name    = "verify"
-            image   = var.node_prep_image
-            command = ["sh", "-c", local.node_prep_verify_script]
-            security_context {
-              allow_privilege_escalation = false
-              read_only_root_filesystem  = true
-            }
-          }
-        }
-        # ensure, then remove: both single kubectl calls (no shell in the
-        # image); "kubectl taint ... -" fails on an absent taint, the ensure
-        # step makes it present on every run
-        dynamic "init_container" {
-          for_each = local.prep_gate ? {
-            taint   = "${var.node_prep_taint_key}=pending:NoSchedule"
-            untaint = "${var.node_prep_taint_key}=pending:NoSchedule-"
-          } : {}
-          content {
-            name    = init_container.key
-            image   = var.kubectl_image
-            command = concat(["kubectl", "taint", "node", "$(NODE_NAME)", init_container.value],
-            init_container.key == "taint" ? ["--overwrite"] : [])
+            name    = "gate"
+            image   = var.node_prep_gate_image
+            command = ["sh", "-c", local.node_prep_gate_script]
             env {
               name = "NODE_NAME"
               value_from {
@@ -229,25 +241,103 @@ resource "kubernetes_daemon_set_v1" "node_prep" {
                 }
               }
             }
+            env {
+              name  = "TAINT_KEY"
+              value = var.node_prep_taint_key
+            }
+            env {
+              name  = "GATE_INTERVAL_S"
+              value = tostring(var.node_prep_gate_interval_s)
+            }
+            env {
+              # kubectl's discovery cache: the root filesystem is read-only
+              name  = "HOME"
+              value = "/tmp"
+            }
+            volume_mount {
+              name       = "gate-token"
+              mount_path = "/var/run/secrets/kubernetes.io/serviceaccount"
+              read_only  = true
+            }
+            volume_mount {
+              name       = "gate-tmp"
+              mount_path = "/tmp"
+            }
+            resources {
+              requests = { cpu = "5m", memory = "32Mi" }
+              limits   = { memory = "128Mi" }
+            }
             security_context {
               allow_privilege_escalation = false
+              read_only_root_filesystem  = true
               run_as_non_root            = true
               run_as_user                = 65532
+              capabilities {
+                drop = ["ALL"]
+              }
             }
           }
         }
-        container {
-          name  = "hold"
-          image = var.pause_image
-          resources {
-            requests = { cpu = "1m", memory = "8Mi" }
-            limits   = { memory = "16Mi" }
+        dynamic "container" {
+          for_each = local.prep_gate ? [] : ["hold"]
+          content {
+            name  = "hold"
+            image = var.pause_image
+            resources {
+              requests = { cpu = "1m", memory = "8Mi" }
+              limits   = { memory = "16Mi" }
+            }
+            security_context {
+              allow_privilege_escalation = false
+              read_only_root_filesystem  = true
+              capabilities {
+                drop = ["ALL"]
+              }
+            }
           }
-          security_context {
-            allow_privilege_escalation = false
-            read_only_root_filesystem  = true
-            capabilities {
-              drop = ["ALL"]
+        }
+        dynamic "volume" {
+          for_each = local.prep_gate ? ["gate-tmp"] : []
+          content {
+            name = volume.value
+            empty_dir {
+              size_limit = "16Mi"
+            }
+          }
+        }
+        # the gate's API token, for the gate container only (what automount
+        # would give every container: token, cluster CA, namespace)
+        dynamic "volume" {
+          for_each = local.prep_gate ? ["gate-token"] : []
+          content {
+            name = volume.value
+            projected {
+              default_mode = "0444"
+              sources {
+                service_account_token {
+                  path               = "token"
+                  expiration_seconds = 3607
+                }
+              }
+              sources {
+                config_map {
+                  name = "kube-root-ca.crt"
+                  items {
+                    key  = "ca.crt"
+                    path = "ca.crt"
+                  }
+                }
+              }
+              sources {
+                downward_api {
+                  items {
+                    path = "namespace"
+                    field_ref {
+                      field_path = "metadata.namespace"
+                    }
+                  }
+                }
+              }
             }
           }
         }

@@ -36,3 +36,17 @@ output "gpu_node_selector" {
   value       = var.gpu_node_selector
   description = "Labels that select MI355X nodes."
 }
+
+output "node_prep_gate" {
+  value = local.prep_gate ? {
+    taint_key            = var.node_prep_taint_key
+    reconcile_interval_s = var.node_prep_gate_interval_s
+    image                = var.node_prep_gate_image
+  } : null
+  description = "The node-prep startup-taint gate (node_prep_startup_taint): the taint its reconciler removes from each GPU node after verifying the host prep, and how often it re-checks; null when off."
+
+  precondition {
+    condition     = !var.node_prep_startup_taint || var.node_prep_enabled
+    error_message = "node_prep_startup_taint needs node_prep_enabled: the node-prep DaemonSet is what removes the startup taint, and without it every GPU node would stay NoSchedule for the validation Job and every workload."
+  }
+}

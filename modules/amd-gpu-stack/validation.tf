@@ -11,37 +11,40 @@
   time-to-GPU-ready.
 ********************************************/
 locals {
-  validation_args = concat([
-    "--gpus", tostring(var.validation_gpu_count),
-    "--size", tostring(var.validation_gemm_size),
-    "--tflops-floor", tostring(var.validation_tflops_floor),
-    "--min-hbm-gb", tostring(var.validation_min_hbm_gb),
-    "--allreduce-max-mib", tostring(var.validation_allreduce_max_mib),
-    "--json",
-  ], var.validation_fp8 ? [
-    "--fp8-tflops-floor", tostring(var.validation_fp8_tflops_floor),
-  ] : ["--no-fp8"], var.validation_p2p_floor_gbps > 0 ? [
-    "--p2p-floor-gbps", tostring(var.validation_p2p_floor_gbps),
-  ] : [], var.validation_gpu_count > 1 && var.validation_rccl_busbw_floor_gbps > 0 ? [
-    "--rccl-busbw-floor-gbps", tostring(var.validation_rccl_busbw_floor_gbps),
-  ] : [], var.validation_gpu_count > 1 && var.validation_xgmi_busbw_floor_gbps > 0 ? [
-    "--xgmi-busbw-floor-gbps", tostring(var.validation_xgmi_busbw_floor_gbps),
-  ] : [], var.validation_gpu_count > 1 ? [
+  validation_multi_gpu = var.validation_gpu_count > 1
+  validation_args = concat(
+    [
+      "--gpus", tostring(var.validation_gpu_count),
+      "--size", tostring(var.validation_gemm_size),
+      "--tflops-floor", tostring(var.validation_tflops_floor),
+      "--min-hbm-gb", tostring(var.validation_min_hbm_gb),
+      "--allreduce-max-mib", tostring(var.validation_allreduce_max_mib),
+      "--json",
+    ],
+    var.validation_fp8 ? [
+      "--fp8-tflops-floor", tostring(var.validation_fp8_tflops_floor),
+    ] : ["--no-fp8"],
+    var.validation_p2p_floor_gbps > 0 ? [
+      "--p2p-floor-gbps", tostring(var.validation_p2p_floor_gbps),
+    ] : [],
+    local.validation_multi_gpu && var.validation_rccl_busbw_floor_gbps > 0 ? [
+      "--rccl-busbw-floor-gbps", tostring(var.validation_rccl_busbw_floor_gbps),
+    ] : [],
+    local.validation_multi_gpu && var.validation_xgmi_busbw_floor_gbps > 0 ? [
+      "--xgmi-busbw-floor-gbps", tostring(var.validation_xgmi_busbw_floor_gbps),
+    ] : [],
     # the hand-written all-reduce runs in the configuration a mini-sweep picks
     # (blocks per rank x one-shot cutoff, well under 2 s at 8 GPUs)
-    "--xgmi-tune",
-  ] : [], var.node_prep_enabled && var.validation_require_host_prep ? [
-    "--require-host-prep",
-  ] : [], var.validation_require_iommu_pt ? [
-    "--require-iommu-pt",
-  ] : [], [
+    local.validation_multi_gpu ? ["--xgmi-tune"] : [],
+    var.node_prep_enabled && var.validation_require_host_prep ? ["--require-host-prep"] : [],
+    var.validation_require_iommu_pt ? ["--require-iommu-pt"] : [],
     # one-line verdict surfaced as the pod's termination message
-    "--termination-log", "/dev/termination-log",
-  ])
+    ["--termination-log", "/dev/termination-log"],
+  )
   validation_env = merge({
     # RCCL over the xGMI mesh inside one node; no host network transport needed
-    NCCL_IB_DISABLE      = "1"
-    NCCL_SOCKET_IFNAME   = "lo"
+    NCCL_IB_DISABLE        = "1"
+    NCCL_SOCKET_IFNAME     = "lo"
     HSA_NO_SCRATCH_RECLAIM = "1"
   }, var.validation_env)
 }

@@ -358,6 +358,23 @@ variable "node_prep_iommu_mode" {
   }
 }
 
+variable "node_prep_gate_image" {
+  type        = string
+  default     = "docker.io/alpine/k8s:1.31.4"
+  description = "Image of the node-prep startup-taint gate (node_prep_startup_taint): a long-running reconciler loop, so it needs a POSIX shell and kubectl in one image (registry.k8s.io/kubectl has no shell). Pulled when a GPU node joins: mirror it for air-gapped clusters."
+}
+
+variable "node_prep_gate_interval_s" {
+  type        = number
+  default     = 30
+  description = "Seconds between the gate's checks of its node: a startup taint that a cloud reconciler re-applies (node-group update, pool-taint reconciliation) is removed again, after re-verifying the host prep, within this interval."
+
+  validation {
+    condition     = var.node_prep_gate_interval_s >= 5 && var.node_prep_gate_interval_s <= 600
+    error_message = "node_prep_gate_interval_s must be between 5 and 600 seconds."
+  }
+}
+
 variable "node_prep_image" {
   type        = string
   default     = "docker.io/library/ubuntu:22.04"

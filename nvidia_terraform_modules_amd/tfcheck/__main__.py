@@ -6,7 +6,7 @@ checks, and (``--contract FIXTURE``) diffs the call surface against the
 reference. Exit status 1 on any error finding.
 
 This is the offline stand-in for ``terraform fmt -check && terraform
-validate`` (CONTRIBUTING.md in the reference asks for both, manually); it
+validate`` (``--fmt-write`` is ``terraform fmt -recursive``: tfcheck/fmt.py) (CONTRIBUTING.md in the reference asks for both, manually); it
 does NOT validate provider schemas, which needs the network.
 """
 from __future__ import annotations
@@ -28,6 +28,9 @@ def main(argv=None) -> int:
     ap.add_argument("dirs", nargs="*", default=["."])
     ap.add_argument("--no-vendor-lint", action="store_true")
     ap.add_argument("--no-fmt", action="store_true")
+    ap.add_argument("--fmt-write", action="store_true",
+                    help="rewrite every .tf / .tfvars under DIR in canonical layout "
+                         "(terraform fmt without -check) and exit")
     ap.add_argument("--warnings-as-errors", action="store_true")
     ap.add_argument("--contract", help="reference surface fixture (JSON) to diff against")
     ap.add_argument("--json", action="store_true")
@@ -77,6 +80,15 @@ def main(argv=None) -> int:
             print(f"{verb}: {m}")
         print(f"{len(stale)} README(s) {verb}")
         return 1 if (stale and args.docs_check) else 0
+
+    if args.fmt_write:
+        from .fmt import write_formatted
+
+        changed = [str(f) for d in args.dirs for f in write_formatted(Path(d))]
+        for f in changed:
+            print(f)
+        print(f"{len(changed)} file(s) reformatted")
+        return 0
 
     results = {}
     nerr = 0

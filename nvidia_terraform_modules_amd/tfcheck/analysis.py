@@ -55,7 +55,8 @@ import-target      an import block whose `to` is not a managed resource declared
                    configuration (a module call, a data source, or an address nothing
                    declares: "Configuration for import target does not exist"), or an import
                    block in a module that is not a root (Terraform accepts them only there)
-fmt                tabs / trailing whitespace (terraform fmt would rewrite)
+fmt                terraform fmt layout: indentation, spacing, = / comment alignment
+                   (errors); tabs / trailing whitespace (warnings)
 """
 from __future__ import annotations
 
@@ -758,13 +759,27 @@ def namespace_findings(mod: Module) -> list[Finding]:
 
 
 def fmt_findings(path: Path) -> list[Finding]:
+    """``terraform fmt -check`` offline: tabs and trailing whitespace (warnings)
+    plus every line whose indentation, spacing or ``=`` / comment alignment is
+    not the canonical layout (errors; tfcheck/fmt.py, ``--fmt-write`` fixes them)."""
+    from .fmt import FmtLexError, fmt_diff
+
     out = []
     for f in sorted(Path(path).glob("*.tf")) + sorted(Path(path).glob("*.tfvars")):
-        for i, line in enumerate(f.read_text().splitlines(), 1):
+        text = f.read_text()
+        for i, line in enumerate(text.splitlines(), 1):
             if "\t" in line:
                 out.append(Finding("fmt", "warning", f"{f.name}:{i}", "tab character"))
             if line != line.rstrip():
                 out.append(Finding("fmt", "warning", f"{f.name}:{i}", "trailing whitespace"))
+        try:
+            diff = fmt_diff(text)
+        except FmtLexError as e:
+            out.append(Finding("fmt", "error", f.name, f"cannot lay out: {e}"))
+            continue
+        for i, have, want in diff:
+            out.append(Finding("fmt", "error", f"{f.name}:{i}",
+                               f"terraform fmt would rewrite {have.strip()!r} as {want!r}"))
     return out
 
 

@@ -11,7 +11,8 @@ not need providers, in Terraform's order:
 2. ``count`` / ``for_each`` of every resource, data source and module call,
    expanded into instance addresses; an argument that is only known after
    apply is the same error Terraform reports ("Invalid count argument");
-3. resource ``lifecycle { precondition }`` blocks that are decidable;
+3. resource ``lifecycle { precondition }`` and output ``precondition``
+   blocks that are decidable;
 4. recursion into LOCAL child modules with their evaluated inputs (registry
    modules are listed, not expanded: their source is not vendored).
 
@@ -190,6 +191,18 @@ def _plan_module(mod: Module, inputs: dict, prefix: str, res: PlanResult, ev: Ev
                         continue
                     if c is False:
                         res.errors.append(f"Resource precondition failed: {inst}: {_msg(pc)}")
+
+    # 2b. output preconditions (Terraform checks them at plan time too)
+    for name, o in mod.outputs.items():
+        for pc in o.block.body.blocks_of("precondition"):
+            try:
+                c = ev.eval(pc.body.attr("condition"), scope)
+            except EvalError as x:
+                res.errors.append(f"{prefix}output.{name}: precondition failed to evaluate: {x}")
+                continue
+            if c is False:
+                res.errors.append(f"Module output precondition failed: {prefix}output.{name}: "
+                                  f"{_msg(pc)}")
 
     # 3. module calls
     for name, mc in mod.modules.items():

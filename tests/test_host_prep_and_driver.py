@@ -282,31 +282,19 @@ def test_only_the_gpu_stack_tolerates_the_startup_taint():
     assert not [f for f in analyze(stack) if f.rule == "gpu-toleration"]
 
 
-def test_prep_gate_init_chain_and_rbac():
+def test_prep_gate_rbac_and_reboot_wait():
+    """The gate itself (reconciler container, fake-/proc runs) is covered by
+    tests/test_node_prep_gate.py; here: it is on with the startup taint, its
+    verification reads what the Job checks, the reboot path never lets it start
+    first, and its RBAC is get + patch on nodes only."""
     stack = load_module(ROOT / "modules" / "amd-gpu-stack")
-    spec = _pod_spec(stack.resources["kubernetes_daemon_set_v1.node_prep"])
-    names = [render(b.body.attr("name")) for b in _blocks(spec, "init_container")]
-    dyn = [b for b in _blocks(spec, "dynamic") if b.labels == ["init_container"]]
-    assert names == ['"prep"'] and len(dyn) == 2
     assert _stack_local("prep_gate", node_prep_startup_taint=True) is True
-    verify_fe = _eval(ROOT / "modules" / "amd-gpu-stack", dyn[0].body.attr("for_each"),
-                      node_prep_startup_taint=True)
-    taint_fe = _eval(ROOT / "modules" / "amd-gpu-stack", dyn[1].body.attr("for_each"),
-                     node_prep_startup_taint=True)
-    assert verify_fe == ["verify"]
-    # ensure-then-remove, in that (lexical) order; both single kubectl calls
-    assert list(taint_fe) == ["taint", "untaint"]
-    assert taint_fe["taint"] == f"{PREP}=pending:NoSchedule"
-    assert taint_fe["untaint"] == f"{PREP}=pending:NoSchedule-"
-    cmd = render(_blocks(dyn[1].body, "content")[0].body.attr("command"))
-    assert '"kubectl", "taint", "node", "$(NODE_NAME)"' in cmd and '"--overwrite"' in cmd
-    # verify reads what the Job checks: NUMA balancing and the running containerd's memlock
-    v = "".join(p for p in stack.locals["node_prep_verify_script"][0].parts if isinstance(p, str))
-    assert "/proc/sys/kernel/numa_balancing" in v and "Max locked memory *unlimited" in v
-    # the reboot path waits for the reboot instead of letting the chain untaint first
+    assert _stack_local("prep_gate") is False
+    v = "".join(p for p in stack.locals["node_prep_gate_script"][0].parts if isinstance(p, str))
+    assert "/sys/kernel/numa_balancing" in v and "Max locked memory *unlimited" in v
+    # the reboot path waits for the reboot instead of letting the gate start first
     s = "".join(p for p in stack.locals["node_prep_script"][0].parts if isinstance(p, str))
     assert s.index("systemctl --no-block reboot") < s.index("sleep 600") < s.index("exit 1")
-    # RBAC: get + patch on nodes, nothing else
     role = stack.resources["kubernetes_cluster_role_v1.node_prep"].block.body
     rules = _blocks(role, "rule")
     assert len(rules) == 1
