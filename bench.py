@@ -214,6 +214,7 @@ def main(argv=None) -> int:
     import torch
 
     from nvidia_terraform_modules_amd.models.validation_job import GemmWorkload, hbm_check
+    from nvidia_terraform_modules_amd.ops import smi
     from nvidia_terraform_modules_amd.parallel import collectives as coll
     from nvidia_terraform_modules_amd.parallel import dist
 
@@ -251,9 +252,12 @@ def main(argv=None) -> int:
     # timed window of a short run lands on the transient.
     prewarm = prewarm_settle(wl.step, sync, args.prewarm_s)
 
-    # ---- warmup (untimed): exactly W steps
+    # ---- warmup (untimed): exactly W steps. The power / throttle sample that opens
+    # the telemetry window is read while the last warmup launches still run, so it
+    # adds no idle gap (an idle GPU re-boosts and overshoots its power limit).
     for _ in range(args.warmup):
         wl.step()
+    smi_before = smi.sample(dev) if dev.type == "cuda" else None
     sync()
 
     # ---- timed region: exactly K steps, barrier + sync on both sides; HIP events
@@ -268,6 +272,7 @@ def main(argv=None) -> int:
     tmr.stop()
     sync()
     t1 = time.perf_counter()
+    smi_after = smi.sample(dev) if dev.type == "cuda" else None
     dist.barrier(env)
     my_seconds = tmr.seconds()
     elapsed = dist.all_reduce_max(env, my_seconds)
@@ -290,10 +295,28 @@ def main(argv=None) -> int:
         except Exception as e:  # noqa: BLE001 - reported per rank
             return {"median_GHz": None, "error": f"{type(e).__name__}: {e}"[:200]}
 
+    # The stamped launches follow a re-settle (>= 0.3 s of K1) and 8 more plain
+    # launches queued behind it with no sync, so they run in the steady state the
+    # timed loop ran in - not in the boost / overshoot transient an idle gap (the
+    # all-reduce above) starts (BENCH_r04: 663 -> 897 -> 711 us per stamped launch).
+    if dev.type == "cuda":
+        prewarm_settle(wl.step, sync, 0.3)
+        for _ in range(8):
+            wl.step()
     gclk = _probe("gemm_clock_ghz", wl.a, wl.b, wl.c, steps=min(max(args.steps, 1), 20))
     clk = _probe("clock_probe_ghz", dev)
+    # the clock the TIMED loop ran at: shader cycles per launch are launch-invariant
+    # (1.085-1.091 M at 8192^3), so median cycles / this rank's ms per step
+    timed_clk = None
+    if gclk and gclk.get("per_launch_cycles_median"):
+        cyc = sorted(gclk["per_launch_cycles_median"])
+        timed_clk = round(cyc[len(cyc) // 2] / (my_seconds / args.steps) / 1e9, 4)
+        gclk["ms_per_launch_over_ms_per_step"] = round(
+            gclk["ms_per_launch"] / (my_seconds / args.steps * 1e3), 4)
+    power = smi.window(smi_before, smi_after) if smi_before is not None else None
     per_rank = dist.all_gather_obj(env, {"tflops": round(wl.flops * args.steps / my_seconds / 1e12, 2),
-                                         "clock": clk, "gemm_clock": gclk})
+                                         "clock": clk, "gemm_clock": gclk,
+                                         "timed_loop_clock": timed_clk, "power": power})
 
     # ---- after the timed region: verification + context measurements
     extras: dict = {}
@@ -503,6 +526,15 @@ def main(argv=None) -> int:
         "per_rank_gemm_clock_GHz": [(p["gemm_clock"] or {}).get("launch_GHz") for p in per_rank],
         "per_rank_gemm_clock_p10_GHz": [(p["gemm_clock"] or {}).get("p10_GHz") for p in per_rank],
         "per_rank_gemm_clock": [p["gemm_clock"] for p in per_rank],
+        # median shader cycles per stamped launch / the rank's own timed ms per step
+        "per_rank_timed_loop_clock_GHz": [p["timed_loop_clock"] for p in per_rank],
+        # AMD SMI over [last warmup launches .. end of the timed loop], per rank:
+        # average power (energy counter), PPT (power) and socket-thermal throttle
+        # residency in % of firmware iterations, power / temperature / clock at both ends
+        "per_rank_avg_power_W": [(p["power"] or {}).get("avg_power_W") for p in per_rank],
+        "per_rank_ppt_throttle_pct": [(p["power"] or {}).get("ppt_pct") for p in per_rank],
+        "per_rank_thermal_throttle_pct": [(p["power"] or {}).get("thermal_pct") for p in per_rank],
+        "per_rank_power": [p["power"] for p in per_rank],
         "per_rank_clock_GHz": [(p["clock"] or {}).get("median_GHz") for p in per_rank],
         "per_rank_clock_probe": [p["clock"] for p in per_rank],
         "vs_baseline_note": "reference publishes no TFLOP/s or busbw (BASELINE.json published={})",

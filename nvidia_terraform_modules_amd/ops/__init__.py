@@ -25,6 +25,7 @@ from .kernels import (  # noqa: F401
     fill_uniform_,
     gemm_bf16,
     gemm_bf16_rowsum,
+    clock_summary,
     gemm_clock_ghz,
     gemm_fp8,
     gemm_fp8_rowsum,
@@ -38,6 +39,7 @@ from .kernels import (  # noqa: F401
     k1_splitk_plan,
     ref_gemm_f32,
     sk_ws_bytes,
+    sk_xcc_error,
     stream_copy,
     stream_read,
     verify_bf16,

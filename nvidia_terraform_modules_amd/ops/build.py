@@ -9,6 +9,8 @@ Outputs (all in-tree, so they travel to the GPU box with the repo snapshot):
   linked into the shipping library or the Job binary).
 * ``validation/build/amdgpu-validate`` - the standalone validation-Job binary
   (HIP + RCCL, no Python/PyTorch in the container image).
+* ``nvidia_terraform_modules_amd/ops/libntm_smi.so`` - host-only power /
+  thermal / throttle sampler on libamd_smi (bench.py's per-rank telemetry).
 
 The reference has no native code at all; this replaces the
 CUDA ``vectorAdd`` validator that the NVIDIA GPU Operator chart ran
@@ -131,12 +133,32 @@ def build_exporter(force: bool = False, verbose: bool = True) -> Path:
     return out
 
 
+SMI_LIB_NAME = "libntm_smi.so"
+
+
+def build_smi(force: bool = False, verbose: bool = True) -> Path:
+    """libntm_smi.so: host-only C++ on libamd_smi (power, temperature, clocks,
+    throttle residencies of one GPU by PCI address; ops/smi.py)."""
+    out = PKG_OPS / SMI_LIB_NAME
+    src = SRC / "ntm_smi.cpp"
+    if force or _stale(out, [src]):
+        BUILD.mkdir(parents=True, exist_ok=True)
+        tmp = BUILD / (SMI_LIB_NAME + ".tmp")
+        cxx = shutil.which("g++") or "/opt/rocm/llvm/bin/clang++"
+        _run([cxx, "-std=c++17", "-O2", "-Wall", "-fPIC", "-shared", "-I/opt/rocm/include",
+              str(src), "-L/opt/rocm/lib", "-lamd_smi", "-Wl,-rpath,/opt/rocm/lib", "-o", str(tmp)],
+             verbose)
+        os.replace(tmp, out)
+    return out
+
+
 def build_all(force: bool = False, verbose: bool = True, asan: bool = False) -> dict[str, str]:
     lib = build_library(force=force, verbose=verbose)
     binary = build_binary(force=force, verbose=verbose)
     res = {"library": str(lib), "binary": str(binary),
            "experimental": str(build_experimental(force=force, verbose=verbose)),
-           "exporter": str(build_exporter(force=force, verbose=verbose))}
+           "exporter": str(build_exporter(force=force, verbose=verbose)),
+           "smi": str(build_smi(force=force, verbose=verbose))}
     if asan:
         res["binary_asan"] = str(build_binary(force=force, verbose=verbose, asan=True))
     return res

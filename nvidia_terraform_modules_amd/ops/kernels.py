@@ -225,6 +225,26 @@ def _sk_workspace(dev: torch.device, nbytes: int) -> torch.Tensor:
     return ws
 
 
+def sk_xcc_error(device=None, clear: bool = True) -> int:
+    """The XCD-placement error word of this stream's stream-K workspace
+    (synchronises): 0 while every split tile's parts ran on one XCD, else the
+    first violation a combiner saw (0x80000000 | mode << 28 | tile << 8 |
+    combiner's XCC << 4 | other's XCC; gemm_bf16_sk.hpp). ``clear`` resets it."""
+    dev = torch.device(device) if device is not None else torch.device(
+        "cuda", torch.cuda.current_device())
+    key = (dev.index if dev.index is not None else torch.cuda.current_device(),
+           int(stream_handle() or 0))
+    ws = _SK_WS.get(key)
+    if ws is None:
+        return 0
+    i = lib().ntm_sk_error_word_index()
+    word = ws.view(torch.int32)[i:i + 1]
+    v = int(word.item()) & 0xFFFFFFFF
+    if clear and v:
+        word.zero_()
+    return v
+
+
 def _gemm_bf16_sk(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, rev: bool = False) -> torch.Tensor:
     """Stream-K (gemm_bf16_sk.hpp): fp32 partials of the split tiles and one
     counter per split in this stream's cached workspace (_sk_workspace)."""
@@ -590,14 +610,20 @@ def _ghz_summary(ghz: torch.Tensor) -> dict:
 
 def gemm_clock_ghz(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
                    steps: int = 1) -> dict:
-    """K1's OWN clock: ``steps`` back-to-back launches of the
-    shipping pingpong8o build with a start / end s_memtime + s_memrealtime
-    stamp per workgroup (gemm_bf16_pp6.hpp STAMP 1; C is the real product).
-    Per workgroup and launch, clock = d(shader cycles) / d(100 MHz ticks);
-    returns median / p10 / min / max GHz over all of them and the wall time of
-    the launches. Needs whole 256x256 tiles, K % 128, K >= 256. The MFMA-only
-    ``clock_probe_ghz`` reads the clock of a different load (no LDS or HBM
-    traffic): under shared power the two can differ by 15-20 %."""
+    """K1's OWN clock: ``steps`` back-to-back launches
+    of the shipping pingpong8o build with a start / end s_memtime +
+    s_memrealtime stamp per workgroup and the XCC_ID register of the XCD that
+    ran it (gemm_bf16_pp6.hpp STAMP 1; C is the real product). Per workgroup
+    and launch, clock = d(shader cycles) / d(100 MHz ticks).
+
+    Returns median / p10 / min / max GHz over all workgroups, per-XCD medians
+    keyed by the REAL XCC id, whether the dispatcher's ``blockIdx & 7`` round
+    robin matched those ids, and ``bound_GHz``: per launch the slowest XCD's
+    median clock (the tiles are split evenly over the XCDs, so the slowest
+    one sets the launch time), median over launches. Needs whole 256x256
+    tiles, K % 128, K >= 256. The MFMA-only ``clock_probe_ghz`` reads the clock
+    of a different load (no LDS or HBM traffic): under shared power the two
+    can differ by 15-20 %."""
     _require(a, "a", torch.bfloat16)
     _require(b, "b", torch.bfloat16)
     m, k = a.shape
@@ -608,7 +634,8 @@ def gemm_clock_ghz(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = 
     if out is None:
         out = torch.empty((m, n), dtype=torch.bfloat16, device=a.device)
     _require(out, "out", torch.bfloat16)
-    stamps = torch.zeros((steps, grid, 4), dtype=torch.int64, device=a.device)
+    words = lib().ntm_gemm_bf16_clock_words()
+    stamps = torch.zeros((steps, grid, words), dtype=torch.int64, device=a.device)
     t0 = torch.cuda.Event(enable_timing=True)
     t1 = torch.cuda.Event(enable_timing=True)
     t0.record()
@@ -619,33 +646,56 @@ def gemm_clock_ghz(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = 
               "ntm_gemm_bf16_clock")
     t1.record()
     t1.synchronize()
-    v = stamps.view(-1, 4).double()
-    ghz = (v[:, 2] - v[:, 0]) / (v[:, 3] - v[:, 1]) * 0.1
-    res = _ghz_summary(ghz)
-    res["workgroups"] = res.pop("n")
-    # workgroups b with the same b & 7 share an XCD (the dispatcher's round
-    # robin; a label, not the XCD's id): the spread of the group medians is
-    # the per-XCD clock spread under this load
-    g = ghz.view(steps, grid)
-    groups = [g[:, x::8].reshape(-1) for x in range(min(8, grid))]
-    res["per_xcd_group_median_GHz"] = [_ghz_summary(x)["median_GHz"] for x in groups]
-    res["ms_per_launch"] = round(t0.elapsed_time(t1) / steps, 4)
-    res["launches"] = steps
-    # per launch: medians over workgroups of the shader cycles and the wall window
-    # (us) between a workgroup's two stamps - to set against a profiler's
-    # per-dispatch duration and cycle counters (tools/clock_check.py)
+    return clock_summary(stamps.cpu(), t0.elapsed_time(t1) / steps)
+
+
+def clock_summary(stamps: torch.Tensor, ms_per_launch: float) -> dict:
+    """Summary of a [launches, workgroups, words] record of the clock build
+    (host-side; see ``gemm_clock_ghz``)."""
+    steps, grid = stamps.shape[0], stamps.shape[1]
     sv = stamps.double()
+    ghz = (sv[:, :, 2] - sv[:, :, 0]) / (sv[:, :, 3] - sv[:, :, 1]) * 0.1   # [steps, grid]
+    res = _ghz_summary(ghz.reshape(-1))
+    res["workgroups"] = res.pop("n")
+    # the XCD that really ran each workgroup (XCC_ID register) ...
+    xcc = (stamps[:, :, 4] & 0xF).long()
+    ids = sorted(set(xcc.reshape(-1).tolist()))
+    res["xcc_ids"] = ids
+    res["per_xcc_median_GHz"] = {str(x): _ghz_summary(ghz[xcc == x])["median_GHz"] for x in ids}
+    # ... against the dispatcher's round robin, blockIdx & 7 (what stream-K's
+    # per-XCD tile lists and its write-through / L1-only-acquire protocol assume)
+    resid = torch.arange(grid) & 7
+    seen = {r: sorted(set(xcc[:, resid == r].reshape(-1).tolist())) for r in range(min(8, grid))}
+    one_each = all(len(v) == 1 for v in seen.values())
+    res["xcc_of_blockidx_mod_8"] = {str(r): v for r, v in seen.items()}
+    res["blockidx_mod_8_is_xcc"] = bool(one_each and len({v[0] for v in seen.values()}) == len(seen))
+    # kept for continuity with earlier rounds' JSON: groups by b & 7
+    res["per_xcd_group_median_GHz"] = [_ghz_summary(ghz[:, r::8].reshape(-1))["median_GHz"]
+                                       for r in range(min(8, grid))]
+    res["ms_per_launch"] = round(ms_per_launch, 4)
+    res["launches"] = steps
+    # per launch: medians over workgroups of the shader cycles and of the wall
+    # window (us) between a workgroup's two stamps - to set against a profiler's
+    # per-dispatch duration and cycle counters (tools/clock_check.py)
     cyc = (sv[:, :, 2] - sv[:, :, 0]).median(dim=1).values
     win = ((sv[:, :, 3] - sv[:, :, 1]) / 100.0).median(dim=1).values
-    # per launch: the median workgroup's cycles over the median workgroup's window;
-    # the median over launches is the clock bench.py reports. On the same
-    # dispatches it reads 2.0 / 2.7 % below GRBM_GUI_ACTIVE / 8 XCDs / duration
-    # (two boxes, profiles/r4_clock/; the PMC clock also covers the dispatch's
-    # ramp, when fewer CUs run). The per-workgroup median (median_GHz) reads 5 %
-    # low: the slower XCDs' workgroups pull it down.
-    lg = (cyc / (win * 1e3))
+    # the median workgroup's cycles over the median workgroup's window, median
+    # over launches (2.0 / 2.7 % below GRBM_GUI_ACTIVE / 8 XCDs / duration on the
+    # same dispatches, profiles/r4_clock/)
+    lg = cyc / (win * 1e3)
     lg = lg[torch.isfinite(lg) & (lg > 0)]
     res["launch_GHz"] = round(float(lg.median()), 4) if lg.numel() else None
+    # the launch-bounding clock: every XCD gets the same number of tiles, so the
+    # slowest XCD's workgroups finish last and set the launch time
+    bound, spread = [], []
+    for i in range(steps):
+        per = [float(ghz[i][xcc[i] == x].median()) for x in ids if bool((xcc[i] == x).any())]
+        per = [v for v in per if v == v and v > 0]
+        if per:
+            bound.append(min(per))
+            spread.append(max(per) / min(per) - 1.0)
+    res["bound_GHz"] = round(sorted(bound)[len(bound) // 2], 4) if bound else None
+    res["xcc_clock_spread_pct"] = round(100 * sorted(spread)[len(spread) // 2], 2) if spread else None
     res["per_launch_cycles_median"] = [int(x) for x in cyc.tolist()]
     res["per_launch_window_us_median"] = [round(x, 2) for x in win.tolist()]
     return res

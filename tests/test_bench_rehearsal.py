@@ -74,6 +74,13 @@ def test_torchrun_launch_one_json_line(nproc):
     assert d["per_rank_gemm_clock_GHz"] == [None] * nproc
     assert d["per_rank_gemm_clock_p10_GHz"] == [None] * nproc
     assert len(d["per_rank_gemm_clock"]) == nproc
+    # the timed loop's own clock and each rank's power / throttle
+    # window are reported per rank (None without a GPU)
+    assert d["per_rank_timed_loop_clock_GHz"] == [None] * nproc
+    assert d["per_rank_power"] == [None] * nproc
+    assert d["per_rank_avg_power_W"] == [None] * nproc
+    assert d["per_rank_ppt_throttle_pct"] == [None] * nproc
+    assert d["per_rank_thermal_throttle_pct"] == [None] * nproc
     if nproc > 1:
         # C2 knob sweep: blocks per rank 16..256 x one/two-shot at the
         # tune sizes that fit the sweep cap (1 MiB here; 64 / 256 MiB on a real node),
@@ -141,6 +148,12 @@ def test_bench_on_one_gpu_json_contract(tmp_path):
     assert 0.5 < d["per_rank_gemm_clock_GHz"][0] < 3.0, g
     assert g["p10_GHz"] <= g["median_GHz"] and g["workgroups"] > 0
     assert 0.5 < d["per_rank_clock_GHz"][0] < 3.0
+    assert 0.3 < d["per_rank_timed_loop_clock_GHz"][0] < 3.0
+    assert g["ms_per_launch_over_ms_per_step"] > 0
+    pw = d["per_rank_power"][0]
+    assert "error" not in pw, pw
+    # (a 5-step 2048^3 window is shorter than the energy counter's update period)
+    assert pw["avg_power_W"] is None or pw["avg_power_W"] >= 0, pw
     job = d["validation_job"]
     assert job["ran"] and job["passed"], job
     assert 0 < d["time_to_gpu_ready_in_node_s"] < 30

@@ -757,6 +757,13 @@ def test_gemm_clock_build(ops, m, n, k):
     assert len(r["per_launch_cycles_median"]) == 3 and len(r["per_launch_window_us_median"]) == 3
     xg = r["per_xcd_group_median_GHz"]
     assert len(xg) == 8 and all(r["min_GHz"] <= x <= r["max_GHz"] for x in xg)
+    # the groups are labelled by the XCC_ID register, and on
+    # MI355X (SPX) the dispatcher's blockIdx & 7 round robin IS the XCD - the
+    # placement stream-K's fix-up protocol relies on
+    assert r["xcc_ids"] == list(range(8)), r["xcc_of_blockidx_mod_8"]
+    assert r["blockidx_mod_8_is_xcc"] is True, r["xcc_of_blockidx_mod_8"]
+    assert set(r["per_xcc_median_GHz"]) == {str(x) for x in range(8)}
+    assert r["min_GHz"] <= r["bound_GHz"] <= r["median_GHz"] and r["xcc_clock_spread_pct"] >= 0
     with pytest.raises(ValueError):
         ops.gemm_clock_ghz(a[:, :200], b[:, :200])
 
@@ -803,6 +810,7 @@ def test_stream_k_vs_torch_fp32(ops, m, n, k):
     assert torch.all(out[:, n:] == 7.0)
     first = c.clone()
     assert torch.equal(ops.gemm_bf16(a, b, variant="pingpong8s"), first)
+    assert ops.sk_xcc_error() == 0   # every split tile's parts ran on one XCD
     assert torch.equal(ops.gemm_bf16(a, b, variant="pingpong8s_rev"), first)
 
 
@@ -850,6 +858,7 @@ def test_default_plan_runs_stream_k(ops, m, n, k):
     b = _rand(ops, (n, k), 673)
     c = ops.gemm_bf16(a, b)
     assert torch.equal(c, ops.gemm_bf16(a, b, variant="pingpong8s"))
+    assert ops.sk_xcc_error() == 0
     ref = a.float() @ b.float().T
     atol, rtol = ops.gemm_tolerance(k)
     assert torch.all((c.float() - ref).abs() <= atol + rtol * ref.abs())
@@ -882,3 +891,4 @@ def test_stream_k_split_mode_vs_torch_fp32(ops, m, n, k):
     first = c.clone()
     for _ in range(3):
         assert torch.equal(ops.gemm_bf16(a, b, variant="pingpong8s"), first)
+    assert ops.sk_xcc_error() == 0   # every slice of a tile ran on the combiner's XCD

@@ -92,6 +92,17 @@ __host__ __device__ inline float e4m3_bits_to_f32(uint8_t v) {
   return (v & 0x80) ? -f : f;
 }
 
+// The XCD (XCC) this wave runs on, read from the hardware register (not
+// inferred from blockIdx: the dispatcher's round robin is a convention, which
+// compute partition modes change). Raw register; the id is its low 4 bits.
+__device__ __forceinline__ unsigned xcc_id_raw() {
+  unsigned v;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(v));
+  return v;
+}
+
+__device__ __forceinline__ unsigned xcc_id() { return xcc_id_raw() & 0xFu; }
+
 // Stateless counter-based hash (splitmix64 finaliser). Used for the
 // synthetic uniform [-1, 1) operands so every rank / run is reproducible
 // from (seed, index) without any host->device copy.

@@ -389,6 +389,9 @@ __device__ __forceinline__ void tile_origin(const GemmArgs& p, int tile, int nti
   n0 = tn * BN;
 }
 
+// Words per workgroup of the STAMP 1 clock build's record.
+constexpr int kClockStampWords = 6;
+
 // Clock stamp (STAMP builds): shader-clock and 100 MHz real-time counters read
 // together, the wait inside the statement (cdna_hip_programming.md §7).
 __device__ __forceinline__ void clock_stamp(unsigned long long& t, unsigned long long& rt) {
@@ -399,10 +402,11 @@ __device__ __forceinline__ void clock_stamp(unsigned long long& t, unsigned long
 }
 
 // POL: C store policy of store_c16 (1 = nontemporal, the shipping build).
-// STAMP 1 (diagnostic build, never in the default dispatch): lane 0 of wave 0
-// records s_memtime / s_memrealtime at kernel start and after the last store
-// into p.stamps[4 * blockIdx.x ..]: the GEMM's own clock = d(memtime) /
-// d(realtime) x 100 MHz.
+// STAMP 1 (the clock build, never in the default dispatch): lane 0 of wave 0
+// records s_memtime / s_memrealtime at kernel start and after the last store,
+// then the raw XCC_ID and HW_ID registers, into p.stamps[kClockStampWords *
+// blockIdx.x ..]: the GEMM's own clock = d(memtime) / d(realtime) x 100 MHz,
+// grouped by the XCD that really ran the workgroup.
 // MASK ("pingpong8om"): ragged C - ceil(M/256) x
 // ceil(N/256) tiles, sources clamped per tile (src_clamped), stores masked.
 // TAIL (with MASK): K % 128 != 0 - T = ceil(K / 128) * 2 K-tiles; the pieces
@@ -608,12 +612,17 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_pp6_kernel(GemmArgs p) 
   if constexpr (STAMP == 1) {
     unsigned long long t1, rt1;
     clock_stamp(t1, rt1);
+    unsigned hw;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    const unsigned xcc = xcc_id_raw();
     if (threadIdx.x == 0) {
-      unsigned long long* o = p.stamps + 4 * (size_t)blockIdx.x;
+      unsigned long long* o = p.stamps + kClockStampWords * (size_t)blockIdx.x;
       o[0] = t0;
       o[1] = rt0;
       o[2] = t1;
       o[3] = rt1;
+      o[4] = xcc;
+      o[5] = hw;
     }
   }
 }

@@ -48,6 +48,17 @@
 // partial is stored write-through (sc1), every storing wave waits vmcnt(0),
 // barrier, thread 0 adds to the counter; the combiner's thread 0 acquires
 // (this CU's L1) before any wave reads the partial with plain loads.
+//
+// That acquire is enough only because every part of a split tile runs on the
+// SAME XCD (so its plain loads hit the L2 the partial was written through to,
+// never a stale line another XCD's L2 kept from an earlier launch): both modes
+// deal tiles per XCD by the dispatcher's round robin, blockIdx & 7. The kernels
+// CHECK that invariant instead of assuming it: each part's first counter add
+// also carries the XCC_ID register of the XCD it runs on (tag fields above the
+// protocol bits; split mode adds the id and its square, so the S parts agree
+// iff sum = S x and sum of squares = S x^2), and the combiner compares them with
+// its own. A mismatch sets the workspace's error word (kErrWord, sticky until
+// the host clears it; ops.sk_xcc_error): C is then not trusted.
 #pragma once
 
 #include "ntm/gemm_bf16_pp3.hpp"
@@ -64,6 +75,11 @@ using ::ntm::gemm3::tile3;
 
 constexpr size_t kPartialBytes = (size_t)BM * BN * 4;  // one fp32 256x256 partial
 constexpr size_t kCounterBytes = 4096;                 // counter block at the workspace start
+// error word (last of the counter block): 0, or the first XCD-placement
+// violation a combiner saw: 0x80000000 | mode << 28 | tile << 8 | mine << 4 | other
+constexpr int kErrWord = (int)(kCounterBytes / 4) - 1;
+// two-round mode: the head's / tail's XCC tag (id + 1) above the protocol bits
+constexpr int kHeadTagShift = 8, kTailTagShift = 16;
 
 struct SkArgs {
   float* ws;      // kCounterBytes of counters (zero on entry, left zero), then G slots x 2 partials
@@ -86,7 +102,7 @@ constexpr int kMaxSlices = 8;
 
 __host__ __device__ inline bool sk_decompose(int M, int N, int K, int cus, SkArgs& s) {
   // one 4-byte counter per workgroup slot (or per tile) in the kCounterBytes block
-  if (M <= 0 || N <= 0 || K <= 0 || cus < 8 || (cus % 8) != 0 || cus > (int)(kCounterBytes / 4))
+  if (M <= 0 || N <= 0 || K <= 0 || cus < 8 || (cus % 8) != 0 || cus + 8 > kErrWord)
     return false;
   s.ntiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   s.G = cus;
@@ -247,6 +263,16 @@ __device__ __forceinline__ void reset_counter(unsigned* cnt) {
   if (threadIdx.x == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// First placement violation wins (the word is read and cleared by the host).
+__device__ __forceinline__ void report_xcc_error(unsigned* cnt_base, unsigned code) {
+  if (threadIdx.x == 0) {
+    unsigned expect = 0u;
+    __hip_atomic_compare_exchange_strong(cnt_base + kErrWord, &expect, 0x80000000u | code,
+                                         __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 constexpr int kEpiSk = kEpiDefault | kEpiMask;
 
 // REV (test build): each workgroup runs its stream-K segments in range order
@@ -307,6 +333,7 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_sk_kernel(GemmArgs p, S
   // All of it is uniform; readfirstlane keeps it out of VGPRs, which the K
   // loop needs every one of.
   const int x = b & 7, j = b >> 3, W = s.G >> 3;
+  const unsigned my_xcc = xcc_id();
   const int nx = (s.ntiles - s.D - x + 7) >> 3;  // this XCD's stream-K tiles
   const int U = nx * s.Tp;
   const int u0 = __builtin_amdgcn_readfirstlane((int)((long)j * U / W));
@@ -347,15 +374,22 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_sk_kernel(GemmArgs p, S
       unsigned* cnt = s.cnt + slot;
       const unsigned arrive = tail ? 4u : 1u, written = arrive << 1;
       const unsigned other_written = tail ? 2u : 8u;
+      // this part's XCC tag rides on its first counter add
+      const unsigned tag = (my_xcc + 1u) << (tail ? kTailTagShift : kHeadTagShift);
       // the part this segment order runs first (the head; REV: the tail) writes
       // without looking: the other part has almost never written yet
       const bool writer = REV ? tail : head;
-      unsigned o = writer ? 0u : counter_add<false>(cnt, arrive, bcast);
+      unsigned o = writer ? 0u : counter_add<false>(cnt, arrive + tag, bcast);
       if (!(o & other_written)) {
         write_partial(mine, acc);
-        o = counter_add<true>(cnt, written, bcast);
+        o = counter_add<true>(cnt, written + (writer ? tag : 0u), bcast);
       }
       if (o & other_written) {
+        // the other part's first add (which carried its tag) precedes its WRITTEN
+        const unsigned other_xcc = ((o >> (tail ? kHeadTagShift : kTailTagShift)) & 0xFFu) - 1u;
+        if (other_xcc != my_xcc)
+          report_xcc_error(s.cnt, (unsigned)(slot & 0xFFFF) << 8 | (my_xcc & 0xF) << 4 |
+                                      (other_xcc & 0xF));
         acquire_all();
         add_partial(other, acc);
         reset_counter(cnt);
@@ -415,8 +449,14 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_sks_kernel(GemmArgs p, 
   float* part = s.ws + (kCounterBytes + (size_t)tile * s.S * kPartialBytes) / 4;
   unsigned* cnt = s.cnt + tile;
   write_partial(part + (size_t)slice * (kPartialBytes / 4), acc);
-  const unsigned o = counter_add<true>(cnt, 1u, bcast);
-  if (o != (unsigned)(s.S - 1)) return;  // uniform
+  // count (bits 0-7) + XCC id (8-15) + its square (16-31): S <= 8 parts, id < 16
+  const unsigned xc = xcc_id();
+  const unsigned tag = 1u + (xc << 8) + ((xc * xc) << 16);
+  const unsigned o = counter_add<true>(cnt, tag, bcast);
+  if ((o & 0xFFu) != (unsigned)(s.S - 1)) return;  // uniform
+  const unsigned all = o + tag, S = (unsigned)s.S;
+  if (((all >> 8) & 0xFFu) != S * xc || (all >> 16) != S * xc * xc)
+    report_xcc_error(s.cnt, 1u << 28 | (unsigned)(tile & 0xFFFF) << 8 | (xc & 0xF) << 4);
   acquire_all();
   // every slice's partial (its own too, already written) summed in slice order,
   // so C does not depend on which slice combines (no second accumulator set)

@@ -486,6 +486,11 @@ NTM_API int ntm_gemm_bf16_splitk(int variant, int splits, const void* A, const v
 // rounds of tiles dealt out as K-tile pairs over every CU, fp32 partials of the
 // split tiles in ws. ntm_sk_ws_bytes = 0: stream-K does not serve (M, N, K) on
 // this device (the tile count is a multiple of the CUs, or at most one round).
+// Index (in 4-byte words) of the stream-K workspace's XCD-placement error word
+// (gemm_bf16_sk.hpp kErrWord): nonzero after a launch in which some part of a
+// split tile ran on a different XCD than the part that combined it.
+NTM_API int ntm_sk_error_word_index() { return ntm::gemmsk::kErrWord; }
+
 NTM_API size_t ntm_sk_ws_bytes(int M, int N, int K) {
   ntm::gemmsk::SkArgs s;
   if (!ntm::gemmsk::shape_ok_sk(M, N, K) ||
@@ -810,8 +815,11 @@ NTM_API int ntm_clock_probe(int grid, int iters, void* out, float* sink, void* s
 
 // GEMM clock: the shipping pingpong8o build with a start / end
 // s_memtime + s_memrealtime stamp per workgroup (gemm_bf16_pp6.hpp STAMP 1).
-// Whole 256x256 tiles, more tiles than CUs; stamps = 4 u64 per workgroup
-// (ntm_gemm_bf16_clock_grid workgroups). C is the real product.
+// Whole 256x256 tiles, more tiles than CUs; stamps = ntm_gemm_bf16_clock_words()
+// u64 per workgroup (start / end shader clock and real time, XCC_ID, HW_ID;
+// ntm_gemm_bf16_clock_grid workgroups). C is the real product.
+NTM_API int ntm_gemm_bf16_clock_words() { return ntm::gemm6::kClockStampWords; }
+
 NTM_API int ntm_gemm_bf16_clock_grid(int M, int N) {
   if (M <= 0 || N <= 0 || M % 256 || N % 256) return 0;
   return ntm::gemm6::pp6_grid((M / 256) * (N / 256));
