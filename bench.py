@@ -313,6 +313,12 @@ def main(argv=None) -> int:
         timed_clk = round(cyc[len(cyc) // 2] / (my_seconds / args.steps) / 1e9, 4)
         gclk["ms_per_launch_over_ms_per_step"] = round(
             gclk["ms_per_launch"] / (my_seconds / args.steps * 1e3), 4)
+        # share of a timed step the bounding XCD's workgroups spend between their
+        # stamps (the rest: dispatch ramp, drain, launch gap): timed-loop clock =
+        # bound clock x this fraction
+        if gclk.get("bound_GHz"):
+            gclk["bound_window_fraction"] = round(
+                cyc[len(cyc) // 2] / (gclk["bound_GHz"] * 1e9) / (my_seconds / args.steps), 4)
     power = smi.window(smi_before, smi_after) if smi_before is not None else None
     per_rank = dist.all_gather_obj(env, {"tflops": round(wl.flops * args.steps / my_seconds / 1e12, 2),
                                          "clock": clk, "gemm_clock": gclk,
@@ -523,7 +529,14 @@ def main(argv=None) -> int:
         "per_rank_tflops": [p["tflops"] for p in per_rank],
         # in-kernel clock: per stamped launch the median workgroup's cycles / window,
         # median over launches (within 2-3 % of the PMC clock, profiles/r4_clock/)
-        "per_rank_gemm_clock_GHz": [(p["gemm_clock"] or {}).get("launch_GHz") for p in per_rank],
+        # the launch-bounding clock: per stamped launch the slowest XCD's median
+        # workgroup clock (every XCD gets the same tiles, so it finishes last);
+        # the all-workgroup median beside it, and the per-XCD spread
+        "per_rank_gemm_clock_GHz": [(p["gemm_clock"] or {}).get("bound_GHz") for p in per_rank],
+        "per_rank_gemm_clock_median_GHz": [(p["gemm_clock"] or {}).get("launch_GHz")
+                                           for p in per_rank],
+        "per_rank_xcd_clock_spread_pct": [(p["gemm_clock"] or {}).get("xcc_clock_spread_pct")
+                                          for p in per_rank],
         "per_rank_gemm_clock_p10_GHz": [(p["gemm_clock"] or {}).get("p10_GHz") for p in per_rank],
         "per_rank_gemm_clock": [p["gemm_clock"] for p in per_rank],
         # median shader cycles per stamped launch / the rank's own timed ms per step

@@ -77,6 +77,8 @@ def _declare(lib: ctypes.CDLL) -> None:
         "ntm_gemm_bf16_clock_grid": ([c_int, c_int], c_int),
         "ntm_gemm_bf16_clock_words": ([], c_int),
         "ntm_sk_error_word_index": ([], c_int),
+        "ntm_plan_cus": ([], c_int),
+        "ntm_set_cus_override": ([c_int], None),
         "ntm_gemm_bf16_clock": ([c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp,
                                  c_vp], c_int),
         "ntm_stream_copy": ([c_vp, c_vp, c_size, c_vp], c_int),

@@ -107,7 +107,12 @@ def _default_ws_bytes(m: int, n: int, k: int) -> int:
     wsb = _DEFAULT_WS.get(key)
     if wsb is None:
         _, top, _, sp = k1_splitk_plan(m, n, k)  # raises if no kernel serves the shape
-        wsb = -1 if top == "pingpong8s" else lib().ntm_splitk_ws_bytes(m, n, k, sp) if sp > 1 else 0
+        if top == "pingpong8s":
+            # stream-K only where its own launch serves the shape (the plan and the
+            # launch size for the same CUs; belt and braces): else the unsplit plan
+            wsb = -1 if sk_ws_bytes(m, n, k) > 0 else 0
+        else:
+            wsb = lib().ntm_splitk_ws_bytes(m, n, k, sp) if sp > 1 else 0
         _DEFAULT_WS[key] = wsb
     return wsb
 

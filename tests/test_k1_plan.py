@@ -257,3 +257,38 @@ def test_stream_k_decomposition_serves(k1_plan, m, n, k, served):
     from nvidia_terraform_modules_amd import ops
 
     assert (ops.sk_ws_bytes(m, n, k) > 0) == served
+
+
+@pytest.mark.parametrize("cus", [256, 128, 80, 32])
+def test_plan_and_launch_agree_on_the_cu_count(k1_plan, cus):
+    """the plan's stream-K choice is made for the CU count the launch
+    sizes its grid for (device_cus: 256 on MI355X in SPX mode, fewer in a DPX /
+    CPX partition), so the default dispatch never picks a stream-K plan whose
+    launch would refuse the shape. Forced CU counts, host only."""
+    import random
+
+    from nvidia_terraform_modules_amd import ops
+    from nvidia_terraform_modules_amd.ops import kernels
+    from nvidia_terraform_modules_amd.ops._lib import lib
+
+    rng = random.Random(cus)
+    shapes = [(4472, 5688, 5832), (4672, 1472, 6696), (1000, 1000, 1000), (8192, 8192, 8192)]
+    shapes += [(rng.randrange(256, 9000), rng.randrange(32, 1200) * 8, rng.randrange(16, 1500) * 8)
+               for _ in range(60)]
+    lib().ntm_set_cus_override(cus)
+    kernels._DEFAULT_WS.clear()
+    try:
+        assert lib().ntm_plan_cus() == cus
+        picked = 0
+        for m, n, k in shapes:
+            _, top, _, _ = ops.k1_splitk_plan(m, n, k)
+            if top == "pingpong8s":
+                picked += 1
+                assert ops.sk_ws_bytes(m, n, k) > 0, (m, n, k)
+                assert kernels._default_ws_bytes(m, n, k) == -1
+        if cus % 8 == 0 and cus >= 32:
+            assert picked > 0
+    finally:
+        lib().ntm_set_cus_override(0)
+        kernels._DEFAULT_WS.clear()
+    assert lib().ntm_plan_cus() == 256      # no GPU here: the documented default

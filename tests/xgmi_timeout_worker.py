@@ -17,11 +17,19 @@ from nvidia_terraform_modules_amd.parallel.xgmi import XgmiAllReduce  # noqa: E4
 
 def main():
     env = init(backend="gloo", device_type="cuda")
-    ar = XgmiAllReduce(env, max_bytes=1 << 20, nblk=8, spin_limit=4096, entry_spin_limit=4096)
+    # one communicator per algorithm (both set up collectively): the two-shot one
+    # with its one-shot cutoff at 0, so the two-shot entry-timeout and poison path
+    # really runs (128 KiB is under the default 256 KiB cutoff)
+    comms = {False: XgmiAllReduce(env, max_bytes=1 << 20, nblk=8, one_shot_max_bytes=0,
+                                  spin_limit=4096, entry_spin_limit=4096),
+             True: XgmiAllReduce(env, max_bytes=1 << 20, nblk=8, spin_limit=4096,
+                                 entry_spin_limit=4096)}
     rep = {"rank": env.rank}
     if env.rank == 0:
         n = env.world_size
         for one_shot, count in ((False, 8 * n * 4096), (True, 8 * n * 64)):
+            ar = comms[one_shot]
+            assert (count * 2 <= ar.one_shot_max_bytes) == one_shot
             t = torch.ones(count, dtype=torch.bfloat16, device=env.device)
             try:
                 ar(t, check=True)
@@ -29,9 +37,10 @@ def main():
             except RuntimeError as e:
                 rep[f"raised_{int(one_shot)}"] = str(e)
             rep[f"all_nan_{int(one_shot)}"] = bool(torch.isnan(t.float()).all())
-        rep["timed_out"] = ar.timed_out()
+        rep["timed_out"] = all(ar.timed_out() for ar in comms.values())
     barrier(env)   # rank 1 never launches; it only waits here
-    ar.close()
+    for ar in comms.values():
+        ar.close()
     print(json.dumps(rep), flush=True)
     shutdown(env)
 

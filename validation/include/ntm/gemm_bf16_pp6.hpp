@@ -630,8 +630,17 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_pp6_kernel(GemmArgs p) 
 #undef NTM_PHT
 #undef NTM_ST
 
-// Grid: one workgroup per CU (LDS allows no more), fewer if there are fewer tiles.
-inline int pp6_grid(int ntiles) {
+// The CUs the persistent / stream-K grids are sized for (one workgroup per CU)
+// and the default plan prices its rounds over: the device's count (its compute
+// partition's in DPX / CPX modes), 256 without a device. cu_override() > 0
+// replaces it (tests of the plan on other partition sizes, ntm_set_cus_override).
+inline int& cu_override() {
+  static int v = 0;
+  return v;
+}
+
+inline int device_cus() {
+  if (cu_override() > 0) return cu_override();
   static int cus = 0;
   if (cus == 0) {
     int dev = 0;
@@ -641,6 +650,12 @@ inline int pp6_grid(int ntiles) {
     else
       cus = prop.multiProcessorCount;
   }
+  return cus;
+}
+
+// Grid: one workgroup per CU (LDS allows no more), fewer if there are fewer tiles.
+inline int pp6_grid(int ntiles) {
+  const int cus = device_cus();
   return ntiles < cus ? ntiles : cus;
 }
 

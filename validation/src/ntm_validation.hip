@@ -110,7 +110,7 @@ constexpr bool kPlanMaskedPersistent = false;
 // rounds (8192x8192x4096 / 4096x8192x4096 / 8192x4096x4096: 1300 / 1289 / 1282
 // vs 1279 / 1258 / 1253 TF/s, profiles/r3_tiles/), so 0.80 against 0.78; it
 // wastes fewer edge rows where M is ragged and N a multiple of 256.
-constexpr double kCUs = 256.0;
+// (the CU count the rounds are priced over is the launch's own: device_cus())
 struct SmallTile {
   int variant, tm, tn;
   double eff;
@@ -206,7 +206,10 @@ constexpr double kSkSplitMinFixup = 8e-6;
 // costs the same cycles in both dtypes); only the tiles with an fp8 build - the
 // 256x256 kernel and the wave-specialised ones - and no split-K.
 inline K1Plan plan_k1(int M, int N, int K, bool splitk = false, bool fp8 = false) {
-  auto rounds = [](double tiles) { return tiles <= 0 ? 0.0 : __builtin_ceil(tiles / kCUs); };
+  // the CUs the launches below run on (256 on MI355X in SPX mode; fewer in a
+  // DPX / CPX partition): stream-K's decomposition must be the launch's own
+  const double kCUs = (double)ntm::gemm6::device_cus();
+  auto rounds = [&](double tiles) { return tiles <= 0 ? 0.0 : __builtin_ceil(tiles / kCUs); };
   const double inf = 1e300;
   // the 256x256 kernel on whole tiles: pingpong8c (K % 128). K % 128 != 0 goes
   // to the masked build's partial-K path (22), measured faster than pingpong8b
@@ -490,6 +493,12 @@ NTM_API int ntm_gemm_bf16_splitk(int variant, int splits, const void* A, const v
 // (gemm_bf16_sk.hpp kErrWord): nonzero after a launch in which some part of a
 // split tile ran on a different XCD than the part that combined it.
 NTM_API int ntm_sk_error_word_index() { return ntm::gemmsk::kErrWord; }
+
+// The CU count the plan and the persistent / stream-K launches use, and a test
+// override of it (0 = the device's own; host only: a CPU test of the plan on
+// partition sizes other than 256 - never set it around real launches).
+NTM_API int ntm_plan_cus() { return ntm::gemm6::device_cus(); }
+NTM_API void ntm_set_cus_override(int cus) { ntm::gemm6::cu_override() = cus > 0 ? cus : 0; }
 
 NTM_API size_t ntm_sk_ws_bytes(int M, int N, int K) {
   ntm::gemmsk::SkArgs s;

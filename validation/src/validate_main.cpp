@@ -885,7 +885,9 @@ bool run_xgmi(const std::vector<int>& devs, const Opts& o, std::vector<CollRow>&
     double best_t = 1e300;
     std::string tab = "[";
     for (const int nb : kTuneNblk) {
-      if (nb > nblk_cap || !ok) continue;
+      // no size fits the sweep cap: nothing to time, keep the defaults (nblk 32,
+      // the default cutoff) rather than "choosing" cutoff 0 on an empty table
+      if (nb > nblk_cap || !ok || tsizes.empty()) continue;
       double t1[3] = {1e300, 1e300, 1e300}, t2[3] = {1e300, 1e300, 1e300};
       for (size_t k = 0; k < tsizes.size() && ok; ++k)
         for (const int os : {1, 2}) {
