@@ -30,7 +30,7 @@ def _require(t: torch.Tensor, name: str, dtype: torch.dtype) -> None:
         raise ValueError(f"{name} must be 2-D with unit inner stride")
 
 
-GEMM_VARIANTS = {"default": 0, "pingpong8sf": 52, "pingpong8": 1, "pingpong8b": 4,
+GEMM_VARIANTS = {"default": 0, "pingpong8": 1, "pingpong8b": 4,
                  "pingpong8c": 5, "pingpong8cw": 10, "pingpong8cwe": 11,
                  "pingpong8cwn": 12, "pingpong8cwne": 13, "tile128": 15,
                  "tile256x128": 16, "tile160": 17, "tile256x160": 18, "tile128w4": 19,
@@ -148,10 +148,6 @@ def gemm_bf16(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
                              "(masked tiles: N % 4, K % 8; others: whole tiles, K % 128)")
     elif variant == "default":
         _default_ws_bytes(m, n, k)  # the native plan is the one authority on what it serves
-    elif variant == "pingpong8sf":  # stream-K fractional mode (one round, even K split)
-        if not skf_ws_bytes(m, n, k):
-            raise ValueError(f"shape ({m},{n},{k}) not served by stream-K fractional mode "
-                             "(N % 8, K % 8, K >= 256; one round of 256x256 tiles, some cut)")
     elif variant in ("pingpong8s", "pingpong8s_rev"):  # stream-K (two-round or split mode)
         if not sk_ws_bytes(m, n, k):
             raise ValueError(f"shape ({m},{n},{k}) not served by stream-K (N % 8, K % 8, K >= 128; "
@@ -169,8 +165,6 @@ def gemm_bf16(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
         raise ValueError("out has the wrong shape")
     if variant in ("pingpong8s", "pingpong8s_rev"):
         return _gemm_bf16_sk(a, b, out, rev=variant == "pingpong8s_rev")
-    if variant == "pingpong8sf":
-        return _gemm_bf16_sk(a, b, out, frac=True)
     if splits > 1:
         if variant not in MASKED_TILES:
             raise ValueError(f"split-K runs on {sorted(MASKED_TILES)}, not {variant}")
@@ -208,15 +202,6 @@ def gemm_bf16(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
         a.stride(0), b.stride(0), out.stride(0), stream_handle())
     check(rc, "ntm_gemm_bf16")
     return out
-
-
-def skf_ws_bytes(m: int, n: int, k: int) -> int:
-    """Workspace of stream-K's fractional mode ("pingpong8sf") for (M, N, K) on
-    this device; 0 when it does not serve the shape (more than one round of
-    256x256 tiles, or no tile would be cut)."""
-    if m <= 0 or n <= 0 or k <= 0:
-        return 0
-    return int(lib().ntm_skf_ws_bytes(m, n, k))
 
 
 def sk_ws_bytes(m: int, n: int, k: int) -> int:
@@ -265,16 +250,14 @@ def sk_xcc_error(device=None, clear: bool = True) -> int:
     return v
 
 
-def _gemm_bf16_sk(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, rev: bool = False,
-                  frac: bool = False) -> torch.Tensor:
+def _gemm_bf16_sk(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, rev: bool = False) -> torch.Tensor:
     """Stream-K (gemm_bf16_sk.hpp): fp32 partials of the split tiles and one
     counter per split in this stream's cached workspace (_sk_workspace)."""
     m, k = a.shape
     n = b.shape[0]
-    wsb = skf_ws_bytes(m, n, k) if frac else sk_ws_bytes(m, n, k)
+    wsb = sk_ws_bytes(m, n, k)
     ws = _sk_workspace(a.device, wsb)
-    fn = (lib().ntm_gemm_bf16_skf if frac else
-          lib_experimental().ntm_gemm_bf16_sk_rev if rev else lib().ntm_gemm_bf16_sk)
+    fn = lib_experimental().ntm_gemm_bf16_sk_rev if rev else lib().ntm_gemm_bf16_sk
     rc = fn(a.data_ptr(), b.data_ptr(), out.data_ptr(), m, n, k, a.stride(0), b.stride(0),
             out.stride(0), ws.data_ptr(), wsb, stream_handle())
     check(rc, "ntm_gemm_bf16_sk")

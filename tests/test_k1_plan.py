@@ -293,43 +293,3 @@ def test_plan_and_launch_agree_on_the_cu_count(k1_plan, cus):
         kernels._DEFAULT_WS.clear()
     assert lib().ntm_plan_cus() == 256      # no GPU here: the documented default
 
-
-def _frac_model(ntiles, Tp, cus=256, max_parts=16):
-    """Python mirror of sk_decompose_frac / gemm_bf16_skf_kernel's ranges."""
-    W = cus // 8
-    nmax, nmin = (ntiles + 7) // 8, (ntiles // 8 if ntiles >= 8 else 1)
-    F = min(W, nmax * max_parts, nmin * Tp)
-    if ntiles > cus or Tp < 2 or F <= nmax:
-        return None
-    out = []
-    for x in range(8):
-        nx = (ntiles - x + 7) // 8
-        if nx <= 0:
-            continue
-        U = nx * Tp
-        ranges = [(j * U // F, (j + 1) * U // F) for j in range(F)]
-        out.append((x, nx, U, F, ranges))
-    return out
-
-
-@pytest.mark.parametrize("ntiles,Tp", [(143, 113), (182, 110), (84, 70), (16, 8), (1, 2),
-                                       (255, 40), (129, 3), (8, 2), (57, 2), (250, 2)])
-def test_fractional_ranges_cover_each_pair_once(ntiles, Tp):
-    """The fractional stream-K decomposition: per XCD the F ranges are non-empty,
-    partition [0, U) and span at most two tiles; tile k's parts are exactly the
-    workgroups frac_first_part(k) .. frac_last_part(k), at most 16 of them -
-    so every cut tile's counter reaches its part count and is combined once."""
-    model = _frac_model(ntiles, Tp)
-    if model is None:
-        return
-    for x, nx, U, F, ranges in model:
-        assert all(b > a for a, b in ranges)                         # non-empty
-        assert ranges[0][0] == 0 and ranges[-1][1] == U
-        assert all(ranges[i][1] == ranges[i + 1][0] for i in range(F - 1))
-        for j, (a, b) in enumerate(ranges):
-            assert (b - 1) // Tp - a // Tp <= 1                      # <= two tiles
-        for k in range(nx):
-            jf = ((k * Tp + 1) * F - 1) // U
-            jl = ((k + 1) * Tp * F - 1) // U
-            holders = [j for j, (a, b) in enumerate(ranges) if a < (k + 1) * Tp and b > k * Tp]
-            assert holders == list(range(jf, jl + 1)) and len(holders) <= 16

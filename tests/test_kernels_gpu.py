@@ -893,40 +893,3 @@ def test_stream_k_split_mode_vs_torch_fp32(ops, m, n, k):
         assert torch.equal(ops.gemm_bf16(a, b, variant="pingpong8s"), first)
     assert ops.sk_xcc_error() == 0   # every slice of a tile ran on the combiner's XCD
 
-
-SKF_SHAPES = [(2792, 3160, 14432),  # 143 tiles (0.56 round): every CU gets 0.56 of a tile
-              (1560, 6496, 14080),  # 182 tiles, 3 parts max
-              (2840, 1768, 8904),   # 84 tiles: 32 CUs per XCD over 10-11 tiles
-              (4152, 1096, 16056),  # K % 128 != 0
-              (1000, 1000, 1000),   # 16 tiles, partial K
-              (256, 256, 256),      # 1 tile on one XCD: 2 pairs, 2 parts
-              (2008, 8120, 3736)]   # 256 tiles exactly: no tile cut -> not served
-
-
-@pytest.mark.parametrize("m,n,k", SKF_SHAPES)
-def test_stream_k_fractional_vs_torch_fp32(ops, m, n, k):
-    """pingpong8sf (round 5, gemm_bf16_sk.hpp skf): one round of 256x256 tiles
-    whose K work is split evenly over every CU, cut tiles fixed up through fp32
-    partials (the last part to arrive sums all parts in part order). vs the fp32
-    product; columns past C never written; repeated launches bitwise equal
-    (counters left at 0); every part of a tile ran on the combiner's XCD."""
-    if not ops.kernels.skf_ws_bytes(m, n, k):
-        with pytest.raises(ValueError):
-            ops.gemm_bf16(torch.empty((m, k), dtype=torch.bfloat16, device="cuda"),
-                          torch.empty((n, k), dtype=torch.bfloat16, device="cuda"),
-                          variant="pingpong8sf")
-        assert ((m + 255) // 256) * ((n + 255) // 256) >= 256
-        return
-    a = _rand(ops, (m, k), 691 + k)
-    b = _rand(ops, (n, k), 693 + n)
-    out = torch.full((m, n + 8), 7.0, dtype=torch.bfloat16, device="cuda")
-    c = ops.gemm_bf16(a, b, out[:, :n], variant="pingpong8sf")
-    ref = a.float() @ b.float().T
-    atol, rtol = ops.gemm_tolerance(k)
-    err = (c.float() - ref).abs()
-    assert torch.all(err <= atol + rtol * ref.abs()), float(err.max())
-    assert torch.all(out[:, n:] == 7.0)
-    first = c.clone()
-    for _ in range(3):
-        assert torch.equal(ops.gemm_bf16(a, b, variant="pingpong8sf"), first)
-    assert ops.sk_xcc_error() == 0

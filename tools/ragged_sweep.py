@@ -22,7 +22,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from nvidia_terraform_modules_amd import ops  # noqa: E402
 
-CANDIDATES = ("pingpong8s", "pingpong8sf", "pingpong8cm", "tile128", "tile256x128", "tile160", "tile160x128",
+CANDIDATES = ("pingpong8s", "pingpong8cm", "tile128", "tile256x128", "tile160", "tile160x128",
               "tile128x160", "tile128x256")
 
 
@@ -78,8 +78,6 @@ def main():
         if args.candidates:
             for v in CANDIDATES:
                 if v == "pingpong8s" and not ops.sk_ws_bytes(m, n, k):
-                    continue
-                if v == "pingpong8sf" and not ops.kernels.skf_ws_bytes(m, n, k):
                     continue
                 fns[v] = lambda v=v: ops.gemm_bf16(a, b, c, variant=v)
         t = {name: [] for name in fns}

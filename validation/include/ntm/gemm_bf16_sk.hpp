@@ -90,8 +90,6 @@ struct SkArgs {
   int ntiles;
   int S = 0;      // split mode (at most half a round of tiles): K slices per tile, else 0
   unsigned long long* stamps = nullptr;  // STAMP builds: 16 per workgroup
-  int F = 0;      // fractional mode (one round): workgroups used per XCD, else 0
-  int P = 0;      // fractional mode: most parts any tile is cut into (partial slots per tile)
 };
 
 // Tiles, pairs and the whole-tile prefix for (M, N, K) on `cus` CUs.
@@ -126,58 +124,6 @@ __host__ __device__ inline bool sk_decompose(int M, int N, int K, int cus, SkArg
 }
 
 inline size_t sk_ws_bytes(int G) { return kCounterBytes + (size_t)G * 2 * kPartialBytes; }
-
-// Fractional mode (gemm_bf16_skf_kernel, one round of tiles): XCD x's n_x tiles
-// (v = x + 8k) as U = n_x Tp K-tile pairs, split into F EQUAL contiguous ranges
-// [j U / F, (j + 1) U / F), one per workgroup j of the XCD - every CU gets the
-// same K work whatever n_x is (split mode's S = W / n_x equal slices leave
-// W - S n_x CUs idle, and a 0.55-0.95 round of tiles cannot be split at all).
-// A range covers the end of one tile and the start of the next (or lies inside
-// one tile); tile k's parts are workgroups jf(k) .. jl(k). F = the XCD's
-// workgroups, capped so no tile is cut into more than kMaxFracParts parts.
-constexpr int kMaxFracParts = 16;
-
-__host__ __device__ inline int frac_first_part(int k, int Tp, int F, int U) {
-  return (int)((((long)k * Tp + 1) * F - 1) / U);      // the range holding pair k Tp
-}
-__host__ __device__ inline int frac_last_part(int k, int Tp, int F, int U) {
-  return (int)(((long)(k + 1) * Tp * F - 1) / U);      // ... holding pair (k + 1) Tp - 1
-}
-
-inline bool sk_decompose_frac(int M, int N, int K, int cus, SkArgs& s) {
-  if (M <= 0 || N <= 0 || K <= 0 || cus < 8 || (cus % 8) != 0 || cus + 8 > kErrWord) return false;
-  s.ntiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
-  s.G = cus;
-  s.Tp = (K + 2 * BK - 1) / (2 * BK);
-  s.S = 0;
-  s.D = 0;
-  const int W = cus / 8;
-  if (s.ntiles > cus || s.Tp < 2) return false;  // one round; a tile of >= 2 pairs
-  const int nmax = (s.ntiles + 7) / 8, nmin = s.ntiles >= 8 ? s.ntiles / 8 : 1;
-  int F = W;
-  if (F > nmax * kMaxFracParts) F = nmax * kMaxFracParts;
-  // every range non-empty on every XCD that has tiles (U >= F): a part that
-  // never arrives would leave its tile uncombined
-  if (F > nmin * s.Tp) F = nmin * s.Tp;
-  if (F <= nmax) return false;                   // no tile would be cut: data-parallel
-  s.F = F;
-  int pmax = 1;
-  for (int x = 0; x < 8; ++x) {
-    const int nx = (s.ntiles - x + 7) / 8;
-    if (nx <= 0) continue;
-    const int U = nx * s.Tp;
-    for (int k = 0; k < nx; ++k) {
-      const int parts = frac_last_part(k, s.Tp, F, U) - frac_first_part(k, s.Tp, F, U) + 1;
-      pmax = parts > pmax ? parts : pmax;
-    }
-  }
-  s.P = pmax;
-  return pmax <= kMaxFracParts;
-}
-
-inline size_t sk_ws_bytes_frac(const SkArgs& s) {
-  return kCounterBytes + (size_t)s.ntiles * s.P * kPartialBytes;
-}
 
 __host__ __device__ inline bool shape_ok_sk(int M, int N, int K) {
   return M > 0 && N > 0 && (N % 8) == 0 && K >= 2 * BK && (K % 8) == 0;
@@ -518,104 +464,6 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_sks_kernel(GemmArgs p, 
   for (int q = 0; q < s.S; ++q) add_partial(part + (size_t)q * (kPartialBytes / 4), acc);
   reset_counter(cnt);
   store_tile_epi<false, kEpiSk>(p, c, acc, m0, n0, lane_now());
-}
-
-// Fractional mode (see sk_decompose_frac): workgroup j of XCD x takes pairs
-// [j U / F, (j + 1) U / F) of its XCD's tile list. It runs the part that STARTS
-// a tile (pair 0: the head of the next tile) before the part that ENDS one (the
-// tail of the previous), so at any moment an XCD's heads are all at one K
-// offset and its tails at another (two panel streams in L2, not F). A tile cut
-// into P parts: each part writes its fp32 partial (write-through) to slot
-// (tile, part) and adds to the tile's counter - 1 + its XCC id << 6 + id^2 <<
-// 15 (count in bits 0-5, P <= 16); the part that draws P - 1 checks every part
-// ran on its XCD, sums all P partials in part order (C does not depend on who
-// combines), stores C and resets the counter. An uncut tile stores directly.
-template <bool TAIL>
-__global__ void __launch_bounds__(kThreads, 2) gemm_bf16_skf_kernel(GemmArgs p, SkArgs s) {
-  __shared__ __attribute__((aligned(16))) char smem[kLdsBytes3 + 16];  // ONE __shared__ array
-  int* bcast = (int*)(smem + kLdsBytes3);
-  const int b = (int)blockIdx.x;
-  const int x = b & 7, j = b >> 3;
-  const int nx = (s.ntiles - x + 7) >> 3;
-  if (nx <= 0 || j >= s.F) return;  // uniform: the whole workgroup leaves
-  const int U = nx * s.Tp;
-  const int u0 = __builtin_amdgcn_readfirstlane((int)((long)j * U / s.F));
-  const int u1 = __builtin_amdgcn_readfirstlane((int)((long)(j + 1) * U / s.F));
-  if (u1 <= u0) return;
-  const int k0 = u0 / s.Tp, k1 = (u1 - 1) / s.Tp;
-  const int pa0 = u0 - k0 * s.Tp, pb1 = u1 - k1 * s.Tp;
-  const unsigned xc = xcc_id();
-  const unsigned tag = 1u + (xc << 6) + ((xc * xc) << 15);
-  Ctx c;
-  c.lds = smem;
-  const int lane = threadIdx.x & 63;
-  c.w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  c.wr = c.w >> 2;
-  c.wc = c.w & 3;
-  c.frag_off = (lane & 15) * 64 + ((lane >> 4) ^ ((lane >> 2) & 2)) * 16;
-  if constexpr (TAIL) {
-    c.K = p.K;
-    const int r = lane >> 2;
-    c.lane_col = ((lane & 3) ^ (((r >> 3) & 1) << 1)) * 8;
-  }
-  Frags3 f;
-  f32x4 acc[2][2][4][2];
-  // one range spans at most two tiles (U / F <= Tp): head of k1 first, then k0's part
-  const int nseg = k1 > k0 ? 2 : 1;
-  for (int q = 0; q < nseg; ++q) {
-    const int k = (nseg == 2 && q == 0) ? k1 : k0;
-    const int pa = k == k0 ? pa0 : 0;
-    const int pb = k == k1 ? pb1 : s.Tp;
-    const int v = x + 8 * k;  // the tile's index in the grid raster
-    int tm, tn;
-    tile_coords_of<kGroupM>(v, s.ntiles, p.M, p.N, tm, tn);
-    const int m0 = __builtin_amdgcn_readfirstlane(tm * BM);
-    const int n0 = __builtin_amdgcn_readfirstlane(tn * BN);
-    set_sources(p, c, m0, n0, lane_now());
-    zero_acc(acc);
-    k_range<TAIL>(p, c, f, acc, 2 * pa, 2 * pb);
-    const int jf = frac_first_part(k, s.Tp, s.F, U);
-    const int parts = frac_last_part(k, s.Tp, s.F, U) - jf + 1;
-    bool store = parts == 1;
-    if (!store) {
-      float* part = s.ws + (kCounterBytes + (size_t)v * s.P * kPartialBytes) / 4;
-      unsigned* cnt = s.cnt + v;
-      write_partial(part + (size_t)(j - jf) * (kPartialBytes / 4), acc);
-      const unsigned o = counter_add<true>(cnt, tag, bcast);
-      if ((o & 0x3Fu) == (unsigned)(parts - 1)) {  // uniform: the last part combines
-        const unsigned all = o + tag, P = (unsigned)parts;
-        if (((all >> 6) & 0x1FFu) != P * xc || (all >> 15) != P * xc * xc)
-          report_xcc_error(s.cnt, 2u << 28 | (unsigned)(v & 0xFFFF) << 8 | (xc & 0xF) << 4);
-        acquire_all();
-        zero_acc(acc);
-        for (int i = 0; i < parts; ++i) add_partial(part + (size_t)i * (kPartialBytes / 4), acc);
-        reset_counter(cnt);
-        store = true;
-      }
-    }
-    if (store) store_tile_epi<false, kEpiSk>(p, c, acc, m0, n0, lane_now());
-    raw_barrier();  // staging reads done before the next prologue's DMA
-  }
-}
-
-// Launch the fractional mode on `cus` workgroups; workspace sk_ws_bytes_frac,
-// counter block zero on entry (left zero). hipErrorInvalidValue where it does
-// not serve (more than one round, or no tile would be cut).
-inline hipError_t launch_gemm_bf16_skf(const GemmArgs& a, int cus, void* ws, size_t ws_bytes,
-                                       hipStream_t stream) {
-  SkArgs s;
-  if (!shape_ok_sk(a.M, a.N, a.K) || a.rowsum || a.lda < a.K || a.ldb < a.K || a.ldc < a.N ||
-      (a.lda % 8) || (a.ldb % 8) || (a.ldc % 8) || !sk_decompose_frac(a.M, a.N, a.K, cus, s) ||
-      ws == nullptr || ws_bytes < sk_ws_bytes_frac(s) || (reinterpret_cast<size_t>(ws) % 16))
-    return hipErrorInvalidValue;
-  s.ws = (float*)ws;
-  s.cnt = (unsigned*)ws;
-  const dim3 g((unsigned)s.G), blk(kThreads);
-  if (a.K % (2 * BK))
-    hipLaunchKernelGGL((gemm_bf16_skf_kernel<true>), g, blk, 0, stream, a, s);
-  else
-    hipLaunchKernelGGL((gemm_bf16_skf_kernel<false>), g, blk, 0, stream, a, s);
-  return hipGetLastError();
 }
 
 // Launch on `cus` workgroups with the caller's workspace (sk_ws_bytes(cus)).

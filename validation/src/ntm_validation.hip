@@ -524,33 +524,6 @@ NTM_API int ntm_gemm_bf16_sk(const void* A, const void* B, void* C, int M, int N
                                                S(stream));
 }
 
-// Stream-K fractional mode ("pingpong8sf", gemm_bf16_sk.hpp skf): one round of
-// 256x256 tiles whose K work is split EVENLY over every CU (cut tiles fixed up
-// through fp32 partials). ntm_skf_ws_bytes = 0: it does not serve (M, N, K).
-NTM_API size_t ntm_skf_ws_bytes(int M, int N, int K) {
-  ntm::gemmsk::SkArgs s;
-  if (!ntm::gemmsk::shape_ok_sk(M, N, K) ||
-      !ntm::gemmsk::sk_decompose_frac(M, N, K, ntm::gemm6::pp6_grid(1 << 30), s))
-    return 0;
-  return ntm::gemmsk::sk_ws_bytes_frac(s);
-}
-
-NTM_API int ntm_gemm_bf16_skf(const void* A, const void* B, void* C, int M, int N, int K, int lda,
-                              int ldb, int ldc, void* ws, size_t ws_bytes, void* stream) {
-  ntm::gemm::GemmArgs a;
-  a.A = (const __bf16*)A;
-  a.B = (const __bf16*)B;
-  a.C = (__bf16*)C;
-  a.M = M;
-  a.N = N;
-  a.K = K;
-  a.lda = lda;
-  a.ldb = ldb;
-  a.ldc = ldc;
-  return (int)ntm::gemmsk::launch_gemm_bf16_skf(a, ntm::gemm6::pp6_grid(1 << 30), ws, ws_bytes,
-                                                S(stream));
-}
-
 // The default dispatch with split-K allowed: ws (ws_bytes) is the caller's
 // workspace; when the split-K plan needs more than ws_bytes (or ws is null) the
 // unsplit plan runs instead.
