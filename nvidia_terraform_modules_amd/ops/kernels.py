@@ -37,7 +37,7 @@ GEMM_VARIANTS = {"default": 0, "pingpong8": 1, "pingpong8b": 4,
                  "tile256x128w4": 20, "tile160w4": 21, "pingpong8cm": 22, "tile160x128": 23,
                  "tile128x160": 24, "tile128x256": 26, "pingpong8o": 25,
                  "pp8o_g128": 41, "pp8o_g128_nostore": 42, "pp8o_nostore": 43,
-                 "pingpong8om": 47, "pingpong8od": 48, "pingpong8s": 49,
+                 "pingpong8om": 47, "pingpong8od": 48, "pingpong8s": 49, "pingpong8op": 53,
                  "pingpong8omd": 51}
 
 
@@ -47,7 +47,7 @@ EXPERIMENTAL_VARIANTS = frozenset({"pingpong8", "pingpong8cw",
                                    "pingpong8cwe", "pingpong8cwn", "pingpong8cwne",
                                    "tile128w4", "tile256x128w4", "tile160w4",
                                    "pp8o_g128", "pp8o_g128_nostore", "pp8o_nostore",
-                                   "pingpong8od", "pingpong8omd"})
+                                   "pingpong8od", "pingpong8omd", "pingpong8op"})
 
 # (TM, TN) of the 4-wave tile kernels (gemm_bf16_t128.hpp)
 TILE_SHAPES = {"tile128": (128, 128), "tile256x128": (256, 128), "tile160": (160, 160),
@@ -701,6 +701,24 @@ def clock_summary(stamps: torch.Tensor, ms_per_launch: float) -> dict:
             spread.append(max(per) / min(per) - 1.0)
     res["bound_GHz"] = round(sorted(bound)[len(bound) // 2], 4) if bound else None
     res["xcc_clock_spread_pct"] = round(100 * sorted(spread)[len(spread) // 2], 2) if spread else None
+    # when each XCD's last workgroup ended, after the launch's first start (us,
+    # median over launches): the gap between the first and the last XCD to finish
+    # is how long the faster XCDs idle at the end of every launch
+    rt0 = sv[:, :, 1].min(dim=1).values                      # [steps]
+    fin = {x: [] for x in ids}
+    for i in range(steps):
+        for x in ids:
+            sel = xcc[i] == x
+            if bool(sel.any()):
+                fin[x].append(float((sv[i, :, 3][sel].max() - rt0[i]) / 100.0))
+    res["per_xcc_finish_us"] = {str(x): round(sorted(v)[len(v) // 2], 2) for x, v in fin.items() if v}
+    idle = []
+    for i in range(steps):
+        ends = [float((sv[i, :, 3][xcc[i] == x].max() - rt0[i]) / 100.0)
+                for x in ids if bool((xcc[i] == x).any())]
+        if ends:
+            idle.append(max(ends) - min(ends))
+    res["xcc_finish_spread_us"] = round(sorted(idle)[len(idle) // 2], 2) if idle else None
     res["per_launch_cycles_median"] = [int(x) for x in cyc.tolist()]
     res["per_launch_window_us_median"] = [round(x, 2) for x in win.tolist()]
     return res

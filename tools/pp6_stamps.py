@@ -35,6 +35,10 @@ def main() -> int:
     ap.add_argument("--k", type=int, default=8192)
     ap.add_argument("--warm-s", type=float, default=1.0)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--grids", default="256,128")
+    ap.add_argument("--modes", default="1,0",
+                    help="1 stored, 0 not stored, 2 stored + spread (shipping), "
+                         "3 = 2 + next-tile L2 touches (PF), 4 = not stored + PF")
     args = ap.parse_args()
     m = n = args.size
     k = args.k
@@ -43,8 +47,9 @@ def main() -> int:
     c = torch.empty((m, n), dtype=torch.bfloat16, device="cuda")
     L = lib_experimental()
     base = {}
-    for grid in (256, 128):
-        for store in (1, 0):
+    modes = [int(x) for x in args.modes.split(",")]
+    for grid in (int(g) for g in args.grids.split(",")):
+        for store in modes:
             st = torch.zeros((grid, 17), dtype=torch.int64, device="cuda")
 
             def run():
@@ -66,15 +71,14 @@ def main() -> int:
             tot = float(d.sum(dim=1).median())
             row = {"grid": grid, "store": store, "phase_cycles_median": dict(zip(PHASES, [
                 round(x) for x in med])), "window_cycles_median": round(tot)}
-            if store == 0:
-                base[grid] = (med, tot)
-            else:
-                base.setdefault(("s", grid), (med, tot))
+            base[(store, grid)] = (med, tot)
             print(json.dumps(row), flush=True)
-        (ms, ts), (mn, tn) = base[("s", grid)], base[grid]
-        print(json.dumps({"grid": grid, "store_minus_nostore_cycles": dict(zip(
-            PHASES, [round(x - y) for x, y in zip(ms, mn)])), "window_excess_cycles": round(ts - tn)}),
-            flush=True)
+        for a_, b_ in ((1, 0), (3, 2), (4, 0)):
+            if (a_, grid) in base and (b_, grid) in base:
+                (ms, ts), (mn, tn) = base[(a_, grid)], base[(b_, grid)]
+                print(json.dumps({"grid": grid, "modes": [a_, b_], "minus_cycles": dict(zip(
+                    PHASES, [round(x - y) for x, y in zip(ms, mn)])),
+                    "window_delta_cycles": round(ts - tn)}), flush=True)
     return 0
 
 
