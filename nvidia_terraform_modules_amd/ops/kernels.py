@@ -37,7 +37,7 @@ GEMM_VARIANTS = {"default": 0, "pingpong8": 1, "pingpong8b": 4,
                  "tile256x128w4": 20, "tile160w4": 21, "pingpong8cm": 22, "tile160x128": 23,
                  "tile128x160": 24, "tile128x256": 26, "pingpong8o": 25,
                  "pp8o_g128": 41, "pp8o_g128_nostore": 42, "pp8o_nostore": 43,
-                 "pingpong8om": 47, "pingpong8od": 48, "pingpong8s": 49, "pingpong8op": 53,
+                 "pingpong8om": 47, "pingpong8od": 48, "pingpong8s": 49,
                  "pingpong8omd": 51}
 
 
@@ -47,7 +47,7 @@ EXPERIMENTAL_VARIANTS = frozenset({"pingpong8", "pingpong8cw",
                                    "pingpong8cwe", "pingpong8cwn", "pingpong8cwne",
                                    "tile128w4", "tile256x128w4", "tile160w4",
                                    "pp8o_g128", "pp8o_g128_nostore", "pp8o_nostore",
-                                   "pingpong8od", "pingpong8omd", "pingpong8op"})
+                                   "pingpong8od", "pingpong8omd"})
 
 # (TM, TN) of the 4-wave tile kernels (gemm_bf16_t128.hpp)
 TILE_SHAPES = {"tile128": (128, 128), "tile256x128": (256, 128), "tile160": (160, 160),

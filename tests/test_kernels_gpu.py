@@ -690,25 +690,6 @@ def test_persistent_overlap_vs_torch_fp32(ops, variant, m, n, k):
     assert torch.equal(c, ops.gemm_bf16(a, b, variant="pingpong8c"))
 
 
-@pytest.mark.parametrize("m,n,k", [(256, 256, 384), (1024, 512, 1024), (4608, 4608, 512),
-                                   (8192, 8192, 384), (2304, 1792, 768), (8192, 8192, 8192)])
-def test_persistent_l2_touch_build_vs_torch_fp32(ops, m, n, k):
-    """pingpong8op (round 5): the shipping pingpong8od plus the
-    next tile's K-tiles 0 / 1 touched into L2 during K-tiles T-4 / T-3 (LDS-DMA
-    into the scratch slice, counted in the phase waits). K >= 384 (T >= 6; the
-    shortest, T = 6, peels every steady pair). vs fp32, and bitwise equal to the
-    shipping build: the touches change no MFMA operand."""
-    a = _rand(ops, (m, k), 611 + k)
-    b = _rand(ops, (n, k), 613 + n)
-    c = ops.gemm_bf16(a, b, variant="pingpong8op")
-    ref = a.float() @ b.float().T
-    atol, rtol = ops.gemm_tolerance(k)
-    assert torch.all((c.float() - ref).abs() <= atol + rtol * ref.abs())
-    assert torch.equal(c, ops.gemm_bf16(a, b, variant="pingpong8od"))
-    with pytest.raises(RuntimeError):      # T = 4: refused, nothing launched
-        ops.gemm_bf16(a[:, :256].contiguous(), b[:, :256].contiguous(), variant="pingpong8op")
-
-
 @pytest.mark.parametrize("m,n,k", [(256, 256, 512), (2048, 1024, 1024), (4608, 4608, 512),
                                    (8192, 8192, 2048), (8192, 8192, 512)])
 def test_fp8_persistent_overlap_vs_torch_fp32(ops, m, n, k):

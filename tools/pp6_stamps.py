@@ -37,8 +37,7 @@ def main() -> int:
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--grids", default="256,128")
     ap.add_argument("--modes", default="1,0",
-                    help="1 stored, 0 not stored, 2 stored + spread (shipping), "
-                         "3 = 2 + next-tile L2 touches (PF), 4 = not stored + PF")
+                    help="1 stored, 0 not stored, 2 stored + spread (the shipping build)")
     args = ap.parse_args()
     m = n = args.size
     k = args.k
@@ -73,7 +72,7 @@ def main() -> int:
                 round(x) for x in med])), "window_cycles_median": round(tot)}
             base[(store, grid)] = (med, tot)
             print(json.dumps(row), flush=True)
-        for a_, b_ in ((1, 0), (3, 2), (4, 0)):
+        for a_, b_ in ((1, 0), (2, 0)):
             if (a_, grid) in base and (b_, grid) in base:
                 (ms, ts), (mn, tn) = base[(a_, grid)], base[(b_, grid)]
                 print(json.dumps({"grid": grid, "modes": [a_, b_], "minus_cycles": dict(zip(

@@ -84,8 +84,6 @@ def main():
         shapes = SHAPES_FP8 + SHAPES_RAGGED if fp8 else SHAPES_160 if tn == 160 else SHAPES
         if v.startswith("pingpong8o"):
             shapes = SHAPES_PERSIST + (SHAPES_PERSIST_RAGGED if v in ("pingpong8om", "pingpong8omd") else [])
-            if v == "pingpong8op":   # the L2-touch build needs K >= 384 (T >= 6)
-                shapes = [s for s in shapes if s[2] >= 384] + [(8192, 8192, 384), (2048, 2048, 640)]
         if v.startswith("pingpong8s"):
             shapes = SHAPES_SK if v == "pingpong8s" else SHAPES_SK[:7]  # REV: two-round mode
         if splits > 1:

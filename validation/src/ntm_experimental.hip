@@ -76,9 +76,8 @@ NTM_API int ntm_gemm_bf16_experimental(int variant, const void* A, const void* B
     // stores) were removed after measurement (profiles/r4_stg/).
     // 48: boundary stores spread one block per phase (SPREAD) = the shipping 25
     case 48: return (int)ntm::gemm6::launch_gemm_bf16_pp6<1, 0, true>(a, S(stream));
-    // pingpong8op (round 5): the shipping pingpong8od + the next tile's K-tiles
-    // 0 / 1 touched into L2 over K-tiles T-4 / T-3 (gemm_bf16_pp6.hpp PF)
-    case 53: return (int)ntm::gemm6::launch_gemm_bf16_pp6<1, 0, true, true>(a, S(stream));
+    // 53 (round 5, pingpong8op: the next tile's K-tiles 0 / 1 touched into L2 over
+    // K-tiles T-4 / T-3) was removed after measurement (profiles/r5_pf/).
     // 51: pingpong8om (ragged C) with the spread boundary stores
     case 51: return (int)ntm::gemm6::launch_gemm_bf16_pp6_masked<1, true>(a, S(stream));
     default: return (int)hipErrorInvalidValue;
@@ -126,8 +125,7 @@ NTM_API int ntm_gemm_bf16_sk_stamp(const void* A, const void* B, void* C, int M,
 // pingpong8o boundary-phase stamps (gemm_bf16_pp6.hpp STAMP 2): grid 128 or 256
 // workgroups (a multiple of 8, <= tiles, each workgroup >= 2 tiles), store 1 =
 // C stored (nontemporal) / 0 = not stored / 2 = stored, spread over the boundary
-// phases (the shipping build) / 3 = 2 + the next tile's panels touched into L2
-// (PF) / 4 = not stored + PF; stamps: 17 u64 per workgroup.
+// phases (the shipping build); stamps: 17 u64 per workgroup.
 NTM_API int ntm_gemm_bf16_pp6_stamp(int grid, int store, const void* A, const void* B, void* C,
                                     int M, int N, int K, int lda, int ldb, int ldc, void* stamps,
                                     void* stream) {
@@ -139,8 +137,6 @@ NTM_API int ntm_gemm_bf16_pp6_stamp(int grid, int store, const void* A, const vo
     case 0: return (int)launch_gemm_bf16_pp6_grid<2, 2>(a, grid, S(stream));
     case 1: return (int)launch_gemm_bf16_pp6_grid<1, 2>(a, grid, S(stream));
     case 2: return (int)launch_gemm_bf16_pp6_grid<1, 2, true>(a, grid, S(stream));
-    case 3: return (int)launch_gemm_bf16_pp6_grid<1, 2, true, true>(a, grid, S(stream));
-    case 4: return (int)launch_gemm_bf16_pp6_grid<2, 2, false, true>(a, grid, S(stream));
     default: return (int)hipErrorInvalidValue;
   }
 }
