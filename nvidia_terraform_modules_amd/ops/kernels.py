@@ -47,7 +47,7 @@ EXPERIMENTAL_VARIANTS = frozenset({"pingpong8", "pingpong8cw",
                                    "pingpong8cwe", "pingpong8cwn", "pingpong8cwne",
                                    "tile128w4", "tile256x128w4", "tile160w4",
                                    "pp8o_g128", "pp8o_g128_nostore", "pp8o_nostore",
-                                   "pingpong8od", "pingpong8omd"})
+                                   "pingpong8od", "pingpong8omd", "pingpong8om"})
 
 # (TM, TN) of the 4-wave tile kernels (gemm_bf16_t128.hpp)
 TILE_SHAPES = {"tile128": (128, 128), "tile256x128": (256, 128), "tile160": (160, 160),

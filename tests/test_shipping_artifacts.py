@@ -38,8 +38,6 @@ ALLOWED_K1 = {
     "ntm::gemm6::gemm_bf16_pp6_kernel<1, 0, false, false, true, false>",
     "ntm::gemm6::gemm_bf16_pp6_kernel<1, 1, false, false, true, false>",  # clock stamps
     "ntm::gemm6::gemm_bf16_pp6_kernel<1, 0, false, false, true, true>",   # K1-fp8
-    "ntm::gemm6::gemm_bf16_pp6_kernel<1, 0, true, false, false, false>",  # pingpong8om
-    "ntm::gemm6::gemm_bf16_pp6_kernel<1, 0, true, true, false, false>",   # + partial K
     # stream-K over the last two rounds of 256x256 tiles (pingpong8s <TAIL, REV, STAMP>)
     "ntm::gemmsk::gemm_bf16_sk_kernel<false, false, false>",
     "ntm::gemmsk::gemm_bf16_sk_kernel<true, false, false>",
@@ -111,5 +109,6 @@ def test_shipping_artifact_has_only_default_dispatch_k1(path):
 def test_experimental_library_holds_the_experiments():
     ks = _kernels(EXP)
     for fam in ("gemm_bf16_pp3_stamp_kernel", "gemm_bf16_sk_kernel<false, true, false>", "mfma_rate_kernel",
-                "mfma_f8_probe_kernel"):
+                "mfma_f8_probe_kernel",
+                "gemm_bf16_pp6_kernel<1, 0, true, false, false, false>"):   # pingpong8om
         assert any(fam in k for k in ks), fam

@@ -78,6 +78,13 @@ NTM_API int ntm_gemm_bf16_experimental(int variant, const void* A, const void* B
     case 48: return (int)ntm::gemm6::launch_gemm_bf16_pp6<1, 0, true>(a, S(stream));
     // 53 (round 5, pingpong8op: the next tile's K-tiles 0 / 1 touched into L2 over
     // K-tiles T-4 / T-3) was removed after measurement (profiles/r5_pf/).
+    // 47: pingpong8om, the persistent overlap kernel on ragged C (masked edge
+    // tiles, partial K; pingpong8cm where it does not serve). Off the plan since
+    // round 4 (profiles/r4_om/), moved out of the shipping library in round 5.
+    case 47:
+      if (!ntm::gemm6::shape_ok6m(M, N, K) || (lda % 8) || (ldb % 8) || (ldc % 8))
+        return (int)ntm::gemm3::launch_gemm_bf16_pp3_masked(a, S(stream));
+      return (int)ntm::gemm6::launch_gemm_bf16_pp6_masked<1>(a, S(stream));
     // 51: pingpong8om (ragged C) with the spread boundary stores
     case 51: return (int)ntm::gemm6::launch_gemm_bf16_pp6_masked<1, true>(a, S(stream));
     default: return (int)hipErrorInvalidValue;

@@ -80,11 +80,9 @@ constexpr bool kPp6Spread = true;
 // to +2.0 % at 8192^3 and +2.6 to +4.4 % at 8192x8192x4096 over knob 30 on
 // each of 3 boxes (profiles/r4_ab/fp8_spread_*), never below it.
 constexpr bool kFp8Persistent = true;
-// 47 = pingpong8om, the persistent overlap kernel on ragged C (masked edge
-// tiles, partial K): the plan runs it in place of 22 when the masked 256x256
-// part has more tiles than CUs (round 4, profiles/r4_om/)
-constexpr int kPersistentMaskedVariant = 47;
-constexpr bool kPlanMaskedPersistent = false;
+// pingpong8om (variant 47, the persistent overlap kernel on ragged C) measured
+// no better than pingpong8cm under the plan (round 4, profiles/r4_om/), so the
+// plan never runs it; it lives in libntm_experimental.so (round 5 hygiene).
 
 // Tile-shape plan of the default dispatch: the smallest predicted time
 // rounds(tiles) x tile_area / efficiency over 256 CUs, where the efficiencies
@@ -289,11 +287,6 @@ inline K1Plan plan_k1(int M, int N, int K, bool splitk = false, bool fp8 = false
   if (fp8 && kFp8Persistent && best.feasible() && best.top_variant == kDefaultVariant &&
       ntm::gemm6::shape_ok6(best.top_rows, N, K))
     best.top_variant = kPersistentVariant;
-  // ... and on ragged C (masked edge tiles; K > 128, K % 8)
-  if (kPlanMaskedPersistent && !fp8 && best.feasible() && best.top_variant == 22 &&
-      ntm::gemm6::shape_ok6m(best.top_rows, N, K) &&
-      (double)((best.top_rows + 255) / 256) * ((N + 255) / 256) > kCUs)
-    best.top_variant = kPersistentMaskedVariant;
   if (!splitk || !best.feasible()) return best;
   // Split-K: C too small to fill 256 CUs with a long K (e.g. 280x6352x7568: 80
   // tiles of 160x160 -> 3 slices of 240 tiles, 631 vs 321 TF/s unsplit).
@@ -428,12 +421,6 @@ NTM_API int ntm_gemm_bf16_variant(int variant, const void* A, const void* B,
       if (!ntm::gemm6::shape_ok6(M, N, K) || (lda % 8) || (ldb % 8) || (ldc % 8))
         return (int)ntm::gemm3::launch_gemm_bf16_pp3(a, S(stream));
       return (int)ntm::gemm6::launch_gemm_bf16_pp6<1, 0, kPp6Spread>(a, S(stream));
-    // persistent + masked (pingpong8om): ragged C over more than one round of
-    // 256x256 tiles (K % 128, K >= 256; otherwise pingpong8cm)
-    case 47:
-      if (!ntm::gemm6::shape_ok6m(M, N, K) || (lda % 8) || (ldb % 8) || (ldc % 8))
-        return (int)ntm::gemm3::launch_gemm_bf16_pp3_masked(a, S(stream));
-      return (int)ntm::gemm6::launch_gemm_bf16_pp6_masked<1>(a, S(stream));
     // gemm_bf16_t128.hpp: 128x128 / 256x128 / 160x160 tiles on the wave-specialised
     // kernel (4 DMA-producer + 4 MFMA-consumer waves), 256x160 on the 4-wave one
     case 15: return (int)ntm::gemmt::launch_gemm_bf16_tile_ws<4>(a, S(stream));
