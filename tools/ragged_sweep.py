@@ -63,6 +63,8 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--candidates", action="store_true",
                     help="also time every candidate variant that serves the shape")
+    ap.add_argument("--splitk", default="",
+                    help="also time these split-K candidates, e.g. tile160/s2,tile256x128/s3")
     ap.add_argument("--lo", type=float, default=0.3)
     ap.add_argument("--hi", type=float, default=1.0)
     args = ap.parse_args()
@@ -80,6 +82,9 @@ def main():
                 if v == "pingpong8s" and not ops.sk_ws_bytes(m, n, k):
                     continue
                 fns[v] = lambda v=v: ops.gemm_bf16(a, b, c, variant=v)
+        for spec in (x for x in args.splitk.split(",") if x):
+            v, _, sp = spec.partition("/s")
+            fns[spec] = lambda v=v, sp=int(sp): ops.gemm_bf16(a, b, c, variant=v, splits=sp)
         t = {name: [] for name in fns}
         for r in range(args.rounds):
             order = list(fns.items())
