@@ -76,7 +76,7 @@ inline hipError_t launch_gemm_fp8_knob(const void* A, const void* B, __bf16* C, 
 // v_mfma_scale_f32_16x16x128_f8f6f4 (e4m3, unit scales), else
 // v_mfma_f32_16x16x32_bf16. out[wave] = {cycles, realtime ticks}; the sums
 // keep the accumulators live.
-template <bool F8>
+template <bool F8, bool W32 = false>
 __global__ void __launch_bounds__(256) mfma_rate_kernel(int iters, unsigned seed,
                                                         unsigned long long* out, float* sink) {
   const int lane = threadIdx.x & 63;
@@ -91,6 +91,10 @@ __global__ void __launch_bounds__(256) mfma_rate_kernel(int iters, unsigned seed
   f32x4 acc[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  typedef float f32x16 __attribute__((ext_vector_type(16)));
+  f32x16 acc32[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) acc32[j] = f32x16{};
   typedef int i32x4 __attribute__((ext_vector_type(4)));
   const i32x4 al = {a[0], a[1], a[2], a[3]}, bl = {b[0], b[1], b[2], b[3]};
   const unsigned long long t0 = __builtin_amdgcn_s_memtime();
@@ -102,6 +106,10 @@ __global__ void __launch_bounds__(256) mfma_rate_kernel(int iters, unsigned seed
     for (int j = 0; j < 8; ++j) {
       if constexpr (F8)
         ::ntm::gemm::mfma_f8_agpr(acc[j], a, b);
+      else if constexpr (W32)  // 32x32x16: 2x the MACs per instruction, 4 accumulators of 16
+        asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0"
+            : "+a"(acc32[j & 3])
+            : "v"(al), "v"(bl));
       else
         asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[j]) : "v"(al), "v"(bl));
     }
@@ -110,6 +118,10 @@ __global__ void __launch_bounds__(256) mfma_rate_kernel(int iters, unsigned seed
   float s = 0.f;
 #pragma unroll
   for (int j = 0; j < 8; ++j) s += acc[j][0] + acc[j][1] + acc[j][2] + acc[j][3];
+  if constexpr (W32) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) s += acc32[j][0] + acc32[j][15];
+  }
   const unsigned long long t1 = __builtin_amdgcn_s_memtime();
   const unsigned long long r1 = __builtin_amdgcn_s_memrealtime();
   if (s == 12345.678f) sink[0] = s;

@@ -164,11 +164,15 @@ NTM_API int ntm_gemm_bf16_stamp(int mode, const void* A, const void* B, void* C,
                                                       (unsigned long long*)stamps, S(stream));
 }
 
-// Matrix-core issue rate (gemm_fp8_diag.hpp mfma_rate_kernel); out: 2 u64 per
-// wave (grid x 4 waves), sink: 1 float.
+// Matrix-core issue rate (gemm_fp8_diag.hpp mfma_rate_kernel): f8 0 = bf16
+// 16x16x32, 1 = e4m3 16x16x128, 2 = bf16 32x32x16; out: 2 u64 per wave (grid x
+// 4 waves), sink: 1 float.
 NTM_API int ntm_mfma_rate(int f8, int grid, int iters, void* out, float* sink, void* stream) {
   if (grid <= 0 || iters <= 0) return (int)hipErrorInvalidValue;
-  if (f8)
+  if (f8 == 2)   // bf16 v_mfma_f32_32x32x16 (2x the MACs per instruction)
+    hipLaunchKernelGGL((ntm::fp8::mfma_rate_kernel<false, true>), dim3(grid), dim3(256), 0,
+                       S(stream), iters, 7u, (unsigned long long*)out, sink);
+  else if (f8)
     hipLaunchKernelGGL(ntm::fp8::mfma_rate_kernel<true>, dim3(grid), dim3(256), 0, S(stream),
                        iters, 7u, (unsigned long long*)out, sink);
   else
