@@ -124,6 +124,8 @@ def _declare_experimental(lib: ctypes.CDLL) -> None:
                                c_vp], c_int),
         "ntm_gemm_bf16_sk_rev": ([c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int,
                                   c_vp, c_size, c_vp], c_int),
+        "ntm_gemm_bf16_sk_nopair": ([c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int,
+                                     c_vp, c_size, c_vp], c_int),
         "ntm_gemm_bf16_sk_stamp": ([c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int,
                                     c_vp, c_size, c_vp, c_vp], c_int),
         "ntm_gemm_bf16_pp6_stamp": ([c_int, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int,

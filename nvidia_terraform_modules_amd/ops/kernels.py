@@ -148,7 +148,7 @@ def gemm_bf16(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
                              "(masked tiles: N % 4, K % 8; others: whole tiles, K % 128)")
     elif variant == "default":
         _default_ws_bytes(m, n, k)  # the native plan is the one authority on what it serves
-    elif variant in ("pingpong8s", "pingpong8s_rev"):  # stream-K (two-round or split mode)
+    elif variant in ("pingpong8s", "pingpong8s_rev", "pingpong8s_nopair"):  # stream-K
         if not sk_ws_bytes(m, n, k):
             raise ValueError(f"shape ({m},{n},{k}) not served by stream-K (N % 8, K % 8, K >= 128; "
                              "256x256 tiles: more than the CUs and not a multiple of them, or "
@@ -163,8 +163,9 @@ def gemm_bf16(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
     _require(out, "out", torch.bfloat16)
     if tuple(out.shape) != (m, n):
         raise ValueError("out has the wrong shape")
-    if variant in ("pingpong8s", "pingpong8s_rev"):
-        return _gemm_bf16_sk(a, b, out, rev=variant == "pingpong8s_rev")
+    if variant in ("pingpong8s", "pingpong8s_rev", "pingpong8s_nopair"):
+        return _gemm_bf16_sk(a, b, out, rev=variant == "pingpong8s_rev",
+                             nopair=variant == "pingpong8s_nopair")
     if splits > 1:
         if variant not in MASKED_TILES:
             raise ValueError(f"split-K runs on {sorted(MASKED_TILES)}, not {variant}")
@@ -250,14 +251,18 @@ def sk_xcc_error(device=None, clear: bool = True) -> int:
     return v
 
 
-def _gemm_bf16_sk(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, rev: bool = False) -> torch.Tensor:
+def _gemm_bf16_sk(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, rev: bool = False,
+                  nopair: bool = False) -> torch.Tensor:
     """Stream-K (gemm_bf16_sk.hpp): fp32 partials of the split tiles and one
-    counter per split in this stream's cached workspace (_sk_workspace)."""
+    counter per split in this stream's cached workspace (_sk_workspace).
+    rev / nopair: experimental builds (segments reversed; split mode's
+    S-partial protocol also at S = 2)."""
     m, k = a.shape
     n = b.shape[0]
     wsb = sk_ws_bytes(m, n, k)
     ws = _sk_workspace(a.device, wsb)
-    fn = lib_experimental().ntm_gemm_bf16_sk_rev if rev else lib().ntm_gemm_bf16_sk
+    fn = (lib_experimental().ntm_gemm_bf16_sk_rev if rev else
+          lib_experimental().ntm_gemm_bf16_sk_nopair if nopair else lib().ntm_gemm_bf16_sk)
     rc = fn(a.data_ptr(), b.data_ptr(), out.data_ptr(), m, n, k, a.stride(0), b.stride(0),
             out.stride(0), ws.data_ptr(), wsb, stream_handle())
     check(rc, "ntm_gemm_bf16_sk")

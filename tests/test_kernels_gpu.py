@@ -864,7 +864,8 @@ def test_default_plan_runs_stream_k(ops, m, n, k):
     assert torch.all((c.float() - ref).abs() <= atol + rtol * ref.abs())
 
 
-SKS_SHAPES = [(4672, 1472, 6696),   # 114 tiles: 2 K slices each
+SKS_SHAPES = [(4672, 1472, 6696),   # 114 tiles: 2 K slices each (head / tail protocol)
+              (4096, 2048, 8192),   # 128 tiles, whole K pairs: 2 slices
               (2048, 2048, 4096),   # 64 tiles: 4 slices
               (280, 6352, 7568),    # 50 tiles: 4 slices, K % 128 != 0
               (1000, 1000, 1000),   # 16 tiles: 8 slices of one pair, partial K
@@ -892,4 +893,7 @@ def test_stream_k_split_mode_vs_torch_fp32(ops, m, n, k):
     for _ in range(3):
         assert torch.equal(ops.gemm_bf16(a, b, variant="pingpong8s"), first)
     assert ops.sk_xcc_error() == 0   # every slice of a tile ran on the combiner's XCD
+    # the round-4 S-partial protocol: at S = 2 the head / tail protocol's own + other
+    # is the same fp32 sum as partial0 + partial1 (commutative), so bitwise equal
+    assert torch.equal(ops.gemm_bf16(a, b, variant="pingpong8s_nopair"), first)
 

@@ -42,8 +42,11 @@ ALLOWED_K1 = {
     "ntm::gemmsk::gemm_bf16_sk_kernel<false, false, false>",
     "ntm::gemmsk::gemm_bf16_sk_kernel<true, false, false>",
     # its split mode (at most half a round of tiles) <TAIL>
-    "ntm::gemmsk::gemm_bf16_sks_kernel<false>",
-    "ntm::gemmsk::gemm_bf16_sks_kernel<true>",
+    "ntm::gemmsk::gemm_bf16_sks_kernel<false, false>",
+    "ntm::gemmsk::gemm_bf16_sks_kernel<true, false>",
+    # ... at S = 2: the head / tail protocol <TAIL, PAIR> (round 5)
+    "ntm::gemmsk::gemm_bf16_sks_kernel<false, true>",
+    "ntm::gemmsk::gemm_bf16_sks_kernel<true, true>",
     "ntm::gemm2::gemm_bf16_pp2_kernel<false, 0>",
     "ntm::gemm2::gemm_bf16_pp2_kernel<false, 3>",
     "ntm::gemm2::gemm_bf16_pp2_kernel<true, 0>",

@@ -47,7 +47,9 @@ SHAPES_PERSIST_RAGGED = [(4472, 5688, 5832), (4608, 4360, 456), (5000, 4104, 768
 SHAPES_SK = [(4472, 5688, 5832), (4608, 4608, 1024), (6144, 6144, 2048), (4472, 5688, 200),
              (8192, 2304, 128), (5000, 4104, 4096), (1000, 17000, 384),
              # split mode (at most half a round of tiles)
-             (4672, 1472, 6696), (2048, 2048, 4096), (280, 6352, 7568), (1000, 1000, 1000)]
+             (4672, 1472, 6696), (2048, 2048, 4096), (280, 6352, 7568), (1000, 1000, 1000),
+             # split mode at S = 2: the head / tail protocol (round 5)
+             (4096, 2048, 8192), (2840, 1768, 8904), (256, 256, 256)]
 # shapes where the default plan runs stream-K (two-round / split mode) or a
 # split-K small tile picked by the ragged-C pricing (profiles/r4_sks)
 SHAPES_DEFAULT_SK = [(4672, 1472, 6696), (976, 5712, 9680), (4064, 1312, 5448),

@@ -409,12 +409,16 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_sk_kernel(GemmArgs p, S
 // Split mode ("pingpong8s" on at most half a round of tiles): XCD x's tiles
 // v = x + 8k (k < n_x), each in S K slices [s Tp / S, (s + 1) Tp / S) pairs;
 // workgroup j of the XCD runs slice j / n_x of tile k = j % n_x (the rest of
-// the XCD's workgroups exit at once). Every slice writes its fp32 partial
-// (write-through) and adds 1 to the tile's counter; the one that draws S - 1
-// sums the other S - 1 partials into its registers, stores C and resets the
-// counter. Nobody waits. C is the same whoever combines: it sums all S
-// partials from memory in slice order.
-template <bool TAIL>
+// the XCD's workgroups exit at once). S >= 3: every slice writes its fp32
+// partial (write-through) and adds 1 to the tile's counter; the one that draws
+// S - 1 sums the other S - 1 partials into its registers, stores C and resets
+// the counter. Nobody waits. C is the same whoever combines: it sums all S
+// partials from memory in slice order. S = 2: the head / tail protocol of the
+// two-round mode (round 5: one partial write + one read per tile).
+// PAIR (S = 2 only, chosen at launch): the head / tail protocol below; a
+// separate instantiation, so the S >= 3 build keeps round 4's register
+// allocation (sharing one body cost it 18-24 % at S = 4 with K % 128 != 0).
+template <bool TAIL, bool PAIR = false>
 __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_sks_kernel(GemmArgs p, SkArgs s) {
   __shared__ __attribute__((aligned(16))) char smem[kLdsBytes3 + 16];  // ONE __shared__ array
   int* bcast = (int*)(smem + kLdsBytes3);
@@ -448,6 +452,35 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_sks_kernel(GemmArgs p, 
   k_range<TAIL>(p, c, f, acc, 2 * pa, 2 * pb);
   float* part = s.ws + (kCounterBytes + (size_t)tile * s.S * kPartialBytes) / 4;
   unsigned* cnt = s.cnt + tile;
+  if constexpr (PAIR) {
+    // two slices: the two-round mode's head / tail protocol (slice 0 = head, the
+    // writer). The first to finish writes its partial; the other usually finds it
+    // written and adds it to its own registers - one partial write and one read
+    // per tile instead of two and two. own + other is commutative in fp32, so C
+    // is the same whichever slice combines.
+    const bool tail = slice == 1;
+    const unsigned arrive = tail ? 4u : 1u, written = arrive << 1;
+    const unsigned other_written = tail ? 2u : 8u;
+    const unsigned xc = xcc_id();
+    const unsigned tag = (xc + 1u) << (tail ? kTailTagShift : kHeadTagShift);
+    float* mine = part + (tail ? kPartialBytes / 4 : 0);
+    const float* other = part + (tail ? 0 : kPartialBytes / 4);
+    unsigned o = tail ? counter_add<false>(cnt, arrive + tag, bcast) : 0u;
+    if (!(o & other_written)) {
+      write_partial(mine, acc);
+      o = counter_add<true>(cnt, written + (tail ? 0u : tag), bcast);
+    }
+    if (!(o & other_written)) return;  // uniform: the other slice combines
+    const unsigned other_xcc = ((o >> (tail ? kHeadTagShift : kTailTagShift)) & 0xFFu) - 1u;
+    if (other_xcc != xc)
+      report_xcc_error(s.cnt, 1u << 28 | (unsigned)(tile & 0xFFFF) << 8 | (xc & 0xF) << 4 |
+                                  (other_xcc & 0xF));
+    acquire_all();
+    add_partial(other, acc);
+    reset_counter(cnt);
+    store_tile_epi<false, kEpiSk>(p, c, acc, m0, n0, lane_now());
+    return;
+  }
   write_partial(part + (size_t)slice * (kPartialBytes / 4), acc);
   // count (bits 0-7) + XCC id (8-15) + its square (16-31): S <= 8 parts, id < 16
   const unsigned xc = xcc_id();
@@ -472,7 +505,8 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_sks_kernel(GemmArgs p, 
 // it for every stream-K launch on one stream (no per-call memset dispatch). Returns hipErrorInvalidValue
 // for shapes stream-K does not serve (sk_decompose: tiles a multiple of the
 // CUs, or one round of them with fewer than 2 K slices per tile).
-template <bool REV = false, bool STAMP = false>
+// HT = false (experimental A/B build): split mode's S-partial protocol also for S = 2.
+template <bool REV = false, bool STAMP = false, bool HT = true>
 inline hipError_t launch_gemm_bf16_sk(const GemmArgs& a, int cus, void* ws, size_t ws_bytes,
                                       hipStream_t stream, unsigned long long* stamps = nullptr) {
   SkArgs s;
@@ -487,10 +521,18 @@ inline hipError_t launch_gemm_bf16_sk(const GemmArgs& a, int cus, void* ws, size
   const dim3 g((unsigned)s.G), blk(kThreads);
   if (s.S >= 2) {  // split mode (REV / STAMP do not apply)
     if (REV || STAMP) return hipErrorInvalidValue;
-    if (a.K % (2 * BK))
-      hipLaunchKernelGGL((gemm_bf16_sks_kernel<true>), g, blk, 0, stream, a, s);
-    else
-      hipLaunchKernelGGL((gemm_bf16_sks_kernel<false>), g, blk, 0, stream, a, s);
+    const bool pair = HT && s.S == 2;
+    if (a.K % (2 * BK)) {
+      if (pair)
+        hipLaunchKernelGGL((gemm_bf16_sks_kernel<true, true>), g, blk, 0, stream, a, s);
+      else
+        hipLaunchKernelGGL((gemm_bf16_sks_kernel<true, false>), g, blk, 0, stream, a, s);
+    } else {
+      if (pair)
+        hipLaunchKernelGGL((gemm_bf16_sks_kernel<false, true>), g, blk, 0, stream, a, s);
+      else
+        hipLaunchKernelGGL((gemm_bf16_sks_kernel<false, false>), g, blk, 0, stream, a, s);
+    }
     return hipGetLastError();
   }
   if (a.K % (2 * BK))

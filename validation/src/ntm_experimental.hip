@@ -129,6 +129,16 @@ NTM_API int ntm_gemm_bf16_sk_stamp(const void* A, const void* B, void* C, int M,
       a, ntm::gemm6::pp6_grid(1 << 30), ws, ws_bytes, S(stream), (unsigned long long*)stamps);
 }
 
+// Stream-K split mode with the S-partial protocol also at S = 2 (the round-4
+// build; the shipping one uses the head / tail protocol there): A/B only.
+NTM_API int ntm_gemm_bf16_sk_nopair(const void* A, const void* B, void* C, int M, int N, int K,
+                                    int lda, int ldb, int ldc, void* ws, size_t ws_bytes,
+                                    void* stream) {
+  const ntm::gemm::GemmArgs a = args(A, B, C, M, N, K, lda, ldb, ldc);
+  return (int)ntm::gemmsk::launch_gemm_bf16_sk<false, false, false>(
+      a, ntm::gemm6::pp6_grid(1 << 30), ws, ws_bytes, S(stream));
+}
+
 // pingpong8o boundary-phase stamps (gemm_bf16_pp6.hpp STAMP 2): grid 128 or 256
 // workgroups (a multiple of 8, <= tiles, each workgroup >= 2 tiles), store 1 =
 // C stored (nontemporal) / 0 = not stored / 2 = stored, spread over the boundary
