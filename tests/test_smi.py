@@ -67,3 +67,35 @@ def test_sample_on_mi355x():
     assert s["temp_hotspot_c"] and 10 < s["temp_hotspot_c"] < 120, s
     assert s["gfxclk_mhz"] and 100 < s["gfxclk_mhz"] < 3000, s
     assert s["energy_uj"] is not None and s["accumulation_counter"] is not None, s
+
+
+def test_clock_summary_groups_by_real_xcc_and_finds_the_bounding_xcd():
+    """ops.clock_summary (host side of gemm_clock_ghz) on a synthetic record:
+    8 XCDs, XCD 3 the slowest; the dispatcher's round robin intact, then broken."""
+    import torch
+
+    from nvidia_terraform_modules_amd.ops.kernels import clock_summary
+
+    steps, grid = 4, 64
+    st = torch.zeros((steps, grid, 6), dtype=torch.int64)
+    ghz = {x: 1.70 - (0.10 if x == 3 else 0.01 * x) for x in range(8)}
+    for i in range(steps):
+        for b in range(grid):
+            x = b & 7
+            win_ticks = 65000                          # 650 us at 100 MHz
+            st[i, b, 0] = 10_000 + i * 1_000_000       # start cycles
+            st[i, b, 1] = 500 + i * 100_000 + (b >> 3)  # start ticks (ramp)
+            st[i, b, 3] = st[i, b, 1] + win_ticks
+            st[i, b, 2] = st[i, b, 0] + int(ghz[x] * 1e9 * win_ticks / 1e8)
+            st[i, b, 4] = x                            # XCC_ID
+    r = clock_summary(st, 0.68)
+    assert r["xcc_ids"] == list(range(8)) and r["blockidx_mod_8_is_xcc"] is True
+    assert abs(r["per_xcc_median_GHz"]["3"] - 1.60) < 1e-3
+    assert abs(r["bound_GHz"] - 1.60) < 1e-3            # the slowest XCD bounds the launch
+    assert r["xcc_clock_spread_pct"] > 6
+    assert r["launches"] == steps and r["ms_per_launch"] == 0.68
+    assert r["xcc_finish_spread_us"] >= 0
+    # an XCD layout the round robin does not explain: flagged, and grouped by the register
+    st[:, :, 4] = (torch.arange(grid) // 8) % 8
+    r = clock_summary(st, 0.68)
+    assert r["blockidx_mod_8_is_xcc"] is False
