@@ -43,7 +43,7 @@ _P2 = {"==": "EQOP", "!=": "NEQ", "<=": "LTE", ">=": "GTE", "&&": "AND", "||": "
 _P1 = {"{": "OBRACE", "}": "CBRACE", "[": "OBRACK", "]": "CBRACK", "(": "OPAREN",
        ")": "CPAREN", "=": "EQUAL", ",": "COMMA", ".": "DOT", ":": "COLON", "?": "QUESTION",
        "+": "PLUS", "-": "MINUS", "*": "STAR", "/": "SLASH", "%": "PERCENT", "<": "LT",
-       ">": "GT", "!": "BANG"}
+       ">": "GT", "!": "BANG", "~": "TILDE"}
 # a minus after one of these is a negation (no space after it)
 _NEG_BEFORE = {None, "OPAREN", "OBRACE", "OBRACK", "EQUAL", "COLON", "COMMA", "QUESTION",
                "PLUS", "STAR", "SLASH", "PERCENT", "MINUS", "EQOP", "NEQ", "GT", "GTE", "LT",
@@ -266,6 +266,8 @@ def _space_after(subject: Tok, before: Tok | None, after: Tok) -> bool | None:
         return (before.kind if before is not None else None) not in _NEG_BEFORE
     if sk == "BANG":
         return None      # "!x": not pinned by the corpus; never flagged
+    if sk == "TILDE" or ak == "TILDE":
+        return None      # template strip markers ("${~ x ~}"): never flagged
     if sk == "OBRACE" or ak == "CBRACE":
         return not (sk == "OBRACE" and ak == "CBRACE")
     if sk in ("TINTERP", "TCONTROL") and ak == "OBRACE":

@@ -57,6 +57,8 @@ GOOD = [
   ] : []
 }
 ''',
+    # template strip markers and directives are lexed, never flagged
+    'locals {\n  s = "${~ var.a ~}%{ if var.b }x%{ endif }"\n}\n',
     # a heredoc is never re-indented, and an attribute after it stays in its run
     '''locals {
   script = <<-EOT
