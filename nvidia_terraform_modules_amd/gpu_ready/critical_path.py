@@ -79,10 +79,11 @@ DRIVER_READY_S = {"operator": 240.0, "daemonsets": 300.0}
 # amd.com/gpu with the kubelet and the labeller - the SURVEY §7.4 lever
 PLUGIN_READY_S = 30.0
 # the host-prep gate (node-prep DaemonSet with the startup taint): prep script,
-# the queued containerd restart, the verify step's kubelet retry (10 s
-# backoff) and two kubectl calls incl. the kubectl image pull. It runs beside
-# the driver install, so the Job waits for the LONGER of the two: off the
-# path with a driver to install, on it with a preinstalled driver.
+# the queued containerd restart (done before kubelet can start the next
+# container), the gate container's image pull, its first verify + untaint
+# (a failed verify waits node_prep_gate_interval_s, 30 s, for the next check).
+# It runs beside the driver install, so the Job waits for the LONGER of the
+# two: off the path with a driver to install, on it with a preinstalled driver.
 PREP_GATE_S = 45.0
 PREP_GATE_MARK = "kubernetes_cluster_role_v1.node_prep"
 
