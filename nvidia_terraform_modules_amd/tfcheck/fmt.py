@@ -380,7 +380,7 @@ def write_formatted(root: Path) -> list[Path]:
     changed = []
     for f in hcl_files(root):
         text = f.read_text()
-        new = "\n".join(ln.rstrip() for ln in formatted(text).split("\n"))
+        new = formatted(text)   # heredoc bodies and comments stay byte for byte
         if new != text:
             f.write_text(new)
             changed.append(f)

@@ -171,3 +171,15 @@ def test_reference_corpus():
     for name, d in dirty.items():
         for _, have, want in d:
             assert "\t" in have or have.split() == want.split(), (name, have, want)
+
+
+def test_fmt_write_keeps_heredoc_bodies(tmp_path):
+    f = tmp_path / "main.tf"
+    src = 'locals {\n  a  = 1\n  s = <<-EOT\n    keep trailing   \n  EOT\n}\n'
+    f.write_text(src)
+    from nvidia_terraform_modules_amd.tfcheck.fmt import write_formatted
+
+    assert write_formatted(tmp_path) == [f]
+    out = f.read_text()
+    assert "    keep trailing   \n" in out and "  a = 1\n" in out
+    assert write_formatted(tmp_path) == []            # idempotent
