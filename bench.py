@@ -310,7 +310,15 @@ def main(argv=None) -> int:
     # the clock the TIMED loop ran at: shader cycles per launch are launch-invariant
     # (1.085-1.091 M at 8192^3), so median cycles / this rank's ms per step
     timed_clk = None
-    if gclk and gclk.get("per_launch_cycles_median"):
+    # (only where the timed kernel IS the clock build's: the default plan runs
+    # pingpong8o - at 2048^3 it runs a small tile, whose cycles these are not)
+    same_kernel = False
+    if dev.type == "cuda" and hasattr(backend, "k1_plan"):
+        try:
+            same_kernel = backend.k1_plan(args.size, args.size, args.size)[1] == "pingpong8o"
+        except ValueError:
+            same_kernel = False
+    if same_kernel and gclk and gclk.get("per_launch_cycles_median"):
         cyc = sorted(gclk["per_launch_cycles_median"])
         timed_clk = round(cyc[len(cyc) // 2] / (my_seconds / args.steps) / 1e9, 4)
         gclk["ms_per_launch_over_ms_per_step"] = round(

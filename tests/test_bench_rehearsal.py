@@ -148,8 +148,9 @@ def test_bench_on_one_gpu_json_contract(tmp_path):
     assert 0.5 < d["per_rank_gemm_clock_GHz"][0] < 3.0, g
     assert g["p10_GHz"] <= g["median_GHz"] and g["workgroups"] > 0
     assert 0.5 < d["per_rank_clock_GHz"][0] < 3.0
-    assert 0.3 < d["per_rank_timed_loop_clock_GHz"][0] < 3.0
-    assert g["ms_per_launch_over_ms_per_step"] > 0
+    # at 2048^3 the timed loop runs a small tile, not the clock build's pingpong8o:
+    # no timed-loop clock is derived from the clock build's cycles
+    assert d["per_rank_timed_loop_clock_GHz"] == [None]
     pw = d["per_rank_power"][0]
     assert "error" not in pw, pw
     # (a 5-step 2048^3 window is shorter than the energy counter's update period)
