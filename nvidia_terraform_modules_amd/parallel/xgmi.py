@@ -159,12 +159,7 @@ class XgmiAllReduce:
         try:
             for name, nbytes, uncached in (("in", max_bytes, 0), ("out", max_bytes, 0),
                                            ("sig", L.ntm_xgmi_signal_bytes(nblk), 1)):
-                p = ctypes.c_void_p()
-                check(L.ntm_malloc(ctypes.byref(p), nbytes, uncached), "ntm_malloc")
-                self._own.append(p.value)
-                h = ctypes.create_string_buffer(64)
-                check(L.ntm_ipc_handle(p.value, h), "ntm_ipc_handle")
-                handles[name] = (p.value, h.raw)
+                handles[name] = _alloc_exported(L, nbytes, uncached, self._own)
             check(L.ntm_memset_async(handles["sig"][0], 0, L.ntm_xgmi_signal_bytes(nblk), None),
                   "memset")
             torch.cuda.synchronize()
@@ -291,6 +286,29 @@ class XgmiAllReduce:
         for p in self._own:
             self.L.ntm_free(p)
         self._own = []
+
+
+def _alloc_exported(L, nbytes: int, uncached: int, own: list) -> tuple:
+    """Allocate ``nbytes`` and export its IPC handle: (pointer, 64 handle bytes).
+
+    Every allocation goes into ``own`` (freed by close). hipIpcGetMemHandle can
+    refuse a fresh allocation with "invalid value" when the allocator handed
+    back a range whose previous export a peer process has not finished
+    releasing: the driver's dmabuf release runs after hipIpcCloseMemHandle and
+    the close barrier return (seen once at world 8, round 5, after round 4's
+    collective close made it rare). That allocation is kept, not freed, so the
+    one retry gets a different range; a second refusal is raised."""
+    last = 0
+    for _ in range(2):
+        p = ctypes.c_void_p()
+        check(L.ntm_malloc(ctypes.byref(p), nbytes, uncached), "ntm_malloc")
+        own.append(p.value)
+        h = ctypes.create_string_buffer(64)
+        last = L.ntm_ipc_handle(p.value, h)
+        if last == 0:
+            return p.value, h.raw
+    check(last, "ntm_ipc_handle")
+    raise AssertionError("unreachable")
 
 
 def _copy_d2d(dst: int, src: int, nbytes: int) -> None:
