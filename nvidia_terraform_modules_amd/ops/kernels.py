@@ -38,7 +38,8 @@ GEMM_VARIANTS = {"default": 0, "pingpong8": 1, "pingpong8b": 4,
                  "tile128x160": 24, "tile128x256": 26, "pingpong8o": 25,
                  "pp8o_g128": 41, "pp8o_g128_nostore": 42, "pp8o_nostore": 43,
                  "pingpong8om": 47, "pingpong8od": 48, "pingpong8s": 49,
-                 "pingpong8omd": 51}
+                 "pingpong8omd": 51, "pp192x256": 27, "pp256x192": 28,
+                 "pp224x256": 29}
 
 
 # variants built only into libntm_experimental.so (tests / tools): never selected
@@ -47,7 +48,7 @@ EXPERIMENTAL_VARIANTS = frozenset({"pingpong8", "pingpong8cw",
                                    "pingpong8cwe", "pingpong8cwn", "pingpong8cwne",
                                    "tile128w4", "tile256x128w4", "tile160w4",
                                    "pp8o_g128", "pp8o_g128_nostore", "pp8o_nostore",
-                                   "pingpong8od", "pingpong8omd", "pingpong8om"})
+                                   "pingpong8od", "pingpong8omd", "pingpong8om", "pp224x256"})
 
 # (TM, TN) of the 4-wave tile kernels (gemm_bf16_t128.hpp)
 TILE_SHAPES = {"tile128": (128, 128), "tile256x128": (256, 128), "tile160": (160, 160),
@@ -98,6 +99,13 @@ def k1_splitk_plan(m: int, n: int, k: int) -> tuple[int, str, str, int]:
 # (M, N, K) -> split-K workspace bytes of the default plan (0 = unsplit); a
 # plan is validated once per shape
 _DEFAULT_WS: dict[tuple[int, int, int], int] = {}
+
+
+def set_plan_pp_tiles(on: bool) -> None:
+    """A/B knob for tools (tools/plan_ab.py): let the plan use the 192x256 /
+    256x192 ping-pong tiles (the default) or not. Process-wide."""
+    lib().ntm_set_plan_pp_tiles(1 if on else 0)
+    _DEFAULT_WS.clear()
 
 
 def _default_ws_bytes(m: int, n: int, k: int) -> int:
@@ -153,7 +161,9 @@ def gemm_bf16(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
             raise ValueError(f"shape ({m},{n},{k}) not served by stream-K (N % 8, K % 8, K >= 128; "
                              "256x256 tiles: more than the CUs and not a multiple of them, or "
                              "few enough for >= 2 K slices per tile in one round)")
-    elif variant in ("pingpong8cm", "pingpong8om", "pingpong8omd"):  # 256x256, masked edges (+ K tail)
+    elif variant in ("pingpong8cm", "pingpong8om", "pingpong8omd", "pp192x256", "pp256x192",
+                     "pp224x256"):
+        # 8-wave ping-pong tiles with masked edges (+ K tail)
         if not (m > 0 and n > 0 and n % 8 == 0 and k > 0 and k % 8 == 0):
             raise ValueError(f"shape ({m},{n},{k}) not served by {variant} (N % 8, K % 8)")
     elif not gemm_shape_ok(m, n, k):

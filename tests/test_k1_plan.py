@@ -24,7 +24,8 @@ def k1_plan():
     (2816, 2816, 2816, 2816, "tile128x256", None),   # 242 tiles: one round (128x256 2 % above 256x128)
     (4096, 2048, 4096, 4096, "tile128x256", None),
     (4672, 1472, 6696, 4672, "tile128x256", None),   # hipBLASLt's MT128x256 there (r2_tiles)
-    (3072, 3072, 3072, 3072, "pingpong8c", None),    # whole rounds: 256x256 only
+    (3072, 3072, 3072, 3072, "pp192x256", None),     # 144 256x256 tiles -> 192 of 192x256 (+18 %)
+    (3072, 3072, 512, 3072, "pingpong8c", None),     # K < 1024: the 192-wide tiles stay out
     (4096, 4096, 4096, 4096, "pingpong8c", None),
     (8192, 8192, 8192, 8192, "pingpong8o", None),    # > 256 tiles: the persistent build
     (4096, 8192, 8192, 4096, "pingpong8o", None),    # 512 tiles
@@ -33,14 +34,18 @@ def k1_plan():
     (8192, 8192, 8128, 8192, "pingpong8cm", None),   # K % 128 != 0: partial-K build
     (6144, 6144, 6144, 5376, "pingpong8o", "tile160x128"),  # 3 rounds -> 2 + one of 160x128
     (4352, 4352, 4352, 3840, "pingpong8c", "tile128"),
-    (3200, 3200, 3200, 3200, "pingpong8cm", None),   # one round of masked 256x256 tiles
+    (3200, 3200, 3200, 3200, "pp192x256", None),     # one round of 192x256 tiles (+8 %)
+    (3200, 3200, 616, 3200, "pingpong8cm", None),    # one round of masked 256x256 tiles
     (2080, 3844, 256, 512, "tile128", "tile160"),    # N % 8 != 0: mixed small tiles
     (4000, 4000, 4096, 4000, "pingpong8cm", None),
     (416, 1280, 128, 416, "tile128", None),          # masked edge tiles: one launch
     (1696, 2560, 2560, 1696, "tile160x128", None),   # 11 x 20 tiles: one round
     (5624, 752, 5880, 5624, "tile160x128", None),    # 216 tiles vs 180 of 160x160
     (4072, 1240, 3784, 4072, "tile128x160", None),   # 32 x 8 tiles: one full round
-    (3000, 3000, 3000, 3000, "pingpong8cm", None),   # one-round tiles stay out of 2-round plans
+    (3000, 3000, 3000, 3000, "pp192x256", None),     # 16 x 12 tiles (+13 %)
+    (3000, 3000, 4096, 3000, "pp192x256", None),
+    (3904, 2584, 12760, 3904, "pp256x192", None),    # hipBLASLt's MT256x192 there (r5_h192)
+    (5120, 5120, 256, 5120, "pingpong8o", None),     # never the rest part of a 2-launch plan
     (2400, 3200, 3200, 2400, "tile128x256", None),   # 19 x 13 tiles: one round
     (3200, 5104, 3480, 3200, "tile128x256", None),   # 2 full rounds beat 256x256 + a tile128 rest (+2.4 %)
     (8200, 8192, 8192, 8192, "pingpong8o", "tile128"),  # 8 ragged rows on masked tiles
@@ -58,16 +63,19 @@ def test_plan_is_well_formed(k1_plan, m, n, k):
     top, top_variant, rest = k1_plan(m, n, k)
     small = ("tile128", "tile256x128", "tile160", "tile256x160", "tile160x128", "tile128x160",
              "tile128x256")
-    assert 0 < top <= m and top_variant in small + ("pingpong8c", "pingpong8cm", "pingpong8o")
+    pp = ("pp192x256", "pp256x192")   # one-round, all of C only
+    assert 0 < top <= m and top_variant in small + pp + ("pingpong8c", "pingpong8cm", "pingpong8o")
+    if top_variant in pp:
+        assert top == m and k >= 1024
     if top_variant == "pingpong8o":  # more 256x256 tiles than CUs, else pingpong8c
         assert (top // 256) * (n // 256) > 256 and k >= 256
     assert rest in small
     tm = {"tile128": 128, "tile256x128": 256, "tile160": 160, "tile256x160": 256,
           "tile160x128": 160, "tile128x160": 128, "tile128x256": 128, "pingpong8c": 256,
-          "pingpong8cm": 256,
+          "pingpong8cm": 256, "pp192x256": 192, "pp256x192": 256,
           "pingpong8o": 256}
     masked = ("tile128", "tile256x128", "tile160", "tile160x128", "tile128x160", "tile128x256",
-              "pingpong8cm")
+              "pingpong8cm", "pp192x256", "pp256x192")
     assert top % tm[top_variant] == 0 or (top == m and top_variant in masked)
     if top < m:
         assert (m - top) % tm[rest] == 0 or rest in masked
@@ -293,3 +301,22 @@ def test_plan_and_launch_agree_on_the_cu_count(k1_plan, cus):
         kernels._DEFAULT_WS.clear()
     assert lib().ntm_plan_cus() == 256      # no GPU here: the documented default
 
+
+
+def test_pp_tiles_one_launch_and_toggle(k1_plan):
+    """The 192x256 / 256x192 ping-pong tiles (gemm_bf16_pp3h.hpp) take all of C in
+    one round or nothing, need N % 8 and K >= 1024, never serve fp8, and the
+    tools' A/B knob turns them off and on."""
+    from nvidia_terraform_modules_amd import ops
+
+    try:
+        assert k1_plan(3904, 2584, 12760)[1] == "pp256x192"
+        assert k1_plan(3904, 2588, 12760)[1] != "pp256x192"      # N % 8
+        ops.set_plan_pp_tiles(False)
+        assert k1_plan(3904, 2584, 12760)[1] == "pingpong8cm"
+        ops.set_plan_pp_tiles(True)
+        assert k1_plan(3904, 2584, 12760)[1] == "pp256x192"
+        for m, n, k in [(3904, 2584, 12760), (3072, 3072, 3072), (7288, 1344, 5768)]:
+            assert ops.k1_fp8_plan(m, n, 2 * k)[1] not in ("pp192x256", "pp256x192")
+    finally:
+        ops.set_plan_pp_tiles(True)

@@ -372,7 +372,8 @@ def test_gemm_tile128_rejects_bad_shapes(ops):
 
 
 @pytest.mark.parametrize("variant", ["tile128", "tile256x128", "tile160", "tile160x128",
-                                     "tile128x160", "tile128x256", "pingpong8cm", "default"])
+                                     "tile128x160", "tile128x256", "pingpong8cm", "pp192x256",
+                                     "pp256x192", "default"])
 @pytest.mark.parametrize("m,n,k", [(1000, 1000, 1024), (100, 4096, 256), (1696, 2560, 256),
                                    (2400, 3200, 128), (1, 4, 128), (333, 1004, 384),
                                    (8200, 260, 128), (4000, 4000, 512), (1000, 1000, 1000),
@@ -383,8 +384,8 @@ def test_gemm_masked_edge_tiles(ops, variant, m, n, k):
     N % 8, K % 8): vs fp32, and nothing written outside C - C is a view into
     a sentinel-filled buffer with extra rows below and extra columns to the
     right (ldc > N)."""
-    if variant == "pingpong8cm" and n % 8:
-        pytest.skip("pingpong8cm: N % 8 (8-column store chunks)")
+    if variant in ("pingpong8cm", "pp192x256", "pp256x192", "pp224x256") and n % 8:
+        pytest.skip(f"{variant}: N % 8 (8-column store chunks)")
     a = _rand(ops, (m, k), 971 + m)
     b = _rand(ops, (n, k), 973 + n)
     big = torch.full((m + 37, n + 16), 3.0, dtype=torch.bfloat16, device="cuda")
@@ -398,6 +399,31 @@ def test_gemm_masked_edge_tiles(ops, variant, m, n, k):
     assert torch.all(big[m:] == 3.0) and torch.all(big[:, n:] == 3.0)
     if variant != "default" and m % 256 == 0 and n % 256 == 0:
         assert torch.equal(c, ops.gemm_bf16(a, b, variant="pingpong8"))
+    if variant in ("pp192x256", "pp256x192", "pp224x256"):   # same MFMAs in the same K order
+        assert torch.equal(c, ops.gemm_bf16(a, b, variant="pingpong8cm"))
+
+
+@pytest.mark.parametrize("variant", ["pp192x256", "pp256x192", "pp224x256"])
+@pytest.mark.parametrize("m,n,k", [(3904, 2584, 12760), (7288, 1344, 5768), (3512, 3456, 16040),
+                                   (1312, 6304, 5080), (192, 192, 128), (200, 200, 136),
+                                   (4032, 4032, 1024), (5000, 3000, 2000)])
+def test_gemm_192_tiles(ops, variant, m, n, k):
+    """192x256 / 256x192 ping-pong tiles (gemm_bf16_pp3h.hpp): the ragged one-round
+    shapes hipBLASLt fills with 192-wide tiles, exact multiples of 192, more than one
+    round and the partial-K build - vs fp32, bitwise equal to pingpong8cm, and
+    nothing written outside C."""
+    a = _rand(ops, (m, k), 17 + m)
+    b = _rand(ops, (n, k), 19 + n)
+    big = torch.full((m + 5, n + 8), 3.0, dtype=torch.bfloat16, device="cuda")
+    c = big[:m, :n]
+    ops.gemm_bf16(a, b, c, variant=variant)
+    torch.cuda.synchronize()
+    ref = a.float() @ b.float().T
+    atol, rtol = ops.gemm_tolerance(k)
+    err = (c.float() - ref).abs()
+    assert torch.all(err <= atol + rtol * ref.abs()), float(err.max())
+    assert torch.all(big[m:] == 3.0) and torch.all(big[:, n:] == 3.0)
+    assert torch.equal(c, ops.gemm_bf16(a, b, variant="pingpong8cm"))
 
 
 @pytest.mark.parametrize("variant", ["tile128", "tile256x128", "tile160", "tile160x128",

@@ -47,6 +47,11 @@ ALLOWED_K1 = {
     # ... at S = 2: the head / tail protocol <TAIL, PAIR> (round 5)
     "ntm::gemmsk::gemm_bf16_sks_kernel<false, true>",
     "ntm::gemmsk::gemm_bf16_sks_kernel<true, true>",
+    # one round of 192x256 / 256x192 ping-pong tiles <AH, BH, TAIL> (round 5)
+    "ntm::gemm3h::gemm_bf16_pp3h_kernel<64, 128, false>",
+    "ntm::gemm3h::gemm_bf16_pp3h_kernel<64, 128, true>",
+    "ntm::gemm3h::gemm_bf16_pp3h_kernel<128, 64, false>",
+    "ntm::gemm3h::gemm_bf16_pp3h_kernel<128, 64, true>",
     "ntm::gemm2::gemm_bf16_pp2_kernel<false, 0>",
     "ntm::gemm2::gemm_bf16_pp2_kernel<false, 3>",
     "ntm::gemm2::gemm_bf16_pp2_kernel<true, 0>",
@@ -82,7 +87,7 @@ ALLOWED_K1 = {
 }
 EXPERIMENTAL_ONLY = ("gemm_w4k_kernel", "gemm_w4o_kernel", "gemm_r4k_stamp_kernel",
                      "gemm_bf16_pp3_stamp_kernel", "ntm::gemm::gemm_bf16_kernel",
-                     "mfma_rate_kernel", "mfma_f8_probe_kernel")
+                     "mfma_rate_kernel", "mfma_f8_probe_kernel", "gemm_bf16_pp3h_kernel<96")
 
 
 def _kernels(path: Path) -> set:
@@ -113,5 +118,6 @@ def test_experimental_library_holds_the_experiments():
     ks = _kernels(EXP)
     for fam in ("gemm_bf16_pp3_stamp_kernel", "gemm_bf16_sk_kernel<false, true, false>", "mfma_rate_kernel",
                 "mfma_f8_probe_kernel",
-                "gemm_bf16_pp6_kernel<1, 0, true, false, false, false>"):   # pingpong8om
+                "gemm_bf16_pp6_kernel<1, 0, true, false, false, false>",   # pingpong8om
+                "gemm_bf16_pp3h_kernel<96, 128"):                          # pp224x256
         assert any(fam in k for k in ks), fam

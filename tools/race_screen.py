@@ -33,7 +33,10 @@ SHAPES_160 = [(160, 160, 128), (1280, 800, 384), (2560, 1600, 640), (2560, 2560,
 SHAPES_RAGGED = [(1000, 1000, 1024), (1696, 2560, 640), (333, 1004, 384), (2400, 3200, 512),
                  (1000, 1000, 1000), (333, 1004, 200)]  # the last two: partial K-tiles
 MASKED = ("tile128", "tile256x128", "tile160", "tile160x128", "tile128x160", "tile128x256", "pingpong8cm",
-          "pingpong8om", "pingpong8omd", "default")
+          "pingpong8om", "pingpong8omd", "pp192x256", "pp256x192", "pp224x256", "default")
+# one round of 192-wide ping-pong tiles on ragged C, partial K (the plan's shapes)
+SHAPES_PP = [(3904, 2584, 12760), (7288, 1344, 5768), (3072, 3072, 3072), (200, 200, 136),
+             (1312, 6304, 5080)]
 # skinny C with a long K: the default dispatch splits K here (k1_splitk_plan)
 SHAPES_SPLITK = [(280, 6352, 7568), (128, 8192, 8192), (333, 1004, 2056), (256, 2048, 8200)]
 # persistent overlap kernel (pingpong8o*, K >= 256): 1-4 tiles per workgroup,
@@ -90,6 +93,8 @@ def main():
             shapes = SHAPES_SK if v == "pingpong8s" else SHAPES_SK[:7]  # REV: two-round mode
         if splits > 1:
             shapes = SHAPES_SPLITK + SHAPES_RAGGED
+        elif v in ("pp192x256", "pp256x192", "pp224x256"):
+            shapes = SHAPES_PP + SHAPES_RAGGED
         elif v in MASKED:
             shapes = shapes + SHAPES_RAGGED + (SHAPES_SPLITK + SHAPES_DEFAULT_SK if v == "default" else [])
         for (m, n, k) in shapes:
@@ -97,7 +102,7 @@ def main():
                 continue
             if tm and m % tm and v not in MASKED:
                 continue
-            if v in ("pingpong8cm", "pingpong8om", "pingpong8omd") and n % 8:
+            if v in ("pingpong8cm", "pingpong8om", "pingpong8omd", "pp192x256", "pp256x192", "pp224x256") and n % 8:
                 continue
             a = ops.fill_uniform_(torch.empty((m, k), dtype=dt, device=dev), 5 + m)
             b = ops.fill_uniform_(torch.empty((n, k), dtype=dt, device=dev), 6 + n)

@@ -23,7 +23,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from nvidia_terraform_modules_amd import ops  # noqa: E402
 
 CANDIDATES = ("pingpong8s", "pingpong8cm", "tile128", "tile256x128", "tile160", "tile160x128",
-              "tile128x160", "tile128x256")
+              "tile128x160", "tile128x256", "pp192x256", "pp256x192", "pp224x256")
 
 
 def ragged_shapes(n: int, seed: int, lo: float = 0.3, hi: float = 1.0) -> list:

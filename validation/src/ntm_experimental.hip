@@ -25,6 +25,7 @@
 // what stays is used by a test or a tool under tools/.
 #include "ntm/gemm_bf16.hpp"
 #include "ntm/gemm_bf16_pp3.hpp"
+#include "ntm/gemm_bf16_pp3h.hpp"
 #include "ntm/gemm_bf16_pp3_stamp.hpp"
 #include "ntm/gemm_bf16_pp6.hpp"
 #include "ntm/gemm_bf16_sk.hpp"
@@ -85,6 +86,11 @@ NTM_API int ntm_gemm_bf16_experimental(int variant, const void* A, const void* B
       if (!ntm::gemm6::shape_ok6m(M, N, K) || (lda % 8) || (ldb % 8) || (ldc % 8))
         return (int)ntm::gemm3::launch_gemm_bf16_pp3_masked(a, S(stream));
       return (int)ntm::gemm6::launch_gemm_bf16_pp6_masked<1>(a, S(stream));
+    // 29: 224x256 ping-pong tiles (gemm_bf16_pp3h.hpp, a 96-row A-hi half): on 11
+    // shapes of 0.78-0.91 rounds of 256x256 tiles it won 2-6 % on five and lost
+    // 1-7 % on four against pingpong8cm (profiles/r5_h192/pp224_sweep.log), so
+    // the plan does not use it
+    case 29: return (int)ntm::gemm3h::launch_gemm_bf16_pp3h<96, 128>(a, S(stream));
     // 51: pingpong8om (ragged C) with the spread boundary stores
     case 51: return (int)ntm::gemm6::launch_gemm_bf16_pp6_masked<1, true>(a, S(stream));
     default: return (int)hipErrorInvalidValue;

@@ -13,6 +13,7 @@
 #include "ntm/aux_kernels.hpp"
 #include "ntm/gemm_bf16_pp2.hpp"
 #include "ntm/gemm_bf16_pp3.hpp"
+#include "ntm/gemm_bf16_pp3h.hpp"
 #include "ntm/gemm_bf16_pp6.hpp"
 #include "ntm/gemm_bf16_sk.hpp"
 #include "ntm/gemm_bf16_t128.hpp"
@@ -108,6 +109,16 @@ constexpr bool kFp8Persistent = true;
 // rounds (8192x8192x4096 / 4096x8192x4096 / 8192x4096x4096: 1300 / 1289 / 1282
 // vs 1279 / 1258 / 1253 TF/s, profiles/r3_tiles/), so 0.80 against 0.78; it
 // wastes fewer edge rows where M is ragged and N a multiple of 256.
+// 192x256 / 256x192 (round 5, `pp`: gemm_bf16_pp3h.hpp, the 8-wave ping-pong
+// with one 64-row half; hipBLASLt's MT256x192 / MT192x256 on ragged one-round C,
+// profiles/r5_h192/): one round of them took 0.88-0.96 of the time of
+// pingpong8cm's round of 256x256 tiles on 7 ragged shapes, for 0.75 of the work
+// per CU - eff 0.78-0.85, priced at 0.82. One-round tiles, like 160x128.
+// They serve all of C in one launch only: as the rest part after whole rounds
+// of 256x256 tiles they tied the old plan at best and lost 22-24 % at
+// 5120x5120x128 / 256; below K = 1024 they lost 17-21 % to pingpong8cm
+// (7400x1224x616, 4392x2184x544), where loading the A / B panels for 31 % more
+// tiles dominates (profiles/r5_h192/plan_ab_*.log).
 // (the CU count the rounds are priced over is the launch's own: device_cus())
 struct SmallTile {
   int variant, tm, tn;
@@ -116,6 +127,7 @@ struct SmallTile {
   bool one_round;  // only where its tiles fit in one round of 256 CUs
   bool splitk;     // a split-K candidate (the split model was fitted without 128x256)
   double ragged;   // measured / modelled time of one round on ragged C (stream-K pricing only)
+  bool pp = false;  // 8-wave ping-pong tile (gemm_bf16_pp3h.hpp): N % 8, bf16 only
 };
 // 160x128 / 128x160 are one-round tiles: filling a round the square tiles
 // leave part-idle they win 2-16 % (5624x752x5880, 4072x1240x3784, the rest
@@ -133,7 +145,13 @@ constexpr SmallTile kSmallTiles[] = {{15, 128, 128, 0.60, true, false, true, 1.1
                                      {23, 160, 128, 0.70, true, true, true, 1.37},
                                      {24, 128, 160, 0.70, true, true, true, 1.37},
                                      {26, 128, 256, 0.80, true, false, false, 1.30},
-                                     {18, 256, 160, 0.61, false, false, false, 1.0}};
+                                     {18, 256, 160, 0.61, false, false, false, 1.0},
+                                     {27, 192, 256, 0.82, true, true, false, 1.0, true},
+                                     {28, 256, 192, 0.82, true, true, false, 1.0, true}};
+// host-only A/B knob (tools/plan_ab.py): the plan without the 192-wide tiles
+static bool g_plan_pp = true;
+NTM_API void ntm_set_plan_pp_tiles(int on) { g_plan_pp = on != 0; }
+constexpr int kPpMinK = 1024;
 constexpr double kSplitPenalty = 0.25;  // a second launch, in 128x128-tile-round units
 
 struct K1Plan {
@@ -223,7 +241,8 @@ inline K1Plan plan_k1(int M, int N, int K, bool splitk = false, bool fp8 = false
   double best_cover = inf;
   if (M <= 0 || N <= 0 || K <= 0) return best;
   auto small_ok = [&](const SmallTile& st, int rows) {  // masked: any M, N % 4, K % 8
-    if (fp8 && !st.masked) return false;
+    if (fp8 && (!st.masked || st.pp)) return false;
+    if (st.pp) return g_plan_pp && N % 8 == 0 && K % 8 == 0 && K >= kPpMinK;
     if (st.masked) return N % 4 == 0 && K % 8 == 0;
     return rows % st.tm == 0 && N % st.tn == 0 && K % 128 == 0 && K >= 128;
   };
@@ -248,7 +267,7 @@ inline K1Plan plan_k1(int M, int N, int K, bool splitk = false, bool fp8 = false
                                : small_cost(kSmallTiles[t], m1);
       const int rest = M - m1;
       for (int r = 0; r < nsmall; ++r) {
-        if (rest > 0 && !small_ok(kSmallTiles[r], rest)) continue;
+        if (rest > 0 && (kSmallTiles[r].pp || !small_ok(kSmallTiles[r], rest))) continue;
         if (rest == 0 && r > 0) break;  // no rest part: one candidate is enough
         const double cost = top + (rest > 0 ? small_cost(kSmallTiles[r], rest) + kSplitPenalty : 0.0);
         if (cost >= inf) continue;  // a one-round tile over more than one round
@@ -432,6 +451,9 @@ NTM_API int ntm_gemm_bf16_variant(int variant, const void* A, const void* B,
     case 18: return (int)ntm::gemmt::launch_gemm_bf16_tile<8, 5>(a, S(stream));
     // 256x256 on ragged C: clamped loads, masked LDS-staged stores
     case 22: return (int)ntm::gemm3::launch_gemm_bf16_pp3_masked(a, S(stream));
+    // 192x256 / 256x192 on the same ping-pong (gemm_bf16_pp3h.hpp): ragged C, one round
+    case 27: return (int)ntm::gemm3h::launch_gemm_bf16_pp3h<64, 128>(a, S(stream));
+    case 28: return (int)ntm::gemm3h::launch_gemm_bf16_pp3h<128, 64>(a, S(stream));
     default: return (int)hipErrorInvalidValue;  // experimental variants: libntm_experimental.so
   }
 }
