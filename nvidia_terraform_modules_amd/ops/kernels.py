@@ -102,7 +102,7 @@ _DEFAULT_WS: dict[tuple[int, int, int], int] = {}
 
 
 def set_plan_pp_tiles(on: bool) -> None:
-    """A/B knob for tools (tools/plan_ab.py): let the plan use the 192x256 /
+    """A/B knob for tools (tools/pp_plan_ab.py): let the plan use the 192x256 /
     256x192 ping-pong tiles (the default) or not. Process-wide."""
     lib().ntm_set_plan_pp_tiles(1 if on else 0)
     _DEFAULT_WS.clear()

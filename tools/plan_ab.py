@@ -1,89 +1,80 @@
-"""A/B of the default K1 plan with and without the 192x256 / 256x192 ping-pong
-tiles (developer tool): per shape, the default dispatch with the tiles (new),
-without them (old) and hipBLASLt, timed interleaved, median over rounds; the
-plans both ways. Shapes: --shapes MxNxK,... or a seeded ragged set
-(tools/ragged_sweep.py's generator) or --random (uniform M, N, K).
+"""A/B of a dispatch-plan change (developer tool): for each case, time the
+default dispatch (the plan in the built library) against an explicit earlier
+plan "ROWS:TOP:REST" (rows [0, ROWS) on TOP, the rest on REST; a variant
+"tile128/s4" = split-K in 4 slices) and hipBLASLt, interleaved in one process;
+the explicit plan is checked against the default result. One JSON line per case.
 
-    python tools/plan_ab.py --shapes 3072x3072x3072,5120x5120x5120 [--rounds 7 --iters 20]
+    python tools/plan_ab.py --cases 3072x3072x3072=3072:pingpong8c:tile128,...
 """
 import argparse
 import json
 import os
-import random
-import statistics
 import sys
 
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from nvidia_terraform_modules_amd import ops  # noqa: E402
-from ragged_sweep import ragged_shapes, timed  # noqa: E402
+
+
+def timed(fn, iters):
+    fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / iters
+
+
+def run(a, b, c, v):
+    v, _, sk = v.partition("/s")
+    ops.gemm_bf16(a, b, c, variant=v, splits=int(sk) if sk else 1)
 
 
 def main():
-    ap = argparse.ArgumentParser(description=__doc__,
-                                 formatter_class=argparse.RawDescriptionHelpFormatter)
-    ap.add_argument("--shapes", default="")
-    ap.add_argument("--n", type=int, default=24)
-    ap.add_argument("--seed", type=int, default=11)
-    ap.add_argument("--random", action="store_true", help="uniform M, N, K in [256, 8192] % 8")
-    ap.add_argument("--changed-only", action="store_true", help="skip shapes whose plan is the same")
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--cases", required=True)
     ap.add_argument("--rounds", type=int, default=7)
-    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--iters", type=int, default=30)
     args = ap.parse_args()
-    if args.shapes:
-        shapes = [tuple(int(x) for x in s.split("x")) for s in args.shapes.split(",") if s]
-    elif args.random:
-        rng = random.Random(args.seed)
-        shapes = [tuple(rng.randrange(256, 8193, 8) for _ in range(3)) for _ in range(args.n)]
-    else:
-        shapes = ragged_shapes(args.n, args.seed)
-    rows = []
-    for m, n, k in shapes:
-        ops.set_plan_pp_tiles(False)
-        old_plan = list(ops.k1_splitk_plan(m, n, k))
-        ops.set_plan_pp_tiles(True)
-        new_plan = list(ops.k1_splitk_plan(m, n, k))
-        if args.changed_only and old_plan == new_plan:
-            continue
+    ok_all = True
+    for case in args.cases.split(","):
+        shape, spec = case.split("=")
+        m, n, k = (int(x) for x in shape.split("x"))
+        rows, top, rest = spec.split(":")
+        r = int(rows)
         a = ops.fill_uniform_(torch.empty((m, k), dtype=torch.bfloat16, device="cuda"), 1)
         b = ops.fill_uniform_(torch.empty((n, k), dtype=torch.bfloat16, device="cuda"), 2)
         c = torch.empty((m, n), dtype=torch.bfloat16, device="cuda")
+        ref = ops.gemm_bf16(a, b).float()
+        atol, rtol = ops.gemm_tolerance(k)
 
-        def run(on):
-            ops.set_plan_pp_tiles(on)
-            ops.gemm_bf16(a, b, c)
-
-        fns = {"new": lambda: run(True), "old": lambda: run(False),
-               "hipblaslt": lambda: torch.matmul(a, b.T, out=c)}
-        t = {name: [] for name in fns}
-        for r in range(args.rounds):
-            order = list(fns.items())
-            for name, fn in (order if r % 2 == 0 else order[::-1]):
-                t[name].append(timed(fn, args.iters))
-        ops.set_plan_pp_tiles(True)
-        med = {name: statistics.median(v) for name, v in t.items()}
-        row = {"shape": [m, n, k], "old_plan": old_plan, "new_plan": new_plan}
-        row.update({f"{name}_us": round(v * 1e3, 1) for name, v in med.items()})
-        row["new_over_old"] = round(med["old"] / med["new"], 3)
-        row["new_over_hipblaslt"] = round(med["hipblaslt"] / med["new"], 3)
-        row["old_over_hipblaslt"] = round(med["hipblaslt"] / med["old"], 3)
-        rows.append(row)
+        def old():
+            run(a[:r], b, c[:r], top)
+            if r < m:
+                run(a[r:], b, c[r:], rest)
+        old()
+        torch.cuda.synchronize()
+        ok = bool(torch.all((c.float() - ref).abs() <= atol + rtol * ref.abs()))
+        ok_all &= ok
+        fns = {"new": lambda: ops.gemm_bf16(a, b, c), "old": old,
+               "torch": lambda: torch.matmul(a, b.T, out=c)}
+        t = {x: [] for x in fns}
+        for _ in range(args.rounds):
+            for x, fn in fns.items():
+                t[x].append(timed(fn, args.iters))
+        fl = 2.0 * m * n * k
+        row = {"shape": [m, n, k], "new_plan": list(ops.kernels.k1_splitk_plan(m, n, k)),
+               "old_plan": spec, "old_ok": ok}
+        for x, v in t.items():
+            v.sort()
+            row[x] = round(fl / v[len(v) // 2] / 1e9, 1)
+        row["new/old"] = round(row["new"] / row["old"], 3)
         print(json.dumps(row), flush=True)
-        del a, b, c
-    if rows:
-        nr = [r["new_over_hipblaslt"] for r in rows]
-        orr = [r["old_over_hipblaslt"] for r in rows]
-        print(json.dumps({"summary": True, "shapes": len(rows),
-                          "new_ahead": sum(x > 1.0 for x in nr),
-                          "new_below_0.97": sum(x < 0.97 for x in nr),
-                          "old_ahead": sum(x > 1.0 for x in orr),
-                          "old_below_0.97": sum(x < 0.97 for x in orr),
-                          "new_min": min(nr), "new_median": statistics.median(nr),
-                          "new_over_old_min": min(r["new_over_old"] for r in rows),
-                          "new_over_old_median": statistics.median(r["new_over_old"] for r in rows)}),
-              flush=True)
+    return 0 if ok_all else 1
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -148,7 +148,7 @@ constexpr SmallTile kSmallTiles[] = {{15, 128, 128, 0.60, true, false, true, 1.1
                                      {18, 256, 160, 0.61, false, false, false, 1.0},
                                      {27, 192, 256, 0.82, true, true, false, 1.0, true},
                                      {28, 256, 192, 0.82, true, true, false, 1.0, true}};
-// host-only A/B knob (tools/plan_ab.py): the plan without the 192-wide tiles
+// host-only A/B knob (tools/pp_plan_ab.py): the plan without the 192-wide tiles
 static bool g_plan_pp = true;
 NTM_API void ntm_set_plan_pp_tiles(int on) { g_plan_pp = on != 0; }
 constexpr int kPpMinK = 1024;
