@@ -151,6 +151,24 @@ constexpr SmallTile kSmallTiles[] = {{15, 128, 128, 0.60, true, false, true, 1.1
 // host-only A/B knob (tools/pp_plan_ab.py): the plan without the 192-wide tiles
 static bool g_plan_pp = true;
 NTM_API void ntm_set_plan_pp_tiles(int on) { g_plan_pp = on != 0; }
+// The counted vmcnt phase P (0..3) of the 192-wide ping-pong build <ah, bh>
+// waits for (Geo::vmc, gemm_bf16_pp3h.hpp; 128 / 128 is pingpong8c's 10): host
+// only, for the CPU model of the DMA schedule (tests/test_pp3h_schedule_model.py).
+NTM_API int ntm_pp3h_vmcnt(int ah, int bh, int phase) {
+  using namespace ntm::gemm3h;
+  if (phase < 0 || phase > 3) return -1;
+  int v[4];
+  auto fill = [&](auto geo) {
+    using G = decltype(geo);
+    v[0] = G::vmc(0), v[1] = G::vmc(1), v[2] = G::vmc(2), v[3] = G::vmc(3);
+  };
+  if (ah == 64 && bh == 128) fill(Geo<64, 128>{});
+  else if (ah == 128 && bh == 64) fill(Geo<128, 64>{});
+  else if (ah == 96 && bh == 128) fill(Geo<96, 128>{});
+  else if (ah == 128 && bh == 128) fill(Geo<128, 128>{});
+  else return -1;
+  return v[phase];
+}
 constexpr int kPpMinK = 1024;
 constexpr double kSplitPenalty = 0.25;  // a second launch, in 128x128-tile-round units
 
