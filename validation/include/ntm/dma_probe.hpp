@@ -1,0 +1,81 @@
+// LDS-DMA access-pattern probe (experimental library only): which per-CU
+// resource makes K1 slow when the rows of A / B are only 16-byte aligned
+// (K % 16 == 8, profiles/r5_h192/)? The loads of the 256x256 ping-pong are
+// replayed with no MFMAs: per K-tile, four 128-row halves, each wave staging
+// 16 rows x 64 k as two 16-B-per-lane glds pieces (k chunks 0-3, then 4-7),
+// counted vmcnt(10) as in the kernel. Every workgroup streams the same 512
+// rows, so the XCD's L2 serves them (as the GEMM's shared A / B panels).
+//
+// MODE 0: the kernel's pattern at the given row pitch (aligned or not).
+// MODE 1: at a misaligned pitch, each row's K-tile t re-based to whole 64-B
+//         quads that never straddle a line: piece 1 = the second half of the
+//         row's aligned line t, piece 2 = the first half of line t + 1 - two
+//         L1 accesses per row per K-tile as when aligned, but each line still
+//         fetched by two different K-tiles (the accesses of a half-line ring
+//         in LDS; the data is the wrong k window - timing only).
+// MODE 2: at a misaligned pitch, each row re-based down to its aligned line -
+//         the aligned pattern on the same rows (what a 3-line ring would load).
+#pragma once
+
+#include "ntm/gemm_bf16.hpp"
+
+namespace ntm {
+namespace dprobe {
+
+using namespace ::ntm::gemm;
+
+template <int MODE>
+__global__ void __launch_bounds__(512) dma_probe_kernel(const __bf16* base, int pitch, int T,
+                                                        int reps) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * kTileBytes];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int r = lane >> 2, cl = lane & 3;
+  const char* rows[4];
+#pragma unroll
+  for (int h = 0; h < 4; ++h) {
+    const char* p = (const char*)(base + (size_t)(h * 128 + w * 16 + r) * pitch);
+    if constexpr (MODE != 0) p = (const char*)((size_t)p & ~(size_t)127);
+    rows[h] = p;
+  }
+  for (int rep = 0; rep < reps; ++rep) {
+    for (int t = 0; t < T; ++t) {
+#pragma unroll
+      for (int h = 0; h < 4; ++h) {
+        const char* s1;
+        const char* s2;
+        if constexpr (MODE == 1) {
+          s1 = rows[h] + (size_t)t * 128 + 64 + cl * 16;
+          s2 = rows[h] + (size_t)(t + 1) * 128 + cl * 16;
+        } else {
+          s1 = rows[h] + (size_t)t * 128 + cl * 16;
+          s2 = s1 + 64;
+        }
+        char* d = smem + (t & 1) * kTileBytes + h * kHalfBytes + (2 * w) * 1024;
+        glds16((const __bf16*)s1, d);
+        glds16((const __bf16*)s2, d + 1024);
+        wait_vmcnt<10>();
+      }
+    }
+  }
+  wait_vmcnt<0>();
+}
+
+// rows of the probe: 512 (4 halves x 128); the buffer must hold 512 rows of
+// `pitch` elements plus (T + 1) * 64 + 64 elements past the last row start
+inline hipError_t launch_dma_probe(int mode, const __bf16* base, int pitch, int T, int reps,
+                                   int grid, hipStream_t s) {
+  if (T < 1 || reps < 1 || grid < 1 || pitch < (T + 1) * 64 + 64) return hipErrorInvalidValue;
+  if (mode == 0)
+    hipLaunchKernelGGL(dma_probe_kernel<0>, dim3(grid), dim3(512), 0, s, base, pitch, T, reps);
+  else if (mode == 1)
+    hipLaunchKernelGGL(dma_probe_kernel<1>, dim3(grid), dim3(512), 0, s, base, pitch, T, reps);
+  else if (mode == 2)
+    hipLaunchKernelGGL(dma_probe_kernel<2>, dim3(grid), dim3(512), 0, s, base, pitch, T, reps);
+  else
+    return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+}  // namespace dprobe
+}  // namespace ntm

@@ -23,6 +23,7 @@
 // (variant 39 / fp8 knob 12, gemm_w4k.hpp: 4 waves x 128x128 per wave, one
 // barrier per K-tile; it tied the 8-wave default, profiles/r3_k1));
 // what stays is used by a test or a tool under tools/.
+#include "ntm/dma_probe.hpp"
 #include "ntm/gemm_bf16.hpp"
 #include "ntm/gemm_bf16_pp3.hpp"
 #include "ntm/gemm_bf16_pp3h.hpp"
@@ -259,4 +260,12 @@ NTM_API int ntm_stream_copy_spol(const void* src, void* dst, size_t bytes, int u
   NTM_SPOL(8, 0) NTM_SPOL(8, 1) NTM_SPOL(8, 2) NTM_SPOL(8, 3) NTM_SPOL(8, 4) NTM_SPOL(8, 5)
 #undef NTM_SPOL
   return (int)hipGetLastError();
+}
+
+// LDS-DMA access-pattern probe (dma_probe.hpp; tools/dma_probe.py): the 256x256
+// ping-pong's loads with no MFMAs, mode 0 / 1 / 2, `grid` workgroups of 512.
+NTM_API int ntm_dma_probe(int mode, const void* base, int pitch, int T, int reps, int grid,
+                          void* stream) {
+  return (int)ntm::dprobe::launch_dma_probe(mode, (const __bf16*)base, pitch, T, reps, grid,
+                                            S(stream));
 }
