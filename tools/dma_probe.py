@@ -7,7 +7,8 @@ ping-pong's loads without MFMAs, on rows whose pitch is 128-B aligned or only
      K-tile, each line still fetched by two K-tiles)
   2  misaligned rows re-based down to their aligned line (the aligned pattern)
 
-Prints per-CU GB/s of staged bytes, interleaved rounds, median.
+Prints per-CU GB/s of staged bytes, interleaved rounds, median. --depths 0,1,2,3
+repeats it with 5 / 8 / 12 / 16 halves in flight (counted vmcnt 10 / 16 / 24 / 32).
 
     python tools/dma_probe.py [--k 4096 --grid 256 --reps 20 --rounds 7]
 """
@@ -29,11 +30,16 @@ def main():
     ap.add_argument("--grid", type=int, default=256)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--depths", default="0", help="in-flight depths: 0..3 = vmcnt 10 / 16 / 24 / 32")
     args = ap.parse_args()
     L = lib_experimental()
     T = args.k // 64 - 2
-    cases = {"aligned/0": (0, args.k), "misaligned/0": (0, args.k + 8),
-             "misaligned/1": (1, args.k + 8), "misaligned/2": (2, args.k + 8)}
+    cases = {}
+    for d in (int(x) for x in args.depths.split(",")):
+        sfx = "" if d == 0 else f"@vm{(10, 16, 24, 32)[d]}"
+        cases.update({"aligned/0" + sfx: (10 * d, args.k), "misaligned/0" + sfx: (10 * d, args.k + 8),
+                      "misaligned/1" + sfx: (10 * d + 1, args.k + 8),
+                      "misaligned/2" + sfx: (10 * d + 2, args.k + 8)})
     bufs = {p: torch.zeros(513 * p, dtype=torch.bfloat16, device="cuda") for p in {args.k, args.k + 8}}
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 

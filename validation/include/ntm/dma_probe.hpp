@@ -24,7 +24,17 @@ namespace dprobe {
 
 using namespace ::ntm::gemm;
 
-template <int MODE>
+template <int N>
+__device__ __forceinline__ void wait_vm_deep() {
+  if constexpr (N == 10) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+  if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  if constexpr (N == 24) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+  if constexpr (N == 32) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+}
+
+// VM: the counted wait after each half (10 = the kernel's: 5 halves in flight;
+// deeper values only exist here, where nothing reads the LDS)
+template <int MODE, int VM = 10>
 __global__ void __launch_bounds__(512) dma_probe_kernel(const __bf16* base, int pitch, int T,
                                                         int reps) {
   __shared__ __attribute__((aligned(16))) char smem[2 * kTileBytes];
@@ -54,7 +64,7 @@ __global__ void __launch_bounds__(512) dma_probe_kernel(const __bf16* base, int 
         char* d = smem + (t & 1) * kTileBytes + h * kHalfBytes + (2 * w) * 1024;
         glds16((const __bf16*)s1, d);
         glds16((const __bf16*)s2, d + 1024);
-        wait_vmcnt<10>();
+        wait_vm_deep<VM>();
       }
     }
   }
@@ -66,14 +76,18 @@ __global__ void __launch_bounds__(512) dma_probe_kernel(const __bf16* base, int 
 inline hipError_t launch_dma_probe(int mode, const __bf16* base, int pitch, int T, int reps,
                                    int grid, hipStream_t s) {
   if (T < 1 || reps < 1 || grid < 1 || pitch < (T + 1) * 64 + 64) return hipErrorInvalidValue;
-  if (mode == 0)
-    hipLaunchKernelGGL(dma_probe_kernel<0>, dim3(grid), dim3(512), 0, s, base, pitch, T, reps);
-  else if (mode == 1)
-    hipLaunchKernelGGL(dma_probe_kernel<1>, dim3(grid), dim3(512), 0, s, base, pitch, T, reps);
-  else if (mode == 2)
-    hipLaunchKernelGGL(dma_probe_kernel<2>, dim3(grid), dim3(512), 0, s, base, pitch, T, reps);
-  else
-    return hipErrorInvalidValue;
+  // mode + 10 * d: d = 0..3 -> counted wait 10 / 16 / 24 / 32 (5 / 8 / 12 / 16 halves in flight)
+  const int d = mode / 10;
+  mode %= 10;
+  if (mode > 2 || d > 3) return hipErrorInvalidValue;
+#define NTM_DPROBE(M, V) \
+  if (mode == M && (V) == (d == 0 ? 10 : d == 1 ? 16 : d == 2 ? 24 : 32)) \
+    hipLaunchKernelGGL((dma_probe_kernel<M, V>), dim3(grid), dim3(512), 0, s, base, pitch, T, reps);
+  NTM_DPROBE(0, 10) NTM_DPROBE(1, 10) NTM_DPROBE(2, 10)
+  NTM_DPROBE(0, 16) NTM_DPROBE(1, 16) NTM_DPROBE(2, 16)
+  NTM_DPROBE(0, 24) NTM_DPROBE(1, 24) NTM_DPROBE(2, 24)
+  NTM_DPROBE(0, 32) NTM_DPROBE(1, 32) NTM_DPROBE(2, 32)
+#undef NTM_DPROBE
   return hipGetLastError();
 }
 
