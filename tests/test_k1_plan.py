@@ -320,3 +320,33 @@ def test_pp_tiles_one_launch_and_toggle(k1_plan):
             assert ops.k1_fp8_plan(m, n, 2 * k)[1] not in ("pp192x256", "pp256x192")
     finally:
         ops.set_plan_pp_tiles(True)
+
+
+def test_plan_cache_returns_the_search_result(k1_plan, splitk_plan):
+    """Plans are memoised per host thread (a 256-slot table keyed by M, N, K, the
+    CU count, split-K, fp8 and the pp-tile knob): many more shapes than slots,
+    asked twice in different orders, give the same answers, and the knobs in the
+    key still change the plan."""
+    import random
+
+    from nvidia_terraform_modules_amd import ops
+    from nvidia_terraform_modules_amd.ops._lib import lib
+
+    rng = random.Random(11)
+    shapes = [tuple(rng.randrange(8, 8193, 8) for _ in range(3)) for _ in range(700)]
+    first = [(k1_plan(*s), splitk_plan(*s)) for s in shapes]
+    second = [(k1_plan(*s), splitk_plan(*s)) for s in reversed(shapes)][::-1]
+    assert first == second
+    assert k1_plan(3904, 2584, 12760) == (3904, "pp256x192", "pp256x192")
+    try:
+        lib().ntm_set_cus_override(128)   # 231 tiles no longer fit one round
+        assert k1_plan(3904, 2584, 12760) == (2816, "pingpong8cm", "tile160")
+    finally:
+        lib().ntm_set_cus_override(0)
+    assert k1_plan(3904, 2584, 12760) == (3904, "pp256x192", "pp256x192")
+    ops.set_plan_pp_tiles(False)
+    try:
+        assert k1_plan(3904, 2584, 12760)[1] == "pingpong8cm"
+    finally:
+        ops.set_plan_pp_tiles(True)
+    assert k1_plan(3904, 2584, 12760)[1] == "pp256x192"

@@ -239,7 +239,7 @@ constexpr double kSkSplitMinFixup = 8e-6;
 // fp8 (K1-fp8's plan): K counted in bf16-sized pairs of e4m3 values (a K-tile
 // costs the same cycles in both dtypes); only the tiles with an fp8 build - the
 // 256x256 kernel and the wave-specialised ones - and no split-K.
-inline K1Plan plan_k1(int M, int N, int K, bool splitk = false, bool fp8 = false) {
+inline K1Plan plan_k1_search(int M, int N, int K, bool splitk, bool fp8) {
   // the CUs the launches below run on (256 on MI355X in SPX mode; fewer in a
   // DPX / CPX partition): stream-K's decomposition must be the launch's own
   const double kCUs = (double)ntm::gemm6::device_cus();
@@ -385,6 +385,45 @@ inline K1Plan plan_k1(int M, int N, int K, bool splitk = false, bool fp8 = false
     }
   }
   return split;
+}
+
+// The plan is an exhaustive search over tiles and row splits: 3-25 us of host
+// time per shape, paid on every default-dispatch call until round 5 (twice in
+// ntm_gemm_bf16_ex). For C of a few microseconds that made the launch
+// host-bound (6712x280x368: 18.3 us per call against 8.0 for its own tile,
+// profiles/r5_h192/small_shapes_sweep.log). Plans are memoised per host thread
+// in a small direct-mapped table keyed by everything the search reads.
+struct PlanKey {
+  int M, N, K, cus;
+  bool splitk, fp8, pp;
+  bool operator==(const PlanKey& o) const {
+    return M == o.M && N == o.N && K == o.K && cus == o.cus && splitk == o.splitk &&
+           fp8 == o.fp8 && pp == o.pp;
+  }
+};
+struct PlanEntry {
+  PlanKey key;
+  K1Plan plan;
+  double unsplit_s, sk_s;  // the search's debug outputs (ntm_k1_plan_times)
+  bool valid;
+};
+constexpr int kPlanCacheSlots = 256;
+
+inline K1Plan plan_k1(int M, int N, int K, bool splitk = false, bool fp8 = false) {
+  static thread_local PlanEntry cache[kPlanCacheSlots] = {};
+  const PlanKey key{M, N, K, ntm::gemm6::device_cus(), splitk, fp8, g_plan_pp};
+  const unsigned h = ((unsigned)M * 2654435761u) ^ ((unsigned)N * 40503u) ^ ((unsigned)K * 97u) ^
+                     ((unsigned)key.cus << 3) ^ (splitk ? 0x55u : 0u) ^ (fp8 ? 0xAAu : 0u) ^
+                     (g_plan_pp ? 0x100u : 0u);
+  PlanEntry& e = cache[(h ^ (h >> 8) ^ (h >> 16)) % kPlanCacheSlots];
+  if (e.valid && e.key == key) {
+    g_plan_debug_unsplit_s = e.unsplit_s;
+    g_plan_debug_sk_s = e.sk_s;
+    return e.plan;
+  }
+  const K1Plan p = plan_k1_search(M, N, K, splitk, fp8);
+  e = PlanEntry{key, p, g_plan_debug_unsplit_s, g_plan_debug_sk_s, true};
+  return p;
 }
 
 // The split-K plan's predicted seconds for (M, N, K): the best unsplit plan and
