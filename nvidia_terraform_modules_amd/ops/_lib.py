@@ -62,6 +62,9 @@ def _declare(lib: ctypes.CDLL) -> None:
                               c_size, c_vp], c_int),
         "ntm_splitk_ws_bytes": ([c_int, c_int, c_int, c_int], c_size),
         "ntm_sk_ws_bytes": ([c_int, c_int, c_int], c_size),
+        "ntm_skh_ws_bytes": ([c_int, c_int, c_int, c_int], c_size),
+        "ntm_gemm_bf16_skh": ([c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int,
+                               c_vp, c_size, c_vp], c_int),
         "ntm_k1_plan_times": ([c_int, c_int, c_int, c_vp, c_vp], c_int),
         "ntm_gemm_bf16_sk": ([c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp,
                               c_size, c_vp], c_int),

@@ -39,7 +39,7 @@ GEMM_VARIANTS = {"default": 0, "pingpong8": 1, "pingpong8b": 4,
                  "pp8o_g128": 41, "pp8o_g128_nostore": 42, "pp8o_nostore": 43,
                  "pingpong8om": 47, "pingpong8od": 48, "pingpong8s": 49,
                  "pingpong8omd": 51, "pp192x256": 27, "pp256x192": 28,
-                 "pp224x256": 29}
+                 "pp224x256": 29, "pp192x256s": 54, "pp256x192s": 55}
 
 
 # variants built only into libntm_experimental.so (tests / tools): never selected
@@ -101,11 +101,30 @@ def k1_splitk_plan(m: int, n: int, k: int) -> tuple[int, str, str, int]:
 _DEFAULT_WS: dict[tuple[int, int, int], int] = {}
 
 
-def set_plan_pp_tiles(on: bool) -> None:
+# (M, N, K) -> the stream-K variant of a stream-K default plan
+_DEFAULT_SK: dict[tuple[int, int, int], str] = {}
+
+# stream-K split mode on the 192-wide ping-pong tiles (gemm_bf16_skh.hpp)
+SKH_VARIANTS = ("pp192x256s", "pp256x192s")
+SK_VARIANTS = ("pingpong8s",) + SKH_VARIANTS
+
+
+def set_plan_pp_tiles(on: bool = True, split: bool | None = None) -> None:
     """A/B knob for tools (tools/pp_plan_ab.py): let the plan use the 192x256 /
-    256x192 ping-pong tiles (the default) or not. Process-wide."""
-    lib().ntm_set_plan_pp_tiles(1 if on else 0)
+    256x192 ping-pong tiles on all of C (``on``) and in stream-K split mode
+    (``split``, default: as ``on``). The shipping plan has both. Process-wide."""
+    split = on if split is None else split
+    lib().ntm_set_plan_pp_tiles((1 if on else 0) | (2 if split else 0))
     _DEFAULT_WS.clear()
+    _DEFAULT_SK.clear()
+
+
+def skh_ws_bytes(variant: str, m: int, n: int, k: int) -> int:
+    """Workspace of stream-K split mode on a 192-wide tile ("pp192x256s" /
+    "pp256x192s") for (M, N, K) on this device; 0 when it does not serve it."""
+    if m <= 0 or n <= 0 or k <= 0:
+        return 0
+    return int(lib().ntm_skh_ws_bytes(GEMM_VARIANTS[variant], m, n, k))
 
 
 def _default_ws_bytes(m: int, n: int, k: int) -> int:
@@ -115,10 +134,13 @@ def _default_ws_bytes(m: int, n: int, k: int) -> int:
     wsb = _DEFAULT_WS.get(key)
     if wsb is None:
         _, top, _, sp = k1_splitk_plan(m, n, k)  # raises if no kernel serves the shape
-        if top == "pingpong8s":
+        if top in SK_VARIANTS:
             # stream-K only where its own launch serves the shape (the plan and the
             # launch size for the same CUs; belt and braces): else the unsplit plan
-            wsb = -1 if sk_ws_bytes(m, n, k) > 0 else 0
+            ok = (sk_ws_bytes(m, n, k) if top == "pingpong8s" else skh_ws_bytes(top, m, n, k)) > 0
+            wsb = -1 if ok else 0
+            if ok:
+                _DEFAULT_SK[key] = top
         else:
             wsb = lib().ntm_splitk_ws_bytes(m, n, k, sp) if sp > 1 else 0
         _DEFAULT_WS[key] = wsb
@@ -156,6 +178,10 @@ def gemm_bf16(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
                              "(masked tiles: N % 4, K % 8; others: whole tiles, K % 128)")
     elif variant == "default":
         _default_ws_bytes(m, n, k)  # the native plan is the one authority on what it serves
+    elif variant in SKH_VARIANTS:
+        if not skh_ws_bytes(variant, m, n, k):
+            raise ValueError(f"shape ({m},{n},{k}) not served by {variant} (N % 8, K % 8, "
+                             "K >= 128; at most half a round of its tiles, >= 2 K slices each)")
     elif variant in ("pingpong8s", "pingpong8s_rev", "pingpong8s_nopair"):  # stream-K
         if not sk_ws_bytes(m, n, k):
             raise ValueError(f"shape ({m},{n},{k}) not served by stream-K (N % 8, K % 8, K >= 128; "
@@ -176,6 +202,8 @@ def gemm_bf16(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
     if variant in ("pingpong8s", "pingpong8s_rev", "pingpong8s_nopair"):
         return _gemm_bf16_sk(a, b, out, rev=variant == "pingpong8s_rev",
                              nopair=variant == "pingpong8s_nopair")
+    if variant in SKH_VARIANTS:
+        return _gemm_bf16_sk(a, b, out, sk_variant=variant)
     if splits > 1:
         if variant not in MASKED_TILES:
             raise ValueError(f"split-K runs on {sorted(MASKED_TILES)}, not {variant}")
@@ -199,7 +227,7 @@ def gemm_bf16(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
         check(rc, "ntm_gemm_bf16_experimental")
         return out
     if variant == "default" and _default_ws_bytes(m, n, k) < 0:
-        return _gemm_bf16_sk(a, b, out)
+        return _gemm_bf16_sk(a, b, out, sk_variant=_DEFAULT_SK[(m, n, k)])
     if variant == "default" and _default_ws_bytes(m, n, k):
         wsb = _default_ws_bytes(m, n, k)
         ws = torch.empty((wsb + 3) // 4, dtype=torch.float32, device=a.device)
@@ -262,13 +290,22 @@ def sk_xcc_error(device=None, clear: bool = True) -> int:
 
 
 def _gemm_bf16_sk(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, rev: bool = False,
-                  nopair: bool = False) -> torch.Tensor:
-    """Stream-K (gemm_bf16_sk.hpp): fp32 partials of the split tiles and one
-    counter per split in this stream's cached workspace (_sk_workspace).
-    rev / nopair: experimental builds (segments reversed; split mode's
-    S-partial protocol also at S = 2)."""
+                  nopair: bool = False, sk_variant: str = "pingpong8s") -> torch.Tensor:
+    """Stream-K (gemm_bf16_sk.hpp; sk_variant "pp192x256s" / "pp256x192s": split
+    mode on the 192-wide tiles, gemm_bf16_skh.hpp): fp32 partials of the split
+    tiles and one counter per split in this stream's cached workspace
+    (_sk_workspace). rev / nopair: experimental builds (segments reversed; split
+    mode's S-partial protocol also at S = 2)."""
     m, k = a.shape
     n = b.shape[0]
+    if sk_variant in SKH_VARIANTS:
+        wsb = skh_ws_bytes(sk_variant, m, n, k)
+        ws = _sk_workspace(a.device, wsb)
+        rc = lib().ntm_gemm_bf16_skh(GEMM_VARIANTS[sk_variant], a.data_ptr(), b.data_ptr(),
+                                     out.data_ptr(), m, n, k, a.stride(0), b.stride(0),
+                                     out.stride(0), ws.data_ptr(), wsb, stream_handle())
+        check(rc, "ntm_gemm_bf16_skh")
+        return out
     wsb = sk_ws_bytes(m, n, k)
     ws = _sk_workspace(a.device, wsb)
     fn = (lib_experimental().ntm_gemm_bf16_sk_rev if rev else

@@ -128,7 +128,7 @@ def test_splitk_plan_for_skinny_long_k(splitk_plan, m, n, k, variant, splits):
 
 @pytest.mark.parametrize("m,n,k", [(8192, 8192, 8192), (4096, 4096, 4096), (1000, 3112, 768),
                                    (3200, 3200, 3200), (6144, 6144, 6144), (2080, 3844, 256),
-                                   (2048, 2048, 4096), (3072, 2048, 6144), (8008, 536, 2896)])
+                                   (2048, 2048, 4096), (8008, 536, 2896)])
 def test_splitk_plan_keeps_unsplit_plan(k1_plan, splitk_plan, m, n, k):
     """Chip-filling C or short K: split-K is not worth its fp32 partials, and the
     plan is exactly the unsplit one."""
@@ -139,9 +139,31 @@ def test_splitk_plan_keeps_unsplit_plan(k1_plan, splitk_plan, m, n, k):
                                    (1872, 2224, 5208)])
 def test_splitk_plan_takes_stream_k_on_ragged_one_round_c(k1_plan, splitk_plan, m, n, k):
     """One round of a small tile on ragged C runs 1.1-1.5x its modelled time;
-    stream-K's split mode measured 9-39 % faster there (profiles/r4_sks/)."""
+    stream-K's split mode measured 9-39 % faster there (profiles/r4_sks/), on the
+    256x256 or (round 5) the 192-wide tiles."""
     assert k1_plan(m, n, k)[1].startswith("tile")
-    assert splitk_plan(m, n, k) == (m, "pingpong8s", "pingpong8s", 1)
+    top, tv, rest, sp = splitk_plan(m, n, k)
+    assert (top, sp) == (m, 1) and tv == rest and tv in ("pingpong8s", "pp192x256s", "pp256x192s")
+
+
+@pytest.mark.parametrize("m,n,k,variant", [
+    (4152, 1096, 16056, "pp256x192s"),   # 85 256x256 tiles = 22 of 32 CUs per XCD busy
+    (2840, 1768, 8904, "pp192x256s"),
+    (4800, 1168, 15776, "pp192x256s"),
+    (3072, 2048, 6144, "pp192x256s"),    # was tile128x256: +6.7 % (profiles/r5_skh/)
+    (4672, 1472, 6696, "pingpong8s"),    # 256x256 split mode stays where it is faster
+])
+def test_splitk_plan_split_mode_on_192_tiles(splitk_plan, m, n, k, variant):
+    """Split mode on the 192-wide ping-pong tiles (gemm_bf16_skh.hpp): more CUs
+    busy for 0.75 of the work each; off with the A/B knob's split bit."""
+    from nvidia_terraform_modules_amd import ops
+
+    assert splitk_plan(m, n, k) == (m, variant, variant, 1)
+    try:
+        ops.set_plan_pp_tiles(True, split=False)
+        assert splitk_plan(m, n, k)[1] not in ("pp192x256s", "pp256x192s")
+    finally:
+        ops.set_plan_pp_tiles(True)
 
 
 @pytest.mark.parametrize("m,n,k", [(m, n, k) for m in (64, 333, 1000, 2048)

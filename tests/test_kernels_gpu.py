@@ -923,3 +923,47 @@ def test_stream_k_split_mode_vs_torch_fp32(ops, m, n, k):
     # is the same fp32 sum as partial0 + partial1 (commutative), so bitwise equal
     assert torch.equal(ops.gemm_bf16(a, b, variant="pingpong8s_nopair"), first)
 
+
+SKH_SHAPES = [(4152, 1096, 16056),  # 110 192x256 / 102 256x192 tiles: 2 slices, K % 16 == 8
+              (2840, 1768, 8904),   # the shapes the plan sends there
+              (5976, 888, 8720),
+              (1000, 1000, 4096),   # 24 / 20 tiles: 8 slices
+              (1000, 1000, 1000),   # partial K, one pair per slice
+              (192, 256, 256),      # one tile, 2 slices of one pair
+              (2048, 1536, 6144)]   # exact tiles
+
+
+@pytest.mark.parametrize("variant", ["pp192x256s", "pp256x192s"])
+@pytest.mark.parametrize("m,n,k", SKH_SHAPES)
+def test_stream_k_split_mode_192_tiles_vs_torch_fp32(ops, variant, m, n, k):
+    """Split mode on the 192-wide ping-pong tiles (gemm_bf16_skh.hpp, round 5):
+    vs the fp32 product, no column past C written, repeat launches give the same
+    bytes, every slice ran on the combiner's XCD."""
+    if not ops.kernels.skh_ws_bytes(variant, m, n, k):
+        pytest.skip(f"{variant}: more than half a round of its tiles")
+    a = _rand(ops, (m, k), 681 + k)
+    b = _rand(ops, (n, k), 683 + n)
+    out = torch.full((m, n + 8), 7.0, dtype=torch.bfloat16, device="cuda")
+    c = ops.gemm_bf16(a, b, out[:, :n], variant=variant)
+    ref = a.float() @ b.float().T
+    atol, rtol = ops.gemm_tolerance(k)
+    err = (c.float() - ref).abs()
+    assert torch.all(err <= atol + rtol * ref.abs()), float(err.max())
+    assert torch.all(out[:, n:] == 7.0)
+    first = c.clone()
+    for _ in range(3):
+        assert torch.equal(ops.gemm_bf16(a, b, variant=variant), first)
+    assert ops.sk_xcc_error() == 0
+
+
+@pytest.mark.parametrize("m,n,k", [(4152, 1096, 16056), (2840, 1768, 8904)])
+def test_default_runs_split_mode_on_192_tiles(ops, m, n, k):
+    """The default plan picks split mode on a 192-wide tile for these shapes, and
+    the default dispatch gives that variant's bytes."""
+    top = ops.k1_splitk_plan(m, n, k)[1]
+    assert top in ("pp192x256s", "pp256x192s")
+    a = _rand(ops, (m, k), 5)
+    b = _rand(ops, (n, k), 6)
+    assert torch.equal(ops.gemm_bf16(a, b), ops.gemm_bf16(a, b, variant=top))
+    assert ops.sk_xcc_error() == 0
+

@@ -52,6 +52,15 @@ ALLOWED_K1 = {
     "ntm::gemm3h::gemm_bf16_pp3h_kernel<64, 128, true>",
     "ntm::gemm3h::gemm_bf16_pp3h_kernel<128, 64, false>",
     "ntm::gemm3h::gemm_bf16_pp3h_kernel<128, 64, true>",
+    # ... in stream-K split mode <AH, BH, TAIL, PAIR> (round 5)
+    "ntm::gemmskh::gemm_bf16_sksh_kernel<64, 128, false, false>",
+    "ntm::gemmskh::gemm_bf16_sksh_kernel<64, 128, false, true>",
+    "ntm::gemmskh::gemm_bf16_sksh_kernel<64, 128, true, false>",
+    "ntm::gemmskh::gemm_bf16_sksh_kernel<64, 128, true, true>",
+    "ntm::gemmskh::gemm_bf16_sksh_kernel<128, 64, false, false>",
+    "ntm::gemmskh::gemm_bf16_sksh_kernel<128, 64, false, true>",
+    "ntm::gemmskh::gemm_bf16_sksh_kernel<128, 64, true, false>",
+    "ntm::gemmskh::gemm_bf16_sksh_kernel<128, 64, true, true>",
     "ntm::gemm2::gemm_bf16_pp2_kernel<false, 0>",
     "ntm::gemm2::gemm_bf16_pp2_kernel<false, 3>",
     "ntm::gemm2::gemm_bf16_pp2_kernel<true, 0>",

@@ -1,5 +1,5 @@
 """A/B of the default K1 plan with and without the 192x256 / 256x192 ping-pong
-tiles (developer tool): per shape, the default dispatch with the tiles (new),
+tiles, or (--split-only) without just their stream-K split mode (developer tool): per shape, the default dispatch with the tiles (new),
 without them (old) and hipBLASLt, timed interleaved, median over rounds; the
 plans both ways. Shapes: --shapes MxNxK,... or a seeded ragged set
 (tools/ragged_sweep.py's generator) or --random (uniform M, N, K).
@@ -30,7 +30,10 @@ def main():
     ap.add_argument("--changed-only", action="store_true", help="skip shapes whose plan is the same")
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--split-only", action="store_true",
+                    help="old = the plan without split mode on the 192-wide tiles only")
     args = ap.parse_args()
+    old_knob = (True, False) if args.split_only else (False, False)
     if args.shapes:
         shapes = [tuple(int(x) for x in s.split("x")) for s in args.shapes.split(",") if s]
     elif args.random:
@@ -40,7 +43,7 @@ def main():
         shapes = ragged_shapes(args.n, args.seed)
     rows = []
     for m, n, k in shapes:
-        ops.set_plan_pp_tiles(False)
+        ops.set_plan_pp_tiles(*old_knob)
         old_plan = list(ops.k1_splitk_plan(m, n, k))
         ops.set_plan_pp_tiles(True)
         new_plan = list(ops.k1_splitk_plan(m, n, k))
@@ -50,11 +53,11 @@ def main():
         b = ops.fill_uniform_(torch.empty((n, k), dtype=torch.bfloat16, device="cuda"), 2)
         c = torch.empty((m, n), dtype=torch.bfloat16, device="cuda")
 
-        def run(on):
-            ops.set_plan_pp_tiles(on)
+        def run(knob):
+            ops.set_plan_pp_tiles(*knob)
             ops.gemm_bf16(a, b, c)
 
-        fns = {"new": lambda: run(True), "old": lambda: run(False),
+        fns = {"new": lambda: run((True, True)), "old": lambda: run(old_knob),
                "hipblaslt": lambda: torch.matmul(a, b.T, out=c)}
         t = {name: [] for name in fns}
         for r in range(args.rounds):

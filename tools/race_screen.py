@@ -89,6 +89,9 @@ def main():
         shapes = SHAPES_FP8 + SHAPES_RAGGED if fp8 else SHAPES_160 if tn == 160 else SHAPES
         if v.startswith("pingpong8o"):
             shapes = SHAPES_PERSIST + (SHAPES_PERSIST_RAGGED if v in ("pingpong8om", "pingpong8omd") else [])
+        if v in ("pp192x256s", "pp256x192s"):
+            shapes = [(4152, 1096, 16056), (2840, 1768, 8904), (1000, 1000, 4096), (1000, 1000, 1000),
+                      (192, 256, 256)]
         if v.startswith("pingpong8s"):
             shapes = SHAPES_SK if v == "pingpong8s" else SHAPES_SK[:7]  # REV: two-round mode
         if splits > 1:

@@ -23,7 +23,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from nvidia_terraform_modules_amd import ops  # noqa: E402
 
 CANDIDATES = ("pingpong8s", "pingpong8cm", "tile128", "tile256x128", "tile160", "tile160x128",
-              "tile128x160", "tile128x256", "pp192x256", "pp256x192", "pp224x256")
+              "tile128x160", "tile128x256", "pp192x256", "pp256x192", "pp224x256",
+              "pp192x256s", "pp256x192s")
 
 
 def ragged_shapes(n: int, seed: int, lo: float = 0.3, hi: float = 1.0) -> list:
@@ -80,6 +81,8 @@ def main():
         if args.candidates:
             for v in CANDIDATES:
                 if v == "pingpong8s" and not ops.sk_ws_bytes(m, n, k):
+                    continue
+                if v in ops.kernels.SKH_VARIANTS and not ops.kernels.skh_ws_bytes(v, m, n, k):
                     continue
                 fns[v] = lambda v=v: ops.gemm_bf16(a, b, c, variant=v)
         for spec in (x for x in args.splitk.split(",") if x):

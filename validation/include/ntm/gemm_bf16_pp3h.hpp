@@ -168,10 +168,11 @@ __device__ __forceinline__ void tile_h(const Ctx& c, gemm3::Frags3& f,
 }
 
 // Block -> output tile: tile_coords_of's bijective XCD remap + GROUP_M raster
-// on TM x TN tiles.
+// on TM x TN tiles; `bid` of `nwg` (blockIdx.x of gridDim.x, or a split-mode
+// workgroup's tile index of the tile count).
 template <int TM, int TN, int GROUP_M = kGroupM>
-__device__ __forceinline__ void tile_coords_h(int M, int N, int& tm, int& tn) {
-  const int bid = (int)blockIdx.x, nwg = (int)gridDim.x;
+__device__ __forceinline__ void tile_coords_of_h(int bid, int nwg, int M, int N, int& tm,
+                                                 int& tn) {
   const int xcd = bid & 7;
   const int q = nwg >> 3, r = nwg & 7;
   const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
@@ -183,6 +184,71 @@ __device__ __forceinline__ void tile_coords_h(int M, int N, int& tm, int& tn) {
   const int in_group = wgid - gid * group;
   tm = first_m + in_group % gsz;
   tn = in_group / gsz;
+}
+
+template <int TM, int TN, int GROUP_M = kGroupM>
+__device__ __forceinline__ void tile_coords_h(int M, int N, int& tm, int& tn) {
+  tile_coords_of_h<TM, TN, GROUP_M>((int)blockIdx.x, (int)gridDim.x, M, N, tm, tn);
+}
+
+// Each lane's source rows are fixed for the whole K loop; clamping them once
+// keeps every load in bounds (the clamped rows only feed C rows / columns the
+// epilogue does not store). A 64-row half: wave w stages 16-row block w >> 1,
+// k-half w & 1 (folded into the source).
+template <int AH, int BH>
+__device__ __forceinline__ void set_sources_h(const GemmArgs& p, Ctx& c, int m0, int n0,
+                                              int lane) {
+  const int r = lane >> 2;
+  const int cl = (lane & 3) ^ (((r >> 3) & 1) << 1);
+  const int ra = m0 + c.w * 16 + r, rb = n0 + c.w * 16 + r;
+  const int ra_hi = AH != 64 ? ra + 128 : m0 + 128 + (c.w >> 1) * 16 + r;
+  const int rb_hi = BH == 128 ? rb + 128 : n0 + 128 + (c.w >> 1) * 16 + r;
+  const int ka_hi = AH != 64 ? 0 : (c.w & 1) * 32, kb_hi = BH == 128 ? 0 : (c.w & 1) * 32;
+  c.src[kALo] = p.A + (size_t)min(ra, p.M - 1) * p.lda + cl * 8;
+  c.src[kAHi] = p.A + (size_t)min(ra_hi, p.M - 1) * p.lda + cl * 8 + ka_hi;
+  c.src[kBLo] = p.B + (size_t)min(rb, p.N - 1) * p.ldb + cl * 8;
+  c.src[kBHi] = p.B + (size_t)min(rb_hi, p.N - 1) * p.ldb + cl * 8 + kb_hi;
+}
+
+// K-tiles [t0, t1) (t0 even, t1 > t0 even; pieces at K-tiles >= t1 are dummies)
+// accumulated onto acc; drained (vmcnt(0)) on return, stagger balanced.
+// prologue: B-lo A-lo B-hi A-hi of t0, B-lo A-lo B-hi of t0 + 1 (virtual phases
+// -7..-1; the wait is phase -1's, a B-hi issue: vmc(3))
+template <int AH, int BH, bool TAIL>
+__device__ __forceinline__ void k_range_h(const GemmArgs& p, const Ctx& c, gemm3::Frags3& f,
+                                          f32x4 (&acc)[2][2][4][2], int t0, int t1) {
+  using G = Geo<AH, BH>;
+  issue_h<kBLo, 128, TAIL>(c, t0, 0, t1);
+  issue_h<kALo, 128, TAIL>(c, t0, 0, t1);
+  issue_h<kBHi, BH, TAIL>(c, t0, 0, t1);
+  issue_h<kAHi, AH, TAIL>(c, t0, 0, t1);
+  issue_h<kBLo, 128, TAIL>(c, t0 + 1, 1, t1);
+  issue_h<kALo, 128, TAIL>(c, t0 + 1, 1, t1);
+  issue_h<kBHi, BH, TAIL>(c, t0 + 1, 1, t1);
+  wait_vm<G::vmc(3)>();
+  raw_barrier();
+  read_b_h<kBLo, 2>(c, f.b0, 0);
+  if (c.wr == 1) raw_barrier();  // ping-pong stagger
+  int t = t0;
+  if constexpr (TAIL) {
+    // the zero-filling issue path only where a piece can reach past K
+    const int t_real = (p.K + BK - 1) / BK;
+    for (; t < t1 && t + 4 < t_real; t += 2) {
+      tile_h<AH, BH, false, false>(c, f, acc, t, t1);
+      tile_h<AH, BH, true, false>(c, f, acc, t + 1, t1);
+    }
+    for (; t < t1; t += 2) {
+      tile_h<AH, BH, false, true>(c, f, acc, t, t1);
+      tile_h<AH, BH, true, true>(c, f, acc, t + 1, t1);
+    }
+  } else {
+    for (; t < t1; t += 2) {
+      tile_h<AH, BH, false, false>(c, f, acc, t, t1);
+      tile_h<AH, BH, true, false>(c, f, acc, t + 1, t1);
+    }
+  }
+  if (c.wr == 0) raw_barrier();  // balance the stagger
+  wait_vmcnt<0>();                // dummy pieces: nothing lands after this
 }
 
 // LDS-staged masked epilogue (store_tile_lds's layout, pitch kStagePitch):
@@ -262,21 +328,7 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_pp3h_kernel(GemmArgs p)
   c.w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   c.wr = c.w >> 2;
   c.wc = c.w & 3;
-  {
-    // Each lane's source rows are fixed for the whole K loop; clamping them
-    // once keeps every load in bounds (the clamped rows only feed C rows /
-    // columns the epilogue does not store).
-    const int r = lane >> 2;
-    const int cl = (lane & 3) ^ (((r >> 3) & 1) << 1);
-    const int ra = m0 + c.w * 16 + r, rb = n0 + c.w * 16 + r;
-    const int ra_hi = AH != 64 ? ra + 128 : m0 + 128 + (c.w >> 1) * 16 + r;
-    const int rb_hi = BH == 128 ? rb + 128 : n0 + 128 + (c.w >> 1) * 16 + r;
-    const int ka_hi = AH != 64 ? 0 : (c.w & 1) * 32, kb_hi = BH == 128 ? 0 : (c.w & 1) * 32;
-    c.src[kALo] = p.A + (size_t)min(ra, p.M - 1) * p.lda + cl * 8;
-    c.src[kAHi] = p.A + (size_t)min(ra_hi, p.M - 1) * p.lda + cl * 8 + ka_hi;
-    c.src[kBLo] = p.B + (size_t)min(rb, p.N - 1) * p.ldb + cl * 8;
-    c.src[kBHi] = p.B + (size_t)min(rb_hi, p.N - 1) * p.ldb + cl * 8 + kb_hi;
-  }
+  set_sources_h<AH, BH>(p, c, m0, n0, lane);
   c.frag_off = (lane & 15) * 64 + ((lane >> 4) ^ ((lane >> 2) & 2)) * 16;
 
   f32x4 acc[2][2][4][2];
@@ -297,40 +349,7 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_pp3h_kernel(GemmArgs p)
     const int r = lane >> 2;
     c.lane_col = ((lane & 3) ^ (((r >> 3) & 1) << 1)) * 8;
   }
-
-  // prologue: B-lo0 A-lo0 B-hi0 A-hi0 B-lo1 A-lo1 B-hi1 (virtual phases -7..-1;
-  // the wait is phase -1's, a B-hi issue: vmc(3))
-  issue_h<kBLo, 128, TAIL>(c, 0, 0, T);
-  issue_h<kALo, 128, TAIL>(c, 0, 0, T);
-  issue_h<kBHi, BH, TAIL>(c, 0, 0, T);
-  issue_h<kAHi, AH, TAIL>(c, 0, 0, T);
-  issue_h<kBLo, 128, TAIL>(c, 1, 1, T);
-  issue_h<kALo, 128, TAIL>(c, 1, 1, T);
-  issue_h<kBHi, BH, TAIL>(c, 1, 1, T);
-  wait_vm<G::vmc(3)>();
-  raw_barrier();
-  read_b_h<kBLo, 2>(c, f.b0, 0);
-  if (c.wr == 1) raw_barrier();  // ping-pong stagger
-
-  if constexpr (TAIL) {
-    const int t_real = (p.K + BK - 1) / BK;
-    int t = 0;
-    for (; t + 4 < t_real; t += 2) {
-      tile_h<AH, BH, false, false>(c, f, acc, t, T);
-      tile_h<AH, BH, true, false>(c, f, acc, t + 1, T);
-    }
-    for (; t < T; t += 2) {
-      tile_h<AH, BH, false, true>(c, f, acc, t, T);
-      tile_h<AH, BH, true, true>(c, f, acc, t + 1, T);
-    }
-  } else {
-    for (int t = 0; t < T; t += 2) {
-      tile_h<AH, BH, false, false>(c, f, acc, t, T);
-      tile_h<AH, BH, true, false>(c, f, acc, t + 1, T);
-    }
-  }
-  if (c.wr == 0) raw_barrier();
-  wait_vmcnt<0>();  // dummy pieces: nothing may land after the WG exits
+  k_range_h<AH, BH, TAIL>(p, c, f, acc, 0, T);
   store_tile_h<AH, BH>(p, c, acc, m0, n0, lane);
 }
 

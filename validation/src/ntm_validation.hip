@@ -16,6 +16,7 @@
 #include "ntm/gemm_bf16_pp3h.hpp"
 #include "ntm/gemm_bf16_pp6.hpp"
 #include "ntm/gemm_bf16_sk.hpp"
+#include "ntm/gemm_bf16_skh.hpp"
 #include "ntm/gemm_bf16_t128.hpp"
 #include "ntm/gemm_fp8.hpp"
 
@@ -148,9 +149,13 @@ constexpr SmallTile kSmallTiles[] = {{15, 128, 128, 0.60, true, false, true, 1.1
                                      {18, 256, 160, 0.61, false, false, false, 1.0},
                                      {27, 192, 256, 0.82, true, true, false, 1.0, true},
                                      {28, 256, 192, 0.82, true, true, false, 1.0, true}};
-// host-only A/B knob (tools/pp_plan_ab.py): the plan without the 192-wide tiles
-static bool g_plan_pp = true;
-NTM_API void ntm_set_plan_pp_tiles(int on) { g_plan_pp = on != 0; }
+// host-only A/B knob (tools/pp_plan_ab.py): bit 0 = the 192-wide tiles on all
+// of C, bit 1 = stream-K split mode on them (3 = the shipping plan)
+static bool g_plan_pp = true, g_plan_pp_split = true;
+NTM_API void ntm_set_plan_pp_tiles(int on) {
+  g_plan_pp = (on & 1) != 0;
+  g_plan_pp_split = (on & 2) != 0;
+}
 // The counted vmcnt phase P (0..3) of the 192-wide ping-pong build <ah, bh>
 // waits for (Geo::vmc, gemm_bf16_pp3h.hpp; 128 / 128 is pingpong8c's 10): host
 // only, for the CPU model of the DMA schedule (tests/test_pp3h_schedule_model.py).
@@ -209,6 +214,11 @@ constexpr int kMaxSplits = 16;
 // scaled by SmallTile::ragged (profiles/r4_sks: 6 of 15 sweep shapes, +9 to
 // +39 % over the small tile).
 constexpr int kStreamKVariant = 49;
+// split mode on the 192-wide ping-pong tiles (gemm_bf16_skh.hpp): a tile of
+// them costs kPpTileTime of a 256x256 tile over the same K (0.75 of the work at
+// the 0.82 efficiency the plan prices them at); its partials are 0.75 the size
+constexpr int kStreamKPp192x256 = 54, kStreamKPp256x192 = 55;
+constexpr double kPpTileTime = 0.75 / 0.82;
 // the last split-K plan's predicted unsplit / stream-K seconds (ntm_k1_plan_times)
 static thread_local double g_plan_debug_unsplit_s = 0.0, g_plan_debug_sk_s = 0.0;
 constexpr double kSkLoopFactor = 1.05;
@@ -331,20 +341,44 @@ inline K1Plan plan_k1_search(int M, int N, int K, bool splitk, bool fp8) {
   const double unsplit = best_cost * unit_s;
   double best_t = unsplit / kSplitKMargin;
   K1Plan split = best;
-  // Stream-K: a partial last round of 256x256 tiles spread over every CU
+  // Stream-K: a partial last round of 256x256 tiles spread over every CU, or
+  // split mode (at most half a round of tiles) on the 256x256 or the 192-wide
+  // tiles; the fastest predicted candidate is priced against the unsplit plan
   ntm::gemmsk::SkArgs sk;
   g_plan_debug_unsplit_s = unsplit;
   g_plan_debug_sk_s = 0.0;
-  if (!fp8 && ntm::gemmsk::shape_ok_sk(M, N, K) && ntm::gemmsk::sk_decompose(M, N, K, (int)kCUs, sk)) {
-    const double tile_s = 4.0 * unit_s * (2.0 * sk.Tp * ntm::gemm::BK / K);  // one 256x256 tile, K in pairs
-    double t_sk;
-    if (sk.S >= 2) {  // split mode: one slice of ceil(Tp / S) pairs per CU, one round
-      const double pairs = (double)((sk.Tp + sk.S - 1) / sk.S);
-      const double fixup = kSkSplitFixed + kSkSplitPerPartial * sk.ntiles * sk.S + kSkSplitPerSlice * sk.S;
-      t_sk = pairs / sk.Tp * tile_s + (fixup > kSkSplitMinFixup ? fixup : kSkSplitMinFixup);
-    } else {
-      t_sk = kSkLoopFactor * ((double)sk.ntiles / kCUs) * tile_s + kSkFixed;
+  double t_sk = 0.0;
+  int sk_variant = 0;
+  auto split_mode_s = [&](const ntm::gemmsk::SkArgs& a, double tile_s, double partial_scale) {
+    // one slice of ceil(Tp / S) pairs per CU, one round, plus the fix-up
+    const double pairs = (double)((a.Tp + a.S - 1) / a.S);
+    const double fixup = kSkSplitFixed + kSkSplitPerPartial * partial_scale * a.ntiles * a.S +
+                         kSkSplitPerSlice * a.S;
+    return pairs / a.Tp * tile_s + (fixup > kSkSplitMinFixup ? fixup : kSkSplitMinFixup);
+  };
+  if (!fp8 && ntm::gemmsk::shape_ok_sk(M, N, K)) {
+    if (ntm::gemmsk::sk_decompose(M, N, K, (int)kCUs, sk)) {
+      const double tile_s = 4.0 * unit_s * (2.0 * sk.Tp * ntm::gemm::BK / K);  // one 256x256 tile, K in pairs
+      t_sk = sk.S >= 2 ? split_mode_s(sk, tile_s, 1.0)
+                       : kSkLoopFactor * ((double)sk.ntiles / kCUs) * tile_s + kSkFixed;
+      sk_variant = kStreamKVariant;
     }
+    if (g_plan_pp_split && K >= kPpMinK) {
+      for (int gi = 0; gi < 2; ++gi) {
+        ntm::gemmsk::SkArgs sh;
+        const bool ok = gi == 0 ? ntm::gemmskh::sk_decompose_h<192, 256>(M, N, K, (int)kCUs, sh)
+                                : ntm::gemmskh::sk_decompose_h<256, 192>(M, N, K, (int)kCUs, sh);
+        if (!ok) continue;
+        const double tile_s = kPpTileTime * 4.0 * unit_s * (2.0 * sh.Tp * ntm::gemm::BK / K);
+        const double t = split_mode_s(sh, tile_s, 0.75);
+        if (sk_variant == 0 || t < t_sk) {
+          t_sk = t;
+          sk_variant = gi == 0 ? kStreamKPp192x256 : kStreamKPp256x192;
+        }
+      }
+    }
+  }
+  if (sk_variant != 0) {
     g_plan_debug_sk_s = t_sk;
     // a single launch of one small tile in one round on ragged C runs slower
     // than the model (SmallTile::ragged): price stream-K against the measured-ish time
@@ -363,7 +397,7 @@ inline K1Plan plan_k1_search(int M, int N, int K, bool splitk, bool fp8) {
                                          : st.ragged;
     g_plan_debug_unsplit_s = unsplit_vs_sk;
     if (t_sk * kSkMargin < unsplit_vs_sk) {
-      split = K1Plan{M, kStreamKVariant, kStreamKVariant, 1};
+      split = K1Plan{M, sk_variant, sk_variant, 1};
       split.sk = true;
       best_t = t_sk * kSkMargin / kSplitKMargin;  // a split-K plan must beat stream-K too
     }
@@ -395,7 +429,8 @@ inline K1Plan plan_k1_search(int M, int N, int K, bool splitk, bool fp8) {
 // in a small direct-mapped table keyed by everything the search reads.
 struct PlanKey {
   int M, N, K, cus;
-  bool splitk, fp8, pp;
+  bool splitk, fp8;
+  int pp;
   bool operator==(const PlanKey& o) const {
     return M == o.M && N == o.N && K == o.K && cus == o.cus && splitk == o.splitk &&
            fp8 == o.fp8 && pp == o.pp;
@@ -411,10 +446,11 @@ constexpr int kPlanCacheSlots = 256;
 
 inline K1Plan plan_k1(int M, int N, int K, bool splitk = false, bool fp8 = false) {
   static thread_local PlanEntry cache[kPlanCacheSlots] = {};
-  const PlanKey key{M, N, K, ntm::gemm6::device_cus(), splitk, fp8, g_plan_pp};
+  const PlanKey key{M, N, K, ntm::gemm6::device_cus(), splitk, fp8,
+                    (g_plan_pp ? 1 : 0) | (g_plan_pp_split ? 2 : 0)};
   const unsigned h = ((unsigned)M * 2654435761u) ^ ((unsigned)N * 40503u) ^ ((unsigned)K * 97u) ^
                      ((unsigned)key.cus << 3) ^ (splitk ? 0x55u : 0u) ^ (fp8 ? 0xAAu : 0u) ^
-                     (g_plan_pp ? 0x100u : 0u);
+                     ((unsigned)key.pp << 8);
   PlanEntry& e = cache[(h ^ (h >> 8) ^ (h >> 16)) % kPlanCacheSlots];
   if (e.valid && e.key == key) {
     g_plan_debug_unsplit_s = e.unsplit_s;
@@ -590,6 +626,40 @@ NTM_API int ntm_gemm_bf16_sk(const void* A, const void* B, void* C, int M, int N
                                                S(stream));
 }
 
+// Split mode on the 192-wide tiles (variant 54: 192x256, 55: 256x192;
+// gemm_bf16_skh.hpp) with a stream-K workspace of ntm_skh_ws_bytes bytes (0:
+// split mode on that tile does not serve (M, N, K) on this device).
+NTM_API size_t ntm_skh_ws_bytes(int variant, int M, int N, int K) {
+  ntm::gemmsk::SkArgs s;
+  const int cus = ntm::gemm6::pp6_grid(1 << 30);
+  if (!ntm::gemmsk::shape_ok_sk(M, N, K)) return 0;
+  const bool ok = variant == kStreamKPp192x256   ? ntm::gemmskh::sk_decompose_h<192, 256>(M, N, K, cus, s)
+                  : variant == kStreamKPp256x192 ? ntm::gemmskh::sk_decompose_h<256, 192>(M, N, K, cus, s)
+                                                 : false;
+  return ok ? ntm::gemmsk::sk_ws_bytes(s.G) : 0;
+}
+
+NTM_API int ntm_gemm_bf16_skh(int variant, const void* A, const void* B, void* C, int M, int N,
+                              int K, int lda, int ldb, int ldc, void* ws, size_t ws_bytes,
+                              void* stream) {
+  ntm::gemm::GemmArgs a;
+  a.A = (const __bf16*)A;
+  a.B = (const __bf16*)B;
+  a.C = (__bf16*)C;
+  a.M = M;
+  a.N = N;
+  a.K = K;
+  a.lda = lda;
+  a.ldb = ldb;
+  a.ldc = ldc;
+  const int cus = ntm::gemm6::pp6_grid(1 << 30);
+  if (variant == kStreamKPp192x256)
+    return (int)ntm::gemmskh::launch_gemm_bf16_skh<64, 128>(a, cus, ws, ws_bytes, S(stream));
+  if (variant == kStreamKPp256x192)
+    return (int)ntm::gemmskh::launch_gemm_bf16_skh<128, 64>(a, cus, ws, ws_bytes, S(stream));
+  return (int)hipErrorInvalidValue;
+}
+
 // The default dispatch with split-K allowed: ws (ws_bytes) is the caller's
 // workspace; when the split-K plan needs more than ws_bytes (or ws is null) the
 // unsplit plan runs instead.
@@ -603,9 +673,16 @@ NTM_API int ntm_gemm_bf16_ex(const void* A, const void* B, void* C, int M, int N
     // stream-K: this entry takes any caller workspace, so it zeroes the counter
     // block first (a caller that keeps a zeroed workspace per stream calls
     // ntm_gemm_bf16_sk directly and saves that dispatch)
-    if (pl.feasible() && pl.sk && ws_bytes >= ntm_sk_ws_bytes(M, N, K) &&
+    if (pl.feasible() && pl.sk && pl.top_variant == kStreamKVariant &&
+        ws_bytes >= ntm_sk_ws_bytes(M, N, K) &&
         hipMemsetAsync(ws, 0, ntm::gemmsk::kCounterBytes, S(stream)) == hipSuccess &&
         ntm_gemm_bf16_sk(A, B, C, M, N, K, lda, ldb, ldc, ws, ws_bytes, stream) == 0)
+      return 0;
+    if (pl.feasible() && pl.sk && pl.top_variant != kStreamKVariant &&
+        ws_bytes >= ntm_skh_ws_bytes(pl.top_variant, M, N, K) &&
+        ntm_skh_ws_bytes(pl.top_variant, M, N, K) > 0 &&
+        hipMemsetAsync(ws, 0, ntm::gemmsk::kCounterBytes, S(stream)) == hipSuccess &&
+        ntm_gemm_bf16_skh(pl.top_variant, A, B, C, M, N, K, lda, ldb, ldc, ws, ws_bytes, stream) == 0)
       return 0;
   }
   return ntm_gemm_bf16_variant(0, A, B, C, M, N, K, lda, ldb, ldc, stream);
