@@ -83,12 +83,35 @@ def sample_at(domain: int, bus: int, dev: int, fn: int = 0) -> dict:
     return out
 
 
-def sample(device) -> dict:
-    """One sample of a PyTorch GPU device (never raises)."""
-    try:
-        return sample_at(*pci_address(device))
-    except Exception as e:  # noqa: BLE001 - telemetry is context only
-        return {"error": f"{type(e).__name__}: {e}"[:200]}
+_stuck = False   # a sample that never returned: AMD SMI is not called again in this process
+
+
+def sample(device, timeout_s: float = 10.0) -> dict:
+    """One sample of a PyTorch GPU device (never raises, never blocks for more
+    than ``timeout_s``). The library call runs on a daemon thread: AMD SMI takes
+    a cross-process lock at init, and a bench rank must not hang on telemetry if
+    another process died holding it. After a timeout the process stops calling
+    AMD SMI (the stuck thread is abandoned at exit)."""
+    global _stuck
+    if _stuck:
+        return {"error": "AMD SMI did not return earlier in this process"}
+    import threading
+
+    box: dict = {}
+
+    def run():
+        try:
+            box["s"] = sample_at(*pci_address(device))
+        except Exception as e:  # noqa: BLE001 - telemetry is context only
+            box["s"] = {"error": f"{type(e).__name__}: {e}"[:200]}
+
+    t = threading.Thread(target=run, name="ntm-smi-sample", daemon=True)
+    t.start()
+    t.join(timeout_s)
+    if t.is_alive():
+        _stuck = True
+        return {"error": f"AMD SMI sample did not return within {timeout_s} s"}
+    return box["s"]
 
 
 def _pct(num_a, num_b, den_a, den_b):

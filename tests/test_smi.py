@@ -99,3 +99,29 @@ def test_clock_summary_groups_by_real_xcc_and_finds_the_bounding_xcd():
     st[:, :, 4] = (torch.arange(grid) // 8) % 8
     r = clock_summary(st, 0.68)
     assert r["blockidx_mod_8_is_xcc"] is False
+
+
+def test_sample_gives_up_on_a_stuck_library(monkeypatch):
+    """A sample that never returns (a cross-process AMD SMI lock held by a dead
+    process) costs the caller at most the timeout, and later samples return at
+    once without calling the library again."""
+    import threading
+    import time
+
+    release = threading.Event()
+    calls = []
+
+    def stuck(*a):
+        calls.append(a)
+        release.wait(30)
+        return {}
+
+    monkeypatch.setattr(smi, "sample_at", stuck)
+    monkeypatch.setattr(smi, "pci_address", lambda d: (0, 0, 0, 0))
+    monkeypatch.setattr(smi, "_stuck", False)
+    t0 = time.monotonic()
+    s = smi.sample("dev", timeout_s=0.2)
+    assert "did not return" in s["error"] and time.monotonic() - t0 < 5
+    s = smi.sample("dev", timeout_s=0.2)
+    assert "earlier" in s["error"] and len(calls) == 1
+    release.set()
