@@ -368,7 +368,9 @@ inline K1Plan plan_k1_search(int M, int N, int K, bool splitk, bool fp8) {
         ntm::gemmsk::SkArgs sh;
         const bool ok = gi == 0 ? ntm::gemmskh::sk_decompose_h<192, 256>(M, N, K, (int)kCUs, sh)
                                 : ntm::gemmskh::sk_decompose_h<256, 192>(M, N, K, (int)kCUs, sh);
-        if (!ok) continue;
+        // S = 2 (the head / tail protocol) only: at S >= 3 it replaced a small tile
+        // on 4 random shapes and lost on 3 (0.88-0.98, profiles/r5_skh/pp_ab_random200.log)
+        if (!ok || sh.S != 2) continue;
         const double tile_s = kPpTileTime * 4.0 * unit_s * (2.0 * sh.Tp * ntm::gemm::BK / K);
         const double t = split_mode_s(sh, tile_s, 0.75);
         if (sk_variant == 0 || t < t_sk) {
