@@ -31,6 +31,8 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--depths", default="0", help="in-flight depths: 0..3 = vmcnt 10 / 16 / 24 / 32")
+    ap.add_argument("--policies", default="", help="cache policies 1..5 = sc0 / nt / sc0 nt / sc1 / "
+                    "sc1 nt (at depth 0)")
     args = ap.parse_args()
     L = lib_experimental()
     T = args.k // 64 - 2
@@ -40,6 +42,9 @@ def main():
         cases.update({"aligned/0" + sfx: (10 * d, args.k), "misaligned/0" + sfx: (10 * d, args.k + 8),
                       "misaligned/1" + sfx: (10 * d + 1, args.k + 8),
                       "misaligned/2" + sfx: (10 * d + 2, args.k + 8)})
+    for a in (int(x) for x in args.policies.split(",") if x):
+        sfx = "@" + ("sc0", "nt", "sc0nt", "sc1", "sc1nt")[a - 1]
+        cases.update({"aligned/0" + sfx: (100 * a, args.k), "misaligned/0" + sfx: (100 * a, args.k + 8)})
     bufs = {p: torch.zeros(513 * p, dtype=torch.bfloat16, device="cuda") for p in {args.k, args.k + 8}}
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 

@@ -32,9 +32,15 @@ __device__ __forceinline__ void wait_vm_deep() {
   if constexpr (N == 32) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
 }
 
+template <int AUX>
+__device__ __forceinline__ void glds16_pol(const void* gsrc, char* lds_dst) {
+  __builtin_amdgcn_global_load_lds((const void NTM_AS1*)gsrc, (void NTM_AS3*)lds_dst, 16, 0, AUX);
+}
+
 // VM: the counted wait after each half (10 = the kernel's: 5 halves in flight;
-// deeper values only exist here, where nothing reads the LDS)
-template <int MODE, int VM = 10>
+// deeper values only exist here, where nothing reads the LDS). AUX: the load's
+// cache-policy bits (gfx950: 1 sc0, 2 nt, 16 sc1).
+template <int MODE, int VM = 10, int AUX = 0>
 __global__ void __launch_bounds__(512) dma_probe_kernel(const __bf16* base, int pitch, int T,
                                                         int reps) {
   __shared__ __attribute__((aligned(16))) char smem[2 * kTileBytes];
@@ -62,8 +68,8 @@ __global__ void __launch_bounds__(512) dma_probe_kernel(const __bf16* base, int 
           s2 = s1 + 64;
         }
         char* d = smem + (t & 1) * kTileBytes + h * kHalfBytes + (2 * w) * 1024;
-        glds16((const __bf16*)s1, d);
-        glds16((const __bf16*)s2, d + 1024);
+        glds16_pol<AUX>(s1, d);
+        glds16_pol<AUX>(s2, d + 1024);
         wait_vm_deep<VM>();
       }
     }
@@ -76,7 +82,23 @@ __global__ void __launch_bounds__(512) dma_probe_kernel(const __bf16* base, int 
 inline hipError_t launch_dma_probe(int mode, const __bf16* base, int pitch, int T, int reps,
                                    int grid, hipStream_t s) {
   if (T < 1 || reps < 1 || grid < 1 || pitch < (T + 1) * 64 + 64) return hipErrorInvalidValue;
-  // mode + 10 * d: d = 0..3 -> counted wait 10 / 16 / 24 / 32 (5 / 8 / 12 / 16 halves in flight)
+  // mode + 10 * d + 100 * a: d = 0..3 -> counted wait 10 / 16 / 24 / 32 (5 / 8 / 12 / 16
+  // halves in flight); a = 1..5 -> cache policy sc0 / nt / sc0 nt / sc1 / sc1 nt (depth 10)
+  if (mode >= 100) {
+    const int a = mode / 100, m = mode % 100;
+    if (m > 2) return hipErrorInvalidValue;
+#define NTM_DPROBE_POL(A, AUXV)                                                                    \
+  if (a == A) {                                                                                    \
+    if (m == 0) hipLaunchKernelGGL((dma_probe_kernel<0, 10, AUXV>), dim3(grid), dim3(512), 0, s, base, pitch, T, reps); \
+    if (m == 1) hipLaunchKernelGGL((dma_probe_kernel<1, 10, AUXV>), dim3(grid), dim3(512), 0, s, base, pitch, T, reps); \
+    if (m == 2) hipLaunchKernelGGL((dma_probe_kernel<2, 10, AUXV>), dim3(grid), dim3(512), 0, s, base, pitch, T, reps); \
+  }
+    NTM_DPROBE_POL(1, 1) NTM_DPROBE_POL(2, 2) NTM_DPROBE_POL(3, 3) NTM_DPROBE_POL(4, 16)
+    NTM_DPROBE_POL(5, 18)
+#undef NTM_DPROBE_POL
+    if (a > 5) return hipErrorInvalidValue;
+    return hipGetLastError();
+  }
   const int d = mode / 10;
   mode %= 10;
   if (mode > 2 || d > 3) return hipErrorInvalidValue;
