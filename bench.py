@@ -123,6 +123,21 @@ def prewarm_settle(fn, sync, min_s: float, chunk: int = 16) -> dict:
             return {"seconds": round(el, 3), "launches": launches}
 
 
+def power_window(fn, sync, sample, min_s: float, chunk: int = 16):
+    """Two telemetry samples around at least ``min_s`` s of back-to-back ``fn``
+    launches; each is read while ``chunk`` launches are queued, so neither end
+    sees an idle GPU. Returns (before, after, run) for ``smi.window``."""
+    for _ in range(chunk):
+        fn()
+    before = sample()
+    run = prewarm_settle(fn, sync, min_s, chunk)
+    for _ in range(chunk):
+        fn()
+    after = sample()
+    sync()
+    return before, after, run
+
+
 def interleaved_compare(fns: dict, dev, rounds: int, launches: int) -> dict:
     """ABBA timing: in each round every callable runs ``launches`` times under
     its own events, in the given order on even rounds and reversed on odd ones
@@ -301,8 +316,15 @@ def main(argv=None) -> int:
     # launches queued behind it with no sync, so they run in the steady state the
     # timed loop ran in - not in the boost / overshoot transient an idle gap (the
     # all-reduce above) starts (BENCH_r04: 663 -> 897 -> 711 us per stamped launch).
+    power_steady = None
     if dev.type == "cuda":
         prewarm_settle(wl.step, sync, 0.3)
+        # The firmware metrics behind AMD SMI refresh every few tens of ms, so a
+        # short timed loop (20 x 0.67 ms) gets the same counters at both ends. This
+        # window covers >= 0.5 s of the same K1 launches in the steady state the
+        # timed loop left, and stands in for it where the timed window is stale.
+        b, a, run = power_window(wl.step, sync, lambda: smi.sample(dev), 0.5)
+        power_steady = {**smi.window(b, a), "launches": run["launches"]}
         for _ in range(8):
             wl.step()
     gclk = _probe("gemm_clock_ghz", wl.a, wl.b, wl.c, steps=min(max(args.steps, 1), 20))
@@ -330,9 +352,21 @@ def main(argv=None) -> int:
             gclk["bound_window_fraction"] = round(
                 cyc[len(cyc) // 2] / (gclk["bound_GHz"] * 1e9) / (my_seconds / args.steps), 4)
     power = smi.window(smi_before, smi_after) if smi_before is not None else None
+    # the power / throttle figures reported per rank: the timed loop's own window
+    # when it spans >= 0.1 s and its counters advanced, else the steady-state window
+    # beside it (a shorter window holds one or no metrics refresh: quantised or stale)
+    power_src = None
+    if power is not None:
+        power_src = ("timed_loop" if power.get("avg_power_W") is not None
+                     and (power.get("seconds") or 0) >= 0.1 else "steady_window")
     per_rank = dist.all_gather_obj(env, {"tflops": round(wl.flops * args.steps / my_seconds / 1e12, 2),
                                          "clock": clk, "gemm_clock": gclk,
-                                         "timed_loop_clock": timed_clk, "power": power})
+                                         "timed_loop_clock": timed_clk, "power": power,
+                                         "power_steady": power_steady, "power_src": power_src})
+
+    def _pw(p: dict, key: str):
+        src = p["power"] if p["power_src"] == "timed_loop" else p["power_steady"]
+        return (src or {}).get(key)
 
     # ---- after the timed region: verification + context measurements
     extras: dict = {}
@@ -551,13 +585,18 @@ def main(argv=None) -> int:
         "per_rank_gemm_clock": [p["gemm_clock"] for p in per_rank],
         # median shader cycles per stamped launch / the rank's own timed ms per step
         "per_rank_timed_loop_clock_GHz": [p["timed_loop_clock"] for p in per_rank],
-        # AMD SMI over [last warmup launches .. end of the timed loop], per rank:
-        # average power (energy counter), PPT (power) and socket-thermal throttle
-        # residency in % of firmware iterations, power / temperature / clock at both ends
-        "per_rank_avg_power_W": [(p["power"] or {}).get("avg_power_W") for p in per_rank],
-        "per_rank_ppt_throttle_pct": [(p["power"] or {}).get("ppt_pct") for p in per_rank],
-        "per_rank_thermal_throttle_pct": [(p["power"] or {}).get("thermal_pct") for p in per_rank],
+        # AMD SMI per rank: average power (energy counter), PPT (power) and
+        # socket-thermal throttle residency in % of firmware iterations, from the
+        # window named in per_rank_power_window: "timed_loop" = [last warmup launches
+        # .. end of the timed loop]; "steady_window" = >= 0.5 s of the same K1 right
+        # after it (the timed window was under 0.1 s or stale). Both
+        # raw windows (power / temperature / clock at both ends) are kept.
+        "per_rank_avg_power_W": [_pw(p, "avg_power_W") for p in per_rank],
+        "per_rank_ppt_throttle_pct": [_pw(p, "ppt_pct") for p in per_rank],
+        "per_rank_thermal_throttle_pct": [_pw(p, "thermal_pct") for p in per_rank],
+        "per_rank_power_window": [p["power_src"] for p in per_rank],
         "per_rank_power": [p["power"] for p in per_rank],
+        "per_rank_power_steady": [p["power_steady"] for p in per_rank],
         "per_rank_clock_GHz": [(p["clock"] or {}).get("median_GHz") for p in per_rank],
         "per_rank_clock_probe": [p["clock"] for p in per_rank],
         "vs_baseline_note": "reference publishes no TFLOP/s or busbw (BASELINE.json published={})",

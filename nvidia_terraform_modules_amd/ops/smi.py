@@ -131,8 +131,12 @@ def window(before: dict, after: dict) -> dict:
     dt = ((after.get("host_ns") or 0) - (before.get("host_ns") or 0)) / 1e9
     res["seconds"] = round(dt, 4) if dt > 0 else None
     ea, eb = before.get("energy_uj"), after.get("energy_uj")
+    # the firmware metrics table refreshes every few tens of ms: a window shorter
+    # than that reads the same energy / accumulation counters at both ends, which
+    # is "no data", not 0 W (BENCH at 20 x 0.67 ms read 0.0 W at 1388 W socket power)
+    res["stale"] = ea is not None and ea == eb
     res["avg_power_W"] = (round((eb - ea) / 1e6 / dt, 1)
-                          if None not in (ea, eb) and eb >= ea and dt > 0 else None)
+                          if None not in (ea, eb) and eb > ea and dt > 0 else None)
     acc = (before.get("accumulation_counter"), after.get("accumulation_counter"))
     for key, field in (("ppt_pct", "ppt_residency_acc"), ("thermal_pct", "socket_thm_residency_acc"),
                        ("prochot_pct", "prochot_residency_acc"),

@@ -78,6 +78,8 @@ def test_torchrun_launch_one_json_line(nproc):
     # window are reported per rank (None without a GPU)
     assert d["per_rank_timed_loop_clock_GHz"] == [None] * nproc
     assert d["per_rank_power"] == [None] * nproc
+    assert d["per_rank_power_steady"] == [None] * nproc
+    assert d["per_rank_power_window"] == [None] * nproc
     assert d["per_rank_avg_power_W"] == [None] * nproc
     assert d["per_rank_ppt_throttle_pct"] == [None] * nproc
     assert d["per_rank_thermal_throttle_pct"] == [None] * nproc
@@ -153,8 +155,18 @@ def test_bench_on_one_gpu_json_contract(tmp_path):
     assert d["per_rank_timed_loop_clock_GHz"] == [None]
     pw = d["per_rank_power"][0]
     assert "error" not in pw, pw
-    # (a 5-step 2048^3 window is shorter than the energy counter's update period)
-    assert pw["avg_power_W"] is None or pw["avg_power_W"] >= 0, pw
+    # (a 5-step 2048^3 window is shorter than the metrics refresh: stale, no 0 W)
+    assert pw["avg_power_W"] is None or pw["avg_power_W"] > 0, pw
+    assert pw["stale"] is (pw["avg_power_W"] is None), pw
+    # the >= 0.5 s steady-state window beside it always has data, and the reported
+    # power comes from whichever window advanced
+    st = d["per_rank_power_steady"][0]
+    assert "error" not in st and st["seconds"] >= 0.5 and st["stale"] is False, st
+    assert 50 < st["avg_power_W"] < 2000 and 0 <= st["ppt_pct"] <= 100, st
+    src = d["per_rank_power_window"][0]
+    assert src == ("timed_loop" if pw["avg_power_W"] is not None and pw["seconds"] >= 0.1
+                   else "steady_window")
+    assert d["per_rank_avg_power_W"][0] == (pw if src == "timed_loop" else st)["avg_power_W"]
     job = d["validation_job"]
     assert job["ran"] and job["passed"], job
     assert 0 < d["time_to_gpu_ready_in_node_s"] < 30

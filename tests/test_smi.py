@@ -42,6 +42,19 @@ def test_window_unsupported_fields_are_none():
     assert w["ppt_pct"] is None
 
 
+def test_window_shorter_than_the_metrics_refresh_is_stale_not_zero():
+    """BENCH r5: a 20-step timed loop (13 ms) read the same energy counter at both
+    ends; that is no data, not 0 W."""
+    a = _s(energy_uj=5_000_000, accumulation_counter=700, ppt_residency_acc=600)
+    b = _s(host_ns=16_000_000, energy_uj=5_000_000, accumulation_counter=700,
+           ppt_residency_acc=600)
+    w = smi.window(a, b)
+    assert w["stale"] is True and w["avg_power_W"] is None and w["ppt_pct"] is None
+    w = smi.window(a, _s(host_ns=10**9, energy_uj=6_400_000_000, accumulation_counter=1700,
+                         ppt_residency_acc=1600))
+    assert w["stale"] is False and w["avg_power_W"] == 6395.0 and w["ppt_pct"] == 100.0
+
+
 def test_window_carries_sampling_errors():
     w = smi.window({"error": "AMD SMI did not initialise", "host_ns": 1}, _s(host_ns=2))
     assert w["error"] == "AMD SMI did not initialise"
