@@ -42,7 +42,8 @@ def main():
     ap.add_argument("--only-default", action="store_true",
                     help="time the default dispatch and hipBLASLt only (shape sweeps)")
     ap.add_argument("--random", type=int, default=0,
-                    help="append N random shapes (M, N % 8, K % 8 in [256, 8192], seeded)")
+                    help="append N random shapes (M, N, K multiples of 8 in [256, 8192], seeded)")
+    ap.add_argument("--seed", type=int, default=20261016, help="seed of the --random draws")
     ap.add_argument("--dtype", default="bf16", choices=("bf16", "fp8"))
     ap.add_argument("--variants", default="",
                     help="time exactly these variants (masked tiles on any shape) besides "
@@ -51,7 +52,7 @@ def main():
     shapes = [tuple(int(x) for x in sh.split("x")) for sh in args.shapes.split(",") if sh]
     if args.random:
         import random
-        rng = random.Random(20261016)
+        rng = random.Random(args.seed)
         shapes += [tuple(rng.randrange(256, 8193, 8) for _ in range(3)) for _ in range(args.random)]
         if args.dtype == "fp8":   # same draws; N, K rounded up to 16 (torch._scaled_mm's rule)
             shapes = [(m, (n + 15) // 16 * 16, (k + 15) // 16 * 16) for m, n, k in shapes]

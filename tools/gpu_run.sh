@@ -21,6 +21,10 @@
 #   clock      the GEMM's in-kernel clock (stamped pingpong8o) vs GRBM_GUI_ACTIVE of the
 #              same dispatches (one rocprofv3 --pmc pass)
 #   fp8        K1-fp8 vs hipBLASLt fp8: square sizes (gemm_fp8_check) + the 41-shape sweep
+#   standing   where the shipping default plans stand vs hipBLASLt on this box: named bf16
+#              shapes (gemm_check), fp8 (gemm_fp8_check), a seeded ragged one-round set
+#              (ragged_sweep) and 48 seeded random shapes (gemm_policy); STAND_SEED picks
+#              the fresh sets. Run on >= 3 boxes; tools/k1_boxes.py takes the median.
 #   py:<file>  python -u <file> (a tool script; its own args via PYARGS)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
@@ -98,6 +102,20 @@ for s in "${STEPS[@]}"; do
         --random 40 --rounds 5 --iters 20 > "$O/fp8_policy_random.log" 2>&1 \
         || fail "fp8 policy" $? "$O/fp8_policy_random.log"
       python3 -c "import json,statistics,sys; r=[json.loads(l)['default_over_hipblaslt'] for l in open(sys.argv[1]) if l.startswith('{')]; print(f'fp8 default ahead of hipBLASLt on {sum(x > 1 for x in r)} of {len(r)}, median {statistics.median(r):.3f}')" "$O/fp8_policy_random.log" ;;
+    standing)
+      sd=${STAND_SEED:-23}
+      timeout -k 10 600 python -u tools/gemm_check.py --variants default --rounds 7 --iters 30 \
+        --sizes 8192,5120,4096,8192x8192x4096,8192x8192x6144,4472x5688x5832,4152x1096x16056,2840x1768x8904 \
+        > "$O/standing_bf16.log" 2>&1 || fail "standing bf16" $? "$O/standing_bf16.log"
+      timeout -k 10 600 python -u tools/gemm_fp8_check.py --sizes 4096,8192,8192x8192x4096,6144 --no-bf16 \
+        --rounds 7 --iters 30 > "$O/standing_fp8.log" 2>&1 || fail "standing fp8" $? "$O/standing_fp8.log"
+      timeout -k 10 600 python -u tools/ragged_sweep.py --n 24 --seed "$sd" --rounds 5 --iters 10 \
+        > "$O/standing_ragged_seed$sd.log" 2>&1 || fail "standing ragged" $? "$O/standing_ragged_seed$sd.log"
+      timeout -k 10 900 python -u tools/gemm_policy.py --only-default --shapes "" --random 48 --seed "$sd" \
+        --rounds 5 --iters 20 > "$O/standing_random48_seed$sd.log" 2>&1 \
+        || fail "standing random" $? "$O/standing_random48_seed$sd.log"
+      tail -1 "$O/standing_ragged_seed$sd.log"
+      python3 -c "import json,statistics,sys; r=[json.loads(l)['default_over_hipblaslt'] for l in open(sys.argv[1]) if l.startswith('{')]; print(f'random48 seed $sd: ahead on {sum(x > 1 for x in r)} of {len(r)}, below 0.97 {sum(x < 0.97 for x in r)}, min {min(r):.3f}, median {statistics.median(r):.3f}')" "$O/standing_random48_seed$sd.log" ;;
     py:*)
       f=${s#py:}
       timeout -k 10 600 python -u "$f" $PYARGS > "$O/$(basename "$f" .py).log" 2>&1 \

@@ -48,4 +48,7 @@ def main(argv: list[str]) -> int:
 
 
 if __name__ == "__main__":
+    if any(a in ("-h", "--help") for a in sys.argv[1:]):
+        print(__doc__)
+        sys.exit(0)
     sys.exit(main(sys.argv[1:]))

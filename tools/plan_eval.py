@@ -53,4 +53,7 @@ def main(paths):
 
 
 if __name__ == "__main__":
+    if any(a in ("-h", "--help") for a in sys.argv[1:]):
+        print(__doc__)
+        sys.exit(0)
     main(sys.argv[1:] or LOGS)

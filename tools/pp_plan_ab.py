@@ -26,7 +26,7 @@ def main():
     ap.add_argument("--shapes", default="")
     ap.add_argument("--n", type=int, default=24)
     ap.add_argument("--seed", type=int, default=11)
-    ap.add_argument("--random", action="store_true", help="uniform M, N, K in [256, 8192] % 8")
+    ap.add_argument("--random", action="store_true", help="uniform M, N, K in [256, 8192], multiples of 8")
     ap.add_argument("--changed-only", action="store_true", help="skip shapes whose plan is the same")
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=20)
