@@ -192,3 +192,30 @@ def test_pair_busbw_pairs_xgmi_with_rccl_sizes():
     assert all(r["xgmi_over_rccl"] > 1.0 for r in rows)
     assert bench.pair_busbw([R(bytes=512, busbw_GBps=0.0)], [R(bytes=512, busbw_GBps=1.0)])[0][
         "xgmi_over_rccl"] is None
+
+
+def test_power_window_samples_under_load():
+    """bench.power_window: both telemetry samples are read while launches are
+    queued (never on an idle GPU), and the window covers at least min_s."""
+    sys.path.insert(0, str(ROOT))
+    import bench
+
+    queued, events = [0], []
+
+    def fn():
+        queued[0] += 1
+
+    def sync():
+        queued[0] = 0
+        events.append("sync")
+
+    def sample():
+        events.append(("sample", queued[0]))
+        return {"host_ns": len(events)}
+
+    before, after, run = bench.power_window(fn, sync, sample, 0.05, chunk=4)
+    samples = [e for e in events if e != "sync"]
+    assert samples == [("sample", 4), ("sample", 4)]
+    assert events[-1] == "sync" and events.index(samples[0]) == 0
+    assert run["seconds"] >= 0.05 and run["launches"] >= 4
+    assert before["host_ns"] < after["host_ns"]
