@@ -115,7 +115,7 @@ for s in "${STEPS[@]}"; do
         --rounds 5 --iters 20 > "$O/standing_random48_seed$sd.log" 2>&1 \
         || fail "standing random" $? "$O/standing_random48_seed$sd.log"
       tail -1 "$O/standing_ragged_seed$sd.log"
-      python3 -c "import json,statistics,sys; r=[json.loads(l)['default_over_hipblaslt'] for l in open(sys.argv[1]) if l.startswith('{')]; print(f'random48 seed $sd: ahead on {sum(x > 1 for x in r)} of {len(r)}, below 0.97 {sum(x < 0.97 for x in r)}, min {min(r):.3f}, median {statistics.median(r):.3f}')" "$O/standing_random48_seed$sd.log" ;;
+      python3 -c "import json,statistics,sys; r=[(lambda d: d['default_tflops'] / d['torch_tflops'])(json.loads(l)) for l in open(sys.argv[1]) if l.startswith('{')]; print(f'random48 seed $sd: ahead on {sum(x > 1 for x in r)} of {len(r)}, below 0.97 {sum(x < 0.97 for x in r)}, min {min(r):.3f}, median {statistics.median(r):.3f}')" "$O/standing_random48_seed$sd.log" ;;
     py:*)
       f=${s#py:}
       timeout -k 10 600 python -u "$f" $PYARGS > "$O/$(basename "$f" .py).log" 2>&1 \
