@@ -48,6 +48,18 @@ for f in "$dest"/lib/*.so.*; do
   unv=${base%%.so.*}.so
   [ -e "$dest/lib/$unv" ] || ln -s "$base" "$dest/lib/$unv"
 done
+# the image only runs on MI355X: cut every copied library's HIP fat binary to
+# gfx950 (librccl.so: 13 targets, 570 MB -> a 66 MB compressed gfx950 bundle in
+# place; the gzip'd closure drops from 649 to 150 MB and RCCL's first set-up no
+# longer decompresses the other 12 targets: profiles/r5_fatbin). Set
+# NTM_KEEP_FATBIN=1 to keep the vendor bundles as they are.
+here=$(cd "$(dirname "$0")" && pwd)
+if [ "${NTM_KEEP_FATBIN:-0}" != 1 ]; then
+  for f in "$dest"/lib/*.so.*; do
+    [ -L "$f" ] && continue
+    python3 "$here/strip-fatbin.py" "$f" --bundler "$rocm_lib/llvm/bin/clang-offload-bundler"
+  done
+fi
 # sanity: nothing unresolved when only DEST/lib is on the search path
 if LD_LIBRARY_PATH="$dest/lib" ldd "$dest/bin/$(basename "$bin")" | grep -q "not found"; then
   echo "unresolved libraries:" >&2
