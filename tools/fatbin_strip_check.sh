@@ -24,7 +24,7 @@ du -sb "$C" "$S" > "$O/closure_bytes.txt"
 (cd "$C" && tar cf - . | gzip -1 | wc -c) > "$O/stock_gzip1_bytes.txt"
 (cd "$S" && tar cf - . | gzip -1 | wc -c) > "$O/gfx950_gzip1_bytes.txt"
 for i in $(seq 1 "$R"); do
-  for v in stock gfx950; do
+  for v in ${ORDER:-stock gfx950}; do
     d=$C
     [ "$v" = gfx950 ] && d=$S
     LD_LIBRARY_PATH="$d/lib" timeout -k 10 120 "$d/bin/amdgpu-validate" --gpus 1 --size 2048 --iters 3 \
