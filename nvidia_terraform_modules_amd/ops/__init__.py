@@ -39,6 +39,7 @@ from .kernels import (  # noqa: F401
     k1_splitk_plan,
     ref_gemm_f32,
     set_plan_pp_tiles,
+    set_plan_splitk,
     sk_ws_bytes,
     sk_xcc_error,
     stream_copy,

@@ -193,10 +193,33 @@ struct K1Plan {
 // the reduction kernel's reads; an effective rate, not HBM's). Its picks are
 // within 3.3 % of the fastest measured split on every fitted shape. A split plan
 // must beat the unsplit one by kSplitKMargin.
+// Round 5 (profiles/r5_margin/): the model leaves out per-launch fixed costs on
+// both sides, so on small C the unsplit plan is about as optimistic as the
+// split one, and the 1.1 margin kept C unsplit where a split with long slices
+// ran 10-25 % faster. A split whose slices keep >= kLongSliceK of K needs only
+// kSplitKMarginLong against the unsplit plan. Short slices keep 1.1 (at 1.03,
+// three slices of 464 / 621 K lost 22-28 %), and so does any split against a
+// stream-K plan (at 1.03, 256x128 / 2 replaced stream-K split mode on 14
+// shapes and lost on 10, by up to 8 %).
 constexpr double kPerCU = 1650e12 / 256.0;  // the 256x256 kernel's per-CU bf16 rate
 constexpr double kRedFixed = 2e-6;
 constexpr double kRedBW = 2e12;
 constexpr double kSplitKMargin = 1.1;
+constexpr double kSplitKMarginLong = 1.03;
+constexpr int kLongSliceK = 1024;
+// host-only A/B knob (tools/margin_ab.py): the long-slice margin and threshold
+// the plan uses (margin <= 0 / long_k < 0: the shipping values; margin 1.1 =
+// round 4's plan); both are in the plan cache key
+static double g_splitk_margin = 0.0;
+static int g_splitk_min_k = -1;
+NTM_API void ntm_set_plan_splitk(double margin, int long_k) {
+  g_splitk_margin = margin > 0.0 ? margin : 0.0;
+  g_splitk_min_k = long_k >= 0 ? long_k : -1;
+}
+inline double splitk_long_margin() {
+  return g_splitk_margin > 0.0 ? g_splitk_margin : kSplitKMarginLong;
+}
+inline int splitk_long_k() { return g_splitk_min_k >= 0 ? g_splitk_min_k : kLongSliceK; }
 constexpr int kMaxSplits = 16;
 
 // Stream-K ("pingpong8s", gemm_bf16_sk.hpp; needs the caller's workspace, so
@@ -339,7 +362,8 @@ inline K1Plan plan_k1_search(int M, int N, int K, bool splitk, bool fp8) {
   // tiles of 160x160 -> 3 slices of 240 tiles, 631 vs 321 TF/s unsplit).
   const double unit_s = 2.0 * 16384.0 * K / kPerCU;  // cost units -> seconds
   const double unsplit = best_cost * unit_s;
-  double best_t = unsplit / kSplitKMargin;
+  double best_t = inf;        // the fastest split-K candidate so far
+  double sk_bar = inf;        // a split-K plan must also beat a chosen stream-K plan
   K1Plan split = best;
   // Stream-K: a partial last round of 256x256 tiles spread over every CU, or
   // split mode (at most half a round of tiles) on the 256x256 or the 192-wide
@@ -401,7 +425,7 @@ inline K1Plan plan_k1_search(int M, int N, int K, bool splitk, bool fp8) {
     if (t_sk * kSkMargin < unsplit_vs_sk) {
       split = K1Plan{M, sk_variant, sk_variant, 1};
       split.sk = true;
-      best_t = t_sk * kSkMargin / kSplitKMargin;  // a split-K plan must beat stream-K too
+      sk_bar = t_sk * kSkMargin / kSplitKMargin;
     }
   }
   for (const SmallTile& st : kSmallTiles) {
@@ -414,7 +438,8 @@ inline K1Plan plan_k1_search(int M, int N, int K, bool splitk, bool fp8) {
       const double kc = ntm::gemmt::splitk_kc(K, sp);
       const double t = rounds(tiles * slices) * 2.0 * st.tm * st.tn * kc / (kPerCU * st.eff) +
                        kRedFixed + (double)slices * M * N * 4.0 / kRedBW;
-      if (t < best_t) {
+      const double margin = kc >= splitk_long_k() ? splitk_long_margin() : kSplitKMargin;
+      if (t < best_t && t * margin < unsplit && t < sk_bar) {
         best_t = t;
         split = K1Plan{M, st.variant, st.variant, slices};
       }
@@ -433,9 +458,11 @@ struct PlanKey {
   int M, N, K, cus;
   bool splitk, fp8;
   int pp;
+  double margin;
+  int min_k;
   bool operator==(const PlanKey& o) const {
     return M == o.M && N == o.N && K == o.K && cus == o.cus && splitk == o.splitk &&
-           fp8 == o.fp8 && pp == o.pp;
+           fp8 == o.fp8 && pp == o.pp && margin == o.margin && min_k == o.min_k;
   }
 };
 struct PlanEntry {
@@ -449,7 +476,8 @@ constexpr int kPlanCacheSlots = 256;
 inline K1Plan plan_k1(int M, int N, int K, bool splitk = false, bool fp8 = false) {
   static thread_local PlanEntry cache[kPlanCacheSlots] = {};
   const PlanKey key{M, N, K, ntm::gemm6::device_cus(), splitk, fp8,
-                    (g_plan_pp ? 1 : 0) | (g_plan_pp_split ? 2 : 0)};
+                    (g_plan_pp ? 1 : 0) | (g_plan_pp_split ? 2 : 0), g_splitk_margin,
+                    g_splitk_min_k};
   const unsigned h = ((unsigned)M * 2654435761u) ^ ((unsigned)N * 40503u) ^ ((unsigned)K * 97u) ^
                      ((unsigned)key.cus << 3) ^ (splitk ? 0x55u : 0u) ^ (fp8 ? 0xAAu : 0u) ^
                      ((unsigned)key.pp << 8);
