@@ -372,3 +372,25 @@ def test_plan_cache_returns_the_search_result(k1_plan, splitk_plan):
     finally:
         ops.set_plan_pp_tiles(True)
     assert k1_plan(3904, 2584, 12760)[1] == "pp256x192"
+
+
+def test_splitk_margin_by_slice_length(splitk_plan):
+    """Round 5 (profiles/r5_margin): a split whose slices keep >= 1024 of K needs
+    a 1.03 margin over the unsplit plan (1040x2776x5096: 160x160 / 2, 55.2 ->
+    44.0 us); short slices keep 1.1 (2264x328x1392 stays unsplit: three slices
+    of 464 K lost 28 %), and so does a split against stream-K (1136x2728x8072
+    keeps stream-K split mode). The knob brings back round 4's rule, and it is
+    part of the plan cache key."""
+    from nvidia_terraform_modules_amd import ops
+
+    assert splitk_plan(1040, 2776, 5096) == (1040, "tile160", "tile160", 2)
+    assert splitk_plan(3896, 368, 2064) == (3896, "tile128", "tile128", 2)
+    assert splitk_plan(2264, 328, 1392) == (2264, "tile128", "tile128", 1)
+    assert splitk_plan(1136, 2728, 8072)[1] == "pingpong8s"
+    ops.set_plan_splitk(1.1, 0)
+    try:
+        assert splitk_plan(1040, 2776, 5096) == (1040, "tile128", "tile128", 1)
+        assert splitk_plan(3896, 368, 2064) == (3896, "tile128", "tile128", 1)
+    finally:
+        ops.set_plan_splitk()
+    assert splitk_plan(1040, 2776, 5096) == (1040, "tile160", "tile160", 2)
