@@ -438,7 +438,8 @@ inline K1Plan plan_k1_search(int M, int N, int K, bool splitk, bool fp8) {
       const double kc = ntm::gemmt::splitk_kc(K, sp);
       const double t = rounds(tiles * slices) * 2.0 * st.tm * st.tn * kc / (kPerCU * st.eff) +
                        kRedFixed + (double)slices * M * N * 4.0 / kRedBW;
-      const double margin = kc >= splitk_long_k() ? splitk_long_margin() : kSplitKMargin;
+      // (K1-fp8's split-K keeps 1.1: the long-slice margin was measured on bf16 only)
+      const double margin = !fp8 && kc >= splitk_long_k() ? splitk_long_margin() : kSplitKMargin;
       if (t < best_t && t * margin < unsplit && t < sk_bar) {
         best_t = t;
         split = K1Plan{M, st.variant, st.variant, slices};
