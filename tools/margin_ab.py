@@ -46,6 +46,18 @@ def runner(plan, a, b, c):
     return two
 
 
+def runner_fp8(plan, a, b, c):
+    """An explicit K1-fp8 split-K plan (rows, top, rest, splits) as a callable."""
+    rows, top, rest, splits = plan
+    if splits > 1 or rows >= a.shape[0]:
+        return lambda: ops.gemm_fp8(a, b, c, variant=top, splits=splits)
+
+    def two():
+        ops.gemm_fp8(a[:rows], b, c[:rows], variant=top)
+        ops.gemm_fp8(a[rows:], b, c[rows:], variant=rest)
+    return two
+
+
 def main():
     ap = argparse.ArgumentParser(description=__doc__,
                                  formatter_class=argparse.RawDescriptionHelpFormatter)
@@ -53,6 +65,8 @@ def main():
     ap.add_argument("--min-k", type=int, default=-1, help="new rule (-1: shipping)")
     ap.add_argument("--old-margin", type=float, default=1.1)
     ap.add_argument("--old-min-k", type=int, default=0)
+    ap.add_argument("--dtype", default="bf16", choices=("bf16", "fp8"),
+                    help="fp8: K1-fp8's split-K plan with the long-slice margin enabled for it")
     ap.add_argument("--n", type=int, default=3000)
     ap.add_argument("--seed", type=int, default=5)
     ap.add_argument("--max", type=int, default=40, help="time at most this many changed shapes")
@@ -64,28 +78,42 @@ def main():
         shapes = [tuple(int(x) for x in s.split("x")) for s in args.shapes.split(",") if s]
     else:
         rng = random.Random(args.seed)
-        shapes = [tuple(rng.randrange(256, 8193, 8) for _ in range(3)) for _ in range(args.n)]
+        step = 16 if args.dtype == "fp8" else 8   # K1-fp8: N % 8, K % 16
+        shapes = [tuple(rng.randrange(256, 8193, step) for _ in range(3)) for _ in range(args.n)]
+    fp8 = args.dtype == "fp8"
+    plan = ops.k1_fp8_splitk_plan if fp8 else ops.k1_splitk_plan
     ops.set_plan_splitk(args.old_margin, args.old_min_k)
-    old = {s: tuple(ops.k1_splitk_plan(*s)) for s in shapes}
-    ops.set_plan_splitk(args.margin, args.min_k)
-    new = {s: tuple(ops.k1_splitk_plan(*s)) for s in shapes}
+    old = {s: tuple(plan(*s)) for s in shapes}
+    ops.set_plan_splitk(args.margin, args.min_k, fp8=fp8)
+    new = {s: tuple(plan(*s)) for s in shapes}
     ops.set_plan_splitk()
     changed = [s for s in shapes if old[s] != new[s]][: args.max]
     ratios, bad = [], 0
+    one = torch.ones((), device="cuda")
+    dt = torch.float8_e4m3fn if fp8 else torch.bfloat16
     for m, n, k in changed:
-        a = ops.fill_uniform_(torch.empty((m, k), dtype=torch.bfloat16, device="cuda"), 1)
-        b = ops.fill_uniform_(torch.empty((n, k), dtype=torch.bfloat16, device="cuda"), 2)
+        a = ops.fill_uniform_(torch.empty((m, k), dtype=dt, device="cuda"), 1)
+        b = ops.fill_uniform_(torch.empty((n, k), dtype=dt, device="cuda"), 2)
         c_old = torch.empty((m, n), dtype=torch.bfloat16, device="cuda")
         c_new = torch.empty_like(c_old)
         c_t = torch.empty_like(c_old)
-        fns = {"old": runner(old[(m, n, k)], a, b, c_old), "new": runner(new[(m, n, k)], a, b, c_new),
-               "torch": lambda: torch.matmul(a, b.T, out=c_t)}
+        if fp8:
+            fns = {"old": runner_fp8(old[(m, n, k)], a, b, c_old),
+                   "new": runner_fp8(new[(m, n, k)], a, b, c_new),
+                   "torch": lambda: torch._scaled_mm(a, b.T, scale_a=one, scale_b=one,
+                                                     out_dtype=torch.bfloat16)}
+        else:
+            fns = {"old": runner(old[(m, n, k)], a, b, c_old),
+                   "new": runner(new[(m, n, k)], a, b, c_new),
+                   "torch": lambda: torch.matmul(a, b.T, out=c_t)}
         t = {x: [] for x in fns}
         for _ in range(args.rounds):
             for x, fn in fns.items():
                 t[x].append(timed(fn, args.iters))
         torch.cuda.synchronize()
         atol, rtol = ops.gemm_tolerance(k)
+        if fp8:   # e4m3 operands: compare the two plans' bf16 outputs loosely
+            atol, rtol = 4 * atol, 4 * rtol
         ref = c_old.float()
         ok = bool(torch.all((c_new.float() - ref).abs() <= atol + rtol * ref.abs()))
         bad += not ok
@@ -96,7 +124,7 @@ def main():
                           "hipblaslt_us": round(med["torch"], 1), "new_speedup": round(ratios[-1], 3),
                           "new_ok": ok}), flush=True)
     if ratios:
-        print(json.dumps({"summary": True, "new": [args.margin, args.min_k],
+        print(json.dumps({"summary": True, "dtype": args.dtype, "new": [args.margin, args.min_k],
                           "old": [args.old_margin, args.old_min_k], "shapes": len(shapes),
                           "changed": len(changed), "faster": sum(r > 1.0 for r in ratios),
                           "median_speedup": round(statistics.median(ratios), 3),

@@ -210,11 +210,15 @@ constexpr int kLongSliceK = 1024;
 // host-only A/B knob (tools/margin_ab.py): the long-slice margin and threshold
 // the plan uses (margin <= 0 / long_k < 0: the shipping values; margin 1.1 =
 // round 4's plan); both are in the plan cache key
+// fp8_long > 0 also applies the long-slice margin to K1-fp8's split-K (off in
+// the shipping plan)
 static double g_splitk_margin = 0.0;
 static int g_splitk_min_k = -1;
-NTM_API void ntm_set_plan_splitk(double margin, int long_k) {
+static bool g_splitk_fp8_long = false;
+NTM_API void ntm_set_plan_splitk(double margin, int long_k, int fp8_long) {
   g_splitk_margin = margin > 0.0 ? margin : 0.0;
   g_splitk_min_k = long_k >= 0 ? long_k : -1;
+  g_splitk_fp8_long = fp8_long > 0;
 }
 inline double splitk_long_margin() {
   return g_splitk_margin > 0.0 ? g_splitk_margin : kSplitKMarginLong;
@@ -439,7 +443,8 @@ inline K1Plan plan_k1_search(int M, int N, int K, bool splitk, bool fp8) {
       const double t = rounds(tiles * slices) * 2.0 * st.tm * st.tn * kc / (kPerCU * st.eff) +
                        kRedFixed + (double)slices * M * N * 4.0 / kRedBW;
       // (K1-fp8's split-K keeps 1.1: the long-slice margin was measured on bf16 only)
-      const double margin = !fp8 && kc >= splitk_long_k() ? splitk_long_margin() : kSplitKMargin;
+      const double margin = (!fp8 || g_splitk_fp8_long) && kc >= splitk_long_k()
+                                ? splitk_long_margin() : kSplitKMargin;
       if (t < best_t && t * margin < unsplit && t < sk_bar) {
         best_t = t;
         split = K1Plan{M, st.variant, st.variant, slices};
@@ -461,9 +466,11 @@ struct PlanKey {
   int pp;
   double margin;
   int min_k;
+  bool fp8_long;
   bool operator==(const PlanKey& o) const {
     return M == o.M && N == o.N && K == o.K && cus == o.cus && splitk == o.splitk &&
-           fp8 == o.fp8 && pp == o.pp && margin == o.margin && min_k == o.min_k;
+           fp8 == o.fp8 && pp == o.pp && margin == o.margin && min_k == o.min_k &&
+           fp8_long == o.fp8_long;
   }
 };
 struct PlanEntry {
@@ -478,7 +485,7 @@ inline K1Plan plan_k1(int M, int N, int K, bool splitk = false, bool fp8 = false
   static thread_local PlanEntry cache[kPlanCacheSlots] = {};
   const PlanKey key{M, N, K, ntm::gemm6::device_cus(), splitk, fp8,
                     (g_plan_pp ? 1 : 0) | (g_plan_pp_split ? 2 : 0), g_splitk_margin,
-                    g_splitk_min_k};
+                    g_splitk_min_k, g_splitk_fp8_long};
   const unsigned h = ((unsigned)M * 2654435761u) ^ ((unsigned)N * 40503u) ^ ((unsigned)K * 97u) ^
                      ((unsigned)key.cus << 3) ^ (splitk ? 0x55u : 0u) ^ (fp8 ? 0xAAu : 0u) ^
                      ((unsigned)key.pp << 8);
