@@ -119,13 +119,13 @@ def set_plan_pp_tiles(on: bool = True, split: bool | None = None) -> None:
     _DEFAULT_SK.clear()
 
 
-def set_plan_splitk(margin: float = 0.0, long_slice_k: int = -1, fp8: bool = False) -> None:
+def set_plan_splitk(margin: float = 0.0, long_slice_k: int = -1, fp8: bool = True) -> None:
     """A/B knob for tools (tools/margin_ab.py): the factor by which a split-K
     plan whose slices keep at least ``long_slice_k`` of K must beat the unsplit
     plan's predicted time (shorter slices, and any split against stream-K, keep
-    1.1). margin <= 0 / long_slice_k < 0: the shipping 1.03 / 1024; margin 1.1
-    = round 4's plan. ``fp8``: apply it to K1-fp8's split-K too (the shipping
-    plan does not). Process-wide."""
+    1.1). margin <= 0 / long_slice_k < 0: the shipping 1.03 / 1024 (K1-fp8:
+    1088 pairs of e4m3 values); margin 1.1 = round 4's plan. ``fp8`` False keeps
+    K1-fp8's split-K at 1.1. Process-wide."""
     lib().ntm_set_plan_splitk(float(margin), int(long_slice_k), 1 if fp8 else 0)
     _DEFAULT_WS.clear()
     _DEFAULT_SK.clear()

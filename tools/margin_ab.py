@@ -66,7 +66,7 @@ def main():
     ap.add_argument("--old-margin", type=float, default=1.1)
     ap.add_argument("--old-min-k", type=int, default=0)
     ap.add_argument("--dtype", default="bf16", choices=("bf16", "fp8"),
-                    help="fp8: K1-fp8's split-K plan with the long-slice margin enabled for it")
+                    help="fp8: K1-fp8's split-K plan (old rule: 1.1 for fp8 too)")
     ap.add_argument("--n", type=int, default=3000)
     ap.add_argument("--seed", type=int, default=5)
     ap.add_argument("--max", type=int, default=40, help="time at most this many changed shapes")
@@ -82,9 +82,9 @@ def main():
         shapes = [tuple(rng.randrange(256, 8193, step) for _ in range(3)) for _ in range(args.n)]
     fp8 = args.dtype == "fp8"
     plan = ops.k1_fp8_splitk_plan if fp8 else ops.k1_splitk_plan
-    ops.set_plan_splitk(args.old_margin, args.old_min_k)
+    ops.set_plan_splitk(args.old_margin, args.old_min_k, fp8=False)
     old = {s: tuple(plan(*s)) for s in shapes}
-    ops.set_plan_splitk(args.margin, args.min_k, fp8=fp8)
+    ops.set_plan_splitk(args.margin, args.min_k)
     new = {s: tuple(plan(*s)) for s in shapes}
     ops.set_plan_splitk()
     changed = [s for s in shapes if old[s] != new[s]][: args.max]

@@ -207,18 +207,22 @@ constexpr double kRedBW = 2e12;
 constexpr double kSplitKMargin = 1.1;
 constexpr double kSplitKMarginLong = 1.03;
 constexpr int kLongSliceK = 1024;
+// K1-fp8 (K in bf16-sized pairs of e4m3): the same rule from slices of > 1024
+// pairs (profiles/r5_margin/fp8_seed9/10: 28 of 35 changed shapes faster,
+// median 1.15; the two that lost 15-20 % had slices of 1000 / 1016 pairs)
+constexpr int kLongSliceKFp8 = 1088;
 // host-only A/B knob (tools/margin_ab.py): the long-slice margin and threshold
 // the plan uses (margin <= 0 / long_k < 0: the shipping values; margin 1.1 =
 // round 4's plan); both are in the plan cache key
-// fp8_long > 0 also applies the long-slice margin to K1-fp8's split-K (off in
-// the shipping plan)
+// fp8_long = 0 keeps K1-fp8's split-K at 1.1 everywhere (round 4's fp8 plan);
+// < 0: the shipping fp8 rule
 static double g_splitk_margin = 0.0;
 static int g_splitk_min_k = -1;
-static bool g_splitk_fp8_long = false;
+static bool g_splitk_fp8_long = true;
 NTM_API void ntm_set_plan_splitk(double margin, int long_k, int fp8_long) {
   g_splitk_margin = margin > 0.0 ? margin : 0.0;
   g_splitk_min_k = long_k >= 0 ? long_k : -1;
-  g_splitk_fp8_long = fp8_long > 0;
+  g_splitk_fp8_long = fp8_long != 0;
 }
 inline double splitk_long_margin() {
   return g_splitk_margin > 0.0 ? g_splitk_margin : kSplitKMarginLong;
@@ -442,8 +446,9 @@ inline K1Plan plan_k1_search(int M, int N, int K, bool splitk, bool fp8) {
       const double kc = ntm::gemmt::splitk_kc(K, sp);
       const double t = rounds(tiles * slices) * 2.0 * st.tm * st.tn * kc / (kPerCU * st.eff) +
                        kRedFixed + (double)slices * M * N * 4.0 / kRedBW;
-      // (K1-fp8's split-K keeps 1.1: the long-slice margin was measured on bf16 only)
-      const double margin = (!fp8 || g_splitk_fp8_long) && kc >= splitk_long_k()
+      const int long_k = fp8 ? (g_splitk_min_k >= 0 ? g_splitk_min_k : kLongSliceKFp8)
+                             : splitk_long_k();
+      const double margin = (!fp8 || g_splitk_fp8_long) && kc >= long_k
                                 ? splitk_long_margin() : kSplitKMargin;
       if (t < best_t && t * margin < unsplit && t < sk_bar) {
         best_t = t;
