@@ -124,7 +124,7 @@ def set_plan_splitk(margin: float = 0.0, long_slice_k: int = -1, fp8: bool = Tru
     plan whose slices keep at least ``long_slice_k`` of K must beat the unsplit
     plan's predicted time (shorter slices, and any split against stream-K, keep
     1.1). margin <= 0 / long_slice_k < 0: the shipping 1.03 / 1024 (K1-fp8:
-    1088 pairs of e4m3 values); margin 1.1 = round 4's plan. ``fp8`` False keeps
+    1152 pairs of e4m3 values); margin 1.1 = round 4's plan. ``fp8`` False keeps
     K1-fp8's split-K at 1.1. Process-wide."""
     lib().ntm_set_plan_splitk(float(margin), int(long_slice_k), 1 if fp8 else 0)
     _DEFAULT_WS.clear()

@@ -394,3 +394,19 @@ def test_splitk_margin_by_slice_length(splitk_plan):
     finally:
         ops.set_plan_splitk()
     assert splitk_plan(1040, 2776, 5096) == (1040, "tile160", "tile160", 2)
+
+
+def test_fp8_splitk_margin_by_slice_length():
+    """K1-fp8's split-K takes the long-slice margin from slices of >= 1152 pairs
+    of e4m3 values (profiles/r5_margin/fp8_seed*): 496x3872x5584 splits in two
+    (31.4 -> 25.4 us); 336x3856x4144 (slices of 1036 pairs, 16.2 -> 19.4 us
+    when split) stays whole; fp8=False brings back round 4's fp8 plan."""
+    from nvidia_terraform_modules_amd import ops
+
+    assert ops.k1_fp8_splitk_plan(496, 3872, 5584) == (496, "tile128", "tile128", 2)
+    assert ops.k1_fp8_splitk_plan(336, 3856, 4144) == (336, "tile128", "tile128", 1)
+    ops.set_plan_splitk(fp8=False)
+    try:
+        assert ops.k1_fp8_splitk_plan(496, 3872, 5584) == (496, "tile128", "tile128", 1)
+    finally:
+        ops.set_plan_splitk()

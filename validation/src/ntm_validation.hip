@@ -207,10 +207,11 @@ constexpr double kRedBW = 2e12;
 constexpr double kSplitKMargin = 1.1;
 constexpr double kSplitKMarginLong = 1.03;
 constexpr int kLongSliceK = 1024;
-// K1-fp8 (K in bf16-sized pairs of e4m3): the same rule from slices of > 1024
-// pairs (profiles/r5_margin/fp8_seed9/10: 28 of 35 changed shapes faster,
-// median 1.15; the two that lost 15-20 % had slices of 1000 / 1016 pairs)
-constexpr int kLongSliceKFp8 = 1088;
+// K1-fp8 (K in bf16-sized pairs of e4m3): the same rule from slices of >= 1152
+// pairs (profiles/r5_margin/fp8_seed*: of 52 changed shapes on three seeds, the
+// three that lost 15-20 % had slices of 1000-1036 pairs, 1024 / 1088 after
+// rounding to the K tile; from 1152 on, 43 of 49 ran faster, median 1.13)
+constexpr int kLongSliceKFp8 = 1152;
 // host-only A/B knob (tools/margin_ab.py): the long-slice margin and threshold
 // the plan uses (margin <= 0 / long_k < 0: the shipping values; margin 1.1 =
 // round 4's plan); both are in the plan cache key
