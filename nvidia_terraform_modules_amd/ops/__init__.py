@@ -38,7 +38,6 @@ from .kernels import (  # noqa: F401
     k1_plan,
     k1_splitk_plan,
     ref_gemm_f32,
-    set_plan_pp_orient,
     set_plan_pp_tiles,
     set_plan_splitk,
     sk_ws_bytes,

@@ -119,16 +119,6 @@ def set_plan_pp_tiles(on: bool = True, split: bool | None = None) -> None:
     _DEFAULT_SK.clear()
 
 
-def set_plan_pp_orient(on: bool = False) -> None:
-    """A/B knob for tools (experimental, off in the shipping plan): orient the
-    192-wide tiles on all of C by C's shape (the 256-wide side along the
-    shorter dimension, when it fits one round) instead of the edge-waste
-    tie-break alone. Process-wide."""
-    lib().ntm_set_plan_pp_orient(1 if on else 0)
-    _DEFAULT_WS.clear()
-    _DEFAULT_SK.clear()
-
-
 def set_plan_splitk(margin: float = 0.0, long_slice_k: int = -1, fp8: bool = True) -> None:
     """A/B knob for tools (tools/margin_ab.py): the factor by which a split-K
     plan whose slices keep at least ``long_slice_k`` of K must beat the unsplit

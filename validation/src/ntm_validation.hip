@@ -156,10 +156,6 @@ NTM_API void ntm_set_plan_pp_tiles(int on) {
   g_plan_pp = (on & 1) != 0;
   g_plan_pp_split = (on & 2) != 0;
 }
-// host-only A/B knob (off in the shipping plan): orient the 192-wide tiles by
-// C's shape (see plan_k1_search)
-static bool g_plan_pp_orient = false;
-NTM_API void ntm_set_plan_pp_orient(int on) { g_plan_pp_orient = on != 0; }
 // The counted vmcnt phase P (0..3) of the 192-wide ping-pong build <ah, bh>
 // waits for (Geo::vmc, gemm_bf16_pp3h.hpp; 128 / 128 is pingpong8c's 10): host
 // only, for the CPU model of the DMA schedule (tests/test_pp3h_schedule_model.py).
@@ -362,18 +358,6 @@ inline K1Plan plan_k1_search(int M, int N, int K, bool splitk, bool fp8) {
       }
     }
   }
-  // 192-wide tiles on all of C in one round: both orientations cost the same in
-  // the model, and the edge-waste tie-break above picked the slower one on 9 of
-  // 13 measured shapes, where the one whose 256-wide side runs along C's
-  // shorter dimension was faster on 8. Experimental (knob off): it needs fresh
-  // shapes before it ships.
-  if (g_plan_pp_orient && M != N && best.feasible() && best.top_rows == M &&
-      best.top_variant == best.rest_variant && (best.top_variant == 27 || best.top_variant == 28)) {
-    const int want = N < M ? 27 : 28;  // 27: 192x256 (256 along N), 28: 256x192 (256 along M)
-    const int tm = want == 27 ? 192 : 256, tn = want == 27 ? 256 : 192;
-    if (want != best.top_variant && (double)((M + tm - 1) / tm) * ((N + tn - 1) / tn) <= kCUs)
-      best = K1Plan{M, want, want};
-  }
   // whole 256x256 tiles over more than one round: the persistent build
   // (K1-fp8: from one round on, K in bf16-sized pairs)
   if (!fp8 && best.feasible() && best.top_variant == kDefaultVariant && K >= 256 &&
@@ -506,8 +490,7 @@ constexpr int kPlanCacheSlots = 256;
 inline K1Plan plan_k1(int M, int N, int K, bool splitk = false, bool fp8 = false) {
   static thread_local PlanEntry cache[kPlanCacheSlots] = {};
   const PlanKey key{M, N, K, ntm::gemm6::device_cus(), splitk, fp8,
-                    (g_plan_pp ? 1 : 0) | (g_plan_pp_split ? 2 : 0) | (g_plan_pp_orient ? 4 : 0),
-                    g_splitk_margin,
+                    (g_plan_pp ? 1 : 0) | (g_plan_pp_split ? 2 : 0), g_splitk_margin,
                     g_splitk_min_k, g_splitk_fp8_long};
   const unsigned h = ((unsigned)M * 2654435761u) ^ ((unsigned)N * 40503u) ^ ((unsigned)K * 97u) ^
                      ((unsigned)key.cus << 3) ^ (splitk ? 0x55u : 0u) ^ (fp8 ? 0xAAu : 0u) ^
