@@ -54,7 +54,9 @@ done
 # longer decompresses the other 12 targets: profiles/r5_fatbin). Set
 # NTM_KEEP_FATBIN=1 to keep the vendor bundles as they are.
 here=$(cd "$(dirname "$0")" && pwd)
-if [ "${NTM_KEEP_FATBIN:-0}" != 1 ]; then
+if [ "${NTM_KEEP_FATBIN:-0}" != 1 ] && ! command -v python3 > /dev/null; then
+  echo "collect-runtime: no python3 in the build image; vendor fat binaries kept whole" >&2
+elif [ "${NTM_KEEP_FATBIN:-0}" != 1 ]; then
   for f in "$dest"/lib/*.so.*; do
     [ -L "$f" ] && continue
     python3 "$here/strip-fatbin.py" "$f" --bundler "$rocm_lib/llvm/bin/clang-offload-bundler"
