@@ -306,11 +306,36 @@ def test_runtime_closure_is_self_contained(closure):
     assert rc in (0, 2)   # 2 = no GPU in this container
 
 
+def test_runtime_closure_rccl_is_cut_to_gfx950(closure):
+    """collect-runtime.sh runs strip-fatbin.py: the closure's librccl carries a
+    host + gfx950 bundle only (profiles/r5_fatbin)."""
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location(
+        "strip_fatbin", ROOT / "validation" / "image" / "strip-fatbin.py")
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    lib = closure / "lib" / "librccl.so.1"
+    off, size = m.section(str(lib))
+    with open(lib, "rb") as f:
+        f.seek(off)
+        head = f.read(64)
+    assert head[:4] == b"CCOB" and m.bundle_bytes(head) < size // 4
+    res = m.strip(str(lib), "gfx950", "/opt/rocm/lib/llvm/bin/clang-offload-bundler", dry_run=True)
+    assert res["targets"] == 2 and res["changed"] is False, res
+
+
 @pytest.mark.gpu
 def test_runtime_closure_runs_validation_on_gpu(closure):
-    rc, out, err = _run_closure(closure, "--size", "1024", "--iters", "5")
+    """The image's closure on MI355X, RCCL included: its librccl is cut to
+    gfx950, and the all-reduce sweep still runs and verifies."""
+    rc, out, err = _run_closure(closure, "--size", "1024", "--iters", "5", "--rccl",
+                                "--allreduce-max-mib", "4", "--no-p2p")
     assert rc == 0, out + err[-3000:]
-    assert _last_json(out)["passed"]
+    rep = _last_json(out)
+    assert rep["passed"]
+    ar = rep.get("rccl_allreduce") or []
+    assert ar and all(not r.get("wrong") for r in ar), ar
     assert not [p for p in _loaded_from(err) if p.startswith("/opt/rocm")]
 
 
