@@ -56,3 +56,18 @@ locals {
     loc = body.blocks[1].body
     assert render(loc.attr("c")) == 'var.x ? [for k, v in var.m : "${k}=${v}" if v != null] : null'
     assert render(loc.attr("d")) == 'merge(local.a, { k = 1 })[0].name'
+
+
+def test_standing_summary_reproduces_the_committed_round5_standing():
+    """tools/standing_summary.py over profiles/r5_standing (box<X>_*.log) gives
+    exactly the committed summary.jsonl."""
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parents[1]
+    out = subprocess.run([sys.executable, str(root / "tools" / "standing_summary.py"),
+                          str(root / "profiles" / "r5_standing")],
+                         capture_output=True, text=True, check=True).stdout
+    want = (root / "profiles" / "r5_standing" / "summary.jsonl").read_text()
+    assert sorted(out.splitlines()) == sorted(want.splitlines())

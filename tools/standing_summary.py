@@ -10,6 +10,7 @@ one directory per box / gpurun call, and prints one JSON line per row:
   those below 0.97.
 
     python tools/standing_summary.py gpurun_out/r5_standA gpurun_out/r5_standB ...
+    python tools/standing_summary.py profiles/r5_standing      (box<X>_*.log per box)
 """
 from __future__ import annotations
 
@@ -45,16 +46,28 @@ def _set_summary(name: str, ratios: list[tuple[list[int], float]]) -> dict:
             "below_0.97_with_k_mod_16_eq_8": sum(s[2] % 16 == 8 for s, _ in low)}
 
 
+def _boxes(dirs: list[str]) -> list[tuple[str, str]]:
+    """(directory, file prefix) per box: a gpurun_out/<tag> directory holds one
+    box's standing_*.log; a profiles directory holds box<X>_*.log for several."""
+    out = []
+    for d in dirs:
+        pre = sorted({os.path.basename(p).split("_", 1)[0]
+                      for p in glob.glob(os.path.join(d, "box*_*.log"))})
+        out += [(d, p + "_") for p in pre] or [(d, "standing_")]
+    return out
+
+
 def main(dirs: list[str]) -> int:
     if not dirs or any(a in ("-h", "--help") for a in dirs):
         print(__doc__)
         return 0 if dirs else 2
+    boxes = _boxes(dirs)
     named: dict = {}
-    for d in dirs:
-        for path, key_ours, key_hb in (("standing_bf16.log", "default_tflops_med", "torch_tflops_med"),
-                                       ("standing_fp8.log", "ours_fp8_tflops_med",
+    for d, pre in boxes:
+        for path, key_ours, key_hb in (("bf16.log", "default_tflops_med", "torch_tflops_med"),
+                                       ("fp8.log", "ours_fp8_tflops_med",
                                         "hipblaslt_fp8_tflops_med")):
-            p = os.path.join(d, path)
+            p = os.path.join(d, pre + path)
             if not os.path.exists(p):
                 continue
             dtype = "bf16" if "bf16" in path else "fp8"
@@ -66,17 +79,17 @@ def main(dirs: list[str]) -> int:
         print(json.dumps({"dtype": dtype, "shape": shape, "boxes": len(rs),
                           "over_hipblaslt_median": round(statistics.median(rs), 4),
                           "per_box": [round(x, 4) for x in rs]}))
-    for d in dirs:
-        for p in sorted(glob.glob(os.path.join(d, "standing_ragged_seed*.log"))):
+    for d, pre in boxes:
+        for p in sorted(glob.glob(os.path.join(d, pre + "ragged_seed*.log"))):
             rat = [(_shape(r), r["default_over_hipblaslt"]) for r in _rows(p)
                    if "default_over_hipblaslt" in r and not r.get("summary")]
             if rat:
-                print(json.dumps(_set_summary(os.path.basename(p)[9:-4], rat)))
-        for p in sorted(glob.glob(os.path.join(d, "standing_random48_seed*.log"))):
+                print(json.dumps(_set_summary(os.path.basename(p)[len(pre):-4], rat)))
+        for p in sorted(glob.glob(os.path.join(d, pre + "random48_seed*.log"))):
             rat = [(_shape(r), r["default_tflops"] / r["torch_tflops"]) for r in _rows(p)
                    if r.get("torch_tflops")]
             if rat:
-                print(json.dumps(_set_summary(os.path.basename(p)[9:-4], rat)))
+                print(json.dumps(_set_summary(os.path.basename(p)[len(pre):-4], rat)))
     return 0
 
 
