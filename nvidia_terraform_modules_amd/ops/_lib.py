@@ -84,6 +84,7 @@ def _declare(lib: ctypes.CDLL) -> None:
         "ntm_set_cus_override": ([c_int], None),
         "ntm_set_plan_pp_tiles": ([c_int], None),
         "ntm_set_plan_splitk": ([ctypes.c_double, c_int, c_int], None),
+        "ntm_set_plan_splitk_ragged": ([c_int], None),
         "ntm_pp3h_vmcnt": ([c_int, c_int, c_int], c_int),
         "ntm_gemm_bf16_clock": ([c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp,
                                  c_vp], c_int),

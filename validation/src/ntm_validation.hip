@@ -220,6 +220,10 @@ constexpr int kLongSliceKFp8 = 1152;
 static double g_splitk_margin = 0.0;
 static int g_splitk_min_k = -1;
 static bool g_splitk_fp8_long = true;
+// A/B knob (off in the shipping plan): split-K candidates priced against the
+// ragged-scaled unsplit time stream-K already uses
+static bool g_splitk_ragged = false;
+NTM_API void ntm_set_plan_splitk_ragged(int on) { g_splitk_ragged = on != 0; }
 NTM_API void ntm_set_plan_splitk(double margin, int long_k, int fp8_long) {
   g_splitk_margin = margin > 0.0 ? margin : 0.0;
   g_splitk_min_k = long_k >= 0 ? long_k : -1;
@@ -413,23 +417,25 @@ inline K1Plan plan_k1_search(int M, int N, int K, bool splitk, bool fp8) {
       }
     }
   }
+  // a single launch of one small tile in one round on ragged C runs slower
+  // than the model (SmallTile::ragged): stream-K is priced against the
+  // measured-ish time (and split-K too, with the A/B knob below)
+  double unsplit_ragged = unsplit;
+  if (best.top_rows == M && best.top_variant == best.rest_variant)
+    for (const SmallTile& st : kSmallTiles)
+      if (st.variant == best.top_variant &&
+          (double)((M + st.tm - 1) / st.tm) * ((N + st.tn - 1) / st.tn) <= kCUs &&
+          (M % st.tm != 0 || N % st.tn != 0 || K % 128 != 0))
+        // rows of A / B at least 64-byte aligned (K % 32 == 0): a third of it
+        // (4704, 6240, 10720: 1.00-1.16 where 16 / 32-byte rows gave 1.1-1.5)
+        // and 16-byte rows (K % 16 == 8) at least 1.25 (128x128 1.26 / 1.27,
+        // 160x160 1.11 / 1.35 measured)
+        unsplit_ragged *= K % 32 == 0   ? 1.0 + (st.ragged - 1.0) * 0.4
+                          : K % 16 == 8 ? (st.ragged > 1.0 && st.ragged < 1.25 ? 1.25 : st.ragged)
+                                        : st.ragged;
   if (sk_variant != 0) {
     g_plan_debug_sk_s = t_sk;
-    // a single launch of one small tile in one round on ragged C runs slower
-    // than the model (SmallTile::ragged): price stream-K against the measured-ish time
-    double unsplit_vs_sk = unsplit;
-    if (best.top_rows == M && best.top_variant == best.rest_variant)
-      for (const SmallTile& st : kSmallTiles)
-        if (st.variant == best.top_variant &&
-            (double)((M + st.tm - 1) / st.tm) * ((N + st.tn - 1) / st.tn) <= kCUs &&
-            (M % st.tm != 0 || N % st.tn != 0 || K % 128 != 0))
-          // rows of A / B at least 64-byte aligned (K % 32 == 0): a third of it
-          // (4704, 6240, 10720: 1.00-1.16 where 16 / 32-byte rows gave 1.1-1.5)
-          // and 16-byte rows (K % 16 == 8) at least 1.25 (128x128 1.26 / 1.27,
-          // 160x160 1.11 / 1.35 measured)
-          unsplit_vs_sk *= K % 32 == 0   ? 1.0 + (st.ragged - 1.0) * 0.4
-                           : K % 16 == 8 ? (st.ragged > 1.0 && st.ragged < 1.25 ? 1.25 : st.ragged)
-                                         : st.ragged;
+    const double unsplit_vs_sk = unsplit_ragged;
     g_plan_debug_unsplit_s = unsplit_vs_sk;
     if (t_sk * kSkMargin < unsplit_vs_sk) {
       split = K1Plan{M, sk_variant, sk_variant, 1};
@@ -451,7 +457,7 @@ inline K1Plan plan_k1_search(int M, int N, int K, bool splitk, bool fp8) {
                              : splitk_long_k();
       const double margin = (!fp8 || g_splitk_fp8_long) && kc >= long_k
                                 ? splitk_long_margin() : kSplitKMargin;
-      if (t < best_t && t * margin < unsplit && t < sk_bar) {
+      if (t < best_t && t * margin < (g_splitk_ragged ? unsplit_ragged : unsplit) && t < sk_bar) {
         best_t = t;
         split = K1Plan{M, st.variant, st.variant, slices};
       }
@@ -490,7 +496,8 @@ constexpr int kPlanCacheSlots = 256;
 inline K1Plan plan_k1(int M, int N, int K, bool splitk = false, bool fp8 = false) {
   static thread_local PlanEntry cache[kPlanCacheSlots] = {};
   const PlanKey key{M, N, K, ntm::gemm6::device_cus(), splitk, fp8,
-                    (g_plan_pp ? 1 : 0) | (g_plan_pp_split ? 2 : 0), g_splitk_margin,
+                    (g_plan_pp ? 1 : 0) | (g_plan_pp_split ? 2 : 0) | (g_splitk_ragged ? 4 : 0),
+                    g_splitk_margin,
                     g_splitk_min_k, g_splitk_fp8_long};
   const unsigned h = ((unsigned)M * 2654435761u) ^ ((unsigned)N * 40503u) ^ ((unsigned)K * 97u) ^
                      ((unsigned)key.cus << 3) ^ (splitk ? 0x55u : 0u) ^ (fp8 ? 0xAAu : 0u) ^
