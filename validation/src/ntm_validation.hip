@@ -457,7 +457,8 @@ inline K1Plan plan_k1_search(int M, int N, int K, bool splitk, bool fp8) {
                              : splitk_long_k();
       const double margin = (!fp8 || g_splitk_fp8_long) && kc >= long_k
                                 ? splitk_long_margin() : kSplitKMargin;
-      if (t < best_t && t * margin < (g_splitk_ragged ? unsplit_ragged : unsplit) && t < sk_bar) {
+      const double vs = g_splitk_ragged && kc >= splitk_long_k() ? unsplit_ragged : unsplit;
+      if (t < best_t && t * margin < vs && t < sk_bar) {
         best_t = t;
         split = K1Plan{M, st.variant, st.variant, slices};
       }
