@@ -387,12 +387,16 @@ def test_splitk_margin_by_slice_length(splitk_plan):
     assert splitk_plan(3896, 368, 2064) == (3896, "tile128", "tile128", 2)
     assert splitk_plan(2264, 328, 1392) == (2264, "tile128", "tile128", 1)
     assert splitk_plan(1136, 2728, 8072)[1] == "pingpong8s"
+    from nvidia_terraform_modules_amd.ops._lib import lib
+
     ops.set_plan_splitk(1.1, 0)
+    lib().ntm_set_plan_splitk_ragged(0)   # round 4's rule: 1.1, no ragged pricing
     try:
         assert splitk_plan(1040, 2776, 5096) == (1040, "tile128", "tile128", 1)
         assert splitk_plan(3896, 368, 2064) == (3896, "tile128", "tile128", 1)
     finally:
         ops.set_plan_splitk()
+        lib().ntm_set_plan_splitk_ragged(1)
     assert splitk_plan(1040, 2776, 5096) == (1040, "tile160", "tile160", 2)
 
 
@@ -410,3 +414,18 @@ def test_fp8_splitk_margin_by_slice_length():
         assert ops.k1_fp8_splitk_plan(496, 3872, 5584) == (496, "tile128", "tile128", 1)
     finally:
         ops.set_plan_splitk()
+
+
+def test_splitk_priced_against_ragged_unsplit_time(splitk_plan):
+    """Long-slice split-K candidates are priced against the ragged-scaled
+    unsplit time stream-K uses (profiles/r5_margin, fresh seed 14: 46 of 55
+    changed plans faster): 3232x936x4024 splits on 160x160 (48.5 -> 40.6 us);
+    with the knob off it stays on one round of 128x128 tiles."""
+    from nvidia_terraform_modules_amd.ops._lib import lib
+
+    assert splitk_plan(3232, 936, 4024) == (3232, "tile160", "tile160", 2)
+    lib().ntm_set_plan_splitk_ragged(0)
+    try:
+        assert splitk_plan(3232, 936, 4024) == (3232, "tile128", "tile128", 1)
+    finally:
+        lib().ntm_set_plan_splitk_ragged(1)

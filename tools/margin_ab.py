@@ -68,7 +68,8 @@ def main():
     ap.add_argument("--dtype", default="bf16", choices=("bf16", "fp8"),
                     help="fp8: K1-fp8's split-K plan (old rule: 1.1 for fp8 too)")
     ap.add_argument("--ragged", action="store_true",
-                    help="new rule also prices split-K against the ragged-scaled unsplit time")
+                    help="A/B the ragged pricing of long-slice split-K alone (old: without it; "
+                         "without --ragged both sides run without it)")
     ap.add_argument("--n", type=int, default=3000)
     ap.add_argument("--seed", type=int, default=5)
     ap.add_argument("--max", type=int, default=40, help="time at most this many changed shapes")
@@ -85,13 +86,14 @@ def main():
     fp8 = args.dtype == "fp8"
     plan = ops.k1_fp8_splitk_plan if fp8 else ops.k1_splitk_plan
     ops.set_plan_splitk(args.old_margin, args.old_min_k, fp8=False)
-    if args.ragged:   # A/B of the ragged pricing alone: old = the shipping rule
+    ops._lib.lib().ntm_set_plan_splitk_ragged(0)
+    if args.ragged:   # A/B of the ragged pricing alone: old = the margin rule without it
         ops.set_plan_splitk()
     old = {s: tuple(plan(*s)) for s in shapes}
     ops.set_plan_splitk(args.margin, args.min_k)
     ops._lib.lib().ntm_set_plan_splitk_ragged(1 if args.ragged else 0)
     new = {s: tuple(plan(*s)) for s in shapes}
-    ops._lib.lib().ntm_set_plan_splitk_ragged(0)
+    ops._lib.lib().ntm_set_plan_splitk_ragged(1)   # the shipping plan
     ops.set_plan_splitk()
     changed = [s for s in shapes if old[s] != new[s]][: args.max]
     ratios, bad = [], 0

@@ -220,9 +220,13 @@ constexpr int kLongSliceKFp8 = 1152;
 static double g_splitk_margin = 0.0;
 static int g_splitk_min_k = -1;
 static bool g_splitk_fp8_long = true;
-// A/B knob (off in the shipping plan): split-K candidates priced against the
-// ragged-scaled unsplit time stream-K already uses
-static bool g_splitk_ragged = false;
+// Split-K candidates with slices of >= kLongSliceK are priced against the
+// ragged-scaled unsplit time that stream-K already uses (profiles/r5_margin/):
+// 146 changed plans on seeds 12 / 13 - long slices 95 of 129 faster, geo-mean
+// 1.045; short ones lost up to 37 % - then fresh seed 14: 46 of 55 faster,
+// median 1.04, worst 0.875. bf16 only (not measured on K1-fp8). Host-only A/B
+// knob (ntm_set_plan_splitk_ragged).
+static bool g_splitk_ragged = true;
 NTM_API void ntm_set_plan_splitk_ragged(int on) { g_splitk_ragged = on != 0; }
 NTM_API void ntm_set_plan_splitk(double margin, int long_k, int fp8_long) {
   g_splitk_margin = margin > 0.0 ? margin : 0.0;
@@ -457,7 +461,7 @@ inline K1Plan plan_k1_search(int M, int N, int K, bool splitk, bool fp8) {
                              : splitk_long_k();
       const double margin = (!fp8 || g_splitk_fp8_long) && kc >= long_k
                                 ? splitk_long_margin() : kSplitKMargin;
-      const double vs = g_splitk_ragged && kc >= splitk_long_k() ? unsplit_ragged : unsplit;
+      const double vs = g_splitk_ragged && !fp8 && kc >= splitk_long_k() ? unsplit_ragged : unsplit;
       if (t < best_t && t * margin < vs && t < sk_bar) {
         best_t = t;
         split = K1Plan{M, st.variant, st.variant, slices};
