@@ -288,6 +288,9 @@ class XgmiAllReduce:
         self._own = []
 
 
+EXPORT_ATTEMPTS = 5
+
+
 def _alloc_exported(L, nbytes: int, uncached: int, own: list) -> tuple:
     """Allocate ``nbytes`` and export its IPC handle: (pointer, 64 handle bytes).
 
@@ -296,10 +299,17 @@ def _alloc_exported(L, nbytes: int, uncached: int, own: list) -> tuple:
     back a range whose previous export a peer process has not finished
     releasing: the driver's dmabuf release runs after hipIpcCloseMemHandle and
     the close barrier return (seen once at world 8, round 5, after round 4's
-    collective close made it rare). That allocation is kept, not freed, so the
-    one retry gets a different range; a second refusal is raised."""
+    collective close made it rare). That allocation is kept, not freed, so a
+    retry gets a different range. A refused range was refused twice in a row
+    once (world 8, end of round 5), so there are EXPORT_ATTEMPTS tries, with a
+    short growing pause that lets the peers' releases land; the last refusal
+    is raised."""
+    import time
+
     last = 0
-    for _ in range(2):
+    for i in range(EXPORT_ATTEMPTS):
+        if i:
+            time.sleep(0.01 * (2 ** (i - 1)))
         p = ctypes.c_void_p()
         check(L.ntm_malloc(ctypes.byref(p), nbytes, uncached), "ntm_malloc")
         own.append(p.value)
