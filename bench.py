@@ -123,10 +123,21 @@ def prewarm_settle(fn, sync, min_s: float, chunk: int = 16) -> dict:
             return {"seconds": round(el, 3), "launches": launches}
 
 
-def power_window(fn, sync, sample, min_s: float, chunk: int = 16):
+# plain K1 launches queued ahead of a host-blocking AMD SMI read (~43 ms at
+# 8192^3): the read measured 1-40 ms (smi_sample_ms), and the GPU must not go
+# idle under it
+POWER_WINDOW_CHUNK = 64
+# plain K1 launches queued (no sync) ahead of each stamped clock batch (~27 ms,
+# longer than the ~25 ms post-idle transient)
+CLOCK_PREQUEUE = 40
+
+
+def power_window(fn, sync, sample, min_s: float, chunk: int = 16, final_sync: bool = True):
     """Two telemetry samples around at least ``min_s`` s of back-to-back ``fn``
     launches; each is read while ``chunk`` launches are queued, so neither end
-    sees an idle GPU. Returns (before, after, run) for ``smi.window``."""
+    sees an idle GPU. ``final_sync`` False leaves the last chunk running (the
+    caller queues more work behind it at once). Returns (before, after, run)
+    for ``smi.window``."""
     for _ in range(chunk):
         fn()
     before = sample()
@@ -134,8 +145,49 @@ def power_window(fn, sync, sample, min_s: float, chunk: int = 16):
     for _ in range(chunk):
         fn()
     after = sample()
-    sync()
+    if final_sync:
+        sync()
     return before, after, run
+
+
+ENERGY_WINDOW_S = 0.6
+
+
+def energy_compare(kernels: dict, sync, sample, smi_mod, window_s: float = ENERGY_WINDOW_S,
+                   order: str = "ABBA") -> dict:
+    """Joules per TFLOP of each kernel: ``kernels[name] = (launch callable,
+    TF/s)``. Each window is >= ``window_s`` of one kernel's back-to-back
+    launches (``power_window``, samples read under queued launches, after a
+    0.2 s settle on that kernel); the windows run in ``order`` (ABBA: neither
+    kernel always runs on the warmer chip) and each kernel's average power is
+    the mean over its windows. Never raises: a window without energy data gives
+    None."""
+    names = list(kernels)
+    seq = [names[0], names[1], names[1], names[0]] if order == "ABBA" and len(names) == 2 \
+        else names
+    per: dict = {k: [] for k in names}
+    for k in seq:
+        fn = kernels[k][0]
+        prewarm_settle(fn, sync, 0.2)
+        b, a, run = power_window(fn, sync, sample, window_s, chunk=POWER_WINDOW_CHUNK)
+        per[k].append(smi_mod.window(b, a))
+    out = {}
+    for k in names:
+        ws = [w.get("avg_power_W") for w in per[k]]
+        ws = [w for w in ws if w is not None]
+        avg = sum(ws) / len(ws) if ws else None
+        tf = kernels[k][1]
+        out[k] = {"avg_power_W": round(avg, 1) if avg is not None else None,
+                  "tflops": round(tf, 1),
+                  "joules_per_tflop": round(avg / tf, 4) if avg is not None and tf > 0 else None,
+                  "windows_W": [w.get("avg_power_W") for w in per[k]],
+                  "windows_s": [w.get("seconds") for w in per[k]],
+                  "ppt_pct": [w.get("ppt_pct") for w in per[k]]}
+    if len(names) == 2 and all(out[k]["joules_per_tflop"] for k in names):
+        out[f"{names[0]}_over_{names[1]}_joules_per_tflop"] = round(
+            out[names[0]]["joules_per_tflop"] / out[names[1]]["joules_per_tflop"], 4)
+    out["order"] = seq
+    return out
 
 
 def interleaved_compare(fns: dict, dev, rounds: int, launches: int) -> dict:
@@ -250,10 +302,20 @@ def main(argv=None) -> int:
         if dev.type == "cuda":
             torch.cuda.synchronize(dev)
 
+    smi_ms: list = []
+
+    def smi_sample():
+        """One AMD SMI read, its host time recorded (smi_sample_ms in the JSON): a
+        read that outlasts the launches queued behind it leaves the GPU idle."""
+        t = time.perf_counter()
+        r = smi.sample(dev)
+        smi_ms.append(round((time.perf_counter() - t) * 1e3, 3))
+        return r
+
     _ = torch.empty(1, device=dev)
     _CLOCK.mark("hip_init")
     if dev.type == "cuda":
-        smi.sample(dev)   # AMD SMI initialises here, not next to the timed loop
+        smi_sample()   # AMD SMI initialises here, not next to the timed loop
 
     wl = GemmWorkload(args.size, dev, seed=20250117 + env.rank, backend=backend)
     sync()
@@ -270,11 +332,17 @@ def main(argv=None) -> int:
     prewarm = prewarm_settle(wl.step, sync, args.prewarm_s)
 
     # ---- warmup (untimed): exactly W steps. The power / throttle sample that opens
-    # the telemetry window is read while the last warmup launches still run, so it
-    # adds no idle gap (an idle GPU re-boosts and overshoots its power limit).
+    # the telemetry window is read while POWER_WINDOW_CHUNK more pre-warm launches
+    # run (counted in prewarm_launches), with the W warmup steps queued behind
+    # them: an SMI read longer than W launches no longer leaves the GPU idle (an
+    # idle GPU re-boosts and overshoots its power limit) right before the timed loop.
+    if dev.type == "cuda":
+        for _ in range(POWER_WINDOW_CHUNK):
+            wl.step()
+        prewarm["launches"] += POWER_WINDOW_CHUNK
+    smi_before = smi_sample() if dev.type == "cuda" else None
     for _ in range(args.warmup):
         wl.step()
-    smi_before = smi.sample(dev) if dev.type == "cuda" else None
     sync()
 
     # ---- timed region: exactly K steps, barrier + sync on both sides; HIP events
@@ -289,7 +357,7 @@ def main(argv=None) -> int:
     tmr.stop()
     sync()
     t1 = time.perf_counter()
-    smi_after = smi.sample(dev) if dev.type == "cuda" else None
+    smi_after = smi_sample() if dev.type == "cuda" else None
     dist.barrier(env)
     my_seconds = tmr.seconds()
     elapsed = dist.all_reduce_max(env, my_seconds)
@@ -312,10 +380,15 @@ def main(argv=None) -> int:
         except Exception as e:  # noqa: BLE001 - reported per rank
             return {"median_GHz": None, "error": f"{type(e).__name__}: {e}"[:200]}
 
-    # The stamped launches follow a re-settle (>= 0.3 s of K1) and 8 more plain
-    # launches queued behind it with no sync, so they run in the steady state the
-    # timed loop ran in - not in the boost / overshoot transient an idle gap (the
-    # all-reduce above) starts (BENCH_r04: 663 -> 897 -> 711 us per stamped launch).
+    # The stamped launches must run in the steady state the timed loop ran in, not
+    # in the boost / overshoot transient an idle GPU starts (~25 ms of load to
+    # settle; BENCH_r04: 663 -> 897 -> 711 us per stamped launch, BENCH_r05: 640 ->
+    # 861 -> 664 after an AMD SMI read outlasted the launches queued behind it).
+    # So no host-blocking call (SMI sample, sync) comes right before them: after
+    # the power window, each stamped batch is queued behind CLOCK_PREQUEUE plain
+    # launches (~27 ms) with no sync, and a batch whose per-launch windows drift
+    # by more than 3 % (max / min) is stamped again, up to 3 batches
+    # (kernels.gemm_clock_stable; the JSON says how many it took).
     power_steady = None
     if dev.type == "cuda":
         prewarm_settle(wl.step, sync, 0.3)
@@ -323,11 +396,11 @@ def main(argv=None) -> int:
         # short timed loop (20 x 0.67 ms) gets the same counters at both ends. This
         # window covers >= 0.5 s of the same K1 launches in the steady state the
         # timed loop left, and stands in for it where the timed window is stale.
-        b, a, run = power_window(wl.step, sync, lambda: smi.sample(dev), 0.5)
+        b, a, run = power_window(wl.step, sync, lambda: smi_sample(), 0.5,
+                                 chunk=POWER_WINDOW_CHUNK, final_sync=False)
         power_steady = {**smi.window(b, a), "launches": run["launches"]}
-        for _ in range(8):
-            wl.step()
-    gclk = _probe("gemm_clock_ghz", wl.a, wl.b, wl.c, steps=min(max(args.steps, 1), 20))
+    gclk = _probe("gemm_clock_stable", wl.a, wl.b, wl.c, steps=min(max(args.steps, 1), 20),
+                  prequeue=wl.step, prequeue_launches=CLOCK_PREQUEUE)
     clk = _probe("clock_probe_ghz", dev)
     # the clock the TIMED loop ran at: shader cycles per launch are launch-invariant
     # (1.085-1.091 M at 8192^3), so median cycles / this rank's ms per step
@@ -345,6 +418,9 @@ def main(argv=None) -> int:
         timed_clk = round(cyc[len(cyc) // 2] / (my_seconds / args.steps) / 1e9, 4)
         gclk["ms_per_launch_over_ms_per_step"] = round(
             gclk["ms_per_launch"] / (my_seconds / args.steps * 1e3), 4)
+        # the stamped launches ran at the timed loop's pace: otherwise
+        # their clock describes a different power state and must not label the rank
+        gclk["clock_trusted"] = 0.95 <= gclk["ms_per_launch_over_ms_per_step"] <= 1.05
         # share of a timed step the bounding XCD's workgroups spend between their
         # stamps (the rest: dispatch ramp, drain, launch gap): timed-loop clock =
         # bound clock x this fraction
@@ -362,7 +438,8 @@ def main(argv=None) -> int:
     per_rank = dist.all_gather_obj(env, {"tflops": round(wl.flops * args.steps / my_seconds / 1e12, 2),
                                          "clock": clk, "gemm_clock": gclk,
                                          "timed_loop_clock": timed_clk, "power": power,
-                                         "power_steady": power_steady, "power_src": power_src})
+                                         "power_steady": power_steady, "power_src": power_src,
+                                         "smi_ms": smi_ms})
 
     def _pw(p: dict, key: str):
         src = p["power"] if p["power_src"] == "timed_loop" else p["power_steady"]
@@ -389,9 +466,19 @@ def main(argv=None) -> int:
         prewarm_settle(blas, sync, 0.3)
         cmp_ = interleaved_compare({"k1": wl.step, "hipblaslt": blas}, dev,
                                    rounds=args.compare_rounds, launches=20)
-        del cc
         k1_tf = wl.flops / cmp_["k1"]["median_s"] / 1e12
         hb_tf = wl.flops / cmp_["hipblaslt"]["median_s"] / 1e12
+        # energy per flop of each kernel (the headline is power-bound,
+        # so J/TFLOP is what ranks a bf16 change): AMD SMI energy-counter windows of
+        # >= ENERGY_WINDOW_S of back-to-back launches of ONE kernel, in ABBA order,
+        # each sample read under queued launches; J/TFLOP = the window's average
+        # socket power / that kernel's interleaved median TF/s.
+        if dev.type == "cuda":
+            extras["energy_rank0"] = energy_compare(
+                {"k1": (wl.step, k1_tf), "hipblaslt": (blas, hb_tf)}, sync, smi_sample, smi)
+            for k in ("k1", "hipblaslt"):
+                extras[f"{k}_joules_per_tflop"] = extras["energy_rank0"][k]["joules_per_tflop"]
+        del cc
         extras["interleaved_compare_rank0"] = {
             "rounds": args.compare_rounds, "launches_per_round": 20,
             "k1_tflops_median": round(k1_tf, 1), "hipblaslt_tflops_median": round(hb_tf, 1),
@@ -449,73 +536,31 @@ def main(argv=None) -> int:
             extras["p2p_send_GBps"] = pm.as_dict()
             if pm.errors:
                 verified = False
-        tuned = None
         if not args.no_xgmi and n <= 8:
-            # C2 knob sweep first: blocks per rank (16 .. 256) x one-/two-shot at 6
-            # sizes up to 256 MiB (capped by free HBM), the favoured one-shot cutoff
-            # and the best single nblk (xgmi.tune; ~5-10 s at N = 8, bounded by
-            # xgmi.TUNE_BUDGET_S). The main sweep below then runs THAT
-            # configuration. The rehearsal runs both over torch.distributed to pin
-            # the JSON shape and the hand-over.
+            # C2 next to RCCL, on ONE communicator for the knob sweep and the main
+            # sweep (xgmi.c2_sweep: 3 IPC exports per rank in all, a collective
+            # signal reset per blocks-per-rank value). First the knob sweep: blocks
+            # per rank (16 .. 256) x one-/two-shot at 6 sizes up to 256 MiB (capped
+            # by free HBM), the favoured one-shot cutoff and the best single nblk
+            # (~5-10 s at N = 8, bounded by xgmi.TUNE_BUDGET_S); then the RCCL bf16
+            # sizes from 512 B to 1 GiB that split into 8-element chunks per rank,
+            # in place on the registered buffer, no host sync / barrier / staging
+            # per call, in the tuned configuration (the defaults if the tune
+            # failed). The rehearsal runs both over torch.distributed to pin the
+            # JSON shape and the hand-over.
             from nvidia_terraform_modules_amd.parallel import xgmi as xg
 
+            xs = [b for b in coll.sweep_sizes(8, max_b, 4)
+                  if 512 <= b <= 1 << 30 and (b // 2) % (8 * n) == 0]
             fac = None
             if args.rehearsal:
                 fac = lambda nb, mb: xg.ReferenceAllReduce(env, mb, nblk=nb)  # noqa: E731
-            t_tune = time.perf_counter()
-            try:
-                tuned = xg.tune(env, factory=fac, max_bytes=max_b)
-                tuned["seconds"] = round(time.perf_counter() - t_tune, 2)
-                extras["xgmi_tune"] = tuned
-                if tuned["errors"] or tuned["timed_out"]:
-                    verified = False
-            except Exception as e:  # noqa: BLE001 - recorded; the main sweep still runs
-                extras["xgmi_tune"] = {"error": f"{type(e).__name__}: {e}"[:300]}
-                tuned = None
-        if not args.no_xgmi and n <= 8:
-            # C2 next to RCCL: the same sizes, in place on the registered buffer,
-            # no host sync / barrier / staging per call (device-side barriers),
-            # in the tuned configuration (the defaults if the tune failed).
-            # Set-up failures (IPC, peer mapping) are agreed on collectively so no
-            # rank is left waiting in a collective the others skipped; the JSON
-            # line still comes out with the error recorded.
-            from nvidia_terraform_modules_amd.parallel import xgmi as xg
-
-            nblk, cut, src = 64, 256 << 10, "default"
-            if tuned and not tuned["errors"] and not tuned["timed_out"]:
-                nblk, cut, src = tuned["best_nblk"], tuned["best_one_shot_max_bytes"], "xgmi_tune"
-            # the RCCL bf16 sizes from 512 B to 1 GiB (so the two can be paired) that
-            # split into 8-element chunks per rank
-            xs = [b for b in coll.sweep_sizes(8, max_b, 4)
-                  if 512 <= b <= 1 << 30 and (b // 2) % (8 * n) == 0]
-            ar, err = None, ""
-            try:
-                if args.rehearsal:
-                    ar = xg.ReferenceAllReduce(env, max(xs), nblk=nblk, one_shot_max_bytes=cut)
-                else:
-                    ar = xg.XgmiAllReduce(env, max_bytes=max(xs), nblk=nblk, one_shot_max_bytes=cut)
-            except Exception as e:  # noqa: BLE001 - reported, and agreed on below
-                err = f"{type(e).__name__}: {e}"[:300]
-            if dist.all_reduce_max(env, 1.0 if err else 0.0) > 0:
-                extras["xgmi_error"] = err or "set-up failed on another rank"
+            c2, xr = xg.c2_sweep(env, xs, max_b, factory=fac)
+            if not c2.pop("ok"):
                 verified = False
-                if ar is not None:
-                    ar.close(sync_peers=False)  # peers without a communicator do not call
-            else:
-                xr = coll.all_reduce_sweep(env, xs, dtype="bf16", iters=10, warmup=2, impl=ar)
-                extras["xgmi_allreduce_bf16"] = [
-                    {"bytes": r.bytes, "time_us": round(r.time_us, 1),
-                     "busbw_GBps": round(r.busbw_GBps, 1), "errors": r.errors} for r in xr]
-                extras["xgmi_peak_busbw_GBps"] = coll.peak_busbw(xr)
+            extras.update(c2)
+            if xr:
                 extras["xgmi_vs_rccl_bf16"] = pair_busbw(res, xr)
-                extras["xgmi_blocks_per_rank"] = ar.nblk
-                extras["xgmi_one_shot_max_bytes"] = ar.one_shot_max_bytes
-                extras["xgmi_config_source"] = src
-                extras["xgmi_timed_out"] = dist.all_reduce_max(
-                    env, 1.0 if ar.timed_out() else 0.0) > 0
-                ar.close()
-                if any(r.errors for r in xr) or extras["xgmi_timed_out"]:
-                    verified = False
     _CLOCK.mark("collectives_checked")
 
     if (gpu_extras or args.rehearsal) and not args.no_job:
@@ -577,6 +622,13 @@ def main(argv=None) -> int:
         # workgroup clock (every XCD gets the same tiles, so it finishes last);
         # the all-workgroup median beside it, and the per-XCD spread
         "per_rank_gemm_clock_GHz": [(p["gemm_clock"] or {}).get("bound_GHz") for p in per_rank],
+        # stamped batches it took to get one whose per-launch windows agree within 3 %
+        # (kernels.gemm_clock_stable), and whether that batch ran at the timed loop's
+        # pace (ms per stamped launch / timed ms per step within 0.95-1.05)
+        "per_rank_clock_batches": [(p["gemm_clock"] or {}).get("clock_batches") for p in per_rank],
+        "per_rank_clock_trusted": [(p["gemm_clock"] or {}).get("clock_trusted") for p in per_rank],
+        # host time of every AMD SMI read per rank (init, window opens / closes), ms
+        "per_rank_smi_sample_ms": [p["smi_ms"] for p in per_rank],
         "per_rank_gemm_clock_median_GHz": [(p["gemm_clock"] or {}).get("launch_GHz")
                                            for p in per_rank],
         "per_rank_xcd_clock_spread_pct": [(p["gemm_clock"] or {}).get("xcc_clock_spread_pct")

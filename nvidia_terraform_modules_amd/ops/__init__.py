@@ -11,7 +11,8 @@ K2 ``stream_copy``, ``stream_read`` - tuned float4 HBM streams.
 K3 ``fill_uniform_``, ``ref_gemm_f32``, ``verify_bf16``, ``abft_check`` - synthetic
    data, full fp32 reference check and the O(n^2) checksum check;
    ``clock_probe_ghz`` - the shader clock held under a dense MFMA load;
-   ``gemm_clock_ghz`` - the clock K1's own 8192^3-class launches run at.
+   ``gemm_clock_ghz`` - the clock K1's own 8192^3-class launches run at
+   (``gemm_clock_stable``: the same, re-stamped until a batch is transient-free).
 
 Import is cheap; the native library is loaded on first kernel call and raises
 ``NativeLibraryMissing`` if it was not built (no silent fallback).
@@ -27,6 +28,7 @@ from .kernels import (  # noqa: F401
     gemm_bf16_rowsum,
     clock_summary,
     gemm_clock_ghz,
+    gemm_clock_stable,
     gemm_fp8,
     gemm_fp8_rowsum,
     gemm_fp8_shape_ok,

@@ -18,6 +18,7 @@ xgmi_allreduce.hpp):
 from __future__ import annotations
 
 import ctypes
+import time
 
 import torch
 
@@ -126,6 +127,18 @@ class XgmiAllReduce:
     copies (still no host sync). Messages up to ``one_shot_max_bytes`` take the
     one-shot kernel (one read pass over all peers, 2 barriers instead of 3).
 
+    One set-up per lifetime: the three buffers are allocated
+    and exported ONCE; the signal area is sized for ``max_nblk`` blocks per
+    rank (default: the largest of ``TUNE_NBLKS`` and ``nblk``), so
+    :meth:`reconfigure` changes blocks per rank and the one-shot cutoff in
+    place - a collective signal reset, no new export or import. ``tune`` and
+    bench's main C2 sweep share one communicator: 3 ``ntm_ipc_handle`` calls
+    per rank in all (``exports``), where round 5 made six set-up/teardown
+    cycles. ``export_retries`` counts refused exports (kept as a guard only);
+    ``setup_report`` holds every rank's refusals and, for each, whether the
+    refused range overlaps one this process exported before and has since
+    freed (the "peer has not finished releasing it" hypothesis).
+
     Failure contract: the device-side barriers are bounded (``spin_limit`` /
     ``entry_spin_limit``, 0 = the kernel defaults). The entry barrier waits
     up to ~16x longer than the in-kernel phases (it absorbs host skew between
@@ -137,10 +150,14 @@ class XgmiAllReduce:
     ``run(..., check=True)`` / ``ar(t, check=True)`` synchronise and raise on a
     timeout; otherwise poll :meth:`timed_out` (or call
     :meth:`raise_if_timed_out`) at a convenient sync point.
+
+    ``lib`` replaces the native library (tests: a host-memory stub that counts
+    exports); the default is libntm_validation.so.
     """
 
     def __init__(self, env, max_bytes: int, nblk: int = 64, one_shot_max_bytes: int = 256 << 10,
-                 spin_limit: int = 0, entry_spin_limit: int = 0):
+                 spin_limit: int = 0, entry_spin_limit: int = 0, max_nblk: int | None = None,
+                 lib=None):
         from .dist import all_gather_obj
 
         if env.world_size > MAX_RANKS:
@@ -148,24 +165,34 @@ class XgmiAllReduce:
         if not 1 <= nblk <= 1024:
             raise ValueError("nblk must be in 1..1024")
         self.env, self.nblk, self.max_bytes = env, nblk, max_bytes
+        self.max_nblk = max(nblk, max_nblk if max_nblk is not None else max(TUNE_NBLKS))
+        if self.max_nblk > 1024:
+            raise ValueError("max_nblk must be <= 1024")
         self.one_shot_max_bytes = min(one_shot_max_bytes, max_bytes)
         self.spin_limit, self.entry_spin_limit = spin_limit, entry_spin_limit
-        self.L = L = _declare()
-        self._own, self._opened = [], []
+        self.L = L = lib if lib is not None else _declare()
+        self._own, self._opened, self._refused = [], [], []
+        self._sizes: dict[int, int] = {}
+        self._exported_sig = 0
+        self.exports, self.export_retries, self.reconfigures = 0, 0, 0
+        self.refusals: list[dict] = []
+        self._sig_bytes = int(L.ntm_xgmi_signal_bytes(self.max_nblk))
         # Collective-safe set-up: every rank reaches both all_gathers whatever
         # fails locally, and all ranks raise together, so no rank is left
         # waiting in a collective its peers abandoned.
         handles, err = {}, ""
         try:
             for name, nbytes, uncached in (("in", max_bytes, 0), ("out", max_bytes, 0),
-                                           ("sig", L.ntm_xgmi_signal_bytes(nblk), 1)):
-                handles[name] = _alloc_exported(L, nbytes, uncached, self._own)
-            check(L.ntm_memset_async(handles["sig"][0], 0, L.ntm_xgmi_signal_bytes(nblk), None),
-                  "memset")
-            torch.cuda.synchronize()
+                                           ("sig", self._sig_bytes, 1)):
+                handles[name] = self._export(nbytes, uncached)
+            self._zero_signals()
         except Exception as e:  # noqa: BLE001 - re-raised on every rank below
             err = f"rank {env.rank}: {e}"
-        gathered = all_gather_obj(env, {"err": err, "h": {k: v[1] for k, v in handles.items()}})
+        gathered = all_gather_obj(env, {"err": err, "h": {k: v[1] for k, v in handles.items()},
+                                        "refusals": self.refusals})
+        self.setup_report = {"exports_per_rank": 3,
+                             "refusals": [dict(r, rank=i) for i, g in enumerate(gathered)
+                                          for r in g["refusals"]]}
         self._raise_if_any([g["err"] for g in gathered])
         self.ptrs = {"in": [], "out": [], "sig": []}
         try:
@@ -181,21 +208,94 @@ class XgmiAllReduce:
         except Exception as e:  # noqa: BLE001
             err = f"rank {env.rank}: {e}"
         self._raise_if_any(all_gather_obj(env, err))
+        # every export of this communicator succeeded: the ranges refused on the
+        # way go back to the allocator (round 5 kept them until close)
+        for p in self._refused:
+            self._own.remove(p)
+            L.ntm_free(p)
+        self._refused = []
         self.epoch = 0
         self.err = torch.zeros(1, dtype=torch.int32, device=env.device)
+
+    # ---- set-up helpers ---------------------------------------------------------------------
+    def _sync(self) -> None:
+        if self.env.device.type == "cuda":
+            torch.cuda.synchronize(self.env.device)
+
+    def _stream(self):
+        return stream_handle() if self.env.device.type == "cuda" else None
+
+    def _export(self, nbytes: int, uncached: int) -> tuple:
+        p, h = _alloc_exported(self.L, nbytes, uncached, self._own, self)
+        return p, h
+
+    def _zero_signals(self) -> None:
+        check(self.L.ntm_memset_async(self._sig_ptr_local(), 0, self._sig_bytes, None), "memset")
+        self._sync()
+
+    def _sig_ptr_local(self) -> int:
+        # during __init__ the pointer table does not exist yet: the signal area is
+        # this rank's third allocation that exported successfully
+        ptrs = getattr(self, "ptrs", None)
+        if ptrs and ptrs["sig"]:
+            return ptrs["sig"][self.env.rank]
+        return self._exported_sig
 
     def _raise_if_any(self, errs: list) -> None:
         errs = [e for e in errs if e]
         if errs:
-            self.close()
+            self.close()     # every rank reaches this together (after an all_gather)
             raise RuntimeError("XgmiAllReduce set-up failed: " + "; ".join(errs))
 
+    def reconfigure(self, nblk: int, one_shot_max_bytes: int | None = None) -> None:
+        """Change blocks per rank (and the one-shot cutoff) in place, with no new
+        IPC export or import. Collective: every rank calls with the same values.
+        Order: this rank's kernels drain, all ranks meet (so no peer still writes
+        into this rank's signal slots), each zeroes its own signal area, all ranks
+        meet again with their new configuration (so no peer's next-epoch store
+        lands before the zeroing, and a mismatch raises on every rank). Epochs keep
+        growing across it, so a slot left over from an earlier layout is always
+        below the next epoch even without the reset."""
+        from .dist import all_gather_obj, barrier
+
+        cut = self.one_shot_max_bytes if one_shot_max_bytes is None else one_shot_max_bytes
+        err = ""
+        if not 1 <= nblk <= self.max_nblk:
+            err = f"rank {self.env.rank}: nblk {nblk} outside 1..{self.max_nblk} (signal area)"
+        self._sync()
+        if self.env.world_size > 1:
+            barrier(self.env)
+        if not err:
+            try:
+                self._zero_signals()
+            except Exception as e:  # noqa: BLE001 - agreed on below
+                err = f"rank {self.env.rank}: {e}"
+        got = all_gather_obj(self.env, {"cfg": (nblk, min(cut, self.max_bytes)), "err": err})
+        errs = [g["err"] for g in got if g["err"]]
+        if not errs and len({tuple(g["cfg"]) for g in got}) != 1:
+            errs = [f"ranks disagree on (nblk, one_shot_max_bytes): {[g['cfg'] for g in got]}"]
+        if errs:
+            raise RuntimeError("XgmiAllReduce.reconfigure failed: " + "; ".join(errs))
+        self.nblk, self.one_shot_max_bytes = nblk, min(cut, self.max_bytes)
+        self.reconfigures += 1
+
+    def stats(self) -> dict:
+        """Set-up accounting for the bench JSON (this rank)."""
+        return {"exports": self.exports, "export_retries": self.export_retries,
+                "reconfigures": self.reconfigures, "max_nblk": self.max_nblk,
+                "refusals": self.refusals}
+
+    # ---- calls ------------------------------------------------------------------------------
     def buffer(self, numel: int) -> torch.Tensor:
         """bf16 view of the first ``numel`` elements of this rank's registered
         buffer (the in-place operand of :meth:`run`)."""
         if numel * 2 > self.max_bytes:
             raise ValueError("numel exceeds max_bytes")
-        arr = _DeviceArray(self.ptrs["in"][self.env.rank], numel)
+        ptr = self.ptrs["in"][self.env.rank]
+        if self.env.device.type != "cuda":   # host-memory stub library (tests)
+            raw = (ctypes.c_char * (numel * 2)).from_address(ptr)
+            return torch.frombuffer(raw, dtype=torch.bfloat16)
+        arr = _DeviceArray(ptr, numel)
         return torch.as_tensor(arr, device=self.env.device).view(torch.bfloat16)
 
     def _check_count(self, count: int) -> None:
@@ -211,8 +311,14 @@ class XgmiAllReduce:
         rc = self.L.ntm_xgmi_allreduce_bf16_ex(
             _ptrs(self.ptrs["in"]), _ptrs(out), _ptrs(self.ptrs["sig"]), n,
             self.env.rank, 1, self.nblk, count, self.epoch, self.err.data_ptr(),
-            1 if one_shot else 0, self.spin_limit, self.entry_spin_limit, stream_handle())
+            1 if one_shot else 0, self.spin_limit, self.entry_spin_limit, self._stream())
         check(rc, "ntm_xgmi_allreduce_bf16")
+
+    def _copy(self, dst: int, src: int, nbytes: int) -> None:
+        """Stream-ordered device->device copy through the native stream kernel."""
+        if nbytes % 16:
+            raise ValueError("sizes must be 16-byte multiples")
+        check(self.L.ntm_stream_copy(src, dst, nbytes, self._stream()), "ntm_stream_copy")
 
     def run(self, numel: int, check: bool = False) -> torch.Tensor:
         """Sum over ranks of ``buffer(numel)``, in place, stream-ordered.
@@ -220,7 +326,7 @@ class XgmiAllReduce:
         self._check_count(numel)
         if numel * 2 <= self.one_shot_max_bytes:
             self._launch(numel, one_shot=True)
-            _copy_d2d(self.ptrs["in"][self.env.rank], self.ptrs["out"][self.env.rank], numel * 2)
+            self._copy(self.ptrs["in"][self.env.rank], self.ptrs["out"][self.env.rank], numel * 2)
         else:
             self._launch(numel, one_shot=False)
         if check:
@@ -241,10 +347,10 @@ class XgmiAllReduce:
         if t.data_ptr() == mine:
             self.run(count, check=check)
             return t
-        _copy_d2d(mine, t.data_ptr(), nbytes)
+        self._copy(mine, t.data_ptr(), nbytes)
         one = nbytes <= self.one_shot_max_bytes
         self._launch(count, one_shot=one)
-        _copy_d2d(t.data_ptr(), self.ptrs["out" if one else "in"][self.env.rank], nbytes)
+        self._copy(t.data_ptr(), self.ptrs["out" if one else "in"][self.env.rank], nbytes)
         if check:
             self.raise_if_timed_out()
         return t
@@ -274,38 +380,55 @@ class XgmiAllReduce:
         hipIpcGetMemHandle fail ("invalid argument") on a rank whose new
         allocation reused a still-imported range (tune's back-to-back
         communicators at world 8). ``sync_peers=False`` only on error paths
-        where the peers may not all call close."""
+        where the peers may not all call close. Every freed exported range is
+        remembered (``_FREED_EXPORTS``) so a later refusal can be matched to it."""
         from .dist import barrier
 
-        torch.cuda.synchronize()
+        self._sync()
         for p in self._opened:
             self.L.ntm_ipc_close(p)
         self._opened = []
         if sync_peers and self.env.world_size > 1:
             barrier(self.env)
+        now = time.monotonic()
         for p in self._own:
             self.L.ntm_free(p)
-        self._own = []
+            if p in self._sizes:
+                _FREED_EXPORTS.append((p, self._sizes[p], now))
+        self._own, self._refused = [], []
 
 
 EXPORT_ATTEMPTS = 5
+HIP_ERROR_INVALID_VALUE = 1
+
+# (pointer, bytes, monotonic time freed) of every exported range this process
+# has freed: a refused export is checked against it (the root-cause question of
+# VERDICT r5 #1 - is the refused range one a peer imported before?)
+_FREED_EXPORTS: list[tuple[int, int, float]] = []
 
 
-def _alloc_exported(L, nbytes: int, uncached: int, own: list) -> tuple:
+def _overlaps_freed_export(p: int, nbytes: int) -> dict:
+    now = time.monotonic()
+    for q, qn, t in reversed(_FREED_EXPORTS):
+        if p < q + qn and q < p + nbytes:
+            return {"overlaps_prev_export": True, "prev_export_ptr": hex(q),
+                    "freed_s_ago": round(now - t, 4)}
+    return {"overlaps_prev_export": False}
+
+
+def _alloc_exported(L, nbytes: int, uncached: int, own: list, comm=None) -> tuple:
     """Allocate ``nbytes`` and export its IPC handle: (pointer, 64 handle bytes).
 
     Every allocation goes into ``own`` (freed by close). hipIpcGetMemHandle can
-    refuse a fresh allocation with "invalid value" when the allocator handed
-    back a range whose previous export a peer process has not finished
-    releasing: the driver's dmabuf release runs after hipIpcCloseMemHandle and
-    the close barrier return (seen once at world 8, round 5, after round 4's
-    collective close made it rare). That allocation is kept, not freed, so a
-    retry gets a different range. A refused range was refused twice in a row
-    once (world 8, end of round 5), so there are EXPORT_ATTEMPTS tries, with a
-    short growing pause that lets the peers' releases land; the last refusal
-    is raised."""
-    import time
-
+    refuse a fresh allocation with "invalid value" (hipErrorInvalidValue, 1):
+    seen at world 8 in round 5 when back-to-back communicators reused ranges a
+    peer had imported; the single shared communicator of tune + the main sweep
+    removes that churn, and this retry stays as a guard. Only that code is
+    retried (any other is raised at once); a refused allocation is kept, not
+    freed, so the retry gets a different range, with a short growing pause.
+    ``comm`` (an XgmiAllReduce) counts exports and retries and records each
+    refusal with its attempt number and whether the refused range overlaps an
+    exported range this process freed earlier (_FREED_EXPORTS)."""
     last = 0
     for i in range(EXPORT_ATTEMPTS):
         if i:
@@ -315,29 +438,39 @@ def _alloc_exported(L, nbytes: int, uncached: int, own: list) -> tuple:
         own.append(p.value)
         h = ctypes.create_string_buffer(64)
         last = L.ntm_ipc_handle(p.value, h)
+        if comm is not None:
+            comm.exports += 1
         if last == 0:
+            if comm is not None:
+                comm._sizes[p.value] = nbytes
+                if uncached:
+                    comm._exported_sig = p.value
             return p.value, h.raw
+        if comm is not None:
+            comm.export_retries += 1
+            comm._refused.append(p.value)
+            comm.refusals.append({"attempt": i + 1, "code": int(last), "bytes": nbytes,
+                                  "ptr": hex(p.value), **_overlaps_freed_export(p.value, nbytes)})
+        if last != HIP_ERROR_INVALID_VALUE:
+            break
     check(last, "ntm_ipc_handle")
     raise AssertionError("unreachable")
 
 
-def _copy_d2d(dst: int, src: int, nbytes: int) -> None:
-    """Stream-ordered device->device copy through the native stream kernel."""
-    if nbytes % 16 == 0:
-        check(lib().ntm_stream_copy(src, dst, nbytes, stream_handle()), "ntm_stream_copy")
-    else:
-        raise ValueError("sizes must be 16-byte multiples")
-
-
 class ReferenceAllReduce:
     """The knob surface of :class:`XgmiAllReduce` (``nblk``,
-    ``one_shot_max_bytes``, ``timed_out``, ``close``) over
-    ``torch.distributed.all_reduce``: lets CPU/gloo rehearsals run
-    :func:`tune` end to end and pin its JSON shape. Not a measurement."""
+    ``one_shot_max_bytes``, ``reconfigure``, ``stats``, ``timed_out``,
+    ``close``) over ``torch.distributed.all_reduce``: lets CPU/gloo rehearsals
+    run :func:`tune` / :func:`c2_sweep` end to end and pin their JSON shape.
+    Not a measurement; it exports nothing."""
 
-    def __init__(self, env, max_bytes: int, nblk: int = 64, one_shot_max_bytes: int = 256 << 10):
+    def __init__(self, env, max_bytes: int, nblk: int = 64, one_shot_max_bytes: int = 256 << 10,
+                 max_nblk: int | None = None):
         self.env, self.nblk, self.max_bytes = env, nblk, max_bytes
+        self.max_nblk = max(nblk, max_nblk if max_nblk is not None else max(TUNE_NBLKS))
         self.one_shot_max_bytes = min(one_shot_max_bytes, max_bytes)
+        self.reconfigures = 0
+        self.setup_report = {"exports_per_rank": 0, "refusals": []}
 
     def __call__(self, t: torch.Tensor, check: bool = False) -> torch.Tensor:
         import torch.distributed as tdist
@@ -345,6 +478,20 @@ class ReferenceAllReduce:
         if self.env.world_size > 1:
             tdist.all_reduce(t)
         return t
+
+    def reconfigure(self, nblk: int, one_shot_max_bytes: int | None = None) -> None:
+        from .dist import all_gather_obj
+
+        cut = self.one_shot_max_bytes if one_shot_max_bytes is None else one_shot_max_bytes
+        got = all_gather_obj(self.env, (nblk, cut))
+        if len(set(got)) != 1 or not 1 <= nblk <= self.max_nblk:
+            raise RuntimeError(f"reconfigure: bad or disagreeing (nblk, cutoff): {got}")
+        self.nblk, self.one_shot_max_bytes = nblk, min(cut, self.max_bytes)
+        self.reconfigures += 1
+
+    def stats(self) -> dict:
+        return {"exports": 0, "export_retries": 0, "reconfigures": self.reconfigures,
+                "max_nblk": self.max_nblk, "refusals": []}
 
     def timed_out(self) -> bool:
         return False
@@ -356,11 +503,12 @@ class ReferenceAllReduce:
 # C2 knob sweep (the first 8-GPU run must say whether the
 # design or a constant is at fault, and run the tuned configuration). Sizes
 # reach the bandwidth regime (64 / 256 MiB) and blocks per rank one per CU.
-# Budget at N = 8: 5 communicators (one IPC set-up each, ~0.1-0.5 s) x 6
-# sizes x <= 2 algorithms x 12 calls (256 MiB two-shot: ~1-3 ms a call at
-# 200-600 GB/s busbw), plus one full-element check per point - ~5-10 s in all.
-# TUNE_BUDGET_S bounds it: once the slowest rank has spent that long, the
-# remaining nblk values are skipped (agreed collectively, recorded).
+# Budget at N = 8: ONE communicator (one IPC set-up, ~0.1-0.5 s, then a
+# collective signal reset per nblk) x 6 sizes x <= 2 algorithms x 12 calls
+# (256 MiB two-shot: ~1-3 ms a call at 200-600 GB/s busbw), plus one
+# full-element check per point - ~5-10 s in all. TUNE_BUDGET_S bounds it: once
+# the slowest rank has spent that long, the remaining nblk values are skipped
+# (agreed collectively, recorded).
 TUNE_SIZES = (64 << 10, 256 << 10, 1 << 20, 16 << 20, 64 << 20, 256 << 20)
 TUNE_NBLKS = (16, 32, 64, 128, 256)
 TUNE_CUTOFFS = (64 << 10, 256 << 10, 1 << 20)
@@ -369,7 +517,7 @@ TUNE_BUDGET_S = 30.0
 
 def tune(env, sizes=TUNE_SIZES, nblks=TUNE_NBLKS, cutoffs=TUNE_CUTOFFS, iters: int = 10,
          warmup: int = 2, factory=None, max_bytes: int | None = None,
-         budget_s: float = TUNE_BUDGET_S) -> dict:
+         budget_s: float = TUNE_BUDGET_S, ar=None, sweep=None) -> dict:
     """Sweep blocks per rank x algorithm (one-shot where a size is <= the
     largest cutoff, two-shot always) at each size, every element checked.
     Returns the full table, the best (nblk, algorithm) per size, the one-shot
@@ -378,41 +526,52 @@ def tune(env, sizes=TUNE_SIZES, nblks=TUNE_NBLKS, cutoffs=TUNE_CUTOFFS, iters: i
     sizes fastest (what the main sweep / a communicator should use).
     ``max_bytes`` drops larger sizes; ``budget_s`` stops after the nblk value
     during which the slowest rank passed it (collective decision).
-    ``factory(nblk, max_bytes)`` builds the communicator (default
-    :class:`XgmiAllReduce`); set-up is collective, so every rank must call."""
-    import time
 
+    ONE communicator serves every nblk (:meth:`XgmiAllReduce.reconfigure`): the
+    caller's ``ar`` (left open - bench's main sweep goes on with it), else one
+    built here by ``factory(nblk, max_bytes)`` (default :class:`XgmiAllReduce`,
+    signal area for ``max(nblks)``) and closed at the end. Set-up and
+    reconfigure are collective, so every rank must call. ``sweep`` replaces
+    ``collectives.all_reduce_sweep`` (tests)."""
     from .collectives import all_reduce_sweep
     from .dist import all_reduce_max
 
+    sweep = sweep or all_reduce_sweep
     if max_bytes is not None:
         sizes = tuple(s for s in sizes if s <= max_bytes)
     if not sizes:
         raise ValueError("no tune size fits max_bytes")
-    factory = factory or (lambda nb, mb: XgmiAllReduce(env, max_bytes=mb, nblk=nb))
     max_b = max(sizes)
+    own = ar is None
+    if own:
+        factory = factory or (lambda nb, mb: XgmiAllReduce(env, max_bytes=mb, nblk=nb,
+                                                           max_nblk=max(nblks)))
+        ar = factory(nblks[0], max_b)
+    elif ar.max_bytes < max_b:
+        raise ValueError("the shared communicator is smaller than the largest tune size")
     table, errors, timed_out = [], 0, False
     t0 = time.perf_counter()
     swept = []
-    for nb in nblks:
-        if swept and all_reduce_max(env, time.perf_counter() - t0) > budget_s:
-            break
-        swept.append(nb)
-        ar = factory(nb, max_b)
-        try:
+    try:
+        for nb in nblks:
+            if swept and all_reduce_max(env, time.perf_counter() - t0) > budget_s:
+                break
+            swept.append(nb)
+            ar.reconfigure(nb, 0)
             for size in sizes:
                 for algo in ("1shot", "2shot"):
                     if algo == "1shot" and size > max(cutoffs):
                         continue
+                    # rank-local and identical on every rank: which kernel each call runs
                     ar.one_shot_max_bytes = size if algo == "1shot" else 0
-                    r = all_reduce_sweep(env, [size], dtype="bf16", iters=iters, warmup=warmup,
-                                         impl=ar)[0]
+                    r = sweep(env, [size], dtype="bf16", iters=iters, warmup=warmup, impl=ar)[0]
                     errors += r.errors
                     table.append({"nblk": nb, "bytes": r.bytes, "algo": algo,
                                   "time_us": round(r.time_us, 2),
                                   "busbw_GBps": round(r.busbw_GBps, 2), "errors": r.errors})
             timed_out = timed_out or ar.timed_out()
-        finally:
+    finally:
+        if own:
             ar.close()
 
     def best(size, algos):
@@ -448,4 +607,72 @@ def tune(env, sizes=TUNE_SIZES, nblks=TUNE_NBLKS, cutoffs=TUNE_CUTOFFS, iters: i
             "best_one_shot_max_bytes": best_cut, "best_nblk": best_nblk,
             "cutoff_total_time_us": {str(c): round(v, 2) for c, v in score.items()},
             "nblk_total_time_us": {str(nb): round(v, 2) for nb, v in per_nblk.items()},
-            "budget_s": budget_s, "errors": errors, "timed_out": timed_out}
+            "budget_s": budget_s, "errors": errors, "timed_out": timed_out,
+            "shared_communicator": not own}
+
+
+def c2_sweep(env, main_sizes: list[int], tune_max_bytes: int, factory=None, iters: int = 10,
+             warmup: int = 2, tune_kwargs: dict | None = None, sweep=None) -> tuple[dict, list]:
+    """bench.py's C2 block at N > 1: the knob sweep (:func:`tune`) and then the
+    main sweep at ``main_sizes`` in the tuned configuration, on ONE
+    communicator (3 IPC exports per rank in all). Returns
+    (JSON keys, the main sweep's CollResults). Set-up failures are agreed on
+    collectively, so no rank is left waiting in a collective the others
+    skipped; the keys then carry the error. ``ok`` is False on any error,
+    element mismatch or device-barrier timeout."""
+    from .collectives import all_reduce_sweep, peak_busbw
+    from .dist import all_gather_obj, all_reduce_max
+
+    sweep = sweep or all_reduce_sweep
+    tune_kwargs = dict(tune_kwargs or {})
+    nblks = tuple(tune_kwargs.get("nblks", TUNE_NBLKS))
+    tune_sizes = [s for s in tune_kwargs.get("sizes", TUNE_SIZES) if s <= tune_max_bytes]
+    max_b = max(list(main_sizes) + tune_sizes)
+    factory = factory or (lambda nb, mb: XgmiAllReduce(env, max_bytes=mb, nblk=nb,
+                                                       max_nblk=max(nblks)))
+    out: dict = {"ok": True}
+    ar, err = None, ""
+    try:
+        ar = factory(64 if 64 in nblks else nblks[0], max_b)
+    except Exception as e:  # noqa: BLE001 - reported, and agreed on below
+        err = f"{type(e).__name__}: {e}"[:300]
+    if all_reduce_max(env, 1.0 if err else 0.0) > 0:
+        out.update(ok=False, xgmi_error=err or "set-up failed on another rank")
+        if ar is not None:
+            ar.close(sync_peers=False)   # peers without a communicator do not call
+        return out, []
+    tuned = None
+    try:
+        t_tune = time.perf_counter()
+        tuned = tune(env, max_bytes=tune_max_bytes, ar=ar, sweep=sweep, **tune_kwargs)
+        tuned["seconds"] = round(time.perf_counter() - t_tune, 2)
+        out["xgmi_tune"] = tuned
+        if tuned["errors"] or tuned["timed_out"]:
+            out["ok"] = False
+    except Exception as e:  # noqa: BLE001 - recorded; the main sweep still runs
+        out["xgmi_tune"] = {"error": f"{type(e).__name__}: {e}"[:300]}
+        tuned = None
+    nblk, cut, src = 64, 256 << 10, "default"
+    if tuned and not tuned["errors"] and not tuned["timed_out"]:
+        nblk, cut, src = tuned["best_nblk"], tuned["best_one_shot_max_bytes"], "xgmi_tune"
+    ar.reconfigure(nblk, cut)
+    xr = sweep(env, list(main_sizes), dtype="bf16", iters=iters, warmup=warmup, impl=ar)
+    st = all_gather_obj(env, ar.stats())
+    out.update({
+        "xgmi_allreduce_bf16": [{"bytes": r.bytes, "time_us": round(r.time_us, 1),
+                                 "busbw_GBps": round(r.busbw_GBps, 1), "errors": r.errors}
+                                for r in xr],
+        "xgmi_peak_busbw_GBps": peak_busbw(xr),
+        "xgmi_blocks_per_rank": ar.nblk, "xgmi_one_shot_max_bytes": ar.one_shot_max_bytes,
+        "xgmi_config_source": src,
+        "xgmi_timed_out": all_reduce_max(env, 1.0 if ar.timed_out() else 0.0) > 0,
+        # set-up accounting over ranks: one export per buffer per rank is the target
+        "xgmi_exports_per_rank": [s["exports"] for s in st],
+        "xgmi_export_retries": sum(s["export_retries"] for s in st),
+        "xgmi_reconfigures": st[0]["reconfigures"],
+        "xgmi_export_refusals": [dict(r, rank=i) for i, s in enumerate(st) for r in s["refusals"]],
+    })
+    ar.close()
+    if any(r.errors for r in xr) or out["xgmi_timed_out"]:
+        out["ok"] = False
+    return out, xr

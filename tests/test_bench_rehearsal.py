@@ -104,9 +104,16 @@ def test_torchrun_launch_one_json_line(nproc):
         assert tune["best_nblk"] in tune["nblks"]
         assert d["xgmi_config_source"] == "xgmi_tune"
         assert d["xgmi_blocks_per_rank"] == tune["best_nblk"]
-        assert d["xgmi_one_shot_max_bytes"] == min(tune["best_one_shot_max_bytes"],
-                                                   max(r["bytes"] for r in d["xgmi_allreduce_bf16"]))
+        # (the shared communicator is sized for the larger of the two sweeps)
+        comm_bytes = max([r["bytes"] for r in d["xgmi_allreduce_bf16"]] + tune["sizes"])
+        assert d["xgmi_one_shot_max_bytes"] == min(tune["best_one_shot_max_bytes"], comm_bytes)
         assert all(r["errors"] == 0 for r in d["xgmi_allreduce_bf16"])
+        # tune and the main sweep share ONE communicator (one
+        # reconfigure per swept nblk + the hand-over); set-up accounting per rank
+        assert tune["shared_communicator"] is True
+        assert d["xgmi_reconfigures"] == len(tune["nblks"]) + 1
+        assert d["xgmi_exports_per_rank"] == [0] * nproc     # the reference path exports nothing
+        assert d["xgmi_export_retries"] == 0 and d["xgmi_export_refusals"] == []
     if nproc > 1:
         assert all(r["errors"] == 0 for r in d["allreduce_bf16"] + d["allreduce_fp32"])
         assert d["allreduce_bf16"][0]["bytes"] == 8
@@ -167,6 +174,14 @@ def test_bench_on_one_gpu_json_contract(tmp_path):
     assert src == ("timed_loop" if pw["avg_power_W"] is not None and pw["seconds"] >= 0.1
                    else "steady_window")
     assert d["per_rank_avg_power_W"][0] == (pw if src == "timed_loop" else st)["avg_power_W"]
+    # every SMI read is timed, the stamped clock batch count is
+    # reported, and both kernels' energy per flop is measured
+    assert len(d["per_rank_smi_sample_ms"][0]) >= 5
+    assert 1 <= d["per_rank_clock_batches"][0] <= 3
+    assert 0.1 < d["k1_joules_per_tflop"] < 10 and 0.1 < d["hipblaslt_joules_per_tflop"] < 10
+    en = d["energy_rank0"]
+    assert en["order"] == ["k1", "hipblaslt", "hipblaslt", "k1"]
+    assert all(s >= 0.6 for s in en["k1"]["windows_s"] + en["hipblaslt"]["windows_s"]), en
     job = d["validation_job"]
     assert job["ran"] and job["passed"], job
     assert 0 < d["time_to_gpu_ready_in_node_s"] < 30
@@ -219,3 +234,66 @@ def test_power_window_samples_under_load():
     assert events[-1] == "sync" and events.index(samples[0]) == 0
     assert run["seconds"] >= 0.05 and run["launches"] >= 4
     assert before["host_ns"] < after["host_ns"]
+
+
+def test_energy_compare_abba_joules_per_tflop():
+    """bench.energy_compare: ABBA windows, each >= window_s of one
+    kernel, J/TFLOP = mean window power / that kernel's TF/s."""
+    sys.path.insert(0, str(ROOT))
+    import bench
+
+    t = [0.0]
+    cur = {"k": None}
+    power = {"a": 1400.0, "b": 1500.0}
+    energy = [0.0]
+
+    def mk(name):
+        def fn():
+            cur["k"] = name
+            t[0] += 0.001
+            energy[0] += power[name] * 0.001
+        return fn
+
+    def sample():
+        return {"host_ns": int(t[0] * 1e9), "energy_uj": int(energy[0] * 1e6)}
+
+    class Smi:
+        @staticmethod
+        def window(b, a):
+            from nvidia_terraform_modules_amd.ops import smi
+            return smi.window(b, a)
+
+    out = bench.energy_compare({"a": (mk("a"), 1600.0), "b": (mk("b"), 1500.0)},
+                               lambda: None, sample, Smi, window_s=0.01)
+    assert out["order"] == ["a", "b", "b", "a"]
+    assert out["a"]["avg_power_W"] == pytest.approx(1400.0, rel=1e-3)
+    assert out["a"]["joules_per_tflop"] == pytest.approx(1400 / 1600, rel=1e-3)
+    assert out["b"]["joules_per_tflop"] == pytest.approx(1.0, rel=1e-3)
+    assert out["a_over_b_joules_per_tflop"] == pytest.approx(0.875, rel=1e-3)
+    assert len(out["a"]["windows_W"]) == 2
+
+
+def test_gemm_clock_stable_restamps_a_drifting_batch(monkeypatch):
+    """kernels.gemm_clock_stable: a batch whose per-launch windows
+    drift > 3 % is stamped again (up to 3), each behind the pre-queued launches."""
+    from nvidia_terraform_modules_amd.ops import kernels
+
+    batches = iter([[640.0, 861.0, 664.0], [660.0, 668.0, 664.0], [600.0, 700.0, 650.0]])
+    calls = []
+
+    def fake(a, b, out=None, steps=1, prequeue=None, prequeue_launches=0):
+        calls.append(prequeue_launches)
+        return {"per_launch_window_us_median": next(batches), "bound_GHz": 1.6}
+
+    monkeypatch.setattr(kernels, "gemm_clock_ghz", fake)
+    r = kernels.gemm_clock_stable(None, None, steps=3, prequeue=lambda: None,
+                                  prequeue_launches=40)
+    assert r["clock_batches"] == 2 and r["clock_stable"] is True
+    assert r["per_launch_window_us_median"] == [660.0, 668.0, 664.0]
+    assert r["clock_batch_drift_pct"][0] > 30 and r["clock_batch_drift_pct"][1] < 3
+    assert calls == [40, 40]
+    # never stable: the least drifted of the 3 batches, flagged
+    batches = iter([[600.0, 700.0], [600.0, 640.0], [600.0, 900.0]])
+    r = kernels.gemm_clock_stable(None, None, steps=2, prequeue=lambda: None)
+    assert r["clock_batches"] == 3 and r["clock_stable"] is False
+    assert r["per_launch_window_us_median"] == [600.0, 640.0]

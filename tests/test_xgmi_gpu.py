@@ -122,6 +122,14 @@ def test_ipc_allreduce_processes(world):
 
         assert {t["nblk"] for t in tune["table"]} == {nb for nb in TUNE_NBLKS if nb * world <= 1024}
         assert tune["best_nblk"] in {t["nblk"] for t in tune["table"]}
+        # tune + main sweep on ONE communicator (3 exports per rank),
+        # after a first communicator was closed; no export refused on any rank
+        c2 = rep["c2"]
+        assert tune["shared_communicator"] is True and c2["ok"] is True, c2
+        assert c2["xgmi_exports_per_rank"] == [3] * world, c2
+        assert c2["xgmi_export_retries"] == 0, c2["xgmi_export_refusals"]
+        assert rep["first_comm"]["exports"] == 3 and rep["first_comm"]["export_retries"] == 0
+        assert all(x["errors"] == 0 for x in c2["xgmi_allreduce_bf16"])
 
 
 @pytest.mark.parametrize("one_shot", [False, True])

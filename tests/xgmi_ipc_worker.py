@@ -46,15 +46,22 @@ def main():
     for r in all_reduce_sweep(env, [512, 2048, 1 << 20], dtype="bf16", iters=3, warmup=1, impl=ar):
         results.append({"count": r.count, "wrong": r.errors, "timeout": ar.timed_out(),
                         "path": "bench_sweep", "busbw_GBps": r.busbw_GBps})
+    first = ar.stats()
     ar.close()
-    # bench.py's N > 1 knob sweep (nblk x one-shot / two-shot x cutoff), each
+    # bench.py's N > 1 C2 block exactly (xgmi.c2_sweep): the knob sweep (nblk x
+    # one-shot / two-shot x cutoff) and the main sweep on ONE communicator, each
     # point element-checked; on one GPU only the nblk whose blocks of all ranks
     # are co-resident
-    from nvidia_terraform_modules_amd.parallel.xgmi import TUNE_NBLKS, tune
-    tr = tune(env, sizes=(64 << 10, 1 << 20), nblks=[nb for nb in TUNE_NBLKS if nb * n <= 1024],
-              iters=2, warmup=1)
-    print(json.dumps({"rank": env.rank, "results": results,
-                      "tune": {k: tr[k] for k in ("table", "errors", "timed_out", "best_nblk")}}), flush=True)
+    from nvidia_terraform_modules_amd.parallel.xgmi import TUNE_NBLKS, c2_sweep
+    nblks = tuple(nb for nb in TUNE_NBLKS if nb * n <= 1024)
+    c2, _ = c2_sweep(env, [512, 2048, 1 << 20], 1 << 20, iters=2, warmup=1,
+                     tune_kwargs={"sizes": (64 << 10, 1 << 20), "nblks": nblks, "iters": 2,
+                                  "warmup": 1})
+    tr = c2["xgmi_tune"]
+    print(json.dumps({"rank": env.rank, "results": results, "first_comm": first,
+                      "c2": {k: v for k, v in c2.items() if k != "xgmi_tune"},
+                      "tune": {k: tr[k] for k in ("table", "errors", "timed_out", "best_nblk",
+                                                  "shared_communicator")}}), flush=True)
     shutdown(env)
 
 
