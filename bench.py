@@ -253,6 +253,37 @@ def run_validation_job(n: int, timeout_s: float = 240.0) -> dict:
     }
 
 
+SK_CHECK_SHAPE = (4152, 1096, 16056)
+
+
+def sk_product_check(backend, dev) -> dict:
+    """One default-dispatch launch of SK_CHECK_SHAPE (stream-K split mode on a
+    192-wide tile) under NTM_SK_CHECK=1, verified against the fp32 reference
+    kernel. Never raises: a placement violation or a wrong element is reported
+    as ok False."""
+    import torch
+
+    m, n, k = SK_CHECK_SHAPE
+    os.environ["NTM_SK_CHECK"] = "1"
+    res: dict = {"shape": [m, n, k]}
+    try:
+        res["variant"] = backend.k1_splitk_plan(m, n, k)[1]
+        a = backend.fill_uniform_(torch.empty((m, k), dtype=torch.bfloat16, device=dev), 9101)
+        b = backend.fill_uniform_(torch.empty((n, k), dtype=torch.bfloat16, device=dev), 9102)
+        try:
+            c = backend.gemm_bf16(a, b)
+            res["sk_xcc_error"] = 0
+        except backend.SkPlacementError as e:
+            res.update(ok=False, sk_xcc_error=str(e)[:200])
+            return res
+        atol, rtol = backend.gemm_tolerance(k)
+        rep = backend.verify_bf16(c, backend.ref_gemm_f32(a, b), atol, rtol)
+        res.update(bad=rep.bad, max_abs_err=rep.max_abs_err, ok=rep.ok)
+    except Exception as e:  # noqa: BLE001 - reported
+        res.update(ok=False, error=f"{type(e).__name__}: {e}"[:200])
+    return res
+
+
 def pair_busbw(rccl, xgmi) -> list:
     """C2 against RCCL at the message sizes both sweeps ran (bf16, in place,
     same timing loop): one row per shared size with both busbw and the ratio."""
@@ -455,6 +486,14 @@ def main(argv=None) -> int:
         extras["verify_rank0"] = rep.as_dict()
         extras["verify_bad_total"] = int(bad)
     _CLOCK.mark("gemm_verified")
+    if not args.no_check and dev.type == "cuda" and hasattr(backend, "sk_check_enabled"):
+        # stream-K placement check on the product path: the split-mode
+        # shape the default plan runs on a 192-wide tile, through the default
+        # dispatch with NTM_SK_CHECK=1 (a placement violation raises there), checked
+        # against the fp32 reference; the word is recorded per rank.
+        extras["sk_check_rank0"] = sk_product_check(backend, dev)
+        if not extras["sk_check_rank0"].get("ok"):
+            verified = False
 
     gpu_extras = not args.no_extras and not args.rehearsal
     if gpu_extras:

@@ -44,6 +44,9 @@ from .kernels import (  # noqa: F401
     set_plan_splitk,
     sk_ws_bytes,
     sk_xcc_error,
+    SkPlacementError,
+    set_sk_fault_inject,
+    sk_check_enabled,
     stream_copy,
     stream_read,
     verify_bf16,

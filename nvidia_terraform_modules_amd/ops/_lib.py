@@ -80,6 +80,9 @@ def _declare(lib: ctypes.CDLL) -> None:
         "ntm_gemm_bf16_clock_grid": ([c_int, c_int], c_int),
         "ntm_gemm_bf16_clock_words": ([], c_int),
         "ntm_sk_error_word_index": ([], c_int),
+        "ntm_set_sk_fault_inject": ([c_int], None),
+        "ntm_gemm_bf16_skh_ex": ([c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int,
+                                  c_vp, c_size, c_int, c_vp], c_int),
         "ntm_plan_cus": ([], c_int),
         "ntm_set_cus_override": ([c_int], None),
         "ntm_set_plan_pp_tiles": ([c_int], None),

@@ -301,6 +301,41 @@ def sk_xcc_error(device=None, clear: bool = True) -> int:
     return v
 
 
+class SkPlacementError(RuntimeError):
+    """A stream-K launch saw parts of a split tile on different XCDs: the
+    write-through / L1-only-acquire protocol's invariant broke, so C is not
+    trusted (gemm_bf16_sk.hpp). Raised by the default dispatch under
+    ``NTM_SK_CHECK=1`` (bench.py sets it; the validation Job checks the word
+    itself)."""
+
+
+def sk_check_enabled() -> bool:
+    """``NTM_SK_CHECK=1``: every stream-K launch of ``gemm_bf16`` reads (and
+    clears) this stream's placement error word afterwards and raises
+    :class:`SkPlacementError` when it is set. Costs one host sync per stream-K
+    launch, so it is opt-in; the plain 256x256 / small-tile paths are unaffected."""
+    import os
+
+    return os.environ.get("NTM_SK_CHECK", "0") not in ("", "0")
+
+
+def set_sk_fault_inject(on: bool = True) -> None:
+    """Fault injection for the placement check (tests): while on, the head /
+    slice 0 of every split tile claims a wrong XCC, so every stream-K launch
+    sets the error word. Process-wide."""
+    lib().ntm_set_sk_fault_inject(1 if on else 0)
+
+
+def _sk_checked(dev: torch.device, out: torch.Tensor) -> torch.Tensor:
+    if sk_check_enabled():
+        w = sk_xcc_error(dev, clear=True)
+        if w:
+            raise SkPlacementError(
+                f"stream-K placement violation (error word 0x{w:08x}: tile {(w >> 8) & 0xFFFF}, "
+                f"combiner XCC {(w >> 4) & 0xF}, other XCC {w & 0xF}); C is not trusted")
+    return out
+
+
 def _gemm_bf16_sk(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, rev: bool = False,
                   nopair: bool = False, sk_variant: str = "pingpong8s") -> torch.Tensor:
     """Stream-K (gemm_bf16_sk.hpp; sk_variant "pp192x256s" / "pp256x192s": split
@@ -317,7 +352,7 @@ def _gemm_bf16_sk(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, rev: bool
                                      out.data_ptr(), m, n, k, a.stride(0), b.stride(0),
                                      out.stride(0), ws.data_ptr(), wsb, stream_handle())
         check(rc, "ntm_gemm_bf16_skh")
-        return out
+        return _sk_checked(a.device, out)
     wsb = sk_ws_bytes(m, n, k)
     ws = _sk_workspace(a.device, wsb)
     fn = (lib_experimental().ntm_gemm_bf16_sk_rev if rev else
@@ -325,7 +360,7 @@ def _gemm_bf16_sk(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, rev: bool
     rc = fn(a.data_ptr(), b.data_ptr(), out.data_ptr(), m, n, k, a.stride(0), b.stride(0),
             out.stride(0), ws.data_ptr(), wsb, stream_handle())
     check(rc, "ntm_gemm_bf16_sk")
-    return out
+    return _sk_checked(a.device, out)
 
 
 def gemm_fp8_shape_ok(m: int, n: int, k: int) -> bool:

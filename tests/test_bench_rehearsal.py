@@ -174,6 +174,11 @@ def test_bench_on_one_gpu_json_contract(tmp_path):
     assert src == ("timed_loop" if pw["avg_power_W"] is not None and pw["seconds"] >= 0.1
                    else "steady_window")
     assert d["per_rank_avg_power_W"][0] == (pw if src == "timed_loop" else st)["avg_power_W"]
+    # the stream-K split-mode shape through the default dispatch under
+    # NTM_SK_CHECK=1, verified and with a clear placement word
+    sk = d["sk_check_rank0"]
+    assert sk["ok"] and sk["bad"] == 0 and sk["sk_xcc_error"] == 0, sk
+    assert sk["variant"] in ("pp192x256s", "pp256x192s")
     # every SMI read is timed, the stamped clock batch count is
     # reported, and both kernels' energy per flop is measured
     assert len(d["per_rank_smi_sample_ms"][0]) >= 5

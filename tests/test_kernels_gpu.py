@@ -969,3 +969,36 @@ def test_default_runs_split_mode_on_192_tiles(ops, m, n, k):
     assert torch.equal(ops.gemm_bf16(a, b), ops.gemm_bf16(a, b, variant=top))
     assert ops.sk_xcc_error() == 0
 
+
+
+@pytest.mark.parametrize("variant,m,n,k", [("default", 4152, 1096, 16056),   # skh, head/tail
+                                           ("pp192x256s", 1000, 1000, 4096),  # skh, 8 slices
+                                           ("pingpong8s", 4672, 1472, 6696),  # sks, head/tail
+                                           ("pingpong8s", 2048, 2048, 4096),   # sks, 4 slices
+                                           ("pingpong8s", 4608, 4352, 2048)])  # two-round mode
+def test_sk_placement_fault_raises_on_the_product_path(ops, monkeypatch, variant, m, n, k):
+    """with NTM_SK_CHECK=1 the dispatch reads and clears the
+    placement word after every stream-K launch; the injected wrong-XCC tag
+    (set_sk_fault_inject) makes it raise SkPlacementError, naming the tile. Off
+    again, the same call passes and the word is clear."""
+    if variant == "pingpong8s":
+        assert ops.sk_ws_bytes(m, n, k) > 0
+    a = _rand(ops, (m, k), 11)
+    b = _rand(ops, (n, k), 12)
+    monkeypatch.setenv("NTM_SK_CHECK", "1")
+    good = ops.gemm_bf16(a, b, variant=variant)          # no fault: no raise
+    ops.set_sk_fault_inject(True)
+    try:
+        with pytest.raises(ops.SkPlacementError, match="not trusted"):
+            ops.gemm_bf16(a, b, variant=variant)
+    finally:
+        ops.set_sk_fault_inject(False)
+    assert ops.sk_xcc_error() == 0                       # read and cleared by the raise
+    assert torch.equal(ops.gemm_bf16(a, b, variant=variant), good)
+    monkeypatch.setenv("NTM_SK_CHECK", "0")               # off: the word stays sticky, no raise
+    ops.set_sk_fault_inject(True)
+    try:
+        ops.gemm_bf16(a, b, variant=variant)
+    finally:
+        ops.set_sk_fault_inject(False)
+    assert ops.sk_xcc_error() != 0 and ops.sk_xcc_error() == 0

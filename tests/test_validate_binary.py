@@ -67,6 +67,11 @@ def test_binary_passes_and_writes_sidecar_outputs(tmp_path):
     assert rep["gpus"][0]["gemm_fp8_wrong"] == 0 and rep["gpus"][0]["gemm_fp8_tflops"] > 0
     assert rep["gpus"][0]["gemm_fp8_abft_bad_rows"] == 0
     assert rep["gpus"][0]["hbm_read_GBps"] > 1000
+    # the stream-K split-mode self-check ran on a 192-wide tile,
+    # matched the fp32 reference and left the placement error word zero
+    g0 = rep["gpus"][0]
+    assert g0["sk_split_variant"] in (54, 55) and g0["sk_split_wrong"] == 0, g0
+    assert g0["sk_xcc_error"] == 0 and 0 < g0["sk_split_ms"] < 50, g0
     assert rep["start_epoch_s"] > 1.6e9 and rep["end_epoch_s"] >= rep["start_epoch_s"]
     t = json.loads(term.read_text())
     assert t["passed"] is True and len(term.read_bytes()) < 4096
@@ -91,6 +96,26 @@ def test_binary_fault_injection_fails_loudly(tmp_path, kind, needle):
     rep = _last_json(out)
     assert not rep["passed"] and any(needle in f for f in rep["failures"])
     assert json.loads(term.read_text())["passed"] is False
+
+
+@pytest.mark.gpu
+def test_binary_sk_placement_fault_fails_the_job(tmp_path):
+    """NTM_FAULT_INJECT=sk_xcc makes the split-mode launch claim a
+    wrong XCC; the kernel's placement check sets the error word and the Job fails
+    (exit 1) naming it - with C still numerically right, so only the word can
+    catch it. The Job's verdict stays under 1 s at 1 GPU without the fault."""
+    _have_bin()
+    rc, out, _ = _run("--size", "1024", "--iters", "5", "--no-fp8",
+                      env={"NTM_FAULT_INJECT": "sk_xcc"})
+    rep = _last_json(out)
+    assert rc == 1 and not rep["passed"]
+    g0 = rep["gpus"][0]
+    assert g0["sk_xcc_error"] & 0x80000000, g0
+    assert any("different XCDs" in f for f in rep["failures"]), rep["failures"]
+    rc, out, _ = _run("--gpus", "1", "--size", "8192", "--iters", "10")
+    rep = _last_json(out)
+    assert rc == 0 and rep["gpus"][0]["sk_xcc_error"] == 0
+    assert rep["phases_s"]["end"] < 1.0, rep["phases_s"]
 
 
 @pytest.mark.gpu

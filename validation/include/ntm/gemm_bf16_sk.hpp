@@ -90,7 +90,17 @@ struct SkArgs {
   int ntiles;
   int S = 0;      // split mode (at most half a round of tiles): K slices per tile, else 0
   unsigned long long* stamps = nullptr;  // STAMP builds: 16 per workgroup
+  // fault injection (tests, the Job's self-check): the head / slice 0 of every
+  // split tile claims XCC_ID ^ fault, so every placement check fails; 0 = off
+  unsigned fault = 0;
 };
+
+// Process-wide fault-injection value the launchers copy into SkArgs::fault
+// (ntm_set_sk_fault_inject; host only).
+inline unsigned& sk_fault_inject() {
+  static unsigned v = 0;
+  return v;
+}
 
 // Tiles, pairs and the whole-tile prefix for (M, N, K) on `cus` CUs.
 // Two-round mode (S = 0): more tiles than CUs, not a multiple of them.
@@ -375,7 +385,8 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_sk_kernel(GemmArgs p, S
       const unsigned arrive = tail ? 4u : 1u, written = arrive << 1;
       const unsigned other_written = tail ? 2u : 8u;
       // this part's XCC tag rides on its first counter add
-      const unsigned tag = (my_xcc + 1u) << (tail ? kTailTagShift : kHeadTagShift);
+      const unsigned me = tail ? my_xcc : my_xcc ^ s.fault;
+      const unsigned tag = (me + 1u) << (tail ? kTailTagShift : kHeadTagShift);
       // the part this segment order runs first (the head; REV: the tail) writes
       // without looking: the other part has almost never written yet
       const bool writer = REV ? tail : head;
@@ -387,8 +398,8 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_sk_kernel(GemmArgs p, S
       if (o & other_written) {
         // the other part's first add (which carried its tag) precedes its WRITTEN
         const unsigned other_xcc = ((o >> (tail ? kHeadTagShift : kTailTagShift)) & 0xFFu) - 1u;
-        if (other_xcc != my_xcc)
-          report_xcc_error(s.cnt, (unsigned)(slot & 0xFFFF) << 8 | (my_xcc & 0xF) << 4 |
+        if (other_xcc != me)
+          report_xcc_error(s.cnt, (unsigned)(slot & 0xFFFF) << 8 | (me & 0xF) << 4 |
                                       (other_xcc & 0xF));
         acquire_all();
         add_partial(other, acc);
@@ -461,7 +472,7 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_sks_kernel(GemmArgs p, 
     const bool tail = slice == 1;
     const unsigned arrive = tail ? 4u : 1u, written = arrive << 1;
     const unsigned other_written = tail ? 2u : 8u;
-    const unsigned xc = xcc_id();
+    const unsigned xc = xcc_id() ^ (tail ? 0u : s.fault);
     const unsigned tag = (xc + 1u) << (tail ? kTailTagShift : kHeadTagShift);
     float* mine = part + (tail ? kPartialBytes / 4 : 0);
     const float* other = part + (tail ? 0 : kPartialBytes / 4);
@@ -483,7 +494,7 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_sks_kernel(GemmArgs p, 
   }
   write_partial(part + (size_t)slice * (kPartialBytes / 4), acc);
   // count (bits 0-7) + XCC id (8-15) + its square (16-31): S <= 8 parts, id < 16
-  const unsigned xc = xcc_id();
+  const unsigned xc = xcc_id() ^ (slice == 0 ? s.fault : 0u);
   const unsigned tag = 1u + (xc << 8) + ((xc * xc) << 16);
   const unsigned o = counter_add<true>(cnt, tag, bcast);
   if ((o & 0xFFu) != (unsigned)(s.S - 1)) return;  // uniform
@@ -517,6 +528,7 @@ inline hipError_t launch_gemm_bf16_sk(const GemmArgs& a, int cus, void* ws, size
   s.ws = (float*)ws;
   s.cnt = (unsigned*)ws;
   s.stamps = stamps;
+  s.fault = sk_fault_inject();
   if (STAMP && stamps == nullptr) return hipErrorInvalidValue;
   const dim3 g((unsigned)s.G), blk(kThreads);
   if (s.S >= 2) {  // split mode (REV / STAMP do not apply)

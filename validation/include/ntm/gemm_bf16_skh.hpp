@@ -132,7 +132,7 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_sksh_kernel(GemmArgs p,
     const bool tail = slice == 1;
     const unsigned arrive = tail ? 4u : 1u, written = arrive << 1;
     const unsigned other_written = tail ? 2u : 8u;
-    const unsigned xc = xcc_id();
+    const unsigned xc = xcc_id() ^ (tail ? 0u : s.fault);
     const unsigned tag = (xc + 1u) << (tail ? kTailTagShift : kHeadTagShift);
     float* mine = part + (tail ? kPartialBytes / 4 : 0);
     const float* other = part + (tail ? 0 : kPartialBytes / 4);
@@ -153,7 +153,7 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_sksh_kernel(GemmArgs p,
     return;
   }
   write_partial_h<AH, BH>(part + (size_t)slice * (kPartialBytes / 4), acc);
-  const unsigned xc = xcc_id();
+  const unsigned xc = xcc_id() ^ (slice == 0 ? s.fault : 0u);
   const unsigned tag = 1u + (xc << 8) + ((xc * xc) << 16);
   const unsigned o = counter_add<true>(cnt, tag, bcast);
   if ((o & 0xFFu) != (unsigned)(s.S - 1)) return;  // uniform
@@ -172,7 +172,7 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_sksh_kernel(GemmArgs p,
 // mode on this tile does not serve (M, N, K).
 template <int AH, int BH>
 inline hipError_t launch_gemm_bf16_skh(const GemmArgs& a, int cus, void* ws, size_t ws_bytes,
-                                       hipStream_t stream) {
+                                       hipStream_t stream, int fault = -1) {
   using G = Geo<AH, BH>;
   SkArgs s;
   if (!shape_ok_sk(a.M, a.N, a.K) || a.rowsum || a.lda < a.K || a.ldb < a.K || a.ldc < a.N ||
@@ -182,6 +182,7 @@ inline hipError_t launch_gemm_bf16_skh(const GemmArgs& a, int cus, void* ws, siz
     return hipErrorInvalidValue;
   s.ws = (float*)ws;
   s.cnt = (unsigned*)ws;
+  s.fault = fault < 0 ? sk_fault_inject() : (unsigned)fault;  // -1: the process-wide value
   const dim3 g((unsigned)s.G), blk(kThreads);
   const bool pair = s.S == 2;
   if (a.K % (2 * BK)) {

@@ -651,6 +651,10 @@ NTM_API int ntm_gemm_bf16_splitk(int variant, int splits, const void* A, const v
 // (gemm_bf16_sk.hpp kErrWord): nonzero after a launch in which some part of a
 // split tile ran on a different XCD than the part that combined it.
 NTM_API int ntm_sk_error_word_index() { return ntm::gemmsk::kErrWord; }
+// Fault injection for that check (tests, the Job's self-check): nonzero makes the
+// head / slice 0 of every split tile claim XCC_ID ^ v, so every stream-K launch
+// after this call sets the error word. Process-wide; 0 = off.
+NTM_API void ntm_set_sk_fault_inject(int v) { ntm::gemmsk::sk_fault_inject() = (unsigned)v; }
 
 // The CU count the plan and the persistent / stream-K launches use, and a test
 // override of it (0 = the device's own; host only: a CPU test of the plan on
@@ -713,6 +717,30 @@ NTM_API int ntm_gemm_bf16_skh(int variant, const void* A, const void* B, void* C
     return (int)ntm::gemmskh::launch_gemm_bf16_skh<64, 128>(a, cus, ws, ws_bytes, S(stream));
   if (variant == kStreamKPp256x192)
     return (int)ntm::gemmskh::launch_gemm_bf16_skh<128, 64>(a, cus, ws, ws_bytes, S(stream));
+  return (int)hipErrorInvalidValue;
+}
+
+// ntm_gemm_bf16_skh with this launch's own fault-injection value (the Job runs
+// one thread per GPU and corrupts only the last GPU's launch; -1 = the
+// process-wide ntm_set_sk_fault_inject value).
+NTM_API int ntm_gemm_bf16_skh_ex(int variant, const void* A, const void* B, void* C, int M, int N,
+                                 int K, int lda, int ldb, int ldc, void* ws, size_t ws_bytes,
+                                 int fault, void* stream) {
+  ntm::gemm::GemmArgs a;
+  a.A = (const __bf16*)A;
+  a.B = (const __bf16*)B;
+  a.C = (__bf16*)C;
+  a.M = M;
+  a.N = N;
+  a.K = K;
+  a.lda = lda;
+  a.ldb = ldb;
+  a.ldc = ldc;
+  const int cus = ntm::gemm6::pp6_grid(1 << 30);
+  if (variant == kStreamKPp192x256)
+    return (int)ntm::gemmskh::launch_gemm_bf16_skh<64, 128>(a, cus, ws, ws_bytes, S(stream), fault);
+  if (variant == kStreamKPp256x192)
+    return (int)ntm::gemmskh::launch_gemm_bf16_skh<128, 64>(a, cus, ws, ws_bytes, S(stream), fault);
   return (int)hipErrorInvalidValue;
 }
 

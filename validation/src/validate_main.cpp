@@ -71,6 +71,11 @@ int ntm_abft_check_fp8(const void*, const void*, const void*, const float*, int,
 int ntm_xgmi_allreduce_bf16(const void* const*, void* const*, unsigned* const*, int, int,
                             int, int, size_t, unsigned, unsigned*, int, void*);
 size_t ntm_xgmi_signal_bytes(int);
+int ntm_k1_plan_splitk(int, int, int, int*, int*, int*, int*);
+size_t ntm_skh_ws_bytes(int, int, int, int);
+int ntm_gemm_bf16_skh_ex(int, const void*, const void*, void*, int, int, int, int, int, int, void*,
+                         size_t, int, void*);
+int ntm_sk_error_word_index();
 }
 
 namespace {
@@ -146,8 +151,9 @@ void usage() {
                "       [--termination-log FILE] [--prom-out FILE] [--fault-inject KIND]\n"
                "       [--pushgateway http://host:port]\n"
                "fault-inject (also env NTM_FAULT_INJECT): corrupt_gemm | corrupt_abft |\n"
-               "       corrupt_fp8 | corrupt_fp8_abft | corrupt_p2p | corrupt_allreduce - corrupts\n"
-               "       the LAST GPU's data to prove detection\n");
+               "       corrupt_fp8 | corrupt_fp8_abft | corrupt_p2p | corrupt_allreduce | sk_xcc -\n"
+               "       corrupts the LAST GPU's data (sk_xcc: its stream-K launch claims a wrong\n"
+               "       XCD) to prove detection\n");
 }
 
 bool parse(int argc, char** argv, Opts& o) {
@@ -281,10 +287,71 @@ struct GpuResult {
   unsigned long long fp8_bad = ~0ull;  // stays ~0 when --no-fp8
   float fp8_max_err = NAN;
   unsigned long long fp8_abft_bad = ~0ull;  // rows failing the fp8 fused checksum (~0: not run)
+  // stream-K split mode self-check (kSkM x kSkN x kSkK on a 192-wide tile)
+  int sk_variant = 0;                    // 54 / 55 (0: not served on this device)
+  unsigned long long sk_bad = ~0ull;     // elements off the fp32 reference (~0: not run)
+  unsigned sk_word = 0;                  // the workspace's XCD-placement error word
+  double sk_ms = 0;
   double hbm_copy_gbps = 0, hbm_read_gbps = 0;
   bool hbm_copy_ok = false;
   double t_init = 0, t_gemm = 0, t_hbm = 0;
 };
+
+// The split-mode self-check shape: 48 x 5 of 192x256 tiles, half a round on
+// 256 CUs, so each tile is cut into K slices combined through the workspace (the
+// ragged shape round 5 moved from 0.82-0.89 to 1.03 of hipBLASLt).
+constexpr int kSkM = 4152, kSkN = 1096, kSkK = 16056;
+
+bool run_sk_check(int dev, bool last, const Opts& o, hipStream_t s, void* V, GpuResult& r) {
+  int top = 0, tv = 0, rest = 0, sp = 0;
+  int variant = 0;
+  if (ntm_k1_plan_splitk(kSkM, kSkN, kSkK, &top, &tv, &rest, &sp) == 0 &&
+      (tv == 54 || tv == 55) && ntm_skh_ws_bytes(tv, kSkM, kSkN, kSkK) > 0)
+    variant = tv;  // what the default dispatch runs for this shape
+  for (int v : {54, 55})
+    if (!variant && ntm_skh_ws_bytes(v, kSkM, kSkN, kSkK) > 0) variant = v;
+  if (!variant) return true;  // a partition with other CU counts: not served, not run
+  r.sk_variant = variant;
+  const size_t ea = (size_t)kSkM * kSkK, eb = (size_t)kSkN * kSkK, ec = (size_t)kSkM * kSkN;
+  const size_t wsb = ntm_skh_ws_bytes(variant, kSkM, kSkN, kSkK);
+  void *A, *B, *C, *W;
+  float* R;
+  CK(hipMalloc(&A, ea * 2));
+  CK(hipMalloc(&B, eb * 2));
+  CK(hipMalloc(&C, ec * 2));
+  CK(hipMalloc(&R, ec * 4));
+  CK(hipMalloc(&W, wsb));
+  CK(hipMemsetAsync(W, 0, wsb, s));  // counters zero on entry (each launch leaves them zero)
+  CK(ntm_fill_uniform_bf16(A, ea, 5000 + 2 * dev, 1.0f, s));
+  CK(ntm_fill_uniform_bf16(B, eb, 5001 + 2 * dev, 1.0f, s));
+  const int fault = (last && o.fault == "sk_xcc") ? 1 : 0;
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  CK(hipEventRecord(e0, s));
+  CK(ntm_gemm_bf16_skh_ex(variant, A, B, C, kSkM, kSkN, kSkK, kSkK, kSkK, kSkN, W, wsb, fault, s));
+  CK(hipEventRecord(e1, s));
+  CK(ntm_ref_gemm_f32(A, B, R, kSkM, kSkN, kSkK, kSkK, kSkK, kSkN, s));
+  CK(hipMemsetAsync(V, 0, 64, s));
+  const float atol = 1e-3f + 4.0f * std::sqrt((float)kSkK) * std::ldexp(1.0f, -20);
+  CK(ntm_verify_bf16(C, R, ec, atol, std::ldexp(1.0f, -7), V, s));
+  unsigned char vr[64];
+  CK(hipMemcpyAsync(vr, V, ntm_verify_result_bytes(), hipMemcpyDeviceToHost, s));
+  CK(hipMemcpyAsync(&r.sk_word, (unsigned*)W + ntm_sk_error_word_index(), 4, hipMemcpyDeviceToHost, s));
+  CK(hipStreamSynchronize(s));
+  std::memcpy(&r.sk_bad, vr, 8);
+  float ms = 0;
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  r.sk_ms = ms;
+  CK(hipEventDestroy(e0));
+  CK(hipEventDestroy(e1));
+  CK(hipFree(A));
+  CK(hipFree(B));
+  CK(hipFree(C));
+  CK(hipFree(R));
+  CK(hipFree(W));
+  return true;
+}
 
 bool run_gpu(int dev, bool last, const Opts& o, GpuResult& r) {
   r.device = dev;
@@ -406,6 +473,13 @@ bool run_gpu(int dev, bool last, const Opts& o, GpuResult& r) {
   }
   CK(hipFree(A));
   CK(hipFree(B));
+
+  // ---- stream-K split mode on a 192-wide tile: the one K1 path
+  // whose correctness rests on a placement invariant (every part of a split tile
+  // on one XCD, gemm_bf16_sk.hpp) - checked against the fp32 reference, and the
+  // kernel's own placement error word must stay zero. fault "sk_xcc" makes the
+  // last GPU's launch claim a wrong XCC and must fail the Job.
+  if (!run_sk_check(dev, last, o, s, V, r)) return false;
 
   // ---- K1-fp8: the same schedule on e4m3 operands (MX-scaled MFMA, unit
   // scales), checked element-wise against the fp32 reference of the e4m3 values
@@ -1178,6 +1252,15 @@ int main(int argc, char** argv) {
   for (auto& r : res) {
     const std::string d = "gpu" + std::to_string(r.device) + ": ";
     if (r.gemm_bad != 0) fail(d + "GEMM verification failed (" + std::to_string(r.gemm_bad) + " elements)");
+    if (r.sk_variant && r.sk_word != 0) {
+      char w[16];
+      std::snprintf(w, sizeof w, "0x%08x", r.sk_word);
+      fail(d + "stream-K split mode: a split tile's parts ran on different XCDs (error word " + w +
+           "); its C is not trusted");
+    }
+    if (r.sk_variant && r.sk_bad != 0)
+      fail(d + "stream-K split-mode GEMM verification failed (" + std::to_string(r.sk_bad) +
+           " elements)");
     if (r.abft_bad_acc != 0 || r.abft_bad_store != 0)
       fail(d + "GEMM ABFT checksum failed (" + std::to_string(r.abft_bad_acc) + " accumulator / " +
            std::to_string(r.abft_bad_store) + " stored rows)");
@@ -1289,6 +1372,10 @@ int main(int argc, char** argv) {
           ",\"gemm_fp8_max_abs_err\":" + jnum(r.fp8_max_err) +
           ",\"gemm_fp8_abft_bad_rows\":" +
           (r.fp8_abft_bad == ~0ull ? std::string("null") : std::to_string(r.fp8_abft_bad)) +
+          ",\"sk_split_variant\":" + std::to_string(r.sk_variant) +
+          ",\"sk_split_wrong\":" + (r.sk_bad == ~0ull ? std::string("null") : std::to_string(r.sk_bad)) +
+          ",\"sk_xcc_error\":" + std::to_string(r.sk_word) +
+          ",\"sk_split_ms\":" + jnum(r.sk_ms) +
           ",\"hbm_copy_GBps\":" + jnum(r.hbm_copy_gbps) +
           ",\"hbm_read_GBps\":" + jnum(r.hbm_read_gbps) + "}";
   }
