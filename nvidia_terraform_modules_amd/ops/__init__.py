@@ -42,6 +42,8 @@ from .kernels import (  # noqa: F401
     ref_gemm_f32,
     set_plan_pp_tiles,
     set_plan_splitk,
+    set_plan_splitk_ragged,
+    set_cus_override,
     sk_ws_bytes,
     sk_xcc_error,
     SkPlacementError,

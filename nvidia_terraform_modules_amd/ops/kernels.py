@@ -110,17 +110,18 @@ SK_VARIANTS = ("pingpong8s",) + SKH_VARIANTS
 
 
 def set_plan_pp_tiles(on: bool = True, split: bool | None = None) -> None:
-    """A/B knob for tools (tools/pp_plan_ab.py): let the plan use the 192x256 /
+    """A/B knob for tools (tools/k1_ab.py pp-tiles): let the plan use the 192x256 /
     256x192 ping-pong tiles on all of C (``on``) and in stream-K split mode
     (``split``, default: as ``on``). The shipping plan has both. Process-wide."""
     split = on if split is None else split
     lib().ntm_set_plan_pp_tiles((1 if on else 0) | (2 if split else 0))
     _DEFAULT_WS.clear()
     _DEFAULT_SK.clear()
+    _FP8_WS.clear()
 
 
 def set_plan_splitk(margin: float = 0.0, long_slice_k: int = -1, fp8: bool = True) -> None:
-    """A/B knob for tools (tools/margin_ab.py): the factor by which a split-K
+    """A/B knob for tools (tools/k1_ab.py margin): the factor by which a split-K
     plan whose slices keep at least ``long_slice_k`` of K must beat the unsplit
     plan's predicted time (shorter slices, and any split against stream-K, keep
     1.1). margin <= 0 / long_slice_k < 0: the shipping 1.03 / 1024 (K1-fp8:
@@ -129,6 +130,27 @@ def set_plan_splitk(margin: float = 0.0, long_slice_k: int = -1, fp8: bool = Tru
     lib().ntm_set_plan_splitk(float(margin), int(long_slice_k), 1 if fp8 else 0)
     _DEFAULT_WS.clear()
     _DEFAULT_SK.clear()
+    _FP8_WS.clear()
+
+
+def set_plan_splitk_ragged(on: bool = True) -> None:
+    """A/B knob for tools (tools/k1_ab.py margin): price long-slice split-K
+    against the ragged-scaled unsplit time (the shipping plan, ``on``) or with
+    round 4's rule. Process-wide; clears the per-shape plan memos here so no
+    later default-dispatch call runs a stale decision."""
+    lib().ntm_set_plan_splitk_ragged(1 if on else 0)
+    _DEFAULT_WS.clear()
+    _DEFAULT_SK.clear()
+    _FP8_WS.clear()
+
+
+def set_cus_override(cus: int = 0) -> None:
+    """Host-only test knob: plan for ``cus`` CUs instead of the device's own (0 =
+    the device's). Never set around real launches. Clears the plan memos."""
+    lib().ntm_set_cus_override(int(cus))
+    _DEFAULT_WS.clear()
+    _DEFAULT_SK.clear()
+    _FP8_WS.clear()
 
 
 def skh_ws_bytes(variant: str, m: int, n: int, k: int) -> int:

@@ -3,6 +3,8 @@ which rows of C go on the 256x256 kernel and which small tile takes the rest.
 No GPU needed - the plan is pure host code in the native library."""
 import pytest
 
+from nvidia_terraform_modules_amd.ops import kernels
+
 
 @pytest.fixture(scope="module")
 def k1_plan():
@@ -305,7 +307,7 @@ def test_plan_and_launch_agree_on_the_cu_count(k1_plan, cus):
     shapes = [(4472, 5688, 5832), (4672, 1472, 6696), (1000, 1000, 1000), (8192, 8192, 8192)]
     shapes += [(rng.randrange(256, 9000), rng.randrange(32, 1200) * 8, rng.randrange(16, 1500) * 8)
                for _ in range(60)]
-    lib().ntm_set_cus_override(cus)
+    kernels.set_cus_override(cus)
     kernels._DEFAULT_WS.clear()
     try:
         assert lib().ntm_plan_cus() == cus
@@ -319,7 +321,7 @@ def test_plan_and_launch_agree_on_the_cu_count(k1_plan, cus):
         if cus % 8 == 0 and cus >= 32:
             assert picked > 0
     finally:
-        lib().ntm_set_cus_override(0)
+        kernels.set_cus_override(0)
         kernels._DEFAULT_WS.clear()
     assert lib().ntm_plan_cus() == 256      # no GPU here: the documented default
 
@@ -361,10 +363,10 @@ def test_plan_cache_returns_the_search_result(k1_plan, splitk_plan):
     assert first == second
     assert k1_plan(3904, 2584, 12760) == (3904, "pp256x192", "pp256x192")
     try:
-        lib().ntm_set_cus_override(128)   # 231 tiles no longer fit one round
+        kernels.set_cus_override(128)   # 231 tiles no longer fit one round
         assert k1_plan(3904, 2584, 12760) == (2816, "pingpong8cm", "tile160")
     finally:
-        lib().ntm_set_cus_override(0)
+        kernels.set_cus_override(0)
     assert k1_plan(3904, 2584, 12760) == (3904, "pp256x192", "pp256x192")
     ops.set_plan_pp_tiles(False)
     try:
@@ -390,13 +392,13 @@ def test_splitk_margin_by_slice_length(splitk_plan):
     from nvidia_terraform_modules_amd.ops._lib import lib
 
     ops.set_plan_splitk(1.1, 0)
-    lib().ntm_set_plan_splitk_ragged(0)   # round 4's rule: 1.1, no ragged pricing
+    kernels.set_plan_splitk_ragged(False)   # round 4's rule: 1.1, no ragged pricing
     try:
         assert splitk_plan(1040, 2776, 5096) == (1040, "tile128", "tile128", 1)
         assert splitk_plan(3896, 368, 2064) == (3896, "tile128", "tile128", 1)
     finally:
         ops.set_plan_splitk()
-        lib().ntm_set_plan_splitk_ragged(1)
+        kernels.set_plan_splitk_ragged(True)
     assert splitk_plan(1040, 2776, 5096) == (1040, "tile160", "tile160", 2)
 
 
@@ -424,8 +426,8 @@ def test_splitk_priced_against_ragged_unsplit_time(splitk_plan):
     from nvidia_terraform_modules_amd.ops._lib import lib
 
     assert splitk_plan(3232, 936, 4024) == (3232, "tile160", "tile160", 2)
-    lib().ntm_set_plan_splitk_ragged(0)
+    kernels.set_plan_splitk_ragged(False)
     try:
         assert splitk_plan(3232, 936, 4024) == (3232, "tile128", "tile128", 1)
     finally:
-        lib().ntm_set_plan_splitk_ragged(1)
+        kernels.set_plan_splitk_ragged(True)

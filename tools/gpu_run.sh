@@ -23,7 +23,7 @@
 #   fp8        K1-fp8 vs hipBLASLt fp8: square sizes (gemm_fp8_check) + the 41-shape sweep
 #   standing   where the shipping default plans stand vs hipBLASLt on this box: named bf16
 #              shapes (gemm_check), fp8 (gemm_fp8_check), a seeded ragged one-round set
-#              (ragged_sweep) and 48 seeded random shapes (gemm_policy); STAND_SEED picks
+#              (k1_ab.py ragged) and 48 seeded random shapes (gemm_policy); STAND_SEED picks
 #              the fresh sets. Run on >= 3 boxes; tools/k1_boxes.py takes the median.
 #   py:<file>  python -u <file> (a tool script; its own args via PYARGS)
 set -o pipefail
@@ -109,7 +109,7 @@ for s in "${STEPS[@]}"; do
         > "$O/standing_bf16.log" 2>&1 || fail "standing bf16" $? "$O/standing_bf16.log"
       timeout -k 10 600 python -u tools/gemm_fp8_check.py --sizes 4096,8192,8192x8192x4096,6144 --no-bf16 \
         --rounds 7 --iters 30 > "$O/standing_fp8.log" 2>&1 || fail "standing fp8" $? "$O/standing_fp8.log"
-      timeout -k 10 600 python -u tools/ragged_sweep.py --n 24 --seed "$sd" --rounds 5 --iters 10 \
+      timeout -k 10 600 python -u tools/k1_ab.py ragged --n 24 --seed "$sd" --rounds 5 --iters 10 \
         > "$O/standing_ragged_seed$sd.log" 2>&1 || fail "standing ragged" $? "$O/standing_ragged_seed$sd.log"
       timeout -k 10 900 python -u tools/gemm_policy.py --only-default --shapes "" --random 48 --seed "$sd" \
         --rounds 5 --iters 20 > "$O/standing_random48_seed$sd.log" 2>&1 \
