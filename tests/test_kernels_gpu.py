@@ -739,6 +739,32 @@ def test_fp8_persistent_overlap_vs_torch_fp32(ops, m, n, k):
             ops.gemm_fp8(a[:, :256], b[:, :256], knob=30)
 
 
+@pytest.mark.parametrize("m,n,k", [(256, 256, 768),      # one tile, T = 6: the peeled pair is t = 2
+                                   (4096, 4096, 768),    # one tile per workgroup, T = 6
+                                   (8192, 4096, 768),    # 2 tiles per workgroup, T = 6
+                                   (8192, 8192, 1024),   # 4 per workgroup, T = 8
+                                   (4608, 4352, 4096),   # 306 tiles: 1-2 per workgroup
+                                   (8192, 8192, 8192)])  # the Job's shape
+def test_fp8_l2_prefetch_build_is_bitwise_equal(ops, m, n, k):
+    """fp8 knob 32 (round 6): the shipping spread-store fp8 build (knob 31) with
+    the next tile's K-tiles 0 / 1 touched into L2 over K-tiles T-4 / T-3 (PF).
+    The touches land in a scratch slice and only change counted waits, so C is
+    bitwise the default's; vs the fp32 product; K below 768 is refused."""
+    a = ops.fill_uniform_(torch.empty((m, k), dtype=torch.float8_e4m3fn, device="cuda"), 41)
+    b = ops.fill_uniform_(torch.empty((n, k), dtype=torch.float8_e4m3fn, device="cuda"), 42)
+    c31 = ops.gemm_fp8(a, b, knob=31)
+    c32 = ops.gemm_fp8(a, b, knob=32)
+    assert torch.equal(c32.view(torch.int16), c31.view(torch.int16))
+    for _ in range(3):
+        assert torch.equal(ops.gemm_fp8(a, b, knob=32).view(torch.int16), c31.view(torch.int16))
+    if m * n <= 4096 * 4096:
+        ref = a.float() @ b.float().T
+        atol, rtol = ops.gemm_tolerance(k)
+        assert ((c32.float() - ref).abs() <= atol + rtol * ref.abs()).all()
+    with pytest.raises(RuntimeError):
+        ops.gemm_fp8(a[:, :512], b[:, :512], knob=32)
+
+
 @pytest.mark.parametrize("m,n,k", [(1000, 1000, 256), (4472, 5688, 640), (4608, 4360, 512),
                                    (8192, 8192, 256), (333, 1000, 384), (5000, 4104, 768),
                                    # partial K (K % 128 != 0): 4, 6, 8 K-tiles, the last

@@ -139,6 +139,27 @@ __device__ __forceinline__ void issue6(const GemmArgs& p, const Ctx& c, int kt, 
   }
 }
 
+// PF builds (round 5): touch half H of the NEXT tile's K-tile
+// T + KO (KO = 0 / 1) into L2 a few phases before the real pieces stage it,
+// as an LDS-DMA into the scratch slice nobody reads (the same form as the
+// dummy pieces, so it needs no VGPR; it counts in vmcnt like them). Without a
+// next tile it re-reads this tile's last K-tile (L2-hot), keeping the counted
+// waits uniform. At a tile boundary every CU of an XCD turns to new A / B
+// panels at once, and pingpong8o's boundary phases waited ~2.7 k cycles for
+// them to come from HBM (profiles/r4_stamps).
+template <int H, int KO>
+__device__ __forceinline__ void prefetch6(const Ctx& c, int T, bool has_next, long dA, long dB) {
+  const long d = (H == kALo || H == kAHi) ? dA : dB;
+  // an opaque copy of the source pointer, so the eight touch addresses are
+  // formed here and not hoisted out of the K loop (16 more live VGPRs spill)
+  const __bf16* base;
+  asm volatile("" : "=v"(base) : "0"(c.src[H]));
+  const __bf16* s = base + (has_next ? d + (long)KO * BK : (long)(T - 1) * BK);
+  // one 16-B chunk per lane: a lane quad spans 64 B of a row, and the piece's
+  // second chunk (s + 32) lies in the same 128-B L2 lines
+  glds16(s, c.lds + kScratch + (2 * c.w) * 1024);
+}
+
 // fp8 (F8 builds): v_mfma_f32_16x16x128_f8f6f4 (e4m3 x e4m3, default unit
 // scales) updating a VGPR accumulator in place. K1-fp8's pingpong8c keeps its
 // accumulators in AGPRs (gemm_bf16.hpp mfma_f8_agpr), which caps its VGPRs at
@@ -301,7 +322,7 @@ struct Edge {
 // when ON (10 otherwise); NX: this phase's piece is past the tile (issue6). A
 // stored quadrant is zeroed for the next tile.
 template <int P, bool ODD, int CONV, int VMC, bool NX, int POL, bool MASK = false, bool TL = false,
-          bool F8 = false>
+          bool F8 = false, int PF = -1, int XV = 0>
 __device__ __forceinline__ void phase6(const GemmArgs& p, const Ctx& c, Frags3& f,
                                        f32x4 (&acc)[2][2][4][2], int t, int T, const Edge& e,
                                        bool on, int c_lane, int lane = 0, int lrow = 0,
@@ -317,15 +338,22 @@ __device__ __forceinline__ void phase6(const GemmArgs& p, const Ctx& c, Frags3& 
   if constexpr (P == 1) issue6<kBLo, NX, MASK, TL>(p, c, t + 2, cur, T, e.has_next, e.dA, e.dB, e.nm0, e.nn0, lane);
   if constexpr (P == 2) issue6<kALo, NX, MASK, TL>(p, c, t + 2, cur, T, e.has_next, e.dA, e.dB, e.nm0, e.nn0, lane);
   if constexpr (P == 3) issue6<kBHi, NX, MASK, TL>(p, c, t + 2, cur, T, e.has_next, e.dA, e.dB, e.nm0, e.nn0, lane);
+  // PF: one L2 touch of the next tile's K-tile 0 / 1 (halves in B-lo A-lo B-hi A-hi
+  // order, the real pieces' order) after this phase's piece
+  if constexpr (PF >= 0) {
+    constexpr int H = (PF & 3) == 0 ? kBLo : (PF & 3) == 1 ? kALo : (PF & 3) == 2 ? kBHi : kAHi;
+    prefetch6<H, PF / 4>(c, T, e.has_next, e.dA, e.dB);
+  }
   // POL 2 (C not stored): no stores in the stream, so the pieces-only count
-  // (round 3's ablation kept the store-counting waits, which then under-waited)
+  // (round 3's ablation kept the store-counting waits, which then under-waited);
+  // XV: the prefetch ops younger than the awaited piece (PF builds)
   if constexpr (VMC == 10 || POL == 2) {
-    wait_vm<10>();
+    wait_vm<10 + XV>();
   } else {
     if (on)
-      wait_vm<VMC>();
+      wait_vm<VMC + XV>();
     else
-      wait_vm<10>();
+      wait_vm<10 + XV>();
   }
   if constexpr (F8 && CONV >= 0) {
     if (on) mfma_wait_states();
@@ -369,6 +397,9 @@ __device__ __forceinline__ void phase6(const GemmArgs& p, const Ctx& c, Frags3& 
 #define NTM_PHT(P, ODD, CV, VMC, NX, ON, TL) \
   phase6<P, ODD, CV, VMC, NX, POL, MASK, TL, F8>(p, c, f, acc, t, T, e, ON, c_lane, lane, lrow, lcol)
 #define NTM_PH(P, ODD, CV, VMC, NX, ON) NTM_PHT(P, ODD, CV, VMC, NX, ON, false)
+// PF builds: steady-state phase with prefetch PF and XV extra ops in its wait
+#define NTM_PHP(P, ODD, CV, VMC, NX, ON, PFI, XVI) \
+  phase6<P, ODD, CV, VMC, NX, POL, MASK, false, F8, PFI, XVI>(p, c, f, acc, t, T, e, ON, c_lane, lane, lrow, lcol)
 // STAMP 2: shader-clock stamp I of wave 0 at a phase start of the workgroup's
 // first tile boundary (K-tiles T-2 / T-1 of its first tile: I = 0..7, K-tiles
 // 0 / 1 of its second: I = 8..15, 16 = after K-tile 1), into p.stamps[17 b + I]
@@ -427,9 +458,10 @@ __device__ __forceinline__ void clock_stamp(unsigned long long& t, unsigned long
 // staging of the boundary stores: exactly 128 MB written instead of 157 MB,
 // no faster. Removed after measurement, profiles/r4_stg/; git history has it.)
 template <int POL, int STAMP = 0, bool MASK = false, bool TAIL = false, bool SPREAD = false,
-          bool F8 = false>
+          bool F8 = false, bool PF = false>
 __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_pp6_kernel(GemmArgs p) {
   static_assert(!TAIL || MASK, "partial K rides on the masked build");
+  static_assert(!PF || (!MASK && !TAIL), "the L2 prefetch is on the whole-tile build");
   __shared__ __attribute__((aligned(16))) char smem[kLdsBytes3];
   unsigned long long t0 = 0, rt0 = 0;
   if constexpr (STAMP == 1) clock_stamp(t0, rt0);
@@ -528,8 +560,13 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_pp6_kernel(GemmArgs p) 
     NTM_ST(15, false);
     NTM_PHT(3, true, -1, SPREAD ? 13 : 10, false, e.prev, TAIL);
     NTM_ST(16, false);
+    // PF: the last steady pair (T-4 / T-3; T >= 6) is peeled to carry the L2
+    // touches. Phase j's wait retires phase j-5's piece; every touch issued
+    // after it - phases j-5 .. j, each after its own piece - may stay in flight
+    // (one op each): vmcnt 11 12 13 14 15 16 16 16 (T-4, T-3), 15 14 13 12 (T-2),
+    // 11 (T-1 P0)
 #pragma nounroll
-    for (t = 2; t < T - (TAIL ? 4 : 2); t += 2) {
+    for (t = 2; t < T - (TAIL ? 4 : 2) - (PF ? 2 : 0); t += 2) {
       NTM_PH(0, false, -1, 10, false, false);
       NTM_PH(1, false, -1, 10, false, false);
       NTM_PH(2, false, -1, 10, false, false);
@@ -556,21 +593,47 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_pp6_kernel(GemmArgs p) 
         NTM_PHT(3, true, -1, 10, false, false, true);
       }
     }
+    if constexpr (PF) {  // T >= 6 (the launcher's rule for PF builds)
+      t = T - 4;
+      NTM_PHP(0, false, -1, 10, false, false, 0, 1);
+      NTM_PHP(1, false, -1, 10, false, false, 1, 2);
+      NTM_PHP(2, false, -1, 10, false, false, 2, 3);
+      NTM_PHP(3, false, -1, 10, false, false, 3, 4);
+      ++t;
+      NTM_PHP(0, true, -1, 10, false, false, 4, 5);
+      NTM_PHP(1, true, -1, 10, false, false, 5, 6);
+      NTM_PHP(2, true, -1, 10, false, false, 6, 6);
+      NTM_PHP(3, true, -1, 10, false, false, 7, 6);
+    }
     // K-tile T-2 stages the next tile's K-tile 0, K-tile T-1 its K-tile 1 (or
     // dummies); with a next tile, q0..q2 leave in P1..P3 of K-tile T-1 (LINE:
     // row half 0 in P2)
     t = T - 2;
-    NTM_ST(0, true);
-    NTM_PHT(0, false, -1, 10, false, false, TAIL);
-    NTM_ST(1, true);
-    NTM_PH(1, false, -1, 10, true, false);
-    NTM_ST(2, true);
-    NTM_PH(2, false, -1, 10, true, false);
-    NTM_ST(3, true);
-    NTM_PH(3, false, -1, 10, true, false);
+    if constexpr (PF) {
+      NTM_ST(0, true);
+      NTM_PHP(0, false, -1, 10, false, false, -1, 5);
+      NTM_ST(1, true);
+      NTM_PHP(1, false, -1, 10, true, false, -1, 4);
+      NTM_ST(2, true);
+      NTM_PHP(2, false, -1, 10, true, false, -1, 3);
+      NTM_ST(3, true);
+      NTM_PHP(3, false, -1, 10, true, false, -1, 2);
+    } else {
+      NTM_ST(0, true);
+      NTM_PHT(0, false, -1, 10, false, false, TAIL);
+      NTM_ST(1, true);
+      NTM_PH(1, false, -1, 10, true, false);
+      NTM_ST(2, true);
+      NTM_PH(2, false, -1, 10, true, false);
+      NTM_ST(3, true);
+      NTM_PH(3, false, -1, 10, true, false);
+    }
     t = T - 1;
     NTM_ST(4, true);
-    NTM_PH(0, true, -1, 10, true, false);
+    if constexpr (PF)
+      NTM_PHP(0, true, -1, 10, true, false, -1, 1);
+    else
+      NTM_PH(0, true, -1, 10, true, false);
     NTM_ST(5, true);
     NTM_PH(1, true, SPREAD ? 10 : 0, 10, true, e.has_next);
     NTM_ST(6, true);
@@ -661,25 +724,26 @@ inline int pp6_grid(int ntiles) {
 
 // Experimental: an explicit grid (a multiple of 8, at most the tile count) and
 // POL 2 (C not stored) - the store-bandwidth study of profiles/r3_stores.
-template <int POL, int STAMP = 0, bool SPREAD = false>
+template <int POL, int STAMP = 0, bool SPREAD = false, bool PF = false>
 inline hipError_t launch_gemm_bf16_pp6_grid(const GemmArgs& a, int grid, hipStream_t stream) {
   if (!shape_ok6(a.M, a.N, a.K) || a.rowsum || a.lda < a.K || a.ldb < a.K || a.ldc < a.N ||
       (a.lda % 8) || (a.ldb % 8) || (a.ldc % 8) || grid <= 0 || grid % 8 ||
-      grid > (a.M / BM) * (a.N / BN))
+      grid > (a.M / BM) * (a.N / BN) || (PF && a.K < 6 * BK))
     return hipErrorInvalidValue;
   if (STAMP != 0 && a.stamps == nullptr) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((gemm_bf16_pp6_kernel<POL, STAMP, false, false, SPREAD>),
+  hipLaunchKernelGGL((gemm_bf16_pp6_kernel<POL, STAMP, false, false, SPREAD, false, PF>),
                      dim3((unsigned)grid), dim3(kThreads), 0, stream, a);
   return hipGetLastError();
 }
 
-template <int POL, int STAMP = 0, bool SPREAD = false>
+template <int POL, int STAMP = 0, bool SPREAD = false, bool PF = false>
 inline hipError_t launch_gemm_bf16_pp6(const GemmArgs& a, hipStream_t stream) {
   if (!shape_ok6(a.M, a.N, a.K) || a.rowsum || a.lda < a.K || a.ldb < a.K || a.ldc < a.N ||
-      (a.lda % 8) || (a.ldb % 8) || (a.ldc % 8) || (STAMP != 0 && a.stamps == nullptr))
+      (a.lda % 8) || (a.ldb % 8) || (a.ldc % 8) || (STAMP != 0 && a.stamps == nullptr) ||
+      (PF && a.K < 6 * BK))
     return hipErrorInvalidValue;
   const int ntiles = (a.M / BM) * (a.N / BN);
-  hipLaunchKernelGGL((gemm_bf16_pp6_kernel<POL, STAMP, false, false, SPREAD>),
+  hipLaunchKernelGGL((gemm_bf16_pp6_kernel<POL, STAMP, false, false, SPREAD, false, PF>),
                      dim3((unsigned)pp6_grid(ntiles)),
                      dim3(kThreads), 0, stream, a);
   return hipGetLastError();
@@ -693,7 +757,10 @@ inline bool fp8_pp6_ok(int M, int N, int K, int lda, int ldb, int ldc) {
          lda >= K && ldb >= K && ldc >= N && (ldc % 8) == 0;
 }
 
-template <bool SPREAD = false>
+// PF: the next tile's K-tiles 0 / 1 touched into L2 over K-tiles T-4 / T-3
+// (round 6: K1-fp8 is not power-bound, so the boundary cycles the touches save
+// can reach the launch time; bf16 lost 0.5-1 % to their energy, profiles/r5_pf).
+template <bool SPREAD = false, bool PF = false>
 inline hipError_t launch_gemm_fp8_pp6(const void* A, const void* B, __bf16* C, int M, int N,
                                       int K, int lda, int ldb, int ldc, hipStream_t stream) {
   GemmArgs a;
@@ -707,10 +774,10 @@ inline hipError_t launch_gemm_fp8_pp6(const void* A, const void* B, __bf16* C, i
   a.ldb = ldb / 2;
   a.ldc = ldc;
   if ((K % 2) || (lda % 16) || (ldb % 16) || !shape_ok6(a.M, a.N, a.K) || a.lda < a.K ||
-      a.ldb < a.K || a.ldc < a.N || (a.ldc % 8))
+      a.ldb < a.K || a.ldc < a.N || (a.ldc % 8) || (PF && a.K < 6 * BK))
     return hipErrorInvalidValue;
   const int ntiles = (a.M / BM) * (a.N / BN);
-  hipLaunchKernelGGL((gemm_bf16_pp6_kernel<1, 0, false, false, SPREAD, true>),
+  hipLaunchKernelGGL((gemm_bf16_pp6_kernel<1, 0, false, false, SPREAD, true, PF>),
                      dim3((unsigned)pp6_grid(ntiles)), dim3(kThreads), 0, stream, a);
   return hipGetLastError();
 }

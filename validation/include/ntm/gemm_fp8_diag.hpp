@@ -58,6 +58,9 @@ inline hipError_t launch_gemm_fp8_knob(const void* A, const void* B, __bf16* C, 
     // 31: the same with the boundary stores spread over 7 phases (SPREAD, as the
     // shipping bf16 build)
     case 31: return ::ntm::gemm6::launch_gemm_fp8_pp6<true>(A, B, C, M, N, K, lda, ldb, ldc, s);
+    // 32 (round 6): knob 31 + the next tile's K-tiles 0 / 1 touched into L2 over
+    // K-tiles T-4 / T-3 (PF; fp8 K >= 768)
+    case 32: return ::ntm::gemm6::launch_gemm_fp8_pp6<true, true>(A, B, C, M, N, K, lda, ldb, ldc, s);
     case 1: hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, kGroupM, false, kEpiDefault, 0, 2>), g, b, 0, s, a); break;
     case 2: hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, 4, false, kEpiDefault, 0, 1>), g, b, 0, s, a); break;
     case 3: hipLaunchKernelGGL((gemm_bf16_pp3_kernel<false, kGroupM, false, kEpiDefault, 2, 1>), g, b, 0, s, a); break;
