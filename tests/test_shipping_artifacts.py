@@ -35,9 +35,9 @@ ALLOWED_K1 = {
     "ntm::gemm3::gemm_bf16_pp3_kernel<false, 8, false, 58, 0, 3>",  # K1-fp8, masked + partial K
     # pingpong8o <POL, STAMP, MASK, TAIL, SPREAD, F8>: > 256 tiles of 256x256
     # (the shipping bf16 build spreads its boundary stores: SPREAD, "pingpong8od")
-    "ntm::gemm6::gemm_bf16_pp6_kernel<1, 0, false, false, true, false>",
-    "ntm::gemm6::gemm_bf16_pp6_kernel<1, 1, false, false, true, false>",  # clock stamps
-    "ntm::gemm6::gemm_bf16_pp6_kernel<1, 0, false, false, true, true>",   # K1-fp8
+    "ntm::gemm6::gemm_bf16_pp6_kernel<1, 0, false, false, true, false, false>",
+    "ntm::gemm6::gemm_bf16_pp6_kernel<1, 1, false, false, true, false, false>",  # clock stamps
+    "ntm::gemm6::gemm_bf16_pp6_kernel<1, 0, false, false, true, true, false>",   # K1-fp8
     # stream-K over the last two rounds of 256x256 tiles (pingpong8s <TAIL, REV, STAMP>)
     "ntm::gemmsk::gemm_bf16_sk_kernel<false, false, false>",
     "ntm::gemmsk::gemm_bf16_sk_kernel<true, false, false>",
@@ -127,6 +127,6 @@ def test_experimental_library_holds_the_experiments():
     ks = _kernels(EXP)
     for fam in ("gemm_bf16_pp3_stamp_kernel", "gemm_bf16_sk_kernel<false, true, false>", "mfma_rate_kernel",
                 "mfma_f8_probe_kernel",
-                "gemm_bf16_pp6_kernel<1, 0, true, false, false, false>",   # pingpong8om
+                "gemm_bf16_pp6_kernel<1, 0, true, false, false, false, false>",   # pingpong8om
                 "gemm_bf16_pp3h_kernel<96, 128"):                          # pp224x256
         assert any(fam in k for k in ks), fam
