@@ -655,7 +655,12 @@ def c2_sweep(env, main_sizes: list[int], tune_max_bytes: int, factory=None, iter
     nblk, cut, src = 64, 256 << 10, "default"
     if tuned and not tuned["errors"] and not tuned["timed_out"]:
         nblk, cut, src = tuned["best_nblk"], tuned["best_one_shot_max_bytes"], "xgmi_tune"
-    ar.reconfigure(nblk, cut)
+    try:
+        ar.reconfigure(nblk, cut)
+    except RuntimeError as e:  # raised on every rank together (gathered errors)
+        out.update(ok=False, xgmi_error=f"{type(e).__name__}: {e}"[:300])
+        ar.close()
+        return out, []
     xr = sweep(env, list(main_sizes), dtype="bf16", iters=iters, warmup=warmup, impl=ar)
     st = all_gather_obj(env, ar.stats())
     out.update({

@@ -242,3 +242,31 @@ def test_overlap_with_a_freed_export_is_reported():
         assert xg._overlaps_freed_export(0x11000, 64)["overlaps_prev_export"] is False
     finally:
         xg._FREED_EXPORTS.pop()
+
+
+def _c2_bad_reconfigure(env):
+    """A communicator whose reconfigure fails collectively: c2_sweep records the
+    error on every rank and returns instead of raising mid-bench."""
+    from nvidia_terraform_modules_amd.parallel import xgmi as xg
+
+    class Bad(xg.ReferenceAllReduce):
+        def reconfigure(self, nblk, one_shot_max_bytes=None):
+            if self.reconfigures >= 2:
+                raise RuntimeError("XgmiAllReduce.reconfigure failed: injected")
+            super().reconfigure(nblk, one_shot_max_bytes)
+
+    out, xr = xg.c2_sweep(env, [512, 2048], 64 << 10,
+                          factory=lambda nb, mb: Bad(env, mb, nblk=nb), iters=1, warmup=0,
+                          tune_kwargs={"sizes": (16 << 10,), "nblks": (16, 32, 64),
+                                       "iters": 1, "warmup": 0})
+    return {"ok": out["ok"], "err": out.get("xgmi_error", ""), "xr": len(xr),
+            "tune_err": out["xgmi_tune"].get("error", "")}
+
+
+def test_c2_sweep_survives_a_collective_reconfigure_failure():
+    res = _run(2, "_c2_bad_reconfigure")
+    for r in res.values():
+        # the third reconfigure (inside tune) fails: tune records it, and the hand-over
+        # reconfigure fails too - reported, no exception escapes, no main sweep
+        assert r["ok"] is False and "injected" in r["tune_err"]
+        assert "injected" in r["err"] and r["xr"] == 0
