@@ -2,7 +2,7 @@
 our default plan - run under rocprofv3 --kernel-trace and read the trace.
 
     rocprofv3 --kernel-trace --stats -d gpurun_out/bl -o run -- \\
-        python3 tools/blaslt_kernels.py 3904x2584x12760 7288x1344x5768
+        python3 tools/experiments/blaslt_kernels.py 3904x2584x12760 7288x1344x5768
 
 Each shape runs hipBLASLt then our default dispatch, `--iters` times each, in
 that order, so the trace's dispatch order maps back to the shapes (printed as
@@ -12,7 +12,7 @@ import json
 import sys
 from pathlib import Path
 
-sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+sys.path.insert(0, str(Path(__file__).resolve().parents[2]))
 
 import torch  # noqa: E402
 

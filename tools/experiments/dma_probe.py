@@ -10,7 +10,7 @@ ping-pong's loads without MFMAs, on rows whose pitch is 128-B aligned or only
 Prints per-CU GB/s of staged bytes, interleaved rounds, median. --depths 0,1,2,3
 repeats it with 5 / 8 / 12 / 16 halves in flight (counted vmcnt 10 / 16 / 24 / 32).
 
-    python tools/dma_probe.py [--k 4096 --grid 256 --reps 20 --rounds 7]
+    python tools/experiments/dma_probe.py [--k 4096 --grid 256 --reps 20 --rounds 7]
 """
 import argparse
 import json
@@ -20,7 +20,7 @@ import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from nvidia_terraform_modules_amd.ops._lib import check, lib_experimental, stream_handle  # noqa: E402
 
 

@@ -4,7 +4,7 @@ data'). Lane l always holds row / column l & 15; candidate maps differ in which
 k each of its 32 bytes carries. Prints which (A map, B map) pair reproduces
 A @ B^T exactly.
 
-    python tools/fp8_layout_probe.py
+    python tools/experiments/fp8_layout_probe.py
 """
 from __future__ import annotations
 
@@ -13,7 +13,7 @@ import json
 import sys
 from pathlib import Path
 
-sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+sys.path.insert(0, str(Path(__file__).resolve().parents[2]))
 
 import torch  # noqa: E402
 

@@ -11,7 +11,7 @@ launches (MI355X_MICROARCH.md 'DVFS give-back' item 6):
 and reports each one's wall time, in-kernel clock (s_memtime over
 s_memrealtime, median over waves) and cycles per K-tile per workgroup.
 
-    python tools/gemm_stamp.py [--size 8192] [--warm-s 2] [--rounds 5]
+    python tools/experiments/gemm_stamp.py [--size 8192] [--warm-s 2] [--rounds 5]
 """
 from __future__ import annotations
 
@@ -21,7 +21,7 @@ import sys
 import time
 from pathlib import Path
 
-sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+sys.path.insert(0, str(Path(__file__).resolve().parents[2]))
 
 import torch  # noqa: E402
 

@@ -13,7 +13,7 @@ import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 from nvidia_terraform_modules_amd import ops  # noqa: E402
 from nvidia_terraform_modules_amd.ops._lib import check, lib_experimental, stream_handle  # noqa: E402

@@ -4,7 +4,7 @@ about --seconds of back-to-back launches, with the AMD SMI power / throttle
 window around them (ops/smi.py) and the in-kernel clock. Tells how much of
 the GEMM's power-capped budget the matrix cores alone draw.
 
-    python tools/mfma_power.py [--seconds 1.5]
+    python tools/experiments/mfma_power.py [--seconds 1.5]
 """
 from __future__ import annotations
 
@@ -14,7 +14,7 @@ import sys
 import time
 from pathlib import Path
 
-sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+sys.path.insert(0, str(Path(__file__).resolve().parents[2]))
 
 import torch  # noqa: E402
 

@@ -2,7 +2,7 @@
 in-kernel clock for v_mfma_f32_16x16x32_bf16 vs v_mfma_scale_f32_16x16x128_f8f6f4
 (e4m3), operands in registers, one wave per SIMD on every CU, random bits.
 
-    python tools/mfma_rate.py [--iters 20000]
+    python tools/experiments/mfma_rate.py [--iters 20000]
 """
 from __future__ import annotations
 
@@ -11,7 +11,7 @@ import json
 import sys
 from pathlib import Path
 
-sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+sys.path.insert(0, str(Path(__file__).resolve().parents[2]))
 
 import torch  # noqa: E402
 

@@ -4,7 +4,7 @@ workgroup; prints the count of differing elements per run and, for the first
 bad run, the count per accumulator row (16-row group of a wave's 128 rows) -
 the fingerprint that located the asm-MFMA hazard in profiles/r3_w4o/.
 
-    python tools/overlap_bitwise_check.py [--variants pingpong8o,pingpong8od] [--repeats 5]
+    python tools/experiments/overlap_bitwise_check.py [--variants pingpong8o,pingpong8od] [--repeats 5]
 """
 from __future__ import annotations
 
@@ -12,7 +12,7 @@ import argparse
 import sys
 from pathlib import Path
 
-sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+sys.path.insert(0, str(Path(__file__).resolve().parents[2]))
 
 import torch  # noqa: E402
 

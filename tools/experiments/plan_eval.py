@@ -6,7 +6,7 @@ the worst shapes. Caveat: a split-K small-tile plan (splits > 1) is timed only
 as "default", so it is credited with the fastest default measured for that
 shape, whichever plan ran it. Treat a changed split-K pick as unmeasured.
 
-    python tools/plan_eval.py [logs...]   (defaults: the round-4 calibration logs)
+    python tools/experiments/plan_eval.py [logs...]   (defaults: the round-4 calibration logs)
 Host only.
 """
 import math
@@ -14,7 +14,7 @@ import json
 import os
 import sys
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from nvidia_terraform_modules_amd.ops import kernels as K  # noqa: E402
 
 LOGS = ["profiles/r4_sks/split_vs_default.log", "profiles/r4_sks/split_sweep.log",

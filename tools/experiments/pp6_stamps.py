@@ -4,7 +4,7 @@ start from K-tile T-2 of a workgroup's first tile to K-tile 1 of its second
 (gemm_bf16_pp6.hpp STAMP 2), on 256 and 128 workgroups, with C stored and
 not stored. A diagnostic build: read its SHARES, not its run time.
 
-    python tools/pp6_stamps.py [--size 8192] [--k 8192] [--warm-s 1]
+    python tools/experiments/pp6_stamps.py [--size 8192] [--k 8192] [--warm-s 1]
 
 Prints one JSON line per (grid, store) with the median over workgroups of
 each phase's cycles (16 phases: T-2 P0..P3, T-1 P0..P3, next tile 0 P0..P3,
@@ -19,7 +19,7 @@ import sys
 import time
 from pathlib import Path
 
-sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+sys.path.insert(0, str(Path(__file__).resolve().parents[2]))
 
 PHASES = [f"{kt}P{p}" for kt in ("T-2", "T-1", "n0", "n1") for p in range(4)]
 

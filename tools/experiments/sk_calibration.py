@@ -1,7 +1,7 @@
 """Tabulate the K1 plan's predicted unsplit / stream-K times against measured
 gemm_check.py medians (default plan, pingpong8s, hipBLASLt).
 
-Usage: python tools/sk_calibration.py gpurun_out/<run>/gemm_check.log [...]
+Usage: python tools/experiments/sk_calibration.py gpurun_out/<run>/gemm_check.log [...]
 Host only: the plan's times come from ntm_k1_plan_times (no GPU needed).
 """
 import ctypes
@@ -9,7 +9,7 @@ import json
 import os
 import sys
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from nvidia_terraform_modules_amd.ops import _lib, kernels  # noqa: E402
 
 

@@ -2,7 +2,7 @@
 per-workgroup s_memrealtime stamps (STAMP build, experimental library) at each
 stream-K segment's K loop start / end, after its fix-up and after its C store.
 
-    python tools/sk_stamps.py [--shape 4472x5688x5832] [--reps 5]
+    python tools/experiments/sk_stamps.py [--shape 4472x5688x5832] [--reps 5]
 
 Prints one JSON line per shape: medians over workgroups and launches (µs) of
 each segment kind's K loop, fix-up and store, the K-loop time per K-tile pair,
@@ -17,7 +17,7 @@ import statistics
 import sys
 from pathlib import Path
 
-sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+sys.path.insert(0, str(Path(__file__).resolve().parents[2]))
 
 
 def main() -> int:

@@ -4,7 +4,7 @@ on TOPVARIANT and the rest on RESTVARIANT (two launches; ROWS = M: one), interle
 median TF/s; every split is checked against the default result (fp32 tolerance). A variant
 "tile128/s8" runs split-K in 8 K slices.
 
-    python tools/split_check.py --shape 3200x3200x3200 --splits 1920:tile160:tile128
+    python tools/experiments/split_check.py --shape 3200x3200x3200 --splits 1920:tile160:tile128
 """
 import argparse
 import json
@@ -13,7 +13,7 @@ import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from nvidia_terraform_modules_amd import ops  # noqa: E402
 
 

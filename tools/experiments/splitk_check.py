@@ -3,7 +3,7 @@ with 1..8 K slices, the default dispatch and hipBLASLt (torch.matmul) on
 M x N x K shapes, plus the max error of each split against the unsplit result;
 one JSON line per shape.
 
-    python tools/splitk_check.py --shapes 280x6352x7568 [--splits 1,2,3,4,6,8]
+    python tools/experiments/splitk_check.py --shapes 280x6352x7568 [--splits 1,2,3,4,6,8]
 """
 import argparse
 import json
@@ -12,7 +12,7 @@ import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from nvidia_terraform_modules_amd import ops  # noqa: E402
 
 

@@ -4,7 +4,7 @@ bitwise against knob 0 (same MFMA order), then timed in interleaved rounds
 next to the 4-wave tile kernel (tile*w4) and hipBLASLt (torch.matmul) after a clock
 settle; one JSON line per (shape, tile).
 
-    python tools/ws_knobs.py --shapes 8192x8192x8192 --tiles 1 [--knobs 0,1,2,3]
+    python tools/experiments/ws_knobs.py --shapes 8192x8192x8192 --tiles 1 [--knobs 0,1,2,3]
 """
 import argparse
 import json
@@ -13,7 +13,7 @@ import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from nvidia_terraform_modules_amd import ops  # noqa: E402
 from nvidia_terraform_modules_amd.ops._lib import check, lib_experimental, stream_handle  # noqa: E402
 

@@ -4,7 +4,7 @@ XCD (real XCC_ID) the median workgroup clock and the time its last workgroup
 ended. Every XCD gets the same tiles, so the slowest XCD sets the launch time
 and ``xcc_finish_spread_us`` is how long the others idle at its end.
 
-    python tools/xcd_balance.py [--shapes 8192x8192x8192,8192x8192x4096] [--launches 30]
+    python tools/experiments/xcd_balance.py [--shapes 8192x8192x8192,8192x8192x4096] [--launches 30]
 """
 import argparse
 import json
@@ -13,7 +13,7 @@ import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from nvidia_terraform_modules_amd import ops  # noqa: E402
 
 KEYS = ("bound_GHz", "launch_GHz", "xcc_clock_spread_pct", "per_xcc_median_GHz",

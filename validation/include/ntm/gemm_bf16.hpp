@@ -178,7 +178,7 @@ __device__ __forceinline__ void mma_quadrant(f32x4 (&acc)[4][2],
 // lane's 16-B chunk) concatenate into one 32-byte operand of
 // v_mfma_scale_f32_16x16x128_f8f6f4 (unit E8M0 scales). A dot product only
 // needs A and B to use the same k order, which they do (same image, same
-// reads; pinned by tools/fp8_layout_probe.py). 8 MFMAs of 32 cycles do twice
+// reads; pinned by tools/experiments/fp8_layout_probe.py). 8 MFMAs of 32 cycles do twice
 // the bf16 quadrant's work in the same 256 cycles.
 typedef int i32x8 __attribute__((ext_vector_type(8)));
 

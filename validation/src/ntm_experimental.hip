@@ -262,7 +262,7 @@ NTM_API int ntm_stream_copy_spol(const void* src, void* dst, size_t bytes, int u
   return (int)hipGetLastError();
 }
 
-// LDS-DMA access-pattern probe (dma_probe.hpp; tools/dma_probe.py): the 256x256
+// LDS-DMA access-pattern probe (dma_probe.hpp; tools/experiments/dma_probe.py): the 256x256
 // ping-pong's loads with no MFMAs, mode 0 / 1 / 2, `grid` workgroups of 512.
 NTM_API int ntm_dma_probe(int mode, const void* base, int pitch, int T, int reps, int grid,
                           void* stream) {

@@ -186,7 +186,7 @@ struct K1Plan {
   bool feasible() const { return top_rows >= 0; }
 };
 
-// Split-K time model (seconds), fitted on MI355X (tools/splitk_check.py, 14
+// Split-K time model (seconds), fitted on MI355X (tools/experiments/splitk_check.py, 14
 // shapes x 3 tiles x up to 6 slice counts, profiles/r2_splitk/): a round of
 // tm x tn tiles over kc costs 2 tm tn kc / (kPerCU eff); the fp32 partials cost
 // kRedFixed + slices M N 4 / kRedBW (the partial stores in the tile epilogue +
