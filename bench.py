@@ -73,6 +73,10 @@ def parse(argv=None):
     ap.add_argument("--rehearsal", action="store_true",
                     help="CPU/gloo + PyTorch reference ops: rehearses the multi-process "
                          "orchestration and the JSON contract; NOT a measurement (tests only)")
+    ap.add_argument("--shared-gpu", action="store_true",
+                    help="every rank on cuda:0 with a gloo process group: rehearses the N > 1 "
+                         "path with the real kernels (C2 over HIP IPC included) on a one-GPU box; "
+                         "NOT a measurement (tests only; set GPU_MAX_HW_QUEUES=1)")
     return ap.parse_args(argv)
 
 
@@ -322,7 +326,13 @@ def main(argv=None) -> int:
         from nvidia_terraform_modules_amd import ops as backend
 
     _CLOCK.mark("runtime_import")
-    env = dist.init(backend="gloo", device_type="cpu") if args.rehearsal else dist.init()
+    if args.rehearsal:
+        env = dist.init(backend="gloo", device_type="cpu")
+    elif args.shared_gpu:
+        os.environ["LOCAL_RANK"] = "0"      # every rank on the one GPU
+        env = dist.init(backend="gloo", device_type="cuda")
+    else:
+        env = dist.init()
     if env.world_size != args.gpus and env.is_main:
         print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={env.world_size}; "
               f"using WORLD_SIZE", file=sys.stderr)
@@ -632,6 +642,8 @@ def main(argv=None) -> int:
         "dtype": "bf16",
         "data": ("REHEARSAL: CPU/gloo + PyTorch reference ops - orchestration test, NOT a "
                  "measurement" if args.rehearsal else
+                 "SHARED-GPU REHEARSAL: every rank on cuda:0, gloo group - NOT a measurement"
+                 if args.shared_gpu else
                  "synthetic (uniform[-1,1) bf16 operands generated on device, hash RNG)"),
         "config": {
             "model": f"validation-job K1 GEMM C[{args.size}x{args.size}] = A[{args.size}x{args.size}]"
@@ -692,6 +704,7 @@ def main(argv=None) -> int:
         "per_rank_clock_probe": [p["clock"] for p in per_rank],
         "vs_baseline_note": "reference publishes no TFLOP/s or busbw (BASELINE.json published={})",
         **({"rehearsal": True} if args.rehearsal else {}),
+        **({"shared_gpu_rehearsal": True} if args.shared_gpu else {}),
         **extras,
     }
     if env.is_main:
