@@ -541,6 +541,10 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_pp6_kernel(GemmArgs p) 
   // their registers around the back edge.
   for (;;) {
     int t = 0;
+    // STAMP 3 (ablation, experimental library only; C is wrong): a workgroup on an
+    // odd XCD cuts its LAST tile's K loop by 2 p.splitk_kc K-tiles - the timing of
+    // a launch whose odd XCDs (the slower ones, profiles/r6_xcd) carry less work
+    const int Tl = STAMP == 3 && !e.has_next && (blockIdx.x & 1) ? T - 2 * p.splitk_kc : T;
     // K-tile 0: q3 of the previous tile leaves in P0 (SPREAD: blocks of q0..q3 in P0..P3)
     NTM_ST(8, false);
     NTM_PHT(0, false, SPREAD ? 13 : 3, SPREAD ? 16 : 22, false, e.prev, TAIL);
@@ -566,7 +570,7 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_pp6_kernel(GemmArgs p) 
     // (one op each): vmcnt 11 12 13 14 15 16 16 16 (T-4, T-3), 15 14 13 12 (T-2),
     // 11 (T-1 P0)
 #pragma nounroll
-    for (t = 2; t < T - (TAIL ? 4 : 2) - (PF ? 2 : 0); t += 2) {
+    for (t = 2; t < Tl - (TAIL ? 4 : 2) - (PF ? 2 : 0); t += 2) {
       NTM_PH(0, false, -1, 10, false, false);
       NTM_PH(1, false, -1, 10, false, false);
       NTM_PH(2, false, -1, 10, false, false);
@@ -608,7 +612,7 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_pp6_kernel(GemmArgs p) 
     // K-tile T-2 stages the next tile's K-tile 0, K-tile T-1 its K-tile 1 (or
     // dummies); with a next tile, q0..q2 leave in P1..P3 of K-tile T-1 (LINE:
     // row half 0 in P2)
-    t = T - 2;
+    t = Tl - 2;
     if constexpr (PF) {
       NTM_ST(0, true);
       NTM_PHP(0, false, -1, 10, false, false, -1, 5);
@@ -628,7 +632,7 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_bf16_pp6_kernel(GemmArgs p) 
       NTM_ST(3, true);
       NTM_PH(3, false, -1, 10, true, false);
     }
-    t = T - 1;
+    t = Tl - 1;
     NTM_ST(4, true);
     if constexpr (PF)
       NTM_PHP(0, true, -1, 10, true, false, -1, 1);
@@ -739,8 +743,9 @@ inline hipError_t launch_gemm_bf16_pp6_grid(const GemmArgs& a, int grid, hipStre
 template <int POL, int STAMP = 0, bool SPREAD = false, bool PF = false>
 inline hipError_t launch_gemm_bf16_pp6(const GemmArgs& a, hipStream_t stream) {
   if (!shape_ok6(a.M, a.N, a.K) || a.rowsum || a.lda < a.K || a.ldb < a.K || a.ldc < a.N ||
-      (a.lda % 8) || (a.ldb % 8) || (a.ldc % 8) || (STAMP != 0 && a.stamps == nullptr) ||
-      (PF && a.K < 6 * BK))
+      (a.lda % 8) || (a.ldb % 8) || (a.ldc % 8) ||
+      (STAMP != 0 && STAMP != 3 && a.stamps == nullptr) || (PF && a.K < 6 * BK) ||
+      (STAMP == 3 && (a.splitk_kc < 0 || a.K / BK - 2 * a.splitk_kc < 4)))
     return hipErrorInvalidValue;
   const int ntiles = (a.M / BM) * (a.N / BN);
   hipLaunchKernelGGL((gemm_bf16_pp6_kernel<POL, STAMP, false, false, SPREAD, false, PF>),

@@ -146,6 +146,15 @@ NTM_API int ntm_gemm_bf16_sk_nopair(const void* A, const void* B, void* C, int M
       a, ntm::gemm6::pp6_grid(1 << 30), ws, ws_bytes, S(stream));
 }
 
+// Ablation (round 6, profiles/r6_xcd): the shipping pingpong8o with each odd-XCD
+// workgroup's last tile cut by 2 * cut_pairs K-tiles (C is WRONG; timing only).
+NTM_API int ntm_gemm_bf16_pp6_oddcut(int cut_pairs, const void* A, const void* B, void* C, int M,
+                                     int N, int K, int lda, int ldb, int ldc, void* stream) {
+  ntm::gemm::GemmArgs a = args(A, B, C, M, N, K, lda, ldb, ldc);
+  a.splitk_kc = cut_pairs;
+  return (int)ntm::gemm6::launch_gemm_bf16_pp6<1, 3, true>(a, S(stream));
+}
+
 // pingpong8o boundary-phase stamps (gemm_bf16_pp6.hpp STAMP 2): grid 128 or 256
 // workgroups (a multiple of 8, <= tiles, each workgroup >= 2 tiles), store 1 =
 // C stored (nontemporal) / 0 = not stored / 2 = stored, spread over the boundary
