@@ -502,6 +502,7 @@ def main(argv=None) -> int:
         # dispatch with NTM_SK_CHECK=1 (a placement violation raises there), checked
         # against the fp32 reference; the word is recorded per rank.
         extras["sk_check_rank0"] = sk_product_check(backend, dev)
+        extras["sk_xcc_error"] = extras["sk_check_rank0"].get("sk_xcc_error")
         if not extras["sk_check_rank0"].get("ok"):
             verified = False
 

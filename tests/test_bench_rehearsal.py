@@ -178,7 +178,7 @@ def test_bench_on_one_gpu_json_contract(tmp_path):
     # NTM_SK_CHECK=1, verified and with a clear placement word
     sk = d["sk_check_rank0"]
     assert sk["ok"] and sk["bad"] == 0 and sk["sk_xcc_error"] == 0, sk
-    assert sk["variant"] in ("pp192x256s", "pp256x192s")
+    assert sk["variant"] in ("pp192x256s", "pp256x192s") and d["sk_xcc_error"] == 0
     # every SMI read is timed, the stamped clock batch count is
     # reported, and both kernels' energy per flop is measured
     assert len(d["per_rank_smi_sample_ms"][0]) >= 5
