@@ -186,7 +186,9 @@ def energy_compare(kernels: dict, sync, sample, smi_mod, window_s: float = ENERG
                   "joules_per_tflop": round(avg / tf, 4) if avg is not None and tf > 0 else None,
                   "windows_W": [w.get("avg_power_W") for w in per[k]],
                   "windows_s": [w.get("seconds") for w in per[k]],
-                  "ppt_pct": [w.get("ppt_pct") for w in per[k]]}
+                  "ppt_pct": [w.get("ppt_pct") for w in per[k]],
+                  # the firmware's gfx clock at each window's end
+                  "gfxclk_mhz": [(w.get("gfxclk_mhz") or [None, None])[1] for w in per[k]]}
     if len(names) == 2 and all(out[k]["joules_per_tflop"] for k in names):
         out[f"{names[0]}_over_{names[1]}_joules_per_tflop"] = round(
             out[names[0]]["joules_per_tflop"] / out[names[1]]["joules_per_tflop"], 4)
