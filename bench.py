@@ -461,6 +461,11 @@ def main(argv=None) -> int:
         timed_clk = round(cyc[len(cyc) // 2] / (my_seconds / args.steps) / 1e9, 4)
         gclk["ms_per_launch_over_ms_per_step"] = round(
             gclk["ms_per_launch"] / (my_seconds / args.steps * 1e3), 4)
+        # the stamped batch's clock measured the way the timed loop's is (median
+        # cycles / wall ms per launch, dispatch ramp and drain included): the
+        # like-for-like partner of per_rank_timed_loop_clock_GHz; bound_GHz counts
+        # only the stamp windows (bound_window_fraction of a step)
+        gclk["launch_wall_GHz"] = round(cyc[len(cyc) // 2] / (gclk["ms_per_launch"] * 1e-3) / 1e9, 4)
         # the stamped launches ran at the timed loop's pace: otherwise
         # their clock describes a different power state and must not label the rank
         gclk["clock_trusted"] = 0.95 <= gclk["ms_per_launch_over_ms_per_step"] <= 1.05
@@ -679,6 +684,8 @@ def main(argv=None) -> int:
         # stamped batches it took to get one whose per-launch windows agree within 3 %
         # (kernels.gemm_clock_stable), and whether that batch ran at the timed loop's
         # pace (ms per stamped launch / timed ms per step within 0.95-1.05)
+        "per_rank_gemm_launch_wall_clock_GHz": [(p["gemm_clock"] or {}).get("launch_wall_GHz")
+                                                for p in per_rank],
         "per_rank_clock_batches": [(p["gemm_clock"] or {}).get("clock_batches") for p in per_rank],
         "per_rank_clock_trusted": [(p["gemm_clock"] or {}).get("clock_trusted") for p in per_rank],
         # host time of every AMD SMI read per rank (init, window opens / closes), ms
