@@ -431,3 +431,29 @@ def test_splitk_priced_against_ragged_unsplit_time(splitk_plan):
         assert splitk_plan(3232, 936, 4024) == (3232, "tile128", "tile128", 1)
     finally:
         kernels.set_plan_splitk_ragged(True)
+
+
+def test_sk_check_flag_wiring(monkeypatch):
+    """NTM_SK_CHECK switches the product-path check on; with it on,
+    a set placement word raises SkPlacementError naming tile and XCCs, and the word is
+    read with clear=True; with it off the word is not read at all."""
+    calls = []
+
+    def fake_word(device=None, clear=True):
+        calls.append(clear)
+        return 0x80000000 | 1 << 28 | 42 << 8 | 3 << 4 | 5
+
+    monkeypatch.setattr(kernels, "sk_xcc_error", fake_word)
+    monkeypatch.delenv("NTM_SK_CHECK", raising=False)
+    assert not kernels.sk_check_enabled()
+    out = object()
+    assert kernels._sk_checked(None, out) is out and calls == []
+    monkeypatch.setenv("NTM_SK_CHECK", "0")
+    assert not kernels.sk_check_enabled()
+    monkeypatch.setenv("NTM_SK_CHECK", "1")
+    assert kernels.sk_check_enabled()
+    with pytest.raises(kernels.SkPlacementError, match=r"tile 42, combiner XCC 3, other XCC 5"):
+        kernels._sk_checked(None, out)
+    assert calls == [True]
+    monkeypatch.setattr(kernels, "sk_xcc_error", lambda device=None, clear=True: 0)
+    assert kernels._sk_checked(None, out) is out
