@@ -23,7 +23,8 @@ from nvidia_terraform_modules_amd.ops._lib import check, lib_experimental, strea
 
 FORMS = (("bf16_16x16x32", 0, 2 * 16 * 16 * 32, 8),
          ("bf16_32x32x16", 2, 2 * 32 * 32 * 16, 8),
-         ("fp8_16x16x128", 1, 2 * 16 * 16 * 128, 8))
+         ("fp8_16x16x128", 1, 2 * 16 * 16 * 128, 8),
+         ("fp8_32x32x64", 3, 2 * 32 * 32 * 64, 8))
 
 
 def main() -> int:

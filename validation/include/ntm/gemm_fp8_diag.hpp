@@ -107,7 +107,9 @@ __global__ void __launch_bounds__(256) mfma_rate_kernel(int iters, unsigned seed
     // 8 accumulators through v_accvgpr_mov chains every iteration
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      if constexpr (F8)
+      if constexpr (F8 && W32)  // f8f6f4 32x32x64: 2x the MACs per instruction
+        asm("v_mfma_f32_32x32x64_f8f6f4 %0, %1, %2, %0" : "+a"(acc32[j & 3]) : "v"(a), "v"(b));
+      else if constexpr (F8)
         ::ntm::gemm::mfma_f8_agpr(acc[j], a, b);
       else if constexpr (W32)  // 32x32x16: 2x the MACs per instruction, 4 accumulators of 16
         asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0"

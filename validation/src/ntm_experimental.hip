@@ -195,7 +195,10 @@ NTM_API int ntm_gemm_bf16_stamp(int mode, const void* A, const void* B, void* C,
 // 4 waves), sink: 1 float.
 NTM_API int ntm_mfma_rate(int f8, int grid, int iters, void* out, float* sink, void* stream) {
   if (grid <= 0 || iters <= 0) return (int)hipErrorInvalidValue;
-  if (f8 == 2)   // bf16 v_mfma_f32_32x32x16 (2x the MACs per instruction)
+  if (f8 == 3)   // e4m3 v_mfma_f32_32x32x64_f8f6f4 (2x the MACs of 16x16x128)
+    hipLaunchKernelGGL((ntm::fp8::mfma_rate_kernel<true, true>), dim3(grid), dim3(256), 0,
+                       S(stream), iters, 7u, (unsigned long long*)out, sink);
+  else if (f8 == 2)   // bf16 v_mfma_f32_32x32x16 (2x the MACs per instruction)
     hipLaunchKernelGGL((ntm::fp8::mfma_rate_kernel<false, true>), dim3(grid), dim3(256), 0,
                        S(stream), iters, 7u, (unsigned long long*)out, sink);
   else if (f8)
