@@ -1028,3 +1028,22 @@ def test_sk_placement_fault_raises_on_the_product_path(ops, monkeypatch, variant
     finally:
         ops.set_sk_fault_inject(False)
     assert ops.sk_xcc_error() != 0 and ops.sk_xcc_error() == 0
+
+
+@pytest.mark.parametrize("m,n,k", [(256, 256, 512), (2048, 1024, 1024), (4608, 4352, 2048)])
+def test_dma4k_energy_study_builds_match_the_default(ops, m, n, k):
+    """The 4-wave 128x128-per-wave builds restored for the energy study
+    (profiles/r6_fp8, tools/experiments/energy_ab.py): bf16 variant dma4k_d3 and
+    fp8 knob 12 agree with the default within tolerance (different MFMA order)."""
+    a = _rand(ops, (m, k), 51)
+    b = _rand(ops, (n, k), 52)
+    ref = a.float() @ b.float().T
+    atol, rtol = ops.gemm_tolerance(k)
+    c = ops.gemm_bf16(a, b, variant="dma4k_d3")
+    assert ((c.float() - ref).abs() <= atol + rtol * ref.abs()).all()
+    a8 = ops.fill_uniform_(torch.empty((m, 2 * k), dtype=torch.float8_e4m3fn, device="cuda"), 53)
+    b8 = ops.fill_uniform_(torch.empty((n, 2 * k), dtype=torch.float8_e4m3fn, device="cuda"), 54)
+    ref8 = a8.float() @ b8.float().T
+    atol8, rtol8 = ops.gemm_tolerance(2 * k)
+    c8 = ops.gemm_fp8(a8, b8, knob=12)
+    assert ((c8.float() - ref8).abs() <= atol8 + rtol8 * ref8.abs()).all()

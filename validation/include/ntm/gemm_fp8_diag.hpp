@@ -12,6 +12,7 @@
 #include "ntm/gemm_bf16_pp3.hpp"
 #include "ntm/gemm_fp8.hpp"
 #include "ntm/gemm_bf16_pp6.hpp"
+#include "ntm/gemm_w4k.hpp"
 
 namespace ntm {
 namespace fp8 {
@@ -58,6 +59,9 @@ inline hipError_t launch_gemm_fp8_knob(const void* A, const void* B, __bf16* C, 
     // 31: the same with the boundary stores spread over 7 phases (SPREAD, as the
     // shipping bf16 build)
     case 31: return ::ntm::gemm6::launch_gemm_fp8_pp6<true>(A, B, C, M, N, K, lda, ldb, ldc, s);
+    // 12 (restored in round 6 for the energy study, profiles/r6_fp8): the 4-wave
+    // one-barrier-per-K-tile kernel, 128x128 per wave, DMA every 2 MFMAs (gemm_w4k.hpp)
+    case 12: return ::ntm::w4k::launch_gemm_fp8_w4k<2>(A, B, C, M, N, K, lda, ldb, ldc, s);
     // 32 (round 6): knob 31 + the next tile's K-tiles 0 / 1 touched into L2 over
     // K-tiles T-4 / T-3 (PF; fp8 K >= 768)
     case 32: return ::ntm::gemm6::launch_gemm_fp8_pp6<true, true>(A, B, C, M, N, K, lda, ldb, ldc, s);

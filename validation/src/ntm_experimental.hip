@@ -30,6 +30,7 @@
 #include "ntm/gemm_bf16_pp3_stamp.hpp"
 #include "ntm/gemm_bf16_pp6.hpp"
 #include "ntm/gemm_bf16_sk.hpp"
+#include "ntm/gemm_w4k.hpp"
 #include "ntm/gemm_bf16_t128.hpp"
 #include "ntm/gemm_fp8_diag.hpp"
 #include "ntm/stream_policy_exp.hpp"
@@ -66,6 +67,10 @@ NTM_API int ntm_gemm_bf16_experimental(int variant, const void* A, const void* B
     case 11:
     case 12:
     case 13: return (int)ntm::gemm3::launch_gemm_bf16_pp3_knob(a, variant + 2, S(stream));
+    // 4 waves x 128x128, one barrier per K-tile, two K-tile LDS-DMA buffers, a DMA
+    // piece every 3 MFMA pairs (gemm_w4k.hpp; restored in round 6 for the energy
+    // study, profiles/r6_fp8)
+    case 39: return (int)ntm::w4k::launch_gemm_bf16_w4k<3>(a, S(stream));
     case 19: return (int)ntm::gemmt::launch_gemm_bf16_tile<4>(a, S(stream));
     case 20: return (int)ntm::gemmt::launch_gemm_bf16_tile<8>(a, S(stream));
     case 21: return (int)ntm::gemmt::launch_gemm_bf16_tile<5, 5>(a, S(stream));
