@@ -130,6 +130,7 @@ def _declare_experimental(lib: ctypes.CDLL) -> None:
             [c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp], c_int),
         "ntm_mfma_f8_probe": ([c_vp, c_vp, c_vp, c_vp], c_int),
         "ntm_mfma_rate": ([c_int, c_int, c_int, c_vp, c_vp, c_vp], c_int),
+        "ntm_mfma_toggle": ([c_int, c_int, c_int, c_vp, c_vp, c_vp], c_int),
         "ntm_dma_probe": ([c_int, c_vp, c_int, c_int, c_int, c_int, c_vp], c_int),
         "ntm_gemm_fp8_knob": ([c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                                c_vp], c_int),

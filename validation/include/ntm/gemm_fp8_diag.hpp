@@ -141,5 +141,73 @@ __global__ void __launch_bounds__(256) mfma_rate_kernel(int iters, unsigned seed
   }
 }
 
+// Operand-toggle energy probe (round 6): mfma_rate_kernel issues the same two
+// operand registers on every MFMA, so its power is that of an idle operand
+// path. This probe issues 16 v_mfma_f32_16x16x32_bf16 per iteration into 8
+// AGPR accumulators with the operands of a pp6 quadrant (a[4][2], b[2][2],
+// random bf16 bits) in one of these orders:
+//   PAT 0  fixed: a[0][0] x b[0][0] every MFMA (mfma_rate_kernel's load)
+//   PAT 1  zero operands
+//   PAT 2  one operand changes per MFMA (b alternates, a fixed)
+//   PAT 3  both operands change on every MFMA
+//   PAT 4  mma_q's order: ks, mt, nt (both change at every mt step)
+//   PAT 5  snake: ks, mt, nt reversed on odd mt (one operand changes per MFMA
+//          inside a ks; the 8-MFMA distance between dependent MFMAs is kept)
+// asm volatile pins the issue order.
+template <int PAT>
+__global__ void __launch_bounds__(256) mfma_toggle_kernel(int iters, unsigned seed,
+                                                          unsigned long long* out, float* sink) {
+  typedef int i32x4 __attribute__((ext_vector_type(4)));
+  const int lane = threadIdx.x & 63;
+  i32x4 a[4][2], b[2][2];
+#pragma unroll
+  for (int s = 0; s < 12; ++s) {
+    i32x4 v;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const unsigned h =
+          (unsigned)mix64(((unsigned long long)seed << 32) ^ (unsigned)((lane * 12 + s) * 4 + i));
+      v[i] = PAT == 1 ? 0 : (int)(h & 0xBFBFBFBFu);  // |x| < 2, random sign / mantissa
+    }
+    if (s < 8) a[s >> 1][s & 1] = v;
+    else b[(s - 8) >> 1][s & 1] = v;
+  }
+  f32x4 acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+  const unsigned long long r0 = __builtin_amdgcn_s_memrealtime();
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const int nt = PAT == 5 && (mt & 1) ? 1 - i : i;
+          const int j = mt * 2 + nt;
+          const int q = (ks * 4 + mt) * 2 + i;  // issue slot 0..15
+          const i32x4& sa = PAT <= 1   ? a[0][0]
+                            : PAT == 2 ? a[0][0]
+                            : PAT == 3 ? a[q & 1][0]
+                                       : a[mt][ks];
+          const i32x4& sb = PAT <= 1 ? b[0][0] : PAT <= 3 ? b[q & 1][0] : b[nt][ks];
+          asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[j]) : "v"(sb), "v"(sa));
+        }
+  }
+  ::ntm::gemm::mfma_drain();
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s += acc[j][0] + acc[j][1] + acc[j][2] + acc[j][3];
+  const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+  const unsigned long long r1 = __builtin_amdgcn_s_memrealtime();
+  if (s == 12345.678f) sink[0] = s;
+  if (lane == 0) {
+    const size_t w = (size_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+    out[2 * w] = t1 - t0;
+    out[2 * w + 1] = r1 - r0;
+  }
+}
+
 }  // namespace fp8
 }  // namespace ntm

@@ -215,6 +215,24 @@ NTM_API int ntm_mfma_rate(int f8, int grid, int iters, void* out, float* sink, v
   return (int)hipGetLastError();
 }
 
+// Operand-toggle energy probe (gemm_fp8_diag.hpp mfma_toggle_kernel): 16
+// bf16 16x16x32 MFMAs per iteration in operand order pat 0..5.
+NTM_API int ntm_mfma_toggle(int pat, int grid, int iters, void* out, float* sink, void* stream) {
+  if (grid <= 0 || iters <= 0) return (int)hipErrorInvalidValue;
+  auto* o = (unsigned long long*)out;
+  switch (pat) {
+#define NTM_TOGGLE(P)                                                                         \
+  case P:                                                                                     \
+    hipLaunchKernelGGL(ntm::fp8::mfma_toggle_kernel<P>, dim3(grid), dim3(256), 0, S(stream), \
+                       iters, 7u, o, sink);                                                   \
+    break;
+    NTM_TOGGLE(0) NTM_TOGGLE(1) NTM_TOGGLE(2) NTM_TOGGLE(3) NTM_TOGGLE(4) NTM_TOGGLE(5)
+#undef NTM_TOGGLE
+    default: return (int)hipErrorInvalidValue;
+  }
+  return (int)hipGetLastError();
+}
+
 // Wave-specialised tile kernel schedule knobs (gemm_bf16_t128.hpp kWs*):
 // shape 0 = 128x128, 1 = 256x128, 2 = 160x160; knob 0..8.
 template <int MT, int NT>
