@@ -2,8 +2,9 @@
 
 mfma_power.py's probe issues the same two operand registers on every MFMA.
 This one (gemm_fp8_diag.hpp mfma_toggle_kernel) issues a pp6 quadrant's 16
-v_mfma_f32_16x16x32_bf16 per iteration in six operand orders (fixed, zero,
-one operand changing, both changing, mma_q's order, snake order) and reports,
+v_mfma_f32_16x16x32_bf16 per iteration in seven forms (fixed, zero,
+one operand changing, both changing, mma_q's order, snake order, mma_q's
+order with VGPR instead of AGPR accumulators) and reports,
 for each, the sustained TF/s, clock, package power and joules per TFLOP under
 the power limit. Rounds interleave the patterns so that drift hits all alike.
 
@@ -25,7 +26,8 @@ import torch  # noqa: E402
 from nvidia_terraform_modules_amd.ops import smi  # noqa: E402
 from nvidia_terraform_modules_amd.ops._lib import check, lib_experimental, stream_handle  # noqa: E402
 
-PATTERNS = ("fixed", "zero", "one_changes", "both_change", "mma_q_order", "snake_order")
+PATTERNS = ("fixed", "zero", "one_changes", "both_change", "mma_q_order", "snake_order",
+            "mma_q_order_vgpr_acc")
 FLOP_PER_ITER = 16 * 2 * 16 * 16 * 32
 
 
@@ -60,6 +62,7 @@ def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--seconds", type=float, default=1.0)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--patterns", default="", help="comma-separated subset of the names")
     ap.add_argument("--iters", type=int, default=10000)
     ap.add_argument("--grid", type=int, default=256)
     args = ap.parse_args()
@@ -69,7 +72,8 @@ def main() -> int:
     L = lib_experimental()
     rows = {name: [] for name in PATTERNS}
     for r in range(args.rounds):
-        order = range(len(PATTERNS)) if r % 2 == 0 else reversed(range(len(PATTERNS)))
+        pats = [PATTERNS.index(p) for p in args.patterns.split(",")] if args.patterns else list(range(len(PATTERNS)))
+        order = pats if r % 2 == 0 else pats[::-1]
         for pat in order:
             row = run(L, pat, args.grid, args.iters, args.seconds, out, sink, dev)
             row["round"] = r
@@ -77,6 +81,8 @@ def main() -> int:
             print(json.dumps(row), flush=True)
     summary = {}
     for name, rs in rows.items():
+        if not rs:
+            continue
         summary[name] = {k: statistics.median([x[k] for x in rs if x[k] is not None] or [0])
                          for k in ("tflops", "clock_GHz", "avg_power_W", "j_per_tflop")}
     print(json.dumps({"summary": summary}), flush=True)

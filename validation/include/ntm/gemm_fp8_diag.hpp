@@ -153,6 +153,8 @@ __global__ void __launch_bounds__(256) mfma_rate_kernel(int iters, unsigned seed
 //   PAT 4  mma_q's order: ks, mt, nt (both change at every mt step)
 //   PAT 5  snake: ks, mt, nt reversed on odd mt (one operand changes per MFMA
 //          inside a ks; the 8-MFMA distance between dependent MFMAs is kept)
+//   PAT 6  PAT 4 with the accumulators in arch VGPRs (K1 bf16's form) instead
+//          of AGPRs (hipBLASLt's form)
 // asm volatile pins the issue order.
 template <int PAT>
 __global__ void __launch_bounds__(256) mfma_toggle_kernel(int iters, unsigned seed,
@@ -192,7 +194,10 @@ __global__ void __launch_bounds__(256) mfma_toggle_kernel(int iters, unsigned se
                             : PAT == 3 ? a[q & 1][0]
                                        : a[mt][ks];
           const i32x4& sb = PAT <= 1 ? b[0][0] : PAT <= 3 ? b[q & 1][0] : b[nt][ks];
-          asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[j]) : "v"(sb), "v"(sa));
+          if constexpr (PAT == 6)
+            asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(acc[j]) : "v"(sb), "v"(sa));
+          else
+            asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[j]) : "v"(sb), "v"(sa));
         }
   }
   ::ntm::gemm::mfma_drain();

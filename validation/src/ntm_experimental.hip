@@ -216,7 +216,7 @@ NTM_API int ntm_mfma_rate(int f8, int grid, int iters, void* out, float* sink, v
 }
 
 // Operand-toggle energy probe (gemm_fp8_diag.hpp mfma_toggle_kernel): 16
-// bf16 16x16x32 MFMAs per iteration in operand order pat 0..5.
+// bf16 16x16x32 MFMAs per iteration in operand order pat 0..6.
 NTM_API int ntm_mfma_toggle(int pat, int grid, int iters, void* out, float* sink, void* stream) {
   if (grid <= 0 || iters <= 0) return (int)hipErrorInvalidValue;
   auto* o = (unsigned long long*)out;
@@ -227,6 +227,7 @@ NTM_API int ntm_mfma_toggle(int pat, int grid, int iters, void* out, float* sink
                        iters, 7u, o, sink);                                                   \
     break;
     NTM_TOGGLE(0) NTM_TOGGLE(1) NTM_TOGGLE(2) NTM_TOGGLE(3) NTM_TOGGLE(4) NTM_TOGGLE(5)
+    NTM_TOGGLE(6)
 #undef NTM_TOGGLE
     default: return (int)hipErrorInvalidValue;
   }
