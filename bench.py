@@ -18,7 +18,10 @@ without a cloud account; this measures the GPU half on real hardware:
   check, C1 RCCL all-reduce busbw sweep (N > 1; --p2p adds the per-pair
   send/recv link matrix), the validation Job's own binary on the same n
   GPUs (its process-start -> verdict time), and the in-node
-  time-to-GPU-ready phases (process start -> HIP init -> verified).
+  time-to-GPU-ready phases (process start -> HIP init -> verified). All of it
+  runs under a deadline (``--extras-timeout-s``, ExtrasWatchdog): if a hung
+  peer or link blocks a collective, rank 0 still prints the line, with
+  ``extras_timed_out`` naming the phase.
 
 Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--size 8192]
 For N > 1 the driver launches it under ``torch.distributed.run``; launched
@@ -70,6 +73,11 @@ def parse(argv=None):
                     help="skip running the validation Job binary (amdgpu-validate) on the n GPUs "
                          "after the timed region")
     ap.add_argument("--out", default="", help="also write the JSON line to this file")
+    ap.add_argument("--extras-timeout-s", type=float, default=300.0,
+                    help="deadline for everything after the timed region (verification, "
+                         "comparisons, collective sweeps, the Job): past it rank 0 prints the "
+                         "JSON line with what it has and extras_timed_out = the phase it was in, "
+                         "and every rank exits (ExtrasWatchdog)")
     ap.add_argument("--rehearsal", action="store_true",
                     help="CPU/gloo + PyTorch reference ops: rehearses the multi-process "
                          "orchestration and the JSON contract; NOT a measurement (tests only)")
@@ -301,6 +309,62 @@ def pair_busbw(rccl, xgmi) -> list:
             for r in xgmi if r.bytes in rccl_at]
 
 
+class ExtrasWatchdog:
+    """Deadline for the work after the timed region, on every rank.
+
+    The headline number is final once the per-rank results are gathered. What
+    follows (verification, the hipBLASLt comparison, the RCCL and xGMI sweeps,
+    the Job binary) runs collectives that a hung peer or link would block
+    forever, and then no JSON line would come out. When the deadline passes,
+    rank 0 prints the line from what it has, with ``extras_timed_out`` naming the
+    phase it was in, and every rank leaves with ``os._exit`` (a blocked collective
+    cannot be unwound). ``phase`` is set by the main thread as it goes.
+
+    ``NTM_BENCH_INJECT_HANG=<phase>:<rank>`` makes that rank stall when it enters
+    that phase (tests of this path only)."""
+
+    def __init__(self, seconds: float, rank: int, on_expire):
+        import threading
+
+        self.phase = "verify"
+        self.rank = rank
+        self._lock = threading.Lock()
+        self._owner = None          # "main" or "deadline": who prints and exits
+        self._on_expire = on_expire
+        self._t = threading.Timer(seconds, self._fire) if seconds > 0 else None
+        if self._t is not None:
+            self._t.daemon = True
+            self._t.start()
+
+    def enter(self, phase: str) -> None:
+        self.phase = phase
+        if os.environ.get("NTM_BENCH_INJECT_HANG") == f"{phase}:{self.rank}":
+            time.sleep(3600)
+
+    def claim(self) -> bool:
+        """The main thread is done: True if it still owns the output (the
+        deadline has not fired), and the deadline can no longer fire."""
+        with self._lock:
+            if self._owner is None:
+                self._owner = "main"
+        if self._t is not None:
+            self._t.cancel()
+        return self._owner == "main"
+
+    def _fire(self) -> None:
+        with self._lock:
+            if self._owner is not None:
+                return
+            self._owner = "deadline"
+        code = 0
+        try:
+            code = self._on_expire(self.phase)
+        finally:
+            sys.stdout.flush()
+            sys.stderr.flush()
+            os._exit(code)
+
+
 def relaunch_distributed(args) -> int:
     """Start torch.distributed.run as a CHILD process (never exec) and return its rc."""
     port = os.environ.get("MASTER_PORT", "29531")
@@ -489,13 +553,34 @@ def main(argv=None) -> int:
                                          "power_steady": power_steady, "power_src": power_src,
                                          "smi_ms": smi_ms})
 
-    def _pw(p: dict, key: str):
-        src = p["power"] if p["power_src"] == "timed_loop" else p["power_steady"]
-        return (src or {}).get(key)
+    make_line = _make_line_factory(args, n, prewarm, wall_elapsed, ms_per_step, total_tflops,
+                                   per_rank)
 
-    # ---- after the timed region: verification + context measurements
+    def emit(line: dict) -> None:
+        if env.is_main:
+            s = json.dumps(line)
+            print(s, flush=True)
+            if args.out:
+                with open(args.out, "w") as f:
+                    f.write(s + "\n")
+
+    # ---- after the timed region: verification + context measurements, under a
+    # deadline (ExtrasWatchdog): a hung collective must not swallow the JSON line
     extras: dict = {}
     verified = None
+
+    def on_deadline(phase: str) -> int:
+        if env.is_main:
+            line = make_line(dict(extras), verified)
+            line["extras_timed_out"] = phase
+            line["extras_timeout_s"] = args.extras_timeout_s
+            emit(line)
+            print(f"[bench] extras deadline ({args.extras_timeout_s:.0f} s) passed in phase "
+                  f"{phase!r}: JSON line printed, exiting", file=sys.stderr)
+        return 0 if verified in (None, True) else 1
+
+    wd = ExtrasWatchdog(args.extras_timeout_s, env.rank, on_deadline)
+    wd.enter("verify")
     if not args.no_check:
         rep = wl.verify()
         bad = dist.all_reduce_sum(env, float(rep.bad))
@@ -503,6 +588,7 @@ def main(argv=None) -> int:
         extras["verify_rank0"] = rep.as_dict()
         extras["verify_bad_total"] = int(bad)
     _CLOCK.mark("gemm_verified")
+    wd.enter("sk_check")
     if not args.no_check and dev.type == "cuda" and hasattr(backend, "sk_check_enabled"):
         # stream-K placement check on the product path: the split-mode
         # shape the default plan runs on a 192-wide tile, through the default
@@ -514,6 +600,7 @@ def main(argv=None) -> int:
             verified = False
 
     gpu_extras = not args.no_extras and not args.rehearsal
+    wd.enter("hipblaslt_compare")
     if gpu_extras:
         # K1 vs hipBLASLt on the same operands, INTERLEAVED (ABAB rounds, median of
         # each), after re-settling the clock on hipBLASLt itself: neither side gets
@@ -562,6 +649,7 @@ def main(argv=None) -> int:
     if dev.type == "cuda":
         torch.cuda.empty_cache()
 
+    wd.enter("hbm")
     if gpu_extras:
         h = hbm_check(dev, 2 << 30, 10)
         extras["hbm_copy_GBps_rank0"] = h["copy_GBps"]
@@ -569,6 +657,7 @@ def main(argv=None) -> int:
         extras["hbm_capacity_gb"] = h["capacity_total_gb"]
     _CLOCK.mark("hbm_checked")
 
+    wd.enter("rccl_sweep")
     if not args.no_extras and n > 1:
         # nccl-tests style: bf16 from 8 B (latency end) and fp32 from 1 MiB, x4 steps
         max_b = int(dist.all_reduce_max(env, -coll.max_message_bytes(
@@ -607,6 +696,7 @@ def main(argv=None) -> int:
             # JSON shape and the hand-over.
             from nvidia_terraform_modules_amd.parallel import xgmi as xg
 
+            wd.enter("xgmi")
             xs = [b for b in coll.sweep_sizes(8, max_b, 4)
                   if 512 <= b <= 1 << 30 and (b // 2) % (8 * n) == 0]
             fac = None
@@ -628,103 +718,114 @@ def main(argv=None) -> int:
         # Every rank's GPU work is done (barrier); the other ranks then leave, and
         # rank 0 touches no GPU between the child and its print, so whatever the
         # child does, the JSON line still comes out.
+        wd.enter("job")
         dist.barrier(env)
         if not env.is_main:
+            if not wd.claim():
+                time.sleep(3600)   # the deadline's thread is exiting the process
             dist.shutdown(env)
             return 0 if verified in (None, True) else 1
         extras["validation_job"] = run_validation_job(n)
+    wd.enter("report")
     _CLOCK.mark("done")
-
-    line = {
-        "metric": METRIC,
-        "value_component": VALUE_COMPONENT,
-        "value": round(total_tflops, 2),
-        "unit": "TFLOP/s",
-        "n_gpus": n,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(ms_per_step, 4),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "bf16",
-        "data": ("REHEARSAL: CPU/gloo + PyTorch reference ops - orchestration test, NOT a "
-                 "measurement" if args.rehearsal else
-                 "SHARED-GPU REHEARSAL: every rank on cuda:0, gloo group - NOT a measurement"
-                 if args.shared_gpu else
-                 "synthetic (uniform[-1,1) bf16 operands generated on device, hash RNG)"),
-        "config": {
-            "model": f"validation-job K1 GEMM C[{args.size}x{args.size}] = A[{args.size}x{args.size}]"
-                     f" * B[{args.size}x{args.size}]^T, bf16 in/out, fp32 accumulate",
-            "global_batch": n,
-            "seq_len": args.size,
-            "parallelism": f"dp{n}",
-            "baseline_config": BASELINE_CONFIG,
-        },
-        "verified": verified,
-        "timing": "HIP events around the K launches (max over ranks); host clock "
-                  "around the barrier+sync-bracketed region in timed_region_wall_s",
-        "timed_region_wall_s": round(wall_elapsed, 6),
-        "prewarm_s": prewarm["seconds"],
-        "prewarm_launches": prewarm["launches"],
-        # in-node part of time-to-GPU-ready = the Job binary's process start -> verdict on
-        # these n GPUs; the bench process's own (torch import included) is kept beside it
-        "time_to_gpu_ready_in_node_s": (
-            round(extras["validation_job"]["process_start_to_verdict_s"], 3)
-            if (extras.get("validation_job") or {}).get("passed") else None),
-        "bench_process_to_verified_s": round(_CLOCK.elapsed("gemm_verified"), 3),
-        "in_node_phases_s": {k: round(v, 4) for k, v in _CLOCK.durations().items()},
-        "per_rank_tflops": [p["tflops"] for p in per_rank],
-        # in-kernel clock: per stamped launch the median workgroup's cycles / window,
-        # median over launches (within 2-3 % of the PMC clock, profiles/r4_clock/)
-        # the launch-bounding clock: per stamped launch the slowest XCD's median
-        # workgroup clock (every XCD gets the same tiles, so it finishes last);
-        # the all-workgroup median beside it, and the per-XCD spread
-        "per_rank_gemm_clock_GHz": [(p["gemm_clock"] or {}).get("bound_GHz") for p in per_rank],
-        # stamped batches it took to get one whose per-launch windows agree within 3 %
-        # (kernels.gemm_clock_stable), and whether that batch ran at the timed loop's
-        # pace (ms per stamped launch / timed ms per step within 0.95-1.05)
-        "per_rank_gemm_launch_wall_clock_GHz": [(p["gemm_clock"] or {}).get("launch_wall_GHz")
-                                                for p in per_rank],
-        "per_rank_clock_batches": [(p["gemm_clock"] or {}).get("clock_batches") for p in per_rank],
-        "per_rank_clock_trusted": [(p["gemm_clock"] or {}).get("clock_trusted") for p in per_rank],
-        # host time of every AMD SMI read per rank (init, window opens / closes), ms
-        "per_rank_smi_sample_ms": [p["smi_ms"] for p in per_rank],
-        "per_rank_gemm_clock_median_GHz": [(p["gemm_clock"] or {}).get("launch_GHz")
-                                           for p in per_rank],
-        "per_rank_xcd_clock_spread_pct": [(p["gemm_clock"] or {}).get("xcc_clock_spread_pct")
-                                          for p in per_rank],
-        "per_rank_gemm_clock_p10_GHz": [(p["gemm_clock"] or {}).get("p10_GHz") for p in per_rank],
-        "per_rank_gemm_clock": [p["gemm_clock"] for p in per_rank],
-        # median shader cycles per stamped launch / the rank's own timed ms per step
-        "per_rank_timed_loop_clock_GHz": [p["timed_loop_clock"] for p in per_rank],
-        # AMD SMI per rank: average power (energy counter), PPT (power) and
-        # socket-thermal throttle residency in % of firmware iterations, from the
-        # window named in per_rank_power_window: "timed_loop" = [last warmup launches
-        # .. end of the timed loop]; "steady_window" = >= 0.5 s of the same K1 right
-        # after it (the timed window was under 0.1 s or stale). Both
-        # raw windows (power / temperature / clock at both ends) are kept.
-        "per_rank_avg_power_W": [_pw(p, "avg_power_W") for p in per_rank],
-        "per_rank_ppt_throttle_pct": [_pw(p, "ppt_pct") for p in per_rank],
-        "per_rank_thermal_throttle_pct": [_pw(p, "thermal_pct") for p in per_rank],
-        "per_rank_power_window": [p["power_src"] for p in per_rank],
-        "per_rank_power": [p["power"] for p in per_rank],
-        "per_rank_power_steady": [p["power_steady"] for p in per_rank],
-        "per_rank_clock_GHz": [(p["clock"] or {}).get("median_GHz") for p in per_rank],
-        "per_rank_clock_probe": [p["clock"] for p in per_rank],
-        "vs_baseline_note": "reference publishes no TFLOP/s or busbw (BASELINE.json published={})",
-        **({"rehearsal": True} if args.rehearsal else {}),
-        **({"shared_gpu_rehearsal": True} if args.shared_gpu else {}),
-        **extras,
-    }
-    if env.is_main:
-        s = json.dumps(line)
-        print(s, flush=True)
-        if args.out:
-            with open(args.out, "w") as f:
-                f.write(s + "\n")
+    line = make_line(extras, verified)
+    if not wd.claim():
+        time.sleep(3600)       # the deadline's thread printed the line and is exiting
+    emit(line)
     dist.shutdown(env)
     return 0 if verified in (None, True) else 1
+
+
+def _make_line_factory(args, n, prewarm, wall_elapsed, ms_per_step, total_tflops, per_rank):
+    def _pw(p: dict, key: str):
+        src = p["power"] if p["power_src"] == "timed_loop" else p["power_steady"]
+        return (src or {}).get(key)
+
+    def make_line(extras: dict, verified) -> dict:
+        return {
+            "metric": METRIC,
+            "value_component": VALUE_COMPONENT,
+            "value": round(total_tflops, 2),
+            "unit": "TFLOP/s",
+            "n_gpus": n,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": ("REHEARSAL: CPU/gloo + PyTorch reference ops - orchestration test, NOT a "
+                     "measurement" if args.rehearsal else
+                     "SHARED-GPU REHEARSAL: every rank on cuda:0, gloo group - NOT a measurement"
+                     if args.shared_gpu else
+                     "synthetic (uniform[-1,1) bf16 operands generated on device, hash RNG)"),
+            "config": {
+                "model": f"validation-job K1 GEMM C[{args.size}x{args.size}] = A[{args.size}x{args.size}]"
+                         f" * B[{args.size}x{args.size}]^T, bf16 in/out, fp32 accumulate",
+                "global_batch": n,
+                "seq_len": args.size,
+                "parallelism": f"dp{n}",
+                "baseline_config": BASELINE_CONFIG,
+            },
+            "verified": verified,
+            "timing": "HIP events around the K launches (max over ranks); host clock "
+                      "around the barrier+sync-bracketed region in timed_region_wall_s",
+            "timed_region_wall_s": round(wall_elapsed, 6),
+            "prewarm_s": prewarm["seconds"],
+            "prewarm_launches": prewarm["launches"],
+            # in-node part of time-to-GPU-ready = the Job binary's process start -> verdict on
+            # these n GPUs; the bench process's own (torch import included) is kept beside it
+            "time_to_gpu_ready_in_node_s": (
+                round(extras["validation_job"]["process_start_to_verdict_s"], 3)
+                if (extras.get("validation_job") or {}).get("passed") else None),
+            "bench_process_to_verified_s": round(_CLOCK.elapsed("gemm_verified"), 3),
+            "in_node_phases_s": {k: round(v, 4) for k, v in _CLOCK.durations().items()},
+            "per_rank_tflops": [p["tflops"] for p in per_rank],
+            # in-kernel clock: per stamped launch the median workgroup's cycles / window,
+            # median over launches (within 2-3 % of the PMC clock, profiles/r4_clock/)
+            # the launch-bounding clock: per stamped launch the slowest XCD's median
+            # workgroup clock (every XCD gets the same tiles, so it finishes last);
+            # the all-workgroup median beside it, and the per-XCD spread
+            "per_rank_gemm_clock_GHz": [(p["gemm_clock"] or {}).get("bound_GHz") for p in per_rank],
+            # stamped batches it took to get one whose per-launch windows agree within 3 %
+            # (kernels.gemm_clock_stable), and whether that batch ran at the timed loop's
+            # pace (ms per stamped launch / timed ms per step within 0.95-1.05)
+            "per_rank_gemm_launch_wall_clock_GHz": [(p["gemm_clock"] or {}).get("launch_wall_GHz")
+                                                    for p in per_rank],
+            "per_rank_clock_batches": [(p["gemm_clock"] or {}).get("clock_batches") for p in per_rank],
+            "per_rank_clock_trusted": [(p["gemm_clock"] or {}).get("clock_trusted") for p in per_rank],
+            # host time of every AMD SMI read per rank (init, window opens / closes), ms
+            "per_rank_smi_sample_ms": [p["smi_ms"] for p in per_rank],
+            "per_rank_gemm_clock_median_GHz": [(p["gemm_clock"] or {}).get("launch_GHz")
+                                               for p in per_rank],
+            "per_rank_xcd_clock_spread_pct": [(p["gemm_clock"] or {}).get("xcc_clock_spread_pct")
+                                              for p in per_rank],
+            "per_rank_gemm_clock_p10_GHz": [(p["gemm_clock"] or {}).get("p10_GHz") for p in per_rank],
+            "per_rank_gemm_clock": [p["gemm_clock"] for p in per_rank],
+            # median shader cycles per stamped launch / the rank's own timed ms per step
+            "per_rank_timed_loop_clock_GHz": [p["timed_loop_clock"] for p in per_rank],
+            # AMD SMI per rank: average power (energy counter), PPT (power) and
+            # socket-thermal throttle residency in % of firmware iterations, from the
+            # window named in per_rank_power_window: "timed_loop" = [last warmup launches
+            # .. end of the timed loop]; "steady_window" = >= 0.5 s of the same K1 right
+            # after it (the timed window was under 0.1 s or stale). Both
+            # raw windows (power / temperature / clock at both ends) are kept.
+            "per_rank_avg_power_W": [_pw(p, "avg_power_W") for p in per_rank],
+            "per_rank_ppt_throttle_pct": [_pw(p, "ppt_pct") for p in per_rank],
+            "per_rank_thermal_throttle_pct": [_pw(p, "thermal_pct") for p in per_rank],
+            "per_rank_power_window": [p["power_src"] for p in per_rank],
+            "per_rank_power": [p["power"] for p in per_rank],
+            "per_rank_power_steady": [p["power_steady"] for p in per_rank],
+            "per_rank_clock_GHz": [(p["clock"] or {}).get("median_GHz") for p in per_rank],
+            "per_rank_clock_probe": [p["clock"] for p in per_rank],
+            "vs_baseline_note": "reference publishes no TFLOP/s or busbw (BASELINE.json published={})",
+            **({"rehearsal": True} if args.rehearsal else {}),
+            **({"shared_gpu_rehearsal": True} if args.shared_gpu else {}),
+            **extras,
+        }
+
+    return make_line
 
 
 if __name__ == "__main__":

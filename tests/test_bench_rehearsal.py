@@ -57,6 +57,7 @@ def test_torchrun_launch_one_json_line(nproc):
     assert d["config"]["parallelism"] == f"dp{nproc}" and d["config"]["global_batch"] == nproc
     assert d["higher_is_better"] is True and d["scaling"] == "weak" and d["dtype"] == "bf16"
     assert d["value"] > 0 and d["verified"] is True and d["rehearsal"] is True
+    assert "extras_timed_out" not in d                  # the deadline did not fire
     assert "NOT a measurement" in d["data"]
     # clock-settle pre-warm (untimed, wall-time based) and event timing are reported
     assert d["prewarm_s"] >= 0.2 and d["prewarm_launches"] > 0
@@ -119,6 +120,33 @@ def test_torchrun_launch_one_json_line(nproc):
         assert d["allreduce_bf16"][0]["bytes"] == 8
         pm = d["p2p_send_GBps"]
         assert pm["ranks"] == nproc and pm["errors"] == 0 and pm["min_GBps"] > 0
+
+
+@pytest.mark.parametrize("phase", ["xgmi", "rccl_sweep"])
+def test_hung_collective_still_prints_the_line(phase):
+    """A peer that hangs after the timed region (here rank 1, injected at the start
+    of a collective phase) must not swallow the JSON line: at the extras deadline
+    rank 0 prints the line it has, naming the phase, and every rank exits."""
+    env = _env()
+    env["NTM_BENCH_INJECT_HANG"] = f"{phase}:1"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_port()}", str(ROOT / "bench.py"),
+           "--gpus", "2", "--steps", "2", "--warmup", "1", "--size", "256",
+           "--allreduce-max-mib", "1", "--rehearsal", "--prewarm-s", "0.1",
+           "--extras-timeout-s", "25"]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = _json_lines(p.stdout)
+    assert len(lines) == 1, p.stdout[-2000:]
+    d = lines[0]
+    assert CONTRACT_KEYS <= set(d) and d["value"] > 0 and d["n_gpus"] == 2
+    assert d["extras_timed_out"] == phase and d["extras_timeout_s"] == 25
+    assert d["verified"] is True            # the GEMM check ran before the hang
+    assert "validation_job" not in d
+    if phase == "xgmi":                     # what ran before the hang is kept
+        assert d["allreduce_bf16"] and "xgmi_allreduce_bf16" not in d
+    else:
+        assert "allreduce_bf16" not in d
 
 
 def test_self_relaunch_as_child_process():
