@@ -15,6 +15,9 @@
 //         in LDS; the data is the wrong k window - timing only).
 // MODE 2: at a misaligned pitch, each row re-based down to its aligned line -
 //         the aligned pattern on the same rows (what a 3-line ring would load).
+// MODE 3: MODE 0's bytes, but each instruction covers 8 rows x 128 B (8 lanes
+//         per row: whole lines) instead of 16 rows x 64 B (each line split over
+//         two instructions): the energy question of profiles/r6_edec.
 #pragma once
 
 #include "ntm/gemm_bf16.hpp"
@@ -46,12 +49,12 @@ __global__ void __launch_bounds__(512) dma_probe_kernel(const __bf16* base, int 
   __shared__ __attribute__((aligned(16))) char smem[2 * kTileBytes];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int r = lane >> 2, cl = lane & 3;
+  const int r = MODE == 3 ? lane >> 3 : lane >> 2, cl = MODE == 3 ? lane & 7 : lane & 3;
   const char* rows[4];
 #pragma unroll
   for (int h = 0; h < 4; ++h) {
     const char* p = (const char*)(base + (size_t)(h * 128 + w * 16 + r) * pitch);
-    if constexpr (MODE != 0) p = (const char*)((size_t)p & ~(size_t)127);
+    if constexpr (MODE == 1 || MODE == 2) p = (const char*)((size_t)p & ~(size_t)127);
     rows[h] = p;
   }
   for (int rep = 0; rep < reps; ++rep) {
@@ -63,6 +66,9 @@ __global__ void __launch_bounds__(512) dma_probe_kernel(const __bf16* base, int 
         if constexpr (MODE == 1) {
           s1 = rows[h] + (size_t)t * 128 + 64 + cl * 16;
           s2 = rows[h] + (size_t)(t + 1) * 128 + cl * 16;
+        } else if constexpr (MODE == 3) {   // rows r and r + 8, whole 128-B lines
+          s1 = rows[h] + (size_t)t * 128 + cl * 16;
+          s2 = s1 + (size_t)8 * pitch * 2;
         } else {
           s1 = rows[h] + (size_t)t * 128 + cl * 16;
           s2 = s1 + 64;
@@ -101,6 +107,10 @@ inline hipError_t launch_dma_probe(int mode, const __bf16* base, int pitch, int 
   }
   const int d = mode / 10;
   mode %= 10;
+  if (mode == 3 && d == 0) {
+    hipLaunchKernelGGL((dma_probe_kernel<3, 10>), dim3(grid), dim3(512), 0, s, base, pitch, T, reps);
+    return hipGetLastError();
+  }
   if (mode > 2 || d > 3) return hipErrorInvalidValue;
 #define NTM_DPROBE(M, V) \
   if (mode == M && (V) == (d == 0 ? 10 : d == 1 ? 16 : d == 2 ? 24 : 32)) \
