@@ -19,9 +19,10 @@ without a cloud account; this measures the GPU half on real hardware:
   send/recv link matrix), the validation Job's own binary on the same n
   GPUs (its process-start -> verdict time), and the in-node
   time-to-GPU-ready phases (process start -> HIP init -> verified). All of it
-  runs under a deadline (``--extras-timeout-s``, ExtrasWatchdog): if a hung
-  peer or link blocks a collective, rank 0 still prints the line, with
-  ``extras_timed_out`` naming the phase.
+  but the Job child (which has its own time limit) runs under a deadline
+  (``--extras-timeout-s``, ExtrasWatchdog): if a hung peer or link blocks a
+  collective, rank 0 still prints the line, with ``extras_timed_out`` naming
+  the phase.
 
 Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--size 8192]
 For N > 1 the driver launches it under ``torch.distributed.run``; launched
@@ -74,8 +75,9 @@ def parse(argv=None):
                          "after the timed region")
     ap.add_argument("--out", default="", help="also write the JSON line to this file")
     ap.add_argument("--extras-timeout-s", type=float, default=300.0,
-                    help="deadline for everything after the timed region (verification, "
-                         "comparisons, collective sweeps, the Job): past it rank 0 prints the "
+                    help="deadline for the work after the timed region (verification, "
+                         "comparisons, collective sweeps; the Job child has its own limit): past "
+                         "it rank 0 prints the "
                          "JSON line with what it has and extras_timed_out = the phase it was in, "
                          "and every rank exits (ExtrasWatchdog)")
     ap.add_argument("--rehearsal", action="store_true",
@@ -313,9 +315,11 @@ class ExtrasWatchdog:
     """Deadline for the work after the timed region, on every rank.
 
     The headline number is final once the per-rank results are gathered. What
-    follows (verification, the hipBLASLt comparison, the RCCL and xGMI sweeps,
-    the Job binary) runs collectives that a hung peer or link would block
-    forever, and then no JSON line would come out. When the deadline passes,
+    follows (verification, the hipBLASLt comparison, the RCCL and xGMI sweeps)
+    runs collectives that a hung peer or link would block forever, and then no
+    JSON line would come out. The deadline is disarmed before the Job binary
+    runs: that child has its own time limit, and exiting under it would leave
+    it running on the GPUs. When the deadline passes,
     rank 0 prints the line from what it has, with ``extras_timed_out`` naming the
     phase it was in, and every rank leaves with ``os._exit`` (a blocked collective
     cannot be unwound). ``phase`` is set by the main thread as it goes.
@@ -725,6 +729,10 @@ def main(argv=None) -> int:
                 time.sleep(3600)   # the deadline's thread is exiting the process
             dist.shutdown(env)
             return 0 if verified in (None, True) else 1
+        # the Job child has its own time limit; the deadline stops here, so it never
+        # exits this process with the child still running on the GPUs
+        if not wd.claim():
+            time.sleep(3600)   # the deadline's thread is exiting the process
         extras["validation_job"] = run_validation_job(n)
     wd.enter("report")
     _CLOCK.mark("done")
