@@ -28,4 +28,5 @@ module "amd_gpu_stack" {
   validation_image        = var.gpu_validation_image
   validation_tflops_floor = var.gpu_validation_tflops_floor
   validation_gpu_count    = var.gpus_per_node
+  validation_node_count   = max(1, var.gpu_node_pool_count)
 }

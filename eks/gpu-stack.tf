@@ -31,6 +31,7 @@ module "amd_gpu_stack" {
   validation_enabled      = var.gpu_validation_enabled
   validation_image        = var.gpu_validation_image
   validation_gpu_count    = var.gpus_per_node
+  validation_node_count   = max(1, var.desired_count_gpu_nodes)
   validation_tflops_floor = var.gpu_validation_tflops_floor
 
   depends_on = [module.eks, module.cpu_node_pool]

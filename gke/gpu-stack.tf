@@ -30,6 +30,7 @@ module "amd_gpu_stack" {
   validation_image        = var.gpu_validation_image
   validation_tflops_floor = var.gpu_validation_tflops_floor
   validation_gpu_count    = tonumber(var.gpu_count)
+  validation_node_count   = max(1, var.num_gpu_nodes * length(var.node_zones))
 
   depends_on = [google_container_node_pool.system]
 }

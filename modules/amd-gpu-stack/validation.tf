@@ -9,9 +9,14 @@
   the hand-written HIP bf16 / fp8 MFMA GEMMs + HBM stream + RCCL all-reduce
   over xGMI + a per-link xGMI pull matrix. Job completion timestamp == end of
   time-to-GPU-ready.
+  One pod per GPU node (validation_node_count, from the pools' size at
+  creation): all pods run at once, a required anti-affinity on the hostname
+  puts each on its own node, and the Job completes when every node passed.
 ********************************************/
 locals {
-  validation_multi_gpu = var.validation_gpu_count > 1
+  validation_multi_gpu  = var.validation_gpu_count > 1
+  validation_multi_node = var.validation_node_count > 1
+  validation_labels     = merge(local.common_labels, { "app.kubernetes.io/name" = "amd-gpu-validation" })
   validation_args = concat(
     [
       "--gpus", tostring(var.validation_gpu_count),
@@ -55,7 +60,7 @@ resource "kubernetes_job_v1" "gpu_validation" {
   metadata {
     name      = "amd-gpu-validation"
     namespace = local.namespace
-    labels    = merge(local.common_labels, { "app.kubernetes.io/name" = "amd-gpu-validation" })
+    labels    = local.validation_labels
     annotations = {
       "amd-gpu-stack/gpu-node-pools" = local.node_pool_hash
       "amd-gpu-stack/stack-mode"     = var.gpu_stack_mode
@@ -63,20 +68,35 @@ resource "kubernetes_job_v1" "gpu_validation" {
   }
 
   spec {
-    backoff_limit              = var.validation_backoff_limit
+    # one pod per node: a retry could land on a node that already passed and
+    # hide the node that failed, so several nodes get no retry
+    backoff_limit              = local.validation_multi_node ? 0 : var.validation_backoff_limit
     active_deadline_seconds    = var.validation_active_deadline_seconds
     ttl_seconds_after_finished = 86400
-    completions                = 1
-    parallelism                = 1
+    completions                = var.validation_node_count
+    parallelism                = var.validation_node_count
 
     template {
       metadata {
-        labels = merge(local.common_labels, { "app.kubernetes.io/name" = "amd-gpu-validation" })
+        labels = local.validation_labels
       }
       spec {
         restart_policy = "Never"
         host_ipc       = true # RCCL peer-to-peer IPC between the ranks' GPU buffers
         node_selector  = var.gpu_node_selector
+
+        # every pod on its own GPU node (the pods run at once: parallelism =
+        # completions), also when validation_gpu_count leaves room for two
+        affinity {
+          pod_anti_affinity {
+            required_during_scheduling_ignored_during_execution {
+              label_selector {
+                match_labels = { "app.kubernetes.io/name" = "amd-gpu-validation" }
+              }
+              topology_key = "kubernetes.io/hostname"
+            }
+          }
+        }
 
         # The GPU taint only: NOT the node-prep startup taint
         # (node_prep_startup_taint), so the Job schedules on a node only after

@@ -239,6 +239,17 @@ variable "validation_gpu_count" {
   }
 }
 
+variable "validation_node_count" {
+  type        = number
+  default     = 1
+  description = "GPU nodes the validation Job covers: one pod per node, all at once (completions = parallelism = this, required pod anti-affinity on the hostname). The roots pass the GPU pools' size at creation, so apply returns only once every GPU node has passed. Above 1 the Job's backoffLimit is 0: a retry could land on a node that already passed and hide the one that failed."
+
+  validation {
+    condition     = var.validation_node_count >= 1 && floor(var.validation_node_count) == var.validation_node_count
+    error_message = "validation_node_count must be a whole number >= 1."
+  }
+}
+
 variable "validation_gemm_size" {
   type        = number
   default     = 8192

@@ -11,8 +11,9 @@
 ``record`` runs the apply as a CHILD process (output passed through and saved
 line by line), and meanwhile polls the cluster with kubectl: the first time
 any node reports ``amd.com/gpu`` allocatable becomes the ``gpu_allocatable``
-stamp, and the validation Job pod's termination message (amdgpu-validate's
-one-line verdict) becomes ``validation_done``. kubectl failures before the
+stamp, and the validation Job pods' termination messages (amdgpu-validate's
+one-line verdicts, one pod per GPU node: ``--validation-pods``) give
+``validation_done``, the last pod's finish. kubectl failures before the
 cluster exists are expected and ignored. ``critical-path`` is the offline
 model over the plan graph (prior durations, or measured ones from a log).
 The reference has none of this (its only figure is "~5 minutes" after apply,
@@ -53,15 +54,44 @@ def _kubectl_json(kubectl: list[str], args: list[str], timeout: float = 20.0):
 
 
 class ClusterWatcher(threading.Thread):
-    """Polls nodes for amd.com/gpu allocatable and the validation pod for its
-    termination message until stopped."""
+    """Polls nodes for amd.com/gpu allocatable and the validation pods for
+    their termination messages until stopped.
 
-    def __init__(self, kubectl: list[str], namespace: str, poll_s: float):
+    The Job runs one pod per GPU node (the module's validation_node_count):
+    ``expected_pods`` of them. ``report`` is set once they have all reported:
+    the verdict of the pod that finished LAST (its ``end_epoch_s`` is the
+    validation_done stamp), with ``per_node`` listing every pod's node, finish
+    time and verdict. If apply returns first, ``finish`` builds it from the
+    pods seen so far, with ``nodes_validated`` < ``nodes_expected``."""
+
+    def __init__(self, kubectl: list[str], namespace: str, poll_s: float,
+                 expected_pods: int = 1):
         super().__init__(daemon=True)
         self.kubectl, self.ns, self.poll_s = kubectl, namespace, poll_s
+        self.expected_pods = max(1, expected_pods)
         self.events: list[dict] = []          # k8s-event-shaped records
+        self.reports: dict[str, dict] = {}    # pod name -> its verdict
         self.report: dict | None = None
         self._stop_evt = threading.Event()
+
+    def _merge(self) -> dict | None:
+        if not self.reports:
+            return None
+        last = max(self.reports.values(), key=lambda r: r["end_epoch_s"])
+        out = {k: v for k, v in last.items() if not k.startswith("_")}
+        out["per_node"] = [
+            {"pod": pod, "node": r.get("_node"), "end_epoch_s": r["end_epoch_s"],
+             "passed": r.get("passed", r.get("ok"))}
+            for pod, r in sorted(self.reports.items(), key=lambda kv: kv[1]["end_epoch_s"])]
+        out["nodes_validated"] = len(self.reports)
+        out["nodes_expected"] = self.expected_pods
+        return out
+
+    def finish(self) -> None:
+        """Apply has returned: one last poll, then the report from what was seen."""
+        self.poll_once()
+        if self.report is None:
+            self.report = self._merge()
 
     def poll_once(self) -> None:
         now = time.time()
@@ -80,6 +110,9 @@ class ClusterWatcher(threading.Thread):
             pods = _kubectl_json(self.kubectl, ["-n", self.ns, "get", "pods", "-l",
                                                 "app.kubernetes.io/name=amd-gpu-validation"])
             for it in (pods or {}).get("items", []):
+                name = it.get("metadata", {}).get("name", "?")
+                if name in self.reports:
+                    continue
                 for cs in it.get("status", {}).get("containerStatuses", []):
                     term = cs.get("state", {}).get("terminated")
                     if not term or not term.get("message"):
@@ -88,13 +121,18 @@ class ClusterWatcher(threading.Thread):
                         rep = json.loads(term["message"])
                     except json.JSONDecodeError:
                         continue
+                    if not isinstance(rep, dict):
+                        continue
                     fin = term.get("finishedAt")
                     if fin:
                         from .apply_timeline import parse_ts
                         rep.setdefault("end_epoch_s", parse_ts(fin))
                     else:
                         rep.setdefault("end_epoch_s", now)
-                    self.report = rep
+                    rep["_node"] = it.get("spec", {}).get("nodeName")
+                    self.reports[name] = rep
+            if len(self.reports) >= self.expected_pods:
+                self.report = self._merge()
 
     def run(self) -> None:
         while not self._stop_evt.is_set():
@@ -115,7 +153,7 @@ def cmd_record(a) -> int:
         return 2
     watcher = None
     if a.kubectl:
-        watcher = ClusterWatcher(shlex.split(a.kubectl), a.namespace, a.poll)
+        watcher = ClusterWatcher(shlex.split(a.kubectl), a.namespace, a.poll, a.validation_pods)
         watcher.start()
     t0 = time.time()
     with open(out / "apply.jsonl", "w") as log:
@@ -127,9 +165,9 @@ def cmd_record(a) -> int:
             log.flush()
         rc = proc.wait()
     if watcher is not None:
-        watcher.poll_once()              # apply returned after the Job: catch up
         watcher.stop()
         watcher.join(timeout=a.poll + 30)
+        watcher.finish()                 # apply returned after the Job: catch up
         (out / "k8s_events.json").write_text(json.dumps({"items": watcher.events}, indent=1))
         if watcher.report is not None:
             (out / "validation.json").write_text(json.dumps(watcher.report, indent=1))
@@ -196,6 +234,9 @@ def main(argv=None) -> int:
     r.add_argument("--kubectl", default="", help='e.g. "kubectl --kubeconfig ./kubeconfig"')
     r.add_argument("--namespace", default="kube-amd-gpu")
     r.add_argument("--poll", type=float, default=10.0)
+    r.add_argument("--validation-pods", type=int, default=1,
+                   help="validation pods to wait for: the module's validation_node_count (one "
+                        "per GPU node); validation_done = the last one's finish")
     r.add_argument("command", nargs=argparse.REMAINDER)
     t = sub.add_parser("timeline", help="phase table from saved logs")
     t.add_argument("apply_log")

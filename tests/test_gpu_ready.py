@@ -153,9 +153,16 @@ if "nodes" in args:
     print(json.dumps({"items": [{"metadata": {"name": "gpu-node-0"},
                                  "status": {"allocatable": {"amd.com/gpu": "8"}}}]}))
 elif "pods" in args:
-    msg = json.dumps({"passed": True, "n_gpus": 8, "gemm_tflops_aggregate": 12345.0})
-    print(json.dumps({"items": [{"status": {"containerStatuses": [{"state": {"terminated": {
-        "exitCode": 0, "message": msg, "finishedAt": "2030-01-01T00:00:00Z"}}}]}}]}))
+    # one validation pod per GPU node (STUB_PODS), finishing a second apart
+    items = []
+    for i in range(int(os.environ.get("STUB_PODS", "1"))):
+        msg = json.dumps({"passed": True, "n_gpus": 8, "gemm_tflops_aggregate": 12345.0 + i})
+        items.append({"metadata": {"name": f"amd-gpu-validation-{i}"},
+                      "spec": {"nodeName": f"gpu-node-{i}"},
+                      "status": {"containerStatuses": [{"state": {"terminated": {
+                          "exitCode": 0, "message": msg,
+                          "finishedAt": f"2030-01-01T00:00:0{i}Z"}}}]}})
+    print(json.dumps({"items": items}))
 else:
     sys.exit(1)
 '''
@@ -197,6 +204,47 @@ def test_cli_record_with_stub_terraform_and_kubectl(tmp_path):
                          str(out / "apply.jsonl"), "--json"], capture_output=True, text=True,
                         timeout=60, cwd=Path(__file__).resolve().parents[1])
     assert p2.returncode == 0 and json.loads(p2.stdout)["resources"]
+
+
+def test_cli_record_waits_for_every_node_pod(tmp_path):
+    """With one validation pod per GPU node, validation_done is the LAST pod's
+    finish and the report lists every node's verdict."""
+    import os
+    import subprocess
+    import sys
+
+    bindir = tmp_path / "bin"
+    bindir.mkdir()
+    _stub(bindir / "terraform", TF_STUB)
+    _stub(bindir / "kubectl", KUBECTL_STUB)
+    env = dict(os.environ, PATH=f"{bindir}:{os.environ['PATH']}",
+               STUB_STATE=str(tmp_path / "kstate"), STUB_PODS="3")
+    out = tmp_path / "run"
+    p = subprocess.run([sys.executable, "-m", "nvidia_terraform_modules_amd.gpu_ready", "record",
+                        "--out", str(out), "--kubectl", "kubectl", "--poll", "0.2",
+                        "--validation-pods", "3", "--",
+                        "terraform", "apply", "-json", "-auto-approve"],
+                       capture_output=True, text=True, env=env, timeout=120,
+                       cwd=Path(__file__).resolve().parents[1])
+    assert p.returncode == 0, p.stderr
+    rep = json.loads((out / "validation.json").read_text())
+    assert rep["nodes_validated"] == rep["nodes_expected"] == 3
+    assert [n["node"] for n in rep["per_node"]] == ["gpu-node-0", "gpu-node-1", "gpu-node-2"]
+    assert all(n["passed"] for n in rep["per_node"])
+    assert rep["end_epoch_s"] == max(n["end_epoch_s"] for n in rep["per_node"])
+    assert rep["gemm_tflops_aggregate"] == 12347.0          # the last pod's verdict
+    assert not any(k.startswith("_") for k in rep)
+
+
+def test_watcher_reports_partial_coverage_when_apply_returns_first():
+    from nvidia_terraform_modules_amd.gpu_ready.__main__ import ClusterWatcher
+
+    w = ClusterWatcher(["false"], "ns", 0.1, expected_pods=2)
+    w.reports["p0"] = {"passed": True, "end_epoch_s": 5.0, "_node": "n0"}
+    w.poll_once()                      # kubectl fails: nothing new, still waiting for p1
+    assert w.report is None
+    w.finish()
+    assert w.report["nodes_validated"] == 1 and w.report["nodes_expected"] == 2
 
 
 def test_cli_critical_path_json(tmp_path):

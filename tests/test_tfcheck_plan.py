@@ -195,3 +195,75 @@ def test_crd_janitor_deletes_only_crds_this_release_installs():
     no_nfd = _stack_local("crd_cleanup_list", install_node_feature_discovery=False)
     assert not any(c.endswith(".nfd.k8s-sigs.io") for c in no_nfd)
     assert no_nfd[0] == "deviceconfigs.amd.com"
+
+
+def _stack_eval(expr, **overrides):
+    """Evaluate an expression of modules/amd-gpu-stack (variable defaults +
+    overrides, the module's locals; cluster_name defaults to "c")."""
+    from nvidia_terraform_modules_amd.tfcheck.config import load_module
+
+    overrides.setdefault("cluster_name", "c")
+    mod = load_module(ROOT / "modules" / "amd-gpu-stack")
+    ev = Evaluator()
+    variables = {}
+    for vn, v in mod.variables.items():
+        if vn in overrides:
+            variables[vn] = overrides[vn]
+        elif not v.required:
+            variables[vn] = convert(ev.eval(v.block.body.attr("default"), Scope({}, {})),
+                                    v.type_expr)
+    scope = Scope(variables, {n: e for n, (e, _, _) in mod.locals.items()}, str(mod.path))
+    return ev.eval(expr, scope)
+
+
+def _job_spec():
+    from nvidia_terraform_modules_amd.tfcheck.config import load_module
+
+    job = load_module(ROOT / "modules" / "amd-gpu-stack").resources[
+        "kubernetes_job_v1.gpu_validation"].block.body
+    return job.blocks_of("spec")[0].body
+
+
+@pytest.mark.parametrize("nodes,backoff", [(1, 1), (3, 0)])
+def test_validation_job_runs_one_pod_per_gpu_node(nodes, backoff):
+    """Every GPU node the pools start with gets its own validation pod, all at
+    once, and apply waits for all of them; with several nodes a failed pod is
+    not retried (the retry could land on a node that already passed)."""
+    spec = _job_spec()
+    assert _stack_eval(spec.attr("completions"), validation_node_count=nodes) == nodes
+    assert _stack_eval(spec.attr("parallelism"), validation_node_count=nodes) == nodes
+    assert _stack_eval(spec.attr("backoff_limit"), validation_node_count=nodes) == backoff
+    tmpl = spec.blocks_of("template")[0].body
+    pod_labels = _stack_eval(tmpl.blocks_of("metadata")[0].body.attr("labels"))
+    pod = tmpl.blocks_of("spec")[0].body
+    anti = pod.blocks_of("affinity")[0].body.blocks_of("pod_anti_affinity")[0].body
+    req = anti.blocks_of("required_during_scheduling_ignored_during_execution")[0].body
+    assert _stack_eval(req.attr("topology_key")) == "kubernetes.io/hostname"
+    sel = _stack_eval(req.blocks_of("label_selector")[0].body.attr("match_labels"))
+    assert sel.items() <= pod_labels.items()       # the pods repel each other
+
+
+def test_validation_node_count_must_be_a_whole_positive_number(tmp_path):
+    from nvidia_terraform_modules_amd.tfcheck.config import load_module
+
+    v = load_module(ROOT / "modules" / "amd-gpu-stack").variables["validation_node_count"]
+    cond = v.block.body.blocks_of("validation")[0].body.attr("condition")
+    ev = Evaluator()
+    for n, ok in ((1, True), (4, True), (0, False), (1.5, False)):
+        assert ev.eval(cond, Scope({"validation_node_count": n}, {})) is ok
+
+
+@pytest.mark.parametrize("root,variables,expected", [
+    ("eks", {"desired_count_gpu_nodes": 3}, 3),
+    ("eks", {"desired_count_gpu_nodes": 0}, 1),
+    ("gke", {"num_gpu_nodes": 2, "node_zones": ["z-a", "z-b"]}, 4),
+    ("gke", {"num_gpu_nodes": 1, "node_zones": ["z-a"]}, 1),
+    ("aks", {"gpu_node_pool_count": 2}, 2),
+])
+def test_roots_validate_every_gpu_node_they_create(root, variables, expected):
+    """The roots size the Job from the GPU pools' node count at creation (GKE:
+    node_count is per zone)."""
+    from nvidia_terraform_modules_amd.tfcheck.config import load_module
+
+    call = load_module(ROOT / root).modules["amd_gpu_stack"].block.body
+    assert Evaluator().eval(call.attr("validation_node_count"), Scope(variables, {})) == expected
