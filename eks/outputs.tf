@@ -76,6 +76,6 @@ output "gpu_resource_name" {
 }
 
 output "gpu_validation_job" {
-  description = "Name of the validation Job; its pod's termination message holds the one-line verdict."
+  description = "Name of the validation Job (one pod per GPU node); each pod's termination message holds its node's one-line verdict."
   value       = module.amd_gpu_stack.validation_job_name
 }
