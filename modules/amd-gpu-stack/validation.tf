@@ -12,6 +12,8 @@
   One pod per GPU node (validation_node_count, from the pools' size at
   creation): all pods run at once, a required anti-affinity on the hostname
   puts each on its own node, and the Job completes when every node passed.
+  (The reference's GPU group starts with 2 nodes, /root/reference/eks/
+  variables.tf:86-90, and nothing checks either of them.)
 ********************************************/
 locals {
   validation_multi_gpu  = var.validation_gpu_count > 1
