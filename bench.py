@@ -327,7 +327,7 @@ class ExtrasWatchdog:
     ``NTM_BENCH_INJECT_HANG=<phase>:<rank>`` makes that rank stall when it enters
     that phase (tests of this path only)."""
 
-    def __init__(self, seconds: float, rank: int, on_expire):
+    def __init__(self, seconds: float, rank: int, on_expire, exit_fn=None):
         import threading
 
         self.phase = "verify"
@@ -335,6 +335,7 @@ class ExtrasWatchdog:
         self._lock = threading.Lock()
         self._owner = None          # "main" or "deadline": who prints and exits
         self._on_expire = on_expire
+        self._exit = exit_fn or os._exit
         self._t = threading.Timer(seconds, self._fire) if seconds > 0 else None
         if self._t is not None:
             self._t.daemon = True
@@ -366,7 +367,7 @@ class ExtrasWatchdog:
         finally:
             sys.stdout.flush()
             sys.stderr.flush()
-            os._exit(code)
+            self._exit(code)
 
 
 def relaunch_distributed(args) -> int:

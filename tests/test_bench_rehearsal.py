@@ -149,6 +149,33 @@ def test_hung_collective_still_prints_the_line(phase):
         assert "allreduce_bf16" not in d
 
 
+def test_extras_watchdog_ownership():
+    """Exactly one of the main thread and the deadline prints the line: a claim
+    before the deadline cancels it; a deadline that fired first keeps it."""
+    import threading
+    import time
+
+    sys.path.insert(0, str(ROOT))
+    import bench
+
+    fired, exited = threading.Event(), []
+
+    def on_expire(phase):
+        fired.set()
+        return 7
+
+    wd = bench.ExtrasWatchdog(0.2, 0, on_expire, exit_fn=exited.append)
+    assert wd.claim() is True
+    time.sleep(0.4)
+    assert not fired.is_set() and exited == []
+    wd = bench.ExtrasWatchdog(0.05, 0, on_expire, exit_fn=exited.append)
+    wd.enter("xgmi")
+    assert fired.wait(2.0)
+    time.sleep(0.05)
+    assert exited == [7] and wd.claim() is False
+    assert bench.ExtrasWatchdog(0, 0, on_expire).claim() is True     # 0 = no deadline
+
+
 def test_self_relaunch_as_child_process():
     """`python bench.py --gpus 2` without WORLD_SIZE starts torch.distributed.run
     as a CHILD (never exec) and propagates its exit status."""
