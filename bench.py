@@ -300,6 +300,44 @@ def sk_product_check(backend, dev) -> dict:
     return res
 
 
+def node_topology(env, dev) -> dict:
+    """What the run ran on, for reading a scaling curve: every rank's device
+    (name, PCI bus id, UUID, CUs, HBM), the peer-access matrix over the
+    node's visible GPUs (rank 0) and the RCCL version. Never raises."""
+    import torch
+
+    from nvidia_terraform_modules_amd.parallel import dist
+
+    mine: dict = {"rank": env.rank, "device": str(dev)}
+    if dev.type == "cuda":
+        try:
+            p = torch.cuda.get_device_properties(dev)
+            mine.update(name=p.name, gcn_arch=getattr(p, "gcnArchName", None),
+                        cus=p.multi_processor_count,
+                        hbm_gb=round(p.total_memory / 1e9, 1),
+                        pci_bus_id=getattr(p, "pci_bus_id", None),
+                        pci_device_id=getattr(p, "pci_device_id", None),
+                        uuid=str(getattr(p, "uuid", "")) or None)
+        except Exception as e:  # noqa: BLE001 - diagnostic only
+            mine["error"] = f"{type(e).__name__}: {e}"[:200]
+    out: dict = {"ranks": dist.all_gather_obj(env, mine)}
+    if env.is_main and dev.type == "cuda":
+        try:
+            k = torch.cuda.device_count()
+            out["visible_gpus"] = k
+            out["peer_access"] = [[i == j or bool(torch.cuda.can_device_access_peer(i, j))
+                                   for j in range(k)] for i in range(k)]
+        except Exception as e:  # noqa: BLE001
+            out["peer_access_error"] = f"{type(e).__name__}: {e}"[:200]
+        try:
+            out["rccl_version"] = ".".join(str(x) for x in torch.cuda.nccl.version())
+        except Exception:  # noqa: BLE001
+            out["rccl_version"] = None
+    out["torch"] = torch.__version__
+    out["hip"] = getattr(torch.version, "hip", None)
+    return out
+
+
 def pair_busbw(rccl, xgmi) -> list:
     """C2 against RCCL at the message sizes both sweeps ran (bf16, in place,
     same timing loop): one row per shared size with both busbw and the ratio."""
@@ -585,6 +623,8 @@ def main(argv=None) -> int:
         return 0 if verified in (None, True) else 1
 
     wd = ExtrasWatchdog(args.extras_timeout_s, env.rank, on_deadline)
+    wd.enter("topology")
+    extras["node_topology"] = node_topology(env, dev)
     wd.enter("verify")
     if not args.no_check:
         rep = wl.verify()

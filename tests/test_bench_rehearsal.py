@@ -58,6 +58,9 @@ def test_torchrun_launch_one_json_line(nproc):
     assert d["higher_is_better"] is True and d["scaling"] == "weak" and d["dtype"] == "bf16"
     assert d["value"] > 0 and d["verified"] is True and d["rehearsal"] is True
     assert "extras_timed_out" not in d                  # the deadline did not fire
+    topo = d["node_topology"]                           # what the run ran on, per rank
+    assert [r["rank"] for r in topo["ranks"]] == list(range(nproc))
+    assert topo["torch"]
     assert "NOT a measurement" in d["data"]
     # clock-settle pre-warm (untimed, wall-time based) and event timing are reported
     assert d["prewarm_s"] >= 0.2 and d["prewarm_launches"] > 0
@@ -203,6 +206,9 @@ def test_bench_on_one_gpu_json_contract(tmp_path):
     d = lines[0]
     assert CONTRACT_KEYS <= set(d) and d["n_gpus"] == 1 and d["verified"] is True
     assert d["value"] > 50 and "rehearsal" not in d
+    topo = d["node_topology"]
+    assert topo["ranks"][0]["cus"] == 256 and "gfx950" in (topo["ranks"][0]["gcn_arch"] or "")
+    assert topo["visible_gpus"] >= 1 and topo["peer_access"][0][0] is True
     assert d["hipblaslt_tflops_per_gpu_rank0"] > 0 and d["hbm_copy_GBps_rank0"] > 1000
     cmp_ = d["interleaved_compare_rank0"]       # K1 vs hipBLASLt, ABAB rounds
     assert cmp_["rounds"] == len(cmp_["k1_tflops_rounds"]) == len(cmp_["hipblaslt_tflops_rounds"])
