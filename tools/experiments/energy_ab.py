@@ -5,7 +5,8 @@ the interleaved median (bench.interleaved_compare); energy comes from AMD SMI
 windows of >= --window-s of one kernel each, in palindromic order (A B C C B A)
 so no kernel always runs on the warmer chip; J/TFLOP = mean window power / TF/s.
 
-    python tools/experiments/energy_ab.py [--bf16-alt dma4k_d3] [--fp8-knob 12]
+    python tools/experiments/energy_ab.py [--bf16-alt dma4k_d3[,dma4kh,...]] [--fp8-knob 12]
+    (--fp8-knob 0 skips the fp8 comparison)
 """
 from __future__ import annotations
 
@@ -66,14 +67,21 @@ def main() -> int:
     b = ops.fill_uniform_(torch.empty((n, n), dtype=torch.bfloat16, device=dev), 2)
     c = torch.empty((n, n), dtype=torch.bfloat16, device=dev)
     ref = ops.gemm_bf16(a, b)
-    alt = ops.gemm_bf16(a, b, variant=args.bf16_alt)
-    ok = bool(torch.equal(alt, ref)) or bool(((alt.float() - ref.float()).abs() <= 1e-2 * (1 + ref.float().abs())).all())
-    res = measure({"default": lambda: ops.gemm_bf16(a, b, c),
-                   args.bf16_alt: lambda: ops.gemm_bf16(a, b, c, variant=args.bf16_alt),
-                   "hipblaslt": lambda: torch.matmul(a, b.T, out=c)}, fl, dev, args.rounds,
-                  args.iters, args.window_s)
+    alts = [v for v in args.bf16_alt.split(",") if v]
+    ok = {}
+    for v in alts:
+        alt = ops.gemm_bf16(a, b, variant=v)
+        ok[v] = bool(torch.equal(alt, ref)) or bool(
+            ((alt.float() - ref.float()).abs() <= 1e-2 * (1 + ref.float().abs())).all())
+    fns = {"default": lambda: ops.gemm_bf16(a, b, c)}
+    for v in alts:
+        fns[v] = (lambda v=v: ops.gemm_bf16(a, b, c, variant=v))
+    fns["hipblaslt"] = lambda: torch.matmul(a, b.T, out=c)
+    res = measure(fns, fl, dev, args.rounds, args.iters, args.window_s)
     print(json.dumps({"dtype": "bf16", "size": n, "alt_ok": ok, **res}), flush=True)
-    del a, b, ref, alt
+    del a, b, ref
+    if not args.fp8_knob:
+        return 0
     a8 = ops.fill_uniform_(torch.empty((n, n), dtype=torch.float8_e4m3fn, device=dev), 3)
     b8 = ops.fill_uniform_(torch.empty((n, n), dtype=torch.float8_e4m3fn, device=dev), 4)
     ref = ops.gemm_fp8(a8, b8)
