@@ -151,70 +151,6 @@ __device__ __forceinline__ void step(const Ctx& c, f32x4 (&acc)[8][8], Frags8& f
   __builtin_amdgcn_sched_barrier(0);
 }
 
-// Round 6 "dma4kh" (bf16 only): the same tile, waves and LDS image, but each
-// K-tile runs as two k-half PASSES over all 64 accumulators (pass 0: k-half 0
-// of every (mt, nt), pass 1: k-half 1) instead of both halves per slot.
-// Why: `step` refreshes its one fragment set only after a slot's last use, so
-// row 0 of every step waits on reads issued at the end of the previous one
-// (exposed LDS latency), and its back-to-back MFMA pairs on one accumulator
-// cost ~107 cycles per K-tile even with no loads (profiles/r3_k1, MFMA-only
-// 2155 vs 2048). With passes, set ks of Frags8 is double-buffered at k-half
-// granularity - the structure of hipBLASLt's 4-wave MT256x256x64 loop:
-//   pass 0 (64 MFMAs on set 0 = tile t, k-half 0) + reads of tile t k-half 1
-//          into set 1 (buffer BUF);
-//   lgkmcnt(0) (every read of BUF retired), vmcnt(0) (tile t+1 landed: the
-//          only pieces in flight), barrier;
-//   pass 1 (64 MFMAs on set 1) + the 16 DMA pieces of tile t+2 into BUF + the
-//          reads of tile t+1 k-half 0 into set 0 (buffer BUF ^ 1).
-// RAW: tile t+1's pieces (issued in pass 1 of step t-1) land before step t's
-//      barrier; read after it. WAR: BUF's reads (k-half 0 in step t-1 pass 1,
-//      k-half 1 in step t pass 0) retire before step t's barrier; tile t+2's
-//      DMA follows it. Per accumulator the K order is unchanged (k-half 0
-//      then 1 of each K-tile), so C is bitwise equal to the default's.
-// DI: one DMA piece every DI MFMAs of pass 1; RD: one fragment read every RD
-// MFMAs from the start of each pass.
-template <int BUF, int DI, int RD>
-__device__ __forceinline__ void step_kh(const Ctx& c, f32x4 (&acc)[8][8], Frags8& f, int t, int T,
-                                        int w) {
-  static_assert(DI >= 1 && 15 * DI < 64 && RD >= 1 && 15 * RD < 64, "pieces / reads in a pass");
-#pragma unroll
-  for (int mt = 0; mt < 8; ++mt)
-#pragma unroll
-    for (int nt = 0; nt < 8; ++nt) {
-      mfma_bf16(acc[mt][nt], f.b[nt][0], f.a[mt][0]);
-      const int j = mt * 8 + nt;
-      if ((j % RD) == 0 && j / RD < 16) {  // tile t k-half 1 -> set 1: A[0..7], B[0..7]
-        const int r = j / RD;
-        const char* p = c.lds + BUF * kBuf + (r < 8 ? c.rd_a : c.rd_b) + (r & 7) * 2048 + 1024;
-        if (r < 8)
-          f.a[r][1] = *(const bf16x8*)p;
-        else
-          f.b[r & 7][1] = *(const bf16x8*)p;
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // every read of BUF retired
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // tile t+1 landed (this wave's pieces)
-  raw_barrier();                                       // tile t+1 visible; BUF free
-#pragma unroll
-  for (int mt = 0; mt < 8; ++mt)
-#pragma unroll
-    for (int nt = 0; nt < 8; ++nt) {
-      mfma_bf16(acc[mt][nt], f.b[nt][1], f.a[mt][1]);
-      const int j = mt * 8 + nt;
-      if ((j % DI) == 0 && j / DI < 16) issue_piece(c, t + 2, T, BUF, w, j / DI);
-      if ((j % RD) == 0 && j / RD < 16) {  // tile t+1 k-half 0 -> set 0
-        const int r = j / RD;
-        const char* p = c.lds + (BUF ^ 1) * kBuf + (r < 8 ? c.rd_a : c.rd_b) + (r & 7) * 2048;
-        if (r < 8)
-          f.a[r][0] = *(const bf16x8*)p;
-        else
-          f.b[r & 7][0] = *(const bf16x8*)p;
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-}
-
 // LDS-staged epilogue (the caller drained its DMA and passed a barrier).
 template <bool NT>
 __device__ __forceinline__ void store_tile(const GemmArgs& p, char* lds, const f32x4 (&acc)[8][8],
@@ -331,49 +267,6 @@ __global__ void __launch_bounds__(kThreads, 1) gemm_w4k_kernel(GemmArgs p) {
   store_tile<true>(p, smem, acc, m0, n0, w, wr, wc, lane);
 }
 
-// dma4kh (step_kh): tiles 0 and 1 in flight, tile 0 landed, its k-half-0
-// fragments read into set 0.
-template <int DI, int RD>
-__global__ void __launch_bounds__(kThreads, 1) gemm_w4kh_kernel(GemmArgs p) {
-  __shared__ __attribute__((aligned(16))) char smem[kLds];
-  Ctx c;
-  int m0, n0, lane, w, wr, wc;
-  setup(p, smem, c, m0, n0, lane, w, wr, wc);
-  f32x4 acc[8][8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int T = p.K / 64;  // even, >= 4
-  Frags8 f;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) issue_piece(c, 0, T, 0, w, i);
-#pragma unroll
-  for (int i = 0; i < 16; ++i) issue_piece(c, 1, T, 1, w, i);
-  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-  raw_barrier();
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    f.a[i][0] = *(const bf16x8*)(c.lds + c.rd_a + i * 2048);
-    f.b[i][0] = *(const bf16x8*)(c.lds + c.rd_b + i * 2048);
-  }
-  int t = 0;
-  do {
-    step_kh<0, DI, RD>(c, acc, f, t, T, w);
-    step_kh<1, DI, RD>(c, acc, f, t + 1, T, w);
-    t += 2;
-  } while (t < T - 2);
-  step_kh<0, DI, RD>(c, acc, f, t, T, w);
-  step_kh<1, DI, RD>(c, acc, f, t + 1, T, w);
-
-  ::ntm::gemm::mfma_drain();
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // dummy pieces landed before LDS reuse
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  raw_barrier();
-  store_tile<true>(p, smem, acc, m0, n0, w, wr, wc, lane);
-}
-
 inline bool operands_ok(const GemmArgs& a) {
   return (long long)a.M * a.lda * 2 < (1ll << 31) && (long long)a.N * a.ldb * 2 < (1ll << 31);
 }
@@ -387,18 +280,6 @@ inline hipError_t launch_gemm_bf16_w4k(const GemmArgs& a, hipStream_t stream) {
     return hipErrorInvalidValue;
   const dim3 g((unsigned)((a.M / BM) * (a.N / BN))), b(kThreads);
   hipLaunchKernelGGL((gemm_w4k_kernel<DI, false>), g, b, 0, stream, a);
-  return hipGetLastError();
-}
-
-// dma4kh (bf16): the same shape rule as launch_gemm_bf16_w4k.
-template <int DI = 3, int RD = 2>
-inline hipError_t launch_gemm_bf16_w4kh(const GemmArgs& a, hipStream_t stream) {
-  if (a.M <= 0 || a.N <= 0 || a.K < 256 || (a.M % BM) || (a.N % BN) || (a.K % 128) ||
-      a.lda < a.K || a.ldb < a.K || a.ldc < a.N || (a.lda % 8) || (a.ldb % 8) || (a.ldc % 8) ||
-      a.rowsum || !operands_ok(a))
-    return hipErrorInvalidValue;
-  const dim3 g((unsigned)((a.M / BM) * (a.N / BN))), b(kThreads);
-  hipLaunchKernelGGL((gemm_w4kh_kernel<DI, RD>), g, b, 0, stream, a);
   return hipGetLastError();
 }
 

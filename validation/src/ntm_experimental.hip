@@ -71,12 +71,8 @@ NTM_API int ntm_gemm_bf16_experimental(int variant, const void* A, const void* B
     // piece every 3 MFMA pairs (gemm_w4k.hpp; restored in round 6 for the energy
     // study, profiles/r6_fp8)
     case 39: return (int)ntm::w4k::launch_gemm_bf16_w4k<3>(a, S(stream));
-    // 56-58 (round 6, "dma4kh"): the same 4-wave tile in two k-half passes per
-    // K-tile, fragments double-buffered per k-half (gemm_w4k.hpp step_kh);
-    // DMA piece every DI / fragment read every RD MFMAs: (3, 2), (2, 2), (4, 3)
-    case 56: return (int)ntm::w4k::launch_gemm_bf16_w4kh<3, 2>(a, S(stream));
-    case 57: return (int)ntm::w4k::launch_gemm_bf16_w4kh<2, 2>(a, S(stream));
-    case 58: return (int)ntm::w4k::launch_gemm_bf16_w4kh<4, 3>(a, S(stream));
+    // 56-58 (round 6, "dma4kh": the same 4-wave tile in two k-half passes per
+    // K-tile) were removed after measurement: 4-9 % slower (profiles/r6_w4kh/).
     case 19: return (int)ntm::gemmt::launch_gemm_bf16_tile<4>(a, S(stream));
     case 20: return (int)ntm::gemmt::launch_gemm_bf16_tile<8>(a, S(stream));
     case 21: return (int)ntm::gemmt::launch_gemm_bf16_tile<5, 5>(a, S(stream));
