@@ -123,61 +123,28 @@ __device__ __forceinline__ void mma(f32x4& acc, const Frags8& f, int mt, int nt)
 
 // One K-tile step on buffer BUF (fragments of tile t in f on entry, of t+1 on
 // exit). DI: one DMA piece every DI slots from the barrier on.
-// KS (bf16 only, round 6 "dma4kr"): each row issues k-half 0 of its 8 slots,
-// then k-half 1, instead of both halves slot by slot, so no MFMA reads the
-// accumulator the previous one writes (dma4k's MFMA-only loop runs 2155 cycles
-// per K-tile against the 2048 floor, profiles/r3_k1). The DMA pieces keep
-// their places (one every 2 DI MFMAs from the barrier on); row 7 refreshes
-// B[nt] per k-half, each after that half's last use. Per accumulator the K
-// order is unchanged, so C is bitwise equal to dma4k's.
-template <int BUF, int DI, bool F8, bool KS = false>
+template <int BUF, int DI, bool F8>
 __device__ __forceinline__ void step(const Ctx& c, f32x4 (&acc)[8][8], Frags8& f, int t, int T,
                                      int w) {
   static_assert(DI >= 1 && 15 * DI <= 55, "16 pieces within rows 1..7");
-  static_assert(!(KS && F8), "k-split rows are a bf16 schedule");
-  if constexpr (KS) {
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int nt = 0; nt < 8; ++nt) {
-        mfma_bf16(acc[0][nt], f.b[nt][ks], f.a[0][ks]);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-  } else {
-#pragma unroll
-    for (int nt = 0; nt < 8; ++nt) {
-      mma<F8>(acc[0][nt], f, 0, nt);
-      __builtin_amdgcn_sched_barrier(0);
-    }
+  for (int nt = 0; nt < 8; ++nt) {
+    mma<F8>(acc[0][nt], f, 0, nt);
+    __builtin_amdgcn_sched_barrier(0);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile t+1 landed (this wave's pieces)
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   raw_barrier();  // tile t+1 visible; every read of tile t retired
 #pragma unroll
   for (int mt = 1; mt < 8; ++mt) {
-    if constexpr (KS) {
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int nt = 0; nt < 8; ++nt) {
-          mfma_bf16(acc[mt][nt], f.b[nt][ks], f.a[mt][ks]);
-          const int q = (mt - 1) * 16 + ks * 8 + nt;  // MFMA 0..111 after the barrier
-          if ((q % (2 * DI)) == 0 && q / (2 * DI) < 16) issue_piece(c, t + 2, T, BUF, w, q / (2 * DI));
-          if (ks == 0 && nt == 1) read_a(c, f, BUF ^ 1, mt - 1);  // row mt-1 done
-          if (mt == 7)  // B[nt] k-half ks after its last use
-            f.b[nt][ks] = *(const bf16x8*)(c.lds + (BUF ^ 1) * kBuf + c.rd_b + nt * 2048 + ks * 1024);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-    } else {
-#pragma unroll
-      for (int nt = 0; nt < 8; ++nt) {
-        mma<F8>(acc[mt][nt], f, mt, nt);
-        const int j = (mt - 1) * 8 + nt;  // 0..55
-        if ((j % DI) == 0 && j / DI < 16) issue_piece(c, t + 2, T, BUF, w, j / DI);
-        if (nt == 1) read_a(c, f, BUF ^ 1, mt - 1);  // A[mt-1]: its last MFMA was row mt-1
-        if (mt == 7) read_b(c, f, BUF ^ 1, nt);      // B[nt] after slot (7, nt)
-        __builtin_amdgcn_sched_barrier(0);
-      }
+    for (int nt = 0; nt < 8; ++nt) {
+      mma<F8>(acc[mt][nt], f, mt, nt);
+      const int j = (mt - 1) * 8 + nt;  // 0..55
+      if ((j % DI) == 0 && j / DI < 16) issue_piece(c, t + 2, T, BUF, w, j / DI);
+      if (nt == 1) read_a(c, f, BUF ^ 1, mt - 1);  // A[mt-1]: its last MFMA was row mt-1
+      if (mt == 7) read_b(c, f, BUF ^ 1, nt);      // B[nt] after slot (7, nt)
+      __builtin_amdgcn_sched_barrier(0);
     }
   }
   read_a(c, f, BUF ^ 1, 7);
@@ -265,7 +232,7 @@ __device__ __forceinline__ void prologue(const Ctx& c, Frags8& f, int T, int w) 
   }
 }
 
-template <int DI, bool F8, bool KS = false>
+template <int DI, bool F8>
 __global__ void __launch_bounds__(kThreads, 1) gemm_w4k_kernel(GemmArgs p) {
   __shared__ __attribute__((aligned(16))) char smem[kLds];
   Ctx c;
@@ -286,12 +253,12 @@ __global__ void __launch_bounds__(kThreads, 1) gemm_w4k_kernel(GemmArgs p) {
   // loop exit straight into the epilogue made it keep scratch copies
   int t = 0;
   do {
-    step<0, DI, F8, KS>(c, acc, f, t, T, w);
-    step<1, DI, F8, KS>(c, acc, f, t + 1, T, w);
+    step<0, DI, F8>(c, acc, f, t, T, w);
+    step<1, DI, F8>(c, acc, f, t + 1, T, w);
     t += 2;
   } while (t < T - 2);
-  step<0, DI, F8, KS>(c, acc, f, t, T, w);
-  step<1, DI, F8, KS>(c, acc, f, t + 1, T, w);
+  step<0, DI, F8>(c, acc, f, t, T, w);
+  step<1, DI, F8>(c, acc, f, t + 1, T, w);
 
   ::ntm::gemm::mfma_drain();
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // dummy pieces landed before LDS reuse
@@ -304,15 +271,15 @@ inline bool operands_ok(const GemmArgs& a) {
   return (long long)a.M * a.lda * 2 < (1ll << 31) && (long long)a.N * a.ldb * 2 < (1ll << 31);
 }
 
-// bf16: M, N % 256, K % 128, K >= 256. KS: the k-split row order (dma4kr).
-template <int DI = 3, bool KS = false>
+// bf16: M, N % 256, K % 128, K >= 256.
+template <int DI = 3>
 inline hipError_t launch_gemm_bf16_w4k(const GemmArgs& a, hipStream_t stream) {
   if (a.M <= 0 || a.N <= 0 || a.K < 256 || (a.M % BM) || (a.N % BN) || (a.K % 128) ||
       a.lda < a.K || a.ldb < a.K || a.ldc < a.N || (a.lda % 8) || (a.ldb % 8) || (a.ldc % 8) ||
       a.rowsum || !operands_ok(a))
     return hipErrorInvalidValue;
   const dim3 g((unsigned)((a.M / BM) * (a.N / BN))), b(kThreads);
-  hipLaunchKernelGGL((gemm_w4k_kernel<DI, false, KS>), g, b, 0, stream, a);
+  hipLaunchKernelGGL((gemm_w4k_kernel<DI, false>), g, b, 0, stream, a);
   return hipGetLastError();
 }
 

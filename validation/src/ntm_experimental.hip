@@ -73,9 +73,8 @@ NTM_API int ntm_gemm_bf16_experimental(int variant, const void* A, const void* B
     case 39: return (int)ntm::w4k::launch_gemm_bf16_w4k<3>(a, S(stream));
     // 56-58 (round 6, "dma4kh": the same 4-wave tile in two k-half passes per
     // K-tile) were removed after measurement: 4-9 % slower (profiles/r6_w4kh/).
-    // 56 (round 6, "dma4kr"): dma4k_d3 with each row's k-half 0 MFMAs before its
-    // k-half 1 ones (no back-to-back MFMA on one accumulator; gemm_w4k.hpp KS)
-    case 56: return (int)ntm::w4k::launch_gemm_bf16_w4k<3, true>(a, S(stream));
+    // 56 (round 6, "dma4kr": dma4k_d3 with each row's k-half 0 MFMAs before its
+    // k-half 1 ones) was removed after measurement: 2 % slower (profiles/r6_w4kh/).
     case 19: return (int)ntm::gemmt::launch_gemm_bf16_tile<4>(a, S(stream));
     case 20: return (int)ntm::gemmt::launch_gemm_bf16_tile<8>(a, S(stream));
     case 21: return (int)ntm::gemmt::launch_gemm_bf16_tile<5, 5>(a, S(stream));
