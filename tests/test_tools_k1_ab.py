@@ -40,3 +40,18 @@ def test_ragged_shapes_are_seeded_one_round_and_ragged():
         assert mm % 8 == nn % 8 == k % 8 == 0 and 1024 <= k <= 16384
     assert all(x % 16 == 0 for sh in m.uniform_shapes(20, 1, 16) for x in sh)
     assert m.parse_shapes("8x16x32,64x64x64") == [(8, 16, 32), (64, 64, 64)]
+
+
+def test_every_tool_script_compiles_and_indexes():
+    """Every script under tools/ at least byte-compiles (no silent rot in the
+    developer tools), and every experiment is indexed in tools/README.md."""
+    import py_compile
+
+    scripts = sorted((ROOT / "tools").rglob("*.py"))
+    assert len(scripts) > 20
+    for f in scripts:
+        py_compile.compile(str(f), doraise=True, cfile=None)
+    index = (ROOT / "tools" / "README.md").read_text()
+    missing = [f.name for f in (ROOT / "tools" / "experiments").glob("*.py")
+               if f"`{f.name}`" not in index]
+    assert not missing, f"not in tools/README.md: {missing}"
