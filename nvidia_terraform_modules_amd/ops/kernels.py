@@ -40,7 +40,7 @@ GEMM_VARIANTS = {"default": 0, "pingpong8": 1, "pingpong8b": 4,
                  "pingpong8om": 47, "pingpong8od": 48, "pingpong8s": 49,
                  "pingpong8omd": 51, "pp192x256": 27, "pp256x192": 28,
                  "pp224x256": 29, "pp192x256s": 54, "pp256x192s": 55,
-                 "dma4k_d3": 39, "dma4kx": 59, "dma4kx_b": 60, "dma4kx_c": 61}
+                 "dma4k_d3": 39}
 
 
 # variants built only into libntm_experimental.so (tests / tools): never selected
@@ -50,7 +50,7 @@ EXPERIMENTAL_VARIANTS = frozenset({"pingpong8", "pingpong8cw",
                                    "tile128w4", "tile256x128w4", "tile160w4",
                                    "pp8o_g128", "pp8o_g128_nostore", "pp8o_nostore",
                                    "pingpong8od", "pingpong8omd", "pingpong8om", "pp224x256",
-                                   "dma4k_d3", "dma4kx", "dma4kx_b", "dma4kx_c"})
+                                   "dma4k_d3"})
 
 # (TM, TN) of the 4-wave tile kernels (gemm_bf16_t128.hpp)
 TILE_SHAPES = {"tile128": (128, 128), "tile256x128": (256, 128), "tile160": (160, 160),

@@ -1030,22 +1030,6 @@ def test_sk_placement_fault_raises_on_the_product_path(ops, monkeypatch, variant
     assert ops.sk_xcc_error() != 0 and ops.sk_xcc_error() == 0
 
 
-@pytest.mark.parametrize("variant", ["dma4kx", "dma4kx_b", "dma4kx_c"])
-@pytest.mark.parametrize("m,n,k", [(256, 256, 256), (512, 768, 1024), (4608, 4352, 2048)])
-def test_dma4kx_three_barrier_builds_equal_dma4k(ops, variant, m, n, k):
-    """dma4kx (gemm_w4k.hpp step_x: three barriers per K-tile, per-operand LDS
-    recycling, counted vmcnt) keeps every accumulator's K order: bitwise equal to
-    dma4k_d3, within the fp32 reference's tolerance, stable on repeat."""
-    a = _rand(ops, (m, k), 71)
-    b = _rand(ops, (n, k), 72)
-    ref = a.float() @ b.float().T
-    atol, rtol = ops.gemm_tolerance(k)
-    c = ops.gemm_bf16(a, b, variant=variant)
-    assert ((c.float() - ref).abs() <= atol + rtol * ref.abs()).all()
-    assert torch.equal(c, ops.gemm_bf16(a, b, variant="dma4k_d3"))
-    assert torch.equal(ops.gemm_bf16(a, b, variant=variant), c)
-
-
 @pytest.mark.parametrize("m,n,k", [(256, 256, 512), (2048, 1024, 1024), (4608, 4352, 2048)])
 def test_dma4k_energy_study_builds_match_the_default(ops, m, n, k):
     """The 4-wave 128x128-per-wave builds restored for the energy study

@@ -151,75 +151,6 @@ __device__ __forceinline__ void step(const Ctx& c, f32x4 (&acc)[8][8], Frags8& f
   __builtin_amdgcn_sched_barrier(0);
 }
 
-// Round 6 "dma4kx" (bf16 only): the 4-wave tile with hipBLASLt's wait
-// structure (profiles/r6_w4kh: dma4k_d3 spends 18.5 % of its wave cycles in
-// s_waitcnt / barrier waits, hipBLASLt 4.8 %). One K-tile = 128 MFMAs, index
-// q: q < 64 -> k-half 0 of (mt, nt) = (q / 8, q % 8) on fragment set 0,
-// q >= 64 -> k-half 1 on set 1. Three barriers; the LDS buffer BUF of tile t
-// is recycled per operand, and the wait for tile t+1 is counted:
-//   q in [0, 8):     read tile t A k-half 1 -> set 1
-//   q == P1:         lgkmcnt(0), barrier 1   (every wave done reading BUF's A)
-//   after P1:        8 DMA pieces of tile t+2's A into BUF, one every DA MFMAs;
-//                    read tile t B k-half 1 -> set 1 (q in [P1, P1 + 8))
-//   q == P2:         lgkmcnt(0), barrier 2   (every wave done reading BUF's B)
-//   after P2:        8 DMA pieces of tile t+2's B into BUF, one every DB MFMAs
-//   q == P3:         vmcnt(16): the 16 pieces younger than tile t+1's are tile
-//                    t+2's, so tile t+1 has landed (this wave); barrier 3
-//   after P3:        read tile t+1 k-half 0 -> set 0 (16 reads from BUF ^ 1)
-// RAW: tile t+1's pieces (issued in iteration t-1) land before barrier 3 of
-//      iteration t; its k-half-0 reads follow it, its k-half-1 reads come in
-//      iteration t+1. WAR: BUF's A reads (k-half 0 after barrier 3 of t-1,
-//      k-half 1 before barrier 1 of t) retire before barrier 1; its B reads
-//      before barrier 2; the A / B pieces of tile t+2 follow those barriers.
-// Set 0 is last used at q = 63 < P3; set 1 at q = 127, refilled in the next
-// iteration before P1 / P2 - after its k-half-1 MFMAs of this one. Per
-// accumulator the K order is unchanged: C is bitwise equal to dma4k's.
-template <int BUF, int P1, int P2, int P3, int DA, int DB>
-__device__ __forceinline__ void step_x(const Ctx& c, f32x4 (&acc)[8][8], Frags8& f, int t, int T,
-                                       int w) {
-  static_assert(P1 >= 8 && P2 >= P1 + 8 + 1 && P2 > P1 + 7 * DA && P3 > P2 + 7 * DB &&
-                    P3 <= 112 && P3 >= 64,
-                "barrier / piece placement");
-#pragma unroll
-  for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-  for (int mt = 0; mt < 8; ++mt)
-#pragma unroll
-  for (int nt = 0; nt < 8; ++nt) {
-    const int q = ks * 64 + mt * 8 + nt;
-    if (q == P1) {
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      raw_barrier();
-    }
-    if (q == P2) {
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      raw_barrier();
-    }
-    if (q == P3) {
-      asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-      raw_barrier();
-    }
-    mfma_bf16(acc[mt][nt], f.b[nt][ks], f.a[mt][ks]);
-    if (q < 8)
-      f.a[q][1] = *(const bf16x8*)(c.lds + BUF * kBuf + c.rd_a + q * 2048 + 1024);
-    if (q >= P1 && q < P1 + 8)
-      f.b[q - P1][1] = *(const bf16x8*)(c.lds + BUF * kBuf + c.rd_b + (q - P1) * 2048 + 1024);
-    if (q >= P1 && (q - P1) % DA == 0 && (q - P1) / DA < 8)
-      issue_piece(c, t + 2, T, BUF, w, (q - P1) / DA);  // pieces 0..7: A
-    if (q >= P2 && (q - P2) % DB == 0 && (q - P2) / DB < 8)
-      issue_piece(c, t + 2, T, BUF, w, 8 + (q - P2) / DB);  // pieces 8..15: B
-    if (q >= P3 && q < P3 + 16) {
-      const int r = q - P3;  // A[0..7] then B[0..7], k-half 0 of tile t+1
-      const char* p = c.lds + (BUF ^ 1) * kBuf + (r < 8 ? c.rd_a : c.rd_b) + (r & 7) * 2048;
-      if (r < 8)
-        f.a[r][0] = *(const bf16x8*)p;
-      else
-        f.b[r & 7][0] = *(const bf16x8*)p;
-    }
-    __builtin_amdgcn_sched_barrier(0);
-  }
-}
-
 // LDS-staged epilogue (the caller drained its DMA and passed a barrier).
 template <bool NT>
 __device__ __forceinline__ void store_tile(const GemmArgs& p, char* lds, const f32x4 (&acc)[8][8],
@@ -336,49 +267,6 @@ __global__ void __launch_bounds__(kThreads, 1) gemm_w4k_kernel(GemmArgs p) {
   store_tile<true>(p, smem, acc, m0, n0, w, wr, wc, lane);
 }
 
-// dma4kx kernel (step_x): tiles 0 and 1 in flight, tile 0 landed, its k-half-0
-// fragments read into set 0.
-template <int P1, int P2, int P3, int DA, int DB>
-__global__ void __launch_bounds__(kThreads, 1) gemm_w4kx_kernel(GemmArgs p) {
-  __shared__ __attribute__((aligned(16))) char smem[kLds];
-  Ctx c;
-  int m0, n0, lane, w, wr, wc;
-  setup(p, smem, c, m0, n0, lane, w, wr, wc);
-  f32x4 acc[8][8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int T = p.K / 64;  // even, >= 4
-  Frags8 f;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) issue_piece(c, 0, T, 0, w, i);
-#pragma unroll
-  for (int i = 0; i < 16; ++i) issue_piece(c, 1, T, 1, w, i);
-  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // tile 0 landed (this wave)
-  raw_barrier();
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    f.a[i][0] = *(const bf16x8*)(c.lds + c.rd_a + i * 2048);
-    f.b[i][0] = *(const bf16x8*)(c.lds + c.rd_b + i * 2048);
-  }
-  int t = 0;
-  do {
-    step_x<0, P1, P2, P3, DA, DB>(c, acc, f, t, T, w);
-    step_x<1, P1, P2, P3, DA, DB>(c, acc, f, t + 1, T, w);
-    t += 2;
-  } while (t < T - 2);
-  step_x<0, P1, P2, P3, DA, DB>(c, acc, f, t, T, w);
-  step_x<1, P1, P2, P3, DA, DB>(c, acc, f, t + 1, T, w);
-
-  ::ntm::gemm::mfma_drain();
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // dummy pieces landed before LDS reuse
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  raw_barrier();
-  store_tile<true>(p, smem, acc, m0, n0, w, wr, wc, lane);
-}
-
 inline bool operands_ok(const GemmArgs& a) {
   return (long long)a.M * a.lda * 2 < (1ll << 31) && (long long)a.N * a.ldb * 2 < (1ll << 31);
 }
@@ -392,18 +280,6 @@ inline hipError_t launch_gemm_bf16_w4k(const GemmArgs& a, hipStream_t stream) {
     return hipErrorInvalidValue;
   const dim3 g((unsigned)((a.M / BM) * (a.N / BN))), b(kThreads);
   hipLaunchKernelGGL((gemm_w4k_kernel<DI, false>), g, b, 0, stream, a);
-  return hipGetLastError();
-}
-
-// dma4kx (bf16): the shape rule of launch_gemm_bf16_w4k.
-template <int P1 = 24, int P2 = 48, int P3 = 96, int DA = 3, int DB = 3>
-inline hipError_t launch_gemm_bf16_w4kx(const GemmArgs& a, hipStream_t stream) {
-  if (a.M <= 0 || a.N <= 0 || a.K < 256 || (a.M % BM) || (a.N % BN) || (a.K % 128) ||
-      a.lda < a.K || a.ldb < a.K || a.ldc < a.N || (a.lda % 8) || (a.ldb % 8) || (a.ldc % 8) ||
-      a.rowsum || !operands_ok(a))
-    return hipErrorInvalidValue;
-  const dim3 g((unsigned)((a.M / BM) * (a.N / BN))), b(kThreads);
-  hipLaunchKernelGGL((gemm_w4kx_kernel<P1, P2, P3, DA, DB>), g, b, 0, stream, a);
   return hipGetLastError();
 }
 

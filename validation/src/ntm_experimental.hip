@@ -75,13 +75,9 @@ NTM_API int ntm_gemm_bf16_experimental(int variant, const void* A, const void* B
     // K-tile) were removed after measurement: 4-9 % slower (profiles/r6_w4kh/).
     // 56 (round 6, "dma4kr": dma4k_d3 with each row's k-half 0 MFMAs before its
     // k-half 1 ones) was removed after measurement: 2 % slower (profiles/r6_w4kh/).
-    // 59-61 (round 6, "dma4kx"): the 4-wave tile with hipBLASLt's wait structure -
-    // three barriers per K-tile, per-operand buffer recycling, a counted vmcnt
-    // (gemm_w4k.hpp step_x); barriers at MFMA P1 / P2 / P3, A / B pieces every
-    // DA / DB MFMAs: (24, 48, 96, 3, 3), (24, 56, 104, 4, 5), (16, 40, 96, 2, 6)
-    case 59: return (int)ntm::w4k::launch_gemm_bf16_w4kx<24, 48, 96, 3, 3>(a, S(stream));
-    case 60: return (int)ntm::w4k::launch_gemm_bf16_w4kx<24, 56, 104, 4, 5>(a, S(stream));
-    case 61: return (int)ntm::w4k::launch_gemm_bf16_w4kx<16, 40, 96, 2, 6>(a, S(stream));
+    // 59-61 (round 6, "dma4kx": hipBLASLt's wait structure - three barriers per
+    // K-tile, per-operand LDS recycling, a counted vmcnt) were removed after
+    // measurement: 4-6 % behind dma4k_d3 (profiles/r6_w4kh/).
     case 19: return (int)ntm::gemmt::launch_gemm_bf16_tile<4>(a, S(stream));
     case 20: return (int)ntm::gemmt::launch_gemm_bf16_tile<8>(a, S(stream));
     case 21: return (int)ntm::gemmt::launch_gemm_bf16_tile<5, 5>(a, S(stream));
