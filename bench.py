@@ -9,7 +9,10 @@ without a cloud account; this measures the GPU half on real hardware:
 * each step = one hand-written K1 GEMM, M = N = K = 8192 bf16 (fp32 acc) per
   GPU on synthetic uniform[-1,1) operands generated on device (weak scaling),
 * an untimed clock-settle pre-warm (``--prewarm-s`` wall seconds of K1,
-  reported as ``prewarm_s``), then W untimed warmup steps, then EXACTLY K
+  reported as ``prewarm_s``), then an untimed choice of the K1 build for this
+  box (``select_k1``: the 8-wave pingpong8o and the 4-wave dma4k_d3, both
+  hand-written, timed interleaved; ``per_rank_k1_variant``; ``--k1-variant NAME``
+  times one build), then W untimed warmup steps, then EXACTLY K
   steps bracketed by barrier + synchronize and timed with HIP events, max over
   ranks; ``value`` = aggregate TFLOP/s over all GPUs,
 * after the timed region (never inside it): full-matrix verification against
@@ -73,6 +76,10 @@ def parse(argv=None):
     ap.add_argument("--no-job", action="store_true",
                     help="skip running the validation Job binary (amdgpu-validate) on the n GPUs "
                          "after the timed region")
+    ap.add_argument("--k1-variant", default="auto",
+                    help="the K1 build of the timed loop: auto = the faster of the 8-wave plan "
+                         "and the 4-wave dma4k_d3 on this box (select_k1); or a build name "
+                         "(default, dma4k_d3) to time that one")
     ap.add_argument("--out", default="", help="also write the JSON line to this file")
     ap.add_argument("--extras-timeout-s", type=float, default=300.0,
                     help="deadline for the work after the timed region (verification, "
@@ -300,6 +307,33 @@ def sk_product_check(backend, dev) -> dict:
     return res
 
 
+K1_SELECT_MARGIN = 0.005
+
+
+def select_k1(wl, backend, dev, sync, rounds: int = 9, launches: int = 20) -> dict | None:
+    """Pick the K1 build the timed loop runs on THIS box (untimed, after the
+    pre-warm). The shipping 8-wave pingpong8o and the 4-wave dma4k_d3 trade
+    places under the power limit: -3 % .. +1.8 % for dma4k_d3 on three boxes
+    (profiles/r6_w4kh). Both are timed interleaved, ABAB, each after its own
+    short settle; a build other than the default wins only when its median is
+    K1_SELECT_MARGIN faster. Sets ``wl.variant``; returns what was measured."""
+    cands = backend.k1_candidates(wl.m, wl.n, wl.k)
+    if len(cands) < 2:
+        return None
+    fns = {v: (lambda v=v: backend.gemm_bf16(wl.a, wl.b, wl.c, variant=v)) for v in cands}
+    for fn in fns.values():
+        prewarm_settle(fn, sync, 0.15)
+    cmp_ = interleaved_compare(fns, dev, rounds=rounds, launches=launches)
+    med = {v: cmp_[v]["median_s"] for v in cands}
+    best = min(cands, key=lambda v: med[v])
+    chosen = best if med[best] < med["default"] * (1 - K1_SELECT_MARGIN) else "default"
+    wl.variant = chosen
+    prewarm_settle(wl.step, sync, 0.2)          # settle on the chosen build
+    return {"candidates": cands, "chosen": chosen, "margin": K1_SELECT_MARGIN,
+            "tflops_median": {v: round(wl.flops / med[v] / 1e12, 1) for v in cands},
+            "rounds": rounds, "launches_per_round": launches}
+
+
 def node_topology(env, dev) -> dict:
     """What the run ran on, for reading a scaling curve: every rank's device
     (name, PCI bus id, UUID, CUs, HBM), the peer-access matrix over the
@@ -480,6 +514,13 @@ def main(argv=None) -> int:
     # 695 -> 950 -> 680 us per 8192^3 launch, profiles/r2_bench/). Without this the
     # timed window of a short run lands on the transient.
     prewarm = prewarm_settle(wl.step, sync, args.prewarm_s)
+    # ---- which hand-written K1 build the timed loop runs on this box (untimed)
+    k1_sel = None
+    if args.k1_variant != "auto":
+        wl.variant = args.k1_variant
+        prewarm_settle(wl.step, sync, 0.2)
+    elif dev.type == "cuda" and hasattr(backend, "k1_candidates"):
+        k1_sel = select_k1(wl, backend, dev, sync)
 
     # ---- warmup (untimed): exactly W steps. The power / throttle sample that opens
     # the telemetry window is read while POWER_WINDOW_CHUNK more pre-warm launches
@@ -558,7 +599,7 @@ def main(argv=None) -> int:
     # (only where the timed kernel IS the clock build's: the default plan runs
     # pingpong8o - at 2048^3 it runs a small tile, whose cycles these are not)
     same_kernel = False
-    if dev.type == "cuda" and hasattr(backend, "k1_plan"):
+    if dev.type == "cuda" and hasattr(backend, "k1_plan") and wl.variant == "default":
         try:
             same_kernel = backend.k1_plan(args.size, args.size, args.size)[1] == "pingpong8o"
         except ValueError:
@@ -594,7 +635,8 @@ def main(argv=None) -> int:
                                          "clock": clk, "gemm_clock": gclk,
                                          "timed_loop_clock": timed_clk, "power": power,
                                          "power_steady": power_steady, "power_src": power_src,
-                                         "smi_ms": smi_ms})
+                                         "smi_ms": smi_ms, "k1_variant": wl.variant,
+                                         "k1_selection": k1_sel})
 
     make_line = _make_line_factory(args, n, prewarm, wall_elapsed, ms_per_step, total_tflops,
                                    per_rank)
@@ -831,6 +873,10 @@ def _make_line_factory(args, n, prewarm, wall_elapsed, ms_per_step, total_tflops
             "bench_process_to_verified_s": round(_CLOCK.elapsed("gemm_verified"), 3),
             "in_node_phases_s": {k: round(v, 4) for k, v in _CLOCK.durations().items()},
             "per_rank_tflops": [p["tflops"] for p in per_rank],
+            # the hand-written K1 build each rank's timed loop ran (select_k1: the
+            # faster of pingpong8o and dma4k_d3 on that box), and what decided it
+            "per_rank_k1_variant": [p["k1_variant"] for p in per_rank],
+            "per_rank_k1_selection": [p["k1_selection"] for p in per_rank],
             # in-kernel clock: per stamped launch the median workgroup's cycles / window,
             # median over launches (within 2-3 % of the PMC clock, profiles/r4_clock/)
             # the launch-bounding clock: per stamped launch the slowest XCD's median

@@ -37,6 +37,7 @@ from .kernels import (  # noqa: F401
     FP8_VARIANTS,
     k1_fp8_plan,
     k1_fp8_splitk_plan,
+    k1_candidates,
     k1_plan,
     k1_splitk_plan,
     ref_gemm_f32,

@@ -49,8 +49,7 @@ EXPERIMENTAL_VARIANTS = frozenset({"pingpong8", "pingpong8cw",
                                    "pingpong8cwe", "pingpong8cwn", "pingpong8cwne",
                                    "tile128w4", "tile256x128w4", "tile160w4",
                                    "pp8o_g128", "pp8o_g128_nostore", "pp8o_nostore",
-                                   "pingpong8od", "pingpong8omd", "pingpong8om", "pp224x256",
-                                   "dma4k_d3"})
+                                   "pingpong8od", "pingpong8omd", "pingpong8om", "pp224x256"})
 
 # (TM, TN) of the 4-wave tile kernels (gemm_bf16_t128.hpp)
 TILE_SHAPES = {"tile128": (128, 128), "tile256x128": (256, 128), "tile160": (160, 160),
@@ -109,6 +108,20 @@ _DEFAULT_SK: dict[tuple[int, int, int], str] = {}
 # stream-K split mode on the 192-wide ping-pong tiles (gemm_bf16_skh.hpp)
 SKH_VARIANTS = ("pp192x256s", "pp256x192s")
 SK_VARIANTS = ("pingpong8s",) + SKH_VARIANTS
+
+
+def k1_candidates(m: int, n: int, k: int, lda: int | None = None, ldb: int | None = None,
+                  ldc: int | None = None) -> list[str]:
+    """K1 builds worth timing on the box itself for an (m, n, k) GEMM: the default
+    plan, plus the 4-wave ``dma4k_d3`` where its shape rule holds (M, N % 256,
+    K % 128, K >= 256, rows 16-byte aligned, operands < 2 GiB). Under the power
+    limit the two trade places box by box (profiles/r6_w4kh), so bench.py times
+    both after its pre-warm and runs the faster (bench.select_k1)."""
+    lda, ldb, ldc = lda or k, ldb or k, ldc or n
+    ok = (m % 256 == 0 and n % 256 == 0 and k % 128 == 0 and k >= 256 and
+          not (lda % 8 or ldb % 8 or ldc % 8) and m * lda * 2 < (1 << 31) and
+          n * ldb * 2 < (1 << 31))
+    return ["default", "dma4k_d3"] if ok else ["default"]
 
 
 def set_plan_pp_tiles(on: bool = True, split: bool | None = None) -> None:

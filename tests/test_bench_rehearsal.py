@@ -179,6 +179,43 @@ def test_extras_watchdog_ownership():
     assert bench.ExtrasWatchdog(0, 0, on_expire).claim() is True     # 0 = no deadline
 
 
+def test_select_k1_keeps_the_default_unless_clearly_faster(monkeypatch):
+    """select_k1 times the candidate K1 builds interleaved and switches away from
+    the default plan only for a median K1_SELECT_MARGIN faster."""
+    import types
+
+    sys.path.insert(0, str(ROOT))
+    import bench
+
+    wl = types.SimpleNamespace(m=8192, n=8192, k=8192, a=None, b=None, c=None,
+                               flops=2.0 * 8192 ** 3, variant="default", step=lambda: None)
+    calls = []
+    backend = types.SimpleNamespace(
+        k1_candidates=lambda m, n, k: ["default", "dma4k_d3"],
+        gemm_bf16=lambda a, b, c, variant="default": calls.append(variant))
+    monkeypatch.setattr(bench, "prewarm_settle", lambda fn, sync, s: fn())
+    for t_alt, want in ((0.990, "dma4k_d3"), (0.997, "default"), (1.02, "default")):
+        monkeypatch.setattr(bench, "interleaved_compare", lambda fns, dev, rounds, launches, t=t_alt: {
+            "default": {"median_s": 1.0}, "dma4k_d3": {"median_s": t}})
+        wl.variant = "default"
+        sel = bench.select_k1(wl, backend, None, lambda: None)
+        assert sel["chosen"] == wl.variant == want
+        assert set(sel["tflops_median"]) == {"default", "dma4k_d3"}
+    assert {"default", "dma4k_d3"} <= set(calls)          # both builds really ran
+    one = types.SimpleNamespace(k1_candidates=lambda m, n, k: ["default"])
+    assert bench.select_k1(wl, one, None, lambda: None) is None
+
+
+def test_k1_candidates_shape_rule():
+    from nvidia_terraform_modules_amd.ops.kernels import k1_candidates
+
+    assert k1_candidates(8192, 8192, 8192) == ["default", "dma4k_d3"]
+    assert k1_candidates(8192, 8192, 4096) == ["default", "dma4k_d3"]
+    assert k1_candidates(8192, 8000, 8192) == ["default"]        # N % 256
+    assert k1_candidates(4096, 4096, 192) == ["default"]         # K % 128 and K >= 256
+    assert k1_candidates(256, 256, 8192, lda=8196) == ["default"]  # 16-B rows
+
+
 def test_self_relaunch_as_child_process():
     """`python bench.py --gpus 2` without WORLD_SIZE starts torch.distributed.run
     as a CHILD (never exec) and propagates its exit status."""
@@ -206,6 +243,10 @@ def test_bench_on_one_gpu_json_contract(tmp_path):
     d = lines[0]
     assert CONTRACT_KEYS <= set(d) and d["n_gpus"] == 1 and d["verified"] is True
     assert d["value"] > 50 and "rehearsal" not in d
+    # the K1 build the timed loop ran: the faster hand-written one on this box
+    sel = d["per_rank_k1_selection"][0]
+    assert d["per_rank_k1_variant"][0] == sel["chosen"] in ("default", "dma4k_d3")
+    assert all(v > 0 for v in sel["tflops_median"].values())
     topo = d["node_topology"]
     assert topo["ranks"][0]["cus"] == 256 and "gfx950" in (topo["ranks"][0]["gcn_arch"] or "")
     assert topo["visible_gpus"] >= 1 and topo["peer_access"][0][0] is True

@@ -94,7 +94,11 @@ ALLOWED_K1 = {
     "ntm::gemmt::gemm_bf16_tile_ws_kernel<4, 8, 0, true, true>",
     "ntm::gemmt::gemm_bf16_tile_kernel<8, 5>",
 }
-EXPERIMENTAL_ONLY = ("gemm_w4k_kernel", "gemm_w4o_kernel", "gemm_r4k_stamp_kernel",
+# The 4-wave bf16 build (dma4k_d3, gemm_w4k_kernel<3, false>) ships since round 6:
+# bench.select_k1 times it against the plan on each box (profiles/r6_w4kh). Its
+# fp8 build (knob 12) stays experimental.
+SHIPPED_4WAVE = "ntm::w4k::gemm_w4k_kernel<3, false>"
+EXPERIMENTAL_ONLY = ("gemm_w4k_kernel<2, true>", "gemm_w4o_kernel", "gemm_r4k_stamp_kernel",
                      "gemm_bf16_pp3_stamp_kernel", "ntm::gemm::gemm_bf16_kernel",
                      "mfma_rate_kernel", "mfma_f8_probe_kernel", "gemm_bf16_pp3h_kernel<96")
 
@@ -121,6 +125,7 @@ def test_shipping_artifact_has_only_default_dispatch_k1(path):
     assert k1 == ALLOWED_K1, (sorted(k1 - ALLOWED_K1), sorted(ALLOWED_K1 - k1))
     for bad in EXPERIMENTAL_ONLY:
         assert not [k for k in ks if bad in k], bad
+    assert {k for k in ks if "gemm_w4k_kernel" in k} == {SHIPPED_4WAVE}
 
 
 def test_experimental_library_holds_the_experiments():

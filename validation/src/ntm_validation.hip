@@ -19,6 +19,7 @@
 #include "ntm/gemm_bf16_skh.hpp"
 #include "ntm/gemm_bf16_t128.hpp"
 #include "ntm/gemm_fp8.hpp"
+#include "ntm/gemm_w4k.hpp"
 
 #define NTM_API extern "C" __attribute__((visibility("default")))
 
@@ -603,6 +604,11 @@ NTM_API int ntm_gemm_bf16_variant(int variant, const void* A, const void* B,
     // 192x256 / 256x192 on the same ping-pong (gemm_bf16_pp3h.hpp): ragged C, one round
     case 27: return (int)ntm::gemm3h::launch_gemm_bf16_pp3h<64, 128>(a, S(stream));
     case 28: return (int)ntm::gemm3h::launch_gemm_bf16_pp3h<128, 64>(a, S(stream));
+    // dma4k_d3 (gemm_w4k.hpp): 4 waves x 128x128 per wave on 256x256 tiles, a DMA
+    // piece every 3 slots. Not on the plan: under the power limit it trades places
+    // with pingpong8o box by box (-3 % .. +1.8 %, profiles/r6_w4kh), so bench.py
+    // measures both on the box it runs on and times the faster (select_k1).
+    case 39: return (int)ntm::w4k::launch_gemm_bf16_w4k<3>(a, S(stream));
     default: return (int)hipErrorInvalidValue;  // experimental variants: libntm_experimental.so
   }
 }
