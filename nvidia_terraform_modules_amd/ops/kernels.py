@@ -210,7 +210,9 @@ def gemm_bf16(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None,
     and whole tiles) for small, mid-size and ragged C,
     else "pingpong8c" when K % 128 == 0, else "pingpong8b" (8 waves, two per SIMD, staggered, balanced 8/4/8/4 LDS read
     schedule; 8c adds parity-alternating B buffers and a tail-free K loop),
-    "pingpong8" (the first 12/4/8/0 schedule) - see validation/include.
+    "pingpong8" (the first 12/4/8/0 schedule), "dma4k_d3" (4 waves x 128x128 per
+    wave on 256x256 tiles, off the plan; bench.select_k1 times it against the plan
+    on each box) - see validation/include.
     ``splits`` > 1 (masked tiles only): split-K into that many K slices, fp32
     partials in a workspace from PyTorch's allocator, then one reduction kernel.
     """
