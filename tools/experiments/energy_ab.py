@@ -5,7 +5,7 @@ the interleaved median (bench.interleaved_compare); energy comes from AMD SMI
 windows of >= --window-s of one kernel each, in palindromic order (A B C C B A)
 so no kernel always runs on the warmer chip; J/TFLOP = mean window power / TF/s.
 
-    python tools/experiments/energy_ab.py [--bf16-alt dma4k_d3[,dma4kh,...]] [--fp8-knob 12]
+    python tools/experiments/energy_ab.py [--bf16-alt dma4k_d3[,OTHER,...]] [--fp8-knob 12]
     (--fp8-knob 0 skips the fp8 comparison)
 """
 from __future__ import annotations
