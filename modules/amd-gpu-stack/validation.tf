@@ -134,6 +134,16 @@ resource "kubernetes_job_v1" "gpu_validation" {
               value = env.value
             }
           }
+          # the node's name in the verdict, the metrics and the termination message
+          # (one pod per GPU node)
+          env {
+            name = "NODE_NAME"
+            value_from {
+              field_ref {
+                field_path = "spec.nodeName"
+              }
+            }
+          }
 
           resources {
             limits = {

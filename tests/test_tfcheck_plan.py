@@ -241,6 +241,13 @@ def test_validation_job_runs_one_pod_per_gpu_node(nodes, backoff):
     assert _stack_eval(req.attr("topology_key")) == "kubernetes.io/hostname"
     sel = _stack_eval(req.blocks_of("label_selector")[0].body.attr("match_labels"))
     assert sel.items() <= pod_labels.items()       # the pods repel each other
+    # each pod's verdict names its node (NODE_NAME from the downward API)
+    ctr = pod.blocks_of("container")[0].body
+    envs = [e.body for e in ctr.blocks_of("env")]
+    node = [e for e in envs if e.attr("name") is not None and _stack_eval(e.attr("name")) == "NODE_NAME"]
+    assert node, "no NODE_NAME env"
+    ref = node[0].blocks_of("value_from")[0].body.blocks_of("field_ref")[0].body
+    assert _stack_eval(ref.attr("field_path")) == "spec.nodeName"
 
 
 def test_validation_node_count_must_be_a_whole_positive_number(tmp_path):

@@ -25,6 +25,7 @@ def _have_bin():
 def _run(*args, env=None, timeout=300):
     e = dict(os.environ)
     e.pop("NTM_FAULT_INJECT", None)
+    e.pop("NODE_NAME", None)          # set per test: the outputs then carry it
     e.update(env or {})
     p = subprocess.run([str(BIN), *args], capture_output=True, text=True, timeout=timeout, env=e)
     return p.returncode, p.stdout, p.stderr
@@ -44,9 +45,10 @@ def test_no_gpu_is_environment_error():
             pytest.skip("a GPU is visible")
     except ImportError:
         pass
-    rc, out, _ = _run("--size", "256", timeout=60)
+    rc, out, _ = _run("--size", "256", timeout=60, env={"NODE_NAME": "gpu-node-3"})
     assert rc == 2
-    assert json.loads(out.strip().splitlines()[-1])["passed"] is False
+    rep = json.loads(out.strip().splitlines()[-1])
+    assert rep["passed"] is False and rep["node"] == "gpu-node-3"   # the Job's pod names its node
 
 
 def _last_json(out):
@@ -80,6 +82,21 @@ def test_binary_passes_and_writes_sidecar_outputs(tmp_path):
     assert 'amdgpu_validate_gemm_tflops{gpu="0"}' in metrics
     assert 'amdgpu_validate_gemm_fp8_tflops{gpu="0"}' in metrics
     assert json.loads(full.read_text()) == rep
+
+
+@pytest.mark.gpu
+def test_binary_names_its_node_in_every_output(tmp_path):
+    """One validation pod per GPU node: the Job sets NODE_NAME (downward API), and
+    the verdict, the termination message and the metrics carry it."""
+    _have_bin()
+    term, prom = tmp_path / "term", tmp_path / "m.prom"
+    rc, out, err = _run("--gpus", "1", "--size", "1024", "--iters", "5", "--no-fp8",
+                        "--termination-log", str(term), "--prom-out", str(prom),
+                        env={"NODE_NAME": "gpu-node-7"})
+    assert rc == 0, out + err
+    assert _last_json(out)["node"] == "gpu-node-7"
+    assert json.loads(term.read_text())["node"] == "gpu-node-7"
+    assert 'amdgpu_validate_passed{node="gpu-node-7"} 1' in prom.read_text()
 
 
 @pytest.mark.gpu

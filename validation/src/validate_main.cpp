@@ -1233,7 +1233,9 @@ int main(int argc, char** argv) {
   if (o.require_iommu_pt && !hp.iommu_pt) fail("host prep: iommu=pt missing from /proc/cmdline");
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
-    std::printf("{\"passed\":false,\"failures\":[\"no AMD GPU visible\"]}\n");
+    const char* nn = std::getenv("NODE_NAME");
+    std::printf("{\"passed\":false,%s\"failures\":[\"no AMD GPU visible\"]}\n",
+                nn ? ("\"node\":" + jstr(nn) + ",").c_str() : "");
     return 2;
   }
   const int n = o.gpus > 0 ? std::min(o.gpus, ndev) : ndev;
@@ -1308,12 +1310,17 @@ int main(int argc, char** argv) {
   for (auto& c : rccl_rows) peak_rccl = std::max(peak_rccl, c.busbw);
   for (auto& c : xgmi_rows) peak_xgmi = std::max(peak_xgmi, c.busbw);
   const bool passed = g_failures.empty();
+  // the Kubernetes node this ran on (NODE_NAME from the downward API in the
+  // module's Job, one pod per GPU node): every verdict and metric names it
+  const char* node_env = std::getenv("NODE_NAME");
+  const std::string node = node_env ? node_env : "";
   std::string prom_text;
   {
     std::ostringstream p;
     p << "# HELP amdgpu_validate_passed 1 if every validation check passed.\n"
       << "# TYPE amdgpu_validate_passed gauge\n"
-      << "amdgpu_validate_passed " << (passed ? 1 : 0) << "\n"
+      << "amdgpu_validate_passed" << (node.empty() ? "" : "{node=" + jstr(node) + "}") << " "
+      << (passed ? 1 : 0) << "\n"
       << "# TYPE amdgpu_validate_seconds gauge\n"
       << "amdgpu_validate_seconds " << jnum(t_end - t_start) << "\n"
       << "# TYPE amdgpu_validate_gemm_tflops gauge\n";
@@ -1352,6 +1359,7 @@ int main(int argc, char** argv) {
   }
   std::string js = "{";
   js += "\"tool\":\"amdgpu-validate\",\"passed\":" + std::string(g_failures.empty() ? "true" : "false");
+  if (!node.empty()) js += ",\"node\":" + jstr(node);
   js += ",\"n_gpus\":" + std::to_string(n) + ",\"gemm_size\":" + std::to_string(o.size);
   js += ",\"gemm_tflops_aggregate\":" + jnum(agg);
   js += ",\"gpus\":[";
@@ -1416,6 +1424,7 @@ int main(int argc, char** argv) {
     // Kubernetes surfaces this file as the pod's termination message
     // (truncated at 4 KiB): the one-line verdict an operator sees first.
     std::string t = "{\"passed\":" + std::string(passed ? "true" : "false") +
+                    (node.empty() ? std::string() : ",\"node\":" + jstr(node)) +
                     ",\"n_gpus\":" + std::to_string(n) + ",\"gemm_tflops_aggregate\":" + jnum(agg) +
                     ",\"rccl_peak_busbw_GBps\":" + jnum(peak_rccl) +
                     ",\"seconds\":" + jnum(t_end - t_start) + ",\"failures\":[";
