@@ -58,7 +58,9 @@ class ClusterWatcher(threading.Thread):
     their termination messages until stopped.
 
     The Job runs one pod per GPU node (the module's validation_node_count):
-    ``expected_pods`` of them. ``report`` is set once they have all reported:
+    ``expected_pods`` of them, and as many GPU nodes are watched for their
+    first ``amd.com/gpu`` (one GPUAllocatable event each; the timeline's
+    gpu_allocatable stamp is the earliest). ``report`` is set once they have all reported:
     the verdict of the pod that finished LAST (its ``end_epoch_s`` is the
     validation_done stamp), with ``per_node`` listing every pod's node, finish
     time and verdict. If apply returns first, ``finish`` builds it from the
@@ -93,17 +95,24 @@ class ClusterWatcher(threading.Thread):
         if self.report is None:
             self.report = self._merge()
 
+    def _gpu_nodes(self) -> set:
+        return {e["involvedObject"]["name"] for e in self.events}
+
     def poll_once(self) -> None:
         now = time.time()
-        if not self.events:
+        # one GPUAllocatable event per node, the first poll that sees its
+        # amd.com/gpu; polled until every expected GPU node has reported
+        if len(self._gpu_nodes()) < self.expected_pods:
+            seen = self._gpu_nodes()
             nodes = _kubectl_json(self.kubectl, ["get", "nodes"])
             for it in (nodes or {}).get("items", []):
                 alloc = it.get("status", {}).get("allocatable", {})
                 n = alloc.get("amd.com/gpu")
-                if n not in (None, "0", 0):
+                name = it["metadata"]["name"]
+                if n not in (None, "0", 0) and name not in seen:
                     self.events.append({
                         "lastTimestamp": _iso(now),
-                        "involvedObject": {"kind": "Node", "name": it["metadata"]["name"]},
+                        "involvedObject": {"kind": "Node", "name": name},
                         "reason": "GPUAllocatable",
                         "message": f"amd.com/gpu allocatable {n}"})
         if self.report is None:
@@ -137,7 +146,7 @@ class ClusterWatcher(threading.Thread):
     def run(self) -> None:
         while not self._stop_evt.is_set():
             self.poll_once()
-            if self.events and self.report is not None:
+            if len(self._gpu_nodes()) >= self.expected_pods and self.report is not None:
                 return
             self._stop_evt.wait(self.poll_s)
 

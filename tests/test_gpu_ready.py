@@ -150,8 +150,10 @@ args = sys.argv[1:]
 if n < 2:
     sys.exit(1)                       # cluster not there yet
 if "nodes" in args:
-    print(json.dumps({"items": [{"metadata": {"name": "gpu-node-0"},
-                                 "status": {"allocatable": {"amd.com/gpu": "8"}}}]}))
+    # every GPU node (STUB_PODS of them) reports its GPUs
+    print(json.dumps({"items": [{"metadata": {"name": f"gpu-node-{i}"},
+                                 "status": {"allocatable": {"amd.com/gpu": "8"}}}
+                                for i in range(int(os.environ.get("STUB_PODS", "1")))]}))
 elif "pods" in args:
     # one validation pod per GPU node (STUB_PODS), finishing a second apart
     items = []
@@ -227,6 +229,9 @@ def test_cli_record_waits_for_every_node_pod(tmp_path):
                        capture_output=True, text=True, env=env, timeout=120,
                        cwd=Path(__file__).resolve().parents[1])
     assert p.returncode == 0, p.stderr
+    ev = json.loads((out / "k8s_events.json").read_text())["items"]
+    assert sorted(e["involvedObject"]["name"] for e in ev) == ["gpu-node-0", "gpu-node-1",
+                                                             "gpu-node-2"]
     rep = json.loads((out / "validation.json").read_text())
     assert rep["nodes_validated"] == rep["nodes_expected"] == 3
     assert [n["node"] for n in rep["per_node"]] == ["gpu-node-0", "gpu-node-1", "gpu-node-2"]
